@@ -1,0 +1,533 @@
+// Flash attention forward + backward for every attention on the SAM2 step:
+//   * Hiera windowed / q-pooled / global MHSA   (hieradet.py:56-81)      head_dim 56/96/72
+//   * memory-attention RoPE self + cross attn   (transformer.py:275-311) head_dim 256, Lk <= 7*1028
+//   * two-way decoder token<->image attention   (transformer.py:231-248) head_dim 32 / 16
+// Softmax(scale * Q K^T) V with online (base-2) softmax, optional in-kernel
+// dropout on P (counter-hash mask, regenerated in backward), LSE saved for the
+// backward.  Q/K/V/O are addressed with (batch, head, row) strides and a
+// contiguous head dim, so the projections' [B, L, H, d] outputs are consumed in
+// place.  head_dim is zero-padded to DP (multiple of 32) in registers/LDS only.
+//
+// Backward = two kernels (no atomics): dQ per query block, dK/dV per key block.
+#include "common.h"
+
+struct AttnArgs {
+  int B, H, Lq, Lk, D;
+  const void* q; int64_t sqb, sqh, sql;
+  const void* k; int64_t skb, skh, skl;
+  const void* v; int64_t svb, svh, svl;
+  void* o; int64_t sob, soh, sol;        // forward: O ; backward: dO
+  const void* fo; int64_t sfb, sfh, sfl; // backward: forward output O (for Di)
+  void* dq; int64_t sdqb, sdqh, sdql;
+  void* dk; int64_t sdkb, sdkh, sdkl;
+  void* dv; int64_t sdvb, sdvh, sdvl;
+  float* lse;  // [B*H*Lq]
+  float* di;   // [B*H*Lq] backward workspace: rowsum(dO*O)
+  float scale;
+  float p_drop;
+  uint64_t seed;
+};
+
+int s2h_prof_begin(hipStream_t st, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
+void s2h_prof_end(int slot, hipStream_t st);
+
+#define LOG2E 1.4426950408889634f
+#define LN2 0.6931471805599453f
+
+template <typename T> struct AttnCfg;
+template <> struct AttnCfg<bf16> { static constexpr int BKEY = 64, NW_DKV = 4; };
+template <> struct AttnCfg<float> { static constexpr int BKEY = 32, NW_DKV = 2; };
+template <typename T, int DP> struct DkvBQ {
+  static constexpr int v = DP >= 256 ? (sizeof(T) == 2 ? 32 : 16) : (sizeof(T) == 2 ? 64 : 32);
+};
+
+// Load ROWS x DP tile (rows r0.., d contiguous) into LDS, natural [row][d] layout.
+template <typename T, int ROWS, int DP, int STRIDE, int NTHR>
+__device__ __forceinline__ void lds_load_rows(T* dst, const T* src, int64_t ld, int r0, int nrows, int D, int tid) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int NV = ROWS * DP / VEC;
+  for (int v = tid; v < NV; v += NTHR) {
+    int row = v / (DP / VEC), d = (v % (DP / VEC)) * VEC;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (r0 + row < nrows && d < D) val = *(const uint4*)(src + (int64_t)(r0 + row) * ld + d);
+    *(uint4*)(dst + row * STRIDE + d) = val;
+  }
+}
+// Same source tile stored transposed: dst[d][row].
+template <typename T, int ROWS, int DP, int STRIDE, int NTHR>
+__device__ __forceinline__ void lds_load_rows_t(T* dst, const T* src, int64_t ld, int r0, int nrows, int D, int tid) {
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int NV = ROWS * DP / VEC;
+  for (int v = tid; v < NV; v += NTHR) {
+    int row = v % ROWS, d = (v / ROWS) * VEC;
+    uint4 val = make_uint4(0, 0, 0, 0);
+    if (r0 + row < nrows && d < D) val = *(const uint4*)(src + (int64_t)(r0 + row) * ld + d);
+    const T* t = (const T*)&val;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) dst[(d + j) * STRIDE + row] = t[j];
+  }
+}
+// A-operand fragment of 16 rows x KSTEP straight from global (rows >= nrows, d >= D -> 0)
+template <typename T>
+__device__ __forceinline__ typename Mfma<T>::frag frag_global(const T* base, int64_t ld, int row, int nrows, int d, int D) {
+  using MF = Mfma<T>;
+  if (row < nrows && d < D) {
+    if constexpr (sizeof(T) == 2) return *(const bf16x8*)(base + (int64_t)row * ld + d);
+    else return base[(int64_t)row * ld + d];
+  }
+  return MF::zero();
+}
+
+// ------------------------------------------------------------------ forward
+template <typename T, int DP>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  using MF = Mfma<T>;
+  constexpr int BKEY = AttnCfg<T>::BKEY;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int KS = DP + VEC, VS = BKEY + VEC, PS = BKEY + VEC;
+  constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16;
+  __shared__ __attribute__((aligned(16))) T smem[BKEY * KS + DP * VS + 4 * 16 * PS];
+  T* Ks = smem;
+  T* Vt = Ks + BKEY * KS;
+  T* Ps = Vt + DP * VS;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qw = blockIdx.x * 64 + w * 16;  // first query row of this wave
+  const T* Q = (const T*)a.q + b * a.sqb + h * a.sqh;
+  const T* K = (const T*)a.k + b * a.skb + h * a.skh;
+  const T* V = (const T*)a.v + b * a.svb + h * a.svh;
+  const float sl2 = a.scale * LOG2E;
+  const bool drop = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
+  const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+
+  typename MF::frag qf[NQF];
+#pragma unroll
+  for (int s = 0; s < NQF; ++s)
+    qf[s] = frag_global<T>(Q, a.sql, qw + (lane & 15), a.Lq, s * MF::KSTEP + (lane >> 4) * MF::KPL, a.D);
+
+  f32x4 o[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { m[r] = -INFINITY; l[r] = 0.f; }
+
+  const int nkt = (a.Lk + BKEY - 1) / BKEY;
+  T* Pw = Ps + w * 16 * PS;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * BKEY;
+    __syncthreads();
+    lds_load_rows<T, BKEY, DP, KS, 256>(Ks, K, a.skl, k0, a.Lk, a.D, tid);
+    lds_load_rows_t<T, BKEY, DP, VS, 256>(Vt, V, a.svl, k0, a.Lk, a.D, tid);
+    __syncthreads();
+
+    f32x4 s[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NQF; ++t) {
+        typename MF::frag bk = MF::load(&Ks[(j * 16 + (lane & 15)) * KS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+        s[j] = MF::mma(qf[t], bk, s[j]);
+      }
+    }
+    float mx[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mx[r] = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const bool kvalid = k0 + j * 16 + (lane & 15) < a.Lk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = kvalid ? s[j][r] * sl2 : -INFINITY;
+        s[j][r] = x;
+        mx[r] = fmaxf(mx[r], x);
+      }
+    }
+    float alpha[4], rs[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      mx[r] = row16_max(mx[r]);
+      float mn = fmaxf(m[r], mx[r]);
+      alpha[r] = exp2f(m[r] - mn);
+      m[r] = mn;
+      rs[r] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int key = k0 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float p = exp2f(s[j][r] - m[r]);
+        rs[r] += p;
+        if (drop) {
+          const int qi = qw + (lane >> 4) * 4 + r;
+          uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+          p = s2h_keep(a.seed, idx, thresh) ? p * inv_keep : 0.f;
+        }
+        Pw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) l[r] = l[r] * alpha[r] + row16_sum(rs[r]);
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[d][r] *= alpha[r];
+    __syncthreads();
+    constexpr int NPF = BKEY / MF::KSTEP;
+    typename MF::frag pf[NPF];
+#pragma unroll
+    for (int t = 0; t < NPF; ++t) pf[t] = MF::load(&Pw[(lane & 15) * PS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int t = 0; t < NPF; ++t) {
+        typename MF::frag bv = MF::load(&Vt[(d * 16 + (lane & 15)) * VS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+        o[d] = MF::mma(pf[t], bv, o[d]);
+      }
+  }
+
+  T* O = (T*)a.o + b * a.sob + h * a.soh;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = qw + (lane >> 4) * 4 + r;
+    const float inv = 1.f / l[r];
+    if (row < a.Lq) {
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const int col = d * 16 + (lane & 15);
+        if (col < a.D) O[(int64_t)row * a.sol + col] = from_f32<T>(o[d][r] * inv);
+      }
+      if ((lane & 15) == 0) a.lse[(int64_t)bh * a.Lq + row] = (m[r] + log2f(l[r])) * LN2;
+    }
+  }
+}
+
+// ------------------------------------------------- backward: Di = rowsum(dO*O)
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nrows = (int64_t)a.B * a.H * a.Lq;
+  if (row >= nrows) return;
+  const int qi = row % a.Lq;
+  const int bh = row / a.Lq, b = bh / a.H, h = bh % a.H;
+  const T* dO = (const T*)a.o + b * a.sob + h * a.soh + (int64_t)qi * a.sol;
+  const T* O = (const T*)a.fo + b * a.sfb + h * a.sfh + (int64_t)qi * a.sfl;
+  float acc = 0.f;
+  for (int d = lane; d < a.D; d += 64) acc += to_f32(dO[d]) * to_f32(O[d]);
+  acc = wave_sum(acc);
+  if (lane == 0) a.di[row] = acc;
+}
+
+// ------------------------------------------------------- backward: dQ
+template <typename T, int DP>
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  using MF = Mfma<T>;
+  constexpr int BKEY = AttnCfg<T>::BKEY;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int KS = DP + VEC, TS = BKEY + VEC, PS = BKEY + VEC;
+  constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16;
+  __shared__ __attribute__((aligned(16))) T smem[2 * BKEY * KS + DP * TS + 4 * 16 * PS];
+  T* Ks = smem;
+  T* Vs = Ks + BKEY * KS;
+  T* Kt = Vs + BKEY * KS;
+  T* Ss = Kt + DP * TS;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int qw = blockIdx.x * 64 + w * 16;
+  const T* Q = (const T*)a.q + b * a.sqb + h * a.sqh;
+  const T* K = (const T*)a.k + b * a.skb + h * a.skh;
+  const T* V = (const T*)a.v + b * a.svb + h * a.svh;
+  const T* dO = (const T*)a.o + b * a.sob + h * a.soh;
+  const float sl2 = a.scale * LOG2E;
+  const bool drop = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
+  const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+
+  typename MF::frag qf[NQF], gf[NQF];
+#pragma unroll
+  for (int s = 0; s < NQF; ++s) {
+    const int d = s * MF::KSTEP + (lane >> 4) * MF::KPL;
+    qf[s] = frag_global<T>(Q, a.sql, qw + (lane & 15), a.Lq, d, a.D);
+    gf[s] = frag_global<T>(dO, a.sol, qw + (lane & 15), a.Lq, d, a.D);
+  }
+  float lse2[4], di[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = qw + (lane >> 4) * 4 + r;
+    lse2[r] = row < a.Lq ? a.lse[(int64_t)bh * a.Lq + row] * LOG2E : 0.f;
+    di[r] = row < a.Lq ? a.di[(int64_t)bh * a.Lq + row] : 0.f;
+  }
+  f32x4 dq[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  T* Sw = Ss + w * 16 * PS;
+  const int nkt = (a.Lk + BKEY - 1) / BKEY;
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int k0 = kt * BKEY;
+    __syncthreads();
+    lds_load_rows<T, BKEY, DP, KS, 256>(Ks, K, a.skl, k0, a.Lk, a.D, tid);
+    lds_load_rows<T, BKEY, DP, KS, 256>(Vs, V, a.svl, k0, a.Lk, a.D, tid);
+    lds_load_rows_t<T, BKEY, DP, TS, 256>(Kt, K, a.skl, k0, a.Lk, a.D, tid);
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NQF; ++t) {
+        const int off = (j * 16 + (lane & 15)) * KS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+        s = MF::mma(qf[t], MF::load(&Ks[off]), s);
+        dp = MF::mma(gf[t], MF::load(&Vs[off]), dp);
+      }
+      const int key = k0 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = qw + (lane >> 4) * 4 + r;
+        float p = (key < a.Lk && qi < a.Lq) ? exp2f(s[r] * sl2 - lse2[r]) : 0.f;
+        float g = dp[r];
+        if (drop) {
+          uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+          g = s2h_keep(a.seed, idx, thresh) ? g * inv_keep : 0.f;
+        }
+        Sw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p * (g - di[r]));
+      }
+    }
+    __syncthreads();
+    constexpr int NPF = BKEY / MF::KSTEP;
+    typename MF::frag sf[NPF];
+#pragma unroll
+    for (int t = 0; t < NPF; ++t) sf[t] = MF::load(&Sw[(lane & 15) * PS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int t = 0; t < NPF; ++t)
+        dq[d] = MF::mma(sf[t], MF::load(&Kt[(d * 16 + (lane & 15)) * TS + t * MF::KSTEP + (lane >> 4) * MF::KPL]), dq[d]);
+  }
+  T* dQ = (T*)a.dq + b * a.sdqb + h * a.sdqh;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = qw + (lane >> 4) * 4 + r;
+    if (row < a.Lq)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const int col = d * 16 + (lane & 15);
+        if (col < a.D) dQ[(int64_t)row * a.sdql + col] = from_f32<T>(dq[d][r] * a.scale);
+      }
+  }
+}
+
+// ------------------------------------------------------ backward: dK, dV
+template <typename T, int DP>
+__global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(AttnArgs a) {
+  using MF = Mfma<T>;
+  constexpr int NW = AttnCfg<T>::NW_DKV;
+  constexpr int NT = NW * 64;
+  constexpr int BQ = DkvBQ<T, DP>::v;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int KS = DP + VEC, QS = BQ + VEC;
+  constexpr int NKF = DP / MF::KSTEP, NB = BQ / 16, ND = DP / 16, NPF = BQ / MF::KSTEP;
+  __shared__ __attribute__((aligned(16))) T smem[2 * NW * 16 * KS + 2 * BQ * KS + 2 * DP * QS + 2 * NW * 16 * QS];
+  __shared__ float stat[2 * BQ];
+  T* Kn = smem;
+  T* Vn = Kn + NW * 16 * KS;
+  T* Qs = Vn + NW * 16 * KS;
+  T* Gs = Qs + BQ * KS;
+  T* Qt = Gs + BQ * KS;
+  T* Gt = Qt + DP * QS;
+  T* Pb = Gt + DP * QS;
+  T* Sb = Pb + NW * 16 * QS;
+  float* lse_s = stat;
+  float* di_s = stat + BQ;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int kb = blockIdx.x * NW * 16;  // first key of the workgroup
+  const int kw = kb + w * 16;           // first key of this wave
+  const T* Q = (const T*)a.q + b * a.sqb + h * a.sqh;
+  const T* K = (const T*)a.k + b * a.skb + h * a.skh;
+  const T* V = (const T*)a.v + b * a.svb + h * a.svh;
+  const T* dO = (const T*)a.o + b * a.sob + h * a.soh;
+  const float sl2 = a.scale * LOG2E;
+  const bool drop = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
+  const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+
+  lds_load_rows<T, NW * 16, DP, KS, NT>(Kn, K, a.skl, kb, a.Lk, a.D, tid);
+  lds_load_rows<T, NW * 16, DP, KS, NT>(Vn, V, a.svl, kb, a.Lk, a.D, tid);
+
+  f32x4 dk[ND], dv[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+  T* Pw = Pb + w * 16 * QS;
+  T* Sw = Sb + w * 16 * QS;
+  const T* Kw = Kn + w * 16 * KS;
+  const T* Vw = Vn + w * 16 * KS;
+
+  const int nqt = (a.Lq + BQ - 1) / BQ;
+  for (int qt = 0; qt < nqt; ++qt) {
+    const int q0 = qt * BQ;
+    __syncthreads();
+    lds_load_rows<T, BQ, DP, KS, NT>(Qs, Q, a.sql, q0, a.Lq, a.D, tid);
+    lds_load_rows<T, BQ, DP, KS, NT>(Gs, dO, a.sol, q0, a.Lq, a.D, tid);
+    lds_load_rows_t<T, BQ, DP, QS, NT>(Qt, Q, a.sql, q0, a.Lq, a.D, tid);
+    lds_load_rows_t<T, BQ, DP, QS, NT>(Gt, dO, a.sol, q0, a.Lq, a.D, tid);
+    for (int i = tid; i < BQ; i += NT) {
+      const int qi = q0 + i;
+      lse_s[i] = qi < a.Lq ? a.lse[(int64_t)bh * a.Lq + qi] * LOG2E : 0.f;
+      di_s[i] = qi < a.Lq ? a.di[(int64_t)bh * a.Lq + qi] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < NKF; ++t) {
+        const int ao = (lane & 15) * KS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+        const int bo = (j * 16 + (lane & 15)) * KS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+        s = MF::mma(MF::load(&Kw[ao]), MF::load(&Qs[bo]), s);
+        dp = MF::mma(MF::load(&Vw[ao]), MF::load(&Gs[bo]), dp);
+      }
+      const int qc = j * 16 + (lane & 15);  // query column within tile
+      const int qi = q0 + qc;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kw + (lane >> 4) * 4 + r;
+        const bool valid = key < a.Lk && qi < a.Lq;
+        float p = valid ? exp2f(s[r] * sl2 - lse_s[qc]) : 0.f;
+        float pd = p, g = dp[r];
+        if (drop) {
+          uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+          bool keep = valid && s2h_keep(a.seed, idx, thresh);
+          pd = keep ? p * inv_keep : 0.f;
+          g = keep ? g * inv_keep : 0.f;
+        }
+        Pw[((lane >> 4) * 4 + r) * QS + qc] = from_f32<T>(pd);
+        Sw[((lane >> 4) * 4 + r) * QS + qc] = from_f32<T>(p * (g - di_s[qc]));
+      }
+    }
+    __syncthreads();
+    typename MF::frag pf[NPF], sf[NPF];
+#pragma unroll
+    for (int t = 0; t < NPF; ++t) {
+      const int o = (lane & 15) * QS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+      pf[t] = MF::load(&Pw[o]);
+      sf[t] = MF::load(&Sw[o]);
+    }
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int t = 0; t < NPF; ++t) {
+        const int o = (d * 16 + (lane & 15)) * QS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+        dv[d] = MF::mma(pf[t], MF::load(&Gt[o]), dv[d]);
+        dk[d] = MF::mma(sf[t], MF::load(&Qt[o]), dk[d]);
+      }
+  }
+  T* dK = (T*)a.dk + b * a.sdkb + h * a.sdkh;
+  T* dV = (T*)a.dv + b * a.sdvb + h * a.sdvh;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int key = kw + (lane >> 4) * 4 + r;
+    if (key < a.Lk)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        const int col = d * 16 + (lane & 15);
+        if (col < a.D) {
+          dK[(int64_t)key * a.sdkl + col] = from_f32<T>(dk[d][r] * a.scale);
+          dV[(int64_t)key * a.sdvl + col] = from_f32<T>(dv[d][r]);
+        }
+      }
+  }
+}
+
+// ------------------------------------------------------------------ launch
+template <typename T, int DP>
+static int attn_fwd_launch(const AttnArgs& a, hipStream_t st) {
+  dim3 grid((a.Lq + 63) / 64, a.B * a.H);
+  const int slot = s2h_prof_begin(st, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
+  hipLaunchKernelGGL((attn_fwd_kernel<T, DP>), grid, dim3(256), 0, st, a);
+  s2h_prof_end(slot, st);
+  return (int)hipGetLastError();
+}
+template <typename T, int DP>
+static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.B * a.H * a.Lq;
+  hipLaunchKernelGGL((attn_bwd_pre_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0, st, a);
+  dim3 gq((a.Lq + 63) / 64, a.B * a.H);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP>), gq, dim3(256), 0, st, a);
+  constexpr int NW = AttnCfg<T>::NW_DKV;
+  dim3 gk((a.Lk + NW * 16 - 1) / (NW * 16), a.B * a.H);
+  hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DP>), gk, dim3(NW * 64), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <typename T, bool FWD>
+static int attn_dispatch(const AttnArgs& a, hipStream_t st) {
+  if (a.D <= 32) return FWD ? attn_fwd_launch<T, 32>(a, st) : attn_bwd_launch<T, 32>(a, st);
+  if (a.D <= 64) return FWD ? attn_fwd_launch<T, 64>(a, st) : attn_bwd_launch<T, 64>(a, st);
+  if (a.D <= 96) return FWD ? attn_fwd_launch<T, 96>(a, st) : attn_bwd_launch<T, 96>(a, st);
+  if (a.D <= 128) return FWD ? attn_fwd_launch<T, 128>(a, st) : attn_bwd_launch<T, 128>(a, st);
+  if (a.D <= 256) return FWD ? attn_fwd_launch<T, 256>(a, st) : attn_bwd_launch<T, 256>(a, st);
+  return (int)hipErrorInvalidValue;
+}
+
+static bool attn_aligned(int dt, int D, const void* p, int64_t s1, int64_t s2, int64_t s3) {
+  const int vec = dt == S2H_BF16 ? 8 : 4;
+  return ((uintptr_t)p % 16 == 0) && D % vec == 0 && s1 % vec == 0 && s2 % vec == 0 && s3 % vec == 0;
+}
+
+extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
+                            const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                            const void* k, int64_t skb, int64_t skh, int64_t skl,
+                            const void* v, int64_t svb, int64_t svh, int64_t svl,
+                            void* o, int64_t sob, int64_t soh, int64_t sol,
+                            float* lse, float scale, float p_drop, uint64_t seed, hipStream_t st) {
+  if (B * H <= 0 || Lq <= 0) return 0;
+  if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
+  if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
+      !attn_aligned(dt, D, v, svb, svh, svl))
+    return (int)hipErrorInvalidValue;
+  AttnArgs a = {};
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.D = D;
+  a.q = q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
+  a.k = k; a.skb = skb; a.skh = skh; a.skl = skl;
+  a.v = v; a.svb = svb; a.svh = svh; a.svl = svl;
+  a.o = o; a.sob = sob; a.soh = soh; a.sol = sol;
+  a.lse = lse; a.scale = scale; a.p_drop = p_drop; a.seed = seed;
+  return dt == S2H_BF16 ? attn_dispatch<bf16, true>(a, st) : attn_dispatch<float, true>(a, st);
+}
+
+extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
+                            const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                            const void* k, int64_t skb, int64_t skh, int64_t skl,
+                            const void* v, int64_t svb, int64_t svh, int64_t svl,
+                            const void* o, int64_t sob, int64_t soh, int64_t sol,
+                            const void* dout, int64_t sgb, int64_t sgh, int64_t sgl,
+                            void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
+                            void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
+                            void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
+                            const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                            hipStream_t st) {
+  if (B * H <= 0 || Lq <= 0) return 0;
+  if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
+  if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
+      !attn_aligned(dt, D, v, svb, svh, svl) || !attn_aligned(dt, D, dout, sgb, sgh, sgl))
+    return (int)hipErrorInvalidValue;
+  AttnArgs a = {};
+  a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.D = D;
+  a.q = q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
+  a.k = k; a.skb = skb; a.skh = skh; a.skl = skl;
+  a.v = v; a.svb = svb; a.svh = svh; a.svl = svl;
+  a.o = (void*)dout; a.sob = sgb; a.soh = sgh; a.sol = sgl;
+  a.fo = o; a.sfb = sob; a.sfh = soh; a.sfl = sol;
+  a.dq = dq; a.sdqb = sdqb; a.sdqh = sdqh; a.sdql = sdql;
+  a.dk = dk; a.sdkb = sdkb; a.sdkh = sdkh; a.sdkl = sdkl;
+  a.dv = dv; a.sdvb = sdvb; a.sdvh = sdvh; a.sdvl = sdvl;
+  a.lse = (float*)lse; a.di = di_ws; a.scale = scale; a.p_drop = p_drop; a.seed = seed;
+  return dt == S2H_BF16 ? attn_dispatch<bf16, false>(a, st) : attn_dispatch<float, false>(a, st);
+}

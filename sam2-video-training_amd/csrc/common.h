@@ -1,0 +1,118 @@
+// Shared device helpers for libsam2hip (gfx950 / CDNA4 only).
+//
+// Element types: every compute kernel is templated on the storage type T of its
+// activations: `float` (fp32-parity mode, f32-input MFMA 16x16x4) or `__bf16`
+// (performance mode, bf16 MFMA 16x16x32).  Accumulation is always fp32.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+enum S2HDtype { S2H_F32 = 0, S2H_BF16 = 1 };
+
+#define S2H_WAVE 64
+
+__device__ __forceinline__ float to_f32(float x) { return x; }
+__device__ __forceinline__ float to_f32(bf16 x) { return (float)x; }
+template <typename T> __device__ __forceinline__ T from_f32(float x);
+template <> __device__ __forceinline__ float from_f32<float>(float x) { return x; }
+template <> __device__ __forceinline__ bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// ---------------------------------------------------------------------------
+// MFMA traits.  Both shapes are 16x16 output tiles with the dtype-independent
+// C/D layout: lane l holds column (l & 15), rows 4*(l >> 4) + r, r = 0..3.
+// Operand layout: lane l supplies A[row l&15][k = (l>>4)*KPL + j] and
+// B[k = (l>>4)*KPL + j][col l&15], j < KPL, one instruction covers KSTEP = 4*KPL.
+// ---------------------------------------------------------------------------
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16> {
+  static constexpr int KPL = 8;
+  static constexpr int KSTEP = 32;
+  typedef bf16x8 frag;
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag load(const bf16* p) { return *(const bf16x8*)p; }
+  static __device__ __forceinline__ frag zero() { frag z; for (int j = 0; j < 8; ++j) z[j] = (bf16)0.f; return z; }
+};
+template <> struct Mfma<float> {
+  static constexpr int KPL = 1;
+  static constexpr int KSTEP = 4;
+  typedef float frag;
+  static __device__ __forceinline__ f32x4 mma(frag a, frag b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ frag load(const float* p) { return *p; }
+  static __device__ __forceinline__ frag zero() { return 0.f; }
+};
+
+// 16-byte vector of T (8 bf16 or 4 f32) for coalesced global loads.
+template <typename T> struct Vec16;
+template <> struct Vec16<bf16> { static constexpr int N = 8; typedef uint4 raw; };
+template <> struct Vec16<float> { static constexpr int N = 4; typedef uint4 raw; };
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+// reduce across the 16 lanes that share (lane >> 4) -- one MFMA row group
+__device__ __forceinline__ float row16_sum(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float row16_max(float v) {
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based dropout RNG (splitmix-style 64-bit hash).  keep(i) is a pure
+// function of (seed, offset, index), so forward and backward regenerate the
+// same mask without storing it.
+__device__ __forceinline__ uint32_t s2h_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (uint32_t)(z >> 32);
+}
+__device__ __forceinline__ bool s2h_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
+  return s2h_hash(seed, idx) >= thresh;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+
+enum S2HAct { S2H_ACT_NONE = 0, S2H_ACT_RELU = 1, S2H_ACT_GELU = 2, S2H_ACT_SIGMOID = 3 };
+
+__device__ __forceinline__ float apply_act(float v, int act) {
+  if (act == S2H_ACT_RELU) return fmaxf(v, 0.f);
+  if (act == S2H_ACT_GELU) return gelu_erf(v);
+  if (act == S2H_ACT_SIGMOID) return 1.f / (1.f + expf(-v));
+  return v;
+}
+
+// derivative of the activation, evaluated at the pre-activation value x
+__device__ __forceinline__ float act_grad(float x, int act) {
+  if (act == S2H_ACT_RELU) return x > 0.f ? 1.f : 0.f;
+  if (act == S2H_ACT_GELU) return gelu_erf_grad(x);
+  if (act == S2H_ACT_SIGMOID) { float s = 1.f / (1.f + expf(-x)); return s * (1.f - s); }
+  return 1.f;
+}
+
+#define S2H_LAUNCH_CHECK() return (int)hipGetLastError()

@@ -1,0 +1,554 @@
+// Bandwidth-bound helpers of the SAM2 step: residual adds, broadcast adds,
+// activations, casts, dropout, 2-D axial RoPE, q-pool max-pool, window
+// (un)partition, FPN nearest top-down, bilinear mask resampling, column sums,
+// NHWC im2col / depthwise conv / transposed-conv scatter.  All grid-stride,
+// coalesced along the contiguous (channel) dimension.
+#include "common.h"
+
+#define GRID_STRIDE(i, n) for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
+
+static inline dim3 ew_grid(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  if (b < 1) b = 1;
+  return dim3((unsigned)b);
+}
+
+#define DISPATCH_T(dt, KERNEL, grid, ...)                                      \
+  do {                                                                         \
+    if ((dt) == S2H_BF16) hipLaunchKernelGGL(KERNEL<bf16>, grid, dim3(256), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<float>, grid, dim3(256), 0, st, __VA_ARGS__); \
+  } while (0)
+
+// ---------------------------------------------------------------- add / axpy
+// out = alpha*a + beta*b   (a or b may be null -> treated as 0)
+template <typename T>
+__global__ void add_kernel(int64_t n, const void* a, const void* b, float alpha, float beta, void* out) {
+  GRID_STRIDE(i, n) {
+    float v = 0.f;
+    if (a) v += alpha * to_f32(((const T*)a)[i]);
+    if (b) v += beta * to_f32(((const T*)b)[i]);
+    ((T*)out)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_add(int dt, int64_t n, const void* a, const void* b, float alpha, float beta, void* out,
+                       hipStream_t st) {
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, add_kernel, ew_grid(n), n, a, b, alpha, beta, out);
+  return (int)hipGetLastError();
+}
+
+// out[i, j] = alpha*a[i, j] + beta*bvec[(i % b_period) * inner + j]   (b row broadcast / periodic)
+template <typename T>
+__global__ void add_bcast_kernel(int64_t outer, int64_t inner, const void* a, float alpha, const void* b,
+                                 int64_t b_period, float beta, void* out) {
+  const int64_t n = outer * inner;
+  GRID_STRIDE(i, n) {
+    const int64_t r = i / inner, c = i - r * inner;
+    float v = beta * to_f32(((const T*)b)[(r % b_period) * inner + c]);
+    if (a) v += alpha * to_f32(((const T*)a)[i]);
+    ((T*)out)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_add_bcast(int dt, int64_t outer, int64_t inner, const void* a, float alpha, const void* b,
+                             int64_t b_period, float beta, void* out, hipStream_t st) {
+  if (outer * inner <= 0) return 0;
+  DISPATCH_T(dt, add_bcast_kernel, ew_grid(outer * inner), outer, inner, a, alpha, b, b_period, beta, out);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------------------- activations
+// y = act(x) * scale + shift
+template <typename T>
+__global__ void act_fwd_kernel(int64_t n, const void* x, int act, float scale, float shift, void* y) {
+  GRID_STRIDE(i, n) ((T*)y)[i] = from_f32<T>(apply_act(to_f32(((const T*)x)[i]), act) * scale + shift);
+}
+extern "C" int s2h_act_fwd(int dt, int64_t n, const void* x, int act, float scale, float shift, void* y,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, act_fwd_kernel, ew_grid(n), n, x, act, scale, shift, y);
+  return (int)hipGetLastError();
+}
+// dx = dy * act'(x_pre) (+ dx if accum)
+template <typename T>
+__global__ void act_bwd_kernel(int64_t n, const void* x, const void* dy, int act, void* dx, int accum) {
+  GRID_STRIDE(i, n) {
+    float v = to_f32(((const T*)dy)[i]) * act_grad(to_f32(((const T*)x)[i]), act);
+    if (accum) v += to_f32(((T*)dx)[i]);
+    ((T*)dx)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_act_bwd(int dt, int64_t n, const void* x, const void* dy, int act, void* dx, int accum,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, act_bwd_kernel, ew_grid(n), n, x, dy, act, dx, accum);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ casts
+__global__ void cast_f32_bf16_kernel(int64_t n, const float* x, bf16* y) { GRID_STRIDE(i, n) y[i] = (bf16)x[i]; }
+__global__ void cast_bf16_f32_kernel(int64_t n, const bf16* x, float* y) { GRID_STRIDE(i, n) y[i] = (float)x[i]; }
+__global__ void copy_f32_kernel(int64_t n, const float* x, float* y) { GRID_STRIDE(i, n) y[i] = x[i]; }
+extern "C" int s2h_cast(int dt_in, int dt_out, int64_t n, const void* x, void* y, hipStream_t st) {
+  if (n <= 0) return 0;
+  if (dt_in == S2H_F32 && dt_out == S2H_BF16)
+    hipLaunchKernelGGL(cast_f32_bf16_kernel, ew_grid(n), dim3(256), 0, st, n, (const float*)x, (bf16*)y);
+  else if (dt_in == S2H_BF16 && dt_out == S2H_F32)
+    hipLaunchKernelGGL(cast_bf16_f32_kernel, ew_grid(n), dim3(256), 0, st, n, (const bf16*)x, (float*)y);
+  else if (dt_in == S2H_F32 && dt_out == S2H_F32)
+    hipLaunchKernelGGL(copy_f32_kernel, ew_grid(n), dim3(256), 0, st, n, (const float*)x, (float*)y);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- dropout
+// mode 0: out = a + keep(i)*b/(1-p)     mode 1: out = keep(i)*b/(1-p)   (also the backward)
+template <typename T>
+__global__ void dropout_kernel(int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out) {
+  const uint32_t thresh = (uint32_t)(p * 4294967296.0);
+  const float inv = 1.f / (1.f - p);
+  GRID_STRIDE(i, n) {
+    float v = s2h_keep(seed, (uint64_t)i, thresh) ? to_f32(((const T*)b)[i]) * inv : 0.f;
+    if (a) v += to_f32(((const T*)a)[i]);
+    ((T*)out)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out,
+                           hipStream_t st) {
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, dropout_kernel, ew_grid(n), n, a, b, p, seed, out);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------ axial RoPE
+// Rotates consecutive pairs (2c, 2c+1) of the first `nrot` rows of every batch:
+// row t uses table row (t % period); inverse=1 rotates by -theta (backward).
+template <typename T>
+__global__ void rope_kernel(int64_t nb, int nrot, int D, const void* x, int64_t sxb, int64_t sxl, void* y,
+                            int64_t syb, int64_t syl, const float* cosv, const float* sinv, int period, int inverse) {
+  const int half = D / 2;
+  const int64_t n = nb * nrot * half;
+  GRID_STRIDE(i, n) {
+    const int c = i % half;
+    const int64_t rt = i / half;
+    const int t = rt % nrot;
+    const int64_t b = rt / nrot;
+    const T* xp = (const T*)x + b * sxb + (int64_t)t * sxl + 2 * c;
+    T* yp = (T*)y + b * syb + (int64_t)t * syl + 2 * c;
+    const int pr = t % period;
+    const float co = cosv[pr * half + c];
+    const float si = inverse ? -sinv[pr * half + c] : sinv[pr * half + c];
+    const float xr = to_f32(xp[0]), xi = to_f32(xp[1]);
+    yp[0] = from_f32<T>(xr * co - xi * si);
+    yp[1] = from_f32<T>(xr * si + xi * co);
+  }
+}
+extern "C" int s2h_rope(int dt, int64_t nb, int nrot, int D, const void* x, int64_t sxb, int64_t sxl, void* y,
+                        int64_t syb, int64_t syl, const float* cosv, const float* sinv, int period, int inverse,
+                        hipStream_t st) {
+  const int64_t n = nb * nrot * (D / 2);
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, rope_kernel, ew_grid(n), nb, nrot, D, x, sxb, sxl, y, syb, syl, cosv, sinv, period, inverse);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------- 2x2 max-pool NHWC
+// x viewed as [B, H, W, C] with row stride ldx (elements between consecutive (b,h,w) pixels)
+template <typename T>
+__global__ void maxpool2_fwd_kernel(int B, int H, int W, int C, const void* x, int64_t ldx, void* y) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int64_t n = (int64_t)B * Ho * Wo * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    int64_t p = i / C;
+    const int xo = p % Wo; p /= Wo;
+    const int yo = p % Ho;
+    const int b = p / Ho;
+    const T* xb = (const T*)x;
+    float m = -INFINITY;
+    for (int dy = 0; dy < 2; ++dy)
+      for (int dx = 0; dx < 2; ++dx) {
+        int64_t pix = ((int64_t)b * H + 2 * yo + dy) * W + 2 * xo + dx;
+        float v = to_f32(xb[pix * ldx + c]);
+        if (v > m || isnan(v)) m = v;
+      }
+    ((T*)y)[i] = from_f32<T>(m);
+  }
+}
+// routes dy to the first maximal element of each window (PyTorch's scan order); writes (not accumulates) dx
+template <typename T>
+__global__ void maxpool2_bwd_kernel(int B, int H, int W, int C, const void* x, int64_t ldx, const void* dy,
+                                    void* dx, int64_t lddx) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int64_t n = (int64_t)B * Ho * Wo * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    int64_t p = i / C;
+    const int xo = p % Wo; p /= Wo;
+    const int yo = p % Ho;
+    const int b = p / Ho;
+    const T* xb = (const T*)x;
+    float m = -INFINITY;
+    int best = 0;
+    for (int k = 0; k < 4; ++k) {
+      int64_t pix = ((int64_t)b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+      float v = to_f32(xb[pix * ldx + c]);
+      if (v > m || isnan(v)) { m = v; best = k; }
+    }
+    const float g = to_f32(((const T*)dy)[i]);
+    for (int k = 0; k < 4; ++k) {
+      int64_t pix = ((int64_t)b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+      ((T*)dx)[pix * lddx + c] = from_f32<T>(k == best ? g : 0.f);
+    }
+  }
+}
+extern "C" int s2h_maxpool2_fwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, void* y,
+                                hipStream_t st) {
+  const int64_t n = (int64_t)B * (H / 2) * (W / 2) * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, maxpool2_fwd_kernel, ew_grid(n), B, H, W, C, x, ldx, y);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_maxpool2_bwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, const void* dy,
+                                void* dx, int64_t lddx, hipStream_t st) {
+  const int64_t n = (int64_t)B * (H / 2) * (W / 2) * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, maxpool2_bwd_kernel, ew_grid(n), B, H, W, C, x, ldx, dy, dx, lddx);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------ window (un)partition NHWC
+// partition (dir 0): win[(b*nh + wy)*nw + wx][iy][ix][c] = x[b][wy*ws+iy][wx*ws+ix][c]  (0 outside H, W)
+// unpartition (dir 1): x[b][y][x][c] = win[...]   (padding dropped)
+// accum: the destination is accumulated into (used for residual-stream backward)
+template <typename T>
+__global__ void window_kernel(int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum) {
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws;
+  const int64_t n = dir == 0 ? (int64_t)B * nh * nw * ws * ws * C : (int64_t)B * H * W * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    int64_t p = i / C;
+    int b, yy, xx;
+    int64_t widx;
+    if (dir == 0) {
+      const int ix = p % ws; p /= ws;
+      const int iy = p % ws; p /= ws;
+      const int wx = p % nw; p /= nw;
+      const int wy = p % nh;
+      b = p / nh;
+      yy = wy * ws + iy; xx = wx * ws + ix;
+      float v = 0.f;
+      if (yy < H && xx < W) v = to_f32(((const T*)src)[(((int64_t)b * H + yy) * W + xx) * C + c]);
+      if (accum) v += to_f32(((T*)dst)[i]);
+      ((T*)dst)[i] = from_f32<T>(v);
+    } else {
+      xx = p % W; p /= W;
+      yy = p % H;
+      b = p / H;
+      widx = ((((int64_t)b * nh + yy / ws) * nw + xx / ws) * ws + yy % ws) * ws + xx % ws;
+      float v = to_f32(((const T*)src)[widx * C + c]);
+      if (accum) v += to_f32(((T*)dst)[i]);
+      ((T*)dst)[i] = from_f32<T>(v);
+    }
+  }
+}
+extern "C" int s2h_window(int dt, int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum,
+                          hipStream_t st) {
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws;
+  const int64_t n = dir == 0 ? (int64_t)B * nh * nw * ws * ws * C : (int64_t)B * H * W * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, window_kernel, ew_grid(n), B, H, W, C, ws, src, dst, dir, accum);
+  return (int)hipGetLastError();
+}
+
+// ----------------------------------------------- FPN nearest x2 top-down
+// out[b,y,x,c] = lat[b,y,x,c] + prev[b,y/2,x/2,c]
+template <typename T>
+__global__ void up2_add_kernel(int B, int H, int W, int C, const void* lat, const void* prev, void* out) {
+  const int64_t n = (int64_t)B * H * W * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    int64_t p = i / C;
+    const int xx = p % W; p /= W;
+    const int yy = p % H;
+    const int b = p / H;
+    float v = to_f32(((const T*)lat)[i]);
+    v += to_f32(((const T*)prev)[(((int64_t)b * (H / 2) + yy / 2) * (W / 2) + xx / 2) * C + c]);
+    ((T*)out)[i] = from_f32<T>(v);
+  }
+}
+// dprev[b,y,x,c] = sum_{2x2} dout[b,2y+dy,2x+dx,c]   (+= if accum)
+template <typename T>
+__global__ void pool2_sum_kernel(int B, int Ho, int Wo, int C, const void* dout, void* dprev, int accum) {
+  const int64_t n = (int64_t)B * Ho * Wo * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    int64_t p = i / C;
+    const int xx = p % Wo; p /= Wo;
+    const int yy = p % Ho;
+    const int b = p / Ho;
+    float v = 0.f;
+    for (int k = 0; k < 4; ++k)
+      v += to_f32(((const T*)dout)[(((int64_t)b * 2 * Ho + 2 * yy + (k >> 1)) * 2 * Wo + 2 * xx + (k & 1)) * C + c]);
+    if (accum) v += to_f32(((T*)dprev)[i]);
+    ((T*)dprev)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_up2_add(int dt, int B, int H, int W, int C, const void* lat, const void* prev, void* out,
+                           hipStream_t st) {
+  const int64_t n = (int64_t)B * H * W * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, up2_add_kernel, ew_grid(n), B, H, W, C, lat, prev, out);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_pool2_sum(int dt, int B, int Ho, int Wo, int C, const void* dout, void* dprev, int accum,
+                             hipStream_t st) {
+  const int64_t n = (int64_t)B * Ho * Wo * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, pool2_sum_kernel, ew_grid(n), B, Ho, Wo, C, dout, dprev, accum);
+  return (int)hipGetLastError();
+}
+
+// --------------------------------------- bilinear resample (align_corners=False)
+// planes [N, hi, wi] f32 -> [N, ho, wo] f32, PyTorch upsample_bilinear2d index rule.
+__device__ __forceinline__ void bil_src(int o, float scale, int in, int& i0, int& i1, float& l1) {
+  float s = scale * (o + 0.5f) - 0.5f;
+  if (s < 0.f) s = 0.f;
+  i0 = (int)s;
+  if (i0 > in - 1) i0 = in - 1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+  l1 = s - (float)i0;
+}
+__global__ void bilinear_fwd_kernel(int N, int hi, int wi, int ho, int wo, const float* x, float* y) {
+  const float sh = (float)hi / ho, sw = (float)wi / wo;
+  const int64_t n = (int64_t)N * ho * wo;
+  GRID_STRIDE(i, n) {
+    const int ox = i % wo;
+    const int64_t r = i / wo;
+    const int oy = r % ho;
+    const int p = r / ho;
+    int y0, y1, x0, x1;
+    float ly, lx;
+    bil_src(oy, sh, hi, y0, y1, ly);
+    bil_src(ox, sw, wi, x0, x1, lx);
+    const float* xp = x + (int64_t)p * hi * wi;
+    const float v = (1.f - ly) * ((1.f - lx) * xp[y0 * wi + x0] + lx * xp[y0 * wi + x1]) +
+                    ly * ((1.f - lx) * xp[y1 * wi + x0] + lx * xp[y1 * wi + x1]);
+    y[i] = v;
+  }
+}
+// gather form of the backward (deterministic): dx[p,iy,ix] = sum over outputs whose taps hit (iy,ix)
+__global__ void bilinear_bwd_kernel(int N, int hi, int wi, int ho, int wo, const float* dy, float* dx) {
+  const float sh = (float)hi / ho, sw = (float)wi / wo;
+  const int64_t n = (int64_t)N * hi * wi;
+  const int ry = (int)ceilf(1.f / sh) + 2, rx = (int)ceilf(1.f / sw) + 2;
+  GRID_STRIDE(i, n) {
+    const int ix = i % wi;
+    const int64_t r = i / wi;
+    const int iy = r % hi;
+    const int p = r / hi;
+    const int cy = (int)((iy + 0.5f) / sh), cx = (int)((ix + 0.5f) / sw);
+    float acc = 0.f;
+    for (int oy = max(0, cy - ry - 1); oy <= min(ho - 1, cy + ry + 1); ++oy) {
+      int y0, y1; float ly;
+      bil_src(oy, sh, hi, y0, y1, ly);
+      float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      for (int ox = max(0, cx - rx - 1); ox <= min(wo - 1, cx + rx + 1); ++ox) {
+        int x0, x1; float lx;
+        bil_src(ox, sw, wi, x0, x1, lx);
+        float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
+        if (wx == 0.f) continue;
+        acc += wy * wx * dy[((int64_t)p * ho + oy) * wo + ox];
+      }
+    }
+    dx[i] = acc;
+  }
+}
+extern "C" int s2h_bilinear_fwd(int N, int hi, int wi, int ho, int wo, const float* x, float* y, hipStream_t st) {
+  const int64_t n = (int64_t)N * ho * wo;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(bilinear_fwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, x, y);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const float* dy, float* dx, hipStream_t st) {
+  const int64_t n = (int64_t)N * hi * wi;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(bilinear_bwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------ column sums
+// out[c] (+)= sum_r x[r*ld + c]  -> f32 (bias gradients, reductions over objects)
+template <typename T>
+__global__ void colsum_kernel(int64_t rows, int cols, const void* x, int64_t ld, float* out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
+  float acc = 0.f;
+  for (int64_t r = r0; r < r1; ++r) acc += to_f32(((const T*)x)[r * ld + c]);
+  atomicAdd(&out[c], acc);
+}
+extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum,
+                          hipStream_t st) {
+  if (cols <= 0) return 0;
+  if (!accum) (void)hipMemsetAsync(out, 0, cols * sizeof(float), st);
+  if (rows <= 0) return (int)hipGetLastError();
+  const int cb = (cols + 255) / 256;
+  int64_t ry = (rows + 255) / 256;
+  int64_t want = 2048 / cb;
+  if (want < 1) want = 1;
+  if (ry > want) ry = want;
+  dim3 grid(cb, (unsigned)ry);
+  if (dt == S2H_BF16) hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, x, ld, out);
+  else hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, x, ld, out);
+  return (int)hipGetLastError();
+}
+// out[j] = sum_{o<O} x[o*inner + j]   written in T (broadcast-input gradients)
+template <typename T>
+__global__ void sum_outer_kernel(int O, int64_t inner, const void* x, void* out, int accum) {
+  GRID_STRIDE(j, inner) {
+    float v = 0.f;
+    for (int o = 0; o < O; ++o) v += to_f32(((const T*)x)[(int64_t)o * inner + j]);
+    if (accum) v += to_f32(((T*)out)[j]);
+    ((T*)out)[j] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* out, int accum, hipStream_t st) {
+  if (inner <= 0) return 0;
+  DISPATCH_T(dt, sum_outer_kernel, ew_grid(inner), O, inner, x, out, accum);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------ NHWC im2col
+// col[(b*Ho+oy)*Wo+ox][c*kh*kw + ky*kw + kx] = x[b][oy*s-p+ky][ox*s-p+kx][c]  (PyTorch weight order)
+template <typename T>
+__global__ void im2col_kernel(int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
+                              const void* x, void* col) {
+  const int Kc = C * kh * kw;
+  const int64_t n = (int64_t)B * Ho * Wo * Kc;
+  GRID_STRIDE(i, n) {
+    const int k = i % Kc;
+    const int64_t p = i / Kc;
+    const int ox = p % Wo;
+    const int oy = (p / Wo) % Ho;
+    const int b = p / ((int64_t)Wo * Ho);
+    const int c = k / (kh * kw), r = k % (kh * kw), ky = r / kw, kx = r % kw;
+    const int yy = oy * stride - pad + ky, xx = ox * stride - pad + kx;
+    float v = 0.f;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = to_f32(((const T*)x)[(((int64_t)b * H + yy) * W + xx) * C + c]);
+    ((T*)col)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_im2col(int dt, int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
+                          const void* x, void* col, hipStream_t st) {
+  const int64_t n = (int64_t)B * Ho * Wo * C * kh * kw;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, im2col_kernel, ew_grid(n), B, H, W, C, kh, kw, stride, pad, Ho, Wo, x, col);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------- depthwise KxK conv NHWC
+template <typename T>
+__global__ void dwconv_kernel(int B, int H, int W, int C, int K, int pad, const void* x, const float* w,
+                              const float* bias, void* y) {
+  const int64_t n = (int64_t)B * H * W * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    int64_t p = i / C;
+    const int xx = p % W; p /= W;
+    const int yy = p % H;
+    const int b = p / H;
+    float acc = bias ? bias[c] : 0.f;
+    for (int ky = 0; ky < K; ++ky) {
+      const int sy = yy - pad + ky;
+      if (sy < 0 || sy >= H) continue;
+      for (int kx = 0; kx < K; ++kx) {
+        const int sx = xx - pad + kx;
+        if (sx < 0 || sx >= W) continue;
+        acc += w[(c * K + ky) * K + kx] * to_f32(((const T*)x)[(((int64_t)b * H + sy) * W + sx) * C + c]);
+      }
+    }
+    ((T*)y)[i] = from_f32<T>(acc);
+  }
+}
+extern "C" int s2h_dwconv(int dt, int B, int H, int W, int C, int K, int pad, const void* x, const float* w,
+                          const float* bias, void* y, hipStream_t st) {
+  const int64_t n = (int64_t)B * H * W * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, dwconv_kernel, ew_grid(n), B, H, W, C, K, pad, x, w, bias, y);
+  return (int)hipGetLastError();
+}
+
+// -------------------------------------------- ConvTranspose2d(k=2, s=2) NHWC
+// GEMM output Y[(b,y,x)][co*4 + dy*2 + dx] (PyTorch weight [Ci, Co, 2, 2] as [Ci, Co*4])
+// scatter (dir 0): out[b,2y+dy,2x+dx,co] = Y[...] + bias[co] (+ add[...])
+// gather  (dir 1): dY[(b,y,x)][co*4+dy*2+dx] = dout[b,2y+dy,2x+dx,co]
+template <typename T>
+__global__ void convt2_kernel(int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                              void* out, int dir) {
+  const int64_t n = (int64_t)B * 2 * H * 2 * W * Co;
+  GRID_STRIDE(i, n) {
+    const int co = i % Co;
+    int64_t p = i / Co;
+    const int ox = p % (2 * W); p /= 2 * W;
+    const int oy = p % (2 * H);
+    const int b = p / (2 * H);
+    const int64_t yi = (((int64_t)b * H + oy / 2) * W + ox / 2) * (4 * Co) + co * 4 + (oy & 1) * 2 + (ox & 1);
+    if (dir == 0) {
+      float v = to_f32(((const T*)Y)[yi]) + (bias ? bias[co] : 0.f);
+      if (add) v += to_f32(((const T*)add)[i]);
+      ((T*)out)[i] = from_f32<T>(v);
+    } else {
+      ((T*)out)[yi] = ((const T*)Y)[i];
+    }
+  }
+}
+extern "C" int s2h_convt2(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                          void* out, int dir, hipStream_t st) {
+  const int64_t n = (int64_t)B * 4 * H * W * Co;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, convt2_kernel, ew_grid(n), B, H, W, Co, Y, bias, add, out, dir);
+  return (int)hipGetLastError();
+}
+
+// -------------------------------------------------- per-row gate / select
+// y[r, j] = gate[r] > 0 ? x[r, j] : fill ;  backward (dir 1): dx = gate > 0 ? dy : 0
+template <typename T>
+__global__ void row_gate_kernel(int64_t rows, int64_t inner, const void* x, const float* gate, float fill, void* y,
+                                int dir) {
+  const int64_t n = rows * inner;
+  GRID_STRIDE(i, n) {
+    const bool on = gate[i / inner] > 0.f;
+    float v = on ? to_f32(((const T*)x)[i]) : (dir == 0 ? fill : 0.f);
+    ((T*)y)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, float fill,
+                            void* y, int dir, hipStream_t st) {
+  if (rows * inner <= 0) return 0;
+  DISPATCH_T(dt, row_gate_kernel, ew_grid(rows * inner), rows, inner, x, gate, fill, y, dir);
+  return (int)hipGetLastError();
+}
+// y[r, j] = x[r, j] + (1 - (gate[r] > 0)) * vec[j]   (no-object embedding / pointer mixing)
+// if scale_x: y = (gate>0)*x + (1-(gate>0))*vec  (fixed_no_obj_ptr form)
+template <typename T>
+__global__ void gate_mix_kernel(int64_t rows, int64_t inner, const void* x, const float* gate, const void* vec,
+                                int vec_period, int scale_x, void* y) {
+  const int64_t n = rows * inner;
+  GRID_STRIDE(i, n) {
+    const float lam = gate[i / inner] > 0.f ? 1.f : 0.f;
+    float xv = to_f32(((const T*)x)[i]);
+    if (scale_x) xv *= lam;
+    const float v = xv + (1.f - lam) * to_f32(((const T*)vec)[(i % inner) % vec_period]);
+    ((T*)y)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_gate_mix(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, const void* vec,
+                            int vec_period, int scale_x, void* y, hipStream_t st) {
+  if (rows * inner <= 0) return 0;
+  DISPATCH_T(dt, gate_mix_kernel, ew_grid(rows * inner), rows, inner, x, gate, vec, vec_period, scale_x, y);
+  return (int)hipGetLastError();
+}

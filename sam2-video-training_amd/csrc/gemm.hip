@@ -1,0 +1,208 @@
+// MFMA-tiled GEMM with fused epilogue for every projection / MLP / 1x1-conv /
+// im2col-conv / hypernetwork product on the SAM2 training step.
+//
+//   C[b](m,n) = act(alpha * sum_k A[b](m,k) B[b](k,n) + bias) + R[b](m,n) + beta*C[b](m,n)
+//
+// A and B are addressed through (row, k) strides so the three products of a
+// Linear layer (fwd Y = X W^T, dgrad dX = dY W, wgrad dW = dY^T X) all run
+// without transposed copies: each operand is either K-contiguous ("KC") or
+// M/N-contiguous, selected at compile time.  Tiles are staged through LDS in a
+// K-contiguous [row][k] image so both MFMA operands read 16-B fragments.
+#include "common.h"
+
+struct GemmArgs {
+  int M, N, K;
+  const void* A; int64_t lda_m, lda_k, sA;
+  const void* B; int64_t ldb_k, ldb_n, sB;
+  void* C; int64_t ldc, sC;
+  const float* bias; int bias_mode;  // 0 none, 1 per column n, 2 per row m
+  const void* R; int64_t ldr, sR;
+  void* X; int64_t ldx, sX;  // aux: aux_mode 1 stores pre-activation, 2 multiplies by act'(X)
+  int aux_mode;
+  float alpha, beta; int act;
+  int vecA, vecB;
+};
+
+template <typename T, int ROWS, int BK, bool KC, int NTHR>
+struct TileLoader {
+  // Loads a ROWS x BK tile (row = m or n, k) into registers, then LDS [row][k].
+  static constexpr int VEC = 16 / sizeof(T);
+  static constexpr int NV = ROWS * BK / VEC / NTHR;
+  static_assert(NV >= 1, "tile too small for thread count");
+  uint4 r[NV];
+
+  __device__ __forceinline__ void load(const T* base, int64_t ld_row, int64_t ld_k, int row0, int k0,
+                                       int nrows, int K, bool vec_ok, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int v = tid + i * NTHR;
+      int row, k;
+      if (KC) { row = v / (BK / VEC); k = (v % (BK / VEC)) * VEC; }
+      else    { k = v / (ROWS / VEC); row = (v % (ROWS / VEC)) * VEC; }
+      int gr = row0 + row, gk = k0 + k;
+      bool full = KC ? (gr < nrows && gk + VEC <= K) : (gk < K && gr + VEC <= nrows);
+      if (full && vec_ok) {
+        const T* ptr = base + (int64_t)gr * ld_row + (int64_t)gk * ld_k;
+        r[i] = *(const uint4*)ptr;
+      } else {
+        T tmp[VEC];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) {
+          int rr = KC ? gr : gr + j;
+          int kk = KC ? gk + j : gk;
+          tmp[j] = (rr < nrows && kk < K) ? base[(int64_t)rr * ld_row + (int64_t)kk * ld_k] : from_f32<T>(0.f);
+        }
+        r[i] = *(uint4*)tmp;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(T* lds, int lds_stride, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      int v = tid + i * NTHR;
+      if (KC) {
+        int row = v / (BK / VEC), k = (v % (BK / VEC)) * VEC;
+        *(uint4*)(lds + row * lds_stride + k) = r[i];
+      } else {
+        int k = v / (ROWS / VEC), row = (v % (ROWS / VEC)) * VEC;
+        const T* t = (const T*)&r[i];
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) lds[(row + j) * lds_stride + k] = t[j];
+      }
+    }
+  }
+};
+
+template <typename T, typename TC, int BM, int BN, bool AKC, bool BKC>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
+  constexpr int BK = 32;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int LS = BK + VEC;  // LDS row stride (elements): +16 B pad
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  using MF = Mfma<T>;
+  __shared__ __attribute__((aligned(16))) T As[BM * LS];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * LS];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int bz = blockIdx.z;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const T* A = (const T*)p.A + (int64_t)bz * p.sA;
+  const T* B = (const T*)p.B + (int64_t)bz * p.sB;
+
+  TileLoader<T, BM, BK, AKC, 256> la;
+  TileLoader<T, BN, BK, BKC, 256> lb;
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (p.K + BK - 1) / BK;
+  la.load(A, p.lda_m, p.lda_k, m0, 0, p.M, p.K, p.vecA, tid);
+  lb.load(B, p.ldb_n, p.ldb_k, n0, 0, p.N, p.K, p.vecB, tid);
+  for (int kt = 0; kt < nk; ++kt) {
+    la.store(As, LS, tid);
+    lb.store(Bs, LS, tid);
+    __syncthreads();
+    if (kt + 1 < nk) {
+      la.load(A, p.lda_m, p.lda_k, m0, (kt + 1) * BK, p.M, p.K, p.vecA, tid);
+      lb.load(B, p.ldb_n, p.ldb_k, n0, (kt + 1) * BK, p.N, p.K, p.vecB, tid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += MF::KSTEP) {
+      typename MF::frag a[MI], b[NI];
+      const int kof = ks + (lane >> 4) * MF::KPL;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = MF::load(&As[(wm * WM + i * 16 + (lane & 15)) * LS + kof]);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = MF::load(&Bs[(wn * WN + j * 16 + (lane & 15)) * LS + kof]);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] = MF::mma(a[i], b[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+
+  TC* C = (TC*)p.C + (int64_t)bz * p.sC;
+  const TC* R = p.R ? (const TC*)p.R + (int64_t)bz * p.sR : nullptr;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      int col = n0 + wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        if (row < p.M && col < p.N) {
+          float v = p.alpha * acc[i][j][r];
+          if (p.bias_mode == 1) v += p.bias[col];
+          else if (p.bias_mode == 2) v += p.bias[row];
+          if (p.aux_mode == 1) ((TC*)p.X)[(int64_t)bz * p.sX + (int64_t)row * p.ldx + col] = from_f32<TC>(v);
+          if (p.aux_mode == 2) v *= act_grad(to_f32(((const TC*)p.X)[(int64_t)bz * p.sX + (int64_t)row * p.ldx + col]), p.act);
+          else v = apply_act(v, p.act);
+          if (R) v += to_f32(R[(int64_t)row * p.ldr + col]);
+          int64_t off = (int64_t)row * p.ldc + col;
+          if (p.beta != 0.f) v += p.beta * to_f32(C[off]);
+          C[off] = from_f32<TC>(v);
+        }
+      }
+    }
+}
+
+template <typename T, typename TC, int BM, int BN>
+static int launch_gemm_tiles(const GemmArgs& a, int batch, hipStream_t st) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch);
+  bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
+  if (akc && bkc) hipLaunchKernelGGL((gemm_kernel<T, TC, BM, BN, true, true>), grid, dim3(256), 0, st, a);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm_kernel<T, TC, BM, BN, true, false>), grid, dim3(256), 0, st, a);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm_kernel<T, TC, BM, BN, false, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((gemm_kernel<T, TC, BM, BN, false, false>), grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <typename T, typename TC>
+static int launch_gemm(const GemmArgs& a, int batch, hipStream_t st) {
+  // Small problems: 64x64 tiles keep enough workgroups in flight on 256 CUs.
+  long tiles128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch;
+  if (tiles128 >= 512) return launch_gemm_tiles<T, TC, 128, 128>(a, batch, st);
+  return launch_gemm_tiles<T, TC, 64, 64>(a, batch, st);
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
+                        const void* A, int64_t lda_m, int64_t lda_k, int64_t sA,
+                        const void* B, int64_t ldb_k, int64_t ldb_n, int64_t sB,
+                        void* C, int64_t ldc, int64_t sC,
+                        const float* bias, int bias_mode,
+                        const void* R, int64_t ldr, int64_t sR,
+                        void* X, int64_t ldx, int64_t sX, int aux_mode,
+                        float alpha, float beta, int act, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  if (!(lda_k == 1 || lda_m == 1) || !(ldb_k == 1 || ldb_n == 1)) return (int)hipErrorInvalidValue;
+  if (dt_ab == S2H_F32 && dt_c != S2H_F32) return (int)hipErrorInvalidValue;
+  GemmArgs a;
+  a.M = M; a.N = N; a.K = K;
+  a.A = A; a.lda_m = lda_m; a.lda_k = lda_k; a.sA = sA;
+  a.B = B; a.ldb_k = ldb_k; a.ldb_n = ldb_n; a.sB = sB;
+  a.C = C; a.ldc = ldc; a.sC = sC;
+  a.bias = bias; a.bias_mode = bias ? bias_mode : 0;
+  a.R = R; a.ldr = ldr; a.sR = sR;
+  a.X = X; a.ldx = ldx; a.sX = sX; a.aux_mode = X ? aux_mode : 0;
+  a.alpha = alpha; a.beta = beta; a.act = act;
+  const int esz = dt_ab == S2H_BF16 ? 2 : 4;
+  const int vec = 16 / esz;
+  // vector loads need a 16-B aligned base, and every row start 16-B aligned
+  int64_t lda_row = (lda_k == 1) ? lda_m : lda_k;
+  int64_t ldb_row = (ldb_k == 1) ? ldb_n : ldb_k;
+  a.vecA = aligned16(A) && (lda_row % vec == 0) && (batch == 1 || sA % vec == 0);
+  a.vecB = aligned16(B) && (ldb_row % vec == 0) && (batch == 1 || sB % vec == 0);
+  if (K <= 0) {
+    a.K = 0;
+  }
+  if (dt_ab == S2H_F32) return launch_gemm<float, float>(a, batch, stream);
+  if (dt_c == S2H_BF16) return launch_gemm<bf16, bf16>(a, batch, stream);
+  return launch_gemm<bf16, float>(a, batch, stream);
+}

@@ -1,0 +1,265 @@
+// Fused mask loss of MultiStepMultiMasksAndIous (losses.py:20-76, 143-238):
+// sigmoid focal (alpha .25, gamma 2) + Dice (+1 smoothing) + IoU-L1, with the
+// per-frame valid-category filter and logit temperature; plus the category
+// merge of masks.py:53-213 (pixelwise max for masks, sigmoid-mass weighted mean
+// for IoU predictions) with its backward.
+//
+// stats[n] = {sum focal, sum sigma, sum t, sum sigma*t, |pred & gt|, |pred | gt|}
+#include "common.h"
+
+#define NSTAT 6
+
+__device__ __forceinline__ float focal_elem(float x, float t, float& p) {
+  p = 1.f / (1.f + expf(-x));
+  const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  const float pt = p * t + (1.f - p) * (1.f - t);
+  const float at = 0.25f * t + 0.75f * (1.f - t);
+  const float q = 1.f - pt;
+  return at * ce * q * q;
+}
+
+// grid (chunks, N): block-reduce partial sums, atomically added into stats (zeroed by caller)
+__global__ __launch_bounds__(256) void mask_stats_kernel(int N, int64_t P, const float* x, int64_t ldx,
+                                                         const uint8_t* tgt, int64_t ldt, float inv_temp,
+                                                         float* stats) {
+  const int n = blockIdx.y;
+  const int64_t chunk = (P + gridDim.x - 1) / gridDim.x;
+  const int64_t p0 = blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+  float acc[NSTAT] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+    const float xv = x[n * ldx + p] * inv_temp;
+    const float t = tgt ? (tgt[n * ldt + p] ? 1.f : 0.f) : 0.f;
+    float s;
+    const float f = focal_elem(xv, t, s);
+    const bool pr = xv > 0.f, gt = t > 0.f;
+    acc[0] += f; acc[1] += s; acc[2] += t; acc[3] += s * t;
+    acc[4] += (pr && gt) ? 1.f : 0.f;
+    acc[5] += (pr || gt) ? 1.f : 0.f;
+  }
+  __shared__ float red[4][NSTAT];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < NSTAT; ++k) {
+    float v = wave_sum(acc[k]);
+    if (lane == 0) red[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < NSTAT) {
+    float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(&stats[n * NSTAT + threadIdx.x], v);
+  }
+}
+
+extern "C" int s2h_mask_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                              float inv_temp, float* stats, hipStream_t st) {
+  if (N <= 0) return 0;
+  (void)hipMemsetAsync(stats, 0, N * NSTAT * sizeof(float), st);
+  int chunks = (int)((P + 4095) / 4096);
+  if (chunks > 256) chunks = 256;
+  if (chunks < 1) chunks = 1;
+  hipLaunchKernelGGL(mask_stats_kernel, dim3(chunks, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp, stats);
+  return (int)hipGetLastError();
+}
+
+// One frame: losses[0..3] += {mask, dice, iou, total}; per-row backward coefficients.
+// coef[n*4 + 0] = focal coefficient, [1] dice A, [2] dice B, [3] d pred_iou.
+__global__ void mask_loss_finalize_kernel(int N, int64_t P, const float* stats, const float* pred_iou,
+                                          const int* valid, float w_mask, float w_dice, float w_iou, float gscale,
+                                          float* losses, float* coef) {
+  if (threadIdx.x != 0) return;
+  int nv = 0;
+  for (int n = 0; n < N; ++n) nv += valid[n] ? 1 : 0;
+  const float inv_nv = nv > 0 ? 1.f / (float)nv : 0.f;
+  float lm = 0.f, ld = 0.f, li = 0.f;
+  for (int n = 0; n < N; ++n) {
+    const float* s = stats + n * NSTAT;
+    float* c = coef + n * 4;
+    if (!valid[n]) { c[0] = c[1] = c[2] = c[3] = 0.f; continue; }
+    lm += s[0] / (float)P;
+    const float den = s[1] + s[2] + 1.f;
+    ld += 1.f - (2.f * s[3] + 1.f) / den;
+    const float actual = s[4] / fmaxf(s[5], 1.f);
+    const float diff = pred_iou[n] - actual;
+    li += fabsf(diff);
+    const float cd = gscale * w_dice * inv_nv;
+    c[0] = gscale * w_mask * inv_nv / (float)P;
+    c[1] = cd * 2.f / den;
+    c[2] = cd * (2.f * s[3] + 1.f) / (den * den);
+    c[3] = gscale * w_iou * inv_nv * (diff > 0.f ? 1.f : (diff < 0.f ? -1.f : 0.f));
+  }
+  lm *= inv_nv; ld *= inv_nv; li *= inv_nv;
+  losses[0] += lm;
+  losses[1] += ld;
+  losses[2] += li;
+  losses[3] += w_mask * lm + w_dice * ld + w_iou * li;
+}
+extern "C" int s2h_mask_loss_finalize(int N, int64_t P, const float* stats, const float* pred_iou, const int* valid,
+                                      float w_mask, float w_dice, float w_iou, float gscale, float* losses,
+                                      float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(mask_loss_finalize_kernel, dim3(1), dim3(64), 0, st, N, P, stats, pred_iou, valid, w_mask,
+                     w_dice, w_iou, gscale, losses, coef);
+  return (int)hipGetLastError();
+}
+
+// dx[n,p] = inv_temp * ( cf * dfocal/dx + (-(A t - B)) * sigma' )
+__global__ void mask_loss_bwd_kernel(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                                     float inv_temp, const float* coef, float* dx, int64_t lddx) {
+  const int64_t n_all = (int64_t)N * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = i / P;
+    const int64_t p = i - (int64_t)n * P;
+    const float* c = coef + n * 4;
+    float g = 0.f;
+    if (c[0] != 0.f || c[1] != 0.f || c[2] != 0.f) {
+      const float xv = x[n * ldx + p] * inv_temp;
+      const float t = tgt[n * ldt + p] ? 1.f : 0.f;
+      const float s = 1.f / (1.f + expf(-xv));
+      const float ds = s * (1.f - s);
+      const float ce = fmaxf(xv, 0.f) - xv * t + log1pf(expf(-fabsf(xv)));
+      const float pt = s * t + (1.f - s) * (1.f - t);
+      const float at = 0.25f * t + 0.75f * (1.f - t);
+      const float q = 1.f - pt;
+      const float dfocal = at * (-2.f * q * (2.f * t - 1.f) * ds * ce + q * q * (s - t));
+      g = c[0] * dfocal - (c[1] * t - c[2]) * ds;
+    }
+    dx[n * lddx + p] = g * inv_temp;
+  }
+}
+extern "C" int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                                 float inv_temp, const float* coef, float* dx, int64_t lddx, hipStream_t st) {
+  const int64_t n = (int64_t)N * P;
+  if (n <= 0) return 0;
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(mask_loss_bwd_kernel, dim3((unsigned)b), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
+                     coef, dx, lddx);
+  return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------- category merge
+// cat_off[c]..cat_off[c+1] index into cat_obj (object ids of category c).
+__global__ void group_max_fwd_kernel(int Ncat, int64_t P, const int* cat_off, const int* cat_obj, const float* x,
+                                     int64_t ldx, float* y, int64_t ldy, int* arg) {
+  const int64_t n = (int64_t)Ncat * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int c = i / P;
+    const int64_t p = i - (int64_t)c * P;
+    float m = 0.f;
+    int best = -1;
+    for (int k = cat_off[c]; k < cat_off[c + 1]; ++k) {
+      const int o = cat_obj[k];
+      const float v = x[o * ldx + p];
+      if (best < 0 || v > m) { m = v; best = o; }
+    }
+    y[c * ldy + p] = m;
+    if (arg) arg[i] = best;
+  }
+}
+// dx[o,p] = (arg[cat(o),p] == o) ? dy[cat(o),p] : 0
+__global__ void group_max_bwd_kernel(int O, int64_t P, const int* obj_cat, const int* arg, const float* dy,
+                                     int64_t lddy, float* dx, int64_t lddx) {
+  const int64_t n = (int64_t)O * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int o = i / P;
+    const int64_t p = i - (int64_t)o * P;
+    const int c = obj_cat[o];
+    dx[o * lddx + p] = (arg[(int64_t)c * P + p] == o) ? dy[c * lddy + p] : 0.f;
+  }
+}
+extern "C" int s2h_group_max_fwd(int Ncat, int64_t P, const int* cat_off, const int* cat_obj, const float* x,
+                                 int64_t ldx, float* y, int64_t ldy, int* arg, hipStream_t st) {
+  const int64_t n = (int64_t)Ncat * P;
+  if (n <= 0) return 0;
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(group_max_fwd_kernel, dim3((unsigned)b), dim3(256), 0, st, Ncat, P, cat_off, cat_obj, x, ldx, y,
+                     ldy, arg);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_group_max_bwd(int O, int64_t P, const int* obj_cat, const int* arg, const float* dy, int64_t lddy,
+                                 float* dx, int64_t lddx, hipStream_t st) {
+  const int64_t n = (int64_t)O * P;
+  if (n <= 0) return 0;
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(group_max_bwd_kernel, dim3((unsigned)b), dim3(256), 0, st, O, P, obj_cat, arg, dy, lddy, dx,
+                     lddx);
+  return (int)hipGetLastError();
+}
+
+// weighted mean per category: y[c] = sum w_o x_o / sum w_o  (plain mean when sum w == 0; 0 if empty)
+// w_o = sum of sigmoid of object o's high-res logits (stats[o*NSTAT + 1]); K values per object.
+__global__ void group_wavg_kernel(int Ncat, int K, const int* cat_off, const int* cat_obj, const float* stats,
+                                  const float* x, float* y) {
+  const int i = threadIdx.x + blockIdx.x * blockDim.x;
+  if (i >= Ncat * K) return;
+  const int c = i / K, k = i % K;
+  float sw = 0.f, sx = 0.f, sm = 0.f;
+  const int cnt = cat_off[c + 1] - cat_off[c];
+  for (int j = cat_off[c]; j < cat_off[c + 1]; ++j) {
+    const int o = cat_obj[j];
+    const float w = stats[o * NSTAT + 1];
+    sw += w; sx += w * x[o * K + k]; sm += x[o * K + k];
+  }
+  y[i] = cnt == 0 ? 0.f : (sw == 0.f ? sm / cnt : sx / sw);
+}
+// backward: dx[o,k] = dy[c,k] * w_o / W ; dw[o] = sum_k dy[c,k] (x_o - y_c) / W   (mean form when W == 0)
+__global__ void group_wavg_bwd_kernel(int O, int K, const int* obj_cat, const int* cat_off, const float* stats,
+                                      const float* x, const float* y, const float* dy, float* dx, float* dw) {
+  const int o = threadIdx.x + blockIdx.x * blockDim.x;
+  if (o >= O) return;
+  const int c = obj_cat[o];
+  const int cnt = cat_off[c + 1] - cat_off[c];
+  float sw = 0.f, acc_w = 0.f;
+  for (int oo = 0; oo < O; ++oo)
+    if (obj_cat[oo] == c) sw += stats[oo * NSTAT + 1];
+  const float wo = stats[o * NSTAT + 1];
+  for (int k = 0; k < K; ++k) {
+    const float g = dy[c * K + k];
+    if (sw == 0.f) {
+      dx[o * K + k] = g / cnt;
+    } else {
+      dx[o * K + k] = g * wo / sw;
+      acc_w += g * (x[o * K + k] - y[c * K + k]) / sw;
+    }
+  }
+  dw[o] = acc_w;
+}
+extern "C" int s2h_group_wavg_fwd(int Ncat, int K, const int* cat_off, const int* cat_obj, const float* stats,
+                                  const float* x, float* y, hipStream_t st) {
+  if (Ncat * K <= 0) return 0;
+  hipLaunchKernelGGL(group_wavg_kernel, dim3((Ncat * K + 63) / 64), dim3(64), 0, st, Ncat, K, cat_off, cat_obj, stats,
+                     x, y);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_group_wavg_bwd(int O, int K, const int* obj_cat, const int* cat_off, const float* stats,
+                                  const float* x, const float* y, const float* dy, float* dx, float* dw,
+                                  hipStream_t st) {
+  if (O <= 0) return 0;
+  hipLaunchKernelGGL(group_wavg_bwd_kernel, dim3((O + 63) / 64), dim3(64), 0, st, O, K, obj_cat, cat_off, stats, x, y,
+                     dy, dx, dw);
+  return (int)hipGetLastError();
+}
+
+// dx[r,p] += coef[r] * sigma'(x[r,p])   (gradient through the sigmoid-mass merge weights)
+__global__ void sigmoid_grad_axpy_kernel(int R, int64_t P, const float* x, int64_t ldx, const float* coef, float* dx,
+                                         int64_t lddx) {
+  const int64_t n = (int64_t)R * P;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int r = i / P;
+    const int64_t p = i - (int64_t)r * P;
+    const float c = coef[r];
+    if (c == 0.f) continue;
+    const float s = 1.f / (1.f + expf(-x[r * ldx + p]));
+    dx[r * lddx + p] += c * s * (1.f - s);
+  }
+}
+extern "C" int s2h_sigmoid_grad_axpy(int R, int64_t P, const float* x, int64_t ldx, const float* coef, float* dx,
+                                     int64_t lddx, hipStream_t st) {
+  const int64_t n = (int64_t)R * P;
+  if (n <= 0) return 0;
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(sigmoid_grad_axpy_kernel, dim3((unsigned)b), dim3(256), 0, st, R, P, x, ldx, coef, dx, lddx);
+  return (int)hipGetLastError();
+}

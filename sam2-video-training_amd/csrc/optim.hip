@@ -1,0 +1,76 @@
+// Optimizer step over the flat fp32 parameter / gradient arena:
+// global grad-norm (deterministic two-stage reduction), clip_grad_norm_ factor
+// computed on device (no host sync), and a fused AdamW update that applies the
+// clip factor on the fly (torch.optim.AdamW semantics, trainer.py:124-130:
+// decoupled decay p *= 1 - lr*wd, m.lerp_(g, 1-b1), v = b2*v + (1-b2) g^2,
+// p -= lr/bc1 * m / (sqrt(v)/sqrt(bc2) + eps)).
+// Also: fp32 -> bf16 shadow-weight refresh for the bf16 compute path.
+#include "common.h"
+
+// partial[b] = sum over block b of x^2
+__global__ __launch_bounds__(256) void sumsq_kernel(int64_t n, const float* x, float* partial) {
+  float acc = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) acc += x[i] * x[i];
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+// out[0] = sqrt(sum partial); out[1] = clip coefficient min(1, max_norm / (norm + 1e-6)) (1 if max_norm <= 0)
+__global__ __launch_bounds__(256) void norm_finalize_kernel(int nb, const float* partial, float max_norm, float* out) {
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) acc += partial[i];
+  __shared__ float red[4];
+  acc = wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+    out[0] = norm;
+    float c = 1.f;
+    if (max_norm > 0.f) {
+      c = max_norm / (norm + 1e-6f);
+      if (c > 1.f) c = 1.f;
+    }
+    out[1] = c;
+  }
+}
+#define NORM_BLOCKS 1024
+extern "C" int s2h_grad_norm(int64_t n, const float* g, float* partial_ws, float max_norm, float* out,
+                             hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(NORM_BLOCKS), dim3(256), 0, st, n, g, partial_ws);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, st, NORM_BLOCKS, partial_ws, max_norm, out);
+  return (int)hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* p, const float* g, float* m, float* v,
+                                                    const float* clip, float lr, float beta1, float beta2, float eps,
+                                                    float wd, float step_size, float bc2_sqrt, bf16* shadow) {
+  const float cf = clip ? clip[1] : 1.f;
+  const float w1 = 1.f - beta1;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float gi = g[i] * cf;
+    float pi = p[i] * (1.f - lr * wd);
+    float mi = m[i];
+    mi = mi + w1 * (gi - mi);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi; m[i] = mi; v[i] = vi;
+    if (shadow) shadow[i] = (bf16)pi;
+  }
+}
+extern "C" int s2h_adamw(int64_t n, float* p, const float* g, float* m, float* v, const float* clip, float lr,
+                         float beta1, float beta2, float eps, float wd, int step, void* bf16_shadow, hipStream_t st) {
+  if (n <= 0) return 0;
+  const double bc1 = 1.0 - pow((double)beta1, (double)step);
+  const double bc2 = 1.0 - pow((double)beta2, (double)step);
+  const float step_size = (float)(lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  int64_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)b), dim3(256), 0, st, n, p, g, m, v, clip, lr, beta1, beta2, eps, wd,
+                     step_size, bc2_sqrt, (bf16*)bf16_shadow);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,65 @@
+// Library metadata + in-library launch profiler.
+//
+// s2h_prof_enable(cap) pre-creates `cap` event pairs; while enabled every
+// attention-forward launch is bracketed by hipEventRecord on the stream it is
+// launched on, together with its shape (B*H, Lq, Lk, D).  bench.py reads the
+// per-launch durations back with s2h_prof_read to price the dominant kernel
+// against the bf16 MFMA roofline (no host sync inside the timed region).
+#include "common.h"
+#include <vector>
+#include <mutex>
+
+extern "C" int s2h_version() { return 1; }
+
+namespace {
+struct ProfRec { hipEvent_t a, b; int64_t meta[5]; };
+std::mutex g_mu;
+std::vector<ProfRec> g_pool;
+int g_used = 0;
+bool g_on = false;
+}  // namespace
+
+extern "C" int s2h_prof_enable(int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& r : g_pool) { (void)hipEventDestroy(r.a); (void)hipEventDestroy(r.b); }
+  g_pool.clear();
+  g_used = 0;
+  g_on = cap > 0;
+  for (int i = 0; i < cap; ++i) {
+    ProfRec r;
+    if (hipEventCreate(&r.a) != hipSuccess || hipEventCreate(&r.b) != hipSuccess) return (int)hipErrorOutOfMemory;
+    g_pool.push_back(r);
+  }
+  return 0;
+}
+extern "C" int s2h_prof_reset() { std::lock_guard<std::mutex> lk(g_mu); g_used = 0; return 0; }
+extern "C" int s2h_prof_count() { std::lock_guard<std::mutex> lk(g_mu); return g_used; }
+
+// internal: returns slot index or -1
+int s2h_prof_begin(hipStream_t st, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4) {
+  if (!g_on) return -1;
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_used >= (int)g_pool.size()) return -1;
+  int i = g_used++;
+  g_pool[i].meta[0] = m0; g_pool[i].meta[1] = m1; g_pool[i].meta[2] = m2; g_pool[i].meta[3] = m3; g_pool[i].meta[4] = m4;
+  (void)hipEventRecord(g_pool[i].a, st);
+  return i;
+}
+void s2h_prof_end(int slot, hipStream_t st) {
+  if (slot < 0) return;
+  (void)hipEventRecord(g_pool[slot].b, st);
+}
+
+// ms[i] = duration of record i; meta[5*i..] = its shape. Synchronises on the events.
+extern "C" int s2h_prof_read(int max, float* ms, int64_t* meta) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int n = g_used < max ? g_used : max;
+  for (int i = 0; i < n; ++i) {
+    (void)hipEventSynchronize(g_pool[i].b);
+    float t = 0.f;
+    (void)hipEventElapsedTime(&t, g_pool[i].a, g_pool[i].b);
+    ms[i] = t;
+    for (int k = 0; k < 5; ++k) meta[5 * i + k] = g_pool[i].meta[k];
+  }
+  return n;
+}

@@ -1,0 +1,101 @@
+"""ctypes binding of libsam2hip.so (the C ABI declared in include/sam2hip.h).
+
+The library is the product: there is no CPU or PyTorch fallback.  Loading fails
+loudly when the shared object is missing, and every launch checks the HIP
+status it returns.  `torch` is imported first so the HIP runtime torch ships
+(same SONAME libamdhip64.so.7) is the one the library binds to: a single
+runtime, shared streams and device pointers.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import c_float, c_int, c_int64, c_uint64, c_void_p
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libsam2hip.so")
+
+P = c_void_p
+I = c_int
+L = c_int64
+F = c_float
+
+# name -> argtypes (restype is int: a hipError_t value, 0 == success)
+SIGNATURES = {
+    "s2h_version": [],
+    "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, F, F, I, P],
+    "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P],
+    "s2h_attn_bwd": [I, I, I, I, I, I,
+                     P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
+                     P, L, L, L, P, L, L, L, P, L, L, L,
+                     P, P, F, F, c_uint64, P],
+    "s2h_layernorm_fwd": [I, I, I, P, L, P, L, I, P, P, P, F, P, L, P, P, P],
+    "s2h_layernorm_bwd": [I, I, I, P, L, P, L, P, P, P, P, L, I, P, P, P],
+    "s2h_add": [I, L, P, P, F, F, P, P],
+    "s2h_add_bcast": [I, L, L, P, F, P, L, F, P, P],
+    "s2h_act_fwd": [I, L, P, I, F, F, P, P],
+    "s2h_act_bwd": [I, L, P, P, I, P, I, P],
+    "s2h_cast": [I, I, L, P, P, P],
+    "s2h_dropout": [I, L, P, P, F, c_uint64, P, P],
+    "s2h_rope": [I, L, I, I, P, L, L, P, L, L, P, P, I, I, P],
+    "s2h_maxpool2_fwd": [I, I, I, I, I, P, L, P, P],
+    "s2h_maxpool2_bwd": [I, I, I, I, I, P, L, P, P, L, P],
+    "s2h_window": [I, I, I, I, I, I, P, P, I, I, P],
+    "s2h_up2_add": [I, I, I, I, I, P, P, P, P],
+    "s2h_pool2_sum": [I, I, I, I, I, P, P, I, P],
+    "s2h_bilinear_fwd": [I, I, I, I, I, P, P, P],
+    "s2h_bilinear_bwd": [I, I, I, I, I, P, P, P],
+    "s2h_colsum": [I, L, I, P, L, P, I, P],
+    "s2h_sum_outer": [I, I, L, P, P, I, P],
+    "s2h_im2col": [I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "s2h_dwconv": [I, I, I, I, I, I, I, P, P, P, P, P],
+    "s2h_convt2": [I, I, I, I, I, P, P, P, P, I, P],
+    "s2h_row_gate": [I, L, L, P, P, F, P, I, P],
+    "s2h_gate_mix": [I, L, L, P, P, P, I, I, P, P],
+    "s2h_mask_stats": [I, L, P, L, P, L, F, P, P],
+    "s2h_mask_loss_finalize": [I, L, P, P, P, F, F, F, F, P, P, P],
+    "s2h_mask_loss_bwd": [I, L, P, L, P, L, F, P, P, L, P],
+    "s2h_group_max_fwd": [I, L, P, P, P, L, P, L, P, P],
+    "s2h_group_max_bwd": [I, L, P, P, P, L, P, L, P],
+    "s2h_group_wavg_fwd": [I, I, P, P, P, P, P, P],
+    "s2h_group_wavg_bwd": [I, I, P, P, P, P, P, P, P, P, P],
+    "s2h_sigmoid_grad_axpy": [I, L, P, L, P, P, L, P],
+    "s2h_grad_norm": [L, P, P, F, P, P],
+    "s2h_adamw": [L, P, P, P, P, P, F, F, F, F, F, I, P, P],
+    "s2h_prof_enable": [I],
+    "s2h_prof_reset": [],
+    "s2h_prof_count": [],
+    "s2h_prof_read": [I, P, P],
+}
+
+_LIB = None
+
+
+class HipKernelError(RuntimeError):
+    pass
+
+
+def lib():
+    """The loaded library (raises if it is missing: no fallback path exists)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"libsam2hip.so not found at {LIB_PATH}; build it with `python __graft_entry__.py` "
+                "or `make -C sam2-video-training_amd/csrc` (there is no CPU fallback)")
+        h = ctypes.CDLL(LIB_PATH)
+        for name, argtypes in SIGNATURES.items():
+            fn = getattr(h, name)
+            fn.argtypes = argtypes
+            fn.restype = c_int
+        _LIB = h
+    return _LIB
+
+
+def call(name, *args):
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise HipKernelError(f"{name} failed with hipError {rc}")
+    return rc

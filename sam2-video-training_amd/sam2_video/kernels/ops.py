@@ -1,0 +1,429 @@
+"""Tensor-level launchers for libsam2hip (no autograd).  Every function launches
+on torch's current HIP stream and returns its output tensor(s).
+
+Conventions: activations are float32 (fp32-parity mode) or bfloat16 (compute
+mode); norms' gamma/beta, biases, LSE/statistics and weight gradients are fp32.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from ._lib import call
+
+F32, BF16 = 0, 1
+ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "sigmoid": 3}
+
+
+def dt(t: torch.Tensor) -> int:
+    if t.dtype == torch.float32:
+        return F32
+    if t.dtype == torch.bfloat16:
+        return BF16
+    raise TypeError(f"libsam2hip supports float32/bfloat16 activations, got {t.dtype}")
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise RuntimeError("libsam2hip kernels run on the GPU only (tensor on %s)" % t.device)
+
+
+# ----------------------------------------------------------------- GEMM
+def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB=0, sC=0,
+         bias=None, bias_mode=1, residual=None, ldr=0, sR=0, aux=None, ldx=0, sX=0, aux_mode=0,
+         alpha=1.0, beta=0.0, act=0):
+    _dev(a, b, c, bias, residual, aux)
+    if bias is not None:
+        assert bias.dtype == torch.float32 and bias.is_contiguous()
+    call("s2h_gemm", dt(a), dt(c), batch, M, N, K,
+         ptr(a), lda_m, lda_k, sA, ptr(b), ldb_k, ldb_n, sB, ptr(c), ldc, sC,
+         ptr(bias), bias_mode, ptr(residual), ldr, sR, ptr(aux), ldx, sX, aux_mode,
+         float(alpha), float(beta), int(act), stream())
+    return c
+
+
+def _rows(x):
+    assert x.stride(-1) == 1, "last dim must be contiguous"
+    return x.numel() // x.shape[-1], x.shape[-1]
+
+
+def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dtype=None):
+    """out = act(x @ w^T + bias) (+ residual); optionally stores the pre-activation in `pre`."""
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N = w.shape[0]
+    assert w.shape[1] == K and w.is_contiguous()
+    if out is None:
+        out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=out_dtype or x.dtype)
+    o2 = out.view(-1, N)
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    p2 = pre.view(-1, N) if pre is not None else None
+    gemm(x2, w, o2, M=M, N=N, K=K, lda_m=x2.stride(0), lda_k=1, ldb_k=1, ldb_n=K, ldc=N,
+         bias=bias, residual=r2, ldr=N, aux=p2, ldx=N, aux_mode=1 if pre is not None else 0, act=ACT[act])
+    return out
+
+
+def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None):
+    """dx = dy @ w   (optionally * act'(pre) elementwise, fusing the previous layer's activation grad)."""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    M, N = dy2.shape
+    K = w.shape[1]
+    if dx is None:
+        dx = torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=dy.dtype)
+    d2 = dx.view(-1, K)
+    p2 = pre.reshape(-1, K) if pre is not None else None
+    gemm(dy2, w, d2, M=M, N=K, K=N, lda_m=dy2.stride(0), lda_k=1, ldb_k=K, ldb_n=1, ldc=K,
+         aux=p2, ldx=K, aux_mode=2 if pre is not None else 0, act=ACT[act] if pre is not None else 0,
+         beta=1.0 if accumulate else 0.0)
+    return dx
+
+
+def linear_wgrad(dy, x, dw, accumulate=True):
+    """dw (fp32 [N, K]) (+)= dy^T @ x."""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    x2 = x.reshape(-1, x.shape[-1])
+    M, N = dy2.shape
+    K = x2.shape[1]
+    assert dw.dtype == torch.float32 and dw.shape == (N, K)
+    gemm(dy2, x2, dw, M=N, N=K, K=M, lda_m=1, lda_k=dy2.stride(0), ldb_k=x2.stride(0), ldb_n=1, ldc=K,
+         beta=1.0 if accumulate else 0.0)
+    return dw
+
+
+def bmm(a, b, out, *, trans_b=False, alpha=1.0, beta=0.0):
+    """Batched out[i] = a[i] @ b[i] (or b[i]^T): a [Bt, M, K], b [Bt, K, N] / [Bt, N, K]."""
+    Bt, M, K = a.shape
+    if trans_b:
+        N = b.shape[1]
+        ldb_k, ldb_n = b.stride(2), b.stride(1)
+    else:
+        N = b.shape[2]
+        ldb_k, ldb_n = b.stride(1), b.stride(2)
+    gemm(a, b, out, M=M, N=N, K=K, lda_m=a.stride(1), lda_k=a.stride(2), ldb_k=ldb_k, ldb_n=ldb_n,
+         ldc=out.stride(1), batch=Bt, sA=a.stride(0), sB=b.stride(0), sC=out.stride(0), alpha=alpha, beta=beta)
+    return out
+
+
+# ------------------------------------------------------------ attention
+def _bhl(t):
+    """strides (batch, head, row) of a [B, L, H, D] view with contiguous D"""
+    assert t.stride(3) == 1
+    return t.stride(0), t.stride(2), t.stride(1)
+
+
+def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0):
+    """q [B, Lq, H, D], k/v [B, Lk, H, D] (any strides, D contiguous) -> o [B, Lq, H, D], lse [B, H, Lq] f32"""
+    _dev(q, k, v, o, lse)
+    B, Lq, H, D = q.shape
+    Lk = k.shape[1]
+    call("s2h_attn_fwd", dt(q), B, H, Lq, Lk, D, ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v),
+         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), stream())
+    return o, lse
+
+
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0):
+    _dev(q, k, v, o, do, lse, dq, dk, dv)
+    B, Lq, H, D = q.shape
+    Lk = k.shape[1]
+    di = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
+    call("s2h_attn_bwd", dt(q), B, H, Lq, Lk, D,
+         ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
+         ptr(dq), *_bhl(dq), ptr(dk), *_bhl(dk), ptr(dv), *_bhl(dv),
+         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), stream())
+    return dq, dk, dv
+
+
+# ------------------------------------------------------------ layernorm
+def layernorm_fwd(x, gamma, beta, eps, y=None, add=None, add_bcast=False, xsum=None):
+    """y = LN(x [+ add]) over the last dim; returns (y, mean, rstd).  If add is given the
+    sum is written to xsum (residual stream)."""
+    rows, C = _rows(x)
+    if y is None:
+        y = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+    mean = torch.empty(rows, device=x.device, dtype=torch.float32)
+    rstd = torch.empty(rows, device=x.device, dtype=torch.float32)
+    call("s2h_layernorm_fwd", dt(x), rows, C, ptr(x), x.stride(-2) if x.dim() > 1 else C,
+         ptr(add), (add.stride(-2) if (add is not None and add.dim() > 1) else C), int(add_bcast), ptr(xsum),
+         ptr(gamma), ptr(beta), float(eps), ptr(y), C, ptr(mean), ptr(rstd), stream())
+    return y, mean, rstd
+
+
+def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dgamma=None, dbeta=None):
+    rows, C = _rows(x)
+    if dx is None:
+        dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+    call("s2h_layernorm_bwd", dt(x), rows, C, ptr(x), C, ptr(dy), C, ptr(gamma), ptr(mean), ptr(rstd),
+         ptr(dx), C, int(accumulate), ptr(dgamma), ptr(dbeta), stream())
+    return dx
+
+
+# ----------------------------------------------------------- elementwise
+def add(a, b, out=None, alpha=1.0, beta=1.0):
+    ref = a if a is not None else b
+    if out is None:
+        out = torch.empty_like(ref)
+    call("s2h_add", dt(ref), ref.numel(), ptr(a), ptr(b), float(alpha), float(beta), ptr(out), stream())
+    return out
+
+
+def add_bcast(a, b, out=None, alpha=1.0, beta=1.0, b_period=1, shape=None):
+    """out[i, :] = alpha*a[i, :] + beta*b[i % b_period, :]  (a may be None -> broadcast copy)"""
+    inner = b.numel() // b_period
+    if out is None:
+        out = torch.empty(shape if shape is not None else a.shape, device=b.device, dtype=b.dtype)
+    outer = out.numel() // inner
+    call("s2h_add_bcast", dt(out), outer, inner, ptr(a), float(alpha), ptr(b), b_period, float(beta), ptr(out),
+         stream())
+    return out
+
+
+def act_fwd(x, act, out=None, scale=1.0, shift=0.0):
+    if out is None:
+        out = torch.empty_like(x)
+    call("s2h_act_fwd", dt(x), x.numel(), ptr(x), ACT[act], float(scale), float(shift), ptr(out), stream())
+    return out
+
+
+def act_bwd(x_pre, dy, act, dx=None, accumulate=False):
+    if dx is None:
+        dx = torch.empty_like(dy)
+    call("s2h_act_bwd", dt(dy), dy.numel(), ptr(x_pre), ptr(dy), ACT[act], ptr(dx), int(accumulate), stream())
+    return dx
+
+
+def cast(x, dtype, out=None):
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    call("s2h_cast", dt(x), dt(out), x.numel(), ptr(x), ptr(out), stream())
+    return out
+
+
+def dropout(b, p, seed, a=None, out=None):
+    """out = (a +) keep*b/(1-p) with the counter-hash mask of (seed, flat index)"""
+    if out is None:
+        out = torch.empty_like(b)
+    call("s2h_dropout", dt(b), b.numel(), ptr(a), ptr(b), float(p), int(seed) & (2**64 - 1), ptr(out), stream())
+    return out
+
+
+def rope(x, y, nrot, cos, sin, period, inverse=False):
+    """x/y [Bt, L, D] views (D contiguous): rotate pairs of the first nrot rows of every batch."""
+    Bt, L, D = x.shape
+    call("s2h_rope", dt(x), Bt, nrot, D, ptr(x), x.stride(0), x.stride(1), ptr(y), y.stride(0), y.stride(1),
+         ptr(cos), ptr(sin), period, int(inverse), stream())
+    return y
+
+
+def maxpool2(x, out=None):
+    """x [B, H, W, C] (pixel stride x.stride(2), C contiguous) -> [B, H/2, W/2, C]"""
+    B, H, W, C = x.shape
+    assert x.stride(1) == W * x.stride(2) and x.stride(0) == H * x.stride(1) and x.stride(3) == 1
+    if out is None:
+        out = torch.empty(B, H // 2, W // 2, C, device=x.device, dtype=x.dtype)
+    call("s2h_maxpool2_fwd", dt(x), B, H, W, C, ptr(x), x.stride(2), ptr(out), stream())
+    return out
+
+
+def maxpool2_bwd(x, dy, dx):
+    B, H, W, C = x.shape
+    call("s2h_maxpool2_bwd", dt(x), B, H, W, C, ptr(x), x.stride(2), ptr(dy), ptr(dx), dx.stride(2), stream())
+    return dx
+
+
+def window_partition(x, ws, out=None, accumulate=False):
+    B, H, W, C = x.shape
+    nh, nw = -(-H // ws), -(-W // ws)
+    if out is None:
+        out = torch.empty(B * nh * nw, ws, ws, C, device=x.device, dtype=x.dtype)
+    call("s2h_window", dt(x), B, H, W, C, ws, ptr(x), ptr(out), 0, int(accumulate), stream())
+    return out
+
+
+def window_unpartition(win, ws, B, H, W, out=None, accumulate=False):
+    C = win.shape[-1]
+    if out is None:
+        out = torch.empty(B, H, W, C, device=win.device, dtype=win.dtype)
+    call("s2h_window", dt(win), B, H, W, C, ws, ptr(win), ptr(out), 1, int(accumulate), stream())
+    return out
+
+
+def up2_add(lat, prev, out=None):
+    B, H, W, C = lat.shape
+    if out is None:
+        out = torch.empty_like(lat)
+    call("s2h_up2_add", dt(lat), B, H, W, C, ptr(lat), ptr(prev), ptr(out), stream())
+    return out
+
+
+def pool2_sum(dout, dprev, accumulate=False):
+    B, Ho, Wo, C = dprev.shape
+    call("s2h_pool2_sum", dt(dout), B, Ho, Wo, C, ptr(dout), ptr(dprev), int(accumulate), stream())
+    return dprev
+
+
+def bilinear(x, ho, wo, out=None):
+    """x [N, hi, wi] f32 -> [N, ho, wo] (align_corners=False)"""
+    N, hi, wi = x.shape
+    if out is None:
+        out = torch.empty(N, ho, wo, device=x.device, dtype=torch.float32)
+    call("s2h_bilinear_fwd", N, hi, wi, ho, wo, ptr(x), ptr(out), stream())
+    return out
+
+
+def bilinear_bwd(dy, hi, wi, dx=None):
+    N, ho, wo = dy.shape
+    if dx is None:
+        dx = torch.empty(N, hi, wi, device=dy.device, dtype=torch.float32)
+    call("s2h_bilinear_bwd", N, hi, wi, ho, wo, ptr(dy), ptr(dx), stream())
+    return dx
+
+
+def colsum(x, out, accumulate=True):
+    """out (fp32 [C]) (+)= x.reshape(-1, C).sum(0)"""
+    rows, C = _rows(x)
+    call("s2h_colsum", dt(x), rows, C, ptr(x), x.stride(-2) if x.dim() > 1 else C, ptr(out), int(accumulate),
+         stream())
+    return out
+
+
+def sum_outer(x, out, accumulate=False):
+    """out[j] = sum_o x[o, j]  (same dtype as x)"""
+    O = x.shape[0]
+    call("s2h_sum_outer", dt(x), O, x.numel() // O, ptr(x), ptr(out), int(accumulate), stream())
+    return out
+
+
+def im2col(x, kh, kw, stride, pad):
+    B, H, W, C = x.shape
+    Ho = (H + 2 * pad - kh) // stride + 1
+    Wo = (W + 2 * pad - kw) // stride + 1
+    col = torch.empty(B * Ho * Wo, C * kh * kw, device=x.device, dtype=x.dtype)
+    call("s2h_im2col", dt(x), B, H, W, C, kh, kw, stride, pad, Ho, Wo, ptr(x), ptr(col), stream())
+    return col, Ho, Wo
+
+
+def dwconv(x, w, bias, pad):
+    B, H, W, C = x.shape
+    K = w.shape[-1]
+    out = torch.empty_like(x)
+    call("s2h_dwconv", dt(x), B, H, W, C, K, pad, ptr(x), ptr(w), ptr(bias), ptr(out), stream())
+    return out
+
+
+def convt2_scatter(Y, B, H, W, Co, bias=None, add=None, out=None):
+    if out is None:
+        out = torch.empty(B, 2 * H, 2 * W, Co, device=Y.device, dtype=Y.dtype)
+    call("s2h_convt2", dt(Y), B, H, W, Co, ptr(Y), ptr(bias), ptr(add), ptr(out), 0, stream())
+    return out
+
+
+def convt2_gather(dout, B, H, W, Co, dY=None):
+    if dY is None:
+        dY = torch.empty(B * H * W, 4 * Co, device=dout.device, dtype=dout.dtype)
+    call("s2h_convt2", dt(dout), B, H, W, Co, ptr(dout), None, None, ptr(dY), 1, stream())
+    return dY
+
+
+def row_gate(x, gate, fill, out=None, backward=False):
+    rows = x.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    call("s2h_row_gate", dt(x), rows, x.numel() // rows, ptr(x), ptr(gate), float(fill), ptr(out), int(backward),
+         stream())
+    return out
+
+
+def gate_mix(x, gate, vec, scale_x=False, out=None):
+    rows = x.shape[0]
+    if out is None:
+        out = torch.empty_like(x)
+    call("s2h_gate_mix", dt(x), rows, x.numel() // rows, ptr(x), ptr(gate), ptr(vec), vec.numel(), int(scale_x),
+         ptr(out), stream())
+    return out
+
+
+# ------------------------------------------------------------------ loss
+NSTAT = 6
+
+
+def mask_stats(x, tgt, inv_temp=1.0, stats=None):
+    """x [N, P] f32 logits, tgt [N, P] uint8/bool (or None) -> stats [N, 6] f32"""
+    N, P = x.shape
+    if stats is None:
+        stats = torch.empty(N, NSTAT, device=x.device, dtype=torch.float32)
+    call("s2h_mask_stats", N, P, ptr(x), x.stride(0), ptr(tgt), tgt.stride(0) if tgt is not None else 0,
+         float(inv_temp), ptr(stats), stream())
+    return stats
+
+
+def mask_loss_finalize(stats, pred_iou, valid, P, weights, gscale, losses, coef):
+    N = stats.shape[0]
+    call("s2h_mask_loss_finalize", N, P, ptr(stats), ptr(pred_iou), ptr(valid), float(weights[0]),
+         float(weights[1]), float(weights[2]), float(gscale), ptr(losses), ptr(coef), stream())
+
+
+def mask_loss_bwd(x, tgt, coef, inv_temp, dx):
+    N, P = x.shape
+    call("s2h_mask_loss_bwd", N, P, ptr(x), x.stride(0), ptr(tgt), tgt.stride(0), float(inv_temp), ptr(coef),
+         ptr(dx), dx.stride(0), stream())
+    return dx
+
+
+def group_max(x, cat_off, cat_obj, ncat, out, arg):
+    P = x.shape[1]
+    call("s2h_group_max_fwd", ncat, P, ptr(cat_off), ptr(cat_obj), ptr(x), x.stride(0), ptr(out), out.stride(0),
+         ptr(arg), stream())
+    return out
+
+
+def group_max_bwd(dy, obj_cat, arg, dx):
+    O, P = dx.shape
+    call("s2h_group_max_bwd", O, P, ptr(obj_cat), ptr(arg), ptr(dy), dy.stride(0), ptr(dx), dx.stride(0), stream())
+    return dx
+
+
+def group_wavg(x, stats, cat_off, cat_obj, ncat, out):
+    K = x.shape[1]
+    call("s2h_group_wavg_fwd", ncat, K, ptr(cat_off), ptr(cat_obj), ptr(stats), ptr(x), ptr(out), stream())
+    return out
+
+
+def group_wavg_bwd(x, y, dy, stats, obj_cat, cat_off, dx, dw):
+    O, K = x.shape
+    call("s2h_group_wavg_bwd", O, K, ptr(obj_cat), ptr(cat_off), ptr(stats), ptr(x), ptr(y), ptr(dy), ptr(dx),
+         ptr(dw), stream())
+
+
+def sigmoid_grad_axpy(x, coef, dx):
+    R, P = x.shape
+    call("s2h_sigmoid_grad_axpy", R, P, ptr(x), x.stride(0), ptr(coef), ptr(dx), dx.stride(0), stream())
+    return dx
+
+
+# ------------------------------------------------------------- optimizer
+def grad_norm(g, max_norm, ws, out):
+    call("s2h_grad_norm", g.numel(), ptr(g), ptr(ws), float(max_norm), ptr(out), stream())
+    return out
+
+
+def adamw(p, g, m, v, clip, lr, beta1, beta2, eps, wd, step, shadow=None):
+    call("s2h_adamw", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(clip), float(lr), float(beta1), float(beta2),
+         float(eps), float(wd), int(step), ptr(shadow), stream())
+
+
+def version():
+    from ._lib import lib
+    return lib().s2h_version()
+
+
+_ = math

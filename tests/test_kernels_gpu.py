@@ -1,0 +1,321 @@
+"""Per-kernel numerics of libsam2hip against plain PyTorch fp32 references of the
+same op (run on the GPU box).  fp32 path (f32-input MFMA) must match to ~1e-5
+relative; bf16 path within bf16 rounding of the inputs."""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _ops():
+    from sam2_video.kernels import ops
+    return ops
+
+
+def _close(a, b, tol):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err:.3e} vs scale {scale:.3e} (tol {tol})"
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (7, 13, 5), (64, 64, 32), (300, 257, 129), (1024, 768, 256),
+                                   (4100, 130, 200)])
+def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
+    ops = _ops()
+    torch.manual_seed(0)
+    x = torch.randn(M, K, device=DEV).to(dtype)
+    w = torch.randn(N, K, device=DEV).to(dtype)
+    b = torch.randn(N, device=DEV)
+    y = ops.linear(x, w, b)
+    ref = x.float() @ w.float().t() + b
+    _close(y, ref, tol)
+    for act in ("relu", "gelu"):
+        pre = torch.empty(M, N, device=DEV, dtype=dtype)
+        y = ops.linear(x, w, b, act=act, pre=pre)
+        r = torch.relu(ref) if act == "relu" else torch.nn.functional.gelu(ref)
+        _close(y, r, tol)
+        _close(pre, ref, tol)
+    dy = torch.randn(M, N, device=DEV).to(dtype)
+    dx = ops.linear_dgrad(dy, w)
+    _close(dx, dy.float() @ w.float(), tol)
+    dw = torch.zeros(N, K, device=DEV)
+    ops.linear_wgrad(dy, x, dw)
+    ops.linear_wgrad(dy, x, dw)  # accumulates
+    _close(dw, 2 * dy.float().t() @ x.float(), tol)
+    r = torch.randn(M, N, device=DEV).to(dtype)
+    y = ops.linear(x, w, b, residual=r)
+    _close(y, ref + r.float(), tol)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
+def test_bmm_layouts(dtype, tol):
+    ops = _ops()
+    a = torch.randn(3, 37, 50, device=DEV).to(dtype)
+    b = torch.randn(3, 50, 70, device=DEV).to(dtype)
+    out = torch.empty(3, 37, 70, device=DEV, dtype=dtype)
+    ops.bmm(a, b, out)
+    _close(out, a.float() @ b.float(), tol)
+    bt = torch.randn(3, 70, 50, device=DEV).to(dtype)
+    ops.bmm(a, bt, out, trans_b=True)
+    _close(out, a.float() @ bt.float().transpose(1, 2), tol)
+    at = torch.randn(3, 50, 37, device=DEV).to(dtype).transpose(1, 2)  # M-contiguous A
+    ops.bmm(at, b, out)
+    _close(out, at.float() @ b.float(), tol)
+
+
+def _ref_attn(q, k, v, scale):
+    # q [B, Lq, H, D]
+    qh, kh, vh = (t.float().transpose(1, 2) for t in (q, k, v))
+    s = (qh @ kh.transpose(-1, -2)) * scale
+    p = s.softmax(-1)
+    return (p @ vh).transpose(1, 2), torch.logsumexp(s, -1)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 5e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("B,H,Lq,Lk,D", [(2, 2, 64, 64, 56), (3, 1, 16, 64, 56), (2, 8, 8, 100, 16),
+                                         (2, 8, 100, 8, 16), (1, 8, 7, 7, 32), (2, 1, 256, 1028, 256),
+                                         (1, 4, 196, 196, 96), (1, 2, 49, 196, 72), (13, 1, 70, 130, 256)])
+def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
+    ops = _ops()
+    torch.manual_seed(1)
+    q = torch.randn(B, Lq, H, D, device=DEV).to(dtype)
+    k = torch.randn(B, Lk, H, D, device=DEV).to(dtype)
+    v = torch.randn(B, Lk, H, D, device=DEV).to(dtype)
+    scale = 1.0 / math.sqrt(D)
+    o = torch.empty_like(q)
+    lse = torch.empty(B, H, Lq, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, scale)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ro, rl = _ref_attn(qr, kr, vr, scale)
+    _close(o, ro, tol)
+    _close(lse, rl, tol)
+    do = torch.randn_like(q)
+    ro.backward(do.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale)
+    _close(dq, qr.grad, 3 * tol)
+    _close(dk, kr.grad, 3 * tol)
+    _close(dv, vr.grad, 3 * tol)
+
+
+def test_attention_strided_qkv():
+    """q/k/v read in place from a fused [B, L, 3, H, d] qkv projection (Hiera)."""
+    ops = _ops()
+    B, L, H, d = 4, 64, 2, 56
+    qkv = torch.randn(B, L, 3, H, d, device=DEV)
+    q, k, v = qkv.unbind(2)
+    o = torch.empty(B, L, H, d, device=DEV)
+    lse = torch.empty(B, H, L, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, d ** -0.5)
+    ro, _ = _ref_attn(q, k, v, d ** -0.5)
+    _close(o, ro, 5e-5)
+
+
+def test_attention_dropout_consistent():
+    """dropout mask regenerated in backward: finite-difference check of the dropped attention."""
+    ops = _ops()
+    torch.manual_seed(2)
+    B, H, L, D = 1, 1, 40, 32
+    q = torch.randn(B, L, H, D, device=DEV, dtype=torch.float64).float()
+    k = torch.randn(B, L, H, D, device=DEV).float()
+    v = torch.randn(B, L, H, D, device=DEV).float()
+    o = torch.empty_like(q)
+    lse = torch.empty(B, H, L, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, 0.2, p_drop=0.3, seed=1234)
+    o2 = torch.empty_like(q)
+    ops.attn_fwd(q, k, v, o2, lse, 0.2, p_drop=0.3, seed=1234)
+    assert torch.equal(o, o2)
+    do = torch.randn_like(o)
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, 0.2, p_drop=0.3, seed=1234)
+    # directional derivative along random dv direction: <do, dO/dv . e> == <dv, e>
+    e = torch.randn_like(v) * 1e-2
+    op = torch.empty_like(o)
+    ops.attn_fwd(q, k, v + e, op, lse.clone(), 0.2, p_drop=0.3, seed=1234)
+    lhs = ((op - o) * do).sum().item()
+    rhs = (dv * e).sum().item()
+    assert abs(lhs - rhs) <= 1e-3 * max(1.0, abs(rhs))
+    eq = torch.randn_like(q) * 1e-3
+    ops.attn_fwd(q + eq, k, v, op, lse.clone(), 0.2, p_drop=0.3, seed=1234)
+    lhs = ((op - o) * do).sum().item()
+    rhs = (dq * eq).sum().item()
+    assert abs(lhs - rhs) <= 2e-2 * max(1e-2, abs(rhs))
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("rows,C", [(1, 112), (1000, 256), (37, 896), (513, 64), (9, 1152)])
+def test_layernorm(dtype, tol, rows, C):
+    ops = _ops()
+    x = torch.randn(rows, C, device=DEV).to(dtype)
+    g = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    y, mu, rs = ops.layernorm_fwd(x, g, b, 1e-6)
+    xr = x.float().clone().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (C,), gr, br, 1e-6)
+    _close(y, yr, tol)
+    dy = torch.randn(rows, C, device=DEV).to(dtype)
+    yr.backward(dy.float())
+    dg = torch.zeros(C, device=DEV)
+    db = torch.zeros(C, device=DEV)
+    dx = ops.layernorm_bwd(x, dy, g, mu, rs, dgamma=dg, dbeta=db)
+    _close(dx, xr.grad, 3 * tol)
+    _close(dg, gr.grad, 3 * tol)
+    _close(db, br.grad, 3 * tol)
+    a = torch.randn(rows, C, device=DEV).to(dtype)
+    xs = torch.empty_like(x)
+    y2, _, _ = ops.layernorm_fwd(x, g, b, 1e-6, add=a, xsum=xs)
+    _close(xs, x.float() + a.float(), tol)
+    _close(y2, torch.nn.functional.layer_norm(xs.float(), (C,), g, b, 1e-6), tol)
+
+
+def test_elementwise_misc():
+    ops = _ops()
+    x = torch.randn(2, 10, 12, 6, device=DEV)
+    y = ops.maxpool2(x)
+    ref = torch.nn.functional.max_pool2d(x.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1)
+    _close(y, ref, 0)
+    xr = x.clone().requires_grad_(True)
+    torch.nn.functional.max_pool2d(xr.permute(0, 3, 1, 2), 2).permute(0, 2, 3, 1).backward(torch.ones_like(y))
+    dx = torch.empty_like(x)
+    ops.maxpool2_bwd(x, torch.ones_like(y), dx)
+    _close(dx, xr.grad, 0)
+    # window partition / unpartition with padding
+    x = torch.randn(2, 9, 11, 5, device=DEV)
+    win = ops.window_partition(x, 4)
+    xp = torch.nn.functional.pad(x, (0, 0, 0, 1, 0, 3))
+    ref = xp.view(2, 3, 4, 3, 4, 5).permute(0, 1, 3, 2, 4, 5).reshape(-1, 4, 4, 5)
+    _close(win, ref, 0)
+    back = ops.window_unpartition(win, 4, 2, 9, 11)
+    _close(back, x, 0)
+    # bilinear
+    lo = torch.randn(3, 16, 16, device=DEV)
+    hi = ops.bilinear(lo, 64, 64)
+    ref = torch.nn.functional.interpolate(lo[:, None], size=(64, 64), mode="bilinear", align_corners=False)[:, 0]
+    _close(hi, ref, 1e-6)
+    lr = lo.clone().requires_grad_(True)
+    g = torch.randn(3, 64, 64, device=DEV)
+    torch.nn.functional.interpolate(lr[:, None], size=(64, 64), mode="bilinear", align_corners=False)[:, 0].backward(g)
+    _close(ops.bilinear_bwd(g, 16, 16), lr.grad, 1e-5)
+    # nearest up2 add + its backward
+    lat = torch.randn(2, 8, 8, 4, device=DEV)
+    prev = torch.randn(2, 4, 4, 4, device=DEV)
+    out = ops.up2_add(lat, prev)
+    ref = lat + prev.repeat_interleave(2, 1).repeat_interleave(2, 2)
+    _close(out, ref, 0)
+    dp = torch.empty_like(prev)
+    ops.pool2_sum(out, dp)
+    _close(dp, out.view(2, 4, 2, 4, 2, 4).sum((2, 4)), 1e-6)
+    # colsum
+    t = torch.randn(1000, 33, device=DEV)
+    cs = torch.zeros(33, device=DEV)
+    ops.colsum(t, cs)
+    _close(cs, t.sum(0), 1e-5)
+
+
+def test_im2col_conv_matches_torch():
+    ops = _ops()
+    x = torch.randn(2, 17, 19, 3, device=DEV)
+    w = torch.randn(8, 3, 7, 7, device=DEV)
+    b = torch.randn(8, device=DEV)
+    col, Ho, Wo = ops.im2col(x, 7, 7, 4, 3)
+    y = ops.linear(col, w.reshape(8, -1), b).view(2, Ho, Wo, 8)
+    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride=4, padding=3).permute(0, 2, 3, 1)
+    _close(y, ref, 2e-5)
+    wd = torch.randn(6, 1, 7, 7, device=DEV)
+    xd = torch.randn(2, 9, 9, 6, device=DEV)
+    yd = ops.dwconv(xd, wd, b[:6], 3)
+    ref = torch.nn.functional.conv2d(xd.permute(0, 3, 1, 2), wd, b[:6], padding=3, groups=6).permute(0, 2, 3, 1)
+    _close(yd, ref, 2e-5)
+
+
+def test_convt2():
+    ops = _ops()
+    B, H, W, Ci, Co = 2, 5, 6, 8, 4
+    x = torch.randn(B, H, W, Ci, device=DEV)
+    w = torch.randn(Ci, Co, 2, 2, device=DEV)
+    b = torch.randn(Co, device=DEV)
+    Y = torch.empty(B * H * W, Co * 4, device=DEV)
+    x2 = x.reshape(-1, Ci)
+    ops.gemm(x2, w, Y, M=B * H * W, N=Co * 4, K=Ci, lda_m=Ci, lda_k=1, ldb_k=Co * 4, ldb_n=1, ldc=Co * 4)
+    out = ops.convt2_scatter(Y, B, H, W, Co, bias=b)
+    ref = torch.nn.functional.conv_transpose2d(x.permute(0, 3, 1, 2), w, b, stride=2).permute(0, 2, 3, 1)
+    _close(out, ref, 2e-5)
+    dY = ops.convt2_gather(out, B, H, W, Co)
+    Y2 = torch.empty_like(Y)
+    Y2.copy_(dY)
+    out2 = ops.convt2_scatter(Y2, B, H, W, Co)
+    _close(out2, out, 0)
+
+
+def test_rope_roundtrip():
+    ops = _ops()
+    Bt, L, D = 3, 20, 8
+    x = torch.randn(Bt, L, D, device=DEV)
+    ang = torch.rand(10, D // 2, device=DEV) * 6
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    y = torch.empty_like(x)
+    ops.rope(x, y, 20, cos, sin, 10)
+    xc = torch.view_as_complex(x.view(Bt, L, D // 2, 2))
+    f = torch.polar(torch.ones_like(ang), ang).repeat(2, 1)
+    ref = torch.view_as_real(xc * f).flatten(2)
+    _close(y, ref, 1e-6)
+    z = torch.empty_like(x)
+    ops.rope(y, z, 20, cos, sin, 10, inverse=True)
+    _close(z, x, 1e-6)
+
+
+def test_mask_loss_and_adamw():
+    ops = _ops()
+    torch.manual_seed(3)
+    N, P = 5, 4096
+    x = torch.randn(N, P, device=DEV) * 3
+    t = (torch.rand(N, P, device=DEV) > 0.7)
+    t[2] = False
+    stats = ops.mask_stats(x, t.view(torch.uint8))
+    xs = x.clone().requires_grad_(True)
+    tf = t.float()
+    pr = xs.sigmoid()
+    ce = torch.nn.functional.binary_cross_entropy_with_logits(xs, tf, reduction="none")
+    p_t = pr * tf + (1 - pr) * (1 - tf)
+    focal = (0.25 * tf + 0.75 * (1 - tf)) * ce * (1 - p_t) ** 2
+    _close(stats[:, 0], focal.detach().sum(1), 1e-5)
+    _close(stats[:, 1], pr.detach().sum(1), 1e-5)
+    valid = t.any(1).int()
+    pred_iou = torch.rand(N, device=DEV)
+    losses = torch.zeros(4, device=DEV)
+    coef = torch.empty(N, 4, device=DEV)
+    ops.mask_loss_finalize(stats, pred_iou, valid, P, (20.0, 1.0, 1.0), 1.0, losses, coef)
+    v = valid.bool()
+    nv = v.sum()
+    lm = (focal.mean(1)[v]).sum() / nv
+    num = 2 * (pr * tf).sum(1) + 1
+    den = pr.sum(1) + tf.sum(1) + 1
+    ld = ((1 - num / den)[v]).sum() / nv
+    tot = 20 * lm + ld
+    _close(losses[0], lm.detach(), 1e-5)
+    _close(losses[1], ld.detach(), 1e-5)
+    tot.backward()
+    dx = torch.empty_like(x)
+    ops.mask_loss_bwd(x, t.view(torch.uint8), coef, 1.0, dx)
+    _close(dx, xs.grad, 1e-4)
+    # AdamW vs torch.optim.AdamW
+    p = torch.randn(1000, device=DEV)
+    g = torch.randn(1000, device=DEV)
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pt], lr=1e-3, weight_decay=0.01, betas=(0.9, 0.999))
+    m = torch.zeros_like(p)
+    vv = torch.zeros_like(p)
+    for step in range(1, 4):
+        pt.grad = g.clone()
+        opt.step()
+        ops.adamw(p, g, m, vv, None, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+    _close(p, pt.detach(), 1e-6)
