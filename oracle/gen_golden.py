@@ -1,0 +1,149 @@
+"""TEST INFRASTRUCTURE ONLY -- generates tests/golden/*.pt from the REFERENCE
+itself (imported through oracle/ref_harness.py; this container only).
+
+Each fixture = one full reference training step (SAM2Model.forward ->
+MultiStepMultiMasksAndIous -> backward, restating SAM2LightningModule.training_step
+trainer.py:256-289 without Lightning) on a deterministic synthetic clip with
+deterministic synthetic weights, fp32, dropout disabled (parity mode).
+
+Stored (all plain tensors, loadable with torch.load(weights_only=True)):
+  inputs checksums, frame-0 point prompts, per-object low-res mask logits per
+  frame, per-frame merged outputs (low-res masks, IoU preds, object scores,
+  high-res sub-sampled logits + checksums), loss terms, per-parameter gradient
+  norms / sums (full gradients for small tensors), the names of trainable
+  parameters whose .grad stays None, and intermediate backbone features.
+
+Usage:  python oracle/gen_golden.py [name ...]
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import ref_harness as H  # noqa: E402
+
+OUT = os.path.join(os.path.dirname(HERE), "tests", "golden")
+
+ALL = ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder", "prompt_encoder"]
+CASES = {
+    # config 1 shape: Hiera-T, 256^2, 4 frames, 13 categories / 4 objects
+    "tiny256_point_all": dict(size="tiny", image_size=256, T=4, n_cat=13, n_obj=4, prompt="point", trainable=ALL),
+    "tiny256_point_mem": dict(size="tiny", image_size=256, T=4, n_cat=13, n_obj=4, prompt="point",
+                              trainable=["memory_attention", "memory_encoder"]),
+    "tiny256_box_all": dict(size="tiny", image_size=256, T=3, n_cat=5, n_obj=3, prompt="box", trainable=ALL),
+    # Hiera-B+ structure (heads 2..16, head_dim 56, q-pool, global blocks 12/16/20) at a small resolution
+    "bplus128_point_all": dict(size="base_plus", image_size=128, T=3, n_cat=4, n_obj=2, prompt="point",
+                               trainable=ALL),
+}
+FULL_GRAD_NUMEL = 4096
+
+
+def reference_batch(clip):
+    """Restates sam2_collate_fn (dataset.py:346-398) into the reference's BatchedVideoDatapoint."""
+    from sam2_video.data.data_utils import BatchedVideoDatapoint, BatchedVideoMetaData
+
+    images = clip["images"][:, None]  # [T, 1, 3, H, W]
+    masks = clip["masks"]
+    T, N = masks.shape[:2]
+    H = images.shape[-2]
+    obj_to_frame_idx = torch.zeros(T, N, 2, dtype=torch.int)
+    obj_to_frame_idx[..., 0] = torch.arange(T, dtype=torch.int)[:, None]
+    ident = torch.zeros(T, N, 3, dtype=torch.long)
+    ident[..., 1] = torch.arange(N)[None]
+    ident[..., 2] = torch.arange(T)[:, None]
+    size = torch.full((T, N, 2), H, dtype=torch.long)
+    meta = BatchedVideoMetaData(unique_objects_identifier=ident, frame_orig_size=size)
+    return BatchedVideoDatapoint(img_batch=images, obj_to_frame_idx=obj_to_frame_idx, masks=masks.bool(),
+                                 metadata=meta, dict_key="video_batch", batch_size=[T])
+
+
+def run_case(name, c, seed=0, clip_idx=7):
+    torch.manual_seed(0)
+    model = H.build_reference_model(c["size"], c["image_size"], c["trainable"], c["prompt"], seed=seed)
+    synth = H.product_file("data/synthetic.py")
+    clip = synth.make_clip(clip_idx, c["T"], c["image_size"], c["n_cat"], c["n_obj"])
+    batch = reference_batch(clip)
+    from sam2_video.model.losses import MultiStepMultiMasksAndIous, CORE_LOSS_KEY
+    from sam2_video.utils import merge_object_results_to_category
+
+    crit = MultiStepMultiMasksAndIous(weight_dict={"loss_mask": 20, "loss_dice": 1, "loss_iou": 1, "loss_class": 0},
+                                      supervise_all_iou=True, iou_use_l1_loss=True, pred_obj_scores=False,
+                                      focal_gamma_obj_score=0.0, focal_alpha_obj_score=-1.0, logit_temperature=1.0)
+    t0 = time.time()
+    # SAM2Model.forward (sam2model.py:153-179), restated to keep the per-object outputs
+    backbone_out = model.forward_image(batch.flat_img_batch)
+    feats = {f"fpn{i}": x.detach().clone() for i, x in enumerate(backbone_out["backbone_fpn"])}
+    backbone_out = model.prepare_prompt_inputs(backbone_out, batch)
+    stages = model.forward_tracking(backbone_out, batch)
+    outs = merge_object_results_to_category(stages, backbone_out["obj_to_cat"], backbone_out["num_categories"])
+    losses = crit(outs, batch.masks)
+    total = losses[CORE_LOSS_KEY]
+    total.backward()
+    dt = time.time() - t0
+
+    g = {}
+    g["meta/T"] = torch.tensor(c["T"])
+    g["meta/image_size"] = torch.tensor(c["image_size"])
+    g["meta/seed"] = torch.tensor(seed)
+    g["meta/clip_idx"] = torch.tensor(clip_idx)
+    g["in/images_sum"] = clip["images"].double().sum()
+    g["in/images_abs"] = clip["images"].double().abs().sum()
+    g["in/masks_count"] = clip["masks"].sum(dim=(2, 3))
+    g["obj_to_cat"] = torch.tensor(backbone_out["obj_to_cat"])
+    pin = backbone_out["point_inputs_per_frame"].get(0)
+    if pin is not None:
+        g["prompt/coords"] = pin["point_coords"].detach().clone()
+        g["prompt/labels"] = pin["point_labels"].detach().clone()
+    for k, v in feats.items():
+        g[f"feat/{k}_sum"] = v.double().sum()
+        g[f"feat/{k}_sq"] = (v.double() ** 2).sum()
+    g["feat/fpn_last"] = feats[f"fpn{len(feats) - 1}"]
+    for t, st in enumerate(stages):
+        g[f"obj/{t}/low_res"] = st["pred_masks"].detach().clone()
+        g[f"obj/{t}/ious"] = st["multistep_pred_ious"][0].detach().clone()
+        g[f"obj/{t}/obj_score"] = st["multistep_object_score_logits"][0].detach().clone()
+    for t, o in enumerate(outs):
+        hr = o["multistep_pred_multimasks_high_res"][0].detach()
+        g[f"cat/{t}/low_res"] = o["pred_masks"].detach().clone()
+        g[f"cat/{t}/high_res_sub"] = hr[:, :, ::8, ::8].clone()
+        g[f"cat/{t}/high_res_sum"] = hr.double().sum()
+        g[f"cat/{t}/high_res_sq"] = (hr.double() ** 2).sum()
+        g[f"cat/{t}/ious"] = o["multistep_pred_ious"][0].detach().clone()
+        g[f"cat/{t}/obj_score"] = o["multistep_object_score_logits"][0].detach().clone()
+    for k in ("loss_mask", "loss_dice", "loss_iou", "loss_class", CORE_LOSS_KEY):
+        v = losses[k]
+        g[f"loss/{k}"] = v.detach().clone() if torch.is_tensor(v) else torch.tensor(float(v))
+    none_grad = []
+    for n, p in model.named_parameters():
+        if not p.requires_grad:
+            continue
+        if p.grad is None:
+            none_grad.append(n)
+            continue
+        g[f"gnorm/{n}"] = p.grad.double().norm()
+        g[f"gsum/{n}"] = p.grad.double().sum()
+        if p.numel() <= FULL_GRAD_NUMEL:
+            g[f"grad/{n}"] = p.grad.detach().clone()
+    g["none_grad"] = none_grad
+    g["trainable"] = [n for n, p in model.named_parameters() if p.requires_grad]
+    g["state_shapes"] = {k: list(v.shape) for k, v in model.state_dict().items()}
+    path = os.path.join(OUT, f"{name}.pt")
+    torch.save(g, path)
+    print(f"{name}: step {dt:.1f}s, loss {float(total):.6f}, {len(none_grad)} none-grad params, "
+          f"{os.path.getsize(path) / 1e6:.2f} MB")
+
+
+def main(argv):
+    os.makedirs(OUT, exist_ok=True)
+    names = argv or list(CASES)
+    for n in names:
+        run_case(n, CASES[n])
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
