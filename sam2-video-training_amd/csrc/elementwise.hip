@@ -552,3 +552,76 @@ extern "C" int s2h_gate_mix(int dt, int64_t rows, int64_t inner, const void* x, 
   DISPATCH_T(dt, gate_mix_kernel, ew_grid(rows * inner), rows, inner, x, gate, vec, vec_period, scale_x, y);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------ Hiera windowed pos-embed finish
+// out[i, j, c] = Y[c, i, j] + win[c, i % ws, j % ws]   (Y = bicubic(pos_embed), fp32 CHW -> T HWC)
+template <typename T>
+__global__ void pos_embed_fwd_kernel(int C, int h, int w, int ws, const float* Y, const float* win, void* out) {
+  const int64_t n = (int64_t)h * w * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    const int64_t p = i / C;
+    const int x = p % w, y = p / w;
+    const float v = Y[((int64_t)c * h + y) * w + x] + win[(c * ws + y % ws) * ws + x % ws];
+    ((T*)out)[i] = from_f32<T>(v);
+  }
+}
+// dY[c, i, j] = dout[i, j, c] (f32) ; dwin[c, a, b] += sum over (i%ws==a, j%ws==b) dout[i, j, c]
+template <typename T>
+__global__ void pos_embed_bwd_kernel(int C, int h, int w, int ws, const void* dout, float* dY, float* dwin) {
+  const int64_t n = (int64_t)h * w * C;
+  GRID_STRIDE(i, n) {
+    const int c = i % C;
+    const int64_t p = i / C;
+    const int x = p % w, y = p / w;
+    const float g = to_f32(((const T*)dout)[i]);
+    if (dY) dY[((int64_t)c * h + y) * w + x] = g;
+    if (dwin) atomicAdd(&dwin[(c * ws + y % ws) * ws + x % ws], g);
+  }
+}
+extern "C" int s2h_pos_embed(int dt, int C, int h, int w, int ws, const float* Y, const float* win, void* out,
+                             hipStream_t st) {
+  const int64_t n = (int64_t)h * w * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, pos_embed_fwd_kernel, ew_grid(n), C, h, w, ws, Y, win, out);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void* dout, float* dY, float* dwin,
+                                 hipStream_t st) {
+  const int64_t n = (int64_t)h * w * C;
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, pos_embed_bwd_kernel, ew_grid(n), C, h, w, ws, dout, dY, dwin);
+  return (int)hipGetLastError();
+}
+
+// ------------------------------------------------ point-prompt embeddings
+// out[r, :] = pe[r, :] * (label != -1) + table[label + 1, :]   (table rows: not_a_point, pe0..pe3)
+// backward: dtable[label + 1, :] += dout[r, :]  (f32, serial over rows -> deterministic)
+template <typename T>
+__global__ void point_embed_kernel(int R, int D, const float* pe, const int* labels, const void* table, void* out) {
+  const int64_t n = (int64_t)R * D;
+  GRID_STRIDE(i, n) {
+    const int r = i / D, d = i % D;
+    const int l = labels[r];
+    float v = (l == -1 ? 0.f : pe[i]) + to_f32(((const T*)table)[(l + 1) * D + d]);
+    ((T*)out)[i] = from_f32<T>(v);
+  }
+}
+template <typename T>
+__global__ void point_embed_bwd_kernel(int R, int D, const int* labels, const void* dout, float* dtable) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  for (int r = 0; r < R; ++r) dtable[(labels[r] + 1) * D + d] += to_f32(((const T*)dout)[(int64_t)r * D + d]);
+}
+extern "C" int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
+                               hipStream_t st) {
+  if (R * D <= 0) return 0;
+  DISPATCH_T(dt, point_embed_kernel, ew_grid((int64_t)R * D), R, D, pe, labels, table, out);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, const void* dout, float* dtable,
+                                   hipStream_t st) {
+  if (R * D <= 0) return 0;
+  DISPATCH_T(dt, point_embed_bwd_kernel, dim3((D + 255) / 256), R, D, labels, dout, dtable);
+  return (int)hipGetLastError();
+}

@@ -19,6 +19,8 @@ struct GemmArgs {
   const void* R; int64_t ldr, sR;
   void* X; int64_t ldx, sX;  // aux: aux_mode 1 stores pre-activation, 2 multiplies by act'(X)
   int aux_mode;
+  const float* cscale;        // optional per-column scale applied after the activation
+  float drop_p; uint64_t seed; // optional dropout after the activation (index = row*N + col)
   float alpha, beta; int act;
   int vecA, vecB;
 };
@@ -142,6 +144,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
           if (p.aux_mode == 1) ((TC*)p.X)[(int64_t)bz * p.sX + (int64_t)row * p.ldx + col] = from_f32<TC>(v);
           if (p.aux_mode == 2) v *= act_grad(to_f32(((const TC*)p.X)[(int64_t)bz * p.sX + (int64_t)row * p.ldx + col]), p.act);
           else v = apply_act(v, p.act);
+          if (p.cscale) v *= p.cscale[col];
+          if (p.drop_p > 0.f) {
+            const uint64_t idx = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
+            v = s2h_keep(p.seed, idx, (uint32_t)(p.drop_p * 4294967296.0)) ? v / (1.f - p.drop_p) : 0.f;
+          }
           if (R) v += to_f32(R[(int64_t)row * p.ldr + col]);
           int64_t off = (int64_t)row * p.ldc + col;
           if (p.beta != 0.f) v += p.beta * to_f32(C[off]);
@@ -179,6 +186,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
                         const float* bias, int bias_mode,
                         const void* R, int64_t ldr, int64_t sR,
                         void* X, int64_t ldx, int64_t sX, int aux_mode,
+                        const float* cscale, float drop_p, uint64_t seed,
                         float alpha, float beta, int act, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (!(lda_k == 1 || lda_m == 1) || !(ldb_k == 1 || ldb_n == 1)) return (int)hipErrorInvalidValue;
@@ -191,6 +199,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   a.bias = bias; a.bias_mode = bias ? bias_mode : 0;
   a.R = R; a.ldr = ldr; a.sR = sR;
   a.X = X; a.ldx = ldx; a.sX = sX; a.aux_mode = X ? aux_mode : 0;
+  a.cscale = cscale; a.drop_p = drop_p; a.seed = seed;
   a.alpha = alpha; a.beta = beta; a.act = act;
   const int esz = dt_ab == S2H_BF16 ? 2 : 4;
   const int vec = 16 / esz;

@@ -67,14 +67,17 @@ __global__ void mask_loss_finalize_kernel(int N, int64_t P, const float* stats, 
                                           const int* valid, float w_mask, float w_dice, float w_iou, float gscale,
                                           float* losses, float* coef) {
   if (threadIdx.x != 0) return;
+  // valid = categories with ground-truth pixels (losses.py:149-152); derived from the stats
+  // when no explicit flags are given
   int nv = 0;
-  for (int n = 0; n < N; ++n) nv += valid[n] ? 1 : 0;
+  for (int n = 0; n < N; ++n) nv += (valid ? valid[n] != 0 : stats[n * NSTAT + 2] > 0.f) ? 1 : 0;
   const float inv_nv = nv > 0 ? 1.f / (float)nv : 0.f;
   float lm = 0.f, ld = 0.f, li = 0.f;
   for (int n = 0; n < N; ++n) {
     const float* s = stats + n * NSTAT;
     float* c = coef + n * 4;
-    if (!valid[n]) { c[0] = c[1] = c[2] = c[3] = 0.f; continue; }
+    const bool vn = valid ? valid[n] != 0 : s[2] > 0.f;
+    if (!vn) { c[0] = c[1] = c[2] = c[3] = 0.f; continue; }
     lm += s[0] / (float)P;
     const float den = s[1] + s[2] + 1.f;
     ld += 1.f - (2.f * s[3] + 1.f) / den;
@@ -103,8 +106,11 @@ extern "C" int s2h_mask_loss_finalize(int N, int64_t P, const float* stats, cons
 
 // dx[n,p] = inv_temp * ( cf * dfocal/dx + (-(A t - B)) * sigma' )
 __global__ void mask_loss_bwd_kernel(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
-                                     float inv_temp, const float* coef, float* dx, int64_t lddx) {
+                                     float inv_temp, const float* coef, float* dx, int64_t lddx, const float* gtot,
+                                     float* dious) {
   const int64_t n_all = (int64_t)N * P;
+  const float gs = gtot ? gtot[3] : 1.f;  // upstream gradient of the weighted total (device scalar)
+  if (dious && blockIdx.x == 0 && threadIdx.x < N) dious[threadIdx.x] = coef[threadIdx.x * 4 + 3] * gs;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
     const int n = i / P;
     const int64_t p = i - (int64_t)n * P;
@@ -122,17 +128,19 @@ __global__ void mask_loss_bwd_kernel(int N, int64_t P, const float* x, int64_t l
       const float dfocal = at * (-2.f * q * (2.f * t - 1.f) * ds * ce + q * q * (s - t));
       g = c[0] * dfocal - (c[1] * t - c[2]) * ds;
     }
-    dx[n * lddx + p] = g * inv_temp;
+    dx[n * lddx + p] = g * inv_temp * gs;
   }
 }
 extern "C" int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
-                                 float inv_temp, const float* coef, float* dx, int64_t lddx, hipStream_t st) {
+                                 float inv_temp, const float* coef, float* dx, int64_t lddx, const float* gtot,
+                                 float* dious, hipStream_t st) {
   const int64_t n = (int64_t)N * P;
   if (n <= 0) return 0;
+  if (N > 256) return (int)hipErrorInvalidValue;
   int64_t b = (n + 255) / 256;
   if (b > 8192) b = 8192;
   hipLaunchKernelGGL(mask_loss_bwd_kernel, dim3((unsigned)b), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
-                     coef, dx, lddx);
+                     coef, dx, lddx, gtot, dious);
   return (int)hipGetLastError();
 }
 

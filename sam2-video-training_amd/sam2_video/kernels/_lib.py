@@ -25,7 +25,7 @@ F = c_float
 # name -> argtypes (restype is int: a hipError_t value, 0 == success)
 SIGNATURES = {
     "s2h_version": [],
-    "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, F, F, I, P],
+    "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, F, F, I, P],
     "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P],
     "s2h_attn_bwd": [I, I, I, I, I, I,
                      P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
@@ -56,7 +56,7 @@ SIGNATURES = {
     "s2h_gate_mix": [I, L, L, P, P, P, I, I, P, P],
     "s2h_mask_stats": [I, L, P, L, P, L, F, P, P],
     "s2h_mask_loss_finalize": [I, L, P, P, P, F, F, F, F, P, P, P],
-    "s2h_mask_loss_bwd": [I, L, P, L, P, L, F, P, P, L, P],
+    "s2h_mask_loss_bwd": [I, L, P, L, P, L, F, P, P, L, P, P, P],
     "s2h_group_max_fwd": [I, L, P, P, P, L, P, L, P, P],
     "s2h_group_max_bwd": [I, L, P, P, P, L, P, L, P],
     "s2h_group_wavg_fwd": [I, I, P, P, P, P, P, P],
@@ -64,6 +64,10 @@ SIGNATURES = {
     "s2h_sigmoid_grad_axpy": [I, L, P, L, P, P, L, P],
     "s2h_grad_norm": [L, P, P, F, P, P],
     "s2h_adamw": [L, P, P, P, P, P, F, F, F, F, F, I, P, P],
+    "s2h_pos_embed": [I, I, I, I, I, P, P, P, P],
+    "s2h_pos_embed_bwd": [I, I, I, I, I, P, P, P, P],
+    "s2h_point_embed": [I, I, I, P, P, P, P, P],
+    "s2h_point_embed_bwd": [I, I, I, P, P, P, P],
     "s2h_prof_enable": [I],
     "s2h_prof_reset": [],
     "s2h_prof_count": [],

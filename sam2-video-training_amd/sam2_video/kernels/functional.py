@@ -1,0 +1,412 @@
+"""Autograd functions over libsam2hip kernels.
+
+Weights live in the flat fp32 parameter arena (sam2_video.kernels.arena): every
+weight-carrying module exposes `.w` (compute-dtype weight), `.b` (fp32 bias) and
+writes its gradients straight into `param._s2h_grad` (a view of the flat fp32
+gradient arena) inside backward, returning None to autograd.  The Parameter is
+still passed as an input so autograd builds the node whenever the parameter is
+trainable, even when the activation does not require grad.
+
+Every op here launches HIP kernels only (no torch arithmetic on the data path);
+torch provides allocation, views and the autograd tape.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from . import ops
+
+_SEED = [0x5EED]
+
+
+def next_seed():
+    _SEED[0] = (_SEED[0] * 6364136223846793005 + 1442695040888963407) & (2**64 - 1)
+    return _SEED[0]
+
+
+def set_seed(s):
+    _SEED[0] = int(s) & (2**64 - 1)
+
+
+def _grad_of(p):
+    return getattr(p, "_s2h_grad", None) if p is not None and p.requires_grad else None
+
+
+# ---------------------------------------------------------------- Linear
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wp, bp, mod, act, residual, drop_p):
+        w = mod.compute_weight()
+        b = mod.compute_bias()
+        pre = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype) if act else None
+        seed = next_seed() if drop_p > 0 else 0
+        out = ops.linear(x, w, b, act=act, pre=pre, residual=residual, drop_p=drop_p, seed=seed)
+        ctx.mod, ctx.act, ctx.drop_p, ctx.seed = mod, act, drop_p, seed
+        ctx.has_res = residual is not None
+        ctx.save_for_backward(x, pre)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, pre = ctx.saved_tensors
+        mod = ctx.mod
+        dy = dy.contiguous()
+        g = ops.dropout(dy, ctx.drop_p, ctx.seed) if ctx.drop_p > 0 else dy
+        dpre = ops.act_bwd(pre, g, ctx.act) if ctx.act else g
+        gw, gb = mod.grad_views()
+        if gw is not None:
+            ops.linear_wgrad(dpre, x, gw.view(gw.shape[0], -1))
+        if gb is not None:
+            ops.colsum(dpre, gb)
+        dx = ops.linear_dgrad(dpre, mod.compute_weight()) if ctx.needs_input_grad[0] else None
+        return dx, None, None, None, None, (dy if ctx.has_res else None), None
+
+
+def linear(x, mod, act=None, residual=None, drop_p=0.0):
+    """drop(act(x @ W^T + b)) (+ residual).  `mod` provides compute_weight(), compute_bias(),
+    grad_views() and `weight`/`bias` anchors (Parameters) for the autograd tape."""
+    return _Linear.apply(x.contiguous(), mod.weight, mod.bias, mod, act, residual, float(drop_p))
+
+
+# ------------------------------------------------------------- LayerNorm
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gp, bp, mod, eps, add, add_bcast):
+        xsum = torch.empty_like(x) if add is not None else None
+        y, mean, rstd = ops.layernorm_fwd(x, gp.detach(), bp.detach(), eps, add=add, add_bcast=add_bcast, xsum=xsum)
+        ctx.mod = mod
+        ctx.has_add = add is not None
+        ctx.add_bcast = add_bcast
+        ctx.save_for_backward(xsum if add is not None else x, mean, rstd)
+        if add is not None:
+            return y, xsum
+        return y
+
+    @staticmethod
+    def backward(ctx, dy, dxsum=None):
+        x, mean, rstd = ctx.saved_tensors
+        mod = ctx.mod
+        dy = dy.contiguous()
+        gw, gb = _grad_of(mod.weight), _grad_of(mod.bias)
+        dx = None
+        if dxsum is not None:
+            dx = dxsum.contiguous().clone()
+            ops.layernorm_bwd(x, dy, mod.weight.detach(), mean, rstd, dx=dx, accumulate=True, dgamma=gw, dbeta=gb)
+        else:
+            dx = ops.layernorm_bwd(x, dy, mod.weight.detach(), mean, rstd, dgamma=gw, dbeta=gb)
+        dadd = None
+        if ctx.has_add:
+            if ctx.add_bcast:
+                dadd = None  # broadcast adds are constants (positional encodings)
+            else:
+                dadd = dx
+        return dx, None, None, None, None, dadd, None
+
+
+def layer_norm(x, mod, eps):
+    return _LayerNorm.apply(x.contiguous(), mod.weight, mod.bias, mod, eps, None, False)
+
+
+def add_layer_norm(x, add, mod, eps):
+    """returns (LN(x + add), x + add) -- fused residual add + norm"""
+    return _LayerNorm.apply(x.contiguous(), mod.weight, mod.bias, mod, eps, add.contiguous(), False)
+
+
+# ------------------------------------------------------------- attention
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, scale, p_drop):
+        B, Lq, H, D = q.shape
+        o = torch.empty(B, Lq, H, D, device=q.device, dtype=q.dtype)
+        lse = torch.empty(B, H, Lq, device=q.device, dtype=torch.float32)
+        seed = next_seed() if p_drop > 0 else 0
+        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed)
+        ctx.scale, ctx.p, ctx.seed = scale, p_drop, seed
+        ctx.save_for_backward(q, k, v, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse = ctx.saved_tensors
+        do = do.contiguous()
+        dq = torch.empty(q.shape, device=q.device, dtype=q.dtype)
+        dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
+        dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
+        ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed)
+        return dq, dk, dv, None, None
+
+
+def attention(q, k, v, scale=None, p_drop=0.0):
+    """softmax(scale q k^T) v over [B, L, H, D] views (head dim contiguous)."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    return _Attention.apply(q, k, v, float(scale), float(p_drop))
+
+
+# ------------------------------------------------------------------ RoPE
+class _Rope(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, nrot, cos, sin, period):
+        # x [Bt, L, D]; rotates rows < nrot, copies the rest
+        y = torch.empty_like(x)
+        if nrot < x.shape[1]:
+            y[:, nrot:].copy_(x[:, nrot:])
+        ops.rope(x, y, nrot, cos, sin, period)
+        ctx.nrot, ctx.period = nrot, period
+        ctx.save_for_backward(cos, sin)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        cos, sin = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(dy)
+        if ctx.nrot < dy.shape[1]:
+            dx[:, ctx.nrot:].copy_(dy[:, ctx.nrot:])
+        ops.rope(dy, dx, ctx.nrot, cos, sin, ctx.period, inverse=True)
+        return dx, None, None, None, None
+
+
+def rope(x, nrot, cos, sin, period):
+    return _Rope.apply(x.contiguous(), int(nrot), cos, sin, int(period))
+
+
+# ------------------------------------------------------ elementwise / misc
+class _Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, a, b, alpha, beta):
+        ctx.alpha, ctx.beta = alpha, beta
+        return ops.add(a.contiguous(), b.contiguous(), alpha=alpha, beta=beta)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        da = g if ctx.alpha == 1.0 else ops.add(g, None, alpha=ctx.alpha)
+        db = g if ctx.beta == 1.0 else ops.add(g, None, alpha=ctx.beta)
+        return (da if ctx.needs_input_grad[0] else None), (db if ctx.needs_input_grad[1] else None), None, None
+
+
+def add(a, b, alpha=1.0, beta=1.0):
+    return _Add.apply(a, b, float(alpha), float(beta))
+
+
+class _AddBcast(torch.autograd.Function):
+    """out[o, ...] = alpha*a[o, ...] + beta*b[...]   (b broadcast over the leading dim)."""
+
+    @staticmethod
+    def forward(ctx, a, b, alpha, beta, shape, bparam):
+        out = ops.add_bcast(a.contiguous() if a is not None else None, b.contiguous(), alpha=alpha, beta=beta,
+                            shape=shape if a is None else None)
+        ctx.alpha, ctx.beta, ctx.bshape, ctx.bparam = alpha, beta, b.shape, bparam
+        ctx.has_a = a is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        da = None
+        if ctx.has_a and ctx.needs_input_grad[0]:
+            da = g if ctx.alpha == 1.0 else ops.add(g, None, alpha=ctx.alpha)
+        db = None
+        inner = math.prod(ctx.bshape)
+        O = g.numel() // inner
+        if ctx.bparam is not None:
+            gb = _grad_of(ctx.bparam)
+            if gb is not None:
+                if ctx.beta == 1.0:
+                    ops.colsum(g.view(O, inner), gb.view(-1), accumulate=True)
+                else:
+                    tmp = torch.zeros(inner, device=g.device, dtype=torch.float32)
+                    ops.colsum(g.view(O, inner), tmp)
+                    ops.add(gb.view(-1), tmp, beta=ctx.beta, out=gb.view(-1))
+        elif ctx.needs_input_grad[1]:
+            db = torch.empty(ctx.bshape, device=g.device, dtype=g.dtype)
+            ops.sum_outer(g.view(O, inner), db.view(-1))
+            if ctx.beta != 1.0:
+                db = ops.add(db, None, alpha=ctx.beta)
+        return da, db, None, None, None, None
+
+
+def add_bcast(a, b, alpha=1.0, beta=1.0, shape=None, bparam=None):
+    """a + beta*b with b broadcast over leading dims.  If `bparam` (a Parameter) is given,
+    b is its compute copy and its gradient goes to the arena."""
+    return _AddBcast.apply(a, b, float(alpha), float(beta), shape, bparam)
+
+
+class _Act(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        ctx.act = act
+        ctx.save_for_backward(x)
+        return ops.act_fwd(x.contiguous(), act)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        return ops.act_bwd(x, g.contiguous(), ctx.act), None
+
+
+def act(x, a):
+    return _Act.apply(x, a)
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p):
+        ctx.p = p
+        ctx.seed = next_seed()
+        return ops.dropout(x.contiguous(), p, ctx.seed)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.dropout(g.contiguous(), ctx.p, ctx.seed), None
+
+
+def dropout(x, p, training=True):
+    if not training or p <= 0.0:
+        return x
+    return _Dropout.apply(x, float(p))
+
+
+class _MaxPool2(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        ctx.save_for_backward(x)
+        return ops.maxpool2(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x,) = ctx.saved_tensors
+        dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+        ops.maxpool2_bwd(x, g.contiguous(), dx)
+        return dx
+
+
+def maxpool2(x):
+    """2x2 max-pool of NHWC x (pixel stride may exceed C: reads q out of a fused qkv)."""
+    return _MaxPool2.apply(x)
+
+
+class _WindowPartition(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ws):
+        ctx.ws = ws
+        ctx.shape = x.shape
+        return ops.window_partition(x.contiguous(), ws)
+
+    @staticmethod
+    def backward(ctx, g):
+        B, H, W, C = ctx.shape
+        return ops.window_unpartition(g.contiguous(), ctx.ws, B, H, W), None
+
+
+class _WindowUnpartition(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, win, ws, B, H, W):
+        ctx.ws, ctx.BHW = ws, (B, H, W)
+        return ops.window_unpartition(win.contiguous(), ws, B, H, W)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.window_partition(g.contiguous(), ctx.ws), None, None, None, None
+
+
+def window_partition(x, ws):
+    return _WindowPartition.apply(x, int(ws))
+
+
+def window_unpartition(win, ws, B, H, W):
+    return _WindowUnpartition.apply(win, int(ws), int(B), int(H), int(W))
+
+
+class _Up2Add(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, lat, prev):
+        return ops.up2_add(lat.contiguous(), prev.contiguous())
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        B, H, W, C = g.shape
+        dprev = torch.empty(B, H // 2, W // 2, C, device=g.device, dtype=g.dtype)
+        ops.pool2_sum(g, dprev)
+        return g, dprev
+
+
+def up2_add(lat, prev):
+    """FPN top-down: lat + nearest-x2(prev), NHWC"""
+    return _Up2Add.apply(lat, prev)
+
+
+class _Bilinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, ho, wo):
+        ctx.hw = x.shape[-2:]
+        return ops.bilinear(x.contiguous(), ho, wo)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.bilinear_bwd(g.contiguous(), ctx.hw[0], ctx.hw[1]), None, None
+
+
+def bilinear(x, ho, wo):
+    """[N, hi, wi] f32 -> [N, ho, wo] bilinear (align_corners=False)"""
+    return _Bilinear.apply(x, int(ho), int(wo))
+
+
+class _RowGate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gate, fill):
+        ctx.save_for_backward(gate)
+        return ops.row_gate(x.contiguous(), gate, fill)
+
+    @staticmethod
+    def backward(ctx, g):
+        (gate,) = ctx.saved_tensors
+        return ops.row_gate(g.contiguous(), gate, 0.0, backward=True), None, None
+
+
+def row_gate(x, gate, fill):
+    """x[r] if gate[r] > 0 else fill (gate is a non-differentiable f32 [R])"""
+    return _RowGate.apply(x, gate, float(fill))
+
+
+class _Cast(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, dtype):
+        ctx.dtype = x.dtype
+        return ops.cast(x.contiguous(), dtype)
+
+    @staticmethod
+    def backward(ctx, g):
+        return ops.cast(g.contiguous(), ctx.dtype), None
+
+
+def cast(x, dtype):
+    if x.dtype == dtype:
+        return x
+    return _Cast.apply(x, dtype)
+
+
+class _SumOuter(torch.autograd.Function):
+    """x [1, ...] broadcast to [O, ...]: forward copies, backward sums over O."""
+
+    @staticmethod
+    def forward(ctx, x, O):
+        ctx.O = O
+        out = ops.add_bcast(None, x.contiguous(), shape=(O, *x.shape[1:]))
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        d = torch.empty((1, *g.shape[1:]), device=g.device, dtype=g.dtype)
+        ops.sum_outer(g, d.view(-1))
+        return d, None
+
+
+def expand_batch(x, O):
+    """[1, ...] -> [O, ...] materialised broadcast (grad = sum over O)"""
+    return _SumOuter.apply(x, int(O))

@@ -41,14 +41,14 @@ def _dev(*ts):
 # ----------------------------------------------------------------- GEMM
 def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB=0, sC=0,
          bias=None, bias_mode=1, residual=None, ldr=0, sR=0, aux=None, ldx=0, sX=0, aux_mode=0,
-         alpha=1.0, beta=0.0, act=0):
+         cscale=None, drop_p=0.0, seed=0, alpha=1.0, beta=0.0, act=0):
     _dev(a, b, c, bias, residual, aux)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     call("s2h_gemm", dt(a), dt(c), batch, M, N, K,
          ptr(a), lda_m, lda_k, sA, ptr(b), ldb_k, ldb_n, sB, ptr(c), ldc, sC,
          ptr(bias), bias_mode, ptr(residual), ldr, sR, ptr(aux), ldx, sX, aux_mode,
-         float(alpha), float(beta), int(act), stream())
+         ptr(cscale), float(drop_p), int(seed) & (2**64 - 1), float(alpha), float(beta), int(act), stream())
     return c
 
 
@@ -57,8 +57,9 @@ def _rows(x):
     return x.numel() // x.shape[-1], x.shape[-1]
 
 
-def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dtype=None):
-    """out = act(x @ w^T + bias) (+ residual); optionally stores the pre-activation in `pre`."""
+def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dtype=None, cscale=None,
+           drop_p=0.0, seed=0):
+    """out = drop(act(x @ w^T + bias) * cscale) (+ residual); optionally stores the pre-activation in `pre`."""
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
     N = w.shape[0]
@@ -69,7 +70,8 @@ def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dty
     r2 = residual.reshape(-1, N) if residual is not None else None
     p2 = pre.view(-1, N) if pre is not None else None
     gemm(x2, w, o2, M=M, N=N, K=K, lda_m=x2.stride(0), lda_k=1, ldb_k=1, ldb_n=K, ldc=N,
-         bias=bias, residual=r2, ldr=N, aux=p2, ldx=N, aux_mode=1 if pre is not None else 0, act=ACT[act])
+         bias=bias, residual=r2, ldr=N, aux=p2, ldx=N, aux_mode=1 if pre is not None else 0, act=ACT[act],
+         cscale=cscale, drop_p=drop_p, seed=seed)
     return out
 
 
@@ -372,10 +374,10 @@ def mask_loss_finalize(stats, pred_iou, valid, P, weights, gscale, losses, coef)
          float(weights[1]), float(weights[2]), float(gscale), ptr(losses), ptr(coef), stream())
 
 
-def mask_loss_bwd(x, tgt, coef, inv_temp, dx):
+def mask_loss_bwd(x, tgt, coef, inv_temp, dx, gtot=None, dious=None):
     N, P = x.shape
     call("s2h_mask_loss_bwd", N, P, ptr(x), x.stride(0), ptr(tgt), tgt.stride(0), float(inv_temp), ptr(coef),
-         ptr(dx), dx.stride(0), stream())
+         ptr(dx), dx.stride(0), ptr(gtot), ptr(dious), stream())
     return dx
 
 
@@ -419,6 +421,30 @@ def grad_norm(g, max_norm, ws, out):
 def adamw(p, g, m, v, clip, lr, beta1, beta2, eps, wd, step, shadow=None):
     call("s2h_adamw", p.numel(), ptr(p), ptr(g), ptr(m), ptr(v), ptr(clip), float(lr), float(beta1), float(beta2),
          float(eps), float(wd), int(step), ptr(shadow), stream())
+
+
+def pos_embed(Y, win, h, w, out):
+    """out [h, w, C] = Y [C, h, w] + tile(win [C, ws, ws])"""
+    C = Y.shape[0]
+    ws = win.shape[-1]
+    call("s2h_pos_embed", dt(out), C, h, w, ws, ptr(Y), ptr(win.contiguous()), ptr(out), stream())
+    return out
+
+
+def pos_embed_bwd(dout, dY, dwin, ws):
+    h, w, C = dout.shape
+    call("s2h_pos_embed_bwd", dt(dout), C, h, w, ws, ptr(dout), ptr(dY), ptr(dwin), stream())
+
+
+def point_embed(pe, labels, table, out):
+    R, D = pe.shape
+    call("s2h_point_embed", dt(out), R, D, ptr(pe), ptr(labels), ptr(table), ptr(out), stream())
+    return out
+
+
+def point_embed_bwd(labels, dout, dtable):
+    R, D = dout.shape
+    call("s2h_point_embed_bwd", dt(dout), R, D, ptr(labels), ptr(dout), ptr(dtable), stream())
 
 
 def version():

@@ -1,0 +1,149 @@
+"""Hiera trunk (reference: sam2_video/model/modeling/backbones/hieradet.py, upstream
+sam2.modeling.backbones.hieradet), NHWC on the device.
+
+Same constructor signature / parameter names as the reference (hieradet.py:169-262)
+so SAM2.1 checkpoints load.  Per block: LayerNorm kernel -> (proj + 2x2 max-pool
+shortcut) -> window partition (zero pad) -> fused qkv GEMM -> (q max-pool read
+in place from the qkv tensor) -> flash attention over [windows, L, heads, d] ->
+proj GEMM -> unpartition -> residual-add fused into norm2 -> MLP GEMMs (GELU in
+the epilogue, residual in the second epilogue).
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import torch
+from torch import nn
+
+from ....kernels import functional as FN
+from ....kernels import ops
+from ....kernels.functional_sam import hiera_pos_embed
+from ..layers import MLP, Conv2d, LayerNorm, Linear
+
+
+class MultiScaleAttention(nn.Module):
+    """hieradet.py:39-81"""
+
+    def __init__(self, dim: int, dim_out: int, num_heads: int, q_pool: bool = False):
+        super().__init__()
+        self.dim, self.dim_out, self.num_heads, self.q_pool = dim, dim_out, num_heads, q_pool
+        self.qkv = Linear(dim, dim_out * 3)
+        self.proj = Linear(dim_out, dim_out)
+
+    def forward(self, x):
+        B, H, W, _ = x.shape
+        d, nh = self.dim_out, self.num_heads
+        qkv = self.qkv(x)  # [B, H, W, 3d]
+        qkv5 = qkv.view(B, H * W, 3, nh, d // nh)
+        k, v = qkv5[:, :, 1], qkv5[:, :, 2]
+        if self.q_pool:
+            q = FN.maxpool2(qkv[..., :d])  # pooled straight out of the fused qkv (pixel stride 3d)
+            H, W = H // 2, W // 2
+            q = q.view(B, H * W, nh, d // nh)
+        else:
+            q = qkv5[:, :, 0]
+        o = FN.attention(q, k, v)
+        return self.proj(o.reshape(B, H, W, d))
+
+
+class MultiScaleBlock(nn.Module):
+    """hieradet.py:84-166"""
+
+    def __init__(self, dim, dim_out, num_heads, mlp_ratio=4.0, drop_path=0.0, norm_layer="LayerNorm",
+                 q_stride=None, act_layer=None, window_size=0):
+        super().__init__()
+        self.dim, self.dim_out = dim, dim_out
+        self.norm1 = LayerNorm(dim, eps=1e-6)
+        self.window_size = window_size
+        self.q_stride = q_stride
+        self.attn = MultiScaleAttention(dim, dim_out, num_heads=num_heads, q_pool=bool(q_stride))
+        self.norm2 = LayerNorm(dim_out, eps=1e-6)
+        self.mlp = MLP(dim_out, int(dim_out * mlp_ratio), dim_out, num_layers=2, activation="gelu")
+        if dim != dim_out:
+            self.proj = Linear(dim, dim_out)
+
+    def forward(self, x):
+        B = x.shape[0]
+        xn = self.norm1(x)
+        shortcut = x
+        if self.dim != self.dim_out:
+            shortcut = self.proj(xn)
+            if self.q_stride:
+                shortcut = FN.maxpool2(shortcut)
+        ws = self.window_size
+        H, W = xn.shape[1:3]
+        xw = FN.window_partition(xn, ws) if ws > 0 else xn
+        y = self.attn(xw)
+        if self.q_stride:
+            ws = ws // self.q_stride[0]
+            H, W = shortcut.shape[1:3]
+        if self.window_size > 0:
+            y = FN.window_unpartition(y, ws, B, H, W)
+        h, x = FN.add_layer_norm(shortcut, y, self.norm2, self.norm2.eps)
+        h = self.mlp.layers[0](h, act="gelu")
+        return self.mlp.layers[1](h, residual=x)
+
+
+class PatchEmbed(nn.Module):
+    """backbones/utils.py:63-93 -- conv 7x7/4 as im2col + GEMM"""
+
+    def __init__(self, kernel_size=(7, 7), stride=(4, 4), padding=(3, 3), in_chans=3, embed_dim=768):
+        super().__init__()
+        self.k, self.s, self.p = kernel_size[0], stride[0], padding[0]
+        self.proj = Conv2d(in_chans, embed_dim, self.k, self.s, self.p)
+
+    def forward(self, x_nhwc):
+        T = x_nhwc.shape[0]
+        col, Ho, Wo = ops.im2col(x_nhwc, self.k, self.k, self.s, self.p)
+        return self.proj(col).view(T, Ho, Wo, -1)
+
+
+class Hiera(nn.Module):
+    """hieradet.py:169-299"""
+
+    def __init__(self, embed_dim: int = 96, num_heads: int = 1, drop_path_rate: float = 0.0, q_pool: int = 3,
+                 q_stride: Tuple[int, int] = (2, 2), stages=(2, 3, 16, 3), dim_mul: float = 2.0,
+                 head_mul: float = 2.0, window_pos_embed_bkg_spatial_size=(14, 14), window_spec=(8, 4, 14, 7),
+                 global_att_blocks=(12, 16, 20), weights_path=None, return_interm_layers=True):
+        super().__init__()
+        assert len(stages) == len(window_spec)
+        self.window_spec = window_spec
+        depth = sum(stages)
+        self.q_stride = tuple(q_stride)
+        self.stage_ends = [sum(stages[:i]) - 1 for i in range(1, len(stages) + 1)]
+        self.q_pool_blocks = [x + 1 for x in self.stage_ends[:-1]][:q_pool]
+        self.return_interm_layers = return_interm_layers
+        self.patch_embed = PatchEmbed(embed_dim=embed_dim)
+        self.global_att_blocks = global_att_blocks
+        self.window_pos_embed_bkg_spatial_size = window_pos_embed_bkg_spatial_size
+        self.pos_embed = nn.Parameter(torch.zeros(1, embed_dim, *window_pos_embed_bkg_spatial_size))
+        self.pos_embed_window = nn.Parameter(torch.zeros(1, embed_dim, window_spec[0], window_spec[0]))
+        cur_stage = 1
+        self.blocks = nn.ModuleList()
+        for i in range(depth):
+            dim_out = embed_dim
+            window_size = self.window_spec[cur_stage - 1]
+            if self.global_att_blocks is not None:
+                window_size = 0 if i in self.global_att_blocks else window_size
+            if i - 1 in self.stage_ends:
+                dim_out = int(embed_dim * dim_mul)
+                num_heads = int(num_heads * head_mul)
+                cur_stage += 1
+            self.blocks.append(MultiScaleBlock(dim=embed_dim, dim_out=dim_out, num_heads=num_heads,
+                                               q_stride=self.q_stride if i in self.q_pool_blocks else None,
+                                               window_size=window_size))
+            embed_dim = dim_out
+        self.channel_list = ([self.blocks[i].dim_out for i in self.stage_ends[::-1]] if return_interm_layers
+                             else [self.blocks[-1].dim_out])
+
+    def forward(self, x_nhwc) -> List[torch.Tensor]:
+        """x: [T, H, W, 3] compute dtype -> stage outputs NHWC (high -> low resolution)"""
+        x = self.patch_embed(x_nhwc)
+        pe = hiera_pos_embed(self.pos_embed, self.pos_embed_window, x.shape[1], x.shape[2], x.dtype)
+        x = FN.add_bcast(x, pe)
+        outputs = []
+        for i, blk in enumerate(self.blocks):
+            x = blk(x)
+            if (i == self.stage_ends[-1]) or (i in self.stage_ends and self.return_interm_layers):
+                outputs.append(x)
+        return outputs

@@ -1,0 +1,104 @@
+"""Memory attention (reference memory_attention.py:17-169), batch-first [O, L, C].
+
+Per layer: LN1 -> fused q/k/v GEMM (arena-adjacent weights) -> RoPE(q, k) ->
+flash attention -> out-proj GEMM with dropout + residual in the epilogue;
+LN2 -> q GEMM + RoPE, k GEMM on (memory + memory_pos) + RoPE on the spatial
+rows (table repeated per memory frame, object-pointer rows excluded), v GEMM on
+memory -> flash attention over Lk = n_frames*L + 4*n_ptr -> out-proj (+res);
+LN3 -> linear1 (ReLU + dropout in the epilogue) -> linear2 (+dropout, +res).
+"""
+from __future__ import annotations
+
+import copy
+
+from torch import nn
+
+from ...kernels import functional as FN
+from .layers import FusedLinear, LayerNorm, Linear
+
+
+class MemoryAttentionLayer(nn.Module):
+    """memory_attention.py:17-99"""
+
+    def __init__(self, activation: str, cross_attention: nn.Module, d_model: int, dim_feedforward: int,
+                 dropout: float, pos_enc_at_attn: bool, pos_enc_at_cross_attn_keys: bool,
+                 pos_enc_at_cross_attn_queries: bool, self_attention: nn.Module):
+        super().__init__()
+        assert activation == "relu" and not pos_enc_at_attn and pos_enc_at_cross_attn_keys
+        assert not pos_enc_at_cross_attn_queries
+        self.d_model = d_model
+        self.dim_feedforward = dim_feedforward
+        self.dropout_value = dropout
+        self.self_attn = self_attention
+        self.cross_attn_image = cross_attention
+        self.linear1 = Linear(d_model, dim_feedforward)
+        self.linear2 = Linear(dim_feedforward, d_model)
+        self.norm1 = LayerNorm(d_model)
+        self.norm2 = LayerNorm(d_model)
+        self.norm3 = LayerNorm(d_model)
+        self._fused_qkv = None
+
+    def bind_arena(self, arena):
+        sa = self.self_attn
+        f = FusedLinear([sa.q_proj, sa.k_proj, sa.v_proj], arena)
+        self._fused_qkv = f if f.packed else None
+
+    def arena_groups(self, prefix):
+        sa = prefix + ".self_attn"
+        return [[f"{sa}.q_proj.weight", f"{sa}.k_proj.weight", f"{sa}.v_proj.weight"],
+                [f"{sa}.q_proj.bias", f"{sa}.k_proj.bias", f"{sa}.v_proj.bias"]]
+
+    def _drop(self):
+        return self.dropout_value if self.training else 0.0
+
+    def forward(self, tgt, mem_k, mem_v, num_k_exclude_rope=0):
+        L = tgt.shape[1]
+        C = self.d_model
+        p = self._drop()
+        # self-attention (:58-64), q = k = v = norm1(tgt), RoPE on q and k
+        sa = self.self_attn
+        t2 = self.norm1(tgt)
+        if self._fused_qkv is not None:
+            qkv = self._fused_qkv(t2)
+            q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+        else:
+            q, k, v = sa.q_proj(t2), sa.k_proj(t2), sa.v_proj(t2)
+        q = sa.rope_q(q, L)
+        k = sa.rope_k(k, L)
+        tgt = sa.attend(q, k, v, residual=tgt, out_drop=p)
+        # cross-attention to the memory bank (:66-81)
+        ca = self.cross_attn_image
+        t2 = self.norm2(tgt)
+        q = ca.rope_q(ca.q_proj(t2), L)
+        k = ca.rope_k(ca.k_proj(mem_k), L, num_k_exclude_rope)
+        v = ca.v_proj(mem_v)
+        tgt = ca.attend(q, k, v, residual=tgt, out_drop=p)
+        # feed-forward (:95-98)
+        t2 = self.norm3(tgt)
+        h = self.linear1(t2, act="relu", drop_p=p)
+        return self.linear2(h, residual=tgt, drop_p=p)
+
+
+class MemoryAttention(nn.Module):
+    """memory_attention.py:102-169"""
+
+    def __init__(self, d_model: int, pos_enc_at_input: bool, layer: nn.Module, num_layers: int,
+                 batch_first: bool = True):
+        super().__init__()
+        self.d_model = d_model
+        self.layers = nn.ModuleList([copy.deepcopy(layer) for _ in range(num_layers)])
+        self.num_layers = num_layers
+        self.norm = LayerNorm(d_model)
+        self.pos_enc_at_input = pos_enc_at_input
+        self.batch_first = batch_first
+
+    def forward(self, curr, curr_pos, memory, memory_pos_table, num_obj_ptr_tokens=0, num_objects=1):
+        """curr [L, C] (one frame, shared by all objects), curr_pos [L, C] constant,
+        memory [O, M, 64] (detached bank), memory_pos_table [M, 64] (shared by objects)
+        -> [O, L, C]"""
+        x = FN.add(curr, curr_pos, beta=0.1) if self.pos_enc_at_input else curr
+        x = FN.expand_batch(x.unsqueeze(0), num_objects)
+        mem_k = FN.add_bcast(memory, memory_pos_table)
+        for layer in self.layers:
+            x = layer(x, mem_k, memory, num_k_exclude_rope=num_obj_ptr_tokens)
+        return self.norm(x)

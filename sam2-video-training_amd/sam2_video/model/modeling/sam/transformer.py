@@ -1,0 +1,139 @@
+"""Attention modules (reference sam/transformer.py:19-311), batch-first [B, L, C].
+
+Attention: q/k/v projection GEMMs, flash attention over [B, L, heads, d] views
+of the projections (no head transposes), out-projection GEMM with the residual
+add fused in its epilogue.  RoPEAttention adds the axial 2-D rotary encoding
+(q fully, k on the first Lk - num_k_exclude_rope rows with the table repeated
+every Lq rows, i.e. rope_k_repeat) using cached cos/sin tables."""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import nn
+
+from ....kernels import functional as FN
+from ..layers import MLP, LayerNorm, Linear
+from ..position_encoding import axial_rope_table
+
+
+class Attention(nn.Module):
+    """transformer.py:190-248"""
+
+    def __init__(self, embedding_dim, num_heads, downsample_rate=1, dropout=0.0, kv_in_dim=None):
+        super().__init__()
+        self.embedding_dim = embedding_dim
+        self.kv_in_dim = kv_in_dim if kv_in_dim is not None else embedding_dim
+        self.internal_dim = embedding_dim // downsample_rate
+        self.num_heads = num_heads
+        assert self.internal_dim % num_heads == 0
+        self.q_proj = Linear(embedding_dim, self.internal_dim)
+        self.k_proj = Linear(self.kv_in_dim, self.internal_dim)
+        self.v_proj = Linear(self.kv_in_dim, self.internal_dim)
+        self.out_proj = Linear(self.internal_dim, embedding_dim)
+        self.dropout_p = dropout
+
+    def _p(self):
+        return self.dropout_p if self.training else 0.0
+
+    def attend(self, q, k, v, residual=None, out_drop=0.0):
+        """q [B, Lq, I], k/v [B, Lk, I] projected -> out_proj(attn) (+ residual)"""
+        B, Lq, I = q.shape
+        Lk = k.shape[1]
+        h = self.num_heads
+        o = FN.attention(q.view(B, Lq, h, I // h), k.view(B, Lk, h, I // h), v.view(B, Lk, h, I // h),
+                         p_drop=self._p())
+        return self.out_proj(o.reshape(B, Lq, I), residual=residual, drop_p=out_drop)
+
+    def forward(self, q, k, v, residual=None):
+        return self.attend(self.q_proj(q), self.k_proj(k), self.v_proj(v), residual=residual)
+
+
+class RoPEAttention(Attention):
+    """transformer.py:251-311"""
+
+    def __init__(self, *args, rope_theta=10000.0, rope_k_repeat=False, feat_sizes=(64, 64), **kwargs):
+        super().__init__(*args, **kwargs)
+        self.rope_theta = rope_theta
+        self.rope_k_repeat = rope_k_repeat
+        self.head_dim = self.internal_dim // self.num_heads
+
+    def tables(self, Lq, device):
+        w = h = math.sqrt(Lq)
+        return axial_rope_table(self.head_dim, w, h, self.rope_theta, device)
+
+    def rope_q(self, q, Lq):
+        cos, sin = self.tables(Lq, q.device)
+        return FN.rope(q, Lq, cos, sin, Lq)
+
+    def rope_k(self, k, Lq, num_k_exclude_rope=0):
+        nr = k.shape[1] - num_k_exclude_rope
+        if nr != Lq:
+            assert self.rope_k_repeat
+        cos, sin = self.tables(Lq, k.device)
+        return FN.rope(k, nr, cos, sin, Lq)
+
+    def forward(self, q, k, v, num_k_exclude_rope=0, residual=None, out_drop=0.0):
+        Lq = q.shape[1]
+        qp = self.rope_q(self.q_proj(q), Lq)
+        kp = self.rope_k(self.k_proj(k), Lq, num_k_exclude_rope)
+        return self.attend(qp, kp, self.v_proj(v), residual=residual, out_drop=out_drop)
+
+
+class TwoWayAttentionBlock(nn.Module):
+    """transformer.py:112-187"""
+
+    def __init__(self, embedding_dim, num_heads, mlp_dim=2048, activation=None, attention_downsample_rate=2,
+                 skip_first_layer_pe=False):
+        super().__init__()
+        self.self_attn = Attention(embedding_dim, num_heads)
+        self.norm1 = LayerNorm(embedding_dim)
+        self.cross_attn_token_to_image = Attention(embedding_dim, num_heads, downsample_rate=attention_downsample_rate)
+        self.norm2 = LayerNorm(embedding_dim)
+        self.mlp = MLP(embedding_dim, mlp_dim, embedding_dim, num_layers=2, activation="relu")
+        self.norm3 = LayerNorm(embedding_dim)
+        self.norm4 = LayerNorm(embedding_dim)
+        self.cross_attn_image_to_token = Attention(embedding_dim, num_heads, downsample_rate=attention_downsample_rate)
+        self.skip_first_layer_pe = skip_first_layer_pe
+
+    def forward(self, queries, keys, query_pe, key_pe_table):
+        if self.skip_first_layer_pe:
+            queries = self.self_attn(queries, queries, queries)
+        else:
+            q = FN.add(queries, query_pe)
+            queries = self.self_attn(q, q, queries, residual=queries)
+        queries = self.norm1(queries)
+        q = FN.add(queries, query_pe)
+        k = FN.add_bcast(keys, key_pe_table)
+        queries = self.cross_attn_token_to_image(q, k, keys, residual=queries)
+        queries = self.norm2(queries)
+        queries = self.mlp(queries, residual=queries)
+        queries = self.norm3(queries)
+        q = FN.add(queries, query_pe)
+        keys = self.cross_attn_image_to_token(k, q, queries, residual=keys)
+        keys = self.norm4(keys)
+        return queries, keys
+
+
+class TwoWayTransformer(nn.Module):
+    """transformer.py:19-109"""
+
+    def __init__(self, depth, embedding_dim, num_heads, mlp_dim, activation=None, attention_downsample_rate=2):
+        super().__init__()
+        self.depth = depth
+        self.layers = nn.ModuleList(
+            TwoWayAttentionBlock(embedding_dim, num_heads, mlp_dim, attention_downsample_rate=attention_downsample_rate,
+                                 skip_first_layer_pe=(i == 0)) for i in range(depth))
+        self.final_attn_token_to_image = Attention(embedding_dim, num_heads, downsample_rate=attention_downsample_rate)
+        self.norm_final_attn = LayerNorm(embedding_dim)
+
+    def forward(self, image_embedding, image_pe_table, point_embedding):
+        """image_embedding [B, HW, C]; image_pe_table [HW, C] constant; point_embedding [B, T, C]"""
+        queries, keys = point_embedding, image_embedding
+        for layer in self.layers:
+            queries, keys = layer(queries, keys, point_embedding, image_pe_table)
+        q = FN.add(queries, point_embedding)
+        k = FN.add_bcast(keys, image_pe_table)
+        queries = self.final_attn_token_to_image(q, k, keys, residual=queries)
+        queries = self.norm_final_attn(queries)
+        return queries, keys

@@ -1,0 +1,243 @@
+"""SAM2Model -- drop-in for sam2_video.model.sam2model.SAM2Model (reference
+sam2_video/model/sam2model.py:28-616): same constructor, same
+forward(BatchedVideoDatapoint) -> (per-frame category-level outputs, obj_to_cat),
+same state_dict keys as upstream SAM2 (checkpoints load), same freezing
+semantics.  The heavy lifting runs in libsam2hip on the GPU.
+
+Differences that are not observable in the outputs:
+  * the reference builds an upstream model and grafts its attributes onto a
+    SAM2Base (sam2model.py:80-105); this build instantiates its own modules
+    directly from the same config;
+  * parameters live in a flat device arena (kernels/arena.py) after `load(device)`;
+  * the memory encoder runs without an autograd tape (its outputs are detached
+    into the memory bank in the reference, so it never receives a gradient).
+"""
+from __future__ import annotations
+
+import os
+from collections import OrderedDict
+from typing import Any, Dict, List, Optional, Tuple
+
+import torch
+from torch import nn
+
+from .. import utils
+from ..data.data_utils import BatchedVideoDatapoint
+from ..kernels.arena import ParamArena
+from ..utils.init import synth_tensor
+from ..utils.masks import merge_object_results_to_category
+from .build import instantiate, load_model_config
+from .modeling.sam2_base import SAM2Base
+
+DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32,
+          torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
+
+
+class SAM2Model(SAM2Base):
+    def __init__(self, checkpoint_path: Optional[str], config_path: str, fintuned_model_path: Optional[str] = None,
+                 trainable_modules: Optional[List[str]] = None, device: str = "cuda", prompt_type: str = "point",
+                 forward_backbone_per_frame_for_eval: bool = False, num_pos_points: int = 1,
+                 num_neg_points: int = 0, include_center: bool = True, use_activation_checkpoint: bool = False,
+                 random_init_memory_modules: bool = False, compute_dtype="bf16", image_size: Optional[int] = None,
+                 init_seed: int = 0):
+        self.checkpoint_path = checkpoint_path
+        self.config_path = config_path
+        self.prompt_type = prompt_type
+        assert prompt_type in ["point", "box", "mask"], f"prompt_type must be one of point/box/mask, got {prompt_type}"
+        if prompt_type == "mask":
+            raise NotImplementedError("mask prompts (use_mask_input_as_output_without_sam path) are not built yet")
+        self.forward_backbone_per_frame_for_eval = forward_backbone_per_frame_for_eval
+        self.num_pos_points = num_pos_points
+        self.num_neg_points = num_neg_points
+        self.include_center = include_center
+        self.fintuned_model_path = fintuned_model_path
+        cfg = load_model_config(config_path, image_size)
+        kw = {k: instantiate(v) for k, v in cfg.items() if k != "_target_"}
+        super().__init__(use_activation_checkpoint=use_activation_checkpoint, **kw)
+        self.compute_dtype = DTYPES[compute_dtype]
+        self.arena: Optional[ParamArena] = None
+        self._load_weights(checkpoint_path, init_seed)
+        if fintuned_model_path is not None:
+            self._load_finetuned(fintuned_model_path)
+        if random_init_memory_modules:
+            self._randomly_initialize_memory_modules(init_seed + 1)
+        self._setup_trainable_modules(trainable_modules or ["memory_attention", "memory_encoder"])
+
+    # ----------------------------------------------------------- weights
+    def _load_weights(self, checkpoint_path, seed):
+        sd = self.state_dict()
+        if checkpoint_path and os.path.exists(str(checkpoint_path)):
+            ck = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+            if isinstance(ck, dict) and "model" in ck:
+                ck = ck["model"]
+            self.load_state_dict(ck, strict=True)
+        else:  # offline: deterministic synthetic weights keyed by parameter name
+            self.load_state_dict({k: synth_tensor(k, v.shape, seed) for k, v in sd.items()}, strict=True)
+
+    def _load_finetuned(self, path):
+        """sam2model.py:109-126"""
+        if path.count("all") > 0:
+            sd = torch.load(path, map_location="cpu", weights_only=True)
+            self.load_state_dict(sd if isinstance(sd, (dict, OrderedDict)) else sd.state_dict(), strict=False)
+        else:
+            self.sam_mask_decoder.load_state_dict(torch.load(path, map_location="cpu", weights_only=True), strict=True)
+            pe_path = path.replace(".torch", "_prompt_encoder.torch")
+            if os.path.exists(pe_path):
+                self.sam_prompt_encoder.load_state_dict(torch.load(pe_path, map_location="cpu", weights_only=True),
+                                                        strict=True)
+
+    def _randomly_initialize_memory_modules(self, seed):
+        for name in ("memory_attention", "memory_encoder"):
+            mod = getattr(self, name)
+            for n, p in mod.named_parameters():
+                p.data.copy_(synth_tensor(f"{name}.{n}", p.shape, seed))
+
+    def _get_module_mapping(self) -> Dict[str, nn.Module]:
+        """sam2model.py:550-565"""
+        return {"image_encoder": self.image_encoder, "memory_attention": self.memory_attention,
+                "memory_encoder": self.memory_encoder, "prompt_encoder": self.sam_prompt_encoder,
+                "mask_decoder": self.sam_mask_decoder, "obj_ptr_proj": self.obj_ptr_proj,
+                "obj_ptr_tpos_proj": self.obj_ptr_tpos_proj}
+
+    def _setup_trainable_modules(self, trainable_modules: List[str]) -> None:
+        self.trainable_modules = list(trainable_modules)
+        utils.setup_trainable_modules(self, self._get_module_mapping(), self.trainable_modules)
+
+    def freeze_module(self, module_name):
+        utils.freeze_module_by_name(self._get_module_mapping(), module_name)
+
+    def unfreeze_module(self, module_name):
+        utils.unfreeze_module_by_name(self._get_module_mapping(), module_name)
+
+    def get_trainable_modules(self):
+        return utils.get_trainable_module_names(self._get_module_mapping())
+
+    def never_grad_parameter_names(self) -> List[str]:
+        """Trainable parameters that the training step never reaches with a gradient (their
+        .grad stays None in the reference, so AdamW skips them): the memory encoder and the
+        object-pointer path (both detached into the bank, sam2model.py:340-358), the unused
+        no-memory position encoding, the mask-prompt down-sampling convs (point/box prompts)
+        and the object-score head (its logits only gate; pred_obj_scores=False in the loss)."""
+        out = []
+        for n, p in self.named_parameters():
+            if not p.requires_grad:
+                continue
+            if (n.startswith("memory_encoder.") or n in ("no_mem_pos_enc", "no_obj_ptr", "no_obj_embed_spatial")
+                    or n.startswith("mask_downsample.") or n.startswith("sam_prompt_encoder.mask_downscaling.")
+                    or n.startswith("sam_mask_decoder.pred_obj_score_head.") or n.startswith("obj_ptr_proj.")):
+                out.append(n)
+        return out
+
+    def load(self, device: str = None) -> "SAM2Model":
+        """Move to `device` and build the parameter arena (call again after re-freezing)."""
+        device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+        if device.type != "cuda":
+            raise RuntimeError("SAM2Model runs on MI355X only (libsam2hip has no CPU path)")
+        for name, buf in self.named_buffers():
+            mod = self.get_submodule(name.rsplit(".", 1)[0]) if "." in name else self
+            setattr(mod, name.rsplit(".", 1)[-1], buf.to(device))
+        never = set(self.never_grad_parameter_names())
+        named = list(self.named_parameters())
+        grad_names = [n for n, p in named if p.requires_grad and n not in never]
+        groups = []
+        for i, layer in enumerate(self.memory_attention.layers):
+            groups += layer.arena_groups(f"memory_attention.layers.{i}")
+        self.arena = ParamArena(named, grad_names, self.compute_dtype, device, groups=groups)
+        for m in self.modules():
+            if hasattr(m, "bind_arena"):
+                m.bind_arena(self.arena)
+        return self
+
+    def set_dropout(self, p: float):
+        """override every dropout probability (p=0 gives the deterministic parity mode)"""
+        for m in self.modules():
+            if hasattr(m, "dropout_p"):
+                m.dropout_p = p
+            if hasattr(m, "dropout_value"):
+                m.dropout_value = p
+
+    def count_trainable_parameters(self) -> int:
+        return utils.count_trainable_parameters(self)
+
+    def count_total_parameters(self) -> int:
+        return utils.count_total_parameters(self)
+
+    def get_info(self) -> Dict[str, Any]:
+        return utils.get_model_info(self, self.checkpoint_path, self.config_path, str(self.device))
+
+    # ------------------------------------------------------------- forward
+    def forward(self, input: BatchedVideoDatapoint) -> Tuple[List[Dict[str, Any]], List[int]]:
+        """sam2model.py:153-179"""
+        if self.arena is None:
+            raise RuntimeError("call SAM2Model.load(device) before forward")
+        backbone_out = self.forward_image(input.flat_img_batch)
+        backbone_out = self.prepare_prompt_inputs(backbone_out, input)
+        stages = self.forward_tracking(backbone_out, input)
+        out = merge_object_results_to_category(stages, backbone_out["obj_to_cat"], backbone_out["num_categories"])
+        return out, backbone_out["obj_to_cat"]
+
+    def prepare_prompt_inputs(self, backbone_out, input, start_frame_idx=0):
+        """sam2model.py:181-236 -- frame-0 category masks -> objects -> clicks (host side)"""
+        masks0 = input.masks[start_frame_idx].unsqueeze(1)
+        obj_masks, obj_to_cat, num_categories = utils.cat_to_obj_mask(masks0)
+        backbone_out["num_frames"] = input.num_frames
+        backbone_out["obj_to_cat"] = obj_to_cat
+        backbone_out["num_categories"] = num_categories
+        if self.prompt_type == "box":
+            points, labels = utils.generate_box_prompt(obj_masks)
+        else:
+            points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
+                                                         num_neg_points=self.num_neg_points,
+                                                         include_center=self.include_center)
+        O = len(obj_to_cat)
+        dev = self.arena.device
+        pe0, lab0 = self.sam_prompt_encoder.host_points(points, labels, pad=True)
+        pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
+                                                        pad=True)
+        backbone_out["prompt_cond"] = (pe0.to(dev, non_blocking=True), lab0.to(dev, non_blocking=True))
+        backbone_out["prompt_pad"] = (pe1.to(dev, non_blocking=True), lab1.to(dev, non_blocking=True))
+        backbone_out["point_inputs_per_frame"] = {start_frame_idx: {"point_coords": points, "point_labels": labels}}
+        backbone_out["mask_inputs_per_frame"] = {}
+        return backbone_out
+
+    def forward_tracking(self, backbone_out, input: BatchedVideoDatapoint, return_dict=False):
+        """sam2model.py:266-401 -- sequential frames, detached memory bank pruned to the
+        last num_maskmem-1 non-conditioning frames."""
+        fpn = backbone_out["backbone_fpn"]
+        T = backbone_out["num_frames"]
+        h = w = self.sam_image_embedding_size
+        feats = fpn[-1].reshape(T, h * w, -1)
+        pos = backbone_out["vision_pos_enc"][-1]
+        s0, s1 = fpn[0], fpn[1]
+        O = len(backbone_out["obj_to_cat"])
+        output_dict = {"cond_frame_outputs": {}, "non_cond_frame_outputs": {}}
+        frames = []
+        for t in range(T):
+            is_cond = t == 0
+            feat_t = feats[t]
+            pix = self._prepare_memory_conditioned_features(t, is_cond, feat_t, pos, T, output_dict, O)
+            prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
+            low, high, ious, ptr, score = self._forward_sam_heads(pix, prompt, (s0[t:t + 1], s1[t:t + 1]), O)
+            mfeat, mpos = self._encode_new_memory(feat_t, high, score, O)
+            entry = {"maskmem_features": mfeat, "maskmem_pos_enc": mpos, "obj_ptr": ptr}
+            if is_cond:
+                output_dict["cond_frame_outputs"][t] = entry
+            else:
+                nc = output_dict["non_cond_frame_outputs"]
+                nc[t] = entry
+                while len(nc) > max(self.num_maskmem - 1, 0):
+                    del nc[min(nc)]
+            pin = backbone_out["point_inputs_per_frame"].get(t)
+            low4 = low.view(O, 1, 4 * h, 4 * w)
+            high4 = high.view(O, 1, self.image_size, self.image_size)
+            frames.append({
+                "point_inputs": pin, "mask_inputs": None,
+                "pred_masks": low4, "pred_masks_high_res": high4,
+                "multistep_pred_masks": low4, "multistep_pred_masks_high_res": high4,
+                "multistep_pred_multimasks": [low4], "multistep_pred_multimasks_high_res": [high4],
+                "multistep_pred_ious": [ious], "multistep_point_inputs": [pin],
+                "multistep_object_score_logits": [score],
+            })
+        if return_dict:
+            return output_dict
+        return frames
