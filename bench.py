@@ -1,0 +1,196 @@
+"""Headline benchmark: training clip-frames/s of the SAM2 video fine-tuning step
+(BASELINE.json metric) on synthetic 512^2 8-frame clips, Hiera-B+, 13 objects,
+bf16 compute, all five modules trainable (the north_star "Hiera fwd+bwd").
+
+One step = SAM2LightningModule.training_step on one clip per rank (forward over
+8 frames, category merge, focal/Dice/IoU loss) + backward + RCCL all-reduce of
+the flat gradient arena (N > 1) + grad-norm clip + AdamW.  Inputs are resident
+in HBM before the timed region.  Prints ONE JSON line on rank 0.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sam2-video-training_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+ALL = ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder", "prompt_encoder"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", default="base_plus")
+    ap.add_argument("--image-size", type=int, default=512)
+    ap.add_argument("--frames", type=int, default=8)
+    ap.add_argument("--objects", type=int, default=13)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--trainable", default="all", choices=["all", "mem"])
+    ap.add_argument("--dropout", type=float, default=None, help="override dropout p (default: config, 0.1)")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
+    ap.add_argument("--cpu-frames", type=int, default=4, help="frames of the CPU baseline sample clip")
+    ap.add_argument("--no-prof", action="store_true")
+    return ap.parse_args()
+
+
+def attention_roofline(records):
+    """records: (ms, [BH, Lq, Lk, D, esize]) of every attention-forward launch in the timed region.
+    Dominant kernel = the memory-attention cross attention (head_dim 256, Lk > Lq)."""
+    sel = [(ms, m) for ms, m in records if m[3] == 256 and m[2] > m[1]]
+    if not sel:
+        return None
+    flops = sum(4.0 * m[0] * m[1] * m[2] * m[3] for _, m in sel)
+    ms = sum(t for t, _ in sel)
+    n = len(sel)
+    achieved = flops / (ms * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
+            "kernel": "attn_fwd_kernel<bf16,256> (memory-attention cross-attention)",
+            "launches": n, "avg_launch_ms": round(ms / n, 4),
+            "flops_per_launch_avg": flops / n}
+
+
+def cpu_baseline(args):
+    """CPU oracle (oracle/sam2_oracle.py, fp32 PyTorch-CPU restatement of the reference step)
+    on a bounded sample: one clip of the same shape with `cpu_frames` frames, fwd+loss+bwd."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import sam2_oracle as O
+    from sam2_video.data.synthetic import make_clip
+    from sam2_video.model.configs import model_config
+    from sam2_video.utils.init import synth_tensor
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    cfg = model_config(args.size, args.image_size)
+    trainable = ALL if args.trainable == "all" else ["memory_attention", "memory_encoder"]
+    P = O.make_params(O.param_shapes(cfg), O.trainable_prefixes(trainable), synth_tensor, seed=0)
+    clip = make_clip(10_000, args.cpu_frames, args.image_size, args.objects, args.objects)
+    model = O.OracleSAM2(cfg, P, dropout=0.0)
+    t0 = time.time()
+    stages, merged, aux = model.forward(clip["images"], clip["masks"])
+    losses = O.multistep_loss(merged, clip["masks"])
+    losses["total_loss"].backward()
+    dt = time.time() - t0
+    return {"value": round(args.cpu_frames / dt, 4), "unit": "clip-frames/s", "cores": threads, "kind": "port",
+            "sample": f"1 clip x {args.cpu_frames} frames, {args.size} {args.image_size}^2, {args.objects} objects, "
+                      f"fp32 fwd+loss+bwd (oracle), {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    from sam2_video.data.synthetic import make_clip, sam2_collate_fn
+    from sam2_video.kernels import _lib
+    from sam2_video.kernels import functional as FN
+    from sam2_video.model.sam2model import SAM2Model
+    from sam2_video.training.ddp import init_from_env
+    from sam2_video.training.trainer import SAM2LightningModule, StepRunner
+
+    rank, world, local = init_from_env("nccl")
+    if world == 1:
+        torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    FN.set_seed(1234 + rank)
+    trainable = ALL if args.trainable == "all" else ["memory_attention", "memory_encoder"]
+    model = SAM2Model(None, f"{args.size}@{args.image_size}", trainable_modules=trainable, compute_dtype=args.dtype)
+    if args.dropout is not None:
+        model.set_dropout(args.dropout)
+    loss_cfg = {"type": "multi_step", "gt_stride": 1, "multistep_logit_temperature": 1.0,
+                "weight_dict": {"loss_mask": 20, "loss_dice": 1, "loss_iou": 1, "loss_class": 0},
+                "supervise_all_iou": True, "iou_use_l1_loss": True, "pred_obj_scores": False,
+                "focal_gamma_obj_score": 0.0, "focal_alpha_obj_score": -1.0}
+    opt_cfg = {"type": "AdamW", "lr": 4e-6, "weight_decay": 0.01, "betas": [0.9, 0.999], "warmup_factor": 0.15}
+    module = SAM2LightningModule(model, loss_cfg, opt_cfg, {"enabled": True, "num_cycles": 0.5})
+    module.setup("fit", device)
+    total = args.warmup + args.steps
+    runner = StepRunner(module, total_steps=total, distributed=world > 1)
+
+    # synthetic clips, resident in HBM before timing (clip index = rank + k * world)
+    batches = []
+    for k in range(total):
+        clip = make_clip(rank + k * world, args.frames, args.image_size, args.objects, args.objects)
+        batches.append(sam2_collate_fn([clip]).to(device))
+    torch.cuda.synchronize()
+
+    for k in range(args.warmup):
+        runner(batches[k])
+    torch.cuda.synchronize()
+    if not args.no_prof:
+        _lib.call("s2h_prof_enable", 8192)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.warmup, total):
+        runner(batches[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    roof = None
+    if not args.no_prof:
+        import ctypes
+        n = _lib.lib().s2h_prof_count()
+        ms = (ctypes.c_float * max(n, 1))()
+        meta = (ctypes.c_int64 * (5 * max(n, 1)))()
+        n = _lib.lib().s2h_prof_read(n, ctypes.cast(ms, ctypes.c_void_p), ctypes.cast(meta, ctypes.c_void_p))
+        recs = [(ms[i], [meta[5 * i + j] for j in range(5)]) for i in range(n)]
+        _lib.call("s2h_prof_enable", 0)
+        roof = attention_roofline(recs)
+
+    frames = args.frames * args.steps * world
+    value = frames / elapsed
+    loss_val = float(module.logged["train/total_loss"])
+    result = {
+        "metric": "training clip-frames/sec (512^2 8-frame, Hiera-B+)",
+        "value": round(value, 3),
+        "unit": "clip-frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (N(0,1) images, drifting disc masks; deterministic synthetic weights, no checkpoint)",
+        "config": {"workload": f"SAM2 video fine-tuning step, sam2.1_hiera_{args.size}, {args.image_size}^2, "
+                               f"{args.frames} frames, {args.objects} objects, trainable={args.trainable}",
+                   "global_batch": world, "clips_per_rank": 1, "frames": args.frames,
+                   "image_size": args.image_size, "objects": args.objects, "parallelism": f"dp{world}"},
+        "roofline": roof,
+        "cpu_baseline": None,
+        "final_loss": round(loss_val, 5),
+    }
+    if rank == 0 and world == 1 and args.cpu_baseline:
+        try:
+            result["cpu_baseline"] = cpu_baseline(args)
+        except Exception as e:  # the baseline is reported, never required
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

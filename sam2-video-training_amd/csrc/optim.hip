@@ -18,7 +18,10 @@ __global__ __launch_bounds__(256) void sumsq_kernel(int64_t n, const float* x, f
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 // out[0] = sqrt(sum partial); out[1] = clip coefficient min(1, max_norm / (norm + 1e-6)) (1 if max_norm <= 0)
-__global__ __launch_bounds__(256) void norm_finalize_kernel(int nb, const float* partial, float max_norm, float* out) {
+// grad_scale: the stored gradient is scaled by this factor before use (1/world after a
+// SUM all-reduce); out[1] = grad_scale * clip coefficient, the factor AdamW applies.
+__global__ __launch_bounds__(256) void norm_finalize_kernel(int nb, const float* partial, float max_norm,
+                                                            float grad_scale, float* out) {
   float acc = 0.f;
   for (int i = threadIdx.x; i < nb; i += 256) acc += partial[i];
   __shared__ float red[4];
@@ -26,21 +29,22 @@ __global__ __launch_bounds__(256) void norm_finalize_kernel(int nb, const float*
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]);
+    const float norm = sqrtf(red[0] + red[1] + red[2] + red[3]) * grad_scale;
     out[0] = norm;
     float c = 1.f;
     if (max_norm > 0.f) {
       c = max_norm / (norm + 1e-6f);
       if (c > 1.f) c = 1.f;
     }
-    out[1] = c;
+    out[1] = c * grad_scale;
   }
 }
 #define NORM_BLOCKS 1024
-extern "C" int s2h_grad_norm(int64_t n, const float* g, float* partial_ws, float max_norm, float* out,
-                             hipStream_t st) {
+extern "C" int s2h_grad_norm(int64_t n, const float* g, float* partial_ws, float max_norm, float grad_scale,
+                             float* out, hipStream_t st) {
   hipLaunchKernelGGL(sumsq_kernel, dim3(NORM_BLOCKS), dim3(256), 0, st, n, g, partial_ws);
-  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, st, NORM_BLOCKS, partial_ws, max_norm, out);
+  hipLaunchKernelGGL(norm_finalize_kernel, dim3(1), dim3(256), 0, st, NORM_BLOCKS, partial_ws, max_norm, grad_scale,
+                     out);
   return (int)hipGetLastError();
 }
 

@@ -49,7 +49,12 @@ class BatchedVideoDatapoint:
             self.batch_size = [int(self.img_batch.shape[0])]
 
     def to(self, device, non_blocking=False):
-        return _map(self, lambda t: t.to(device, non_blocking=non_blocking))
+        out = _map(self, lambda t: t.to(device, non_blocking=non_blocking))
+        # keep the host copy of frame 0's masks: connected components + clicks are host-side
+        # work (masks.py:13-50, prompts.py) and can run without a device->host sync
+        hm = getattr(self, "host_masks0", None)
+        out.host_masks0 = hm if hm is not None else (self.masks[0] if not self.masks.is_cuda else None)
+        return out
 
     def pin_memory(self, device=None):
         return _map(self, lambda t: t.pin_memory())

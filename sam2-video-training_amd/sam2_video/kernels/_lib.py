@@ -62,7 +62,7 @@ SIGNATURES = {
     "s2h_group_wavg_fwd": [I, I, P, P, P, P, P, P],
     "s2h_group_wavg_bwd": [I, I, P, P, P, P, P, P, P, P, P],
     "s2h_sigmoid_grad_axpy": [I, L, P, L, P, P, L, P],
-    "s2h_grad_norm": [L, P, P, F, P, P],
+    "s2h_grad_norm": [L, P, P, F, F, P, P],
     "s2h_adamw": [L, P, P, P, P, P, F, F, F, F, F, I, P, P],
     "s2h_pos_embed": [I, I, I, I, I, P, P, P, P],
     "s2h_pos_embed_bwd": [I, I, I, I, I, P, P, P, P],

@@ -39,8 +39,16 @@ def _bicubic_matrix_np(n_in: int, n_out: int):
     return M
 
 
+_DEV_CACHE = {}
+
+
 def bicubic_matrix(n_in, n_out, device):
-    return torch.from_numpy(_bicubic_matrix_np(n_in, n_out)).float().to(device)
+    key = (n_in, n_out, str(device))
+    t = _DEV_CACHE.get(key)
+    if t is None:
+        t = torch.from_numpy(_bicubic_matrix_np(n_in, n_out)).float().to(device)
+        _DEV_CACHE[key] = t
+    return t
 
 
 class _PosEmbed(torch.autograd.Function):

@@ -413,8 +413,9 @@ def sigmoid_grad_axpy(x, coef, dx):
 
 
 # ------------------------------------------------------------- optimizer
-def grad_norm(g, max_norm, ws, out):
-    call("s2h_grad_norm", g.numel(), ptr(g), ptr(ws), float(max_norm), ptr(out), stream())
+def grad_norm(g, max_norm, ws, out, grad_scale=1.0):
+    """out[0] = ||grad_scale*g||, out[1] = grad_scale * clip coefficient (device scalars)"""
+    call("s2h_grad_norm", g.numel(), ptr(g), ptr(ws), float(max_norm), float(grad_scale), ptr(out), stream())
     return out
 
 

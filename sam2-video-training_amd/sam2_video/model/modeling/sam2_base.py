@@ -158,9 +158,15 @@ class SAM2Base(nn.Module):
     def _obj_pos_table(self, pos_list, max_ptr, dtype, device):
         """temporal encoding of object pointers (sam2_base.py:655-672): sine of the signed frame
         distance / (max_ptr - 1), projected to mem_dim, repeated for the C/mem_dim pointer tokens"""
-        t_diff_max = max_ptr - 1
-        pe = get_1d_sine_pe(torch.tensor(pos_list, dtype=torch.float32) / t_diff_max, dim=self.hidden_dim)
-        pe = pe.to(device=device, dtype=dtype)
+        key = (tuple(pos_list), max_ptr, dtype, str(device))
+        pe = self._tpos_cache.get(key) if hasattr(self, "_tpos_cache") else None
+        if pe is None:
+            t_diff_max = max_ptr - 1
+            pe = get_1d_sine_pe(torch.tensor(pos_list, dtype=torch.float32) / t_diff_max, dim=self.hidden_dim)
+            pe = pe.to(device=device, dtype=dtype)
+            if not hasattr(self, "_tpos_cache"):
+                self._tpos_cache = {}
+            self._tpos_cache[key] = pe
         op = self.obj_ptr_tpos_proj(pe)  # [n_ptr, mem_dim]
         return op.repeat_interleave(self.hidden_dim // self.mem_dim, dim=0)
 

@@ -178,8 +178,16 @@ class SAM2Model(SAM2Base):
 
     def prepare_prompt_inputs(self, backbone_out, input, start_frame_idx=0):
         """sam2model.py:181-236 -- frame-0 category masks -> objects -> clicks (host side)"""
-        masks0 = input.masks[start_frame_idx].unsqueeze(1)
+        hm = getattr(input, "host_masks0", None) if start_frame_idx == 0 else None
+        masks0 = (hm if hm is not None else input.masks[start_frame_idx]).unsqueeze(1)
+        # host-side work (runs while the GPU executes the already-queued image encoder)
         obj_masks, obj_to_cat, num_categories = utils.cat_to_obj_mask(masks0)
+        if self.prompt_type == "box":
+            points, labels = utils.generate_box_prompt(obj_masks)
+        else:
+            points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
+                                                         num_neg_points=self.num_neg_points,
+                                                         include_center=self.include_center)
         backbone_out["num_frames"] = input.num_frames
         backbone_out["obj_to_cat"] = obj_to_cat
         backbone_out["num_categories"] = num_categories
@@ -194,8 +202,11 @@ class SAM2Model(SAM2Base):
         pe0, lab0 = self.sam_prompt_encoder.host_points(points, labels, pad=True)
         pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
                                                         pad=True)
-        backbone_out["prompt_cond"] = (pe0.to(dev, non_blocking=True), lab0.to(dev, non_blocking=True))
-        backbone_out["prompt_pad"] = (pe1.to(dev, non_blocking=True), lab1.to(dev, non_blocking=True))
+        # pinned staging so the uploads are asynchronous w.r.t. the queued GPU work
+        backbone_out["prompt_cond"] = (pe0.pin_memory().to(dev, non_blocking=True),
+                                       lab0.pin_memory().to(dev, non_blocking=True))
+        backbone_out["prompt_pad"] = (pe1.pin_memory().to(dev, non_blocking=True),
+                                      lab1.pin_memory().to(dev, non_blocking=True))
         backbone_out["point_inputs_per_frame"] = {start_frame_idx: {"point_coords": points, "point_labels": labels}}
         backbone_out["mask_inputs_per_frame"] = {}
         return backbone_out

@@ -1,0 +1,56 @@
+"""Data-parallel gradient exchange over the flat gradient arena.
+
+Replaces Lightning `strategy=ddp` (README.md:155 of the reference; DDP wraps the
+module and all-reduces 25 MB fp32 buckets during backward).  Here every rank
+owns one clip per step (B == 1, dataset.py:358) and the gradients of all
+trainable parameters sit in ONE contiguous fp32 buffer, so the exchange is a
+handful of large RCCL all-reduces (SUM) over xGMI; the 1/world average is folded
+into the optimizer kernels (grad_scale) instead of an extra pass.
+
+Parameters that never receive a gradient are not in the buffer (the reference's
+DDP with find_unused_parameters=False would fail on them), so the
+bucket set is static.  Buckets: large (default 64 MiB) -- xGMI ring all-reduce is
+per-link bandwidth bound, fewer larger messages amortise the per-collective cost.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class ArenaGradReducer:
+    def __init__(self, grad: torch.Tensor, group=None, bucket_bytes: int = 64 << 20):
+        self.grad = grad
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        n = grad.numel()
+        per = max(1, bucket_bytes // grad.element_size())
+        self.buckets = [grad[i:i + per] for i in range(0, n, per)]
+
+    @property
+    def grad_scale(self) -> float:
+        return 1.0 / self.world
+
+    def reduce(self, async_op: bool = False):
+        """SUM all-reduce of every bucket (returns work handles if async_op)."""
+        if self.world == 1:
+            return []
+        works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op) for b in self.buckets]
+        return works if async_op else []
+
+
+def init_from_env(backend: str = "nccl"):
+    """torch.distributed init from torchrun env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*); returns
+    (rank, world, local_rank).  No-op for a single process without the env."""
+    import os
+    if "RANK" not in os.environ or int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        return 0, 1, int(os.environ.get("LOCAL_RANK", "0"))
+    rank = int(os.environ["RANK"])
+    world = int(os.environ["WORLD_SIZE"])
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if backend == "nccl":
+        torch.cuda.set_device(local)
+    if not dist.is_initialized():
+        import datetime
+        dist.init_process_group(backend=backend, timeout=datetime.timedelta(minutes=10))
+    return rank, world, local

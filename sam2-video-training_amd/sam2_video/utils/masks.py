@@ -46,6 +46,9 @@ def cat_to_obj_mask(cat_frame_masks: torch.Tensor) -> Tuple[torch.Tensor, List[i
     return torch.stack(objs).unsqueeze(1), obj_to_cat, N
 
 
+_GROUP_CACHE = {}
+
+
 class CategoryGroups:
     """device index lists of the object -> category grouping for the merge kernels"""
 
@@ -72,7 +75,10 @@ def merge_object_results_to_category(previous_stages_out: List[Dict[str, Any]], 
     if not previous_stages_out:
         return []
     dev = previous_stages_out[0]["pred_masks_high_res"].device
-    groups = CategoryGroups(obj_to_cat, num_categories, dev)
+    key = (tuple(obj_to_cat), num_categories, str(dev))
+    groups = _GROUP_CACHE.get(key)
+    if groups is None:
+        groups = _GROUP_CACHE[key] = CategoryGroups(obj_to_cat, num_categories, dev)
     merged_all = []
     for fo in previous_stages_out:
         hr = fo["pred_masks_high_res"]
