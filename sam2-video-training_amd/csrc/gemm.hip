@@ -8,7 +8,7 @@
 // without transposed copies: each operand is either K-contiguous ("KC") or
 // M/N-contiguous, selected at compile time.  Tiles are staged through LDS in a
 // K-contiguous [row][k] image so both MFMA operands read 16-B fragments.
-#include "common.h"
+#include "gemm16.h"
 
 struct GemmArgs {
   int M, N, K;
@@ -212,6 +212,17 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
     a.K = 0;
   }
   if (dt_ab == S2H_F32) return launch_gemm<float, float>(a, batch, stream);
-  if (dt_c == S2H_BF16) return launch_gemm<bf16, bf16>(a, batch, stream);
-  return launch_gemm<bf16, float>(a, batch, stream);
+  GemmArgs16 b;
+  b.M = a.M; b.N = a.N; b.K = a.K;
+  b.A = (const bf16*)A; b.lda_m = lda_m; b.lda_k = lda_k; b.sA = sA;
+  b.B = (const bf16*)B; b.ldb_k = ldb_k; b.ldb_n = ldb_n; b.sB = sB;
+  b.C = C; b.ldc = ldc; b.sC = sC;
+  b.bias = a.bias; b.bias_mode = a.bias_mode;
+  b.R = R; b.ldr = ldr; b.sR = sR;
+  b.X = X; b.ldx = ldx; b.sX = sX; b.aux_mode = a.aux_mode;
+  b.cscale = cscale; b.drop_p = drop_p; b.seed = seed;
+  b.alpha = alpha; b.beta = beta; b.act = act;
+  b.vecA = a.vecA; b.vecB = a.vecB;
+  b.out_f32 = dt_c == S2H_F32;
+  return s2h_gemm_bf16(b, batch, stream);
 }

@@ -1,0 +1,22 @@
+// Argument block of the bf16 MFMA GEMM (gemm_bf16.hip), shared with the C-ABI entry in gemm.hip.
+#pragma once
+#include "common.h"
+
+struct GemmArgs16 {
+  int M, N, K;
+  const bf16* A; int64_t lda_m, lda_k, sA;
+  const bf16* B; int64_t ldb_k, ldb_n, sB;
+  void* C; int64_t ldc, sC;
+  const float* bias; int bias_mode;
+  const void* R; int64_t ldr, sR;
+  void* X; int64_t ldx, sX;
+  int aux_mode;
+  const float* cscale;
+  float drop_p; uint64_t seed;
+  float alpha, beta; int act;
+  int vecA, vecB;
+  int splits, kchunk;  // split-K: blockIdx.z = batch * splits + split
+  int out_f32;
+};
+
+int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);

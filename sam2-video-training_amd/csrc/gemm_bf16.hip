@@ -1,0 +1,234 @@
+// bf16 MFMA GEMM for the compute path (fwd / dgrad / wgrad of every projection).
+//
+// Each operand is staged into LDS in the layout its source already has, with
+// 16-B vector loads and 16-B LDS stores (no transposing scalar writes):
+//   K-contiguous source  -> LDS [row][k]  -> fragments by ds_read_b128
+//   row-contiguous source-> LDS [k][row]  -> fragments by ds_read_b64_tr_b16
+//                                            (CDNA4 transposing LDS read, two per fragment)
+// so Y = X W^T (both K-contiguous), dX = dY W (W row-contiguous) and the weight
+// gradient dW = dY^T X (both row-contiguous over the reduction) all run at full
+// LDS bandwidth.  Rows are padded by 16 B (conflict-free ds_read_b128 and
+// transposed reads).  K is split over workgroups (fp32 atomic accumulate into
+// the output) when the output tile count cannot fill the 256 CUs -- the weight
+// gradients reduce over 10^4-10^5 rows into a few hundred KB.
+#include "gemm16.h"
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ bf16x8 tr_frag(const bf16* lds_row0, int ld, int lane) {
+  // rows (8g + q) and (8g + 4 + q) of a [k][row] image, columns 4p..4p+3 of the 16-wide block
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16* a0 = lds_row0 + (8 * g + q) * ld + 4 * p;
+  const bf16* a1 = a0 + 4 * ld;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
+  v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  v8i16 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+
+template <int ROWS, int BK, bool KC>
+struct Stage16 {
+  // ROWS x BK tile; KC: source (row, k) with k contiguous -> LDS [ROWS][BK+8]
+  //                !KC: source (row, k) with row contiguous -> LDS [BK][ROWS+8]
+  static constexpr int NV = ROWS * BK / 8 / 256;
+  static constexpr int LDS_LD = KC ? BK + 8 : ROWS + 8;
+  static constexpr int LDS_ELEMS = KC ? ROWS * (BK + 8) : BK * (ROWS + 8);
+  uint4 r[NV];
+
+  __device__ __forceinline__ void load(const bf16* base, int64_t ld_row, int64_t ld_k, int row0, int k0, int nrows,
+                                       int kend, bool vec_ok, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * 256;
+      int row, k;
+      if (KC) { row = v / (BK / 8); k = (v % (BK / 8)) * 8; }
+      else    { k = v / (ROWS / 8); row = (v % (ROWS / 8)) * 8; }
+      const int gr = row0 + row, gk = k0 + k;
+      const bool full = KC ? (gr < nrows && gk + 8 <= kend) : (gk < kend && gr + 8 <= nrows);
+      if (full && vec_ok) {
+        r[i] = *(const uint4*)(base + (int64_t)gr * ld_row + (int64_t)gk * ld_k);
+      } else {
+        bf16 t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int rr = KC ? gr : gr + j, kk = KC ? gk + j : gk;
+          t[j] = (rr < nrows && kk < kend) ? base[(int64_t)rr * ld_row + (int64_t)kk * ld_k] : (bf16)0.f;
+        }
+        r[i] = *(const uint4*)t;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(bf16* lds, int tid) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int v = tid + i * 256;
+      if (KC) {
+        const int row = v / (BK / 8), k = (v % (BK / 8)) * 8;
+        *(uint4*)(lds + row * LDS_LD + k) = r[i];
+      } else {
+        const int k = v / (ROWS / 8), row = (v % (ROWS / 8)) * 8;
+        *(uint4*)(lds + k * LDS_LD + row) = r[i];
+      }
+    }
+  }
+  // MFMA operand fragment for the 16 rows starting at `row0`, k-step offset ks (32 wide)
+  __device__ __forceinline__ bf16x8 frag(const bf16* lds, int row0, int ks, int lane) const {
+    if (KC) return *(const bf16x8*)(lds + (row0 + (lane & 15)) * LDS_LD + ks + (lane >> 4) * 8);
+    return tr_frag(lds + ks * LDS_LD + row0, LDS_LD, lane);
+  }
+};
+
+template <int BM, int BN, bool AKC, bool BKC>
+__global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
+  constexpr int BK = 64;
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  using SA = Stage16<BM, BK, AKC>;
+  using SB = Stage16<BN, BK, BKC>;
+  __shared__ __attribute__((aligned(16))) bf16 smem[SA::LDS_ELEMS + SB::LDS_ELEMS];
+  bf16* As = smem;
+  bf16* Bs = smem + SA::LDS_ELEMS;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  const int bz = blockIdx.z / p.splits, split = blockIdx.z % p.splits;
+  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  const bf16* A = p.A + (int64_t)bz * p.sA;
+  const bf16* B = p.B + (int64_t)bz * p.sB;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+
+  SA la;
+  SB lb;
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  if (nk > 0) {
+    la.load(A, p.lda_m, p.lda_k, m0, kbeg, p.M, kend, p.vecA, tid);
+    lb.load(B, p.ldb_n, p.ldb_k, n0, kbeg, p.N, kend, p.vecB, tid);
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    la.store(As, tid);
+    lb.store(Bs, tid);
+    __syncthreads();
+    if (kt + 1 < nk) {
+      la.load(A, p.lda_m, p.lda_k, m0, kbeg + (kt + 1) * BK, p.M, kend, p.vecA, tid);
+      lb.load(B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + 1) * BK, p.N, kend, p.vecB, tid);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK; ks += 32) {
+      bf16x8 a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = la.frag(As, wm * WM + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = lb.frag(Bs, wn * WN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  if (p.splits > 1) {  // split-K: fp32 atomic accumulate (output pre-scaled by beta on the host side)
+    float* C = (float*)p.C + (int64_t)bz * p.sC;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int col = n0 + wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * acc[i][j][r]);
+        }
+      }
+    return;
+  }
+  const bf16* R = p.R ? (const bf16*)p.R + (int64_t)bz * p.sR : nullptr;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = n0 + wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        if (row < p.M && col < p.N) {
+          float v = p.alpha * acc[i][j][r];
+          if (p.bias_mode == 1) v += p.bias[col];
+          else if (p.bias_mode == 2) v += p.bias[row];
+          const int64_t xo = (int64_t)bz * p.sX + (int64_t)row * p.ldx + col;
+          if (p.aux_mode == 1) ((bf16*)p.X)[xo] = (bf16)v;
+          if (p.aux_mode == 2) v *= act_grad((float)((const bf16*)p.X)[xo], p.act);
+          else v = apply_act(v, p.act);
+          if (p.cscale) v *= p.cscale[col];
+          if (p.drop_p > 0.f) {
+            const uint64_t idx = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
+            v = s2h_keep(p.seed, idx, (uint32_t)(p.drop_p * 4294967296.0)) ? v / (1.f - p.drop_p) : 0.f;
+          }
+          if (R) v += (float)R[(int64_t)row * p.ldr + col];
+          const int64_t off = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col;
+          if (p.out_f32) {
+            float* C = (float*)p.C;
+            if (p.beta != 0.f) v += p.beta * C[off];
+            C[off] = v;
+          } else {
+            bf16* C = (bf16*)p.C;
+            if (p.beta != 0.f) v += p.beta * (float)C[off];
+            C[off] = (bf16)v;
+          }
+        }
+      }
+    }
+}
+
+template <int BM, int BN>
+static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * batch;
+  a.splits = 1;
+  a.kchunk = a.K;
+  const bool plain = a.out_f32 && !a.bias && !a.R && !a.X && !a.cscale && a.drop_p == 0.f && a.act == 0 &&
+                     (a.beta == 1.f || a.beta == 0.f);
+  if (plain && tiles < 512 && a.K >= 1024) {
+    int s = (768 + tiles - 1) / tiles;
+    int maxs = a.K / 512;
+    if (s > maxs) s = maxs;
+    if (s > 64) s = 64;
+    if (s > 1) {
+      a.splits = s;
+      a.kchunk = ((a.K + s - 1) / s + 63) / 64 * 64;
+      a.splits = (a.K + a.kchunk - 1) / a.kchunk;
+      if (a.beta == 0.f) {
+        for (int b = 0; b < batch; ++b) {
+          if (a.ldc == a.N) {
+            (void)hipMemsetAsync((float*)a.C + (int64_t)b * a.sC, 0, (size_t)a.M * a.N * sizeof(float), st);
+          } else {
+            (void)hipMemset2DAsync((float*)a.C + (int64_t)b * a.sC, a.ldc * sizeof(float), 0,
+                                   a.N * sizeof(float), a.M, st);
+          }
+        }
+      }
+    }
+  }
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * a.splits);
+  const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
+  if (akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, true>), grid, dim3(256), 0, st, a);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, false>), grid, dim3(256), 0, st, a);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, false, true>), grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((gemm16_kernel<BM, BN, false, false>), grid, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
+  GemmArgs16 a = in;
+  const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch;
+  if (t128 >= 256 || (a.M >= 128 && a.N >= 128 && a.K >= 1024)) return launch16_tiles<128, 128>(a, batch, st);
+  return launch16_tiles<64, 64>(a, batch, st);
+}

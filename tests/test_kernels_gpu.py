@@ -54,6 +54,23 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     _close(y, ref + r.float(), tol)
 
 
+@pytest.mark.parametrize("rows,N,K", [(20000, 336, 112), (131072, 112, 336), (13312, 256, 256), (4099, 130, 77)])
+def test_wgrad_split_k(rows, N, K):
+    """Weight gradients reduce over 10^4-10^5 rows into few output tiles: the bf16 GEMM
+    splits the reduction over workgroups with fp32 atomics (accumulate semantics)."""
+    ops = _ops()
+    torch.manual_seed(1)
+    dy = torch.randn(rows, N, device=DEV).to(torch.bfloat16)
+    x = torch.randn(rows, K, device=DEV).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    dw = torch.full((N, K), 0.5, device=DEV)
+    ops.linear_wgrad(dy, x, dw)
+    _close(dw, ref + 0.5, 2e-3)
+    out = torch.full((1, N, K), 7.0, device=DEV)
+    ops.gemm(dy, x, out, M=N, N=K, K=rows, lda_m=1, lda_k=N, ldb_k=K, ldb_n=1, ldc=K, beta=0.0)
+    _close(out[0], ref, 2e-3)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
 def test_bmm_layouts(dtype, tol):
     ops = _ops()
