@@ -95,7 +95,7 @@ def main():
     from sam2_video.kernels import _lib
     from sam2_video.kernels import functional as FN
     from sam2_video.model.sam2model import SAM2Model
-    from sam2_video.training.ddp import init_from_env
+    from sam2_video.training.ddp import init_from_env, shard_clips
     from sam2_video.training.trainer import SAM2LightningModule, StepRunner
 
     rank, world, local = init_from_env("nccl")
@@ -119,8 +119,8 @@ def main():
 
     # synthetic clips, resident in HBM before timing (clip index = rank + k * world)
     batches = []
-    for k in range(total):
-        clip = make_clip(rank + k * world, args.frames, args.image_size, args.objects, args.objects)
+    for idx in shard_clips(total, rank, world):
+        clip = make_clip(idx, args.frames, args.image_size, args.objects, args.objects)
         batches.append(sam2_collate_fn([clip]).to(device))
     torch.cuda.synchronize()
 

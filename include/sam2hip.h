@@ -1,0 +1,240 @@
+/*
+ * sam2hip.h -- C ABI of libsam2hip.so, the MI355X (gfx950) compute path of the
+ * SAM2 video fine-tuning step (SAM2LightningModule.training_step,
+ * reference sam2_video/training/trainer.py:256-289).
+ *
+ * Every entry point takes raw device pointers, int64 element strides, a dtype
+ * tag, scalar parameters and the hipStream_t to launch on.  Nothing allocates
+ * (workspaces are passed in), nothing synchronises, and every call returns a
+ * hipError_t value (0 = success).  Element strides are in elements, not bytes.
+ * Tensors are owned by the caller (the Python host package uses PyTorch's
+ * caching allocator).  The library keeps no per-thread state; forward launches
+ * come from the Python thread, backward launches from the autograd worker.
+ *
+ * Each declaration names the reference operation it replaces (file:line in the
+ * reference repository, sam2_video/... paths; the modeling files are the
+ * vendored SAM2.1 sources under sam2_video/model/modeling/).
+ */
+#ifndef SAM2HIP_H
+#define SAM2HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Same definition as hip_runtime_api.h, so the two headers can be combined. */
+typedef struct ihipStream_t* hipStream_t;
+
+/* dtype tags (`dt` arguments) */
+enum { S2H_F32 = 0, S2H_BF16 = 1 };
+/* fused activations (`act` arguments) */
+enum { S2H_ACT_NONE = 0, S2H_ACT_RELU = 1, S2H_ACT_GELU = 2, S2H_ACT_SIGMOID = 3 };
+
+/* ---------------------------------------------------------------- library */
+/* ABI version (1). */
+int s2h_version(void);
+/* In-library launch profiler: `cap` > 0 pre-creates `cap` HIP event pairs and
+ * brackets every attention-forward launch on its own stream; 0 disables. */
+int s2h_prof_enable(int cap);
+int s2h_prof_reset(void);
+int s2h_prof_count(void);
+/* Copies up to `max` records: ms[i] (event elapsed time) and meta[5*i..] =
+ * (batch*heads, Lq, Lk, head_dim, element size).  Synchronises the events. */
+int s2h_prof_read(int max, float* ms, int64_t* meta);
+
+/* ---------------------------------------------------------------- GEMM
+ * C[b](m,n) = act(alpha * sum_k A[b](m,k) B[b](k,n) + bias) * cscale[n], dropout(p, seed),
+ *             + R[b](m,n) + beta * C[b](m,n)
+ * A addressed as A[m*lda_m + k*lda_k] (one of lda_m, lda_k must be 1), B as
+ * B[k*ldb_k + n*ldb_n] (one of ldb_k, ldb_n must be 1), batch strides sA/sB/sC.
+ * dt_ab: S2H_F32 (fp32 MFMA, parity mode; dt_c must be F32) or S2H_BF16 (bf16 MFMA,
+ * fp32 accumulate; dt_c BF16 or F32).  bias_mode 1 = per column, 2 = per row.
+ * aux_mode 1 stores the pre-activation into X; 2 multiplies by act'(X) (the
+ * activation gradient of the layer that produced X) instead of applying act.
+ * Replaces every nn.Linear / 1x1 nn.Conv2d / im2col conv / matmul on the path:
+ *   hieradet.py:56-81 (qkv, proj), :140 (dim-change proj), sam2_utils.py:112-139 (MLP),
+ *   transformer.py:230-243, 275-311 (q/k/v/out proj), memory_attention.py:58-99 (FFN),
+ *   image_encoder.py:79 (FPN lateral 1x1), mask_decoder.py:66-81 (ConvT 2x2 / conv_s0/s1),
+ *   utils.py:85 (PatchEmbed 7x7/4 conv), memory_encoder.py:43-156 (mask downsampler,
+ *   CXBlock pwconv, pix_feat_proj, out_proj), mask_decoder.py:168-245 (hypernetwork
+ *   product), hieradet.py:273-281 (bicubic pos-embed resize as two GEMMs),
+ *   and their autograd backward (dgrad / wgrad). */
+int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
+             const void* A, int64_t lda_m, int64_t lda_k, int64_t sA,
+             const void* B, int64_t ldb_k, int64_t ldb_n, int64_t sB,
+             void* C, int64_t ldc, int64_t sC,
+             const float* bias, int bias_mode,
+             const void* R, int64_t ldr, int64_t sR,
+             void* X, int64_t ldx, int64_t sX, int aux_mode,
+             const float* cscale, float drop_p, uint64_t seed,
+             float alpha, float beta, int act, hipStream_t stream);
+
+/* ---------------------------------------------------------------- attention
+ * Fused multi-head attention, tensors [B, L, H, D] addressed through
+ * (batch, head, row) strides with contiguous D; lse [B, H, Lq] fp32 (natural log).
+ * Optional attention-probability dropout p_drop with a counter-based hash keyed by
+ * `seed` (regenerated identically in the backward).  D in {32, 64, 96, 128, 256}
+ * for bf16, 32..256 (multiple of 4) for fp32.
+ * Replaces F.scaled_dot_product_attention at hieradet.py:70 (windowed / global
+ * Hiera attention), transformer.py:243 (two-way decoder attention) and
+ * transformer.py:306 (memory-attention RoPE self / cross attention). */
+int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
+                 const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                 const void* k, int64_t skb, int64_t skh, int64_t skl,
+                 const void* v, int64_t svb, int64_t svh, int64_t svl,
+                 void* o, int64_t sob, int64_t soh, int64_t sol,
+                 float* lse, float scale, float p_drop, uint64_t seed, hipStream_t st);
+/* Backward of s2h_attn_fwd; di_ws: fp32 workspace [B*H*Lq]. */
+int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
+                 const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                 const void* k, int64_t skb, int64_t skh, int64_t skl,
+                 const void* v, int64_t svb, int64_t svh, int64_t svl,
+                 const void* o, int64_t sob, int64_t soh, int64_t sol,
+                 const void* dout, int64_t sgb, int64_t sgh, int64_t sgl,
+                 void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
+                 void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
+                 void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
+                 const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, hipStream_t st);
+
+/* ---------------------------------------------------------------- normalisation
+ * Row LayerNorm over C (<= 1280) with an optional fused pre-add:
+ * xsum = x + badd (badd broadcast over rows when b_bcast), y = LN(xsum) * gamma + beta;
+ * saves per-row mean / rstd (fp32).  Replaces nn.LayerNorm (hieradet.py:134-166,
+ * memory_attention.py:43-45,115, transformer.py:63,137-149) and LayerNorm2d
+ * (sam2_utils.py:141-151, NHWC rows) and the residual adds feeding them. */
+int s2h_layernorm_fwd(int dt, int rows, int C, const void* x, int64_t ldx, const void* badd, int64_t ldb,
+                      int b_bcast, void* xsum, const float* gamma, const float* beta, float eps, void* y,
+                      int64_t ldy, float* mean, float* rstd, hipStream_t st);
+/* dx (=, or += when dx_accum), dgamma += , dbeta += (fp32). */
+int s2h_layernorm_bwd(int dt, int rows, int C, const void* x, int64_t ldx, const void* dy, int64_t lddy,
+                      const float* gamma, const float* mean, const float* rstd, void* dx, int64_t lddx,
+                      int dx_accum, float* dgamma, float* dbeta, hipStream_t st);
+
+/* ---------------------------------------------------------------- elementwise / layout
+ * out = alpha*a + beta*b (residual adds, sam2_base.py:680-684 no_mem_embed,
+ * memory_attention.py:140-141 curr + 0.1*pos). */
+int s2h_add(int dt, int64_t n, const void* a, const void* b, float alpha, float beta, void* out, hipStream_t st);
+/* out[o, i] = alpha*a[o, i] + beta*b[i % b_period] (bias / embedding broadcast:
+ * mask_decoder.py:201-209 dense prompt add, sam2_base.py:761-767 no_obj_embed_spatial). */
+int s2h_add_bcast(int dt, int64_t outer, int64_t inner, const void* a, float alpha, const void* b,
+                  int64_t b_period, float beta, void* out, hipStream_t st);
+/* y = act(scale*x + shift) (GELU / ReLU / sigmoid; sam2_base.py:742-747 mask_for_mem). */
+int s2h_act_fwd(int dt, int64_t n, const void* x, int act, float scale, float shift, void* y, hipStream_t st);
+/* dx (=, or += when accum) = dy * act'(x). */
+int s2h_act_bwd(int dt, int64_t n, const void* x, const void* dy, int act, void* dx, int accum, hipStream_t st);
+/* dtype conversion (fp32 <-> bf16; sam2_base.py:391-399 `.float()` of the logits). */
+int s2h_cast(int dt_in, int dt_out, int64_t n, const void* x, void* y, hipStream_t st);
+/* out = a + dropout(b) (b may be NULL: out = dropout(a)); nn.Dropout at
+ * memory_attention.py:40-48 and the post-attention / FFN dropouts. */
+int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out, hipStream_t st);
+/* Axial rotary embedding of the first `nrot` rows of each batch (cos/sin tables
+ * [period, D/2], row r uses entry r % period; inverse = 1 applies the transpose
+ * rotation for the backward).  Replaces apply_rotary_enc (position_encoding.py:212-239)
+ * with compute_axial_cis tables (:192-201) and the key-repeat at transformer.py:291-299. */
+int s2h_rope(int dt, int64_t nb, int nrot, int D, const void* x, int64_t sxb, int64_t sxl, void* y,
+             int64_t syb, int64_t syl, const float* cosv, const float* sinv, int period, int inverse,
+             hipStream_t st);
+/* 2x2/2 max pooling, NHWC with pixel stride ldx (do_pool, hieradet.py:25-36). */
+int s2h_maxpool2_fwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, void* y, hipStream_t st);
+int s2h_maxpool2_bwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, const void* dy,
+                     void* dx, int64_t lddx, hipStream_t st);
+/* window_partition (dir 0) / window_unpartition (dir 1) with zero padding
+ * (backbones/utils.py:16-60); accum adds into dst. */
+int s2h_window(int dt, int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum,
+               hipStream_t st);
+/* FPN top-down: out = lat + nearest_up2(prev) (image_encoder.py:102-134). */
+int s2h_up2_add(int dt, int B, int H, int W, int C, const void* lat, const void* prev, void* out, hipStream_t st);
+/* Backward of the nearest 2x upsample: dprev (+)= 2x2 sum of dout. */
+int s2h_pool2_sum(int dt, int B, int Ho, int Wo, int C, const void* dout, void* dprev, int accum, hipStream_t st);
+/* Bilinear resize, align_corners=False, fp32 [N, hi, wi] -> [N, ho, wo]
+ * (F.interpolate at sam2_base.py:393-399, low-res -> high-res mask logits). */
+int s2h_bilinear_fwd(int N, int hi, int wi, int ho, int wo, const float* x, float* y, hipStream_t st);
+int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const float* dy, float* dx, hipStream_t st);
+/* out[c] (=, or += when accum) = sum_r x[r, c] (bias gradients). */
+int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum, hipStream_t st);
+/* out[i] (=/+=) sum_o x[o, i] (gradient of a per-object broadcast of shared
+ * features: sam2model.py:307-311, mask_decoder.py:201,209 repeat_interleave). */
+int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* out, int accum, hipStream_t st);
+/* NHWC im2col in PyTorch weight order (c, ky, kx) for the strided convolutions
+ * (PatchEmbed utils.py:85; MaskDownSampler memory_encoder.py:43). */
+int s2h_im2col(int dt, int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
+               const void* x, void* col, hipStream_t st);
+/* Depthwise KxK conv, NHWC, fp32 weights [C, K, K] (CXBlock dwconv, memory_encoder.py:84). */
+int s2h_dwconv(int dt, int B, int H, int W, int C, int K, int pad, const void* x, const float* w,
+               const float* bias, void* y, hipStream_t st);
+/* ConvTranspose2d k=2 s=2 as GEMM + scatter (dir 0: out = scatter(Y) + bias (+ add));
+ * dir 1 gathers the output gradient into GEMM layout (mask_decoder.py:66-75). */
+int s2h_convt2(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+               void* out, int dir, hipStream_t st);
+/* y[r, :] = gate[r] > 0 ? x[r, :] : fill; dir 1 = backward (object-score gating to
+ * NO_OBJ_SCORE, sam2_base.py:380-389). */
+int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, float fill,
+                 void* y, int dir, hipStream_t st);
+/* y = (scale_x ? g*x : x) + (1-g)*vec for g = (gate > 0) (obj_ptr / no_obj_ptr mix,
+ * sam2_base.py:413-424; no_obj_embed_spatial sam2_base.py:761-767). */
+int s2h_gate_mix(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, const void* vec,
+                 int vec_period, int scale_x, void* y, hipStream_t st);
+/* Hiera positional embedding: out[h, w, c] = Y[c, h, w] + win[c, h % ws, w % ws]
+ * (bicubic-resized background + tiled window embedding, hieradet.py:273-281). */
+int s2h_pos_embed(int dt, int C, int h, int w, int ws, const float* Y, const float* win, void* out,
+                  hipStream_t st);
+int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void* dout, float* dY, float* dwin,
+                      hipStream_t st);
+/* Point prompt embedding: out[r] = pe[r] + table[label[r] + 1] (label -1 = pad:
+ * table row 0 = not_a_point_embed, pe zeroed), prompt_encoder.py:79-104. */
+int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
+                    hipStream_t st);
+int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, const void* dout, float* dtable, hipStream_t st);
+
+/* ---------------------------------------------------------------- loss + category merge
+ * Per-row mask statistics of logits x/T vs uint8 targets: stats[6*r..] = (focal sum,
+ * sigmoid sum, target sum, sigmoid.target sum, (x>0) & tgt count, (x>0) | tgt count).
+ * sigmoid_focal_loss / dice_loss / iou_loss inputs, losses.py:20-76, 111-248. */
+int s2h_mask_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                   float inv_temp, float* stats, hipStream_t st);
+/* losses[4] = (loss_mask, loss_dice, loss_iou, weighted total) with per-frame
+ * normalisation by valid categories (valid = NULL: target sum > 0); coef[3*N] are the
+ * gradient coefficients consumed by s2h_mask_loss_bwd. */
+int s2h_mask_loss_finalize(int N, int64_t P, const float* stats, const float* pred_iou, const int* valid,
+                           float w_mask, float w_dice, float w_iou, float gscale, float* losses,
+                           float* coef, hipStream_t st);
+/* dx = d(total)/d(logits) * gtot[3] (device scalar upstream gradient); dious likewise. */
+int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                      float inv_temp, const float* coef, float* dx, int64_t lddx, const float* gtot,
+                      float* dious, hipStream_t st);
+/* Pixelwise max of each category's object masks (CSR cat_off / cat_obj), argmax
+ * saved for the backward (merge_object_results_to_category, masks.py:98-115). */
+int s2h_group_max_fwd(int Ncat, int64_t P, const int* cat_off, const int* cat_obj, const float* x,
+                      int64_t ldx, float* y, int64_t ldy, int* arg, hipStream_t st);
+int s2h_group_max_bwd(int O, int64_t P, const int* obj_cat, const int* arg, const float* dy, int64_t lddy,
+                      float* dx, int64_t lddx, hipStream_t st);
+/* Sigmoid-mass weighted mean of per-object scalars (IoU / object scores) per
+ * category, weights = stats (masks.py:98-140); bwd also yields d(weights). */
+int s2h_group_wavg_fwd(int Ncat, int K, const int* cat_off, const int* cat_obj, const float* stats,
+                       const float* x, float* y, hipStream_t st);
+int s2h_group_wavg_bwd(int O, int K, const int* obj_cat, const int* cat_off, const float* stats,
+                       const float* x, const float* y, const float* dy, float* dx, float* dw, hipStream_t st);
+/* dx[r, :] += coef[r] * sigmoid'(x[r, :]) (gradient of the sigmoid-mass weights). */
+int s2h_sigmoid_grad_axpy(int R, int64_t P, const float* x, int64_t ldx, const float* coef, float* dx,
+                          int64_t lddx, hipStream_t st);
+
+/* ---------------------------------------------------------------- optimizer
+ * Global L2 norm of the flat fp32 gradient arena (times grad_scale) and the clip
+ * factor: out[0] = norm, out[1] = min(1, max_norm / (norm + 1e-6)) * grad_scale.
+ * partial_ws: fp32 workspace of >= 1024 floats.  Replaces gradient_clip_val
+ * (torch clip_grad_norm_, configured at trainer / best.yaml:106). */
+int s2h_grad_norm(int64_t n, const float* g, float* partial_ws, float max_norm, float grad_scale,
+                  float* out, hipStream_t st);
+/* Fused AdamW over the flat arena (torch.optim.AdamW semantics, trainer.py:125):
+ * g' = g*clip[1]; p *= 1 - lr*wd; m = b1 m + (1-b1) g'; v = b2 v + (1-b2) g'^2;
+ * p -= lr/(1-b1^step) * m / (sqrt(v)/sqrt(1-b2^step) + eps); optional bf16 shadow copy. */
+int s2h_adamw(int64_t n, float* p, const float* g, float* m, float* v, const float* clip, float lr,
+              float beta1, float beta2, float eps, float wd, int step, void* bf16_shadow, hipStream_t st);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SAM2HIP_H */

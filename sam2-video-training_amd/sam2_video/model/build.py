@@ -69,6 +69,20 @@ def load_model_config(config_path: str, image_size=None) -> dict:
     if not os.path.isabs(path) and not os.path.exists(path):
         here = os.path.join(os.path.dirname(__file__), "..", "configs", path)
         path = here if os.path.exists(here) else path
+    if not os.path.exists(path):
+        # upstream config names as the reference YAMLs spell them (best.yaml:32
+        # `config_path: sam2/sam2.1_hiera_t.yaml`): resolve to the built-in table
+        stem = os.path.basename(name)
+        stem = stem[:-5] if stem.endswith(".yaml") else stem
+        for prefix in ("sam2.1_", "sam2_"):
+            if stem.startswith(prefix):
+                stem = stem[len(prefix):]
+        key = configs.ALIASES.get(stem, stem)
+        if key in configs.TRUNKS:
+            # the reference's own configs/sam2/sam2.1_hiera_t.yaml sets image_size 384 (:88);
+            # upstream SAM2.1 configs use 1024
+            default = 384 if (name.startswith("sam2/") and key == "tiny") else 1024
+            return configs.model_config(key, int(image_size or sz or default))
     with open(path) as f:
         y = yaml.safe_load(f)
     cfg = y.get("model", y)

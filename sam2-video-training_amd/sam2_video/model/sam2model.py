@@ -191,12 +191,6 @@ class SAM2Model(SAM2Base):
         backbone_out["num_frames"] = input.num_frames
         backbone_out["obj_to_cat"] = obj_to_cat
         backbone_out["num_categories"] = num_categories
-        if self.prompt_type == "box":
-            points, labels = utils.generate_box_prompt(obj_masks)
-        else:
-            points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
-                                                         num_neg_points=self.num_neg_points,
-                                                         include_center=self.include_center)
         O = len(obj_to_cat)
         dev = self.arena.device
         pe0, lab0 = self.sam_prompt_encoder.host_points(points, labels, pad=True)

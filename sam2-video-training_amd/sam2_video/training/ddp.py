@@ -39,6 +39,12 @@ class ArenaGradReducer:
         return works if async_op else []
 
 
+def shard_clips(num_steps: int, rank: int, world: int, offset: int = 0):
+    """Clip indices rank r processes at steps 0..num_steps-1: offset + r + k*world
+    (DistributedSampler order without shuffling; every clip goes to exactly one rank)."""
+    return [offset + rank + k * world for k in range(num_steps)]
+
+
 def init_from_env(backend: str = "nccl"):
     """torch.distributed init from torchrun env (RANK, WORLD_SIZE, LOCAL_RANK, MASTER_*); returns
     (rank, world, local_rank).  No-op for a single process without the env."""

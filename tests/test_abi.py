@@ -1,0 +1,90 @@
+"""The drop-in boundary: include/sam2hip.h <-> libsam2hip.so <-> the ctypes binding.
+
+CPU-only checks (no kernel launches): the header compiles as C and C++, the
+library loads, it exports exactly the functions the header declares, and the
+Python binding's argument lists agree with the header prototypes.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "sam2hip.h")
+CSRC = os.path.join(ROOT, "sam2-video-training_amd", "csrc")
+
+_CTYPE = {"int": "I", "int64_t": "L", "float": "F", "uint64_t": "U"}
+
+
+def _prototypes():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\bint\s+(s2h_\w+)\s*\(([^)]*)\)\s*;", text):
+        params = [p.strip() for p in m.group(2).split(",")]
+        if params == ["void"]:
+            params = []
+        kinds = []
+        for p in params:
+            if "*" in p or p.startswith("hipStream_t"):
+                kinds.append("P")
+            else:
+                kinds.append(_CTYPE[p.split()[-2] if len(p.split()) > 1 else p])
+        protos[m.group(1)] = kinds
+    return protos
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from sam2_video.kernels import _lib
+    if not os.path.exists(_lib.LIB_PATH):
+        subprocess.run(["make", "-C", CSRC, f"-j{min(8, os.cpu_count() or 1)}"], check=True,
+                       stdout=subprocess.DEVNULL)
+    return _lib
+
+
+def _exports(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path], check=True, capture_output=True, text=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if re.search(r"\sT\s+s2h_", line)}
+
+
+def test_header_compiles_as_c_and_cxx(tmp_path):
+    for lang, flags in (("c", ["-std=c11"]), ("c++", ["-std=c++17"])):
+        src = tmp_path / f"probe.{ 'c' if lang == 'c' else 'cpp'}"
+        src.write_text('#include "sam2hip.h"\nint probe(void) { return s2h_version(); }\n')
+        subprocess.run(["gcc", "-x", lang, *flags, "-Wall", "-Werror", "-fsyntax-only", "-I",
+                        os.path.join(ROOT, "include"), str(src)], check=True)
+
+
+def test_library_loads_and_reports_version(lib):
+    assert lib.lib().s2h_version() == 1
+
+
+def test_every_header_symbol_is_exported(lib):
+    declared = set(_prototypes())
+    exported = _exports(lib.LIB_PATH)
+    assert declared - exported == set(), f"declared but not exported: {sorted(declared - exported)}"
+    assert exported - declared == set(), f"exported but not declared: {sorted(exported - declared)}"
+    handle = lib.lib()
+    for name in declared:
+        assert getattr(handle, name) is not None
+
+
+def test_binding_matches_header():
+    from sam2_video.kernels import _lib
+    code = {ctypes.c_int: "I", ctypes.c_int64: "L", ctypes.c_float: "F", ctypes.c_uint64: "U", ctypes.c_void_p: "P"}
+    protos = _prototypes()
+    assert set(_lib.SIGNATURES) <= set(protos), sorted(set(_lib.SIGNATURES) - set(protos))
+    for name, argtypes in _lib.SIGNATURES.items():
+        got = [code[t] for t in argtypes]
+        assert got == protos[name], f"{name}: binding {got} != header {protos[name]}"
+
+
+def test_header_declares_the_hot_path_entry_points():
+    protos = _prototypes()
+    for name in ("s2h_gemm", "s2h_attn_fwd", "s2h_attn_bwd", "s2h_layernorm_fwd", "s2h_layernorm_bwd",
+                 "s2h_mask_stats", "s2h_mask_loss_finalize", "s2h_mask_loss_bwd", "s2h_group_max_fwd",
+                 "s2h_grad_norm", "s2h_adamw", "s2h_rope"):
+        assert name in protos
