@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames of the CPU baseline sample clip")
     ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--kernel-table", action="store_true",
+                    help="after timing, profile one extra step and print per-shape GEMM/attention TF/s to stderr")
     return ap.parse_args()
 
 
@@ -61,6 +63,41 @@ def attention_roofline(records):
             "kernel": "attn_fwd_kernel<bf16,256> (memory-attention cross-attention)",
             "launches": n, "avg_launch_ms": round(ms / n, 4),
             "flops_per_launch_avg": flops / n}
+
+
+def read_prof(_lib):
+    """[(ms, [kind, s0..s4])] of every record of the in-library launch profiler"""
+    import ctypes
+    n = _lib.lib().s2h_prof_count()
+    ms = (ctypes.c_float * max(n, 1))()
+    meta = (ctypes.c_int64 * (6 * max(n, 1)))()
+    n = _lib.lib().s2h_prof_read(n, ctypes.cast(ms, ctypes.c_void_p), ctypes.cast(meta, ctypes.c_void_p))
+    return [(ms[i], [meta[6 * i + j] for j in range(6)]) for i in range(n)]
+
+
+def kernel_table(recs):
+    """Per-shape time / achieved TFLOP/s of the GEMM and attention launches of one step."""
+    agg = {}
+    for ms, m in recs:
+        kind = m[0]
+        if kind == 4:
+            b, M, N, K, lay = m[1:]
+            key = ("gemm", f"b{b} {M}x{N}x{K} {'AB'[0] if lay & 2 else 'a'}{'B' if lay & 1 else 'b'}")
+            fl = 2.0 * b * M * N * K
+        else:
+            bh, lq, lk, d, _ = m[1:]
+            key = ("attn_fwd" if kind == 1 else "attn_bwd", f"bh{bh} {lq}x{lk} d{d}")
+            fl = (4.0 if kind == 1 else 10.0) * bh * lq * lk * d
+        a = agg.setdefault(key, [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += ms
+        a[2] += fl
+    rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    tot = sum(v[1] for v in agg.values())
+    out = [f"# profiled step: {tot:.2f} ms in GEMM + attention launches"]
+    for (kind, shape), (n, ms, fl) in rows:
+        out.append(f"{kind:9s} {shape:34s} n={n:4d} {ms:8.3f} ms {fl / (ms * 1e-3) / 1e12:7.1f} TF/s")
+    return "\n".join(out)
 
 
 def cpu_baseline(args):
@@ -147,14 +184,20 @@ def main():
 
     roof = None
     if not args.no_prof:
-        import ctypes
-        n = _lib.lib().s2h_prof_count()
-        ms = (ctypes.c_float * max(n, 1))()
-        meta = (ctypes.c_int64 * (5 * max(n, 1)))()
-        n = _lib.lib().s2h_prof_read(n, ctypes.cast(ms, ctypes.c_void_p), ctypes.cast(meta, ctypes.c_void_p))
-        recs = [(ms[i], [meta[5 * i + j] for j in range(5)]) for i in range(n)]
+        recs = read_prof(_lib)
         _lib.call("s2h_prof_enable", 0)
-        roof = attention_roofline(recs)
+        roof = attention_roofline([(ms, m[1:]) for ms, m in recs if m[0] == 1])
+        if args.kernel_table:
+            # one extra (untimed) step with every GEMM / attention launch recorded
+            _lib.call("s2h_prof_enable", 16384)
+            _lib.call("s2h_prof_select", 7)
+            runner(batches[-1])
+            torch.cuda.synchronize()
+            table = kernel_table(read_prof(_lib))
+            _lib.call("s2h_prof_enable", 0)
+            _lib.call("s2h_prof_select", 1)
+            if rank == 0:
+                print(table, file=sys.stderr, flush=True)
 
     frames = args.frames * args.steps * world
     value = frames / elapsed

@@ -36,12 +36,15 @@ enum { S2H_ACT_NONE = 0, S2H_ACT_RELU = 1, S2H_ACT_GELU = 2, S2H_ACT_SIGMOID = 3
 /* ABI version (1). */
 int s2h_version(void);
 /* In-library launch profiler: `cap` > 0 pre-creates `cap` HIP event pairs and
- * brackets every attention-forward launch on its own stream; 0 disables. */
+ * brackets every launch of a selected kind on the stream it is launched on; 0 disables. */
 int s2h_prof_enable(int cap);
+/* kinds recorded: bit 1 attention forward, 2 attention backward, 4 GEMM (default 1) */
+int s2h_prof_select(int mask);
 int s2h_prof_reset(void);
 int s2h_prof_count(void);
-/* Copies up to `max` records: ms[i] (event elapsed time) and meta[5*i..] =
- * (batch*heads, Lq, Lk, head_dim, element size).  Synchronises the events. */
+/* Copies up to `max` records: ms[i] (event elapsed time) and meta[6*i..] = (kind, shape):
+ * attention (1, 2): (batch*heads, Lq, Lk, head_dim, element size);
+ * GEMM (4): (batch, M, N, K, 2*A_kcontig + B_kcontig + 4*bf16).  Synchronises the events. */
 int s2h_prof_read(int max, float* ms, int64_t* meta);
 
 /* ---------------------------------------------------------------- GEMM

@@ -28,7 +28,7 @@ struct AttnArgs {
   uint64_t seed;
 };
 
-int s2h_prof_begin(hipStream_t st, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
+int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
 void s2h_prof_end(int slot, hipStream_t st);
 
 #define LOG2E 1.4426950408889634f
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
 template <typename T, int DP>
 static int attn_fwd_launch(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.Lq + 63) / 64, a.B * a.H);
-  const int slot = s2h_prof_begin(st, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
+  const int slot = s2h_prof_begin(st, 1, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
   hipLaunchKernelGGL((attn_fwd_kernel<T, DP>), grid, dim3(256), 0, st, a);
   s2h_prof_end(slot, st);
   return (int)hipGetLastError();
@@ -457,12 +457,14 @@ static int attn_fwd_launch(const AttnArgs& a, hipStream_t st) {
 template <typename T, int DP>
 static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.H * a.Lq;
+  const int slot = s2h_prof_begin(st, 2, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
   hipLaunchKernelGGL((attn_bwd_pre_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0, st, a);
   dim3 gq((a.Lq + 63) / 64, a.B * a.H);
   hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP>), gq, dim3(256), 0, st, a);
   constexpr int NW = AttnCfg<T>::NW_DKV;
   dim3 gk((a.Lk + NW * 16 - 1) / (NW * 16), a.B * a.H);
   hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DP>), gk, dim3(NW * 64), 0, st, a);
+  s2h_prof_end(slot, st);
   return (int)hipGetLastError();
 }
 

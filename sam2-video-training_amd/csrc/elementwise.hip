@@ -391,11 +391,59 @@ __global__ void colsum_kernel(int64_t rows, int cols, const void* x, int64_t ld,
   for (int64_t r = r0; r < r1; ++r) acc += to_f32(((const T*)x)[r * ld + c]);
   atomicAdd(&out[c], acc);
 }
+// Vectorised column sum (bias gradients): a thread owns 8 consecutive columns (one 16-B
+// load per row), G = cols/8 threads cover a row, 256/G rows per pass; a block walks a
+// contiguous row range, reduces its row-lanes through LDS and issues one atomic per column.
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t rows, int cols, const T* x, int64_t ld,
+                                                         int64_t rows_per_block, float* out) {
+  constexpr int V = 16 / sizeof(T);
+  const int G = cols / V;
+  const int lanes = 256 / G;  // row lanes per pass
+  const int g = threadIdx.x % G, lane = threadIdx.x / G;
+  __shared__ float red[256 * 8];
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  if (lane < lanes) {
+    for (int64_t r = r0 + lane; r < r1; r += lanes) {
+      const uint4 u = *(const uint4*)(x + r * ld + g * V);
+      const T* t = (const T*)&u;
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += to_f32(t[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[threadIdx.x * V + j] = (lane < lanes) ? acc[j] : 0.f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const int gg = c / V, j = c % V;
+    float s = 0.f;
+    for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * V + j];
+    atomicAdd(&out[c], s);
+  }
+}
+
 extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum,
                           hipStream_t st) {
   if (cols <= 0) return 0;
   if (!accum) (void)hipMemsetAsync(out, 0, cols * sizeof(float), st);
   if (rows <= 0) return (int)hipGetLastError();
+  const int V = dt == S2H_BF16 ? 8 : 4;
+  if (cols % V == 0 && cols / V <= 256 && ld % V == 0 && ((uintptr_t)x & 15) == 0) {
+    // ~1024 blocks, each >= 16 rows
+    int64_t rpb = (rows + 1023) / 1024;
+    if (rpb < 16) rpb = 16;
+    const int64_t nb = (rows + rpb - 1) / rpb;
+    if (dt == S2H_BF16)
+      hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
+                         (const bf16*)x, ld, rpb, out);
+    else
+      hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
+                         (const float*)x, ld, rpb, out);
+    return (int)hipGetLastError();
+  }
   const int cb = (cols + 255) / 256;
   int64_t ry = (rows + 255) / 256;
   int64_t want = 2048 / cb;

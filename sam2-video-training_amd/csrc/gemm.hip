@@ -211,7 +211,14 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   if (K <= 0) {
     a.K = 0;
   }
-  if (dt_ab == S2H_F32) return launch_gemm<float, float>(a, batch, stream);
+  // profiler record: (batch, M, N, K, layout = 2*A_kcontig + B_kcontig + 4*bf16)
+  const int slot = s2h_prof_begin(stream, 4, batch, M, N, K, 2 * (lda_k == 1) + (ldb_k == 1) + 4 * (dt_ab == S2H_BF16));
+  int rc;
+  if (dt_ab == S2H_F32) {
+    rc = launch_gemm<float, float>(a, batch, stream);
+    s2h_prof_end(slot, stream);
+    return rc;
+  }
   GemmArgs16 b;
   b.M = a.M; b.N = a.N; b.K = a.K;
   b.A = (const bf16*)A; b.lda_m = lda_m; b.lda_k = lda_k; b.sA = sA;
@@ -224,5 +231,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   b.alpha = alpha; b.beta = beta; b.act = act;
   b.vecA = a.vecA; b.vecB = a.vecB;
   b.out_f32 = dt_c == S2H_F32;
-  return s2h_gemm_bf16(b, batch, stream);
+  rc = s2h_gemm_bf16(b, batch, stream);
+  s2h_prof_end(slot, stream);
+  return rc;
 }

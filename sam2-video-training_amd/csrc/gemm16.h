@@ -17,6 +17,9 @@ struct GemmArgs16 {
   int vecA, vecB;
   int splits, kchunk;  // split-K: blockIdx.z = batch * splits + split
   int out_f32;
+  int vecC;  // 4-column output groups are vector-aligned
 };
 
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);
+int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
+void s2h_prof_end(int slot, hipStream_t st);

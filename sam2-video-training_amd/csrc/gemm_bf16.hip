@@ -80,6 +80,70 @@ struct Stage16 {
   }
 };
 
+// Finishes outputs (row, col0..col0+3) of batch bz from the fp32 accumulators v4.
+__device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4) {
+  float v[4] = {v4.x, v4.y, v4.z, v4.w};
+  const bool full = col0 + 3 < p.N;
+  if (p.splits > 1) {  // split-K: fp32 atomic accumulate (beta handled on the host side)
+    float* C = (float*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (col0 + e < p.N) atomicAdd(C + e, p.alpha * v[e]);
+    return;
+  }
+  const int64_t xo = (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0;
+  const int64_t co = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
+  const bf16* R = p.R ? (const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0 : nullptr;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int col = col0 + e;
+    if (col >= p.N) break;
+    float x = p.alpha * v[e];
+    if (p.bias_mode == 1) x += p.bias[col];
+    else if (p.bias_mode == 2) x += p.bias[row];
+    if (p.aux_mode == 1) ((bf16*)p.X)[xo + e] = (bf16)x;
+    if (p.aux_mode == 2) x *= act_grad((float)((const bf16*)p.X)[xo + e], p.act);
+    else x = apply_act(x, p.act);
+    if (p.cscale) x *= p.cscale[col];
+    if (p.drop_p > 0.f) {
+      const uint64_t idx = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
+      x = s2h_keep(p.seed, idx, (uint32_t)(p.drop_p * 4294967296.0)) ? x / (1.f - p.drop_p) : 0.f;
+    }
+    if (R) x += (float)R[e];
+    v[e] = x;
+  }
+  if (p.out_f32) {
+    float* C = (float*)p.C + co;
+    if (full && p.vecC) {
+      float4 o = {v[0], v[1], v[2], v[3]};
+      if (p.beta != 0.f) {
+        const float4 c = *(const float4*)C;
+        o.x += p.beta * c.x; o.y += p.beta * c.y; o.z += p.beta * c.z; o.w += p.beta * c.w;
+      }
+      *(float4*)C = o;
+    } else {
+      for (int e = 0; e < 4 && col0 + e < p.N; ++e) C[e] = v[e] + (p.beta != 0.f ? p.beta * C[e] : 0.f);
+    }
+  } else {
+    bf16* C = (bf16*)p.C + co;
+    if (full && p.vecC) {
+      bf16 o[4];
+      if (p.beta != 0.f) {
+        const uint2 c = *(const uint2*)C;
+        const bf16* cb = (const bf16*)&c;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)(v[e] + p.beta * (float)cb[e]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
+      }
+      *(uint2*)C = *(const uint2*)o;
+    } else {
+      for (int e = 0; e < 4 && col0 + e < p.N; ++e) C[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)C[e] : 0.f));
+    }
+  }
+}
+
 template <int BM, int BN, bool AKC, bool BKC>
 __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
   constexpr int BK = 64;
@@ -136,57 +200,31 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
     __syncthreads();
   }
 
-  if (p.splits > 1) {  // split-K: fp32 atomic accumulate (output pre-scaled by beta on the host side)
-    float* C = (float*)p.C + (int64_t)bz * p.sC;
+  // Epilogue through LDS: each wave stages one 16-row slab of its accumulators (static
+  // register indices -- no scratch), then every lane finishes 4 consecutive columns of a
+  // row with a compact loop and vectorised stores.
+  constexpr int EPLD = WN + 4;
+  constexpr int CPR = WN / 4;    // lanes per row
+  constexpr int RPP = 64 / CPR;  // rows per pass
+  static_assert(4 * 16 * EPLD * 4 <= (SA::LDS_ELEMS + SB::LDS_ELEMS) * 2, "epilogue staging fits the tile LDS");
+  float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
+  const int c4 = lane % CPR, rg = lane / CPR;
+  if (nk == 0) __syncthreads();
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+  for (int i = 0; i < MI; ++i) {
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int col = n0 + wn * WN + j * 16 + (lane & 15);
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-          if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * acc[i][j][r]);
-        }
-      }
-    return;
-  }
-  const bf16* R = p.R ? (const bf16*)p.R + (int64_t)bz * p.sR : nullptr;
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const int col = n0 + wn * WN + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (row < p.M && col < p.N) {
-          float v = p.alpha * acc[i][j][r];
-          if (p.bias_mode == 1) v += p.bias[col];
-          else if (p.bias_mode == 2) v += p.bias[row];
-          const int64_t xo = (int64_t)bz * p.sX + (int64_t)row * p.ldx + col;
-          if (p.aux_mode == 1) ((bf16*)p.X)[xo] = (bf16)v;
-          if (p.aux_mode == 2) v *= act_grad((float)((const bf16*)p.X)[xo], p.act);
-          else v = apply_act(v, p.act);
-          if (p.cscale) v *= p.cscale[col];
-          if (p.drop_p > 0.f) {
-            const uint64_t idx = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
-            v = s2h_keep(p.seed, idx, (uint32_t)(p.drop_p * 4294967296.0)) ? v / (1.f - p.drop_p) : 0.f;
-          }
-          if (R) v += (float)R[(int64_t)row * p.ldr + col];
-          const int64_t off = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col;
-          if (p.out_f32) {
-            float* C = (float*)p.C;
-            if (p.beta != 0.f) v += p.beta * C[off];
-            C[off] = v;
-          } else {
-            bf16* C = (bf16*)p.C;
-            if (p.beta != 0.f) v += p.beta * (float)C[off];
-            C[off] = (bf16)v;
-          }
-        }
-      }
+      for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    for (int ps = 0; ps < 16 / RPP; ++ps) {
+      const int rl = rg + ps * RPP;
+      const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
+      const int row = m0 + wm * WM + i * 16 + rl;
+      if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4);
     }
+    __syncthreads();
+  }
 }
 
 template <int BM, int BN>
@@ -217,6 +255,8 @@ static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
       }
     }
   }
+  // 4-column output groups: 16-B (f32) / 8-B (bf16) aligned
+  a.vecC = ((uintptr_t)a.C % (a.out_f32 ? 16 : 8) == 0) && a.ldc % 4 == 0 && (batch == 1 || a.sC % 4 == 0);
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * a.splits);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
   if (akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, true>), grid, dim3(256), 0, st, a);

@@ -1,8 +1,9 @@
 // Library metadata + in-library launch profiler.
 //
-// s2h_prof_enable(cap) pre-creates `cap` event pairs; while enabled every
-// attention-forward launch is bracketed by hipEventRecord on the stream it is
-// launched on, together with its shape (B*H, Lq, Lk, D).  bench.py reads the
+// s2h_prof_enable(cap) pre-creates `cap` event pairs; while enabled every launch
+// of a selected kind (s2h_prof_select mask: 1 attention forward, 2 attention
+// backward, 4 GEMM; default 1) is bracketed by hipEventRecord on the stream it
+// is launched on, together with its kind and shape.  bench.py reads the
 // per-launch durations back with s2h_prof_read to price the dominant kernel
 // against the bf16 MFMA roofline (no host sync inside the timed region).
 #include "common.h"
@@ -12,11 +13,12 @@
 extern "C" int s2h_version() { return 1; }
 
 namespace {
-struct ProfRec { hipEvent_t a, b; int64_t meta[5]; };
+struct ProfRec { hipEvent_t a, b; int64_t meta[6]; };
 std::mutex g_mu;
 std::vector<ProfRec> g_pool;
 int g_used = 0;
 bool g_on = false;
+int g_mask = 1;
 }  // namespace
 
 extern "C" int s2h_prof_enable(int cap) {
@@ -36,12 +38,15 @@ extern "C" int s2h_prof_reset() { std::lock_guard<std::mutex> lk(g_mu); g_used =
 extern "C" int s2h_prof_count() { std::lock_guard<std::mutex> lk(g_mu); return g_used; }
 
 // internal: returns slot index or -1
-int s2h_prof_begin(hipStream_t st, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4) {
-  if (!g_on) return -1;
+extern "C" int s2h_prof_select(int mask) { std::lock_guard<std::mutex> lk(g_mu); g_mask = mask; return 0; }
+
+int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4) {
+  if (!g_on || !(g_mask & kind)) return -1;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_used >= (int)g_pool.size()) return -1;
   int i = g_used++;
-  g_pool[i].meta[0] = m0; g_pool[i].meta[1] = m1; g_pool[i].meta[2] = m2; g_pool[i].meta[3] = m3; g_pool[i].meta[4] = m4;
+  int64_t* m = g_pool[i].meta;
+  m[0] = kind; m[1] = m0; m[2] = m1; m[3] = m2; m[4] = m3; m[5] = m4;
   (void)hipEventRecord(g_pool[i].a, st);
   return i;
 }
@@ -50,7 +55,7 @@ void s2h_prof_end(int slot, hipStream_t st) {
   (void)hipEventRecord(g_pool[slot].b, st);
 }
 
-// ms[i] = duration of record i; meta[5*i..] = its shape. Synchronises on the events.
+// ms[i] = duration of record i; meta[6*i..] = (kind, shape[5]). Synchronises on the events.
 extern "C" int s2h_prof_read(int max, float* ms, int64_t* meta) {
   std::lock_guard<std::mutex> lk(g_mu);
   int n = g_used < max ? g_used : max;
@@ -59,7 +64,7 @@ extern "C" int s2h_prof_read(int max, float* ms, int64_t* meta) {
     float t = 0.f;
     (void)hipEventElapsedTime(&t, g_pool[i].a, g_pool[i].b);
     ms[i] = t;
-    for (int k = 0; k < 5; ++k) meta[5 * i + k] = g_pool[i].meta[k];
+    for (int k = 0; k < 6; ++k) meta[6 * i + k] = g_pool[i].meta[k];
   }
   return n;
 }

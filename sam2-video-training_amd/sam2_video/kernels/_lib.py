@@ -69,6 +69,7 @@ SIGNATURES = {
     "s2h_point_embed": [I, I, I, P, P, P, P, P],
     "s2h_point_embed_bwd": [I, I, I, P, P, P, P],
     "s2h_prof_enable": [I],
+    "s2h_prof_select": [I],
     "s2h_prof_reset": [],
     "s2h_prof_count": [],
     "s2h_prof_read": [I, P, P],

@@ -71,6 +71,19 @@ def test_wgrad_split_k(rows, N, K):
     _close(out[0], ref, 2e-3)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("rows,cols", [(131072, 112), (13312, 2048), (5, 24), (1000, 37), (70000, 256), (3, 4096)])
+def test_colsum_shapes(dtype, rows, cols):
+    ops = _ops()
+    torch.manual_seed(2)
+    x = torch.randn(rows, cols, device=DEV).to(dtype)
+    out = torch.full((cols,), 1.0, device=DEV)
+    ops.colsum(x, out)  # accumulate
+    _close(out, x.float().sum(0) + 1.0, 1e-4)
+    ops.colsum(x, out, accumulate=False)
+    _close(out, x.float().sum(0), 1e-4)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
 def test_bmm_layouts(dtype, tol):
     ops = _ops()
