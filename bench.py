@@ -25,6 +25,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+# algorithmic fwd+bwd TFLOP per clip-frame: config 2 all-trainable
+# 13.75 TF / 8 frames, `mem` 11.14 TF / 8 frames
+STEP_TF_PER_FRAME = {("base_plus", 512, 8, 13, "all"): 13.75 / 8, ("base_plus", 512, 8, 13, "mem"): 11.14 / 8}
 ALL = ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder", "prompt_encoder"]
 
 
@@ -220,6 +223,10 @@ def main():
                    "global_batch": world, "clips_per_rank": 1, "frames": args.frames,
                    "image_size": args.image_size, "objects": args.objects, "parallelism": f"dp{world}"},
         "roofline": roof,
+        # whole-step MFMA utilisation: algorithmic TF per clip-frame x rate / peak
+        "step_mfma_frac": (round(STEP_TF_PER_FRAME[(args.size, args.image_size, args.frames, args.objects, args.trainable)] * value
+                                 / (PEAK_BF16_TFLOPS * world), 4)
+                           if (args.size, args.image_size, args.frames, args.objects, args.trainable) in STEP_TF_PER_FRAME else None),
         "cpu_baseline": None,
         "final_loss": round(loss_val, 5),
     }
