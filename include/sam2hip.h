@@ -74,6 +74,13 @@ int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
              const float* cscale, float drop_p, uint64_t seed,
              float alpha, float beta, int act, hipStream_t stream);
 
+/* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
+ * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),
+ * db[N] (+)= sum over rows of dy (db may be NULL); `accumulate` 0 overwrites both.
+ * bf16 dy/x: one launch, the bias gradient summed from the GEMM's staged dy tiles. */
+int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t lddy, const void* x,
+                     int64_t ldx, float* dw, int64_t lddw, float* db, int accumulate, hipStream_t stream);
+
 /* ---------------------------------------------------------------- attention
  * Fused multi-head attention, tensors [B, L, H, D] addressed through
  * (batch, head, row) strides with contiguous D; lse [B, H, Lq] fp32 (natural log).

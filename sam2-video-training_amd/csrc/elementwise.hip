@@ -522,10 +522,76 @@ __global__ void dwconv_kernel(int B, int H, int W, int C, int K, int pad, const 
     ((T*)y)[i] = from_f32<T>(acc);
   }
 }
+// Channel-vectorised form: a block owns a 64-channel slice of 32 consecutive pixels of one
+// row; the slice's K*K taps are staged in LDS as [tap][64] so every lane reads its 8
+// channels' weights with two 16-B LDS loads, and the 8 channels of x with one 16-B load.
+template <typename T>
+__global__ __launch_bounds__(256) void dwconv_vec_kernel(int B, int H, int W, int C, int K, int pad, const T* x,
+                                                         const float* w, const float* bias, T* y) {
+  __shared__ __attribute__((aligned(16))) float wl[49 * 64];
+  const int cg = threadIdx.x & 7, px = threadIdx.x >> 3;  // 8 channel groups x 32 pixels
+  const int c0 = blockIdx.z * 64;
+  const int row = blockIdx.y;  // b*H + yy
+  const int yy = row % H, b = row / H;
+  const int xx = blockIdx.x * 32 + px;
+  for (int i = threadIdx.x; i < K * K * 64; i += 256) {
+    const int t = i / 64, c = i % 64;
+    wl[t * 64 + c] = w[(int64_t)(c0 + c) * K * K + t];
+  }
+  __syncthreads();
+  if (xx >= W) return;
+  const int cc = c0 + cg * 8;
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = bias ? bias[cc + j] : 0.f;
+  for (int ky = 0; ky < K; ++ky) {
+    const int sy = yy - pad + ky;
+    if (sy < 0 || sy >= H) continue;
+    const T* xr = x + (((int64_t)b * H + sy) * W) * C + cc;
+    for (int kx = 0; kx < K; ++kx) {
+      const int sx = xx - pad + kx;
+      if (sx < 0 || sx >= W) continue;
+      T v[8];
+      if (sizeof(T) == 2) {
+        *(uint4*)v = *(const uint4*)(xr + (int64_t)sx * C);
+      } else {
+        *(uint4*)v = *(const uint4*)(xr + (int64_t)sx * C);
+        *(uint4*)(v + 4) = *(const uint4*)(xr + (int64_t)sx * C + 4);
+      }
+      const float4 w0 = *(const float4*)&wl[(ky * K + kx) * 64 + cg * 8];
+      const float4 w1 = *(const float4*)&wl[(ky * K + kx) * 64 + cg * 8 + 4];
+      acc[0] += w0.x * to_f32(v[0]); acc[1] += w0.y * to_f32(v[1]);
+      acc[2] += w0.z * to_f32(v[2]); acc[3] += w0.w * to_f32(v[3]);
+      acc[4] += w1.x * to_f32(v[4]); acc[5] += w1.y * to_f32(v[5]);
+      acc[6] += w1.z * to_f32(v[6]); acc[7] += w1.w * to_f32(v[7]);
+    }
+  }
+  T o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = from_f32<T>(acc[j]);
+  T* yp = y + (((int64_t)b * H + yy) * W + xx) * C + cc;
+  if (sizeof(T) == 2) {
+    *(uint4*)yp = *(const uint4*)o;
+  } else {
+    *(uint4*)yp = *(const uint4*)o;
+    *(uint4*)(yp + 4) = *(const uint4*)(o + 4);
+  }
+}
+
 extern "C" int s2h_dwconv(int dt, int B, int H, int W, int C, int K, int pad, const void* x, const float* w,
                           const float* bias, void* y, hipStream_t st) {
   const int64_t n = (int64_t)B * H * W * C;
   if (n <= 0) return 0;
+  if (C % 64 == 0 && K <= 7 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    dim3 grid((W + 31) / 32, B * H, C / 64);
+    if (dt == S2H_BF16)
+      hipLaunchKernelGGL(dwconv_vec_kernel<bf16>, grid, dim3(256), 0, st, B, H, W, C, K, pad, (const bf16*)x, w,
+                         bias, (bf16*)y);
+    else
+      hipLaunchKernelGGL(dwconv_vec_kernel<float>, grid, dim3(256), 0, st, B, H, W, C, K, pad, (const float*)x, w,
+                         bias, (float*)y);
+    return (int)hipGetLastError();
+  }
   DISPATCH_T(dt, dwconv_kernel, ew_grid(n), B, H, W, C, K, pad, x, w, bias, y);
   return (int)hipGetLastError();
 }

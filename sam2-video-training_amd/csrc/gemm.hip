@@ -231,7 +231,42 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   b.alpha = alpha; b.beta = beta; b.act = act;
   b.vecA = a.vecA; b.vecB = a.vecB;
   b.out_f32 = dt_c == S2H_F32;
+  b.rowsum = nullptr;
   rc = s2h_gemm_bf16(b, batch, stream);
+  s2h_prof_end(slot, stream);
+  return rc;
+}
+
+extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum,
+                          hipStream_t st);
+
+// Weight (and bias) gradient of a Linear layer y = x W^T + b over `rows` rows:
+//   dw[N, K] (+)= dy[rows, N]^T x[rows, K]      db[N] (+)= sum_rows dy
+// bf16: one GEMM launch (split over the row reduction when the N x K tiles cannot fill the
+// chip) with the bias gradient summed from the staged dy tiles; fp32: GEMM + column sum.
+extern "C" int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t lddy, const void* x,
+                                int64_t ldx, float* dw, int64_t lddw, float* db, int accumulate, hipStream_t stream) {
+  if (N <= 0 || K <= 0) return 0;
+  if (rows > INT32_MAX) return (int)hipErrorInvalidValue;
+  if (!accumulate && db) (void)hipMemsetAsync(db, 0, (size_t)N * sizeof(float), stream);
+  if (dt == S2H_F32) {
+    int rc = s2h_gemm(S2H_F32, S2H_F32, 1, N, K, (int)rows, dy, 1, lddy, 0, x, ldx, 1, 0, dw, lddw, 0, nullptr, 0,
+                      nullptr, 0, 0, nullptr, 0, 0, 0, nullptr, 0.f, 0, 1.f, accumulate ? 1.f : 0.f, 0, stream);
+    if (rc || !db) return rc;
+    return s2h_colsum(dt, rows, N, dy, lddy, db, 1, stream);
+  }
+  const int slot = s2h_prof_begin(stream, 4, 1, N, K, rows, 4);
+  GemmArgs16 b = {};
+  b.M = N; b.N = K; b.K = (int)rows;
+  b.A = (const bf16*)dy; b.lda_m = 1; b.lda_k = lddy; b.sA = 0;
+  b.B = (const bf16*)x; b.ldb_k = ldx; b.ldb_n = 1; b.sB = 0;
+  b.C = dw; b.ldc = lddw; b.sC = 0;
+  b.alpha = 1.f; b.beta = accumulate ? 1.f : 0.f;
+  b.vecA = aligned16(dy) && lddy % 8 == 0;
+  b.vecB = aligned16(x) && ldx % 8 == 0;
+  b.out_f32 = 1;
+  b.rowsum = db;
+  const int rc = s2h_gemm_bf16(b, 1, stream);
   s2h_prof_end(slot, stream);
   return rc;
 }

@@ -18,6 +18,7 @@ struct GemmArgs16 {
   int splits, kchunk;  // split-K: blockIdx.z = batch * splits + split
   int out_f32;
   int vecC;  // 4-column output groups are vector-aligned
+  float* rowsum;  // optional: rowsum[b*M + m] += sum_k A[b](m, k)  (fused bias gradient)
 };
 
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);

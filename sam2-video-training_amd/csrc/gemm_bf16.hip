@@ -176,10 +176,18 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
     la.load(A, p.lda_m, p.lda_k, m0, kbeg, p.M, kend, p.vecA, tid);
     lb.load(B, p.ldb_n, p.ldb_k, n0, kbeg, p.N, kend, p.vecB, tid);
   }
+  // optional fused row sums of A (the bias gradient of a Linear's weight-gradient GEMM):
+  // the first column tile's threads < BM sum their A row out of the staged LDS tile
+  const bool do_rs = p.rowsum != nullptr && blockIdx.x == 0 && tid < BM;
+  float rs = 0.f;
   for (int kt = 0; kt < nk; ++kt) {
     la.store(As, tid);
     lb.store(Bs, tid);
     __syncthreads();
+    if (do_rs) {
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) rs += (float)(AKC ? As[tid * SA::LDS_LD + k] : As[k * SA::LDS_LD + tid]);
+    }
     if (kt + 1 < nk) {
       la.load(A, p.lda_m, p.lda_k, m0, kbeg + (kt + 1) * BK, p.M, kend, p.vecA, tid);
       lb.load(B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + 1) * BK, p.N, kend, p.vecB, tid);
@@ -209,6 +217,7 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
   static_assert(4 * 16 * EPLD * 4 <= (SA::LDS_ELEMS + SB::LDS_ELEMS) * 2, "epilogue staging fits the tile LDS");
   float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
   const int c4 = lane % CPR, rg = lane / CPR;
+  if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
   if (nk == 0) __syncthreads();
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
@@ -243,7 +252,9 @@ static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
       a.splits = s;
       a.kchunk = ((a.K + s - 1) / s + 63) / 64 * 64;
       a.splits = (a.K + a.kchunk - 1) / a.kchunk;
-      if (a.beta == 0.f) {
+      if (a.beta == 0.f && a.ldc == a.N && (batch == 1 || a.sC == (int64_t)a.M * a.N)) {
+        (void)hipMemsetAsync(a.C, 0, (size_t)batch * a.M * a.N * sizeof(float), st);
+      } else if (a.beta == 0.f) {
         for (int b = 0; b < batch; ++b) {
           if (a.ldc == a.N) {
             (void)hipMemsetAsync((float*)a.C + (int64_t)b * a.sC, 0, (size_t)a.M * a.N * sizeof(float), st);

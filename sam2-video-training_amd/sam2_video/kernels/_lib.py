@@ -26,7 +26,8 @@ F = c_float
 SIGNATURES = {
     "s2h_version": [],
     "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, F, F, I, P],
-    "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P],
+    "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
+    "s2h_attn_fwd":[I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P],
     "s2h_attn_bwd": [I, I, I, I, I, I,
                      P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
                      P, L, L, L, P, L, L, L, P, L, L, L,

@@ -57,8 +57,8 @@ class _Linear(torch.autograd.Function):
         dpre = ops.act_bwd(pre, g, ctx.act) if ctx.act else g
         gw, gb = mod.grad_views()
         if gw is not None:
-            ops.linear_wgrad(dpre, x, gw.view(gw.shape[0], -1))
-        if gb is not None:
+            ops.linear_wgrad(dpre, x, gw.view(gw.shape[0], -1), db=gb)
+        elif gb is not None:
             ops.colsum(dpre, gb)
         dx = ops.linear_dgrad(dpre, mod.compute_weight()) if ctx.needs_input_grad[0] else None
         return dx, None, None, None, None, (dy if ctx.has_res else None), None

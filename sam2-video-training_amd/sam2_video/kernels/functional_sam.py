@@ -175,9 +175,11 @@ class _HyperMask(torch.autograd.Function):
         g3 = g.contiguous().view(O, 1, P)
         dh = dup = None
         if ctx.needs_input_grad[0]:
-            dh = torch.empty(O, 1, C, device=up.device, dtype=up.dtype)
+            # a [1 x P] @ [P x C] reduction over P = 16k pixels per object: fp32 output lets the
+            # GEMM split the reduction over workgroups (13 output tiles could not fill the chip)
+            dh = torch.empty(O, 1, C, device=up.device, dtype=torch.float32)
             ops.bmm(g3, up, dh)
-            dh = dh.view(O, C)
+            dh = dh.view(O, C).to(up.dtype)
         if ctx.needs_input_grad[1]:
             dup = torch.empty(O, P, C, device=up.device, dtype=up.dtype)
             # dup[o] = g[o]^T (P x 1) @ hyper[o] (1 x C)

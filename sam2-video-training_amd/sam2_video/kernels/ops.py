@@ -90,15 +90,19 @@ def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None):
     return dx
 
 
-def linear_wgrad(dy, x, dw, accumulate=True):
-    """dw (fp32 [N, K]) (+)= dy^T @ x."""
+def linear_wgrad(dy, x, dw, accumulate=True, db=None):
+    """dw (fp32 [N, K]) (+)= dy^T @ x;  db (fp32 [N], optional) (+)= dy summed over rows."""
     dy2 = dy.reshape(-1, dy.shape[-1])
     x2 = x.reshape(-1, x.shape[-1])
     M, N = dy2.shape
     K = x2.shape[1]
-    assert dw.dtype == torch.float32 and dw.shape == (N, K)
-    gemm(dy2, x2, dw, M=N, N=K, K=M, lda_m=1, lda_k=dy2.stride(0), ldb_k=x2.stride(0), ldb_n=1, ldc=K,
-         beta=1.0 if accumulate else 0.0)
+    assert dw.dtype == torch.float32 and dw.shape == (N, K) and dw.stride(1) == 1
+    assert dy2.dtype == x2.dtype and dy2.stride(1) == 1 and x2.stride(1) == 1
+    if db is not None:
+        assert db.dtype == torch.float32 and db.numel() == N and db.is_contiguous()
+    _dev(dy2, x2, dw, db)
+    call("s2h_linear_wgrad", dt(dy2), M, N, K, ptr(dy2), dy2.stride(0), ptr(x2), x2.stride(0), ptr(dw), dw.stride(0),
+         ptr(db), int(accumulate), stream())
     return dw
 
 

@@ -46,9 +46,14 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     dx = ops.linear_dgrad(dy, w)
     _close(dx, dy.float() @ w.float(), tol)
     dw = torch.zeros(N, K, device=DEV)
-    ops.linear_wgrad(dy, x, dw)
-    ops.linear_wgrad(dy, x, dw)  # accumulates
+    db = torch.zeros(N, device=DEV)
+    ops.linear_wgrad(dy, x, dw, db=db)
+    ops.linear_wgrad(dy, x, dw, db=db)  # accumulates
     _close(dw, 2 * dy.float().t() @ x.float(), tol)
+    _close(db, 2 * dy.float().sum(0), 1e-4)
+    ops.linear_wgrad(dy, x, dw, accumulate=False, db=db)
+    _close(dw, dy.float().t() @ x.float(), tol)
+    _close(db, dy.float().sum(0), 1e-4)
     r = torch.randn(M, N, device=DEV).to(dtype)
     y = ops.linear(x, w, b, residual=r)
     _close(y, ref + r.float(), tol)
@@ -64,8 +69,10 @@ def test_wgrad_split_k(rows, N, K):
     x = torch.randn(rows, K, device=DEV).to(torch.bfloat16)
     ref = dy.float().t() @ x.float()
     dw = torch.full((N, K), 0.5, device=DEV)
-    ops.linear_wgrad(dy, x, dw)
+    db = torch.full((N,), 0.25, device=DEV)
+    ops.linear_wgrad(dy, x, dw, db=db)
     _close(dw, ref + 0.5, 2e-3)
+    _close(db, dy.float().sum(0) + 0.25, 1e-4)
     out = torch.full((1, N, K), 7.0, device=DEV)
     ops.gemm(dy, x, out, M=N, N=K, K=rows, lda_m=1, lda_k=N, ldb_k=K, ldb_n=1, ldc=K, beta=0.0)
     _close(out[0], ref, 2e-3)
@@ -265,6 +272,19 @@ def test_im2col_conv_matches_torch():
     yd = ops.dwconv(xd, wd, b[:6], 3)
     ref = torch.nn.functional.conv2d(xd.permute(0, 3, 1, 2), wd, b[:6], padding=3, groups=6).permute(0, 2, 3, 1)
     _close(yd, ref, 2e-5)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,H,W,C", [(13, 32, 32, 256), (2, 7, 45, 128)])
+def test_dwconv_vectorised(dtype, tol, B, H, W, C):
+    ops = _ops()
+    torch.manual_seed(3)
+    x = torch.randn(B, H, W, C, device=DEV).to(dtype)
+    w = torch.randn(C, 1, 7, 7, device=DEV)
+    b = torch.randn(C, device=DEV)
+    y = ops.dwconv(x, w, b, 3)
+    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w, b, padding=3, groups=C).permute(0, 2, 3, 1)
+    _close(y, ref, tol)
 
 
 def test_convt2():
