@@ -89,13 +89,22 @@ int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t
  * for bf16, 32..256 (multiple of 4) for fp32.
  * Replaces F.scaled_dot_product_attention at hieradet.py:70 (windowed / global
  * Hiera attention), transformer.py:243 (two-way decoder attention) and
- * transformer.py:306 (memory-attention RoPE self / cross attention). */
+ * transformer.py:306 (memory-attention RoPE self / cross attention).
+ * bf16 with head_dim 64/128/256 and >= 128 query rows takes the flash path
+ * (32x32 MFMA, LDS-DMA K/V ring, key range split over workgroups): it wants a
+ * device workspace of s2h_attn_fwd_ws_bytes(...) bytes (ws = NULL / too small
+ * just disables the key split). */
+int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D);
+/* A/B switch (tests, benchmarks): flash_enable = 0 sends every attention to the generic
+ * kernels; returns the previous setting. */
+int s2h_attn_config(int flash_enable);
 int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                  const void* k, int64_t skb, int64_t skh, int64_t skl,
                  const void* v, int64_t svb, int64_t svh, int64_t svl,
                  void* o, int64_t sob, int64_t soh, int64_t sol,
-                 float* lse, float scale, float p_drop, uint64_t seed, hipStream_t st);
+                 float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
+                 hipStream_t st);
 /* Backward of s2h_attn_fwd; di_ws: fp32 workspace [B*H*Lq]. */
 int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,

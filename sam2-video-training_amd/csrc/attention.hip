@@ -30,6 +30,18 @@ struct AttnArgs {
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
 void s2h_prof_end(int slot, hipStream_t st);
+// flash.hip (bf16 long-sequence forward)
+int s2h_flash_eligible(int dt, int Lq, int D);
+int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D);
+int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                  const void* k, int64_t skb, int64_t skh, int64_t skl, const void* v, int64_t svb, int64_t svh,
+                  int64_t svl, void* o, int64_t sob, int64_t soh, int64_t sol, float* lse, float scale, float p_drop,
+                  uint64_t seed, void* ws, int64_t ws_bytes, hipStream_t st);
+
+// Workspace the forward wants (key-split partials of the flash path); 0 = none.
+extern "C" int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D) {
+  return s2h_flash_eligible(dt, Lq, D) ? s2h_flash_ws_bytes(B, H, Lq, Lk, D) : 0;
+}
 
 #define LOG2E 1.4426950408889634f
 #define LN2 0.6931471805599453f
@@ -488,12 +500,20 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                             const void* k, int64_t skb, int64_t skh, int64_t skl,
                             const void* v, int64_t svb, int64_t svh, int64_t svl,
                             void* o, int64_t sob, int64_t soh, int64_t sol,
-                            float* lse, float scale, float p_drop, uint64_t seed, hipStream_t st) {
+                            float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
+                            hipStream_t st) {
   if (B * H <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
       !attn_aligned(dt, D, v, svb, svh, svl))
     return (int)hipErrorInvalidValue;
+  if (s2h_flash_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol)) {
+    const int slot = s2h_prof_begin(st, 1, (int64_t)B * H, Lq, Lk, D, 2);
+    const int rc = s2h_flash_fwd(B, H, Lq, Lk, D, q, sqb, sqh, sql, k, skb, skh, skl, v, svb, svh, svl, o, sob, soh,
+                                 sol, lse, scale, p_drop, seed, ws, ws_bytes, st);
+    s2h_prof_end(slot, st);
+    return rc;
+  }
   AttnArgs a = {};
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.D = D;
   a.q = q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;

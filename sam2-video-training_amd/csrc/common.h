@@ -77,18 +77,34 @@ __device__ __forceinline__ float row16_max(float v) {
   return v;
 }
 
-// Counter-based dropout RNG (splitmix-style 64-bit hash).  keep(i) is a pure
-// function of (seed, offset, index), so forward and backward regenerate the
-// same mask without storing it.
-__device__ __forceinline__ uint32_t s2h_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z ^= z >> 31;
-  return (uint32_t)(z >> 32);
+// Counter-based dropout RNG.  keep(i) is a pure function of (seed, element index), so
+// forward and backward regenerate the same mask without storing it.  One 32-bit hash
+// (lowbias32 finaliser: 2 multiplies, 3 xor-shifts) serves an even/odd PAIR of elements
+// (16 bits each, drop probability quantised to 1/65536): dropout sits inside the
+// attention softmax, where a 64-bit splitmix per element cost more VALU than the math.
+__device__ __forceinline__ uint32_t s2h_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
 }
+__device__ __forceinline__ uint32_t s2h_hash_pair(uint64_t seed, uint64_t pair) {
+  const uint32_t key = s2h_mix32((uint32_t)seed ^ 0x5bd1e995u) ^ (uint32_t)(seed >> 32);
+  return s2h_mix32(((uint32_t)pair + (uint32_t)(pair >> 32) * 0x9E3779B9u) ^ key);
+}
+// thresh = p * 2^32 (the 16 high bits are used)
 __device__ __forceinline__ bool s2h_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
-  return s2h_hash(seed, idx) >= thresh;
+  const uint32_t h = s2h_hash_pair(seed, idx >> 1);
+  const uint32_t u = (idx & 1) ? (h >> 16) : (h & 0xFFFFu);
+  return u >= (thresh >> 16);
+}
+// keep flags of elements 2*pair and 2*pair + 1 from one hash
+__device__ __forceinline__ void s2h_keep_pair(uint64_t seed, uint64_t pair, uint32_t thresh, bool& k0, bool& k1) {
+  const uint32_t h = s2h_hash_pair(seed, pair);
+  k0 = (h & 0xFFFFu) >= (thresh >> 16);
+  k1 = (h >> 16) >= (thresh >> 16);
 }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }

@@ -1,0 +1,380 @@
+// Flash attention forward for the long-sequence attentions of the step (bf16):
+// memory-attention RoPE self / cross attention (transformer.py:275-311; head_dim 256,
+// Lq = 1024, Lk <= 7*1028) and Hiera global attention (hieradet.py:56-81).
+//
+// CDNA4 structure (one workgroup = 8 waves x 16 query rows, two waves per SIMD so one
+// wave's softmax VALU work overlaps the other's MFMAs):
+//   * S^T = K Q^T on v_mfma_f32_16x16x32_bf16 with the KEY on the accumulator row and
+//     the QUERY on the lane: a lane owns one query row, so the online softmax (max, exp2,
+//     sum) runs on lane-local values plus a 4-way cross-lane reduction.
+//   * The probabilities never leave registers: converted to bf16 they ARE the B operand of
+//     O^T = V^T P^T (the key order inside each 32-key MFMA step is permuted identically on
+//     both operands), and O^T keeps the query on the lane, so the online-softmax rescale is
+//     lane-local too (and deferred until a row max grows by 2^8).
+//   * K / V tiles (64 keys) are streamed by LDS-DMA (global_load_lds, 16 B per lane) into a
+//     2-deep ring; 16-B chunks are XOR-swizzled by row on the SOURCE address so the
+//     lane-linear DMA image is read conflict-free by ds_read_b128 (K) and by the
+//     transposing ds_read_b64_tr_b16 (V).  One barrier pair per tile, counted vmcnt.
+//   * Too few query rows to fill 256 CUs (13 objects x 1024 rows = 104 query blocks) ->
+//     the key range is split over workgroups; partial (O, m, l) go to a workspace and a
+//     combine kernel merges them (flash-decoding style).
+#include "common.h"
+
+int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
+void s2h_prof_end(int slot, hipStream_t st);
+
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+#define FL_LOG2E 1.4426950408889634f
+#define FL_LN2 0.6931471805599453f
+#define FL_WAVES 8
+#define FL_QB (FL_WAVES * 16)  // query rows per workgroup
+
+struct FlashArgs {
+  int BH, H, Lq, Lk;
+  const bf16* q; int64_t sqb, sqh, sql;
+  const bf16* k; int64_t skb, skh, skl;
+  const bf16* v; int64_t svb, svh, svl;
+  bf16* o; int64_t sob, soh, sol;
+  float* lse;
+  float sl2;  // scale * log2(e)
+  float p_drop; uint32_t thresh; float inv_keep; uint64_t seed;
+  int splits, tiles_per_split;
+  float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
+  float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
+};
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int DP>
+struct FlashCfg {
+  static constexpr int KT = 64;              // keys per tile
+  static constexpr int ROWB = DP * 2;        // bytes per LDS row (unpadded)
+  static constexpr int NCH = DP / 8;         // 16-B chunks per row
+  static constexpr int RPP = 1024 / ROWB;    // rows per 1-KiB DMA piece
+  static constexpr int TILEB = KT * ROWB;    // bytes per K (or V) tile
+  static constexpr int PIECES = TILEB / 1024;
+  static constexpr int PPW = PIECES / FL_WAVES;  // pieces per wave per operand
+  static constexpr int ND = DP / 16;         // 16-wide d blocks of O^T
+  static constexpr int NT = DP / 32;         // 32-deep d steps of K Q^T
+  static_assert(PPW >= 1, "tile smaller than one DMA piece per wave");
+};
+
+// LDS byte offset of (row, 16-B chunk c) in a swizzled [KT][DP] image
+template <int DP>
+__device__ __forceinline__ int swz(int row, int c) {
+  return row * FlashCfg<DP>::ROWB + ((c ^ (row & (FlashCfg<DP>::NCH - 1))) << 4);
+}
+
+// DMA one K or V tile (keys k0.., rows clamped to [0, Lk)) into a swizzled LDS image
+template <int DP>
+__device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int k0, int Lk, int w, int lane) {
+  using C = FlashCfg<DP>;
+#pragma unroll
+  for (int i = 0; i < C::PPW; ++i) {
+    const int piece = w * C::PPW + i;
+    const int row = piece * C::RPP + lane / C::NCH;
+    const int pos = lane % C::NCH;
+    const int c = pos ^ (row & (C::NCH - 1));
+    const int key = min(k0 + row, Lk - 1);
+    const bf16* g = src + (int64_t)key * ld + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(lds_tile + piece * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+
+template <int DP>
+__global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
+  using C = FlashCfg<DP>;
+  // one LDS array: [2 stages][K tile | V tile]
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int split = blockIdx.z;
+  const int q = blockIdx.x * FL_QB + w * 16 + ql;  // this lane's query row
+  const bf16* Q = a.q + b * a.sqb + h * a.sqh;
+  const bf16* K = a.k + b * a.skb + h * a.skh;
+  const bf16* V = a.v + b * a.svb + h * a.svh;
+  const int ntiles_all = (a.Lk + C::KT - 1) / C::KT;
+  const int t0 = split * a.tiles_per_split;
+  const int t1 = min(ntiles_all, t0 + a.tiles_per_split);
+  const int nt = t1 - t0;
+
+  if (nt > 0) {
+    dma_tile<DP>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+  }
+
+  // Q^T fragments (B operand of K Q^T): lane -> query q, d = 32t + 8g + j
+  bf16x8 qf[C::NT];
+#pragma unroll
+  for (int t = 0; t < C::NT; ++t) {
+    if (q < a.Lq) qf[t] = *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g);
+    else qf[t] = bf16x8{};
+  }
+
+  f32x4 o[C::ND];  // O^T: row d = 16*db + 4g + r, column q
+#pragma unroll
+  for (int d = 0; d < C::ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m = -INFINITY, l = 0.f;
+  const uint64_t drow = ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
+  const int qq = (lane >> 2) & 3, pp = lane & 3;  // transposing-read lane roles
+
+  for (int it = 0; it < nt; ++it) {
+    const int kt = t0 + it;
+    const int k0 = kt * C::KT;
+    char* Kb = smem + (it & 1) * 2 * C::TILEB;
+    char* Vb = Kb + C::TILEB;
+    if (it + 1 < nt) {
+      char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
+      dma_tile<DP>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      // this wave's pieces of tile `it` have landed once all but the 2*PPW just issued retired
+      wait_vmcnt<2 * C::PPW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    // ---- S^T = K Q^T: four 16-key blocks, key = 16*kb + 4g + r on the accumulator row
+    f32x4 s[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int row = kb * 16 + ql;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) {
+        const bf16x8 kf = *(const bf16x8*)(Kb + swz<DP>(row, 4 * t + g));
+        s[kb] = mfma16(kf, qf[t], s[kb]);
+      }
+    }
+    // ---- online softmax (lane-local query row; keys spread over the 4 lane groups)
+    float mx = -INFINITY;
+    if (k0 + C::KT <= a.Lk) {  // full tile (wave-uniform): no key mask
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[kb][r] *= a.sl2;
+          mx = fmaxf(mx, s[kb][r]);
+        }
+    } else {
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = k0 + kb * 16 + 4 * g + r;
+          const float x = key < a.Lk ? s[kb][r] * a.sl2 : -INFINITY;
+          s[kb][r] = x;
+          mx = fmaxf(mx, x);
+        }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    // deferred rescale: keep the running reference max until a row's max grows by more
+    // than 2^8 (p <= 256 stays exact enough in bf16 / fp32)
+    const float mn = (mx > m + 8.f) ? mx : m;
+    const float alpha = (m == -INFINITY) ? (mn == -INFINITY ? 1.f : 0.f) : __builtin_amdgcn_exp2f(m - mn);
+    const float mref = (mn == -INFINITY) ? 0.f : mn;
+    m = mn;
+    float rs = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mref);
+        rs += s[kb][r];
+      }
+    if (a.p_drop > 0.f) {
+      // the 4 keys of a (kb) block are consecutive: two hashes per block when pairs align
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb) {
+        const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
+        bool kp[4];
+        if ((e0 & 1) == 0) {
+          s2h_keep_pair(a.seed, e0 >> 1, a.thresh, kp[0], kp[1]);
+          s2h_keep_pair(a.seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(a.seed, e0 + e, a.thresh);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) s[kb][e] = kp[e] ? s[kb][e] * a.inv_keep : 0.f;
+      }
+    }
+    rs += __shfl_xor(rs, 16);
+    rs += __shfl_xor(rs, 32);
+    l = l * alpha + rs;
+    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+#pragma unroll
+      for (int d = 0; d < C::ND; ++d) o[d] *= alpha;
+    }
+    // P^T as the B operand: 32-key step c, k index 8g + j <-> key 32c + 16(j>>2) + 4g + (j&3)
+    bf16x8 pb[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[c][j] = (bf16)s[2 * c + (j >> 2)][j & 3];
+
+    // ---- O^T += V^T P^T, V^T fragments by transposing LDS reads (same key permutation)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int r0 = 32 * c + 4 * g + qq;
+#pragma unroll
+      for (int d = 0; d < C::ND; ++d) {
+        const int dcol = 16 * d + 4 * pp;  // first of the 4 d this lane addresses
+        const int ch = dcol >> 3, off = (dcol & 7) * 2;
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + swz<DP>(r0, ch) + off));
+        v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + swz<DP>(r0 + 16, ch) + off));
+        v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[d] = mfma16(__builtin_bit_cast(bf16x8, cat), pb[c], o[d]);
+      }
+    }
+    // every wave done reading this stage before it is refilled (LDS reads retired first)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+
+  if (q >= a.Lq) return;
+  if (a.splits == 1) {
+    bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) {
+      bf16 t4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t4[e] = (bf16)(o[d][e] * inv);
+      *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
+    }
+    if (g == 0) a.lse[(int64_t)bh * a.Lq + q] = (m + log2f(l)) * FL_LN2;
+  } else {
+    const int64_t row = (int64_t)split * a.BH * a.Lq + (int64_t)bh * a.Lq + q;
+    float* W = a.ws_o + row * DP;
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) *(float4*)(W + 16 * d + 4 * g) = float4{o[d][0], o[d][1], o[d][2], o[d][3]};
+    if (g == 0) {
+      a.ws_ml[2 * row] = m;
+      a.ws_ml[2 * row + 1] = l;
+    }
+  }
+}
+
+// Merge the key-split partials: one wave per query row, DP/64 columns per lane.
+template <int DP>
+__global__ __launch_bounds__(256) void flash_combine_kernel(FlashArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t rowg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // bh*Lq + q
+  if (rowg >= (int64_t)a.BH * a.Lq) return;
+  const int bh = rowg / a.Lq, q = rowg % a.Lq, b = bh / a.H, h = bh % a.H;
+  const int64_t stride = (int64_t)a.BH * a.Lq;
+  float M = -INFINITY;
+  for (int s = 0; s < a.splits; ++s) M = fmaxf(M, a.ws_ml[2 * (s * stride + rowg)]);
+  const float Mr = M == -INFINITY ? 0.f : M;
+  float L = 0.f;
+  constexpr int PER = DP / 64;
+  float acc[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) acc[j] = 0.f;
+  for (int s = 0; s < a.splits; ++s) {
+    const int64_t r = s * stride + rowg;
+    const float ms = a.ws_ml[2 * r], ls = a.ws_ml[2 * r + 1];
+    const float f = ms == -INFINITY ? 0.f : exp2f(ms - Mr);
+    L += ls * f;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) acc[j] += f * a.ws_o[r * DP + lane * PER + j];
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) O[lane * PER + j] = (bf16)(acc[j] * inv);
+  if (lane == 0) a.lse[rowg] = (Mr + log2f(L)) * FL_LN2;
+}
+
+// Split count: aim at ~3 rounds of 256 workgroups, never fewer than 2 tiles per split.
+static void flash_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
+  const int qblocks = (Lq + FL_QB - 1) / FL_QB;
+  const int base = qblocks * BH;
+  const int ntiles = (Lk + 63) / 64;
+  int s = (768 + base - 1) / base;
+  s = std::max(1, std::min(s, ntiles / 2));
+  tps = (ntiles + s - 1) / s;
+  splits = (ntiles + tps - 1) / tps;
+}
+
+static int g_flash_enabled = 1;
+
+// A/B switch for tests and benchmarks: 0 routes every attention to the generic kernels.
+extern "C" int s2h_attn_config(int flash_enable) {
+  const int prev = g_flash_enabled;
+  g_flash_enabled = flash_enable;
+  return prev;
+}
+
+// eligible: bf16, head_dim exactly 64 / 128 / 256, >= 128 query rows, 16-B aligned rows
+int s2h_flash_eligible(int dt, int Lq, int D) {
+  return g_flash_enabled && dt == S2H_BF16 && (D == 64 || D == 128 || D == 256) && Lq >= 128;
+}
+
+int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
+  int splits, tps;
+  flash_plan(B * H, Lq, Lk, splits, tps);
+  if (splits <= 1) return 0;
+  return (int64_t)splits * B * H * Lq * (D + 2) * 4;
+}
+
+template <int DP>
+static int flash_launch(FlashArgs& a, hipStream_t st) {
+  dim3 grid((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits);
+  hipLaunchKernelGGL((flash_fwd_kernel<DP>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  if (a.splits > 1)
+    hipLaunchKernelGGL((flash_combine_kernel<DP>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0, st,
+                       a);
+  return (int)hipGetLastError();
+}
+
+int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
+                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                  const void* k, int64_t skb, int64_t skh, int64_t skl,
+                  const void* v, int64_t svb, int64_t svh, int64_t svl,
+                  void* o, int64_t sob, int64_t soh, int64_t sol,
+                  float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
+                  hipStream_t st) {
+  FlashArgs a = {};
+  a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
+  a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
+  a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;
+  a.v = (const bf16*)v; a.svb = svb; a.svh = svh; a.svl = svl;
+  a.o = (bf16*)o; a.sob = sob; a.soh = soh; a.sol = sol;
+  a.lse = lse;
+  a.sl2 = scale * FL_LOG2E;
+  a.p_drop = p_drop;
+  a.thresh = (uint32_t)(p_drop * 4294967296.0);
+  a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed;
+  flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
+  const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (D + 2) * 4 : 0;
+  if (need > ws_bytes || (need > 0 && ws == nullptr)) {  // no workspace: one split
+    a.splits = 1;
+    a.tiles_per_split = (Lk + 63) / 64;
+  } else if (a.splits > 1) {
+    a.ws_o = (float*)ws;
+    a.ws_ml = a.ws_o + (int64_t)a.splits * a.BH * Lq * D;
+  }
+  if (D == 256) return flash_launch<256>(a, st);
+  if (D == 128) return flash_launch<128>(a, st);
+  return flash_launch<64>(a, st);
+}

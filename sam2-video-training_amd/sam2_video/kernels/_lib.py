@@ -27,7 +27,9 @@ SIGNATURES = {
     "s2h_version": [],
     "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, F, F, I, P],
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
-    "s2h_attn_fwd":[I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P],
+    "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
+    "s2h_attn_config": [I],
+    "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P, L, P],
     "s2h_attn_bwd": [I, I, I, I, I, I,
                      P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
                      P, L, L, L, P, L, L, L, P, L, L, L,
@@ -79,6 +81,10 @@ SIGNATURES = {
 _LIB = None
 
 
+# entry points that do not return a hipError_t
+RESTYPES = {"s2h_attn_fwd_ws_bytes": c_int64}
+
+
 class HipKernelError(RuntimeError):
     pass
 
@@ -95,7 +101,7 @@ def lib():
         for name, argtypes in SIGNATURES.items():
             fn = getattr(h, name)
             fn.argtypes = argtypes
-            fn.restype = c_int
+            fn.restype = RESTYPES.get(name, c_int)
         _LIB = h
     return _LIB
 

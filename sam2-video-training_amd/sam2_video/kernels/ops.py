@@ -10,7 +10,7 @@ import math
 
 import torch
 
-from ._lib import call
+from ._lib import call, lib
 
 F32, BF16 = 0, 1
 ACT = {None: 0, "none": 0, "relu": 1, "gelu": 2, "sigmoid": 3}
@@ -132,8 +132,11 @@ def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0):
     _dev(q, k, v, o, lse)
     B, Lq, H, D = q.shape
     Lk = k.shape[1]
+    nws = lib().s2h_attn_fwd_ws_bytes(dt(q), B, H, Lq, Lk, D)
+    ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
     call("s2h_attn_fwd", dt(q), B, H, Lq, Lk, D, ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v),
-         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), stream())
+         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), ptr(ws), int(nws),
+         stream())
     return o, lse
 
 

@@ -22,7 +22,7 @@ def _prototypes():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     protos = {}
-    for m in re.finditer(r"\bint\s+(s2h_\w+)\s*\(([^)]*)\)\s*;", text):
+    for m in re.finditer(r"\bint(?:64_t)?\s+(s2h_\w+)\s*\(([^)]*)\)\s*;", text):
         params = [p.strip() for p in m.group(2).split(",")]
         if params == ["void"]:
             params = []

@@ -142,6 +142,44 @@ def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
     _close(dv, vr.grad, 3 * tol)
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,D", [(13, 1, 1024, 7196, 256), (13, 1, 1024, 1024, 256), (2, 2, 1024, 1028, 128),
+                                         (2, 4, 300, 77, 64), (1, 1, 1000, 1031, 256), (3, 1, 128, 40, 256)])
+def test_flash_forward_matches_reference(B, H, Lq, Lk, D):
+    """bf16 long-sequence path (flash.hip): key-split partials + combine, ragged tails."""
+    ops = _ops()
+    torch.manual_seed(4)
+    q = torch.randn(B, Lq, H, D, device=DEV).to(torch.bfloat16)
+    k = torch.randn(B, Lk, H, D, device=DEV).to(torch.bfloat16)
+    v = torch.randn(B, Lk, H, D, device=DEV).to(torch.bfloat16)
+    scale = 1.0 / math.sqrt(D)
+    o = torch.empty_like(q)
+    lse = torch.empty(B, H, Lq, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, scale)
+    ro, rl = _ref_attn(q, k, v, scale)
+    _close(o, ro, 2e-2)
+    _close(lse, rl, 1e-3)
+
+
+def test_flash_dropout_matches_generic_kernel():
+    """Same counter-hash dropout mask in the flash and the generic forward (the backward
+    regenerates it), so both produce the same output up to bf16 rounding."""
+    from sam2_video.kernels._lib import lib
+    ops = _ops()
+    torch.manual_seed(5)
+    B, H, Lq, Lk, D = 2, 1, 256, 700, 256
+    q, k, v = (torch.randn(B, L, H, D, device=DEV).to(torch.bfloat16) for L in (Lq, Lk, Lk))
+    o1, o2 = torch.empty_like(q), torch.empty_like(q)
+    l1, l2 = torch.empty(B, H, Lq, device=DEV), torch.empty(B, H, Lq, device=DEV)
+    ops.attn_fwd(q, k, v, o1, l1, 0.0625, p_drop=0.1, seed=77)
+    prev = lib().s2h_attn_config(0)
+    try:
+        ops.attn_fwd(q, k, v, o2, l2, 0.0625, p_drop=0.1, seed=77)
+    finally:
+        lib().s2h_attn_config(prev)
+    _close(o1, o2, 2e-2)
+    _close(l1, l2, 1e-4)
+
+
 def test_attention_strided_qkv():
     """q/k/v read in place from a fused [B, L, 3, H, d] qkv projection (Hiera)."""
     ops = _ops()
