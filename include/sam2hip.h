@@ -105,7 +105,10 @@ int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  void* o, int64_t sob, int64_t soh, int64_t sol,
                  float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
                  hipStream_t st);
-/* Backward of s2h_attn_fwd; di_ws: fp32 workspace [B*H*Lq]. */
+/* Backward of s2h_attn_fwd; di_ws: fp32 workspace [B*H*Lq].  bf16 with head_dim 128/256
+ * and >= 128 query rows takes the flash path (dQ kernel with key-split fp32 partials in
+ * `ws` of s2h_attn_bwd_ws_bytes(...) bytes, dK/dV kernel per 128-key block). */
+int64_t s2h_attn_bwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D);
 int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                  const void* k, int64_t skb, int64_t skh, int64_t skl,
@@ -115,7 +118,8 @@ int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
                  void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                  void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
-                 const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, hipStream_t st);
+                 const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, void* ws,
+                 int64_t ws_bytes, hipStream_t st);
 
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:

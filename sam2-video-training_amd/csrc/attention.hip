@@ -38,6 +38,20 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sq
                   int64_t svl, void* o, int64_t sob, int64_t soh, int64_t sol, float* lse, float scale, float p_drop,
                   uint64_t seed, void* ws, int64_t ws_bytes, hipStream_t st);
 
+int s2h_flash_bwd_eligible(int dt, int Lq, int D);
+int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D);
+int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                  const void* k, int64_t skb, int64_t skh, int64_t skl, const void* v, int64_t svb, int64_t svh,
+                  int64_t svl, const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout, int64_t sgb,
+                  int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk, int64_t sdkb,
+                  int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl, const float* lse,
+                  float* di_ws, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes, hipStream_t st);
+
+// Workspace the backward wants (key-split dQ partials of the flash path); 0 = none.
+extern "C" int64_t s2h_attn_bwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D) {
+  return s2h_flash_bwd_eligible(dt, Lq, D) ? s2h_flash_bwd_ws_bytes(B, H, Lq, Lk, D) : 0;
+}
+
 // Workspace the forward wants (key-split partials of the flash path); 0 = none.
 extern "C" int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D) {
   return s2h_flash_eligible(dt, Lq, D) ? s2h_flash_ws_bytes(B, H, Lq, Lk, D) : 0;
@@ -533,13 +547,23 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                             void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
                             void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                             void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
-                            const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
-                            hipStream_t st) {
+                            const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, void* ws,
+                            int64_t ws_bytes, hipStream_t st) {
   if (B * H <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
       !attn_aligned(dt, D, v, svb, svh, svl) || !attn_aligned(dt, D, dout, sgb, sgh, sgl))
     return (int)hipErrorInvalidValue;
+  if (s2h_flash_bwd_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol) &&
+      attn_aligned(dt, D, dq, sdqb, sdqh, sdql) && attn_aligned(dt, D, dk, sdkb, sdkh, sdkl) &&
+      attn_aligned(dt, D, dv, sdvb, sdvh, sdvl)) {
+    const int slot = s2h_prof_begin(st, 2, (int64_t)B * H, Lq, Lk, D, 2);
+    const int rc = s2h_flash_bwd(B, H, Lq, Lk, D, q, sqb, sqh, sql, k, skb, skh, skl, v, svb, svh, svl, o, sob, soh,
+                                 sol, dout, sgb, sgh, sgl, dq, sdqb, sdqh, sdql, dk, sdkb, sdkh, sdkl, dv, sdvb, sdvh,
+                                 sdvl, lse, di_ws, scale, p_drop, seed, ws, ws_bytes, st);
+    s2h_prof_end(slot, st);
+    return rc;
+  }
   AttnArgs a = {};
   a.B = B; a.H = H; a.Lq = Lq; a.Lk = Lk; a.D = D;
   a.q = q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;

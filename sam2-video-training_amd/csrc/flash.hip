@@ -18,19 +18,10 @@
 //   * Too few query rows to fill 256 CUs (13 objects x 1024 rows = 104 query blocks) ->
 //     the key range is split over workgroups; partial (O, m, l) go to a workspace and a
 //     combine kernel merges them (flash-decoding style).
-#include "common.h"
+#include "flash_common.h"
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
 void s2h_prof_end(int slot, hipStream_t st);
-
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef short v8i16 __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
-#define FL_LOG2E 1.4426950408889634f
-#define FL_LN2 0.6931471805599453f
-#define FL_WAVES 8
-#define FL_QB (FL_WAVES * 16)  // query rows per workgroup
 
 struct FlashArgs {
   int BH, H, Lq, Lk;
@@ -45,55 +36,6 @@ struct FlashArgs {
   float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
   float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
 };
-
-__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-}
-
-template <int DP>
-struct FlashCfg {
-  static constexpr int KT = 64;              // keys per tile
-  static constexpr int ROWB = DP * 2;        // bytes per LDS row (unpadded)
-  static constexpr int NCH = DP / 8;         // 16-B chunks per row
-  static constexpr int RPP = 1024 / ROWB;    // rows per 1-KiB DMA piece
-  static constexpr int TILEB = KT * ROWB;    // bytes per K (or V) tile
-  static constexpr int PIECES = TILEB / 1024;
-  static constexpr int PPW = PIECES / FL_WAVES;  // pieces per wave per operand
-  static constexpr int ND = DP / 16;         // 16-wide d blocks of O^T
-  static constexpr int NT = DP / 32;         // 32-deep d steps of K Q^T
-  static_assert(PPW >= 1, "tile smaller than one DMA piece per wave");
-};
-
-// LDS byte offset of (row, 16-B chunk c) in a swizzled [KT][DP] image
-template <int DP>
-__device__ __forceinline__ int swz(int row, int c) {
-  return row * FlashCfg<DP>::ROWB + ((c ^ (row & (FlashCfg<DP>::NCH - 1))) << 4);
-}
-
-// DMA one K or V tile (keys k0.., rows clamped to [0, Lk)) into a swizzled LDS image
-template <int DP>
-__device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int k0, int Lk, int w, int lane) {
-  using C = FlashCfg<DP>;
-#pragma unroll
-  for (int i = 0; i < C::PPW; ++i) {
-    const int piece = w * C::PPW + i;
-    const int row = piece * C::RPP + lane / C::NCH;
-    const int pos = lane % C::NCH;
-    const int c = pos ^ (row & (C::NCH - 1));
-    const int key = min(k0 + row, Lk - 1);
-    const bf16* g = src + (int64_t)key * ld + c * 8;
-    __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(lds_tile + piece * 1024),
-                                     16, 0, 0);
-  }
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-}
 
 template <int DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
@@ -113,8 +55,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   const int nt = t1 - t0;
 
   if (nt > 0) {
-    dma_tile<DP>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
-    dma_tile<DP>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP, 64>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP, 64>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
   }
 
   // Q^T fragments (B operand of K Q^T): lane -> query q, d = 32t + 8g + j
@@ -139,8 +81,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     char* Vb = Kb + C::TILEB;
     if (it + 1 < nt) {
       char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
-      dma_tile<DP>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP, 64>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP, 64>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
       // this wave's pieces of tile `it` have landed once all but the 2*PPW just issued retired
       wait_vmcnt<2 * C::PPW>();
     } else {

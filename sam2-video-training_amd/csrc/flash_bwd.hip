@@ -1,0 +1,509 @@
+// Flash attention backward for the long-sequence bf16 attentions (the partner of flash.hip):
+// memory-attention RoPE self / cross attention (transformer.py:275-311, head_dim 256).
+//
+// P is recomputed from Q, K and the forward's LSE; dropout masks are regenerated from the
+// same counter hash.  Three kernels, no atomics:
+//   * Di = rowsum(dO * O)                                 (one wave per query row)
+//   * dQ:  per 128-query block, K / V tiles streamed by LDS-DMA exactly like the forward;
+//          S^T = K Q^T and dP^T = V dO^T keep the query on the lane, so P, dS are
+//          lane-local; dQ^T += K^T dS^T with K^T fragments from transposing LDS reads.
+//          The key range is split over workgroups when the query blocks cannot fill the
+//          chip; fp32 partials are summed (and scaled, cast) by a combine kernel.
+//   * dK / dV: per 128-key block (8 waves x 16 keys, K and V fragments held in registers),
+//          Q / dO tiles of 32 queries streamed by LDS-DMA; S = Q K^T and dP = dO V^T keep
+//          the key on the lane, so P_drop and dS are already the B operands of
+//          dV^T += dO^T P_drop and dK^T += Q^T dS (dO^T / Q^T by transposing reads).
+#include "flash_common.h"
+
+struct FlashBwdArgs {
+  int BH, H, Lq, Lk;
+  const bf16* q; int64_t sqb, sqh, sql;
+  const bf16* k; int64_t skb, skh, skl;
+  const bf16* v; int64_t svb, svh, svl;
+  const bf16* o; int64_t sob, soh, sol;
+  const bf16* g; int64_t sgb, sgh, sgl;  // dO
+  bf16* dq; int64_t sdqb, sdqh, sdql;
+  bf16* dk; int64_t sdkb, sdkh, sdkl;
+  bf16* dv; int64_t sdvb, sdvh, sdvl;
+  const float* lse;  // [BH*Lq] natural log
+  float* di;         // [BH*Lq] rowsum(dO*O)
+  float scale, sl2;
+  float p_drop; uint32_t thresh; float inv_keep; uint64_t seed;
+  int splits, tiles_per_split;
+  float* ws_dq;  // [splits][BH*Lq][DP] fp32 partial dQ (splits > 1)
+};
+
+// ------------------------------------------------------------------ Di
+template <int DP>
+__global__ __launch_bounds__(256) void flash_bwd_di_kernel(FlashBwdArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= (int64_t)a.BH * a.Lq) return;
+  const int bh = row / a.Lq, q = row % a.Lq, b = bh / a.H, h = bh % a.H;
+  const bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
+  const bf16* G = a.g + b * a.sgb + h * a.sgh + (int64_t)q * a.sgl;
+  float s = 0.f;
+  for (int d = lane * 4; d < DP; d += 256) {
+    const uint2 ou = *(const uint2*)(O + d), gu = *(const uint2*)(G + d);
+    const bf16* ob = (const bf16*)&ou;
+    const bf16* gb = (const bf16*)&gu;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s += (float)ob[e] * (float)gb[e];
+  }
+  s = wave_sum(s);
+  if (lane == 0) a.di[row] = s;
+}
+
+// ------------------------------------------------------------------ dQ
+template <int DP>
+__global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
+  using C = FlashCfg<DP, 64>;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][K | V]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int split = blockIdx.z;
+  const int q = blockIdx.x * FL_QB + w * 16 + ql;
+  const bf16* Q = a.q + b * a.sqb + h * a.sqh;
+  const bf16* G = a.g + b * a.sgb + h * a.sgh;
+  const bf16* K = a.k + b * a.skb + h * a.skh;
+  const bf16* V = a.v + b * a.svb + h * a.svh;
+  const int ntiles_all = (a.Lk + C::KT - 1) / C::KT;
+  const int t0 = split * a.tiles_per_split;
+  const int nt = min(ntiles_all, t0 + a.tiles_per_split) - t0;
+
+  if (nt > 0) {
+    dma_tile<DP, 64>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP, 64>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+  }
+  const bool qv = q < a.Lq;
+  bf16x8 qf[C::NT], gf[C::NT];
+#pragma unroll
+  for (int t = 0; t < C::NT; ++t) {
+    qf[t] = qv ? *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g) : bf16x8{};
+    gf[t] = qv ? *(const bf16x8*)(G + (int64_t)q * a.sgl + 32 * t + 8 * g) : bf16x8{};
+  }
+  const float lse2 = qv ? a.lse[(int64_t)bh * a.Lq + q] * FL_LOG2E : 0.f;
+  const float di = qv ? a.di[(int64_t)bh * a.Lq + q] : 0.f;
+  f32x4 acc[C::ND];  // dQ^T: row d = 16*db + 4g + r, column q
+#pragma unroll
+  for (int d = 0; d < C::ND; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const uint64_t drow = ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
+
+  for (int it = 0; it < nt; ++it) {
+    const int k0 = (t0 + it) * C::KT;
+    char* Kb = smem + (it & 1) * 2 * C::TILEB;
+    char* Vb = Kb + C::TILEB;
+    if (it + 1 < nt) {
+      char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
+      dma_tile<DP, 64>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP, 64>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      wait_vmcnt<2 * C::PPW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    wg_barrier();
+
+    f32x4 s[4], dp[4];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int row = kb * 16 + ql;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) {
+        const bf16x8 kf = *(const bf16x8*)(Kb + swz<DP>(row, 4 * t + g));
+        s[kb] = mfma16(kf, qf[t], s[kb]);
+        const bf16x8 vf = *(const bf16x8*)(Vb + swz<DP>(row, 4 * t + g));
+        dp[kb] = mfma16(vf, gf[t], dp[kb]);
+      }
+    }
+    const bool full = k0 + C::KT <= a.Lk;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      bool kp[4] = {true, true, true, true};
+      if (a.p_drop > 0.f) {
+        const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
+        if ((e0 & 1) == 0) {
+          s2h_keep_pair(a.seed, e0 >> 1, a.thresh, kp[0], kp[1]);
+          s2h_keep_pair(a.seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(a.seed, e0 + e, a.thresh);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = full || (k0 + kb * 16 + 4 * g + r < a.Lk);
+        const float p = valid ? __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2) : 0.f;
+        const float dpd = kp[r] ? dp[kb][r] * a.inv_keep : 0.f;
+        s[kb][r] = p * (dpd - di);  // dS (scale applied at the end)
+      }
+    }
+    bf16x8 dsb[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dsb[c][j] = (bf16)s[2 * c + (j >> 2)][j & 3];
+    // dQ^T += K^T dS^T
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int d = 0; d < C::ND; ++d) acc[d] = mfma16(tr_frag_perm<DP>(Kb, 32 * c, 16 * d, lane), dsb[c], acc[d]);
+
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wg_barrier();
+  }
+
+  if (!qv) return;
+  if (a.splits == 1) {
+    bf16* DQ = a.dq + b * a.sdqb + h * a.sdqh + (int64_t)q * a.sdql;
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) {
+      bf16 t4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t4[e] = (bf16)(acc[d][e] * a.scale);
+      *(uint2*)(DQ + 16 * d + 4 * g) = *(const uint2*)t4;
+    }
+  } else {
+    float* W = a.ws_dq + ((int64_t)split * a.BH * a.Lq + (int64_t)bh * a.Lq + q) * DP;
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) *(float4*)(W + 16 * d + 4 * g) = float4{acc[d][0], acc[d][1], acc[d][2], acc[d][3]};
+  }
+}
+
+template <int DP>
+__global__ __launch_bounds__(256) void flash_bwd_dq_combine_kernel(FlashBwdArgs a) {
+  const int64_t rows = (int64_t)a.BH * a.Lq;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;  // 4 consecutive d
+  if (i >= rows * DP) return;
+  const int64_t row = i / DP;
+  const int d = i % DP;
+  float4 s = *(const float4*)(a.ws_dq + i);
+  for (int sp = 1; sp < a.splits; ++sp) {
+    const float4 t = *(const float4*)(a.ws_dq + sp * rows * DP + i);
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  const int bh = row / a.Lq, q = row % a.Lq, b = bh / a.H, h = bh % a.H;
+  bf16 t4[4] = {(bf16)(s.x * a.scale), (bf16)(s.y * a.scale), (bf16)(s.z * a.scale), (bf16)(s.w * a.scale)};
+  *(uint2*)(a.dq + b * a.sdqb + h * a.sdqh + (int64_t)q * a.sdql + d) = *(const uint2*)t4;
+}
+
+// ------------------------------------------------------------------ dK / dV
+template <int DP>
+__global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBwdArgs a) {
+  using C = FlashCfg<DP, 32>;  // 32-query tiles
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][Q | dO]
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int key = blockIdx.x * FL_QB + w * 16 + kl;  // this lane's key (B-operand column)
+  const bool kv = key < a.Lk;
+  const bf16* Q = a.q + b * a.sqb + h * a.sqh;
+  const bf16* G = a.g + b * a.sgb + h * a.sgh;
+  const bf16* K = a.k + b * a.skb + h * a.skh;
+  const bf16* V = a.v + b * a.svb + h * a.svh;
+  const int nt = (a.Lq + C::KT - 1) / C::KT;
+
+  dma_tile<DP, 32>(smem, Q, a.sql, 0, a.Lq, w, lane);
+  dma_tile<DP, 32>(smem + C::TILEB, G, a.sgl, 0, a.Lq, w, lane);
+  bf16x8 kf[C::NT], vf[C::NT];  // B operands: K^T / V^T [k = d][n = key]
+#pragma unroll
+  for (int t = 0; t < C::NT; ++t) {
+    kf[t] = kv ? *(const bf16x8*)(K + (int64_t)key * a.skl + 32 * t + 8 * g) : bf16x8{};
+    vf[t] = kv ? *(const bf16x8*)(V + (int64_t)key * a.svl + 32 * t + 8 * g) : bf16x8{};
+  }
+  f32x4 dk[C::ND], dv[C::ND];  // dK^T / dV^T: row d = 16*db + 4g + r, column key
+#pragma unroll
+  for (int d = 0; d < C::ND; ++d) {
+    dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  const float* LSE = a.lse + (int64_t)bh * a.Lq;
+  const float* DI = a.di + (int64_t)bh * a.Lq;
+
+  for (int it = 0; it < nt; ++it) {
+    const int q0 = it * C::KT;
+    char* Qb = smem + (it & 1) * 2 * C::TILEB;
+    char* Gb = Qb + C::TILEB;
+    // this tile's queries of this lane: q0 + 16*qb + 4g + r  (qb = 0, 1; r = 0..3)
+    float4 lse4[2], di4[2];
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int qr = q0 + 16 * qb + 4 * g;
+      if (qr + 3 < a.Lq && (a.Lq & 3) == 0) {
+        lse4[qb] = *(const float4*)(LSE + qr);
+        di4[qb] = *(const float4*)(DI + qr);
+      } else {
+        float lt[4], dt[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lt[e] = qr + e < a.Lq ? LSE[qr + e] : INFINITY;  // exp2(-inf) = 0: padded queries drop out
+          dt[e] = qr + e < a.Lq ? DI[qr + e] : 0.f;
+        }
+        lse4[qb] = float4{lt[0], lt[1], lt[2], lt[3]};
+        di4[qb] = float4{dt[0], dt[1], dt[2], dt[3]};
+      }
+    }
+    if (it + 1 < nt) {
+      char* Qn = smem + ((it + 1) & 1) * 2 * C::TILEB;
+      dma_tile<DP, 32>(Qn, Q, a.sql, q0 + C::KT, a.Lq, w, lane);
+      dma_tile<DP, 32>(Qn + C::TILEB, G, a.sgl, q0 + C::KT, a.Lq, w, lane);
+      wait_vmcnt<2 * C::PPW>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    wg_barrier();
+
+    f32x4 s[2], dp[2];  // S / dP: row q = 16*qb + 4g + r, column key
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      s[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int row = qb * 16 + kl;
+#pragma unroll
+      for (int t = 0; t < C::NT; ++t) {
+        const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP>(row, 4 * t + g));
+        s[qb] = mfma16(qa, kf[t], s[qb]);
+        const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP>(row, 4 * t + g));
+        dp[qb] = mfma16(ga, vf[t], dp[qb]);
+      }
+    }
+    bf16x8 pdb, dsb;  // B operands over the 32 queries: k index 8g + j <-> q 16(j>>2) + 4g + (j&3)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const float lt[4] = {lse4[qb].x, lse4[qb].y, lse4[qb].z, lse4[qb].w};
+      const float dt[4] = {di4[qb].x, di4[qb].y, di4[qb].z, di4[qb].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qi = q0 + 16 * qb + 4 * g + r;
+        const float p = __builtin_amdgcn_exp2f(s[qb][r] * a.sl2 - lt[r] * FL_LOG2E);
+        bool keep = true;
+        if (a.p_drop > 0.f) keep = s2h_keep(a.seed, ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key, a.thresh);
+        const float pd = keep ? p * a.inv_keep : 0.f;
+        const float dpd = keep ? dp[qb][r] * a.inv_keep : 0.f;
+        pdb[4 * qb + r] = (bf16)pd;
+        dsb[4 * qb + r] = (bf16)(p * (dpd - dt[r]));
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < C::ND; ++d) {
+      dv[d] = mfma16(tr_frag_perm<DP>(Gb, 0, 16 * d, lane), pdb, dv[d]);
+      dk[d] = mfma16(tr_frag_perm<DP>(Qb, 0, 16 * d, lane), dsb, dk[d]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wg_barrier();
+  }
+
+  if (!kv) return;
+  bf16* DK = a.dk + b * a.sdkb + h * a.sdkh + (int64_t)key * a.sdkl;
+  bf16* DV = a.dv + b * a.sdvb + h * a.sdvh + (int64_t)key * a.sdvl;
+#pragma unroll
+  for (int d = 0; d < C::ND; ++d) {
+    bf16 tk[4], tv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tk[e] = (bf16)(dk[d][e] * a.scale);
+      tv[e] = (bf16)dv[d][e];
+    }
+    *(uint2*)(DK + 16 * d + 4 * g) = *(const uint2*)tk;
+    *(uint2*)(DV + 16 * d + 4 * g) = *(const uint2*)tv;
+  }
+}
+
+// dK / dV for head_dim 256: 16-wide MFMAs would need K, V fragments (64) + dK^T, dV^T
+// (128) + S, dP registers beyond 256 per wave, so this form runs one wave per SIMD with
+// the 512-register file: 4 waves x 32 keys on v_mfma_f32_32x32x16_bf16 (also half the LDS
+// operand traffic per FLOP), dK^T / dV^T in 2 x 128 accumulator registers.
+template <int DP>
+__global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a) {
+  constexpr int NWV = 4, QT = 32;
+  using C = FlashCfg<DP, QT, NWV>;
+  constexpr int NT = DP / 16, ND = DP / 32;
+  // [K block: 128 keys][stage][Q | dO] + [stage][wave][lse(32) | Di(32)] (each wave DMAs its
+  // own copy of the row constants).  K lives in LDS (read as the B operand of S = Q K^T),
+  // V in registers: both in registers would leave too few for the rest at 512 per lane.
+  using CK = FlashCfg<DP, NWV * 32, NWV>;
+  constexpr int STAGE = 2 * C::TILEB + NWV * 256;
+  __shared__ __attribute__((aligned(1024))) char smem[CK::TILEB + 2 * STAGE];
+  char* Kblk = smem;
+  char* stages = smem + CK::TILEB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, kl = lane & 31;
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int key = blockIdx.x * (NWV * 32) + w * 32 + kl;
+  const bool kv = key < a.Lk;
+  const bf16* Q = a.q + b * a.sqb + h * a.sqh;
+  const bf16* G = a.g + b * a.sgb + h * a.sgh;
+  const bf16* K = a.k + b * a.skb + h * a.skh;
+  const bf16* V = a.v + b * a.svb + h * a.svh;
+  const int nt = (a.Lq + QT - 1) / QT;
+
+  const float* LSE = a.lse + (int64_t)bh * a.Lq;
+  const float* DI = a.di + (int64_t)bh * a.Lq;
+  // one 4-B-per-lane DMA per stage: lanes 0..31 lse[q0 + lane], lanes 32..63 Di[q0 + lane - 32]
+  auto dma_rows = [&](char* stage, int q0) {
+    const int qi = min(q0 + (lane & 31), a.Lq - 1);
+    const float* src = (lane < 32 ? LSE : DI) + qi;
+    __builtin_amdgcn_global_load_lds((const void*)src,
+                                     (__attribute__((address_space(3))) void*)(stage + 2 * C::TILEB + w * 256), 4, 0, 0);
+  };
+  dma_tile<DP, NWV * 32, NWV>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
+  dma_tile<DP, QT, NWV>(stages, Q, a.sql, 0, a.Lq, w, lane);
+  dma_tile<DP, QT, NWV>(stages + C::TILEB, G, a.sgl, 0, a.Lq, w, lane);
+  dma_rows(stages, 0);
+  bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
+  const int64_t vkey = min(key, a.Lk - 1);
+#pragma unroll
+  for (int t = 0; t < NT; ++t) vf[t] = *(const bf16x8*)(V + vkey * a.svl + 16 * t + 8 * hi);
+  const int krow = w * 32 + kl;  // this lane's key row in the K block
+  f32x16 dk[ND], dv[ND];  // dK^T / dV^T: row d = 32*db + 8(r>>2) + 4hi + (r&3), column key
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    dk[d] = f32x16{};
+    dv[d] = f32x16{};
+  }
+  for (int it = 0; it < nt; ++it) {
+    const int q0 = it * QT;
+    char* Qb = stages + (it & 1) * STAGE;
+    char* Gb = Qb + C::TILEB;
+    const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 256);  // [lse(32) | Di(32)]
+    if (it + 1 < nt) {
+      char* Qn = stages + ((it + 1) & 1) * STAGE;
+      dma_tile<DP, QT, NWV>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
+      dma_tile<DP, QT, NWV>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
+      dma_rows(Qn, q0 + QT);
+      wait_vmcnt<2 * C::PPW + 1>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    wg_barrier();
+
+    f32x16 s = f32x16{}, dp = f32x16{};  // S / dP: row q = 8(r>>2) + 4hi + (r&3), column key
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+      const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP>(kl, 2 * t + hi));
+      const bf16x8 kb = *(const bf16x8*)(Kblk + swz<DP>(krow, 2 * t + hi));
+      s = mfma32(qa, kb, s);
+      const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP>(kl, 2 * t + hi));
+      dp = mfma32(ga, vf[t], dp);
+      if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the fragment prefetch depth
+    }
+    bf16x8 pdb[2], dsb[2];  // 16-query steps c: k index 8hi + j <-> r = 8c + j
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ql = 8 * (r >> 2) + 4 * hi + (r & 3);
+      const int qi = q0 + ql;
+      const float lse_r = rows[ql], di_r = rows[32 + ql];
+      const float p = qi < a.Lq ? __builtin_amdgcn_exp2f(s[r] * a.sl2 - lse_r * FL_LOG2E) : 0.f;
+      bool keep = true;
+      if (a.p_drop > 0.f) keep = s2h_keep(a.seed, ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key, a.thresh);
+      const float pd = keep ? p * a.inv_keep : 0.f;
+      const float dpd = keep ? dp[r] * a.inv_keep : 0.f;
+      pdb[r >> 3][r & 7] = (bf16)pd;
+      dsb[r >> 3][r & 7] = (bf16)(p * (dpd - di_r));
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int d = 0; d < ND; ++d) {
+        dv[d] = mfma32(tr_frag_perm32<DP>(Gb, 16 * c, 32 * d, lane), pdb[c], dv[d]);
+        dk[d] = mfma32(tr_frag_perm32<DP>(Qb, 16 * c, 32 * d, lane), dsb[c], dk[d]);
+        if (d & 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wg_barrier();
+  }
+
+  if (!kv) return;
+  bf16* DK = a.dk + b * a.sdkb + h * a.sdkh + (int64_t)key * a.sdkl;
+  bf16* DV = a.dv + b * a.sdvb + h * a.sdvh + (int64_t)key * a.sdvl;
+#pragma unroll
+  for (int d = 0; d < ND; ++d)
+#pragma unroll
+    for (int G4 = 0; G4 < 4; ++G4) {
+      bf16 tk[4], tv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        tk[e] = (bf16)(dk[d][4 * G4 + e] * a.scale);
+        tv[e] = (bf16)dv[d][4 * G4 + e];
+      }
+      const int d0 = 32 * d + 8 * G4 + 4 * hi;
+      *(uint2*)(DK + d0) = *(const uint2*)tk;
+      *(uint2*)(DV + d0) = *(const uint2*)tv;
+    }
+}
+
+// ------------------------------------------------------------------ host
+static void flash_bwd_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
+  const int base = ((Lq + FL_QB - 1) / FL_QB) * BH;
+  const int ntiles = (Lk + 63) / 64;
+  int s = (512 + base - 1) / base;
+  s = std::max(1, std::min(s, ntiles / 2));
+  tps = (ntiles + s - 1) / s;
+  splits = (ntiles + tps - 1) / tps;
+}
+
+int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D) {
+  int splits, tps;
+  flash_bwd_plan(B * H, Lq, Lk, splits, tps);
+  return splits > 1 ? (int64_t)splits * B * H * Lq * D * 4 : 0;
+}
+
+template <int DP>
+static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
+  const int64_t rows = (int64_t)a.BH * a.Lq;
+  hipLaunchKernelGGL((flash_bwd_di_kernel<DP>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+  hipLaunchKernelGGL((flash_bwd_dq_kernel<DP>), dim3((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits), dim3(FL_WAVES * 64),
+                     0, st, a);
+  if (a.splits > 1)
+    hipLaunchKernelGGL((flash_bwd_dq_combine_kernel<DP>), dim3((unsigned)((rows * DP / 4 + 255) / 256)), dim3(256), 0,
+                       st, a);
+  if constexpr (DP == 256)
+    hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP>), dim3((a.Lk + 127) / 128, a.BH), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP>), dim3((a.Lk + FL_QB - 1) / FL_QB, a.BH), dim3(FL_WAVES * 64), 0, st,
+                       a);
+  return (int)hipGetLastError();
+}
+
+int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
+                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                  const void* k, int64_t skb, int64_t skh, int64_t skl,
+                  const void* v, int64_t svb, int64_t svh, int64_t svl,
+                  const void* o, int64_t sob, int64_t soh, int64_t sol,
+                  const void* dout, int64_t sgb, int64_t sgh, int64_t sgl,
+                  void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
+                  void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
+                  void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
+                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, void* ws,
+                  int64_t ws_bytes, hipStream_t st) {
+  FlashBwdArgs a = {};
+  a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
+  a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
+  a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;
+  a.v = (const bf16*)v; a.svb = svb; a.svh = svh; a.svl = svl;
+  a.o = (const bf16*)o; a.sob = sob; a.soh = soh; a.sol = sol;
+  a.g = (const bf16*)dout; a.sgb = sgb; a.sgh = sgh; a.sgl = sgl;
+  a.dq = (bf16*)dq; a.sdqb = sdqb; a.sdqh = sdqh; a.sdql = sdql;
+  a.dk = (bf16*)dk; a.sdkb = sdkb; a.sdkh = sdkh; a.sdkl = sdkl;
+  a.dv = (bf16*)dv; a.sdvb = sdvb; a.sdvh = sdvh; a.sdvl = sdvl;
+  a.lse = lse; a.di = di_ws;
+  a.scale = scale; a.sl2 = scale * FL_LOG2E;
+  a.p_drop = p_drop;
+  a.thresh = (uint32_t)(p_drop * 4294967296.0);
+  a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed;
+  flash_bwd_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
+  const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * D * 4 : 0;
+  if (need > ws_bytes || (need > 0 && ws == nullptr)) {
+    a.splits = 1;
+    a.tiles_per_split = (Lk + 63) / 64;
+  } else if (a.splits > 1) {
+    a.ws_dq = (float*)ws;
+  }
+  if (D == 256) return flash_bwd_launch<256>(a, st);
+  return flash_bwd_launch<128>(a, st);
+}
+
+// eligible: bf16, head_dim 128 / 256 (32-query DMA tiles need >= 8 KiB), >= 128 query rows
+int s2h_flash_bwd_eligible(int dt, int Lq, int D);
+int s2h_flash_eligible(int dt, int Lq, int D);
+int s2h_flash_bwd_eligible(int dt, int Lq, int D) { return s2h_flash_eligible(dt, Lq, D) && (D == 128 || D == 256); }

@@ -1,0 +1,101 @@
+// Shared pieces of the flash-attention kernels (flash.hip forward, flash_bwd.hip backward):
+// 16x16x32 bf16 MFMA, the XOR-swizzled [rows][DP] LDS image, LDS-DMA of one 64-row tile,
+// counted vmcnt waits.
+#pragma once
+#include "common.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+#define FL_LOG2E 1.4426950408889634f
+#define FL_LN2 0.6931471805599453f
+#define FL_WAVES 8
+#define FL_QB (FL_WAVES * 16)  // query (or key) rows per workgroup
+
+__device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+template <int DP, int ROWS = 64, int NWV = FL_WAVES>
+struct FlashCfg {
+  static constexpr int KT = ROWS;            // rows per streamed tile
+  static constexpr int ROWB = DP * 2;        // bytes per LDS row (unpadded)
+  static constexpr int NCH = DP / 8;         // 16-B chunks per row
+  static constexpr int RPP = 1024 / ROWB;    // rows per 1-KiB DMA piece
+  static constexpr int TILEB = KT * ROWB;    // bytes per tile
+  static constexpr int PIECES = TILEB / 1024;
+  static constexpr int PPW = PIECES / NWV;   // pieces per wave per operand
+  static constexpr int ND = DP / 16;         // 16-wide d blocks
+  static constexpr int NT = DP / 32;         // 32-deep d steps
+  static_assert(PPW >= 1, "tile smaller than one DMA piece per wave");
+};
+
+// LDS byte offset of (row, 16-B chunk c) in a swizzled [rows][DP] image
+template <int DP>
+__device__ __forceinline__ int swz(int row, int c) {
+  return row * (DP * 2) + ((c ^ (row & (DP / 8 - 1))) << 4);
+}
+
+// DMA one tile (rows r0.., clamped to [0, nrows)) into a swizzled LDS image; the chunk
+// permutation is applied to the per-lane SOURCE address (the DMA destination is lane-linear)
+template <int DP, int ROWS, int NWV = FL_WAVES>
+__device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w, int lane) {
+  using C = FlashCfg<DP, ROWS, NWV>;
+#pragma unroll
+  for (int i = 0; i < C::PPW; ++i) {
+    const int piece = w * C::PPW + i;
+    const int row = piece * C::RPP + lane / C::NCH;
+    const int pos = lane % C::NCH;
+    const int c = pos ^ (row & (C::NCH - 1));
+    const int gr = min(r0 + row, nrows - 1);
+    const bf16* g = src + (int64_t)gr * ld + c * 8;
+    __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(lds_tile + piece * 1024),
+                                     16, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void wg_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// 32x32x16 form of the transposing read: A[m = column c0 + (lane & 31)][k = 8hi + j] where
+// k <-> image row  rbase + 4hi + j (j < 4)  and  rbase + 8 + 4hi + (j - 4) (j >= 4), hi = lane >> 5
+// (the row order of a 32x32 accumulator's registers r = 8(j>>2) + ... within a 16-row step).
+template <int DP>
+__device__ __forceinline__ bf16x8 tr_frag_perm32(const char* img, int rbase, int c0, int lane) {
+  const int G = lane >> 4, hi = G >> 1, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int r0 = rbase + 4 * hi + qq;
+  const int dcol = c0 + 16 * (G & 1) + 4 * pp;
+  const int ch = dcol >> 3, off = (dcol & 7) * 2;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP>(r0, ch) + off));
+  v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP>(r0 + 8, ch) + off));
+  v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, cat);
+}
+
+// Transposing fragment read: A[m = column c0 + (lane & 15)][k = 8g + j] of a swizzled image
+// where k <-> image row  rbase + 4g + j (j < 4)  and  rbase + 16 + 4g + (j - 4) (j >= 4).
+template <int DP>
+__device__ __forceinline__ bf16x8 tr_frag_perm(const char* img, int rbase, int c0, int lane) {
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int r0 = rbase + 4 * g + qq;
+  const int dcol = c0 + 4 * pp;
+  const int ch = dcol >> 3, off = (dcol & 7) * 2;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP>(r0, ch) + off));
+  v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP>(r0 + 16, ch) + off));
+  v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, cat);
+}

@@ -145,10 +145,12 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0):
     B, Lq, H, D = q.shape
     Lk = k.shape[1]
     di = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
+    nws = lib().s2h_attn_bwd_ws_bytes(dt(q), B, H, Lq, Lk, D)
+    ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
     call("s2h_attn_bwd", dt(q), B, H, Lq, Lk, D,
          ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
          ptr(dq), *_bhl(dq), ptr(dk), *_bhl(dk), ptr(dv), *_bhl(dv),
-         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), stream())
+         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), ptr(ws), int(nws), stream())
     return dq, dk, dv
 
 

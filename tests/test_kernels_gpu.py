@@ -155,9 +155,17 @@ def test_flash_forward_matches_reference(B, H, Lq, Lk, D):
     o = torch.empty_like(q)
     lse = torch.empty(B, H, Lq, device=DEV)
     ops.attn_fwd(q, k, v, o, lse, scale)
-    ro, rl = _ref_attn(q, k, v, scale)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ro, rl = _ref_attn(qr, kr, vr, scale)
     _close(o, ro, 2e-2)
     _close(lse, rl, 1e-3)
+    do = torch.randn_like(q)
+    ro.backward(do.float())
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale)
+    _close(dq, qr.grad, 4e-2)
+    _close(dk, kr.grad, 4e-2)
+    _close(dv, vr.grad, 4e-2)
 
 
 def test_flash_dropout_matches_generic_kernel():
@@ -171,13 +179,20 @@ def test_flash_dropout_matches_generic_kernel():
     o1, o2 = torch.empty_like(q), torch.empty_like(q)
     l1, l2 = torch.empty(B, H, Lq, device=DEV), torch.empty(B, H, Lq, device=DEV)
     ops.attn_fwd(q, k, v, o1, l1, 0.0625, p_drop=0.1, seed=77)
+    do = torch.randn_like(q)
+    g1 = [torch.empty_like(t) for t in (q, k, v)]
+    g2 = [torch.empty_like(t) for t in (q, k, v)]
+    ops.attn_bwd(q, k, v, o1, do, l1, *g1, 0.0625, p_drop=0.1, seed=77)
     prev = lib().s2h_attn_config(0)
     try:
         ops.attn_fwd(q, k, v, o2, l2, 0.0625, p_drop=0.1, seed=77)
+        ops.attn_bwd(q, k, v, o2, do, l2, *g2, 0.0625, p_drop=0.1, seed=77)
     finally:
         lib().s2h_attn_config(prev)
     _close(o1, o2, 2e-2)
     _close(l1, l2, 1e-4)
+    for a_, b_ in zip(g1, g2):
+        _close(a_, b_, 3e-2)
 
 
 def test_attention_strided_qkv():
