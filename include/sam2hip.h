@@ -74,6 +74,10 @@ int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
              const float* cscale, float drop_p, uint64_t seed,
              float alpha, float beta, int act, hipStream_t stream);
 
+/* A/B switch (tests, benchmarks): glds_enable = 0 keeps every bf16 GEMM on the
+ * register-staged kernel instead of the LDS-DMA one; returns the previous setting. */
+int s2h_gemm_config(int glds_enable);
+
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),
  * db[N] (+)= sum over rows of dy (db may be NULL); `accumulate` 0 overwrites both.
@@ -91,7 +95,7 @@ int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t
  * Hiera attention), transformer.py:243 (two-way decoder attention) and
  * transformer.py:306 (memory-attention RoPE self / cross attention).
  * bf16 with head_dim 64/128/256 and >= 128 query rows takes the flash path
- * (32x32 MFMA, LDS-DMA K/V ring, key range split over workgroups): it wants a
+ * (16x16x32 MFMA, LDS-DMA K/V ring, key range split over workgroups): it wants a
  * device workspace of s2h_attn_fwd_ws_bytes(...) bytes (ws = NULL / too small
  * just disables the key split). */
 int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D);

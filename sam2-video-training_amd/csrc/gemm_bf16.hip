@@ -236,6 +236,219 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
   }
 }
 
+// ======================================================================================
+// LDS-DMA form (the fast path).  Each operand tile is moved global -> LDS by
+// global_load_lds (16 B per lane, no register staging), into a 2-deep ring with ONE
+// barrier per 64-deep K step (the DMA of step k+1 is issued right after the barrier that
+// retires step k, and runs under step k's MFMAs).  The DMA destination is lane-linear, so
+// bank-conflict avoidance is an XOR swizzle of 16-B chunks applied to the per-lane SOURCE
+// address:
+//   K-contiguous operand  -> image [row][64 k] (128-B rows), chunk ^= (row >> 1) & 7,
+//                            fragments by ds_read_b128
+//   row-contiguous operand-> image [64 k][ROWS] (128/256-B rows), chunk ^= 2 * (k & 3),
+//                            fragments by ds_read_b64_tr_b16 (two per fragment)
+// Workgroups are remapped so that consecutive tiles of one row block share an XCD (L2).
+// Requirements (else the register-staged kernel above runs): 16-B aligned bases, row
+// strides and batch strides multiple of 8 elements, the contiguous extent of every
+// operand a multiple of 8.
+template <int ROWS, bool KC>
+struct GImg {
+  static constexpr int BK = 64;
+  static constexpr int RB = KC ? 128 : ROWS * 2;       // bytes per image row
+  static constexpr int BYTES = ROWS * BK * 2;
+  static constexpr int PIECES = BYTES / 1024;          // 1-KiB DMA pieces
+  static constexpr int PPW = PIECES / 4;               // per wave (4 waves)
+  static constexpr int LPR = RB / 16;                  // lanes (16-B chunks) per image row
+  static_assert(PPW >= 1, "tile too small");
+
+  __device__ static __forceinline__ int swz(int r, int c) {
+    return KC ? (c ^ ((r >> 1) & 7)) : (c ^ (2 * (r & 3)));
+  }
+  // DMA rows/k of the tile at (row0, k0); rows >= nrows / k >= kend are clamped to valid
+  // addresses (garbage rows are never stored; the K tail is zeroed in LDS afterwards)
+  __device__ static __forceinline__ void dma(char* img, const bf16* base, int64_t ld_row, int64_t ld_k, int row0, int k0,
+                                            int nrows, int kend, int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+      const int piece = w * PPW + i;
+      const int irow = piece * (1024 / RB) + lane / LPR;  // image row
+      const int c = swz(irow, lane % LPR);                 // logical 16-B chunk held at this slot
+      const bf16* src;
+      if (KC) {
+        const int r = min(row0 + irow, nrows - 1);
+        const int k = k0 + 8 * c < kend ? k0 + 8 * c : k0;
+        src = base + (int64_t)r * ld_row + k;
+      } else {
+        const int k = min(k0 + irow, kend - 1);
+        const int r = row0 + 8 * c < nrows ? row0 + 8 * c : row0;
+        src = base + (int64_t)k * ld_k + r;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+    }
+  }
+  // zero the k >= kvalid part of the image (last K step only)
+  __device__ static __forceinline__ void zero_tail(char* img, int kvalid, int tid) {
+    bf16* e = (bf16*)img;
+    for (int i = tid; i < ROWS * BK; i += 256) {
+      int r, k;
+      if (KC) { r = i / BK; k = i % BK; } else { k = i / ROWS; r = i % ROWS; }
+      if (k < kvalid) continue;
+      const int byte = KC ? r * RB + 16 * swz(r, k >> 3) + 2 * (k & 7) : k * RB + 16 * swz(k, r >> 3) + 2 * (r & 7);
+      e[byte >> 1] = (bf16)0.f;
+    }
+  }
+  // MFMA operand fragment: rows rb..rb+15 of the tile, k step ks (32 deep)
+  __device__ static __forceinline__ bf16x8 frag(const char* img, int rb, int ks, int lane) {
+    const int g = lane >> 4;
+    if (KC) {
+      const int r = rb + (lane & 15);
+      return *(const bf16x8*)(img + r * RB + 16 * swz(r, 4 * ks + g));
+    }
+    const int q = (lane >> 2) & 3, p = lane & 3;
+    const int k = 32 * ks + 8 * g + q;
+    const int col = rb + 4 * p;
+    const char* a0 = img + k * RB + 16 * swz(k, col >> 3) + 2 * (col & 7);
+    const char* a1 = img + (k + 4) * RB + 16 * swz(k + 4, col >> 3) + 2 * (col & 7);
+    v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a0);
+    v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)a1);
+    typedef short v8i16 __attribute__((ext_vector_type(8)));
+    v8i16 cat = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(bf16x8, cat);
+  }
+};
+
+template <int BM, int BN, bool AKC, bool BKC>
+__global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
+  constexpr int BK = 64;
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  using IA = GImg<BM, AKC>;
+  using IB = GImg<BN, BKC>;
+  constexpr int STAGE = IA::BYTES + IB::BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w >> 1, wn = w & 1;
+  // XCD-aware tile order (bijective remap): blocks id, id+8, ... share an XCD; give them
+  // consecutive tiles of one row block so its A tile stays in that XCD's L2
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int xcd = id % 8, qd = nwg / 8, rm = nwg % 8;
+  const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + id / 8;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+  const int bz = blockIdx.z / p.splits, split = blockIdx.z % p.splits;
+  const bf16* A = p.A + (int64_t)bz * p.sA;
+  const bf16* B = p.B + (int64_t)bz * p.sB;
+  const int kbeg = split * p.kchunk;
+  const int kend = min(p.K, kbeg + p.kchunk);
+  const int nk = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_rs = p.rowsum != nullptr && n0 == 0 && tid < BM;
+  float rs = 0.f;
+
+  for (int kt = 0; kt < nk; ++kt) {
+    char* sa = smem + (kt & 1) * STAGE;
+    char* sb = sa + IA::BYTES;
+    if (kt == 0) {
+      IA::dma(sa, A, p.lda_m, p.lda_k, m0, kbeg, p.M, kend, w, lane);
+      IB::dma(sb, B, p.ldb_n, p.ldb_k, n0, kbeg, p.N, kend, w, lane);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) {  // next step's DMA runs under this step's MFMAs
+      char* na = smem + ((kt + 1) & 1) * STAGE;
+      IA::dma(na, A, p.lda_m, p.lda_k, m0, kbeg + (kt + 1) * BK, p.M, kend, w, lane);
+      IB::dma(na + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + 1) * BK, p.N, kend, w, lane);
+    }
+    const int kvalid = kend - (kbeg + kt * BK);
+    if (kvalid < BK) {  // K tail: zero the invalid k of both images (last step only)
+      IA::zero_tail(sa, kvalid, tid);
+      IB::zero_tail(sb, kvalid, tid);
+      __syncthreads();
+    }
+    if (do_rs) {
+#pragma unroll 8
+      for (int k = 0; k < BK; ++k) {
+        const int byte = AKC ? tid * IA::RB + 16 * IA::swz(tid, k >> 3) + 2 * (k & 7)
+                             : k * IA::RB + 16 * IA::swz(k, tid >> 3) + 2 * (tid & 7);
+        rs += (float)*(const bf16*)(sa + byte);
+      }
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 a[MI], b[NI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) a[i] = IA::frag(sa, wm * WM + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = IB::frag(sb, wn * WN + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
+  constexpr int EPLD = WN + 4;
+  static_assert(4 * 16 * EPLD * 4 <= 2 * STAGE, "epilogue staging fits");
+  float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
+    __syncthreads();
+    if (p.splits > 1) {
+      // split-K: one row per instruction, consecutive lanes on consecutive columns (256 B)
+      float* C = (float*)p.C + (int64_t)bz * p.sC;
+      constexpr int RPI = 64 / WN;  // rows per instruction
+      const int col = n0 + wn * WN + lane % WN;
+      for (int rr = lane / WN; rr < 16; rr += RPI) {
+        const int row = m0 + wm * WM + i * 16 + rr;
+        if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
+      }
+    } else {
+      constexpr int CPR = WN / 4, RPP = 64 / CPR;
+      const int c4 = lane % CPR, rg = lane / CPR;
+      for (int ps = 0; ps < 16 / RPP; ++ps) {
+        const int rl = rg + ps * RPP;
+        const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
+        const int row = m0 + wm * WM + i * 16 + rl;
+        if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+static int g_gemm_glds = 1;
+
+// A/B switch (tests, benchmarks): 0 keeps every bf16 GEMM on the register-staged kernel.
+extern "C" int s2h_gemm_config(int glds_enable) {
+  const int prev = g_gemm_glds;
+  g_gemm_glds = glds_enable;
+  return prev;
+}
+
+static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
+  auto al = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
+  const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
+  const int64_t lda = akc ? a.lda_m : a.lda_k, ldb = bkc ? a.ldb_n : a.ldb_k;
+  const int aext = akc ? a.K : a.M, bext = bkc ? a.K : a.N;  // contiguous extents
+  return al(a.A) && al(a.B) && lda % 8 == 0 && ldb % 8 == 0 && aext % 8 == 0 && bext % 8 == 0 &&
+         (batch == 1 || (a.sA % 8 == 0 && a.sB % 8 == 0)) && a.K > 0;
+}
+
 template <int BM, int BN>
 static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * batch;
@@ -268,8 +481,16 @@ static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
   }
   // 4-column output groups: 16-B (f32) / 8-B (bf16) aligned
   a.vecC = ((uintptr_t)a.C % (a.out_f32 ? 16 : 8) == 0) && a.ldc % 4 == 0 && (batch == 1 || a.sC % 4 == 0);
-  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * a.splits);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
+  if (g_gemm_glds && gemm_glds_ok(a, batch)) {
+    dim3 g1(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, batch * a.splits);
+    if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, true, true>), g1, dim3(256), 0, st, a);
+    else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, true, false>), g1, dim3(256), 0, st, a);
+    else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, false, true>), g1, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, false, false>), g1, dim3(256), 0, st, a);
+    return (int)hipGetLastError();
+  }
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * a.splits);
   if (akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, true>), grid, dim3(256), 0, st, a);
   else if (akc && !bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, false>), grid, dim3(256), 0, st, a);
   else if (!akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, false, true>), grid, dim3(256), 0, st, a);

@@ -29,6 +29,7 @@ SIGNATURES = {
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
+    "s2h_gemm_config": [I],
     "s2h_attn_bwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P, L, P],
     "s2h_attn_bwd": [I, I, I, I, I, I,

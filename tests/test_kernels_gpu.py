@@ -59,6 +59,31 @@ def test_linear_fwd_dgrad_wgrad(dtype, tol, M, N, K):
     _close(y, ref + r.float(), tol)
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 768, 256), (300, 264, 200), (4104, 136, 72), (64, 64, 64), (520, 2048, 1032),
+                                   (13312, 256, 2048)])
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+def test_gemm_lds_dma_path(M, N, K, layout):
+    """LDS-DMA GEMM (swizzled images, K tail zeroing, XCD remap) vs torch, every operand layout,
+    plus the fused epilogue (bias, GELU, residual) and fp32 split-K output."""
+    ops = _ops()
+    torch.manual_seed(7)
+    bf = torch.bfloat16
+    a = torch.randn(M, K, device=DEV).to(bf) if layout[0] == "n" else torch.randn(K, M, device=DEV).to(bf).t()
+    b = torch.randn(K, N, device=DEV).to(bf) if layout[1] == "n" else torch.randn(N, K, device=DEV).to(bf).t()
+    ref = a.float() @ b.float()
+    kw = dict(M=M, N=N, K=K, lda_m=a.stride(0), lda_k=a.stride(1), ldb_k=b.stride(0), ldb_n=b.stride(1), ldc=N)
+    out = torch.empty(M, N, device=DEV, dtype=bf)
+    ops.gemm(a, b, out, **kw)
+    _close(out, ref, 1e-2)
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).to(bf)
+    ops.gemm(a, b, out, bias=bias, residual=res, ldr=N, act=2, **kw)
+    _close(out, torch.nn.functional.gelu(ref + bias) + res.float(), 1e-2)
+    o32 = torch.full((M, N), 3.0, device=DEV)
+    ops.gemm(a, b, o32, beta=1.0, **kw)
+    _close(o32, ref + 3.0, 2e-3)
+
+
 @pytest.mark.parametrize("rows,N,K", [(20000, 336, 112), (131072, 112, 336), (13312, 256, 256), (4099, 130, 77)])
 def test_wgrad_split_k(rows, N, K):
     """Weight gradients reduce over 10^4-10^5 rows into few output tiles: the bf16 GEMM
