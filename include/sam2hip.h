@@ -134,10 +134,15 @@ int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
 int s2h_layernorm_fwd(int dt, int rows, int C, const void* x, int64_t ldx, const void* badd, int64_t ldb,
                       int b_bcast, void* xsum, const float* gamma, const float* beta, float eps, void* y,
                       int64_t ldy, float* mean, float* rstd, hipStream_t st);
-/* dx (=, or += when dx_accum), dgamma += , dbeta += (fp32). */
+/* dx = LN'(dy) (+= when dx_accum, or + dres: the residual-stream gradient of the fused
+ * pre-add, so the caller needs no copy), dgamma += , dbeta += (fp32, both or neither).
+ * The weight gradients go through per-block partials in `ws`
+ * (s2h_layernorm_bwd_ws_bytes(dt, rows, C) bytes; may be NULL when dgamma is NULL). */
+int64_t s2h_layernorm_bwd_ws_bytes(int dt, int rows, int C);
 int s2h_layernorm_bwd(int dt, int rows, int C, const void* x, int64_t ldx, const void* dy, int64_t lddy,
                       const float* gamma, const float* mean, const float* rstd, void* dx, int64_t lddx,
-                      int dx_accum, float* dgamma, float* dbeta, hipStream_t st);
+                      int dx_accum, const void* dres, int64_t ldres, float* dgamma, float* dbeta, void* ws,
+                      hipStream_t st);
 
 /* ---------------------------------------------------------------- elementwise / layout
  * out = alpha*a + beta*b (residual adds, sam2_base.py:680-684 no_mem_embed,
@@ -188,6 +193,15 @@ int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* out, int ac
  * (PatchEmbed utils.py:85; MaskDownSampler memory_encoder.py:43). */
 int s2h_im2col(int dt, int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
                const void* x, void* col, hipStream_t st);
+/* Mask down-sampler stage, fused 3x3/2 pad-1 conv + LayerNorm2d(cout) + GELU, NHWC
+ * (memory_encoder.py:17-55 MaskDownSampler.encoder[3i..3i+2] with the SAM2.1 config
+ * kernel_size 3, stride 2, padding 1).  Supported (cin, cout): (1, 4), (4, 16), (16, 64).
+ * x_logit: x is the fp32 high-res mask logits [O, H, W] and the stage applies
+ * sigmoid(x) * scale + shift first (sam2_base.py:742-747).  Weights fp32 [cout, cin, 3, 3].
+ * y [O, ceil(H/2), ceil(W/2), cout]. */
+int s2h_mask_down_stage(int dt, int O, int H, int W, int cin, int cout, const void* x, int x_logit, float scale,
+                        float shift, const float* w, const float* bias, const float* gamma, const float* beta,
+                        float eps, void* y, hipStream_t st);
 /* Depthwise KxK conv, NHWC, fp32 weights [C, K, K] (CXBlock dwconv, memory_encoder.py:84). */
 int s2h_dwconv(int dt, int B, int H, int W, int C, int K, int pad, const void* x, const float* w,
                const float* bias, void* y, hipStream_t st);

@@ -1,0 +1,119 @@
+// Memory-encoder mask down-sampler stage, fused: 3x3 / stride 2 / pad 1 conv +
+// LayerNorm2d (over the output channels) + GELU, NHWC, one thread per output pixel.
+// Replaces MaskDownSampler.encoder[3i .. 3i+2] (memory_encoder.py:17-55:
+// Conv2d(cin, cin*4, 3, 2, 1) -> LayerNorm2d -> GELU; sam2.1_hiera_*.yaml
+// mask_downsampler kernel_size 3, stride 2, padding 1) for the narrow stages
+// (cin 1 -> 4, 4 -> 16, 16 -> 64) where an im2col GEMM wastes the MFMA tile on
+// 4..64 columns and the LayerNorm wastes a wave on 4..64 channels.
+//
+// The first stage can read the decoder's fp32 high-res logits directly and apply
+// the memory-encoder input transform sigmoid(x) * scale + shift
+// (sam2_base.py:742-747, sigmoid_scale_for_mem_enc / sigmoid_bias_for_mem_enc),
+// rounded to the compute dtype as the unfused path stores it; zero padding is
+// applied to the transformed mask (F.conv2d pads its input with zeros).
+//
+// Weights stay in PyTorch order [cout][cin][3][3] (fp32); their indices are wave-
+// uniform compile-time offsets, so they are fetched with scalar loads and used as
+// SGPR operands.  HBM-bound: reads O*H*W*cin, writes O*H/2*W/2*cout elements.
+#include "common.h"
+
+template <typename T, int CIN, int COUT, bool LOGIT>
+__global__ __launch_bounds__(256) void mask_down_kernel(int O, int H, int W, int Ho, int Wo, const void* xin,
+                                                        float scale, float shift, const float* __restrict__ w,
+                                                        const float* __restrict__ bias,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps, T* y) {
+  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t total = (int64_t)O * Ho * Wo;
+  if (p >= total) return;
+  const int ox = (int)(p % Wo);
+  const int64_t t = p / Wo;
+  const int oy = (int)(t % Ho);
+  const int o = (int)(t / Ho);
+  float acc[COUT];
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = 2 * oy - 1 + ky;
+    if (iy < 0 || iy >= H) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = 2 * ox - 1 + kx;
+      if (ix < 0 || ix >= W) continue;
+      const int64_t pix = ((int64_t)o * H + iy) * W + ix;
+      float in[CIN];
+      if constexpr (LOGIT) {
+        const float v = ((const float*)xin)[pix];
+        in[0] = to_f32(from_f32<T>(scale / (1.f + expf(-v)) + shift));
+      } else {
+        const T* xp = (const T*)xin + pix * CIN;
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) in[ci] = to_f32(xp[ci]);
+      }
+#pragma unroll
+      for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+        for (int co = 0; co < COUT; ++co) acc[co] += in[ci] * w[((co * CIN + ci) * 3 + ky) * 3 + kx];
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) s += acc[co];
+  const float mu = s / COUT;
+  float q = 0.f;
+#pragma unroll
+  for (int co = 0; co < COUT; ++co) q += (acc[co] - mu) * (acc[co] - mu);
+  const float rs = 1.f / sqrtf(q / COUT + eps);
+  T* yp = y + p * COUT;
+#pragma unroll
+  for (int co = 0; co < COUT; co += 4) {
+    T r[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) r[j] = from_f32<T>(gelu_erf((acc[co + j] - mu) * rs * gamma[co + j] + beta[co + j]));
+    if constexpr (sizeof(T) == 2) {
+      bf16x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = r[j];
+      *(bf16x4*)(yp + co) = v;
+    } else {
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = r[j];
+      *(f32x4*)(yp + co) = v;
+    }
+  }
+}
+
+template <typename T>
+static int mask_down(int O, int H, int W, int cin, int cout, const void* x, int x_logit, float scale, float shift,
+                     const float* w, const float* b, const float* g, const float* be, float eps, void* y,
+                     hipStream_t st) {
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2 - 3) / 2 + 1
+  const int64_t total = (int64_t)O * Ho * Wo;
+  const dim3 grid((unsigned)((total + 255) / 256)), blk(256);
+  if (cin == 1 && cout == 4 && x_logit)
+    hipLaunchKernelGGL((mask_down_kernel<T, 1, 4, true>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b, g,
+                       be, eps, (T*)y);
+  else if (cin == 1 && cout == 4)
+    hipLaunchKernelGGL((mask_down_kernel<T, 1, 4, false>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b,
+                       g, be, eps, (T*)y);
+  else if (cin == 4 && cout == 16 && !x_logit)
+    hipLaunchKernelGGL((mask_down_kernel<T, 4, 16, false>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b,
+                       g, be, eps, (T*)y);
+  else if (cin == 16 && cout == 64 && !x_logit)
+    hipLaunchKernelGGL((mask_down_kernel<T, 16, 64, false>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b,
+                       g, be, eps, (T*)y);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
+
+extern "C" int s2h_mask_down_stage(int dt, int O, int H, int W, int cin, int cout, const void* x, int x_logit,
+                                   float scale, float shift, const float* w, const float* bias, const float* gamma,
+                                   const float* beta, float eps, void* y, hipStream_t st) {
+  if (O <= 0 || H <= 0 || W <= 0) return 0;
+  if (dt == S2H_BF16)
+    return mask_down<bf16>(O, H, W, cin, cout, x, x_logit, scale, shift, w, bias, gamma, beta, eps, y, st);
+  return mask_down<float>(O, H, W, cin, cout, x, x_logit, scale, shift, w, bias, gamma, beta, eps, y, st);
+}

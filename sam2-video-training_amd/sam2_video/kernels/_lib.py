@@ -37,7 +37,8 @@ SIGNATURES = {
                      P, L, L, L, P, L, L, L, P, L, L, L,
                      P, P, F, F, c_uint64, P, L, P],
     "s2h_layernorm_fwd": [I, I, I, P, L, P, L, I, P, P, P, F, P, L, P, P, P],
-    "s2h_layernorm_bwd": [I, I, I, P, L, P, L, P, P, P, P, L, I, P, P, P],
+    "s2h_layernorm_bwd_ws_bytes": [I, I, I],
+    "s2h_layernorm_bwd": [I, I, I, P, L, P, L, P, P, P, P, L, I, P, L, P, P, P, P],
     "s2h_add": [I, L, P, P, F, F, P, P],
     "s2h_add_bcast": [I, L, L, P, F, P, L, F, P, P],
     "s2h_act_fwd": [I, L, P, I, F, F, P, P],
@@ -55,6 +56,7 @@ SIGNATURES = {
     "s2h_colsum": [I, L, I, P, L, P, I, P],
     "s2h_sum_outer": [I, I, L, P, P, I, P],
     "s2h_im2col": [I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "s2h_mask_down_stage": [I, I, I, I, I, I, P, I, F, F, P, P, P, P, F, P, P],
     "s2h_dwconv": [I, I, I, I, I, I, I, P, P, P, P, P],
     "s2h_convt2": [I, I, I, I, I, P, P, P, P, I, P],
     "s2h_row_gate": [I, L, L, P, P, F, P, I, P],
@@ -84,7 +86,8 @@ _LIB = None
 
 
 # entry points that do not return a hipError_t
-RESTYPES = {"s2h_attn_fwd_ws_bytes": c_int64, "s2h_attn_bwd_ws_bytes": c_int64}
+RESTYPES = {"s2h_attn_fwd_ws_bytes": c_int64, "s2h_attn_bwd_ws_bytes": c_int64,
+            "s2h_layernorm_bwd_ws_bytes": c_int64}
 
 
 class HipKernelError(RuntimeError):

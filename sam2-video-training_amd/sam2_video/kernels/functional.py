@@ -92,8 +92,7 @@ class _LayerNorm(torch.autograd.Function):
         gw, gb = _grad_of(mod.weight), _grad_of(mod.bias)
         dx = None
         if dxsum is not None:
-            dx = dxsum.contiguous().clone()
-            ops.layernorm_bwd(x, dy, mod.weight.detach(), mean, rstd, dx=dx, accumulate=True, dgamma=gw, dbeta=gb)
+            dx = ops.layernorm_bwd(x, dy, mod.weight.detach(), mean, rstd, dres=dxsum.contiguous(), dgamma=gw, dbeta=gb)
         else:
             dx = ops.layernorm_bwd(x, dy, mod.weight.detach(), mean, rstd, dgamma=gw, dbeta=gb)
         dadd = None

@@ -169,12 +169,19 @@ def layernorm_fwd(x, gamma, beta, eps, y=None, add=None, add_bcast=False, xsum=N
     return y, mean, rstd
 
 
-def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dgamma=None, dbeta=None):
+def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dgamma=None, dbeta=None, dres=None):
+    """dx = LN'(dy) (+ dx when accumulate, or + dres); dgamma/dbeta += weight gradients."""
     rows, C = _rows(x)
     if dx is None:
         dx = torch.empty(x.shape, device=x.device, dtype=x.dtype)
+    if dres is not None:
+        assert dres.is_contiguous() and dres.dtype == x.dtype and dres.numel() == x.numel() and not accumulate
+    ws = None
+    if dgamma is not None:
+        nbytes = lib().s2h_layernorm_bwd_ws_bytes(dt(x), rows, C)
+        ws = torch.empty(max(nbytes // 4, 1), device=x.device, dtype=torch.float32)
     call("s2h_layernorm_bwd", dt(x), rows, C, ptr(x), C, ptr(dy), C, ptr(gamma), ptr(mean), ptr(rstd),
-         ptr(dx), C, int(accumulate), ptr(dgamma), ptr(dbeta), stream())
+         ptr(dx), C, int(accumulate), ptr(dres), C, ptr(dgamma), ptr(dbeta), ptr(ws), stream())
     return dx
 
 
@@ -463,3 +470,23 @@ def version():
 
 
 _ = math
+
+
+def mask_down_stage(x, w, bias, gamma, beta, eps, *, logits=None, scale=1.0, shift=0.0, dtype=None):
+    """Fused MaskDownSampler stage: GELU(LN2d(conv3x3/2(x))) on NHWC x [O, H, W, cin];
+    or, with `logits` ([O, H, W] fp32), on sigmoid(logits) * scale + shift (cin = 1)."""
+    cout, cin = w.shape[0], w.shape[1]
+    assert tuple(w.shape[2:]) == (3, 3) and w.dtype == torch.float32 and w.is_contiguous()
+    src = logits if logits is not None else x
+    assert src.is_contiguous()
+    O, H, W = src.shape[0], src.shape[1], src.shape[2]
+    if logits is not None:
+        assert logits.dtype == torch.float32 and cin == 1 and dtype is not None
+    else:
+        assert x.shape[-1] == cin
+        dtype = x.dtype
+    y = torch.empty(O, (H + 1) // 2, (W + 1) // 2, cout, device=src.device, dtype=dtype)
+    call("s2h_mask_down_stage", BF16 if dtype == torch.bfloat16 else F32, O, H, W, cin, cout, ptr(src),
+         int(logits is not None), float(scale), float(shift), ptr(w), ptr(bias), ptr(gamma), ptr(beta), float(eps),
+         ptr(y), stream())
+    return y

@@ -40,11 +40,28 @@ class MaskDownSampler(nn.Module):
         self.encoder = nn.Sequential(*layers)
         self.num_layers = num_layers
 
-    def forward(self, x):
-        """x [O, H, W, 1] compute dtype -> [O, H/16, W/16, embed_dim]"""
-        O = x.shape[0]
+    FUSED = {(1, 4), (4, 16), (16, 64)}  # (cin, cout) of the s2h_mask_down_stage kernel
+
+    def _fused(self, conv):
+        return (self.k, self.s, self.p) == (3, 2, 1) and (conv.in_ch, conv.out_ch) in self.FUSED
+
+    def forward(self, x=None, logits=None, scale=1.0, shift=0.0, dtype=None):
+        """x [O, H, W, 1] compute dtype, or `logits` [O, H, W] fp32 with the memory-encoder
+        input transform sigmoid(logits) * scale + shift fused into the first stage
+        -> [O, H/16, W/16, embed_dim]"""
         for i in range(self.num_layers):
             conv, ln = self.encoder[3 * i], self.encoder[3 * i + 1]
+            if self._fused(conv):
+                x = ops.mask_down_stage(x, conv.weight.detach(), conv.bias.detach(), ln.weight.detach(),
+                                        ln.bias.detach(), ln.eps, logits=logits, scale=scale, shift=shift,
+                                        dtype=dtype)
+                logits = None
+                continue
+            if logits is not None:
+                x = ops.act_fwd(logits, "sigmoid", scale=scale, shift=shift)
+                x = (ops.cast(x, dtype) if dtype != torch.float32 else x).unsqueeze(-1)
+                logits = None
+            O = x.shape[0]
             col, Ho, Wo = ops.im2col(x, self.k, self.k, self.s, self.p)
             y = _lin(col, conv).view(O, Ho, Wo, -1)
             y, _, _ = ops.layernorm_fwd(y, ln.weight.detach(), ln.bias.detach(), ln.eps)
@@ -93,11 +110,12 @@ class MemoryEncoder(nn.Module):
         self.out_dim = out_dim
 
     @torch.no_grad()
-    def forward(self, pix_feat, masks, h, w):
-        """pix_feat [h*w, C] raw frame features (shared by objects); masks [O, H, W, 1] (already
-        sigmoid-scaled) -> (features [O, h, w, out_dim], pos table [h*w, out_dim])"""
+    def forward(self, pix_feat, masks, h, w, scale=1.0, shift=0.0):
+        """pix_feat [h*w, C] raw frame features (shared by objects); masks [O, H, W] fp32 mask
+        logits, transformed as sigmoid(masks) * scale + shift inside the first down-sampler stage
+        -> (features [O, h, w, out_dim], pos table [h*w, out_dim])"""
         O = masks.shape[0]
-        m = self.mask_downsampler(masks)  # [O, h, w, C]
+        m = self.mask_downsampler(logits=masks, scale=scale, shift=shift, dtype=pix_feat.dtype)  # [O, h, w, C]
         p = _lin(pix_feat.detach(), self.pix_feat_proj)  # [h*w, C]
         x = ops.add_bcast(m, p)
         x = self.fuser(x)

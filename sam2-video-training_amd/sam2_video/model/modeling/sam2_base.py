@@ -246,11 +246,9 @@ class SAM2Base(nn.Module):
         + no-object spatial embedding where the object is predicted absent."""
         h = w = self.sam_image_embedding_size
         with torch.no_grad():
-            m = ops.act_fwd(high_res.detach(), "sigmoid", scale=self.sigmoid_scale_for_mem_enc,
-                            shift=self.sigmoid_bias_for_mem_enc)
-            m = ops.cast(m, feat.dtype) if feat.dtype != torch.float32 else m
-            m = m.view(num_objects, self.image_size, self.image_size, 1)
-            mfeat, mpos = self.memory_encoder(feat, m, h, w)
+            m = high_res.detach().view(num_objects, self.image_size, self.image_size)
+            mfeat, mpos = self.memory_encoder(feat, m, h, w, scale=self.sigmoid_scale_for_mem_enc,
+                                              shift=self.sigmoid_bias_for_mem_enc)
             if self.no_obj_embed_spatial is not None:
                 mfeat = ops.gate_mix(mfeat.view(num_objects, -1), score.view(-1).contiguous(),
                                      self.no_obj_embed_spatial._s2h_compute.view(-1)).view(mfeat.shape)
