@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames of the CPU baseline sample clip")
     ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="launch every kernel from Python each step instead of replaying the captured HIP graph")
     ap.add_argument("--kernel-table", action="store_true",
                     help="after timing, profile one extra step and print per-shape GEMM/attention TF/s to stderr")
     return ap.parse_args()
@@ -60,10 +62,12 @@ def attention_roofline(records):
     flops = sum(4.0 * m[0] * m[1] * m[2] * m[3] for _, m in sel)
     ms = sum(t for t, _ in sel)
     n = len(sel)
+    if ms <= 0.0:
+        return None
     achieved = flops / (ms * 1e-3) / 1e12
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-            "kernel": "attn_fwd_kernel<bf16,256> (memory-attention cross-attention)",
+            "kernel": "flash_fwd_kernel<256> (memory-attention cross-attention, bf16)",
             "launches": n, "avg_launch_ms": round(ms / n, 4),
             "flops_per_launch_avg": flops / n}
 
@@ -155,7 +159,8 @@ def main():
     module = SAM2LightningModule(model, loss_cfg, opt_cfg, {"enabled": True, "num_cycles": 0.5})
     module.setup("fit", device)
     total = args.warmup + args.steps
-    runner = StepRunner(module, total_steps=total, distributed=world > 1)
+    graph = not args.no_graph
+    runner = StepRunner(module, total_steps=total, distributed=world > 1, graph=graph)
 
     # synthetic clips, resident in HBM before timing (clip index = rank + k * world)
     batches = []
@@ -167,7 +172,7 @@ def main():
     for k in range(args.warmup):
         runner(batches[k])
     torch.cuda.synchronize()
-    if not args.no_prof:
+    if not args.no_prof and not graph:
         _lib.call("s2h_prof_enable", 8192)
     if world > 1:
         dist.barrier()
@@ -187,14 +192,28 @@ def main():
 
     roof = None
     if not args.no_prof:
+        if graph:
+            # HIP events cannot time kernels inside a replayed graph (ROCm 7.2 rejects external
+            # event nodes in capture): time the same kernels in one eager step right after the
+            # timed region, each launch bracketed by events on its own stream
+            _lib.call("s2h_prof_enable", 8192)
+            runner.graph = False
+            runner(batches[-1])
+            runner.graph = True
+            torch.cuda.synchronize()
         recs = read_prof(_lib)
         _lib.call("s2h_prof_enable", 0)
         roof = attention_roofline([(ms, m[1:]) for ms, m in recs if m[0] == 1])
+        if roof is not None:
+            roof["timing"] = ("HIP events per launch, one eager step after the timed graph replays" if graph
+                              else "HIP events per launch over the timed region")
         if args.kernel_table:
             # one extra (untimed) step with every GEMM / attention launch recorded
             _lib.call("s2h_prof_enable", 16384)
             _lib.call("s2h_prof_select", 7)
+            runner.graph = False  # one eager step: every launch bracketed by its own events
             runner(batches[-1])
+            runner.graph = graph
             torch.cuda.synchronize()
             table = kernel_table(read_prof(_lib))
             _lib.call("s2h_prof_enable", 0)

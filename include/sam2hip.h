@@ -35,6 +35,12 @@ enum { S2H_ACT_NONE = 0, S2H_ACT_RELU = 1, S2H_ACT_GELU = 2, S2H_ACT_SIGMOID = 3
 /* ---------------------------------------------------------------- library */
 /* ABI version (1). */
 int s2h_version(void);
+/* Bind a device-resident uint64 RNG offset (NULL unbinds).  Every dropout site
+ * (s2h_gemm epilogue, s2h_attn_fwd/bwd, s2h_dropout) folds its current value into
+ * the seed it was launched with, at kernel start: a captured HIP graph of the step
+ * replays with fresh dropout masks (memory_attention.py:40-48, transformer.py:304-306
+ * dropout_p) once the host advances the offset between replays; 0 = unchanged seed. */
+int s2h_rng_bind(const void* dev_u64);
 /* In-library launch profiler: `cap` > 0 pre-creates `cap` HIP event pairs and
  * brackets every launch of a selected kind on the stream it is launched on; 0 disables. */
 int s2h_prof_enable(int cap);

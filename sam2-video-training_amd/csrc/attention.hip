@@ -26,6 +26,7 @@ struct AttnArgs {
   float scale;
   float p_drop;
   uint64_t seed;
+  const uint64_t* seed_off;
 };
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
@@ -107,6 +108,7 @@ __device__ __forceinline__ typename Mfma<T>::frag frag_global(const T* base, int
 // ------------------------------------------------------------------ forward
 template <typename T, int DP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using MF = Mfma<T>;
   constexpr int BKEY = AttnCfg<T>::BKEY;
   constexpr int VEC = 16 / sizeof(T);
@@ -252,6 +254,7 @@ __global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs a) {
 // ------------------------------------------------------- backward: dQ
 template <typename T, int DP>
 __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using MF = Mfma<T>;
   constexpr int BKEY = AttnCfg<T>::BKEY;
   constexpr int VEC = 16 / sizeof(T);
@@ -351,6 +354,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
 // ------------------------------------------------------ backward: dK, dV
 template <typename T, int DP>
 __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(AttnArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using MF = Mfma<T>;
   constexpr int NW = AttnCfg<T>::NW_DKV;
   constexpr int NT = NW * 64;
@@ -534,7 +538,7 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.k = k; a.skb = skb; a.skh = skh; a.skl = skl;
   a.v = v; a.svb = svb; a.svh = svh; a.svl = svl;
   a.o = o; a.sob = sob; a.soh = soh; a.sol = sol;
-  a.lse = lse; a.scale = scale; a.p_drop = p_drop; a.seed = seed;
+  a.lse = lse; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   return dt == S2H_BF16 ? attn_dispatch<bf16, true>(a, st) : attn_dispatch<float, true>(a, st);
 }
 
@@ -574,6 +578,6 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.dq = dq; a.sdqb = sdqb; a.sdqh = sdqh; a.sdql = sdql;
   a.dk = dk; a.sdkb = sdkb; a.sdkh = sdkh; a.sdkl = sdkl;
   a.dv = dv; a.sdvb = sdvb; a.sdvh = sdvh; a.sdvl = sdvl;
-  a.lse = (float*)lse; a.di = di_ws; a.scale = scale; a.p_drop = p_drop; a.seed = seed;
+  a.lse = (float*)lse; a.di = di_ws; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   return dt == S2H_BF16 ? attn_dispatch<bf16, false>(a, st) : attn_dispatch<float, false>(a, st);
 }

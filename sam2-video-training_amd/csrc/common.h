@@ -107,6 +107,18 @@ __device__ __forceinline__ void s2h_keep_pair(uint64_t seed, uint64_t pair, uint
   k1 = (h >> 16) >= (thresh >> 16);
 }
 
+// Device-resident RNG offset.  The host binds one uint64 in device memory with s2h_rng_bind;
+// every dropout site folds its value into the per-launch seed when the kernel starts, so a
+// captured HIP graph replays with fresh dropout masks after the host advances the offset
+// (forward and backward of one step read the same value, so the backward regenerates the
+// forward's masks).  Offset 0 (or nothing bound) leaves the seed unchanged.
+const uint64_t* s2h_rng_offset_ptr();  // host side (runtime.hip)
+__device__ __forceinline__ uint64_t s2h_seed(uint64_t seed, const uint64_t* off) {
+  if (!off) return seed;
+  const uint64_t o = *off;
+  return o ? seed ^ (o * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) : seed;
+}
+
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
   float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));

@@ -105,7 +105,9 @@ extern "C" int s2h_cast(int dt_in, int dt_out, int64_t n, const void* x, void* y
 // ---------------------------------------------------------------- dropout
 // mode 0: out = a + keep(i)*b/(1-p)     mode 1: out = keep(i)*b/(1-p)   (also the backward)
 template <typename T>
-__global__ void dropout_kernel(int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out) {
+__global__ void dropout_kernel(int64_t n, const void* a, const void* b, float p, uint64_t seed, const uint64_t* seed_off,
+                               void* out) {
+  seed = s2h_seed(seed, seed_off);
   const uint32_t thresh = (uint32_t)(p * 4294967296.0);
   const float inv = 1.f / (1.f - p);
   GRID_STRIDE(i, n) {
@@ -117,7 +119,7 @@ __global__ void dropout_kernel(int64_t n, const void* a, const void* b, float p,
 extern "C" int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out,
                            hipStream_t st) {
   if (n <= 0) return 0;
-  DISPATCH_T(dt, dropout_kernel, ew_grid(n), n, a, b, p, seed, out);
+  DISPATCH_T(dt, dropout_kernel, ew_grid(n), n, a, b, p, seed, s2h_rng_offset_ptr(), out);
   return (int)hipGetLastError();
 }
 

@@ -31,7 +31,7 @@ struct FlashArgs {
   bf16* o; int64_t sob, soh, sol;
   float* lse;
   float sl2;  // scale * log2(e)
-  float p_drop; uint32_t thresh; float inv_keep; uint64_t seed;
+  float p_drop; uint32_t thresh; float inv_keep; uint64_t seed; const uint64_t* seed_off;
   int splits, tiles_per_split;
   float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
   float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
@@ -39,6 +39,7 @@ struct FlashArgs {
 
 template <int DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using C = FlashCfg<DP>;
   // one LDS array: [2 stages][K tile | V tile]
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];
@@ -307,6 +308,7 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
   a.thresh = (uint32_t)(p_drop * 4294967296.0);
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed;
+  a.seed_off = s2h_rng_offset_ptr();
   flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
   const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (D + 2) * 4 : 0;
   if (need > ws_bytes || (need > 0 && ws == nullptr)) {  // no workspace: one split

@@ -28,7 +28,7 @@ struct FlashBwdArgs {
   const float* lse;  // [BH*Lq] natural log
   float* di;         // [BH*Lq] rowsum(dO*O)
   float scale, sl2;
-  float p_drop; uint32_t thresh; float inv_keep; uint64_t seed;
+  float p_drop; uint32_t thresh; float inv_keep; uint64_t seed; const uint64_t* seed_off;
   int splits, tiles_per_split;
   float* ws_dq;  // [splits][BH*Lq][DP] fp32 partial dQ (splits > 1)
 };
@@ -57,6 +57,7 @@ __global__ __launch_bounds__(256) void flash_bwd_di_kernel(FlashBwdArgs a) {
 // ------------------------------------------------------------------ dQ
 template <int DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using C = FlashCfg<DP, 64>;
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][K | V]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_combine_kernel(FlashBwdArgs 
 // ------------------------------------------------------------------ dK / dV
 template <int DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBwdArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using C = FlashCfg<DP, 32>;  // 32-query tiles
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][Q | dO]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
@@ -315,6 +317,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
 // operand traffic per FLOP), dK^T / dV^T in 2 x 128 accumulator registers.
 template <int DP>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   constexpr int NWV = 4, QT = 32;
   using C = FlashCfg<DP, QT, NWV>;
   constexpr int NT = DP / 16, ND = DP / 32;
@@ -491,6 +494,7 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
   a.thresh = (uint32_t)(p_drop * 4294967296.0);
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed;
+  a.seed_off = s2h_rng_offset_ptr();
   flash_bwd_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
   const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * D * 4 : 0;
   if (need > ws_bytes || (need > 0 && ws == nullptr)) {

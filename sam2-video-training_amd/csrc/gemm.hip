@@ -20,7 +20,7 @@ struct GemmArgs {
   void* X; int64_t ldx, sX;  // aux: aux_mode 1 stores pre-activation, 2 multiplies by act'(X)
   int aux_mode;
   const float* cscale;        // optional per-column scale applied after the activation
-  float drop_p; uint64_t seed; // optional dropout after the activation (index = row*N + col)
+  float drop_p; uint64_t seed; const uint64_t* seed_off; // optional dropout after the activation (index = row*N + col)
   float alpha, beta; int act;
   int vecA, vecB;
 };
@@ -77,6 +77,7 @@ struct TileLoader {
 
 template <typename T, typename TC, int BM, int BN, bool AKC, bool BKC>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
+  if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
   constexpr int BK = 32;
   constexpr int VEC = 16 / sizeof(T);
   constexpr int LS = BK + VEC;  // LDS row stride (elements): +16 B pad
@@ -199,7 +200,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   a.bias = bias; a.bias_mode = bias ? bias_mode : 0;
   a.R = R; a.ldr = ldr; a.sR = sR;
   a.X = X; a.ldx = ldx; a.sX = sX; a.aux_mode = X ? aux_mode : 0;
-  a.cscale = cscale; a.drop_p = drop_p; a.seed = seed;
+  a.cscale = cscale; a.drop_p = drop_p; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   a.alpha = alpha; a.beta = beta; a.act = act;
   const int esz = dt_ab == S2H_BF16 ? 2 : 4;
   const int vec = 16 / esz;
@@ -227,7 +228,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   b.bias = a.bias; b.bias_mode = a.bias_mode;
   b.R = R; b.ldr = ldr; b.sR = sR;
   b.X = X; b.ldx = ldx; b.sX = sX; b.aux_mode = a.aux_mode;
-  b.cscale = cscale; b.drop_p = drop_p; b.seed = seed;
+  b.cscale = cscale; b.drop_p = drop_p; b.seed = seed; b.seed_off = s2h_rng_offset_ptr();
   b.alpha = alpha; b.beta = beta; b.act = act;
   b.vecA = a.vecA; b.vecB = a.vecB;
   b.out_f32 = dt_c == S2H_F32;

@@ -146,6 +146,7 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
 
 template <int BM, int BN, bool AKC, bool BKC>
 __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
+  if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
   using SA = Stage16<BM, BK, AKC>;
@@ -320,6 +321,7 @@ struct GImg {
 
 template <int BM, int BN, bool AKC, bool BKC>
 __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
+  if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
   constexpr int BK = 64;
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
   using IA = GImg<BM, AKC>;

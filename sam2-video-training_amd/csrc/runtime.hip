@@ -13,6 +13,15 @@
 extern "C" int s2h_version() { return 1; }
 
 namespace {
+const uint64_t* g_rng_off = nullptr;
+}
+extern "C" int s2h_rng_bind(const void* dev_u64) {
+  g_rng_off = (const uint64_t*)dev_u64;
+  return 0;
+}
+const uint64_t* s2h_rng_offset_ptr() { return g_rng_off; }
+
+namespace {
 struct ProfRec { hipEvent_t a, b; int64_t meta[6]; };
 std::mutex g_mu;
 std::vector<ProfRec> g_pool;
@@ -40,19 +49,27 @@ extern "C" int s2h_prof_count() { std::lock_guard<std::mutex> lk(g_mu); return g
 // internal: returns slot index or -1
 extern "C" int s2h_prof_select(int mask) { std::lock_guard<std::mutex> lk(g_mu); g_mask = mask; return 0; }
 
+// Launches on a capturing stream are not profiled: an event recorded there is only an
+// intra-graph dependency, and hipEventRecordExternal is rejected in capture on ROCm 7.2.
+static bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(st, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+static void record(hipEvent_t ev, hipStream_t st) { (void)hipEventRecord(ev, st); }
+
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4) {
-  if (!g_on || !(g_mask & kind)) return -1;
+  if (!g_on || !(g_mask & kind) || capturing(st)) return -1;
   std::lock_guard<std::mutex> lk(g_mu);
   if (g_used >= (int)g_pool.size()) return -1;
   int i = g_used++;
   int64_t* m = g_pool[i].meta;
   m[0] = kind; m[1] = m0; m[2] = m1; m[3] = m2; m[4] = m3; m[5] = m4;
-  (void)hipEventRecord(g_pool[i].a, st);
+  record(g_pool[i].a, st);
   return i;
 }
 void s2h_prof_end(int slot, hipStream_t st) {
   if (slot < 0) return;
-  (void)hipEventRecord(g_pool[slot].b, st);
+  record(g_pool[slot].b, st);
 }
 
 // ms[i] = duration of record i; meta[6*i..] = (kind, shape[5]). Synchronises on the events.

@@ -25,6 +25,7 @@ F = c_float
 # name -> argtypes (restype is int: a hipError_t value, 0 == success)
 SIGNATURES = {
     "s2h_version": [],
+    "s2h_rng_bind": [P],
     "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, F, F, I, P],
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],

@@ -38,6 +38,24 @@ def _dev(*ts):
             raise RuntimeError("libsam2hip kernels run on the GPU only (tensor on %s)" % t.device)
 
 
+_RNG_OFFSET = {}
+
+
+def rng_offset(device):
+    """The device-resident uint64 dropout offset bound into libsam2hip (s2h_rng_bind): one per
+    process, never freed (the library keeps its address).  Write it before a step (a fill
+    kernel, no host sync) to draw fresh dropout masks, also on a replayed HIP graph."""
+    t = _RNG_OFFSET.get("t")
+    if t is None:
+        t = torch.zeros(1, dtype=torch.int64, device=device)
+        call("s2h_rng_bind", t.data_ptr())
+        _RNG_OFFSET["t"] = t
+    elif t.device.index != (torch.device(device).index if torch.device(device).index is not None
+                            else torch.cuda.current_device()):
+        raise RuntimeError(f"rng offset already bound on {t.device}, requested {device}")
+    return t
+
+
 # ----------------------------------------------------------------- GEMM
 def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB=0, sC=0,
          bias=None, bias_mode=1, residual=None, ldr=0, sR=0, aux=None, ldx=0, sX=0, aux_mode=0,

@@ -74,7 +74,15 @@ class PositionEmbeddingRandom(nn.Module):
         self.register_buffer("positional_encoding_gaussian_matrix", scale * torch.randn((2, num_pos_feats)))
 
     def _gauss_cpu(self):
-        return self.positional_encoding_gaussian_matrix.detach().float().cpu()
+        """host copy of the (never-trained) gaussian matrix, refreshed only when the buffer is
+        replaced or written: the dense-PE lookup runs inside the captured step, where a
+        device->host copy is not allowed"""
+        b = self.positional_encoding_gaussian_matrix
+        key = (b.data_ptr(), b._version, str(b.device))
+        if getattr(self, "_gauss_key", None) != key:
+            self._gauss_host = b.detach().float().cpu()
+            self._gauss_key = key
+        return self._gauss_host
 
     def dense_table(self, h, w, device, dtype):
         """get_dense_pe (prompt_encoder.py:68-77) as [h*w, C] rows (NHWC)"""

@@ -176,11 +176,13 @@ class SAM2Model(SAM2Base):
         out = merge_object_results_to_category(stages, backbone_out["obj_to_cat"], backbone_out["num_categories"])
         return out, backbone_out["obj_to_cat"]
 
-    def prepare_prompt_inputs(self, backbone_out, input, start_frame_idx=0):
-        """sam2model.py:181-236 -- frame-0 category masks -> objects -> clicks (host side)"""
+    def host_prompt_plan(self, input, start_frame_idx=0) -> Dict[str, Any]:
+        """Host half of prepare_prompt_inputs (sam2model.py:181-236): frame-0 category masks ->
+        objects (opening + connected components) -> clicks -> point encodings.  Pure CPU work on
+        the batch's host copy of frame 0 (no device sync); the captured (graphed) step takes its
+        result as input."""
         hm = getattr(input, "host_masks0", None) if start_frame_idx == 0 else None
         masks0 = (hm if hm is not None else input.masks[start_frame_idx]).unsqueeze(1)
-        # host-side work (runs while the GPU executes the already-queued image encoder)
         obj_masks, obj_to_cat, num_categories = utils.cat_to_obj_mask(masks0)
         if self.prompt_type == "box":
             points, labels = utils.generate_box_prompt(obj_masks)
@@ -188,20 +190,38 @@ class SAM2Model(SAM2Base):
             points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
                                                          num_neg_points=self.num_neg_points,
                                                          include_center=self.include_center)
-        backbone_out["num_frames"] = input.num_frames
-        backbone_out["obj_to_cat"] = obj_to_cat
-        backbone_out["num_categories"] = num_categories
         O = len(obj_to_cat)
-        dev = self.arena.device
         pe0, lab0 = self.sam_prompt_encoder.host_points(points, labels, pad=True)
         pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
                                                         pad=True)
-        # pinned staging so the uploads are asynchronous w.r.t. the queued GPU work
-        backbone_out["prompt_cond"] = (pe0.pin_memory().to(dev, non_blocking=True),
-                                       lab0.pin_memory().to(dev, non_blocking=True))
-        backbone_out["prompt_pad"] = (pe1.pin_memory().to(dev, non_blocking=True),
-                                      lab1.pin_memory().to(dev, non_blocking=True))
-        backbone_out["point_inputs_per_frame"] = {start_frame_idx: {"point_coords": points, "point_labels": labels}}
+        return {"start_frame_idx": start_frame_idx, "obj_to_cat": obj_to_cat, "num_categories": num_categories,
+                "points": points, "labels": labels, "host": (pe0, lab0, pe1, lab1)}
+
+    @staticmethod
+    def upload_prompt_plan(plan, device, out=None):
+        """host tensors of a plan -> device (pinned staging, asynchronous); into `out` when given"""
+        host = [t.pin_memory() for t in plan["host"]]
+        if out is None:
+            return tuple(t.to(device, non_blocking=True) for t in host)
+        for d, h in zip(out, host):
+            d.copy_(h, non_blocking=True)
+        return out
+
+    def prepare_prompt_inputs(self, backbone_out, input, start_frame_idx=0):
+        """sam2model.py:181-236 -- frame-0 category masks -> objects -> clicks.  A batch that carries
+        `prompt_plan` (with `dev` tensors already on the device: the graphed step) skips the host
+        work; otherwise it runs here, while the GPU executes the already-queued image encoder."""
+        plan = getattr(input, "prompt_plan", None)
+        if plan is None or plan.get("start_frame_idx", 0) != start_frame_idx:
+            plan = self.host_prompt_plan(input, start_frame_idx)
+        dev = plan.get("dev") or self.upload_prompt_plan(plan, self.arena.device)
+        backbone_out["num_frames"] = input.num_frames
+        backbone_out["obj_to_cat"] = plan["obj_to_cat"]
+        backbone_out["num_categories"] = plan["num_categories"]
+        backbone_out["prompt_cond"] = (dev[0], dev[1])
+        backbone_out["prompt_pad"] = (dev[2], dev[3])
+        backbone_out["point_inputs_per_frame"] = {start_frame_idx: {"point_coords": plan["points"],
+                                                                    "point_labels": plan["labels"]}}
         backbone_out["mask_inputs_per_frame"] = {}
         return backbone_out
 

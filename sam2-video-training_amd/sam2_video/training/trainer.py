@@ -140,33 +140,110 @@ class SAM2LightningModule(nn.Module):
 
 class StepRunner:
     """One optimizer step of the fit loop: zero grads -> training_step -> backward ->
-    (RCCL all-reduce) -> clip + AdamW (+ schedule).  Everything stays on the device."""
+    (RCCL all-reduce) -> clip + AdamW (+ schedule).  Everything stays on the device.
 
-    def __init__(self, module: SAM2LightningModule, total_steps: int = 1, distributed: bool = False):
+    graph=True captures zero-grad + forward + loss + backward of the step ONCE per input
+    signature (frame count, image size, category/object layout) into a HIP graph and replays
+    it: the ~6k kernel launches of a B+ 512^2 8-frame step cost one graph launch instead of
+    ~6k Python/ctypes launches (the step was host-bound).  Per step, only the host prompt stage
+    (connected components + clicks, sam2model.py:181-236), the copies of the new clip into the
+    graph's static input buffers, the dropout RNG offset and the all-reduce + optimizer run
+    eagerly.  Dropout masks still change every step: kernels fold the device-resident RNG
+    offset into their seeds (s2h_rng_bind)."""
+
+    def __init__(self, module: SAM2LightningModule, total_steps: int = 1, distributed: bool = False,
+                 graph: bool = False):
         self.module = module
         module.configure_optimizers(total_steps)
         self.reducer = ArenaGradReducer(module.model.arena.grad_region()) if distributed else None
         self.global_step = 0
+        self.graph = graph
+        self._graphs: Dict[Any, Dict[str, Any]] = {}
+        self.before_capture = None  # optional callable, run right before a graph is captured
+        from ..kernels import functional as FN
+        from ..kernels.ops import rng_offset
+        self._fn = FN
+        self.rng = rng_offset(module.model.arena.device)
+        # every step (eager, warm-up, capture) draws the same per-launch host seeds; the step-to-step
+        # variation of the dropout masks comes from the device RNG offset alone, so an eager step
+        # and a replay of the captured one use identical masks
+        self.seed_base = FN._SEED[0]
 
-    def __call__(self, batch):
+    def _device_step(self, batch):
         m = self.module
+        self._fn.set_seed(self.seed_base)
         m.model.arena.zero_grad()
         loss = m.training_step(batch, self.global_step)
         loss.backward()
+        return loss
+
+    def _graphed_step(self, batch):
+        model = self.module.model
+        dev = model.arena.device
+        plan = model.host_prompt_plan(batch)
+        key = (tuple(batch.img_batch.shape), tuple(batch.masks.shape), tuple(plan["obj_to_cat"]),
+               plan["num_categories"], tuple(t.shape for t in plan["host"]))
+        ent = self._graphs.get(key)
+        if ent is None:
+            static = _static_batch(batch, dev)
+            plan = dict(plan)
+            plan["dev"] = model.upload_prompt_plan(plan, dev)
+            static.prompt_plan = plan
+            cur = torch.cuda.current_stream(dev)
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(cur)
+            with torch.cuda.stream(side):  # eager warm-up: fills every device-side table cache
+                self._device_step(static)
+            cur.wait_stream(side)
+            if self.before_capture is not None:
+                self.before_capture()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                loss = self._device_step(static)
+            ent = self._graphs[key] = {"graph": g, "batch": static, "loss": loss, "logged": dict(self.module.logged)}
+        else:
+            st = ent["batch"]
+            st.img_batch.copy_(batch.img_batch, non_blocking=True)
+            st.masks.copy_(batch.masks, non_blocking=True)
+            st.obj_to_frame_idx.copy_(batch.obj_to_frame_idx, non_blocking=True)
+            model.upload_prompt_plan(plan, dev, out=st.prompt_plan["dev"])
+            st.prompt_plan.update({k: plan[k] for k in ("points", "labels")})
+        ent["graph"].replay()
+        self.module.logged = dict(ent["logged"])
+        return ent["loss"]
+
+    def __call__(self, batch):
+        m = self.module
+        self.rng.fill_(self.global_step + 1)
+        loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
         scale = 1.0
         if self.reducer is not None:
             self.reducer.reduce()
             scale = self.reducer.grad_scale
         lr = m.lr_at(self.global_step) if m.lr_at is not None else None
         m.optimizer.step(lr=lr, grad_scale=scale)
+        if m.optimizer is not None:
+            m.log("train/learning_rate", m.optimizer.param_groups[0]["lr"])
         self.global_step += 1
         return loss
 
 
-def fit(module: SAM2LightningModule, batches, max_steps: int, device="cuda", log_every: int = 1, distributed=False):
+def _static_batch(batch, device):
+    """device-resident copy of a batch whose tensors serve as a captured graph's input buffers"""
+    from ..data.data_utils import BatchedVideoDatapoint
+    out = BatchedVideoDatapoint(img_batch=batch.img_batch.to(device, copy=True),
+                                obj_to_frame_idx=batch.obj_to_frame_idx.to(device, copy=True),
+                                masks=batch.masks.to(device, copy=True), metadata=batch.metadata,
+                                dict_key=batch.dict_key, batch_size=list(batch.batch_size))
+    out.host_masks0 = None
+    return out
+
+
+def fit(module: SAM2LightningModule, batches, max_steps: int, device="cuda", log_every: int = 1, distributed=False,
+        graph: bool = True):
     """Minimal fit loop (max_steps optimizer steps over an iterable of BatchedVideoDatapoint)."""
     module.setup("fit", device)
-    run = StepRunner(module, max_steps, distributed)
+    run = StepRunner(module, max_steps, distributed, graph=graph)
     hist: List[Dict[str, float]] = []
     t0 = time.time()
     for i, batch in enumerate(batches):
