@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -46,6 +47,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
     ap.add_argument("--cpu-frames", type=int, default=4, help="frames of the CPU baseline sample clip")
     ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--print-losses", action="store_true", help="diagnostic: print every step's loss (host syncs)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the captured HIP graph")
     ap.add_argument("--kernel-table", action="store_true",
@@ -170,7 +172,9 @@ def main():
     torch.cuda.synchronize()
 
     for k in range(args.warmup):
-        runner(batches[k])
+        loss = runner(batches[k])
+        if args.print_losses:
+            print(f"step {k} loss {float(loss):.5f}", file=sys.stderr)
     torch.cuda.synchronize()
     if not args.no_prof and not graph:
         _lib.call("s2h_prof_enable", 8192)
@@ -179,7 +183,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
-        runner(batches[k])
+        loss = runner(batches[k])
+        if args.print_losses:
+            fr = " ".join(f"{float(f['multistep_pred_multimasks_high_res'][0].abs().mean()):.3g}"
+                          f"/{float(f['multistep_pred_ious'][0].abs().mean()):.3g}" for f in module.last_outputs)
+            print(f"step {k} loss {float(loss):.5f} graphs {len(runner._graphs)} frames {fr}", file=sys.stderr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -190,6 +198,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    loss_val = float(module.logged["train/total_loss"])  # last timed step
+    if not math.isfinite(loss_val):
+        print(f"WARNING: non-finite training loss {loss_val} in the timed steps", file=sys.stderr)
     roof = None
     if not args.no_prof:
         if graph:
@@ -201,6 +212,7 @@ def main():
             runner(batches[-1])
             runner.graph = True
             torch.cuda.synchronize()
+            print(f"profiled eager step loss {float(module.logged['train/total_loss']):.5f}", file=sys.stderr)
         recs = read_prof(_lib)
         _lib.call("s2h_prof_enable", 0)
         roof = attention_roofline([(ms, m[1:]) for ms, m in recs if m[0] == 1])
@@ -223,7 +235,6 @@ def main():
 
     frames = args.frames * args.steps * world
     value = frames / elapsed
-    loss_val = float(module.logged["train/total_loss"])
     result = {
         "metric": "training clip-frames/sec (512^2 8-frame, Hiera-B+)",
         "value": round(value, 3),

@@ -475,11 +475,394 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
   }
 }
 
+// ------------------------------------------- few-query / few-key specialisations
+// The two-way decoder's token<->image attentions (transformer.py:231-248, 8 heads,
+// head_dim 16, 8 tokens vs 1024 image rows, O*8 = 104 (batch, head) pairs) leave the
+// kernels above with one useful wave per workgroup looping over the long side: 104
+// workgroups, 16 serial key (or query) tiles each.  Here the 4 waves of a workgroup
+// split the LONG side instead and merge their partial results in LDS at the end.
+//   fwd, Lq <= 16 : waves take key tiles w, w+4, ...; partial (m, l, o) merged
+//   dQ,  Lq <= 16 : waves take key tiles w, w+4, ...; partial dQ summed
+//   dK/dV, Lk <= 16: waves take query tiles w, w+4, ...; partial dK, dV summed
+// Loop trip counts are workgroup-uniform (an idle wave masks its tile) so the barriers
+// are safe.  K / Q rows feed the MFMA B operand straight from global (16-B loads); only
+// the operands that need a transposed (key-major or query-major) fragment go through
+// wave-private LDS.
+template <typename T, int DP>
+__global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
+  using MF = Mfma<T>;
+  constexpr int BKEY = 64;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int VS = BKEY + VEC, PS = BKEY + VEC;
+  constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16, NPF = BKEY / MF::KSTEP;
+  constexpr int WL = DP * VS + 16 * PS;  // wave-private LDS elements
+  __shared__ __attribute__((aligned(16))) T smem[4 * WL];
+  __shared__ float mrg[4][16][DP + 2];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const T* Q = (const T*)a.q + b * a.sqb + h * a.sqh;
+  const T* K = (const T*)a.k + b * a.skb + h * a.skh;
+  const T* V = (const T*)a.v + b * a.svb + h * a.svh;
+  T* Vt = smem + w * WL;
+  T* Pw = Vt + DP * VS;
+  const float sl2 = a.scale * LOG2E;
+  const bool drop = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
+  const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+
+  typename MF::frag qf[NQF];
+#pragma unroll
+  for (int s = 0; s < NQF; ++s)
+    qf[s] = frag_global<T>(Q, a.sql, lane & 15, a.Lq, s * MF::KSTEP + (lane >> 4) * MF::KPL, a.D);
+  f32x4 o[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { m[r] = -INFINITY; l[r] = 0.f; }
+
+  const int nkt = (a.Lk + BKEY - 1) / BKEY;
+  for (int it = 0; it < (nkt + 3) / 4; ++it) {
+    const int kt = it * 4 + w;
+    const int k0 = kt * BKEY;
+    if (kt < nkt) {
+      lds_load_rows_t<T, BKEY, DP, VS, 64>(Vt, V, a.svl, k0, a.Lk, a.D, lane);
+      f32x4 s[NB];
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < NQF; ++t)
+          s[j] = MF::mma(qf[t], frag_global<T>(K, a.skl, k0 + j * 16 + (lane & 15), a.Lk,
+                                               t * MF::KSTEP + (lane >> 4) * MF::KPL, a.D), s[j]);
+      }
+      float mx[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mx[r] = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const bool kvalid = k0 + j * 16 + (lane & 15) < a.Lk;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float x = kvalid ? s[j][r] * sl2 : -INFINITY;
+          s[j][r] = x;
+          mx[r] = fmaxf(mx[r], x);
+        }
+      }
+      float alpha[4], rs[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        mx[r] = row16_max(mx[r]);
+        const float mn = fmaxf(m[r], mx[r]);
+        alpha[r] = exp2f(m[r] - mn);
+        m[r] = mn;
+        rs[r] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        const int key = k0 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = exp2f(s[j][r] - m[r]);
+          rs[r] += p;
+          if (drop) {
+            const int qi = (lane >> 4) * 4 + r;
+            const uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+            p = s2h_keep(a.seed, idx, thresh) ? p * inv_keep : 0.f;
+          }
+          Pw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) l[r] = l[r] * alpha[r] + row16_sum(rs[r]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[d][r] *= alpha[r];
+    }
+    __syncthreads();  // this wave's Vt / Pw writes visible to its own fragment reads
+    if (kt < nkt) {
+      typename MF::frag pf[NPF];
+#pragma unroll
+      for (int t = 0; t < NPF; ++t) pf[t] = MF::load(&Pw[(lane & 15) * PS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int t = 0; t < NPF; ++t)
+          o[d] = MF::mma(pf[t], MF::load(&Vt[(d * 16 + (lane & 15)) * VS + t * MF::KSTEP + (lane >> 4) * MF::KPL]),
+                         o[d]);
+    }
+    __syncthreads();  // reads done before the next tile overwrites Vt / Pw
+  }
+  // merge the 4 waves' (m, l, o)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = (lane >> 4) * 4 + r;
+#pragma unroll
+    for (int d = 0; d < ND; ++d) mrg[w][row][d * 16 + (lane & 15)] = o[d][r];
+    if ((lane & 15) == 0) { mrg[w][row][DP] = m[r]; mrg[w][row][DP + 1] = l[r]; }
+  }
+  __syncthreads();
+  T* O = (T*)a.o + b * a.sob + h * a.soh;
+  for (int e = tid; e < 16 * DP; e += 256) {
+    const int row = e / DP, col = e % DP;
+    if (row >= a.Lq) continue;
+    float M = -INFINITY;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) M = fmaxf(M, mrg[u][row][DP]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const float f = exp2f(mrg[u][row][DP] - M);  // waves without keys: m = -inf -> 0
+      L += mrg[u][row][DP + 1] * f;
+      acc += mrg[u][row][col] * f;
+    }
+    if (col < a.D) O[(int64_t)row * a.sol + col] = from_f32<T>(acc / L);
+    if (col == 0) a.lse[(int64_t)bh * a.Lq + row] = (M + log2f(L)) * LN2;
+  }
+}
+
+template <typename T, int DP>
+__global__ __launch_bounds__(256) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
+  using MF = Mfma<T>;
+  constexpr int BKEY = 64;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int TS = BKEY + VEC, PS = BKEY + VEC;
+  constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16, NPF = BKEY / MF::KSTEP;
+  constexpr int WL = DP * TS + 16 * PS;
+  __shared__ __attribute__((aligned(16))) T smem[4 * WL];
+  __shared__ float mrg[4][16][DP + 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const T* Q = (const T*)a.q + b * a.sqb + h * a.sqh;
+  const T* K = (const T*)a.k + b * a.skb + h * a.skh;
+  const T* V = (const T*)a.v + b * a.svb + h * a.svh;
+  const T* dO = (const T*)a.o + b * a.sob + h * a.soh;
+  T* Kt = smem + w * WL;
+  T* Sw = Kt + DP * TS;
+  const float sl2 = a.scale * LOG2E;
+  const bool drop = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
+  const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+
+  typename MF::frag qf[NQF], gf[NQF];
+#pragma unroll
+  for (int s = 0; s < NQF; ++s) {
+    const int d = s * MF::KSTEP + (lane >> 4) * MF::KPL;
+    qf[s] = frag_global<T>(Q, a.sql, lane & 15, a.Lq, d, a.D);
+    gf[s] = frag_global<T>(dO, a.sol, lane & 15, a.Lq, d, a.D);
+  }
+  float lse2[4], di[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = (lane >> 4) * 4 + r;
+    lse2[r] = row < a.Lq ? a.lse[(int64_t)bh * a.Lq + row] * LOG2E : 0.f;
+    di[r] = row < a.Lq ? a.di[(int64_t)bh * a.Lq + row] : 0.f;
+  }
+  f32x4 dq[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nkt = (a.Lk + BKEY - 1) / BKEY;
+  for (int it = 0; it < (nkt + 3) / 4; ++it) {
+    const int kt = it * 4 + w;
+    const int k0 = kt * BKEY;
+    if (kt < nkt) {
+      lds_load_rows_t<T, BKEY, DP, TS, 64>(Kt, K, a.skl, k0, a.Lk, a.D, lane);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int krow = k0 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int t = 0; t < NQF; ++t) {
+          const int d = t * MF::KSTEP + (lane >> 4) * MF::KPL;
+          s = MF::mma(qf[t], frag_global<T>(K, a.skl, krow, a.Lk, d, a.D), s);
+          dp = MF::mma(gf[t], frag_global<T>(V, a.svl, krow, a.Lk, d, a.D), dp);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int qi = (lane >> 4) * 4 + r;
+          const float p = (krow < a.Lk && qi < a.Lq) ? exp2f(s[r] * sl2 - lse2[r]) : 0.f;
+          float g = dp[r];
+          if (drop) {
+            const uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + krow;
+            g = s2h_keep(a.seed, idx, thresh) ? g * inv_keep : 0.f;
+          }
+          Sw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p * (g - di[r]));
+        }
+      }
+    }
+    __syncthreads();
+    if (kt < nkt) {
+      typename MF::frag sf[NPF];
+#pragma unroll
+      for (int t = 0; t < NPF; ++t) sf[t] = MF::load(&Sw[(lane & 15) * PS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int t = 0; t < NPF; ++t)
+          dq[d] = MF::mma(sf[t], MF::load(&Kt[(d * 16 + (lane & 15)) * TS + t * MF::KSTEP + (lane >> 4) * MF::KPL]),
+                          dq[d]);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int d = 0; d < ND; ++d) mrg[w][(lane >> 4) * 4 + r][d * 16 + (lane & 15)] = dq[d][r];
+  __syncthreads();
+  T* dQ = (T*)a.dq + b * a.sdqb + h * a.sdqh;
+  for (int e = tid; e < 16 * DP; e += 256) {
+    const int row = e / DP, col = e % DP;
+    if (row < a.Lq && col < a.D)
+      dQ[(int64_t)row * a.sdql + col] =
+          from_f32<T>((mrg[0][row][col] + mrg[1][row][col] + mrg[2][row][col] + mrg[3][row][col]) * a.scale);
+  }
+}
+
+template <typename T, int DP>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
+  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
+  using MF = Mfma<T>;
+  constexpr int BQ = sizeof(T) == 2 ? 64 : 32;
+  constexpr int VEC = 16 / sizeof(T);
+  constexpr int KS = DP + VEC, QS = BQ + VEC;
+  constexpr int NKF = DP / MF::KSTEP, NB = BQ / 16, ND = DP / 16, NPF = BQ / MF::KSTEP;
+  constexpr int WL = 2 * DP * QS + 2 * 16 * QS;
+  __shared__ __attribute__((aligned(16))) T smem[2 * 16 * KS + 4 * WL];
+  __shared__ float stat[4][2 * BQ];
+  __shared__ float mrg[4][16][2 * DP];
+  T* Kn = smem;
+  T* Vn = Kn + 16 * KS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  T* Qt = Vn + 16 * KS + w * WL;
+  T* Gt = Qt + DP * QS;
+  T* Pw = Gt + DP * QS;
+  T* Sw = Pw + 16 * QS;
+  float* lse_s = stat[w];
+  float* di_s = stat[w] + BQ;
+
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const T* Q = (const T*)a.q + b * a.sqb + h * a.sqh;
+  const T* K = (const T*)a.k + b * a.skb + h * a.skh;
+  const T* V = (const T*)a.v + b * a.svb + h * a.svh;
+  const T* dO = (const T*)a.o + b * a.sob + h * a.soh;
+  const float sl2 = a.scale * LOG2E;
+  const bool drop = a.p_drop > 0.f;
+  const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
+  const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
+
+  lds_load_rows<T, 16, DP, KS, 256>(Kn, K, a.skl, 0, a.Lk, a.D, tid);
+  lds_load_rows<T, 16, DP, KS, 256>(Vn, V, a.svl, 0, a.Lk, a.D, tid);
+  f32x4 dk[ND], dv[ND];
+#pragma unroll
+  for (int d = 0; d < ND; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
+
+  const int nqt = (a.Lq + BQ - 1) / BQ;
+  for (int it = 0; it < (nqt + 3) / 4; ++it) {
+    const int qt = it * 4 + w;
+    const int q0 = qt * BQ;
+    __syncthreads();  // Kn/Vn loaded (first pass); previous tile's reads done
+    if (qt < nqt) {
+      lds_load_rows_t<T, BQ, DP, QS, 64>(Qt, Q, a.sql, q0, a.Lq, a.D, lane);
+      lds_load_rows_t<T, BQ, DP, QS, 64>(Gt, dO, a.sol, q0, a.Lq, a.D, lane);
+      for (int i = lane; i < BQ; i += 64) {
+        const int qi = q0 + i;
+        lse_s[i] = qi < a.Lq ? a.lse[(int64_t)bh * a.Lq + qi] * LOG2E : 0.f;
+        di_s[i] = qi < a.Lq ? a.di[(int64_t)bh * a.Lq + qi] : 0.f;
+      }
+    }
+    __syncthreads();
+    if (qt < nqt) {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) {
+        f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int qrow = q0 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int t = 0; t < NKF; ++t) {
+          const int ao = (lane & 15) * KS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+          const int d = t * MF::KSTEP + (lane >> 4) * MF::KPL;
+          s = MF::mma(MF::load(&Kn[ao]), frag_global<T>(Q, a.sql, qrow, a.Lq, d, a.D), s);
+          dp = MF::mma(MF::load(&Vn[ao]), frag_global<T>(dO, a.sol, qrow, a.Lq, d, a.D), dp);
+        }
+        const int qc = j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int key = (lane >> 4) * 4 + r;
+          const bool valid = key < a.Lk && qrow < a.Lq;
+          const float p = valid ? exp2f(s[r] * sl2 - lse_s[qc]) : 0.f;
+          float pd = p, g = dp[r];
+          if (drop) {
+            const uint64_t idx = ((uint64_t)bh * a.Lq + qrow) * (uint64_t)a.Lk + key;
+            const bool keep = valid && s2h_keep(a.seed, idx, thresh);
+            pd = keep ? p * inv_keep : 0.f;
+            g = keep ? g * inv_keep : 0.f;
+          }
+          Pw[key * QS + qc] = from_f32<T>(pd);
+          Sw[key * QS + qc] = from_f32<T>(p * (g - di_s[qc]));
+        }
+      }
+    }
+    __syncthreads();
+    if (qt < nqt) {
+      typename MF::frag pf[NPF], sf[NPF];
+#pragma unroll
+      for (int t = 0; t < NPF; ++t) {
+        const int o = (lane & 15) * QS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+        pf[t] = MF::load(&Pw[o]);
+        sf[t] = MF::load(&Sw[o]);
+      }
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int t = 0; t < NPF; ++t) {
+          const int o = (d * 16 + (lane & 15)) * QS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
+          dv[d] = MF::mma(pf[t], MF::load(&Gt[o]), dv[d]);
+          dk[d] = MF::mma(sf[t], MF::load(&Qt[o]), dk[d]);
+        }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+      mrg[w][(lane >> 4) * 4 + r][d * 16 + (lane & 15)] = dk[d][r];
+      mrg[w][(lane >> 4) * 4 + r][DP + d * 16 + (lane & 15)] = dv[d][r];
+    }
+  __syncthreads();
+  T* dK = (T*)a.dk + b * a.sdkb + h * a.sdkh;
+  T* dV = (T*)a.dv + b * a.sdvb + h * a.sdvh;
+  for (int e = tid; e < 16 * DP; e += 256) {
+    const int key = e / DP, col = e % DP;
+    if (key < a.Lk && col < a.D) {
+      const float sk = mrg[0][key][col] + mrg[1][key][col] + mrg[2][key][col] + mrg[3][key][col];
+      const float sv = mrg[0][key][DP + col] + mrg[1][key][DP + col] + mrg[2][key][DP + col] + mrg[3][key][DP + col];
+      dK[(int64_t)key * a.sdkl + col] = from_f32<T>(sk * a.scale);
+      dV[(int64_t)key * a.sdvl + col] = from_f32<T>(sv);
+    }
+  }
+}
+
 // ------------------------------------------------------------------ launch
+// few-query / few-key paths pay off when the long side spans several 64-row tiles
+static bool attn_fewq(const AttnArgs& a) { return a.Lq <= 16 && a.Lk > 128 && a.D <= 64; }
+static bool attn_fewk(const AttnArgs& a) { return a.Lk <= 16 && a.Lq > 128 && a.D <= 64; }
+
 template <typename T, int DP>
 static int attn_fwd_launch(const AttnArgs& a, hipStream_t st) {
   dim3 grid((a.Lq + 63) / 64, a.B * a.H);
   const int slot = s2h_prof_begin(st, 1, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
+  if constexpr (DP <= 64) {
+    if (attn_fewq(a)) {
+      hipLaunchKernelGGL((attn_fwd_fewq_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
+      s2h_prof_end(slot, st);
+      return (int)hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((attn_fwd_kernel<T, DP>), grid, dim3(256), 0, st, a);
   s2h_prof_end(slot, st);
   return (int)hipGetLastError();
@@ -490,10 +873,21 @@ static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
   const int slot = s2h_prof_begin(st, 2, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
   hipLaunchKernelGGL((attn_bwd_pre_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0, st, a);
   dim3 gq((a.Lq + 63) / 64, a.B * a.H);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP>), gq, dim3(256), 0, st, a);
+  bool done_dq = false, done_dkv = false;
+  if constexpr (DP <= 64) {
+    if (attn_fewq(a)) {
+      hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
+      done_dq = true;
+    }
+    if (attn_fewk(a)) {
+      hipLaunchKernelGGL((attn_bwd_dkv_fewk_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
+      done_dkv = true;
+    }
+  }
+  if (!done_dq) hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP>), gq, dim3(256), 0, st, a);
   constexpr int NW = AttnCfg<T>::NW_DKV;
   dim3 gk((a.Lk + NW * 16 - 1) / (NW * 16), a.B * a.H);
-  hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DP>), gk, dim3(NW * 64), 0, st, a);
+  if (!done_dkv) hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DP>), gk, dim3(NW * 64), 0, st, a);
   s2h_prof_end(slot, st);
   return (int)hipGetLastError();
 }

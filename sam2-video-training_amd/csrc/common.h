@@ -144,3 +144,9 @@ __device__ __forceinline__ float act_grad(float x, int act) {
 }
 
 #define S2H_LAUNCH_CHECK() return (int)hipGetLastError()
+
+// Zero-fill as a KERNEL on `st` (elementwise.hip).  Used instead of hipMemset*Async: inside a
+// captured HIP graph the memset nodes were observed to break stream order against the kernel
+// nodes around them on ROCm 7.2 (garbage loss values in replays), kernel nodes never do.
+// rows x cols floats with row stride ld (ld == cols: one contiguous range).
+void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t st);

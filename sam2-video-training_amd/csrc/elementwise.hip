@@ -430,7 +430,7 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t rows, int cols,
 extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum,
                           hipStream_t st) {
   if (cols <= 0) return 0;
-  if (!accum) (void)hipMemsetAsync(out, 0, cols * sizeof(float), st);
+  if (!accum) s2h_zero_f32(out, 1, cols, cols, st);
   if (rows <= 0) return (int)hipGetLastError();
   const int V = dt == S2H_BF16 ? 8 : 4;
   if (cols % V == 0 && cols / V <= 256 && ld % V == 0 && ((uintptr_t)x & 15) == 0) {
@@ -740,4 +740,31 @@ extern "C" int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, cons
   if (R * D <= 0) return 0;
   DISPATCH_T(dt, point_embed_bwd_kernel, dim3((D + 255) / 256), R, D, labels, dout, dtable);
   return (int)hipGetLastError();
+}
+
+// ------------------------------------------------------------------ zero fill
+__global__ __launch_bounds__(256) void zero_f32_kernel(float* p, int64_t rows, int64_t cols, int64_t ld) {
+  const int64_t n = rows * cols;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const int64_t r = i / cols;
+    p[r * ld + (i - r * cols)] = 0.f;
+  }
+}
+__global__ __launch_bounds__(256) void zero_f32x4_kernel(float4* p, int64_t n4) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256)
+    p[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t st) {
+  const int64_t n = rows * cols;
+  if (n <= 0) return;
+  if (ld == cols && (uintptr_t)p % 16 == 0 && n % 4 == 0) {
+    const int64_t n4 = n / 4;
+    int64_t b = (n4 + 255) / 256;
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(zero_f32x4_kernel, dim3((unsigned)b), dim3(256), 0, st, (float4*)p, n4);
+    return;
+  }
+  int64_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)b), dim3(256), 0, st, p, rows, cols, ld);
 }

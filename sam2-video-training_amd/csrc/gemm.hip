@@ -249,7 +249,7 @@ extern "C" int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* 
                                 int64_t ldx, float* dw, int64_t lddw, float* db, int accumulate, hipStream_t stream) {
   if (N <= 0 || K <= 0) return 0;
   if (rows > INT32_MAX) return (int)hipErrorInvalidValue;
-  if (!accumulate && db) (void)hipMemsetAsync(db, 0, (size_t)N * sizeof(float), stream);
+  if (!accumulate && db) s2h_zero_f32(db, 1, N, N, stream);
   if (dt == S2H_F32) {
     int rc = s2h_gemm(S2H_F32, S2H_F32, 1, N, K, (int)rows, dy, 1, lddy, 0, x, ldx, 1, 0, dw, lddw, 0, nullptr, 0,
                       nullptr, 0, 0, nullptr, 0, 0, 0, nullptr, 0.f, 0, 1.f, accumulate ? 1.f : 0.f, 0, stream);

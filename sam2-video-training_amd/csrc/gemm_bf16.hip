@@ -468,16 +468,9 @@ static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
       a.kchunk = ((a.K + s - 1) / s + 63) / 64 * 64;
       a.splits = (a.K + a.kchunk - 1) / a.kchunk;
       if (a.beta == 0.f && a.ldc == a.N && (batch == 1 || a.sC == (int64_t)a.M * a.N)) {
-        (void)hipMemsetAsync(a.C, 0, (size_t)batch * a.M * a.N * sizeof(float), st);
+        s2h_zero_f32((float*)a.C, (int64_t)batch * a.M, a.N, a.N, st);
       } else if (a.beta == 0.f) {
-        for (int b = 0; b < batch; ++b) {
-          if (a.ldc == a.N) {
-            (void)hipMemsetAsync((float*)a.C + (int64_t)b * a.sC, 0, (size_t)a.M * a.N * sizeof(float), st);
-          } else {
-            (void)hipMemset2DAsync((float*)a.C + (int64_t)b * a.sC, a.ldc * sizeof(float), 0,
-                                   a.N * sizeof(float), a.M, st);
-          }
-        }
+        for (int b = 0; b < batch; ++b) s2h_zero_f32((float*)a.C + (int64_t)b * a.sC, a.M, a.N, a.ldc, st);
       }
     }
   }

@@ -53,7 +53,7 @@ __global__ __launch_bounds__(256) void mask_stats_kernel(int N, int64_t P, const
 extern "C" int s2h_mask_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
                               float inv_temp, float* stats, hipStream_t st) {
   if (N <= 0) return 0;
-  (void)hipMemsetAsync(stats, 0, N * NSTAT * sizeof(float), st);
+  s2h_zero_f32(stats, 1, (int64_t)N * NSTAT, (int64_t)N * NSTAT, st);
   int chunks = (int)((P + 4095) / 4096);
   if (chunks > 256) chunks = 256;
   if (chunks < 1) chunks = 1;

@@ -113,6 +113,7 @@ class SAM2LightningModule(nn.Module):
     def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
         """trainer.py:256-289"""
         outs_per_frame, obj_to_cat = self.forward(batch)
+        self.last_outputs = outs_per_frame
         outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
         losses = self.criterion(outs, targets)
         total = losses[CORE_LOSS_KEY]
@@ -200,7 +201,8 @@ class StepRunner:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 loss = self._device_step(static)
-            ent = self._graphs[key] = {"graph": g, "batch": static, "loss": loss, "logged": dict(self.module.logged)}
+            ent = self._graphs[key] = {"graph": g, "batch": static, "loss": loss, "logged": dict(self.module.logged),
+                                       "outputs": self.module.last_outputs}
         else:
             st = ent["batch"]
             st.img_batch.copy_(batch.img_batch, non_blocking=True)
@@ -210,6 +212,7 @@ class StepRunner:
             st.prompt_plan.update({k: plan[k] for k in ("points", "labels")})
         ent["graph"].replay()
         self.module.logged = dict(ent["logged"])
+        self.module.last_outputs = ent["outputs"]
         return ent["loss"]
 
     def __call__(self, batch):

@@ -37,22 +37,37 @@ def _clips(idxs, T=3, S=128, n_cat=4, n_obj=3):
 
 @pytest.mark.parametrize("dropout", [0.0, 0.1])
 def test_graphed_steps_match_eager(dropout):
+    """3 optimizer steps on 3 clips: per-step losses and logged values agree"""
     clips = _clips([11, 12, 13])
-    out = {}
+    out = []
     for graph in (False, True):
         module, run = _runner(graph, dropout)
         losses = [float(run(c).detach()) for c in clips]
         torch.cuda.synchronize()
-        out[graph] = (losses, module.model.arena.grad_region().detach().clone(),
-                      {k: float(v) for k, v in module.logged.items() if torch.is_tensor(v)})
+        out.append((losses, {k: float(v) for k, v in module.logged.items() if torch.is_tensor(v)}))
         assert len(run._graphs) == (1 if graph else 0)
-    (le, pe, loge), (lg, pg, logg) = out[False], out[True]
+    (le, loge), (lg, logg) = out
     for a, b in zip(le, lg):
         assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (le, lg)
-    # last step's gradients (split-K fp32 atomics: summation order may differ run to run)
-    assert (pe - pg).abs().max().item() <= 1e-4 * pe.abs().max().item()
     for k in loge:
         assert abs(loge[k] - logg[k]) <= 1e-5 * max(1.0, abs(loge[k])), k
+
+
+@pytest.mark.parametrize("dropout", [0.0, 0.1])
+def test_graphed_gradients_match_eager(dropout):
+    """lr = 0 (weights fixed): every replayed step's gradients equal the eager step's up to fp32
+    summation order (split-K / bias-gradient atomics: measured ~1e-7 of the largest gradient)"""
+    clips = _clips([14, 15])
+    grads = []
+    for graph in (False, True):
+        module, run = _runner(graph, dropout, lr=0.0)
+        g = []
+        for c in clips:
+            run(c)
+            g.append(module.model.arena.grad_region().detach().clone())
+        grads.append(g)
+    for ge, gg in zip(*grads):
+        assert (ge - gg).abs().max().item() <= 1e-5 * ge.abs().max().item()
 
 
 def test_graph_replays_draw_fresh_dropout_masks():

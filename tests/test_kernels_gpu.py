@@ -143,7 +143,10 @@ def _ref_attn(q, k, v, scale):
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 5e-5), (torch.bfloat16, 2e-2)])
 @pytest.mark.parametrize("B,H,Lq,Lk,D", [(2, 2, 64, 64, 56), (3, 1, 16, 64, 56), (2, 8, 8, 100, 16),
                                          (2, 8, 100, 8, 16), (1, 8, 7, 7, 32), (2, 1, 256, 1028, 256),
-                                         (1, 4, 196, 196, 96), (1, 2, 49, 196, 72), (13, 1, 70, 130, 256)])
+                                         (1, 4, 196, 196, 96), (1, 2, 49, 196, 72), (13, 1, 70, 130, 256),
+                                         # decoder token<->image shapes: few-query / few-key kernels
+                                         (13, 8, 8, 1024, 16), (13, 8, 1024, 8, 16), (2, 3, 5, 300, 32),
+                                         (2, 3, 300, 5, 32), (1, 2, 16, 1000, 64), (1, 2, 1000, 16, 64)])
 def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
     ops = _ops()
     torch.manual_seed(1)
@@ -233,16 +236,17 @@ def test_attention_strided_qkv():
     _close(o, ro, 5e-5)
 
 
-def test_attention_dropout_consistent():
+@pytest.mark.parametrize("Lq,Lk", [(40, 40), (8, 300), (300, 8)])
+def test_attention_dropout_consistent(Lq, Lk):
     """dropout mask regenerated in backward: finite-difference check of the dropped attention."""
     ops = _ops()
     torch.manual_seed(2)
-    B, H, L, D = 1, 1, 40, 32
-    q = torch.randn(B, L, H, D, device=DEV, dtype=torch.float64).float()
-    k = torch.randn(B, L, H, D, device=DEV).float()
-    v = torch.randn(B, L, H, D, device=DEV).float()
+    B, H, D = 1, 1, 32
+    q = torch.randn(B, Lq, H, D, device=DEV, dtype=torch.float64).float()
+    k = torch.randn(B, Lk, H, D, device=DEV).float()
+    v = torch.randn(B, Lk, H, D, device=DEV).float()
     o = torch.empty_like(q)
-    lse = torch.empty(B, H, L, device=DEV)
+    lse = torch.empty(B, H, Lq, device=DEV)
     ops.attn_fwd(q, k, v, o, lse, 0.2, p_drop=0.3, seed=1234)
     o2 = torch.empty_like(q)
     ops.attn_fwd(q, k, v, o2, lse, 0.2, p_drop=0.3, seed=1234)
