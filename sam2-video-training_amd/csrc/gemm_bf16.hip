@@ -81,40 +81,104 @@ struct Stage16 {
 };
 
 // Finishes outputs (row, col0..col0+3) of batch bz from the fp32 accumulators v4.
-__device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4) {
+// Every epilogue option is tested ONCE per 4-column group (uniform scalar branches around
+// 4-wide straight-line code), never per element: per-element option tests made the epilogue
+// SALU-bound (~1.7k SALU + 1.2k VALU instructions per wave for 32 MFMAs at K = 64).
+// `bcol` holds the lane's 4 column biases (loaded once per tile by the caller).
+__device__ __forceinline__ uint2 ld4_bf16(const bf16* ptr, bool full) {
+  if (full) return *(const uint2*)ptr;
+  return make_uint2(0, 0);
+}
+__device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4, const float* bcol) {
   float v[4] = {v4.x, v4.y, v4.z, v4.w};
-  const bool full = col0 + 3 < p.N;
+  const int nval = p.N - col0;
+  if (nval <= 0) return;
+  const bool full = nval >= 4 && p.vecC;
   if (p.splits > 1) {  // split-K: fp32 atomic accumulate (beta handled on the host side)
     float* C = (float*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
-      if (col0 + e < p.N) atomicAdd(C + e, p.alpha * v[e]);
+      if (e < nval) atomicAdd(C + e, p.alpha * v[e]);
     return;
   }
-  const int64_t xo = (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0;
-  const int64_t co = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
-  const bf16* R = p.R ? (const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0 : nullptr;
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const int col = col0 + e;
-    if (col >= p.N) break;
-    float x = p.alpha * v[e];
-    if (p.bias_mode == 1) x += p.bias[col];
-    else if (p.bias_mode == 2) x += p.bias[row];
-    if (p.aux_mode == 1) ((bf16*)p.X)[xo + e] = (bf16)x;
-    if (p.aux_mode == 2) x *= act_grad((float)((const bf16*)p.X)[xo + e], p.act);
-    else x = apply_act(x, p.act);
-    if (p.cscale) x *= p.cscale[col];
-    if (p.drop_p > 0.f) {
-      const uint64_t idx = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
-      x = s2h_keep(p.seed, idx, (uint32_t)(p.drop_p * 4294967296.0)) ? x / (1.f - p.drop_p) : 0.f;
-    }
-    if (R) x += (float)R[e];
-    v[e] = x;
+  for (int e = 0; e < 4; ++e) v[e] = p.alpha * v[e] + bcol[e];
+  if (p.bias_mode == 2) {
+    const float br = p.bias[row];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] += br;
   }
+  if (p.aux_mode == 1) {  // store the pre-activation
+    bf16* X = (bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0;
+    if (full && p.ldx % 4 == 0) {
+      bf16 t[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = (bf16)v[e];
+      *(uint2*)X = *(const uint2*)t;
+    } else {
+      for (int e = 0; e < 4 && e < nval; ++e) X[e] = (bf16)v[e];
+    }
+  }
+  if (p.aux_mode == 2) {  // multiply by act'(pre-activation)
+    const bf16* X = (const bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0;
+    float xs[4];
+    if (full && p.ldx % 4 == 0) {
+      const uint2 r = *(const uint2*)X;
+      const bf16* rb = (const bf16*)&r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xs[e] = (float)rb[e];
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) xs[e] = e < nval ? (float)X[e] : 0.f;
+    }
+    if (p.act == S2H_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = xs[e] > 0.f ? v[e] : 0.f;
+    } else if (p.act != S2H_ACT_NONE) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] *= act_grad(xs[e], p.act);
+    }
+  } else if (p.act == S2H_ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  } else if (p.act != S2H_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
+  }
+  if (p.cscale) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] *= e < nval ? p.cscale[col0 + e] : 0.f;
+  }
+  if (p.drop_p > 0.f) {
+    const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
+    const float inv_keep = 1.f / (1.f - p.drop_p);
+    const uint64_t idx0 = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
+    bool k[4];
+    if ((idx0 & 1) == 0) {
+      s2h_keep_pair(p.seed, idx0 >> 1, thresh, k[0], k[1]);
+      s2h_keep_pair(p.seed, (idx0 >> 1) + 1, thresh, k[2], k[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) k[e] = s2h_keep(p.seed, idx0 + e, thresh);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
+  }
+  if (p.R) {
+    const bf16* R = (const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0;
+    if (full && p.ldr % 4 == 0) {
+      const uint2 r = *(const uint2*)R;
+      const bf16* rb = (const bf16*)&r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] += (float)rb[e];
+    } else {
+      for (int e = 0; e < 4 && e < nval; ++e) v[e] += (float)R[e];
+    }
+  }
+  const int64_t co = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
   if (p.out_f32) {
     float* C = (float*)p.C + co;
-    if (full && p.vecC) {
+    if (full) {
       float4 o = {v[0], v[1], v[2], v[3]};
       if (p.beta != 0.f) {
         const float4 c = *(const float4*)C;
@@ -122,11 +186,11 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
       }
       *(float4*)C = o;
     } else {
-      for (int e = 0; e < 4 && col0 + e < p.N; ++e) C[e] = v[e] + (p.beta != 0.f ? p.beta * C[e] : 0.f);
+      for (int e = 0; e < 4 && e < nval; ++e) C[e] = v[e] + (p.beta != 0.f ? p.beta * C[e] : 0.f);
     }
   } else {
     bf16* C = (bf16*)p.C + co;
-    if (full && p.vecC) {
+    if (full) {
       bf16 o[4];
       if (p.beta != 0.f) {
         const uint2 c = *(const uint2*)C;
@@ -139,9 +203,15 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
       }
       *(uint2*)C = *(const uint2*)o;
     } else {
-      for (int e = 0; e < 4 && col0 + e < p.N; ++e) C[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)C[e] : 0.f));
+      for (int e = 0; e < 4 && e < nval; ++e) C[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)C[e] : 0.f));
     }
   }
+}
+
+// the lane's 4 column biases (zeros when the bias is absent or per row)
+__device__ __forceinline__ void load_bcol(const GemmArgs16& p, int col0, float* bcol) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) bcol[e] = (p.splits == 1 && p.bias_mode == 1 && col0 + e < p.N) ? p.bias[col0 + e] : 0.f;
 }
 
 template <int BM, int BN, bool AKC, bool BKC>
@@ -218,6 +288,8 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
   static_assert(4 * 16 * EPLD * 4 <= (SA::LDS_ELEMS + SB::LDS_ELEMS) * 2, "epilogue staging fits the tile LDS");
   float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
   const int c4 = lane % CPR, rg = lane / CPR;
+  float bcol[4];
+  load_bcol(p, n0 + wn * WN + 4 * c4, bcol);
   if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
   if (nk == 0) __syncthreads();
 #pragma unroll
@@ -231,7 +303,7 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
       const int rl = rg + ps * RPP;
       const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
       const int row = m0 + wm * WM + i * 16 + rl;
-      if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4);
+      if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol);
     }
     __syncthreads();
   }
@@ -403,6 +475,8 @@ __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
   constexpr int EPLD = WN + 4;
   static_assert(4 * 16 * EPLD * 4 <= 2 * STAGE, "epilogue staging fits");
   float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
+  float bcol[4];
+  load_bcol(p, n0 + wn * WN + 4 * ((lane) % (WN / 4)), bcol);
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -426,7 +500,7 @@ __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
         const int rl = rg + ps * RPP;
         const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
         const int row = m0 + wm * WM + i * 16 + rl;
-        if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4);
+        if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol);
       }
     }
     __syncthreads();

@@ -220,21 +220,27 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int C, const 
     part[(int64_t)blockIdx.x * 2 * C + c] = sh[c] + sh[2 * C + c] + sh[4 * C + c] + sh[6 * C + c];
 }
 
-// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][C + c]; 64 columns x 4 slices per block
+// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][C + c].  Grid (column blocks of 64,
+// NS slices of the block partials); 256 threads = 64 columns x 4 interleaved partial rows, so
+// every thread sums only ~nb / (4 NS) values (independent loads in flight), then one atomic
+// per column and slice (NS <= 32 same-address atomics, no contention).
 __global__ __launch_bounds__(256) void ln_wgrad_finalize_kernel(int nb, int C, const float* part, float* dgamma,
                                                                 float* dbeta) {
   __shared__ float sh[4][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sl = threadIdx.x >> 6;
+  const int per = (nb + gridDim.y - 1) / gridDim.y;
+  const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
   float s = 0.f;
-  if (col < 2 * C)
-    for (int b = sl; b < nb; b += 4) s += part[(int64_t)b * 2 * C + col];
+  if (col < 2 * C) {
+#pragma unroll 8
+    for (int b = b0 + sl; b < b1; b += 4) s += part[(int64_t)b * 2 * C + col];
+  }
   sh[sl][threadIdx.x & 63] = s;
   __syncthreads();
-  if (sl == 0 && col < 2 * C) {
+  if (sl == 0 && col < 2 * C && b0 < b1) {
     const float t = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
-    if (col < C) dgamma[col] += t;
-    else dbeta[col - C] += t;
+    atomicAdd(col < C ? &dgamma[col] : &dbeta[col - C], t);
   }
 }
 
@@ -430,9 +436,12 @@ int ln_bwd(int rows, int C, const T* x, int64_t ldx, const T* dy, int64_t lddy, 
     hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 2 * C * sizeof(float), st, rows, C, x, ldx, dy, lddy,
                        gamma, mean, rstd, dx, lddx, dx_accum, dres, ldres, part);
   }
-  if (part)
-    hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64), dim3(256), 0, st, nb, C, part, dgamma,
+  if (part) {
+    int ns = (nb + 31) / 32;
+    if (ns > 32) ns = 32;
+    hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64, ns), dim3(256), 0, st, nb, C, part, dgamma,
                        dbeta);
+  }
   return (int)hipGetLastError();
 }
 }  // namespace
