@@ -74,6 +74,18 @@ def attention_roofline(records):
             "flops_per_launch_avg": flops / n}
 
 
+def pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the latest committed rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes (profiles/*_flash_fwd_pmc.json, written by the recipe in
+    tools/gpu_prof.sh; counters cannot be collected inside this timed run)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_flash_fwd_pmc.json")))
+    if not files:
+        return None, None
+    d = json.load(open(files[-1]))
+    return float(d["bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+
+
 def read_prof(_lib):
     """[(ms, [kind, s0..s4])] of every record of the in-library launch profiler"""
     import ctypes
@@ -217,6 +229,10 @@ def main():
         _lib.call("s2h_prof_enable", 0)
         roof = attention_roofline([(ms, m[1:]) for ms, m in recs if m[0] == 1])
         if roof is not None:
+            roof["traffic"], src = pmc_traffic()
+            if src:
+                roof["traffic_unit"] = "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)"
+                roof["traffic_source"] = src
             roof["timing"] = ("HIP events per launch, one eager step after the timed graph replays" if graph
                               else "HIP events per launch over the timed region")
         if args.kernel_table:
@@ -235,6 +251,15 @@ def main():
 
     frames = args.frames * args.steps * world
     value = frames / elapsed
+
+    # validation IoU (eval/eval.py formulas, in-loop) on a held-out synthetic clip per rank
+    val_clip = make_clip(100_000 + rank, args.frames, args.image_size, args.objects, args.objects)
+    module.validation_step(sam2_collate_fn([val_clip]).to(device))
+    val_iou = float(module.last_eval["avg_scores"]["iou"])
+    if world > 1:
+        t = torch.tensor([val_iou], device=device)
+        dist.all_reduce(t)
+        val_iou = float(t.item()) / world
     result = {
         "metric": "training clip-frames/sec (512^2 8-frame, Hiera-B+)",
         "value": round(value, 3),
@@ -259,6 +284,9 @@ def main():
                            if (args.size, args.image_size, args.frames, args.objects, args.trainable) in STEP_TF_PER_FRAME else None),
         "cpu_baseline": None,
         "final_loss": round(loss_val, 5),
+        # eval.py IoU of the category-merged masks on held-out synthetic clips (random-init weights
+        # after `steps` fine-tuning steps: a pipeline check, not a model-quality number)
+        "val_iou": round(val_iou, 5),
     }
     if rank == 0 and world == 1 and args.cpu_baseline:
         try:

@@ -251,6 +251,11 @@ int s2h_mask_loss_finalize(int N, int64_t P, const float* stats, const float* pr
 int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
                       float inv_temp, const float* coef, float* dx, int64_t lddx, const float* gtot,
                       float* dious, hipStream_t st);
+/* Evaluation counts of one frame (eval/eval.py:16-40 caculate_iou / _dice / _mae on the
+ * binarised category-merged mask pred = logits > 0): counts[4n..4n+3] = |pred & gt|,
+ * |pred | gt|, |pred|, |gt| as uint64 (zeroed by the call).  Validation only, no gradient. */
+int s2h_mask_eval_counts(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                         uint64_t* counts, hipStream_t st);
 /* Pixelwise max of each category's object masks (CSR cat_off / cat_obj), argmax
  * saved for the backward (merge_object_results_to_category, masks.py:98-115). */
 int s2h_group_max_fwd(int Ncat, int64_t P, const int* cat_off, const int* cat_obj, const float* x,

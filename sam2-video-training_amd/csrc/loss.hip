@@ -271,3 +271,57 @@ extern "C" int s2h_sigmoid_grad_axpy(int R, int64_t P, const float* x, int64_t l
   hipLaunchKernelGGL(sigmoid_grad_axpy_kernel, dim3((unsigned)b), dim3(256), 0, st, R, P, x, ldx, coef, dx, lddx);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------------------ evaluation counts
+// Per category n of one frame: counts[n] = {|pred & gt|, |pred | gt|, |pred|, |gt|} with
+// pred = (logits > 0) (the binarised category-merged high-res mask the reference writes out
+// for evaluation) -- exactly the integer sums behind caculate_iou / caculate_dice /
+// caculate_mae (eval/eval.py:16-40): iou = i / (u + 1e-7), dice = 2 i / (|p| + |g| + 1e-7),
+// mae = (|p| + |g| - 2 i) / P.  Integer counts: bit-exact against the CPU restatement.
+__global__ __launch_bounds__(256) void mask_eval_counts_kernel(int64_t P, const float* x, int64_t ldx,
+                                                               const uint8_t* tgt, int64_t ldt,
+                                                               unsigned long long* counts) {
+  const int n = blockIdx.y;
+  const int64_t chunk = (P + gridDim.x - 1) / gridDim.x;
+  const int64_t p0 = blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+  uint32_t c[4] = {0, 0, 0, 0};
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+    const bool pr = x[n * ldx + p] > 0.f;
+    const bool gt = tgt[n * ldt + p] != 0;
+    c[0] += pr && gt;
+    c[1] += pr || gt;
+    c[2] += pr;
+    c[3] += gt;
+  }
+  __shared__ uint32_t red[4][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t v = c[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    if (lane == 0) red[w][k] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    const uint32_t v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(&counts[n * 4 + threadIdx.x], (unsigned long long)v);
+  }
+}
+
+__global__ void zero_u64_kernel(unsigned long long* p, int n) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = 0ull;
+}
+
+extern "C" int s2h_mask_eval_counts(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                                    uint64_t* counts, hipStream_t st) {
+  if (N <= 0) return 0;
+  hipLaunchKernelGGL(zero_u64_kernel, dim3((4 * N + 255) / 256), dim3(256), 0, st, (unsigned long long*)counts, 4 * N);
+  int chunks = (int)((P + 8191) / 8192);
+  if (chunks > 256) chunks = 256;
+  if (chunks < 1) chunks = 1;
+  hipLaunchKernelGGL(mask_eval_counts_kernel, dim3(chunks, N), dim3(256), 0, st, P, x, ldx, tgt, ldt,
+                     (unsigned long long*)counts);
+  return (int)hipGetLastError();
+}

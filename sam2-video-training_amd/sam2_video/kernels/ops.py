@@ -508,3 +508,18 @@ def mask_down_stage(x, w, bias, gamma, beta, eps, *, logits=None, scale=1.0, shi
          int(logits is not None), float(scale), float(shift), ptr(w), ptr(bias), ptr(gamma), ptr(beta), float(eps),
          ptr(y), stream())
     return y
+
+
+def mask_eval_counts(logits, tgt):
+    """[N, 4] int64 counts (|pred & gt|, |pred | gt|, |pred|, |gt|) per category, pred = logits > 0.
+    logits [N, ...] fp32, tgt [N, ...] bool/uint8 of the same pixel count."""
+    N = logits.shape[0]
+    x = logits.reshape(N, -1)
+    t = tgt.reshape(N, -1)
+    if t.dtype == torch.bool:
+        t = t.view(torch.uint8)
+    assert x.dtype == torch.float32 and t.dtype == torch.uint8 and x.shape == t.shape
+    assert x.stride(-1) == 1 and t.stride(-1) == 1
+    out = torch.empty(N, 4, device=x.device, dtype=torch.int64)
+    call("s2h_mask_eval_counts", N, x.shape[1], ptr(x), x.stride(0), ptr(t), t.stride(0), ptr(out), stream())
+    return out

@@ -19,6 +19,7 @@ from typing import Any, Dict, List
 import torch
 from torch import nn
 
+from ..eval.eval import evaluate_clip
 from ..model.build import instantiate
 from ..model.losses import CORE_LOSS_KEY, BCECategoryLoss, MultiStepMultiMasksAndIous
 from .ddp import ArenaGradReducer
@@ -128,7 +129,10 @@ class SAM2LightningModule(nn.Module):
 
     @torch.no_grad()
     def validation_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
-        """trainer.py:291-322 (loss only, no gradient tape)"""
+        """trainer.py:291-322 (loss, no gradient tape) plus the reference's offline evaluation
+        metrics computed in the loop on every frame (eval/eval.py: IoU / Dice / MAE of the
+        category-merged binarised masks, averaged as get_video_scores does): val/iou,
+        val/dice, val/mae."""
         outs_per_frame, _ = self.forward(batch)
         outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
         losses = self.criterion(outs, targets)
@@ -136,6 +140,10 @@ class SAM2LightningModule(nn.Module):
         for k, v in losses.items():
             if k not in (CORE_LOSS_KEY, "logits"):
                 self.log(f"val/{k}", v)
+        scores = evaluate_clip(outs_per_frame, batch.masks)
+        self.last_eval = scores
+        for k, v in scores["avg_scores"].items():
+            self.log(f"val/{k}", v)
         return losses[CORE_LOSS_KEY]
 
 
