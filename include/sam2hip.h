@@ -80,9 +80,13 @@ int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
              const float* cscale, float drop_p, uint64_t seed,
              float alpha, float beta, int act, hipStream_t stream);
 
-/* A/B switch (tests, benchmarks): glds_enable = 0 keeps every bf16 GEMM on the
- * register-staged kernel instead of the LDS-DMA one; returns the previous setting. */
-int s2h_gemm_config(int glds_enable);
+/* A/B switch (tests, benchmarks) for the bf16 GEMM tiling; returns the previous setting.
+ * 0 = automatic by shape, -1 = register-staged kernel, LDS-DMA tilings: 1 = 64x64,
+ * 2 = 128x128, 3 = 128x128 with a 3-deep ring, 4 = 256x128, 5 = 256x256, 6 = 128x256,
+ * 7 = 128x64, 8 = 64x128, 9 = 64x64 with a 3-deep ring;
+ * bits 8+ are measurement-only ablations of the LDS-DMA kernel (results are wrong):
+ * 256 = skip the epilogue stores, 512 = skip the MFMAs. */
+int s2h_gemm_config(int cfg);
 
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),

@@ -19,6 +19,7 @@ struct GemmArgs16 {
   int out_f32;
   int vecC;  // 4-column output groups are vector-aligned
   float* rowsum;  // optional: rowsum[b*M + m] += sum_k A[b](m, k)  (fused bias gradient)
+  int dbg;        // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs
 };
 
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);

@@ -11,6 +11,8 @@
 // transposed reads).  K is split over workgroups (fp32 atomic accumulate into
 // the output) when the output tile count cannot fill the 256 CUs -- the weight
 // gradients reduce over 10^4-10^5 rows into a few hundred KB.
+#include <type_traits>
+
 #include "gemm16.h"
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
@@ -116,7 +118,7 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
       for (int e = 0; e < 4; ++e) t[e] = (bf16)v[e];
       *(uint2*)X = *(const uint2*)t;
     } else {
-      for (int e = 0; e < 4 && e < nval; ++e) X[e] = (bf16)v[e];
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) X[e] = (bf16)v[e];
     }
   }
   if (p.aux_mode == 2) {  // multiply by act'(pre-activation)
@@ -172,7 +174,7 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] += (float)rb[e];
     } else {
-      for (int e = 0; e < 4 && e < nval; ++e) v[e] += (float)R[e];
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) v[e] += (float)R[e];
     }
   }
   const int64_t co = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
@@ -186,7 +188,7 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
       }
       *(float4*)C = o;
     } else {
-      for (int e = 0; e < 4 && e < nval; ++e) C[e] = v[e] + (p.beta != 0.f ? p.beta * C[e] : 0.f);
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) C[e] = v[e] + (p.beta != 0.f ? p.beta * C[e] : 0.f);
     }
   } else {
     bf16* C = (bf16*)p.C + co;
@@ -203,8 +205,17 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
       }
       *(uint2*)C = *(const uint2*)o;
     } else {
-      for (int e = 0; e < 4 && e < nval; ++e) C[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)C[e] : 0.f));
+      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) C[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)C[e] : 0.f));
     }
+  }
+}
+
+// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
   }
 }
 
@@ -324,13 +335,13 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
 // Requirements (else the register-staged kernel above runs): 16-B aligned bases, row
 // strides and batch strides multiple of 8 elements, the contiguous extent of every
 // operand a multiple of 8.
-template <int ROWS, bool KC>
+template <int ROWS, bool KC, int NW = 4>
 struct GImg {
   static constexpr int BK = 64;
   static constexpr int RB = KC ? 128 : ROWS * 2;       // bytes per image row
   static constexpr int BYTES = ROWS * BK * 2;
   static constexpr int PIECES = BYTES / 1024;          // 1-KiB DMA pieces
-  static constexpr int PPW = PIECES / 4;               // per wave (4 waves)
+  static constexpr int PPW = PIECES / NW;              // per wave
   static constexpr int LPR = RB / 16;                  // lanes (16-B chunks) per image row
   static_assert(PPW >= 1, "tile too small");
 
@@ -363,7 +374,7 @@ struct GImg {
   // zero the k >= kvalid part of the image (last K step only)
   __device__ static __forceinline__ void zero_tail(char* img, int kvalid, int tid) {
     bf16* e = (bf16*)img;
-    for (int i = tid; i < ROWS * BK; i += 256) {
+    for (int i = tid; i < ROWS * BK; i += NW * 64) {
       int r, k;
       if (KC) { r = i / BK; k = i % BK; } else { k = i / ROWS; r = i % ROWS; }
       if (k < kvalid) continue;
@@ -391,18 +402,41 @@ struct GImg {
   }
 };
 
-template <int BM, int BN, bool AKC, bool BKC>
-__global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
+// Tile BM x BN on a WGM x WGN grid of waves (each wave WM x WN of 16x16 accumulators),
+// NS-deep LDS-DMA ring: at the top of K step kt the DMA of stage kt is retired with a counted
+// `s_waitcnt vmcnt` that leaves the NS-2 later stages in flight (raw s_barrier, never
+// __syncthreads inside the loop: its fence would drain them), then stage kt+NS-1 is issued
+// into the buffer step kt-1 just finished reading.
+template <int BM, int BN, int WGM, int WGN, int NS>
+struct GemmShape {
+  static constexpr int NW = WGM * WGN, NT = NW * 64;
+  static constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NI = WN / 16;
+  static constexpr int STAGE_BYTES = 2 * 64 * (BM + BN);
+  static constexpr int MINB = NS * STAGE_BYTES <= 80 * 1024 ? 2 : 1;  // workgroups per CU the LDS allows
+};
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, bool AKC, bool BKC>
+__global__ __launch_bounds__((GemmShape<BM, BN, WGM, WGN, NS>::NT), (GemmShape<BM, BN, WGM, WGN, NS>::MINB))
+void gemm16g_kernel(GemmArgs16 p) {
   if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
+  using SH = GemmShape<BM, BN, WGM, WGN, NS>;
   constexpr int BK = 64;
-  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
-  using IA = GImg<BM, AKC>;
-  using IB = GImg<BN, BKC>;
+  constexpr int NW = SH::NW, NT = SH::NT;
+  constexpr int WM = SH::WM, WN = SH::WN, MI = SH::MI, NI = SH::NI;
+  using IA = GImg<BM, AKC, NW>;
+  using IB = GImg<BN, BKC, NW>;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  constexpr int DPS = IA::PPW + IB::PPW;  // DMA instructions per stage per wave
+  __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WGN, wn = w % WGN;
   // XCD-aware tile order (bijective remap): blocks id, id+8, ... share an XCD; give them
   // consecutive tiles of one row block so its A tile stays in that XCD's L2
   const int nwg = gridDim.x, id = blockIdx.x;
@@ -425,20 +459,25 @@ __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
   const bool do_rs = p.rowsum != nullptr && n0 == 0 && tid < BM;
   float rs = 0.f;
 
-  for (int kt = 0; kt < nk; ++kt) {
-    char* sa = smem + (kt & 1) * STAGE;
-    char* sb = sa + IA::BYTES;
-    if (kt == 0) {
-      IA::dma(sa, A, p.lda_m, p.lda_k, m0, kbeg, p.M, kend, w, lane);
-      IB::dma(sb, B, p.ldb_n, p.ldb_k, n0, kbeg, p.N, kend, w, lane);
+#pragma unroll
+  for (int st = 0; st < NS - 1; ++st) {  // prologue: stages 0 .. NS-2 in flight
+    if (st < nk) {
+      char* sa = smem + st * STAGE;
+      IA::dma(sa, A, p.lda_m, p.lda_k, m0, kbeg + st * BK, p.M, kend, w, lane);
+      IB::dma(sa + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + st * BK, p.N, kend, w, lane);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  for (int kt = 0; kt < nk; ++kt) {
+    char* sa = smem + (kt % NS) * STAGE;
+    char* sb = sa + IA::BYTES;
+    if (kt + NS - 2 < nk) vm_wait<(NS - 2) * DPS>();  // stage kt retired, NS-2 later ones stay in flight
+    else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + 1 < nk) {  // next step's DMA runs under this step's MFMAs
-      char* na = smem + ((kt + 1) & 1) * STAGE;
-      IA::dma(na, A, p.lda_m, p.lda_k, m0, kbeg + (kt + 1) * BK, p.M, kend, w, lane);
-      IB::dma(na + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + 1) * BK, p.N, kend, w, lane);
+    if (kt + NS - 1 < nk) {  // refill the buffer step kt-1 read; runs under this step's MFMAs
+      char* na = smem + ((kt + NS - 1) % NS) * STAGE;
+      IA::dma(na, A, p.lda_m, p.lda_k, m0, kbeg + (kt + NS - 1) * BK, p.M, kend, w, lane);
+      IB::dma(na + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + NS - 1) * BK, p.N, kend, w, lane);
     }
     const int kvalid = kend - (kbeg + kt * BK);
     if (kvalid < BK) {  // K tail: zero the invalid k of both images (last step only)
@@ -454,6 +493,7 @@ __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
         rs += (float)*(const bf16*)(sa + byte);
       }
     }
+    if (p.dbg & 2) continue;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 a[MI], b[NI];
@@ -472,11 +512,16 @@ __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
   __syncthreads();
 
   if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
+  // Epilogue through LDS: each wave stages one 16-row slab of its accumulators, then every
+  // lane finishes 4 consecutive columns of a row (epilogue4) with 8-/16-byte stores; rows of
+  // a wave-instruction are 128-B column runs.  (A register-direct variant with swapped MFMA
+  // operands -- 4 consecutive columns per lane, no staging -- measured 1.5-2.6x slower: its
+  // stores scatter 16 rows x 32 B per instruction, and split-K atomics likewise.)
   constexpr int EPLD = WN + 4;
-  static_assert(4 * 16 * EPLD * 4 <= 2 * STAGE, "epilogue staging fits");
+  static_assert(NW * 16 * EPLD * 4 <= NS * STAGE, "epilogue staging fits");
   float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
   float bcol[4];
-  load_bcol(p, n0 + wn * WN + 4 * ((lane) % (WN / 4)), bcol);
+  load_bcol(p, n0 + wn * WN + 4 * (lane % (WN / 4)), bcol);
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
 #pragma unroll
@@ -500,20 +545,11 @@ __global__ __launch_bounds__(256, 2) void gemm16g_kernel(GemmArgs16 p) {
         const int rl = rg + ps * RPP;
         const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
         const int row = m0 + wm * WM + i * 16 + rl;
-        if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol);
+        if (row < p.M && !(p.dbg & 1)) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol);
       }
     }
     __syncthreads();
   }
-}
-
-static int g_gemm_glds = 1;
-
-// A/B switch (tests, benchmarks): 0 keeps every bf16 GEMM on the register-staged kernel.
-extern "C" int s2h_gemm_config(int glds_enable) {
-  const int prev = g_gemm_glds;
-  g_gemm_glds = glds_enable;
-  return prev;
 }
 
 static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
@@ -525,8 +561,8 @@ static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
          (batch == 1 || (a.sA % 8 == 0 && a.sB % 8 == 0)) && a.K > 0;
 }
 
-template <int BM, int BN>
-static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
+// split-K decision + output-group alignment for a BM x BN tiling
+static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * batch;
   a.splits = 1;
   a.kchunk = a.K;
@@ -550,15 +586,25 @@ static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
   }
   // 4-column output groups: 16-B (f32) / 8-B (bf16) aligned
   a.vecC = ((uintptr_t)a.C % (a.out_f32 ? 16 : 8) == 0) && a.ldc % 4 == 0 && (batch == 1 || a.sC % 4 == 0);
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS>
+static int launch_glds(GemmArgs16& a, int batch, hipStream_t st) {
+  plan_splits(a, batch, BM, BN, st);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
-  if (g_gemm_glds && gemm_glds_ok(a, batch)) {
-    dim3 g1(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, batch * a.splits);
-    if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, true, true>), g1, dim3(256), 0, st, a);
-    else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, true, false>), g1, dim3(256), 0, st, a);
-    else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, false, true>), g1, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, false, false>), g1, dim3(256), 0, st, a);
-    return (int)hipGetLastError();
-  }
+  constexpr int NT = GemmShape<BM, BN, WGM, WGN, NS>::NT;
+  dim3 g1(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, batch * a.splits);
+  if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, true, true>), g1, dim3(NT), 0, st, a);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, true, false>), g1, dim3(NT), 0, st, a);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, false, true>), g1, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, false, false>), g1, dim3(NT), 0, st, a);
+  return (int)hipGetLastError();
+}
+
+template <int BM, int BN>
+static int launch16_regs(GemmArgs16& a, int batch, hipStream_t st) {
+  plan_splits(a, batch, BM, BN, st);
+  const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * a.splits);
   if (akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, true>), grid, dim3(256), 0, st, a);
   else if (akc && !bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, false>), grid, dim3(256), 0, st, a);
@@ -567,9 +613,50 @@ static int launch16_tiles(GemmArgs16& a, int batch, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// LDS-DMA tilings (s2h_gemm_config selects one for A/B measurements; 0 = automatic)
+enum GemmCfg {
+  CFG_AUTO = 0, CFG_64 = 1, CFG_128 = 2, CFG_128_NS3 = 3, CFG_256x128 = 4, CFG_256 = 5, CFG_128x256 = 6,
+  CFG_128x64 = 7, CFG_64x128 = 8, CFG_64_NS3 = 9
+};
+static int g_gemm_cfg = CFG_AUTO;
+static int g_gemm_dbg = 0;
+
+extern "C" int s2h_gemm_config(int cfg) {
+  const int prev = g_gemm_cfg | (g_gemm_dbg << 8);
+  g_gemm_cfg = cfg < 0 ? cfg : (cfg & 0xff);
+  g_gemm_dbg = cfg < 0 ? 0 : (cfg >> 8);
+  return prev;
+}
+
+// Tiling by shape, from tools/gemm_probe.py on MI355X (profiles/r01_v9_gemm_probe.log):
+// on this step's shapes (M = 10^4-10^5 rows, N and K of 64..2048) the 64^2 tile wins almost
+// everywhere -- 16 KB of LDS per stage lets ~8 workgroups share a CU, and that occupancy hides
+// the LDS-DMA latency the 2-deep ring cannot (128^2: 1.1-1.5x slower, weight gradients 1.5x);
+// 256^2 (8 waves) only pays on large square problems.
+static int pick_cfg(const GemmArgs16& a, int batch) {
+  const long t256 = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * batch;
+  if (a.M >= 1024 && a.N >= 1024 && a.K >= 1024 && t256 >= 128) return CFG_256;
+  return CFG_64;
+}
+
 int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   GemmArgs16 a = in;
-  const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch;
-  if (t128 >= 256 || (a.M >= 128 && a.N >= 128 && a.K >= 1024)) return launch16_tiles<128, 128>(a, batch, st);
-  return launch16_tiles<64, 64>(a, batch, st);
+  a.dbg = g_gemm_dbg;
+  const int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
+  if (cfg < 0 || !gemm_glds_ok(a, batch)) {  // register-staged fallback (unaligned operands)
+    const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch;
+    if (t128 >= 256 || (a.M >= 128 && a.N >= 128 && a.K >= 1024)) return launch16_regs<128, 128>(a, batch, st);
+    return launch16_regs<64, 64>(a, batch, st);
+  }
+  switch (cfg) {
+    case CFG_64: return launch_glds<64, 64, 2, 2, 2>(a, batch, st);
+    case CFG_128_NS3: return launch_glds<128, 128, 2, 2, 3>(a, batch, st);
+    case CFG_256x128: return launch_glds<256, 128, 4, 2, 2>(a, batch, st);
+    case CFG_256: return launch_glds<256, 256, 2, 4, 2>(a, batch, st);
+    case CFG_128x256: return launch_glds<128, 256, 2, 4, 2>(a, batch, st);
+    case CFG_128x64: return launch_glds<128, 64, 2, 2, 2>(a, batch, st);
+    case CFG_64x128: return launch_glds<64, 128, 2, 2, 2>(a, batch, st);
+    case CFG_64_NS3: return launch_glds<64, 64, 2, 2, 3>(a, batch, st);
+    default: return launch_glds<128, 128, 2, 2, 2>(a, batch, st);
+  }
 }

@@ -84,6 +84,34 @@ def test_gemm_lds_dma_path(M, N, K, layout):
     _close(o32, ref + 3.0, 2e-3)
 
 
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, -1])
+@pytest.mark.parametrize("M,N,K", [(1000, 520, 200), (600, 264, 1100), (13312, 256, 256)])
+@pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
+def test_gemm_every_tiling(cfg, M, N, K, layout):
+    """each forced tiling (64^2, 128^2 2/3-deep ring, 256x128, 256^2, 128x256, register-staged)
+    on ragged shapes and every operand layout, with the fused epilogue and fp32 accumulate"""
+    from sam2_video.kernels import _lib
+    ops = _ops()
+    torch.manual_seed(11)
+    bf = torch.bfloat16
+    a = torch.randn(M, K, device=DEV).to(bf) if layout[0] == "n" else torch.randn(K, M, device=DEV).to(bf).t()
+    b = torch.randn(K, N, device=DEV).to(bf) if layout[1] == "n" else torch.randn(N, K, device=DEV).to(bf).t()
+    ref = a.float() @ b.float()
+    kw = dict(M=M, N=N, K=K, lda_m=a.stride(0), lda_k=a.stride(1), ldb_k=b.stride(0), ldb_n=b.stride(1), ldc=N)
+    prev = _lib.lib().s2h_gemm_config(cfg)
+    try:
+        out = torch.empty(M, N, device=DEV, dtype=bf)
+        bias = torch.randn(N, device=DEV)
+        res = torch.randn(M, N, device=DEV).to(bf)
+        ops.gemm(a, b, out, bias=bias, residual=res, ldr=N, act=1, **kw)
+        _close(out, torch.relu(ref + bias) + res.float(), 1e-2)
+        o32 = torch.full((M, N), 3.0, device=DEV)
+        ops.gemm(a, b, o32, beta=1.0, **kw)
+        _close(o32, ref + 3.0, 2e-3)
+    finally:
+        _lib.lib().s2h_gemm_config(prev)
+
+
 @pytest.mark.parametrize("rows,N,K", [(20000, 336, 112), (131072, 112, 336), (13312, 256, 256), (4099, 130, 77)])
 def test_wgrad_split_k(rows, N, K):
     """Weight gradients reduce over 10^4-10^5 rows into few output tiles: the bf16 GEMM
