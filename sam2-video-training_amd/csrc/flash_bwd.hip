@@ -31,6 +31,8 @@ struct FlashBwdArgs {
   float p_drop; uint32_t thresh; float inv_keep; uint64_t seed; const uint64_t* seed_off;
   int splits, tiles_per_split;
   float* ws_dq;  // [splits][BH*Lq][DP] fp32 partial dQ (splits > 1)
+  int kv_splits, kv_tiles_per_split;  // dK/dV kernel: query range split over workgroups
+  float* ws_dkv;  // [kv_splits][BH*Lk][2][DP] fp32 partial (dK, dV) (kv_splits > 1)
 };
 
 // ------------------------------------------------------------------ Di
@@ -337,7 +339,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
   const bf16* K = a.k + b * a.skb + h * a.skh;
   const bf16* V = a.v + b * a.svb + h * a.svh;
-  const int nt = (a.Lq + QT - 1) / QT;
+  // query tiles [qt0, qt0 + nt) of this workgroup (kv_splits > 1: partial dK / dV)
+  const int nt_all = (a.Lq + QT - 1) / QT;
+  const int qt0 = blockIdx.z * a.kv_tiles_per_split;
+  const int nt = max(0, min(nt_all, qt0 + a.kv_tiles_per_split) - qt0);
+  const int qbase = qt0 * QT;
 
   const float* LSE = a.lse + (int64_t)bh * a.Lq;
   const float* DI = a.di + (int64_t)bh * a.Lq;
@@ -349,9 +355,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
                                      (__attribute__((address_space(3))) void*)(stage + 2 * C::TILEB + w * 256), 4, 0, 0);
   };
   dma_tile<DP, NWV * 32, NWV>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
-  dma_tile<DP, QT, NWV>(stages, Q, a.sql, 0, a.Lq, w, lane);
-  dma_tile<DP, QT, NWV>(stages + C::TILEB, G, a.sgl, 0, a.Lq, w, lane);
-  dma_rows(stages, 0);
+  dma_tile<DP, QT, NWV>(stages, Q, a.sql, qbase, a.Lq, w, lane);
+  dma_tile<DP, QT, NWV>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
+  dma_rows(stages, qbase);
   bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, a.Lk - 1);
 #pragma unroll
@@ -364,7 +370,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     dv[d] = f32x16{};
   }
   for (int it = 0; it < nt; ++it) {
-    const int q0 = it * QT;
+    const int q0 = qbase + it * QT;
     char* Qb = stages + (it & 1) * STAGE;
     char* Gb = Qb + C::TILEB;
     const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 256);  // [lse(32) | Di(32)]
@@ -416,6 +422,18 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   }
 
   if (!kv) return;
+  if (a.kv_splits > 1) {  // fp32 partials, summed (and scaled, cast) by flash_bwd_dkv_combine_kernel
+    float* W = a.ws_dkv + (((int64_t)blockIdx.z * a.BH + bh) * a.Lk + key) * 2 * DP;
+#pragma unroll
+    for (int d = 0; d < ND; ++d)
+#pragma unroll
+      for (int G4 = 0; G4 < 4; ++G4) {
+        const int d0 = 32 * d + 8 * G4 + 4 * hi;
+        *(float4*)(W + d0) = float4{dk[d][4 * G4], dk[d][4 * G4 + 1], dk[d][4 * G4 + 2], dk[d][4 * G4 + 3]};
+        *(float4*)(W + DP + d0) = float4{dv[d][4 * G4], dv[d][4 * G4 + 1], dv[d][4 * G4 + 2], dv[d][4 * G4 + 3]};
+      }
+    return;
+  }
   bf16* DK = a.dk + b * a.sdkb + h * a.sdkh + (int64_t)key * a.sdkl;
   bf16* DV = a.dv + b * a.sdvb + h * a.sdvh + (int64_t)key * a.sdvl;
 #pragma unroll
@@ -434,7 +452,40 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     }
 }
 
+// dK = scale * sum_s partial_dK[s], dV = sum_s partial_dV[s]; 4 consecutive d per thread
+template <int DP>
+__global__ __launch_bounds__(256) void flash_bwd_dkv_combine_kernel(FlashBwdArgs a) {
+  const int64_t rows = (int64_t)a.BH * a.Lk;
+  const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;  // over rows * 2 * DP
+  if (i >= rows * 2 * DP) return;
+  float4 s = *(const float4*)(a.ws_dkv + i);
+  for (int sp = 1; sp < a.kv_splits; ++sp) {
+    const float4 t = *(const float4*)(a.ws_dkv + sp * rows * 2 * DP + i);
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  const int64_t row = i / (2 * DP);
+  const int part = (int)((i / DP) & 1), d = (int)(i % DP);
+  const int bh = row / a.Lk, key = row % a.Lk, b = bh / a.H, h = bh % a.H;
+  const float f = part == 0 ? a.scale : 1.f;
+  bf16 t4[4] = {(bf16)(s.x * f), (bf16)(s.y * f), (bf16)(s.z * f), (bf16)(s.w * f)};
+  bf16* dst = part == 0 ? a.dk + b * a.sdkb + h * a.sdkh + (int64_t)key * a.sdkl + d
+                        : a.dv + b * a.sdvb + h * a.sdvh + (int64_t)key * a.sdvl + d;
+  *(uint2*)dst = *(const uint2*)t4;
+}
+
 // ------------------------------------------------------------------ host
+// dK/dV (head_dim 256): 128-key workgroups, one per CU; when they cannot fill the chip
+// (short key ranges: the memory-attention self-attention, Lk = 1024 x 13 objects = 104
+// blocks) the query range is split over workgroups with fp32 partials.
+static void flash_bwd_kv_plan(int BH, int Lq, int Lk, int& kv_splits, int& tps) {
+  const int base = ((Lk + 127) / 128) * BH;
+  const int nt = (Lq + 31) / 32;
+  int s = base >= 256 ? 1 : 256 / base;
+  s = std::max(1, std::min(s, nt / 4));
+  tps = (nt + s - 1) / s;
+  kv_splits = (nt + tps - 1) / tps;
+}
+
 static void flash_bwd_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
   const int base = ((Lq + FL_QB - 1) / FL_QB) * BH;
   const int ntiles = (Lk + 63) / 64;
@@ -444,10 +495,19 @@ static void flash_bwd_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
   splits = (ntiles + tps - 1) / tps;
 }
 
+// [dQ partials][dK/dV partials], each present only when its kernel splits
+static void flash_bwd_ws_layout(int BH, int Lq, int Lk, int D, int64_t& dq_bytes, int64_t& dkv_bytes) {
+  int splits, tps, kvs, ktps;
+  flash_bwd_plan(BH, Lq, Lk, splits, tps);
+  flash_bwd_kv_plan(BH, Lq, Lk, kvs, ktps);
+  dq_bytes = splits > 1 ? (int64_t)splits * BH * Lq * D * 4 : 0;
+  dkv_bytes = (D == 256 && kvs > 1) ? (int64_t)kvs * BH * Lk * 2 * D * 4 : 0;
+}
+
 int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D) {
-  int splits, tps;
-  flash_bwd_plan(B * H, Lq, Lk, splits, tps);
-  return splits > 1 ? (int64_t)splits * B * H * Lq * D * 4 : 0;
+  int64_t dq_bytes, dkv_bytes;
+  flash_bwd_ws_layout(B * H, Lq, Lk, D, dq_bytes, dkv_bytes);
+  return dq_bytes + dkv_bytes;
 }
 
 template <int DP>
@@ -459,9 +519,13 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_bwd_dq_combine_kernel<DP>), dim3((unsigned)((rows * DP / 4 + 255) / 256)), dim3(256), 0,
                        st, a);
-  if constexpr (DP == 256)
-    hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP>), dim3((a.Lk + 127) / 128, a.BH), dim3(256), 0, st, a);
-  else
+  if constexpr (DP == 256) {
+    hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP>), dim3((a.Lk + 127) / 128, a.BH, a.kv_splits), dim3(256), 0, st, a);
+    if (a.kv_splits > 1) {
+      const int64_t n4 = (int64_t)a.BH * a.Lk * 2 * DP / 4;
+      hipLaunchKernelGGL((flash_bwd_dkv_combine_kernel<DP>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
+    }
+  } else
     hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP>), dim3((a.Lk + FL_QB - 1) / FL_QB, a.BH), dim3(FL_WAVES * 64), 0, st,
                        a);
   return (int)hipGetLastError();
@@ -496,13 +560,15 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
   a.seed = seed;
   a.seed_off = s2h_rng_offset_ptr();
   flash_bwd_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
-  const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * D * 4 : 0;
-  if (need > ws_bytes || (need > 0 && ws == nullptr)) {
-    a.splits = 1;
-    a.tiles_per_split = (Lk + 63) / 64;
-  } else if (a.splits > 1) {
-    a.ws_dq = (float*)ws;
+  flash_bwd_kv_plan(a.BH, Lq, Lk, a.kv_splits, a.kv_tiles_per_split);
+  int64_t dq_bytes, dkv_bytes;
+  flash_bwd_ws_layout(a.BH, Lq, Lk, D, dq_bytes, dkv_bytes);
+  if (dq_bytes + dkv_bytes > ws_bytes || (dq_bytes + dkv_bytes > 0 && ws == nullptr)) {
+    return (int)hipErrorInvalidValue;  // the caller sizes ws with s2h_attn_bwd_ws_bytes
   }
+  if (a.splits > 1) a.ws_dq = (float*)ws;
+  if (dkv_bytes > 0) a.ws_dkv = (float*)((char*)ws + dq_bytes);
+  else { a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32; }
   if (D == 256) return flash_bwd_launch<256>(a, st);
   return flash_bwd_launch<128>(a, st);
 }
