@@ -144,6 +144,58 @@ def attention(q, k, v, scale=None, p_drop=0.0):
     return _Attention.apply(q, k, v, float(scale), float(p_drop))
 
 
+class _QKVAttention(torch.autograd.Function):
+    """Self-attention straight from a packed projection output qkv [B, L, 3, H, d] (q, k, v of a
+    token adjacent, as the fused q/k/v GEMM writes them), optional RoPE on q and k (rope =
+    (cos, sin, period), single head: memory-attention self-attention, transformer.py:275-311).
+    The backward writes dq, dk, dv into ONE [B, L, 3, H, d] gradient through strided kernel
+    outputs (inverse RoPE in place): with three separate slice inputs autograd zero-fills a
+    qkv-sized buffer per slice and adds them (3 fills + 3 copies + 2 adds per attention)."""
+
+    @staticmethod
+    def forward(ctx, qkv, scale, p_drop, rope):
+        B, L, _, H, D = qkv.shape
+        q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+        if rope is not None:
+            cos, sin, period = rope
+            qk = torch.empty(B, L, 2, H, D, device=qkv.device, dtype=qkv.dtype)
+            ops.rope(q.reshape(B, L, H * D) if q.is_contiguous() else q.view(B, L, H * D), qk[:, :, 0].view(B, L, H * D),
+                     L, cos, sin, period)
+            ops.rope(k.view(B, L, H * D), qk[:, :, 1].view(B, L, H * D), L, cos, sin, period)
+            q, k = qk[:, :, 0], qk[:, :, 1]
+        o = torch.empty(B, L, H, D, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(B, H, L, device=qkv.device, dtype=torch.float32)
+        seed = next_seed() if p_drop > 0 else 0
+        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed)
+        ctx.scale, ctx.p, ctx.seed, ctx.rope = scale, p_drop, seed, rope
+        ctx.save_for_backward(qkv, qk if rope is not None else qkv, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, qk, o, lse = ctx.saved_tensors
+        B, L, _, H, D = qkv.shape
+        q, k = qk[:, :, 0], qk[:, :, 1]
+        v = qkv[:, :, 2]
+        dqkv = torch.empty(qkv.shape, device=qkv.device, dtype=qkv.dtype)
+        dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
+        ops.attn_bwd(q, k, v, o, do.contiguous(), lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed)
+        if ctx.rope is not None:
+            cos, sin, period = ctx.rope
+            for g in (dq, dk):
+                g3 = g.view(B, L, H * D)
+                ops.rope(g3, g3, L, cos, sin, period, inverse=True)
+        return dqkv, None, None, None
+
+
+def qkv_attention(qkv, scale=None, p_drop=0.0, rope=None):
+    """softmax(scale q k^T) v with q, k, v = qkv[:, :, 0/1/2] ([B, L, 3, H, d]); rope = (cos, sin,
+    period) rotates q and k (every row) first."""
+    if scale is None:
+        scale = 1.0 / math.sqrt(qkv.shape[-1])
+    return _QKVAttention.apply(qkv, float(scale), float(p_drop), rope)
+
+
 # ------------------------------------------------------------------ RoPE
 class _Rope(torch.autograd.Function):
     @staticmethod

@@ -35,14 +35,14 @@ class MultiScaleAttention(nn.Module):
         d, nh = self.dim_out, self.num_heads
         qkv = self.qkv(x)  # [B, H, W, 3d]
         qkv5 = qkv.view(B, H * W, 3, nh, d // nh)
-        k, v = qkv5[:, :, 1], qkv5[:, :, 2]
         if self.q_pool:
+            k, v = qkv5[:, :, 1], qkv5[:, :, 2]
             q = FN.maxpool2(qkv[..., :d])  # pooled straight out of the fused qkv (pixel stride 3d)
             H, W = H // 2, W // 2
             q = q.view(B, H * W, nh, d // nh)
+            o = FN.attention(q, k, v)
         else:
-            q = qkv5[:, :, 0]
-        o = FN.attention(q, k, v)
+            o = FN.qkv_attention(qkv5)  # one packed dqkv in the backward
         return self.proj(o.reshape(B, H, W, d))
 
 

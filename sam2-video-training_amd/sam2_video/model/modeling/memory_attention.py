@@ -58,14 +58,18 @@ class MemoryAttentionLayer(nn.Module):
         # self-attention (:58-64), q = k = v = norm1(tgt), RoPE on q and k
         sa = self.self_attn
         t2 = self.norm1(tgt)
-        if self._fused_qkv is not None:
+        if self._fused_qkv is not None and sa.num_heads == 1:
+            # one packed q/k/v GEMM; RoPE + attention read it in place and the backward returns
+            # one packed gradient (FN.qkv_attention)
             qkv = self._fused_qkv(t2)
-            q, k, v = qkv[..., :C], qkv[..., C:2 * C], qkv[..., 2 * C:]
+            cos, sin = sa.tables(L, qkv.device)
+            o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p(), rope=(cos, sin, L))
+            tgt = sa.out_proj(o.reshape(qkv.shape[0], L, C), residual=tgt, drop_p=p)
         else:
             q, k, v = sa.q_proj(t2), sa.k_proj(t2), sa.v_proj(t2)
-        q = sa.rope_q(q, L)
-        k = sa.rope_k(k, L)
-        tgt = sa.attend(q, k, v, residual=tgt, out_drop=p)
+            q = sa.rope_q(q, L)
+            k = sa.rope_k(k, L)
+            tgt = sa.attend(q, k, v, residual=tgt, out_drop=p)
         # cross-attention to the memory bank (:66-81)
         ca = self.cross_attn_image
         t2 = self.norm2(tgt)
