@@ -62,9 +62,13 @@ class MultiScaleBlock(nn.Module):
         if dim != dim_out:
             self.proj = Linear(dim, dim_out)
 
-    def forward(self, x):
+    def forward(self, x, xn=None, next_norm=None):
+        """x: residual stream [B, H, W, C]; xn = norm1(x) when the previous block already produced
+        it (fused with its residual add).  With next_norm, returns (x', next_norm(x')) from one
+        fused add + LayerNorm so the stream has a single autograd consumer; else x'."""
         B = x.shape[0]
-        xn = self.norm1(x)
+        if xn is None:
+            xn = self.norm1(x)
         shortcut = x
         if self.dim != self.dim_out:
             shortcut = self.proj(xn)
@@ -81,7 +85,10 @@ class MultiScaleBlock(nn.Module):
             y = FN.window_unpartition(y, ws, B, H, W)
         h, x = FN.add_layer_norm(shortcut, y, self.norm2, self.norm2.eps)
         h = self.mlp.layers[0](h, act="gelu")
-        return self.mlp.layers[1](h, residual=x)
+        if next_norm is None:
+            return self.mlp.layers[1](h, residual=x)
+        t, x = FN.add_layer_norm(x, self.mlp.layers[1](h), next_norm, next_norm.eps)
+        return x, t
 
 
 class PatchEmbed(nn.Module):
@@ -142,8 +149,13 @@ class Hiera(nn.Module):
         pe = hiera_pos_embed(self.pos_embed, self.pos_embed_window, x.shape[1], x.shape[2], x.dtype)
         x = FN.add_bcast(x, pe)
         outputs = []
+        t = None
         for i, blk in enumerate(self.blocks):
-            x = blk(x)
-            if (i == self.stage_ends[-1]) or (i in self.stage_ends and self.return_interm_layers):
+            is_out = (i == self.stage_ends[-1]) or (i in self.stage_ends and self.return_interm_layers)
+            if is_out or i + 1 == len(self.blocks):
+                x, t = blk(x, t), None
+            else:
+                x, t = blk(x, t, next_norm=self.blocks[i + 1].norm1)
+            if is_out:
                 outputs.append(x)
         return outputs

@@ -51,6 +51,35 @@ class MemoryAttentionLayer(nn.Module):
     def _drop(self):
         return self.dropout_value if self.training else 0.0
 
+    def sublayers(self, x, t, mem_k, mem_v, num_k_exclude_rope, next_norm):
+        """The layer on the residual stream x with t = norm1(x) given; returns (x', next_norm(x')).
+        Every residual add is fused with the LayerNorm that reads its result (FN.add_layer_norm:
+        LN(x + y) and x + y from one kernel, and in the backward LN'(.) + the stream's gradient
+        in one pass), so each residual state has a single autograd consumer and no separate
+        gradient-accumulation adds run (memory_attention.py:58-99 order and dropouts)."""
+        L = x.shape[1]
+        C = self.d_model
+        p = self._drop()
+        sa = self.self_attn
+        if self._fused_qkv is not None and sa.num_heads == 1:
+            qkv = self._fused_qkv(t)
+            cos, sin = sa.tables(L, qkv.device)
+            o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p(), rope=(cos, sin, L))
+            y = sa.out_proj(o.reshape(qkv.shape[0], L, C), drop_p=p)
+        else:
+            q = sa.rope_q(sa.q_proj(t), L)
+            k = sa.rope_k(sa.k_proj(t), L)
+            y = sa.attend(q, k, sa.v_proj(t), out_drop=p)
+        t, x = FN.add_layer_norm(x, y, self.norm2, self.norm2.eps)
+        ca = self.cross_attn_image
+        q = ca.rope_q(ca.q_proj(t), L)
+        k = ca.rope_k(ca.k_proj(mem_k), L, num_k_exclude_rope)
+        y = ca.attend(q, k, ca.v_proj(mem_v), out_drop=p)
+        t, x = FN.add_layer_norm(x, y, self.norm3, self.norm3.eps)
+        y = self.linear2(self.linear1(t, act="relu", drop_p=p), drop_p=p)
+        t, x = FN.add_layer_norm(x, y, next_norm, next_norm.eps)
+        return x, t
+
     def forward(self, tgt, mem_k, mem_v, num_k_exclude_rope=0):
         L = tgt.shape[1]
         C = self.d_model
@@ -103,6 +132,8 @@ class MemoryAttention(nn.Module):
         x = FN.add(curr, curr_pos, beta=0.1) if self.pos_enc_at_input else curr
         x = FN.expand_batch(x.unsqueeze(0), num_objects)
         mem_k = FN.add_bcast(memory, memory_pos_table)
-        for layer in self.layers:
-            x = layer(x, mem_k, memory, num_k_exclude_rope=num_obj_ptr_tokens)
-        return self.norm(x)
+        t = self.layers[0].norm1(x)
+        for i, layer in enumerate(self.layers):
+            nxt = self.layers[i + 1].norm1 if i + 1 < len(self.layers) else self.norm
+            x, t = layer.sublayers(x, t, mem_k, memory, num_obj_ptr_tokens, nxt)
+        return t  # = self.norm(x) (memory_attention.py:167)
