@@ -171,6 +171,10 @@ int s2h_cast(int dt_in, int dt_out, int64_t n, const void* x, void* y, hipStream
 /* out = a + dropout(b) (b may be NULL: out = dropout(a)); nn.Dropout at
  * memory_attention.py:40-48 and the post-attention / FFN dropouts. */
 int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out, hipStream_t st);
+/* dx = act'(x_pre) * keep(i) / (1 - p) * dy in one pass: the backward of a Linear epilogue's
+ * act -> dropout (memory_attention.py:95-98); x_pre NULL = no activation. */
+int s2h_act_dropout_bwd(int dt, int64_t n, const void* x_pre, const void* dy, int act, float p, uint64_t seed,
+                        void* dx, hipStream_t st);
 /* Axial rotary embedding of the first `nrot` rows of each batch (cos/sin tables
  * [period, D/2], row r uses entry r % period; inverse = 1 applies the transpose
  * rotation for the backward).  Replaces apply_rotary_enc (position_encoding.py:212-239)

@@ -85,6 +85,28 @@ extern "C" int s2h_act_bwd(int dt, int64_t n, const void* x, const void* dy, int
   return (int)hipGetLastError();
 }
 
+// dx = act'(x_pre) * keep(i) / (1 - p) * dy: the backward of act -> dropout in one pass (the
+// Linear epilogue's forward order, memory_attention.py:95-98 linear1 + ReLU + dropout).  The
+// mask is the forward's counter hash of the flat output index.  x_pre may be null (no act).
+template <typename T>
+__global__ void act_dropout_bwd_kernel(int64_t n, const void* x, const void* dy, int act, float p, uint64_t seed,
+                                       const uint64_t* seed_off, void* dx) {
+  seed = s2h_seed(seed, seed_off);
+  const uint32_t thresh = (uint32_t)(p * 4294967296.0);
+  const float inv = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  GRID_STRIDE(i, n) {
+    float v = (p > 0.f && !s2h_keep(seed, (uint64_t)i, thresh)) ? 0.f : to_f32(((const T*)dy)[i]) * inv;
+    if (x) v *= act_grad(to_f32(((const T*)x)[i]), act);
+    ((T*)dx)[i] = from_f32<T>(v);
+  }
+}
+extern "C" int s2h_act_dropout_bwd(int dt, int64_t n, const void* x_pre, const void* dy, int act, float p,
+                                   uint64_t seed, void* dx, hipStream_t st) {
+  if (n <= 0) return 0;
+  DISPATCH_T(dt, act_dropout_bwd_kernel, ew_grid(n), n, x_pre, dy, act, p, seed, s2h_rng_offset_ptr(), dx);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------ casts
 __global__ void cast_f32_bf16_kernel(int64_t n, const float* x, bf16* y) { GRID_STRIDE(i, n) y[i] = (bf16)x[i]; }
 __global__ void cast_bf16_f32_kernel(int64_t n, const bf16* x, float* y) { GRID_STRIDE(i, n) y[i] = (float)x[i]; }

@@ -12,9 +12,10 @@
 // rounded to the compute dtype as the unfused path stores it; zero padding is
 // applied to the transformed mask (F.conv2d pads its input with zeros).
 //
-// Weights stay in PyTorch order [cout][cin][3][3] (fp32); their indices are wave-
-// uniform compile-time offsets, so they are fetched with scalar loads and used as
-// SGPR operands.  HBM-bound: reads O*H*W*cin, writes O*H/2*W/2*cout elements.
+// Weights arrive in PyTorch order [cout][cin][3][3] (fp32) and are transposed into LDS as
+// [tap][cin][cout] per block (4 output channels per broadcast ds_read_b128; per-weight scalar
+// loads in a rolled tap loop measured 180 us for the 16 -> 64 stage).  HBM-bound: reads
+// O*H*W*cin, writes O*H/2*W/2*cout elements.
 #include "common.h"
 
 template <typename T, int CIN, int COUT, bool LOGIT>
@@ -23,6 +24,14 @@ __global__ __launch_bounds__(256) void mask_down_kernel(int O, int H, int W, int
                                                         const float* __restrict__ bias,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, T* y) {
+  // weights transposed into LDS as [tap][ci][co]: the inner loop reads 4 output channels per
+  // ds_read_b128, the same address on every lane (broadcast)
+  __shared__ __attribute__((aligned(16))) float wl[9 * CIN * COUT];
+  for (int e = threadIdx.x; e < 9 * CIN * COUT; e += 256) {
+    const int co = e % COUT, ci = (e / COUT) % CIN, tap = e / (COUT * CIN);
+    wl[e] = w[(co * CIN + ci) * 9 + tap];
+  }
+  __syncthreads();
   const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t total = (int64_t)O * Ho * Wo;
   if (p >= total) return;
@@ -33,29 +42,30 @@ __global__ __launch_bounds__(256) void mask_down_kernel(int O, int H, int W, int
   float acc[COUT];
 #pragma unroll
   for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+  for (int tap = 0; tap < 9; ++tap) {
+    const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
+    if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
+    const int64_t pix = ((int64_t)o * H + iy) * W + ix;
+    float in[CIN];
+    if constexpr (LOGIT) {
+      const float v = ((const float*)xin)[pix];
+      in[0] = to_f32(from_f32<T>(scale / (1.f + expf(-v)) + shift));
+    } else {
+      const T* xp = (const T*)xin + pix * CIN;
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    const int iy = 2 * oy - 1 + ky;
-    if (iy < 0 || iy >= H) continue;
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = 2 * ox - 1 + kx;
-      if (ix < 0 || ix >= W) continue;
-      const int64_t pix = ((int64_t)o * H + iy) * W + ix;
-      float in[CIN];
-      if constexpr (LOGIT) {
-        const float v = ((const float*)xin)[pix];
-        in[0] = to_f32(from_f32<T>(scale / (1.f + expf(-v)) + shift));
-      } else {
-        const T* xp = (const T*)xin + pix * CIN;
-#pragma unroll
-        for (int ci = 0; ci < CIN; ++ci) in[ci] = to_f32(xp[ci]);
-      }
-#pragma unroll
-      for (int ci = 0; ci < CIN; ++ci)
-#pragma unroll
-        for (int co = 0; co < COUT; ++co) acc[co] += in[ci] * w[((co * CIN + ci) * 3 + ky) * 3 + kx];
+      for (int ci = 0; ci < CIN; ++ci) in[ci] = to_f32(xp[ci]);
     }
+    const float* wt = wl + tap * CIN * COUT;
+#pragma unroll
+    for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+      for (int co = 0; co < COUT; co += 4) {
+        const float4 w4 = *(const float4*)&wt[ci * COUT + co];
+        acc[co] += in[ci] * w4.x;
+        acc[co + 1] += in[ci] * w4.y;
+        acc[co + 2] += in[ci] * w4.z;
+        acc[co + 3] += in[ci] * w4.w;
+      }
   }
   float s = 0.f;
 #pragma unroll

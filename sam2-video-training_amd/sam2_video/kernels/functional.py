@@ -53,8 +53,10 @@ class _Linear(torch.autograd.Function):
         x, pre = ctx.saved_tensors
         mod = ctx.mod
         dy = dy.contiguous()
-        g = ops.dropout(dy, ctx.drop_p, ctx.seed) if ctx.drop_p > 0 else dy
-        dpre = ops.act_bwd(pre, g, ctx.act) if ctx.act else g
+        if ctx.drop_p > 0:
+            dpre = ops.act_dropout_bwd(pre if ctx.act else None, dy, ctx.act, ctx.drop_p, ctx.seed)
+        else:
+            dpre = ops.act_bwd(pre, dy, ctx.act) if ctx.act else dy
         gw, gb = mod.grad_views()
         if gw is not None:
             ops.linear_wgrad(dpre, x, gw.view(gw.shape[0], -1), db=gb)

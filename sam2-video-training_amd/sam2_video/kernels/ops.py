@@ -230,6 +230,15 @@ def act_fwd(x, act, out=None, scale=1.0, shift=0.0):
     return out
 
 
+def act_dropout_bwd(x_pre, dy, act, p, seed, dx=None):
+    """dx = act'(x_pre) * dropout_mask(seed) / (1 - p) * dy (one pass; x_pre None = no act)"""
+    if dx is None:
+        dx = torch.empty_like(dy)
+    call("s2h_act_dropout_bwd", dt(dy), dy.numel(), ptr(x_pre), ptr(dy), ACT[act], float(p), int(seed) & (2**64 - 1),
+         ptr(dx), stream())
+    return dx
+
+
 def act_bwd(x_pre, dy, act, dx=None, accumulate=False):
     if dx is None:
         dx = torch.empty_like(dy)

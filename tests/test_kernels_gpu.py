@@ -511,3 +511,17 @@ def test_mask_down_stage(dtype, tol, cin, cout, H):
     x = torch.randn(O, H, W, cin, device=DEV).to(dtype)
     y = ops.mask_down_stage(x, w, b, g, be, 1e-6)
     _close(y, ref(x.float()), tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act", [None, "relu", "gelu"])
+def test_act_dropout_bwd_fused(dtype, act):
+    """one-pass act' * dropout backward == dropout backward then act backward (same mask)"""
+    ops = _ops()
+    torch.manual_seed(3)
+    pre = torch.randn(1000, 77, device=DEV).to(dtype)
+    dy = torch.randn(1000, 77, device=DEV).to(dtype)
+    got = ops.act_dropout_bwd(pre if act else None, dy, act, 0.1, 4321)
+    g = ops.dropout(dy, 0.1, 4321)
+    ref = ops.act_bwd(pre, g, act) if act else g
+    _close(got, ref, 1e-2 if dtype == torch.bfloat16 else 1e-6)
