@@ -109,8 +109,9 @@ int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t
  * device workspace of s2h_attn_fwd_ws_bytes(...) bytes (ws = NULL / too small
  * just disables the key split). */
 int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D);
-/* A/B switch (tests, benchmarks): flash_enable = 0 sends every attention to the generic
- * kernels; returns the previous setting. */
+/* A/B switch (tests, benchmarks): bit 0 of flash_enable = 0 sends every attention to the
+ * generic kernels; bits 8+ (if non-zero) set the workgroup count the flash forward key split
+ * aims at (default 256).  Returns the previous setting in the same encoding. */
 int s2h_attn_config(int flash_enable);
 int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,

@@ -247,12 +247,18 @@ __global__ __launch_bounds__(256) void flash_combine_kernel(FlashArgs a) {
   if (lane == 0) a.lse[rowg] = (Mr + log2f(L)) * FL_LN2;
 }
 
-// Split count: aim at ~3 rounds of 256 workgroups, never fewer than 2 tiles per split.
+// Split count: as many key splits as keep the grid within one round of 256 workgroups (one
+// per CU), never fewer than 2 key tiles per split.  Measured on the memory-attention shapes
+// (13 objects x 1024 queries x 1024..7196 keys, d 256, tools/attn_bench.py --targets): 2 splits
+// 50 / 110 / 218 us against 92 / 129 / 247 us for the earlier ~3-round target (768) -- every
+// extra split adds an fp32 [rows][D] partial written and re-read by the combine.
+static int g_flash_fwd_target = 256;  // workgroups the key split aims at (s2h_attn_config bits 8+)
+
 static void flash_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
   const int qblocks = (Lq + FL_QB - 1) / FL_QB;
   const int base = qblocks * BH;
   const int ntiles = (Lk + 63) / 64;
-  int s = (768 + base - 1) / base;
+  int s = g_flash_fwd_target / base;
   s = std::max(1, std::min(s, ntiles / 2));
   tps = (ntiles + s - 1) / s;
   splits = (ntiles + tps - 1) / tps;
@@ -262,8 +268,9 @@ static int g_flash_enabled = 1;
 
 // A/B switch for tests and benchmarks: 0 routes every attention to the generic kernels.
 extern "C" int s2h_attn_config(int flash_enable) {
-  const int prev = g_flash_enabled;
-  g_flash_enabled = flash_enable;
+  const int prev = g_flash_enabled | (g_flash_fwd_target << 8);
+  g_flash_enabled = flash_enable & 0xff;
+  g_flash_fwd_target = (flash_enable >> 8) > 0 ? (flash_enable >> 8) : 256;
   return prev;
 }
 

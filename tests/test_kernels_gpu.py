@@ -224,6 +224,26 @@ def test_flash_forward_matches_reference(B, H, Lq, Lk, D):
     _close(dv, vr.grad, 4e-2)
 
 
+@pytest.mark.parametrize("target", [1, 64, 256, 4096])
+def test_flash_forward_split_counts(target):
+    """Every key-split count (s2h_attn_config bits 8+) gives the reference output."""
+    from sam2_video.kernels._lib import lib
+    ops = _ops()
+    torch.manual_seed(6)
+    B, H, Lq, Lk, D = 2, 1, 512, 2000, 256
+    q, k, v = (torch.randn(B, L, H, D, device=DEV).to(torch.bfloat16) for L in (Lq, Lk, Lk))
+    o = torch.empty_like(q)
+    lse = torch.empty(B, H, Lq, device=DEV)
+    prev = lib().s2h_attn_config(1 | (target << 8))
+    try:
+        ops.attn_fwd(q, k, v, o, lse, 0.0625)
+    finally:
+        lib().s2h_attn_config(prev)
+    ro, rl = _ref_attn(q.float(), k.float(), v.float(), 0.0625)
+    _close(o, ro, 2e-2)
+    _close(lse, rl, 1e-3)
+
+
 def test_flash_dropout_matches_generic_kernel():
     """Same counter-hash dropout mask in the flash and the generic forward (the backward
     regenerates it), so both produce the same output up to bf16 rounding."""

@@ -30,11 +30,31 @@ def timeit(fn, iters):
     return s.elapsed_time(e) / iters
 
 
+def sweep_targets(a):
+    for B, H, Lq, Lk, D in SHAPES:
+        q = torch.randn(B, Lq, H, D, device="cuda").to(torch.bfloat16)
+        k = torch.randn(B, Lk, H, D, device="cuda").to(torch.bfloat16)
+        v = torch.randn(B, Lk, H, D, device="cuda").to(torch.bfloat16)
+        o = torch.empty_like(q)
+        lse = torch.empty(B, H, Lq, device="cuda")
+        fl = 4.0 * B * H * Lq * Lk * D
+        row = f"B{B} H{H} {Lq}x{Lk} d{D}:"
+        for t in [int(x) for x in a.targets.split(",")]:
+            lib().s2h_attn_config(1 | (t << 8))
+            tf = timeit(lambda: ops.attn_fwd(q, k, v, o, lse, 1 / math.sqrt(D), p_drop=a.drop, seed=3), a.iters)
+            row += f"  [{t}] {tf * 1e3:.0f} us {fl / tf / 1e9:.0f} TF/s"
+        lib().s2h_attn_config(1)
+        print(row, flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--drop", type=float, default=0.1)
+    ap.add_argument("--targets", default="", help="comma list of flash-forward split targets to sweep")
     a = ap.parse_args()
+    if a.targets:
+        return sweep_targets(a)
     for B, H, Lq, Lk, D in SHAPES:
         q = torch.randn(B, Lq, H, D, device="cuda").to(torch.bfloat16)
         k = torch.randn(B, Lk, H, D, device="cuda").to(torch.bfloat16)

@@ -15,7 +15,7 @@ for M, N, K in ((13312, 2048, 256), (13312, 256, 2048), (13312, 2048, 64), (4096
     x = torch.randn(M, K, device="cuda", dtype=bf)
     w = torch.randn(N, K, device="cuda", dtype=bf)
     out = torch.empty(M, N, device="cuda", dtype=bf)
-    for cfg in (2, 5):
+    for cfg in (1, 2):
         row = []
         for dbg in (0, 1, 2, 3):
             _lib.lib().s2h_gemm_config(cfg | (dbg << 8))
