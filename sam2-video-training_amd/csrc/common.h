@@ -150,3 +150,19 @@ __device__ __forceinline__ float act_grad(float x, int act) {
 // nodes around them on ROCm 7.2 (garbage loss values in replays), kernel nodes never do.
 // rows x cols floats with row stride ld (ld == cols: one contiguous range).
 void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t st);
+
+// LDS-DMA (global_load_lds_dwordx4 / _dword: 16 / 4 B per lane into lds_piece + lane * size)
+// issued through inline asm.  Issued through the builtin, the compiler's waitcnt pass sees an
+// LDS write it cannot tell apart from later ds_reads and puts s_waitcnt vmcnt(0) before the
+// first ds_read after it -- draining every DMA still in flight and serialising a multi-stage
+// ring.  Callers order these with their own counted s_waitcnt vmcnt + s_barrier.
+__device__ __forceinline__ void lds_dma16(const void* src, const void* lds_piece) {
+  const uint32_t m0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_piece);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
+__device__ __forceinline__ void lds_dma4(const void* src, const void* lds_piece) {
+  const uint32_t m0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_piece);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dword %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}

@@ -18,8 +18,9 @@ struct GemmArgs16 {
   int splits, kchunk;  // split-K: blockIdx.z = batch * splits + split
   int out_f32;
   int vecC;  // 4-column output groups are vector-aligned
+  int vec8;  // 8-column groups take 16-B accesses: bit 0 C (bf16 out), bit 1 X, bit 2 R
   float* rowsum;  // optional: rowsum[b*M + m] += sum_k A[b](m, k)  (fused bias gradient)
-  int dbg;        // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs
+  int dbg;        // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
 };
 
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);

@@ -210,6 +210,101 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
   }
 }
 
+// 8 consecutive bf16 outputs (row, col0..col0+7) with one 16-B access per operand -- the
+// store-issue-bound tail of a GEMM costs per instruction, not per byte (the 4-column form
+// issues twice the stores).  Requires (checked by the caller) 8 valid columns, no split-K, a
+// bf16 output and vec8 bit 0; X / R fall back to two 8-B accesses when their bit is clear.
+__device__ __forceinline__ void ld8_bf16(const bf16* ptr, bool wide, float* out) {
+  if (wide) {
+    const uint4 r = *(const uint4*)ptr;
+    const bf16* rb = (const bf16*)&r;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) out[e] = (float)rb[e];
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint2 r = *(const uint2*)(ptr + 4 * h);
+      const bf16* rb = (const bf16*)&r;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) out[4 * h + e] = (float)rb[e];
+    }
+  }
+}
+__device__ __forceinline__ void st8_bf16(bf16* ptr, bool wide, const float* v) {
+  bf16 t[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) t[e] = (bf16)v[e];
+  if (wide) {
+    *(uint4*)ptr = *(const uint4*)t;
+  } else {
+    *(uint2*)ptr = *(const uint2*)t;
+    *(uint2*)(ptr + 4) = *(const uint2*)(t + 4);
+  }
+}
+__device__ __forceinline__ void epilogue8(const GemmArgs16& p, int bz, int row, int col0, const float* vin,
+                                          const float* bcol) {
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = p.alpha * vin[e] + bcol[e];
+  if (p.bias_mode == 2) {
+    const float br = p.bias[row];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += br;
+  }
+  const bool wx = (p.vec8 & 2) != 0, wr = (p.vec8 & 4) != 0;
+  if (p.aux_mode == 1) st8_bf16((bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0, wx, v);
+  if (p.aux_mode == 2) {
+    float xs[8];
+    ld8_bf16((const bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0, wx, xs);
+    if (p.act == S2H_ACT_RELU) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = xs[e] > 0.f ? v[e] : 0.f;
+    } else if (p.act != S2H_ACT_NONE) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] *= act_grad(xs[e], p.act);
+    }
+  } else if (p.act == S2H_ACT_RELU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+  } else if (p.act != S2H_ACT_NONE) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act);
+  }
+  if (p.cscale) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] *= p.cscale[col0 + e];
+  }
+  if (p.drop_p > 0.f) {
+    const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
+    const float inv_keep = 1.f / (1.f - p.drop_p);
+    const uint64_t idx0 = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
+    bool k[8];
+    if ((idx0 & 1) == 0) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) s2h_keep_pair(p.seed, (idx0 >> 1) + h, thresh, k[2 * h], k[2 * h + 1]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) k[e] = s2h_keep(p.seed, idx0 + e, thresh);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
+  }
+  if (p.R) {
+    float rs[8];
+    ld8_bf16((const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0, wr, rs);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += rs[e];
+  }
+  bf16* C = (bf16*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
+  if (p.beta != 0.f) {
+    float cs[8];
+    ld8_bf16(C, true, cs);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += p.beta * cs[e];
+  }
+  st8_bf16(C, true, v);
+}
+
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -220,9 +315,10 @@ __device__ __forceinline__ void static_for(F&& f) {
 }
 
 // the lane's 4 column biases (zeros when the bias is absent or per row)
+template <int V = 4>
 __device__ __forceinline__ void load_bcol(const GemmArgs16& p, int col0, float* bcol) {
 #pragma unroll
-  for (int e = 0; e < 4; ++e) bcol[e] = (p.splits == 1 && p.bias_mode == 1 && col0 + e < p.N) ? p.bias[col0 + e] : 0.f;
+  for (int e = 0; e < V; ++e) bcol[e] = (p.splits == 1 && p.bias_mode == 1 && col0 + e < p.N) ? p.bias[col0 + e] : 0.f;
 }
 
 template <int BM, int BN, bool AKC, bool BKC>
@@ -335,18 +431,22 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
 // Requirements (else the register-staged kernel above runs): 16-B aligned bases, row
 // strides and batch strides multiple of 8 elements, the contiguous extent of every
 // operand a multiple of 8.
-template <int ROWS, bool KC, int NW = 4>
+template <int ROWS, bool KC, int NW = 4, int BK_ = 64>
 struct GImg {
-  static constexpr int BK = 64;
-  static constexpr int RB = KC ? 128 : ROWS * 2;       // bytes per image row
+  static constexpr int BK = BK_;                       // 64 or 32 k per stage
+  static constexpr int RB = KC ? BK * 2 : ROWS * 2;    // bytes per image row
+  static constexpr int CPR = BK / 8;                   // 16-B chunks per K-contiguous row
   static constexpr int BYTES = ROWS * BK * 2;
   static constexpr int PIECES = BYTES / 1024;          // 1-KiB DMA pieces
   static constexpr int PPW = PIECES / NW;              // per wave
   static constexpr int LPR = RB / 16;                  // lanes (16-B chunks) per image row
-  static_assert(PPW >= 1, "tile too small");
+  static_assert(PPW >= 1 && PIECES % NW == 0, "tile too small");
+  static_assert(BK == 64 || BK == 32, "stage depth");
 
+  // K-contiguous: chunk ^= (row >> 1) mod CPR -- conflict-free ds_read_b128 fragments for
+  // both 128-B (BK 64) and 64-B (BK 32) image rows (checked against the b128 lane groups)
   __device__ static __forceinline__ int swz(int r, int c) {
-    return KC ? (c ^ ((r >> 1) & 7)) : (c ^ (2 * (r & 3)));
+    return KC ? (c ^ ((r >> 1) & (CPR - 1))) : (c ^ (2 * (r & 3)));
   }
   // DMA rows/k of the tile at (row0, k0); rows >= nrows / k >= kend are clamped to valid
   // addresses (garbage rows are never stored; the K tail is zeroed in LDS afterwards)
@@ -367,8 +467,7 @@ struct GImg {
         const int r = row0 + 8 * c < nrows ? row0 + 8 * c : row0;
         src = base + (int64_t)k * ld_k + r;
       }
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(img + piece * 1024), 16, 0, 0);
+      lds_dma16(src, img + piece * 1024);
     }
   }
   // zero the k >= kvalid part of the image (last K step only)
@@ -381,6 +480,10 @@ struct GImg {
       const int byte = KC ? r * RB + 16 * swz(r, k >> 3) + 2 * (k & 7) : k * RB + 16 * swz(k, r >> 3) + 2 * (r & 7);
       e[byte >> 1] = (bf16)0.f;
     }
+  }
+  // byte offset of element (row r, k) in the image
+  __device__ static __forceinline__ int at(int r, int k) {
+    return KC ? r * RB + 16 * swz(r, k >> 3) + 2 * (k & 7) : k * RB + 16 * swz(k, r >> 3) + 2 * (r & 7);
   }
   // MFMA operand fragment: rows rb..rb+15 of the tile, k step ks (32 deep)
   __device__ static __forceinline__ bf16x8 frag(const char* img, int rb, int ks, int lane) {
@@ -407,11 +510,11 @@ struct GImg {
 // `s_waitcnt vmcnt` that leaves the NS-2 later stages in flight (raw s_barrier, never
 // __syncthreads inside the loop: its fence would drain them), then stage kt+NS-1 is issued
 // into the buffer step kt-1 just finished reading.
-template <int BM, int BN, int WGM, int WGN, int NS>
+template <int BM, int BN, int WGM, int WGN, int NS, int BK = 64>
 struct GemmShape {
   static constexpr int NW = WGM * WGN, NT = NW * 64;
   static constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NI = WN / 16;
-  static constexpr int STAGE_BYTES = 2 * 64 * (BM + BN);
+  static constexpr int STAGE_BYTES = 2 * BK * (BM + BN);
   static constexpr int MINB = NS * STAGE_BYTES <= 80 * 1024 ? 2 : 1;  // workgroups per CU the LDS allows
 };
 
@@ -421,16 +524,72 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS, bool AKC, bool BKC>
-__global__ __launch_bounds__((GemmShape<BM, BN, WGM, WGN, NS>::NT), (GemmShape<BM, BN, WGM, WGN, NS>::MINB))
+// Epilogue of one wave's WM x WN accumulator block through a wave-private LDS slab `ep`
+// (16 x (WN + 4) fp32): per 16-row slab, stage the accumulators, then every lane finishes 4
+// consecutive columns of a row (epilogue4) with 8-/16-byte stores -- rows of a
+// wave-instruction are 128-B column runs.  The slab is private to the wave, so no workgroup
+// barrier: LDS operations of one wave retire in order.  (A register-direct variant with
+// swapped MFMA operands -- 4 consecutive columns per lane, no staging -- measured 1.5-2.6x
+// slower: its stores scatter 16 rows x 32 B per instruction, and split-K atomics likewise.)
+template <int WM, int WN, int MI, int NI>
+__device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[MI][NI], float* ep, int bz, int mw,
+                                              int nw, int lane) {
+  constexpr int EPLD = WN + 4;
+  float bcol[4], bcol8[8];
+  load_bcol(p, nw + 4 * (lane % (WN / 4)), bcol);
+  load_bcol<8>(p, nw + 8 * (lane % (WN / 8 > 0 ? WN / 8 : 1)), bcol8);
+  // compile-time slab index (a rolled loop would index acc dynamically -> scratch)
+  static_for<0, MI>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+    if (p.splits > 1) {
+      // split-K: one row per instruction, consecutive lanes on consecutive columns (256 B)
+      float* C = (float*)p.C + (int64_t)bz * p.sC;
+      constexpr int RPI = 64 / WN;  // rows per instruction
+      const int col = nw + lane % WN;
+      for (int rr = lane / WN; rr < 16; rr += RPI) {
+        const int row = mw + i * 16 + rr;
+        if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
+      }
+    } else if (WN % 32 == 0 && (p.vec8 & 1) && nw + WN <= p.N) {
+      // 8 columns per lane, one 16-B store each (the wave's column block is entirely valid)
+      constexpr int CPR = WN / 8, RPP = 64 / CPR;
+      const int c8 = lane % CPR, rg = lane / CPR;
+      for (int ps = 0; ps < 16 / RPP; ++ps) {
+        const int rl = rg + ps * RPP;
+        const float4 lo = *(const float4*)&ep[rl * EPLD + 8 * c8];
+        const float4 hi = *(const float4*)&ep[rl * EPLD + 8 * c8 + 4];
+        const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int row = mw + i * 16 + rl;
+        if (row < p.M && !(p.dbg & 1)) epilogue8(p, bz, row, nw + 8 * c8, v8, bcol8);
+      }
+    } else {
+      constexpr int CPR = WN / 4, RPP = 64 / CPR;
+      const int c4 = lane % CPR, rg = lane / CPR;
+      for (int ps = 0; ps < 16 / RPP; ++ps) {
+        const int rl = rg + ps * RPP;
+        const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
+        const int row = mw + i * 16 + rl;
+        if (row < p.M && !(p.dbg & 1)) epilogue4(p, bz, row, nw + 4 * c4, v4, bcol);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  });
+}
+
+template <int BM, int BN, int WGM, int WGN, int NS, int BK, bool AKC, bool BKC>
+__global__ __launch_bounds__((GemmShape<BM, BN, WGM, WGN, NS, BK>::NT), (GemmShape<BM, BN, WGM, WGN, NS, BK>::MINB))
 void gemm16g_kernel(GemmArgs16 p) {
   if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
-  using SH = GemmShape<BM, BN, WGM, WGN, NS>;
-  constexpr int BK = 64;
+  using SH = GemmShape<BM, BN, WGM, WGN, NS, BK>;
   constexpr int NW = SH::NW, NT = SH::NT;
   constexpr int WM = SH::WM, WN = SH::WN, MI = SH::MI, NI = SH::NI;
-  using IA = GImg<BM, AKC, NW>;
-  using IB = GImg<BN, BKC, NW>;
+  using IA = GImg<BM, AKC, NW, BK>;
+  using IB = GImg<BN, BKC, NW, BK>;
   constexpr int STAGE = IA::BYTES + IB::BYTES;
   constexpr int DPS = IA::PPW + IB::PPW;  // DMA instructions per stage per wave
   __shared__ __attribute__((aligned(1024))) char smem[NS * STAGE];
@@ -461,7 +620,7 @@ void gemm16g_kernel(GemmArgs16 p) {
 
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {  // prologue: stages 0 .. NS-2 in flight
-    if (st < nk) {
+    if (st < nk && !(p.dbg & 4)) {
       char* sa = smem + st * STAGE;
       IA::dma(sa, A, p.lda_m, p.lda_k, m0, kbeg + st * BK, p.M, kend, w, lane);
       IB::dma(sa + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + st * BK, p.N, kend, w, lane);
@@ -474,7 +633,7 @@ void gemm16g_kernel(GemmArgs16 p) {
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + NS - 1 < nk) {  // refill the buffer step kt-1 read; runs under this step's MFMAs
+    if (kt + NS - 1 < nk && !(p.dbg & 4)) {  // refill the buffer step kt-1 read; runs under this step's MFMAs
       char* na = smem + ((kt + NS - 1) % NS) * STAGE;
       IA::dma(na, A, p.lda_m, p.lda_k, m0, kbeg + (kt + NS - 1) * BK, p.M, kend, w, lane);
       IB::dma(na + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + NS - 1) * BK, p.N, kend, w, lane);
@@ -487,15 +646,11 @@ void gemm16g_kernel(GemmArgs16 p) {
     }
     if (do_rs) {
 #pragma unroll 8
-      for (int k = 0; k < BK; ++k) {
-        const int byte = AKC ? tid * IA::RB + 16 * IA::swz(tid, k >> 3) + 2 * (k & 7)
-                             : k * IA::RB + 16 * IA::swz(k, tid >> 3) + 2 * (tid & 7);
-        rs += (float)*(const bf16*)(sa + byte);
-      }
+      for (int k = 0; k < BK; ++k) rs += (float)*(const bf16*)(sa + IA::at(tid, k));
     }
     if (p.dbg & 2) continue;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < BK / 32; ++ks) {
       bf16x8 a[MI], b[NI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) a[i] = IA::frag(sa, wm * WM + i * 16, ks, lane);
@@ -512,44 +667,8 @@ void gemm16g_kernel(GemmArgs16 p) {
   __syncthreads();
 
   if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
-  // Epilogue through LDS: each wave stages one 16-row slab of its accumulators, then every
-  // lane finishes 4 consecutive columns of a row (epilogue4) with 8-/16-byte stores; rows of
-  // a wave-instruction are 128-B column runs.  (A register-direct variant with swapped MFMA
-  // operands -- 4 consecutive columns per lane, no staging -- measured 1.5-2.6x slower: its
-  // stores scatter 16 rows x 32 B per instruction, and split-K atomics likewise.)
-  constexpr int EPLD = WN + 4;
-  static_assert(NW * 16 * EPLD * 4 <= NS * STAGE, "epilogue staging fits");
-  float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
-  float bcol[4];
-  load_bcol(p, n0 + wn * WN + 4 * (lane % (WN / 4)), bcol);
-#pragma unroll
-  for (int i = 0; i < MI; ++i) {
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
-    __syncthreads();
-    if (p.splits > 1) {
-      // split-K: one row per instruction, consecutive lanes on consecutive columns (256 B)
-      float* C = (float*)p.C + (int64_t)bz * p.sC;
-      constexpr int RPI = 64 / WN;  // rows per instruction
-      const int col = n0 + wn * WN + lane % WN;
-      for (int rr = lane / WN; rr < 16; rr += RPI) {
-        const int row = m0 + wm * WM + i * 16 + rr;
-        if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
-      }
-    } else {
-      constexpr int CPR = WN / 4, RPP = 64 / CPR;
-      const int c4 = lane % CPR, rg = lane / CPR;
-      for (int ps = 0; ps < 16 / RPP; ++ps) {
-        const int rl = rg + ps * RPP;
-        const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
-        const int row = m0 + wm * WM + i * 16 + rl;
-        if (row < p.M && !(p.dbg & 1)) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol);
-      }
-    }
-    __syncthreads();
-  }
+  tile_epilogue<WM, WN, MI, NI>(p, acc, reinterpret_cast<float*>(smem) + w * 16 * (WN + 4), bz, m0 + wm * WM,
+                                n0 + wn * WN, lane);
 }
 
 static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
@@ -586,18 +705,24 @@ static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st
   }
   // 4-column output groups: 16-B (f32) / 8-B (bf16) aligned
   a.vecC = ((uintptr_t)a.C % (a.out_f32 ? 16 : 8) == 0) && a.ldc % 4 == 0 && (batch == 1 || a.sC % 4 == 0);
+  // 8-column groups with one 16-B access per operand (bf16: base 16-B aligned, strides % 8)
+  auto ok8 = [&](const void* ptr, int64_t ld, int64_t sb) {
+    return ptr && (uintptr_t)ptr % 16 == 0 && ld % 8 == 0 && (batch == 1 || sb % 8 == 0);
+  };
+  a.vec8 = (!a.out_f32 && ok8(a.C, a.ldc, a.sC) ? 1 : 0) | (ok8(a.X, a.ldx, a.sX) ? 2 : 0) |
+           (ok8(a.R, a.ldr, a.sR) ? 4 : 0);
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS>
+template <int BM, int BN, int WGM, int WGN, int NS, int BK = 64>
 static int launch_glds(GemmArgs16& a, int batch, hipStream_t st) {
   plan_splits(a, batch, BM, BN, st);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
-  constexpr int NT = GemmShape<BM, BN, WGM, WGN, NS>::NT;
+  constexpr int NT = GemmShape<BM, BN, WGM, WGN, NS, BK>::NT;
   dim3 g1(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, batch * a.splits);
-  if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, true, true>), g1, dim3(NT), 0, st, a);
-  else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, true, false>), g1, dim3(NT), 0, st, a);
-  else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, false, true>), g1, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, false, false>), g1, dim3(NT), 0, st, a);
+  if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, true>), g1, dim3(NT), 0, st, a);
+  else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, false>), g1, dim3(NT), 0, st, a);
+  else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, true>), g1, dim3(NT), 0, st, a);
+  else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, false>), g1, dim3(NT), 0, st, a);
   return (int)hipGetLastError();
 }
 
@@ -616,7 +741,7 @@ static int launch16_regs(GemmArgs16& a, int batch, hipStream_t st) {
 // LDS-DMA tilings (s2h_gemm_config selects one for A/B measurements; 0 = automatic)
 enum GemmCfg {
   CFG_AUTO = 0, CFG_64 = 1, CFG_128 = 2, CFG_128_NS3 = 3, CFG_256x128 = 4, CFG_256 = 5, CFG_128x256 = 6,
-  CFG_128x64 = 7, CFG_64x128 = 8, CFG_64_NS3 = 9
+  CFG_128x64 = 7, CFG_64x128 = 8, CFG_64_NS3 = 9, CFG_64_K32_NS4 = 10
 };
 static int g_gemm_cfg = CFG_AUTO;
 static int g_gemm_dbg = 0;
@@ -628,14 +753,21 @@ extern "C" int s2h_gemm_config(int cfg) {
   return prev;
 }
 
-// Tiling by shape, from tools/gemm_probe.py on MI355X (profiles/r01_v9_gemm_probe.log):
-// on this step's shapes (M = 10^4-10^5 rows, N and K of 64..2048) the 64^2 tile wins almost
-// everywhere -- 16 KB of LDS per stage lets ~8 workgroups share a CU, and that occupancy hides
-// the LDS-DMA latency the 2-deep ring cannot (128^2: 1.1-1.5x slower, weight gradients 1.5x);
-// 256^2 (8 waves) only pays on large square problems.
+// Tiling by shape.  rocprofv3 kernel traces of tools/gemm_one.py (tools/kt_gemm.sh,
+// profiles/r01_v14_gemm_tilings.txt) and the per-shape table of a profiled training step
+// (bench.py --kernel-table with S2H_GEMM_CFG forced to 1 / 7, profiles/r01_v14_gemm_cfg_step.txt):
+//  * 128x64 (4 waves of 32x32, 24 KB per stage) wins where it still yields >= 1024 tiles --
+//    13312x2048x256 35.7 us vs 38.2 (64^2) / 40.0 (128^2), 131072x448x112 70.1 vs 77.5 --
+//    and on split-K weight gradients with >= 64 of its tiles (2048x256x13312: -17 %);
+//  * 64^2 wins on the narrow outputs (N = 128..256 of 13312 rows, 416 tiles at 128x64: the
+//    occupancy of the smaller tile hides the LDS-DMA latency) and on tiny weight gradients;
+//  * 256^2 (8 waves) only pays on large square problems (4096^3: 146 us vs 170 for 128^2).
 static int pick_cfg(const GemmArgs16& a, int batch) {
   const long t256 = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * batch;
   if (a.M >= 1024 && a.N >= 1024 && a.K >= 1024 && t256 >= 128) return CFG_256;
+  const long t128x64 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64) * batch;
+  const bool split = a.out_f32 && a.K >= 1024 && t128x64 < 512;  // plan_splits' split-K regime
+  if (split ? t128x64 >= 64 : t128x64 >= 1024) return CFG_128x64;
   return CFG_64;
 }
 
@@ -657,6 +789,7 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
     case CFG_128x64: return launch_glds<128, 64, 2, 2, 2>(a, batch, st);
     case CFG_64x128: return launch_glds<64, 128, 2, 2, 2>(a, batch, st);
     case CFG_64_NS3: return launch_glds<64, 64, 2, 2, 3>(a, batch, st);
+    case CFG_64_K32_NS4: return launch_glds<64, 64, 2, 2, 4, 32>(a, batch, st);
     default: return launch_glds<128, 128, 2, 2, 2>(a, batch, st);
   }
 }

@@ -110,6 +110,8 @@ def lib():
             fn = getattr(h, name)
             fn.argtypes = argtypes
             fn.restype = RESTYPES.get(name, c_int)
+        if os.environ.get("S2H_GEMM_CFG"):  # measurement override of the GEMM tiling choice
+            h.s2h_gemm_config(int(os.environ["S2H_GEMM_CFG"]))
         _LIB = h
     return _LIB
 

@@ -11,11 +11,15 @@ from sam2_video.kernels import _lib, ops  # noqa: E402
 from gemm_probe import timeit  # noqa: E402
 
 bf = torch.bfloat16
-for M, N, K in ((13312, 2048, 256), (13312, 256, 2048), (13312, 2048, 64), (4096, 4096, 4096)):
+CFGS = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1, 2]
+SHAPES = [(13312, 2048, 256), (13312, 256, 2048), (13312, 2048, 64), (4096, 4096, 4096)]
+if len(sys.argv) > 2:
+    SHAPES = [tuple(int(v) for v in s.split("x")) for s in sys.argv[2].split(",")]
+for M, N, K in SHAPES:
     x = torch.randn(M, K, device="cuda", dtype=bf)
     w = torch.randn(N, K, device="cuda", dtype=bf)
     out = torch.empty(M, N, device="cuda", dtype=bf)
-    for cfg in (1, 2):
+    for cfg in CFGS:
         row = []
         for dbg in (0, 1, 2, 3):
             _lib.lib().s2h_gemm_config(cfg | (dbg << 8))

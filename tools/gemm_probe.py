@@ -13,7 +13,10 @@ import torch  # noqa: E402
 
 from sam2_video.kernels import _lib, ops  # noqa: E402
 
-CFG_NAMES = {1: "64", 2: "128", 3: "128s3", 4: "256x128", 5: "256", 6: "128x256", 7: "128x64", 8: "64x128", 9: "64s3"}
+CFG_NAMES = {1: "64", 2: "128", 3: "128s3", 4: "256x128", 5: "256", 6: "128x256", 7: "128x64", 8: "64x128", 9: "64s3",
+             10: "64k32s4", 11: "128k32s4", 12: "128k32s5", 13: "256x128k32", 14: "256k32s4", 15: "128x64k32s6",
+             16: "64k32s6", 17: "p64", 18: "p64s3", 19: "p128", 20: "p128x64", 21: "p64x128", 22: "p256",
+             23: "p128s3"}
 # (M, N, K, kind): fwd = x[M,K] @ w[N,K]^T ; dgrad = dy[M,K] @ w[K,N] ; wgrad = dy[K,M]^T @ x[K,N] (fp32 out)
 SHAPES = [
     (13312, 2048, 256, "fwd"), (13312, 256, 2048, "fwd"), (13312, 768, 256, "fwd"), (13312, 256, 256, "fwd"),
