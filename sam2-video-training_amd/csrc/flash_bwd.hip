@@ -75,8 +75,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   const int nt = min(ntiles_all, t0 + a.tiles_per_split) - t0;
 
   if (nt > 0) {
-    dma_tile<DP, 64>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
-    dma_tile<DP, 64>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
   }
   const bool qv = q < a.Lq;
   bf16x8 qf[C::NT], gf[C::NT];
@@ -98,8 +98,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     char* Vb = Kb + C::TILEB;
     if (it + 1 < nt) {
       char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 64>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
-      dma_tile<DP, 64>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
       wait_vmcnt<2 * C::PPW>();
     } else {
       wait_vmcnt<0>();
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   const bf16* V = a.v + b * a.svb + h * a.svh;
   const int nt = (a.Lq + C::KT - 1) / C::KT;
 
-  dma_tile<DP, 32>(smem, Q, a.sql, 0, a.Lq, w, lane);
-  dma_tile<DP, 32>(smem + C::TILEB, G, a.sgl, 0, a.Lq, w, lane);
+  dma_tile<DP, 32, FL_WAVES, true>(smem, Q, a.sql, 0, a.Lq, w, lane);
+  dma_tile<DP, 32, FL_WAVES, true>(smem + C::TILEB, G, a.sgl, 0, a.Lq, w, lane);
   bf16x8 kf[C::NT], vf[C::NT];  // B operands: K^T / V^T [k = d][n = key]
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) {
@@ -249,8 +249,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
     }
     if (it + 1 < nt) {
       char* Qn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 32>(Qn, Q, a.sql, q0 + C::KT, a.Lq, w, lane);
-      dma_tile<DP, 32>(Qn + C::TILEB, G, a.sgl, q0 + C::KT, a.Lq, w, lane);
+      dma_tile<DP, 32, FL_WAVES, true>(Qn, Q, a.sql, q0 + C::KT, a.Lq, w, lane);
+      dma_tile<DP, 32, FL_WAVES, true>(Qn + C::TILEB, G, a.sgl, q0 + C::KT, a.Lq, w, lane);
       wait_vmcnt<2 * C::PPW>();
     } else {
       wait_vmcnt<0>();
@@ -351,12 +351,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   auto dma_rows = [&](char* stage, int q0) {
     const int qi = min(q0 + (lane & 31), a.Lq - 1);
     const float* src = (lane < 32 ? LSE : DI) + qi;
-    __builtin_amdgcn_global_load_lds((const void*)src,
-                                     (__attribute__((address_space(3))) void*)(stage + 2 * C::TILEB + w * 256), 4, 0, 0);
+    lds_dma4(src, stage + 2 * C::TILEB + w * 256);
   };
-  dma_tile<DP, NWV * 32, NWV>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
-  dma_tile<DP, QT, NWV>(stages, Q, a.sql, qbase, a.Lq, w, lane);
-  dma_tile<DP, QT, NWV>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
+  dma_tile<DP, NWV * 32, NWV, true>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
+  dma_tile<DP, QT, NWV, true>(stages, Q, a.sql, qbase, a.Lq, w, lane);
+  dma_tile<DP, QT, NWV, true>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
   bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, a.Lk - 1);
@@ -376,8 +375,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 256);  // [lse(32) | Di(32)]
     if (it + 1 < nt) {
       char* Qn = stages + ((it + 1) & 1) * STAGE;
-      dma_tile<DP, QT, NWV>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
-      dma_tile<DP, QT, NWV>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
+      dma_tile<DP, QT, NWV, true>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
+      dma_tile<DP, QT, NWV, true>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
       dma_rows(Qn, q0 + QT);
       wait_vmcnt<2 * C::PPW + 1>();
     } else {

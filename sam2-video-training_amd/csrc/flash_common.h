@@ -40,7 +40,10 @@ __device__ __forceinline__ int swz(int row, int c) {
 
 // DMA one tile (rows r0.., clamped to [0, nrows)) into a swizzled LDS image; the chunk
 // permutation is applied to the per-lane SOURCE address (the DMA destination is lane-linear)
-template <int DP, int ROWS, int NWV = FL_WAVES>
+// ASM: issue through inline asm (lds_dma16) so the compiler's waitcnt pass does not put
+// vmcnt(0) before later ds_reads; the builtin form is kept where it measured faster (the
+// forward kernel, whose spilled address registers make every scratch reload a vmcnt wait).
+template <int DP, int ROWS, int NWV = FL_WAVES, bool ASM = false>
 __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w, int lane) {
   using C = FlashCfg<DP, ROWS, NWV>;
 #pragma unroll
@@ -51,8 +54,11 @@ __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_
     const int c = pos ^ (row & (C::NCH - 1));
     const int gr = min(r0 + row, nrows - 1);
     const bf16* g = src + (int64_t)gr * ld + c * 8;
-    __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(lds_tile + piece * 1024),
-                                     16, 0, 0);
+    if constexpr (ASM)
+      lds_dma16(g, lds_tile + piece * 1024);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(lds_tile + piece * 1024),
+                                       16, 0, 0);
   }
 }
 
