@@ -41,8 +41,9 @@ template <int DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
   if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using C = FlashCfg<DP>;
+  using I = PadImg<DP>;  // padded K / V images (affine read addresses, no swizzle)
   // one LDS array: [2 stages][K tile | V tile]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * I::TILEB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int split = blockIdx.z;
@@ -56,9 +57,10 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   const int nt = t1 - t0;
 
   if (nt > 0) {
-    dma_tile<DP, 64>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
-    dma_tile<DP, 64>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
   }
+  const int npw = I::pieces(w);
 
   // Q^T fragments (B operand of K Q^T): lane -> query q, d = 32t + 8g + j
   bf16x8 qf[C::NT];
@@ -67,6 +69,10 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     if (q < a.Lq) qf[t] = *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g);
     else qf[t] = bf16x8{};
   }
+  // compiler-visible vmcnt(0): retires the Q loads in the compiler's own bookkeeping too;
+  // otherwise it keeps them "maybe pending" around the key loop and waits vmcnt(0) before
+  // the first MFMA of every tile -- which also drains the (asm, invisible) K/V prefetch
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 
   f32x4 o[C::ND];  // O^T: row d = 16*db + 4g + r, column q
 #pragma unroll
@@ -78,14 +84,14 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   for (int it = 0; it < nt; ++it) {
     const int kt = t0 + it;
     const int k0 = kt * C::KT;
-    char* Kb = smem + (it & 1) * 2 * C::TILEB;
-    char* Vb = Kb + C::TILEB;
+    char* Kb = smem + (it & 1) * 2 * I::TILEB;
+    char* Vb = Kb + I::TILEB;
     if (it + 1 < nt) {
-      char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 64>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
-      dma_tile<DP, 64>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
-      // this wave's pieces of tile `it` have landed once all but the 2*PPW just issued retired
-      wait_vmcnt<2 * C::PPW>();
+      char* Kn = smem + ((it + 1) & 1) * 2 * I::TILEB;
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      // this wave's pieces of tile `it` have landed once all but the 2*npw just issued retired
+      wait_vmcnt_pieces<2, I::PPW_LO>(npw);
     } else {
       wait_vmcnt<0>();
     }
@@ -100,7 +106,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
       const int row = kb * 16 + ql;
 #pragma unroll
       for (int t = 0; t < C::NT; ++t) {
-        const bf16x8 kf = *(const bf16x8*)(Kb + swz<DP>(row, 4 * t + g));
+        const bf16x8 kf = *(const bf16x8*)(Kb + row * I::ROWB + 16 * (4 * t + g));
         s[kb] = mfma16(kf, qf[t], s[kb]);
       }
     }
@@ -179,9 +185,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
 #pragma unroll
       for (int d = 0; d < C::ND; ++d) {
         const int dcol = 16 * d + 4 * pp;  // first of the 4 d this lane addresses
-        const int ch = dcol >> 3, off = (dcol & 7) * 2;
-        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + swz<DP>(r0, ch) + off));
-        v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + swz<DP>(r0 + 16, ch) + off));
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + r0 * I::ROWB + 2 * dcol));
+        v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + (r0 + 16) * I::ROWB + 2 * dcol));
         v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
         o[d] = mfma16(__builtin_bit_cast(bf16x8, cat), pb[c], o[d]);
       }

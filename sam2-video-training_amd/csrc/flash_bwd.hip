@@ -87,6 +87,9 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   }
   const float lse2 = qv ? a.lse[(int64_t)bh * a.Lq + q] * FL_LOG2E : 0.f;
   const float di = qv ? a.di[(int64_t)bh * a.Lq + q] : 0.f;
+  // compiler-visible vmcnt(0): the compiler's own bookkeeping retires these loads here instead
+  // of waiting vmcnt(0) inside the key loop (which would also drain the asm K/V prefetch)
+  __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
   f32x4 acc[C::ND];  // dQ^T: row d = 16*db + 4g + r, column q
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -361,6 +364,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   const int64_t vkey = min(key, a.Lk - 1);
 #pragma unroll
   for (int t = 0; t < NT; ++t) vf[t] = *(const bf16x8*)(V + vkey * a.svl + 16 * t + 8 * hi);
+  __builtin_amdgcn_s_waitcnt(0xF70);  // retire the V loads in the compiler's bookkeeping (see dq)
   const int krow = w * 32 + kl;  // this lane's key row in the K block
   f32x16 dk[ND], dv[ND];  // dK^T / dV^T: row d = 32*db + 8(r>>2) + 4hi + (r&3), column key
 #pragma unroll

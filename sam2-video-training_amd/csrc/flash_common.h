@@ -62,10 +62,55 @@ __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_
   }
 }
 
+// Padded [rows][DP] image: rows of DP*2 + 32 bytes instead of an XOR swizzle.  Reads of
+// 16 rows x 16-B chunks (ds_read_b128) and transposing ds_read_b64_tr_b16 reads of 8 rows
+// are bank-conflict-free for DP 64 / 128 / 256 (row starts step by 8 banks), and a lane's
+// addresses are affine in the column (one base register + immediate offsets) -- the
+// swizzled image needs one address per column block, which in the forward kernel meant
+// ~64 live address VGPRs and scratch spills inside the key loop.  The lane-linear DMA
+// writes the pad slots too (with a copy of chunk 0 of the row: 6 % extra bytes).
+template <int DP, int ROWS = 64, int NWV = FL_WAVES>
+struct PadImg {
+  static constexpr int SPR = DP / 8 + 2;               // 16-B slots per row, 2 of them pad
+  static constexpr int ROWB = SPR * 16;                // bytes per row
+  static constexpr int TILEB = ROWS * ROWB;
+  static constexpr int PIECES = ROWS * SPR / 64;       // 1-KiB DMA pieces
+  static constexpr int PPW_LO = PIECES / NWV;          // pieces of waves >= NHI
+  static constexpr int NHI = PIECES % NWV;             // waves < NHI take one more
+  static_assert((ROWS * SPR) % 64 == 0 && PPW_LO >= 1, "tile shape");
+  __device__ static __forceinline__ int pieces(int w) { return PPW_LO + (w < NHI ? 1 : 0); }
+};
+
+template <int DP, int ROWS = 64, int NWV = FL_WAVES, bool ASM = false>
+__device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w,
+                                             int lane) {
+  using I = PadImg<DP, ROWS, NWV>;
+#pragma unroll
+  for (int i = 0; i < I::PPW_LO + (I::NHI ? 1 : 0); ++i) {
+    if (i == I::PPW_LO && w >= I::NHI) break;  // wave-uniform
+    const int piece = w + i * NWV;
+    const int slot = piece * 64 + lane;
+    const int row = slot / I::SPR, c = slot % I::SPR;
+    const int gr = min(r0 + row, nrows - 1);
+    const bf16* g = src + (int64_t)gr * ld + (c < DP / 8 ? c * 8 : 0);
+    if constexpr (ASM)
+      lds_dma16(g, lds_tile + piece * 1024);
+    else
+      __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)(lds_tile + piece * 1024),
+                                       16, 0, 0);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// vmcnt(M * pieces) for a wave-uniform piece count in {LO, LO + 1}
+template <int M, int LO>
+__device__ __forceinline__ void wait_vmcnt_pieces(int n) {
+  if (n > LO) wait_vmcnt<M * (LO + 1)>();
+  else wait_vmcnt<M * LO>();
 }
 
 __device__ __forceinline__ void wg_barrier() {
