@@ -20,6 +20,25 @@ static inline dim3 ew_grid(int64_t n) {
     else hipLaunchKernelGGL(KERNEL<float>, grid, dim3(256), 0, st, __VA_ARGS__); \
   } while (0)
 
+// 16 B of T as floats (VEC = 8 bf16 / 4 f32)
+template <typename T> struct V16 {
+  static constexpr int VEC = 16 / sizeof(T);
+  static __device__ __forceinline__ void load(const T* p, float* v) {
+    const uint4 r = *(const uint4*)p;
+    const T* e = (const T*)&r;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) v[j] = to_f32(e[j]);
+  }
+  static __device__ __forceinline__ void store(T* p, const float* v) {
+    uint4 r;
+    T* e = (T*)&r;
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) e[j] = from_f32<T>(v[j]);
+    *(uint4*)p = r;
+  }
+};
+static inline bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
 // ---------------------------------------------------------------- add / axpy
 // out = alpha*a + beta*b   (a or b may be null -> treated as 0)
 template <typename T>
@@ -168,12 +187,48 @@ __global__ void rope_kernel(int64_t nb, int nrot, int D, const void* x, int64_t 
     yp[1] = from_f32<T>(xr * si + xi * co);
   }
 }
+// 16 B (VEC/2 complex pairs) per thread, 32-bit index math: the scalar form above spent
+// four 64-bit divisions on every 4-byte pair.  rows = nb * nrot < 2^31.
+template <typename T>
+__global__ void rope_vec_kernel(int rows, int nrot, int D, const void* x, int64_t sxb, int64_t sxl, void* y,
+                                int64_t syb, int64_t syl, const float* cosv, const float* sinv, int period,
+                                int inverse) {
+  constexpr int VEC = V16<T>::VEC, NP = VEC / 2;
+  const int half = D / 2, cpr = D / VEC;  // 16-B chunks per row
+  const int64_t n = (int64_t)rows * cpr;
+  GRID_STRIDE(i, n) {
+    const int ii = (int)i;
+    const int row = ii / cpr, ch = ii - row * cpr;
+    const int b = row / nrot, t = row - b * nrot;
+    const int pr = t % period;
+    float v[VEC], o[VEC];
+    V16<T>::load((const T*)x + (int64_t)b * sxb + (int64_t)t * sxl + ch * VEC, v);
+    const float* cp = cosv + pr * half + ch * NP;
+    const float* sp = sinv + pr * half + ch * NP;
+#pragma unroll
+    for (int j = 0; j < NP; ++j) {
+      const float co = cp[j], si = inverse ? -sp[j] : sp[j];
+      o[2 * j] = v[2 * j] * co - v[2 * j + 1] * si;
+      o[2 * j + 1] = v[2 * j] * si + v[2 * j + 1] * co;
+    }
+    V16<T>::store((T*)y + (int64_t)b * syb + (int64_t)t * syl + ch * VEC, o);
+  }
+}
+
 extern "C" int s2h_rope(int dt, int64_t nb, int nrot, int D, const void* x, int64_t sxb, int64_t sxl, void* y,
                         int64_t syb, int64_t syl, const float* cosv, const float* sinv, int period, int inverse,
                         hipStream_t st) {
   const int64_t n = nb * nrot * (D / 2);
   if (n <= 0) return 0;
-  DISPATCH_T(dt, rope_kernel, ew_grid(n), nb, nrot, D, x, sxb, sxl, y, syb, syl, cosv, sinv, period, inverse);
+  const int vec = dt == S2H_BF16 ? 8 : 4;
+  if (D % vec == 0 && al16(x) && al16(y) && sxb % vec == 0 && sxl % vec == 0 && syb % vec == 0 &&
+      syl % vec == 0 && nb * nrot * (D / vec) < (1ll << 31)) {
+    const int rows = (int)(nb * nrot);
+    DISPATCH_T(dt, rope_vec_kernel, ew_grid((int64_t)rows * (D / vec)), rows, nrot, D, x, sxb, sxl, y, syb, syl,
+               cosv, sinv, period, inverse);
+  } else {
+    DISPATCH_T(dt, rope_kernel, ew_grid(n), nb, nrot, D, x, sxb, sxl, y, syb, syl, cosv, sinv, period, inverse);
+  }
   return (int)hipGetLastError();
 }
 
@@ -277,12 +332,60 @@ __global__ void window_kernel(int B, int H, int W, int C, int ws, const void* sr
     }
   }
 }
+// 16 B of channels per thread, 32-bit pixel index math (pixels < 2^31 / chunks)
+template <typename T>
+__global__ void window_vec_kernel(int B, int H, int W, int C, int ws, const void* src, void* dst, int dir,
+                                  int accum) {
+  constexpr int VEC = V16<T>::VEC;
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws, cc = C / VEC;
+  const int64_t n = (dir == 0 ? (int64_t)B * nh * nw * ws * ws : (int64_t)B * H * W) * cc;
+  GRID_STRIDE(i, n) {
+    const int ii = (int)i;
+    int p = ii / cc;
+    const int c = (ii - p * cc) * VEC;
+    float v[VEC];
+    if (dir == 0) {
+      const int ix = p % ws; p /= ws;
+      const int iy = p % ws; p /= ws;
+      const int wx = p % nw; p /= nw;
+      const int wy = p % nh;
+      const int b = p / nh;
+      const int yy = wy * ws + iy, xx = wx * ws + ix;
+      if (yy < H && xx < W) {
+        V16<T>::load((const T*)src + (((int64_t)b * H + yy) * W + xx) * C + c, v);
+      } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) v[j] = 0.f;
+      }
+    } else {
+      const int xx = p % W; p /= W;
+      const int yy = p % H;
+      const int b = p / H;
+      const int64_t widx = ((((int64_t)b * nh + yy / ws) * nw + xx / ws) * ws + yy % ws) * ws + xx % ws;
+      V16<T>::load((const T*)src + widx * C + c, v);
+    }
+    T* d = (T*)dst + (int64_t)ii * VEC;
+    if (accum) {
+      float a[VEC];
+      V16<T>::load(d, a);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[j] += a[j];
+    }
+    V16<T>::store(d, v);
+  }
+}
+
 extern "C" int s2h_window(int dt, int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum,
                           hipStream_t st) {
   const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws;
   const int64_t n = dir == 0 ? (int64_t)B * nh * nw * ws * ws * C : (int64_t)B * H * W * C;
   if (n <= 0) return 0;
-  DISPATCH_T(dt, window_kernel, ew_grid(n), B, H, W, C, ws, src, dst, dir, accum);
+  const int vec = dt == S2H_BF16 ? 8 : 4;
+  if (C % vec == 0 && al16(src) && al16(dst) && n / vec < (1ll << 31)) {
+    DISPATCH_T(dt, window_vec_kernel, ew_grid(n / vec), B, H, W, C, ws, src, dst, dir, accum);
+  } else {
+    DISPATCH_T(dt, window_kernel, ew_grid(n), B, H, W, C, ws, src, dst, dir, accum);
+  }
   return (int)hipGetLastError();
 }
 

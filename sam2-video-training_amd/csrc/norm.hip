@@ -61,6 +61,23 @@ template <> struct Chunk<float> {
   }
 };
 
+// VEC consecutive fp32 parameters (gamma / beta): 16-B loads when aligned (parameter arena
+// slices need not be), scalar loads otherwise
+template <int VEC>
+__device__ __forceinline__ void load_param(const float* p, float* out) {
+  if (((uintptr_t)p & 15) == 0) {
+#pragma unroll
+    for (int h = 0; h < VEC / 4; ++h) {
+      const f32x4 v = ((const f32x4*)p)[h];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) out[4 * h + j] = v[j];
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) out[j] = p[j];
+  }
+}
+
 // ------------------------------------------------------------ forward (vector)
 template <typename T, int G, int K>
 __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int C, const T* a, int64_t lda, const T* badd,
@@ -74,6 +91,20 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int C, const 
   const int64_t row = ((int64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW + lane / G;
   const bool live = row < rows;
   const int NC = C / VEC;
+  // gamma / beta first: their loads then overlap the row loads instead of adding a memory
+  // round trip after the two reductions (the kernel is one short latency chain per wave)
+  float gv[K][VEC], bv[K][VEC];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int ch = gl + k * G;
+    if (gamma && ch < NC) {
+      load_param<VEC>(gamma + ch * VEC, gv[k]);
+      load_param<VEC>(beta + ch * VEC, bv[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) { gv[k][j] = 1.f; bv[k][j] = 0.f; }
+    }
+  }
   float v[K][VEC];
   float s = 0.f;
 #pragma unroll
@@ -114,10 +145,7 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int C, const 
     if (ch < NC) {
       float o[VEC];
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) {
-        o[j] = (v[k][j] - mu) * rs;
-        if (gamma) o[j] = o[j] * gamma[ch * VEC + j] + beta[ch * VEC + j];
-      }
+      for (int j = 0; j < VEC; ++j) o[j] = (v[k][j] - mu) * rs * gv[k][j] + bv[k][j];
       Chunk<T>::store(y + row * ldy + ch * VEC, o);
     }
   }
@@ -142,27 +170,41 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int C, const 
   for (int k = 0; k < K; ++k)
 #pragma unroll
     for (int j = 0; j < VEC; ++j) { pg[k][j] = 0.f; pb[k][j] = 0.f; }
+  float gk[K][VEC];  // gamma of this lane's chunks, loaded once (row-independent)
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const int ch = gl + k * G;
+    if (gamma && ch < NC) {
+      load_param<VEC>(gamma + ch * VEC, gk[k]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) gk[k][j] = 1.f;
+    }
+  }
   const int64_t stride = (int64_t)gridDim.x * 4 * RPW;
   for (int64_t row = ((int64_t)blockIdx.x * 4 + w) * RPW + lane / G; row - lane / G < rows; row += stride) {
     const bool live = row < rows;
     const float mu = live ? mean[row] : 0.f, rs = live ? rstd[row] : 0.f;
-    float xh[K][VEC], g[K][VEC];
+    float xh[K][VEC], g[K][VEC], r[K][VEC];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k) {
       const int ch = gl + k * G;
 #pragma unroll
-      for (int j = 0; j < VEC; ++j) { xh[k][j] = 0.f; g[k][j] = 0.f; }
+      for (int j = 0; j < VEC; ++j) { xh[k][j] = 0.f; g[k][j] = 0.f; r[k][j] = 0.f; }
       if (live && ch < NC) {
         float xv[VEC], d[VEC];
         Chunk<T>::load(x + row * ldx + ch * VEC, xv);
         Chunk<T>::load(dy + row * lddy + ch * VEC, d);
+        // the addend now, not after the reductions: one memory round trip per row instead of two
+        if (dx_accum || dres)
+          Chunk<T>::load(dx_accum ? dx + row * lddx + ch * VEC : dres + row * ldres + ch * VEC, r[k]);
 #pragma unroll
         for (int j = 0; j < VEC; ++j) {
           xh[k][j] = (xv[j] - mu) * rs;
           pg[k][j] += d[j] * xh[k][j];
           pb[k][j] += d[j];
-          g[k][j] = gamma ? d[j] * gamma[ch * VEC + j] : d[j];
+          g[k][j] = d[j] * gk[k][j];
           s1 += g[k][j];
           s2 += g[k][j] * xh[k][j];
         }
@@ -177,13 +219,7 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int C, const 
         if (ch < NC) {
           float o[VEC];
 #pragma unroll
-          for (int j = 0; j < VEC; ++j) o[j] = rs * (g[k][j] - s1 - xh[k][j] * s2);
-          if (dx_accum || dres) {
-            float r[VEC];
-            Chunk<T>::load(dx_accum ? dx + row * lddx + ch * VEC : dres + row * ldres + ch * VEC, r);
-#pragma unroll
-            for (int j = 0; j < VEC; ++j) o[j] += r[j];
-          }
+          for (int j = 0; j < VEC; ++j) o[j] = rs * (g[k][j] - s1 - xh[k][j] * s2) + r[k][j];
           Chunk<T>::store(dx + row * lddx + ch * VEC, o);
         }
       }

@@ -15,7 +15,8 @@ from ctypes import c_float, c_int, c_int64, c_uint64, c_void_p
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(os.path.dirname(_HERE), "_lib", "libsam2hip.so")
+# S2H_LIB_PATH: measurement override (A/B of two builds of the same library)
+LIB_PATH = os.environ.get("S2H_LIB_PATH") or os.path.join(os.path.dirname(_HERE), "_lib", "libsam2hip.so")
 
 P = c_void_p
 I = c_int

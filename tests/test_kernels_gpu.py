@@ -459,6 +459,56 @@ def test_rope_roundtrip():
     _close(z, x, 1e-6)
 
 
+@pytest.mark.parametrize("dtype,D,nrot", [(torch.bfloat16, 256, 1024), (torch.float32, 64, 50), (torch.bfloat16, 6, 7)])
+def test_rope_vector_path(dtype, D, nrot):
+    """16-B vector RoPE (D % 8 == 0, aligned views) and the scalar fallback (D = 6) on strided
+    views that rotate only the first nrot rows; inverse undoes it."""
+    ops = _ops()
+    torch.manual_seed(12)
+    Bt, L = 3, nrot + 4
+    base = torch.randn(Bt, L, D + 8, device=DEV).to(dtype)
+    x = base[:, :, :D]
+    ang = torch.rand(nrot // 2 + 1, D // 2, device=DEV) * 6
+    cos, sin = ang.cos().contiguous(), ang.sin().contiguous()
+    y = torch.zeros(Bt, L, D, device=DEV, dtype=dtype)
+    ops.rope(x, y, nrot, cos, sin, nrot // 2 + 1)
+    per = nrot // 2 + 1
+    idx = torch.arange(nrot, device=DEV) % per
+    xc = torch.view_as_complex(x[:, :nrot].float().reshape(Bt, nrot, D // 2, 2).contiguous())
+    f = torch.polar(torch.ones_like(ang[idx]), ang[idx])
+    ref = torch.view_as_real(xc * f).flatten(2)
+    tol = 2e-2 if dtype == torch.bfloat16 else 1e-5
+    _close(y[:, :nrot], ref, tol)
+    assert (y[:, nrot:] == 0).all()
+    z = torch.zeros_like(y)
+    ops.rope(y, z, nrot, cos, sin, per, inverse=True)
+    _close(z[:, :nrot], x[:, :nrot].float(), 2 * tol)
+
+
+@pytest.mark.parametrize("dtype,C,H,ws", [(torch.bfloat16, 112, 18, 8), (torch.float32, 96, 14, 7),
+                                          (torch.bfloat16, 12, 9, 4)])
+def test_window_partition_roundtrip(dtype, C, H, ws):
+    """window partition (zero padding) / unpartition (padding dropped), plain and accumulating,
+    vector (C % 8) and scalar (C = 12) paths against a torch reference"""
+    ops = _ops()
+    torch.manual_seed(13)
+    B, W = 2, H + 3
+    x = torch.randn(B, H, W, C, device=DEV).to(dtype)
+    nh, nw = -(-H // ws), -(-W // ws)
+    xp = torch.nn.functional.pad(x.float(), (0, 0, 0, nw * ws - W, 0, nh * ws - H))
+    ref = xp.view(B, nh, ws, nw, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B * nh * nw, ws, ws, C)
+    win = ops.window_partition(x, ws)
+    _close(win, ref, 0)
+    acc = torch.ones_like(win)
+    ops.window_partition(x, ws, out=acc, accumulate=True)
+    _close(acc, ref + 1, 1e-2 if dtype == torch.bfloat16 else 1e-6)
+    back = ops.window_unpartition(win, ws, B, H, W)
+    _close(back, x.float(), 0)
+    acc2 = torch.ones_like(x)
+    ops.window_unpartition(win, ws, B, H, W, out=acc2, accumulate=True)
+    _close(acc2, x.float() + 1, 1e-2 if dtype == torch.bfloat16 else 1e-6)
+
+
 def test_mask_loss_and_adamw():
     ops = _ops()
     torch.manual_seed(3)
