@@ -356,9 +356,9 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     const float* src = (lane < 32 ? LSE : DI) + qi;
     lds_dma4(src, stage + 2 * C::TILEB + w * 256);
   };
-  dma_tile<DP, NWV * 32, NWV, true>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
-  dma_tile<DP, QT, NWV, true>(stages, Q, a.sql, qbase, a.Lq, w, lane);
-  dma_tile<DP, QT, NWV, true>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
+  dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
+  dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
+  dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
   bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, a.Lk - 1);
@@ -379,8 +379,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 256);  // [lse(32) | Di(32)]
     if (it + 1 < nt) {
       char* Qn = stages + ((it + 1) & 1) * STAGE;
-      dma_tile<DP, QT, NWV, true>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
-      dma_tile<DP, QT, NWV, true>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
+      dma_tile<DP, QT, NWV, true, 1>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
+      dma_tile<DP, QT, NWV, true, 1>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
       dma_rows(Qn, q0 + QT);
       wait_vmcnt<2 * C::PPW + 1>();
     } else {
@@ -391,10 +391,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     f32x16 s = f32x16{}, dp = f32x16{};  // S / dP: row q = 8(r>>2) + 4hi + (r&3), column key
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
-      const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP>(kl, 2 * t + hi));
-      const bf16x8 kb = *(const bf16x8*)(Kblk + swz<DP>(krow, 2 * t + hi));
+      const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP, 1>(kl, 2 * t + hi));
+      const bf16x8 kb = *(const bf16x8*)(Kblk + swz<DP, 1>(krow, 2 * t + hi));
       s = mfma32(qa, kb, s);
-      const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP>(kl, 2 * t + hi));
+      const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP, 1>(kl, 2 * t + hi));
       dp = mfma32(ga, vf[t], dp);
       if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the fragment prefetch depth
     }
@@ -416,8 +416,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        dv[d] = mfma32(tr_frag_perm32<DP>(Gb, 16 * c, 32 * d, lane), pdb[c], dv[d]);
-        dk[d] = mfma32(tr_frag_perm32<DP>(Qb, 16 * c, 32 * d, lane), dsb[c], dk[d]);
+        dv[d] = mfma32(tr_frag_perm32<DP, 1>(Gb, 16 * c, 32 * d, lane), pdb[c], dv[d]);
+        dk[d] = mfma32(tr_frag_perm32<DP, 1>(Qb, 16 * c, 32 * d, lane), dsb[c], dk[d]);
         if (d & 1) __builtin_amdgcn_sched_barrier(0);
       }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

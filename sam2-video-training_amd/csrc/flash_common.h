@@ -32,10 +32,24 @@ struct FlashCfg {
   static_assert(PPW >= 1, "tile smaller than one DMA piece per wave");
 };
 
+// XOR applied to the 16-B chunk index of image row `row`.
+//  SW 0: row mod (chunks per row) -- conflict-free for 16-row ds_read_b128 fragments and for
+//        transposing reads that span 8 rows x one 16-B chunk.
+//  SW 1: ((row & 3) << 2) | ((row >> 2) & 3) -- for the dK/dV kernel, whose transposing reads
+//        cover 4 rows x 4 consecutive chunks (32x32x16 fragments): under SW 0 the row only
+//        reached the low 2 chunk bits there and every read was a 4-way bank conflict (PMC:
+//        SQ_LDS_BANK_CONFLICT = half of SQ_LDS_IDX_ACTIVE).  Still conflict-free for its
+//        32-row ds_read_b128 reads.  Needs >= 16 chunks per row (DP >= 128).
+template <int DP, int SW = 0>
+__device__ __forceinline__ int swz_x(int row) {
+  if constexpr (SW == 0) return row & (DP / 8 - 1);
+  static_assert(SW == 0 || DP >= 128, "SW 1 needs 16 chunks per row");
+  return ((row & 3) << 2) | ((row >> 2) & 3);
+}
 // LDS byte offset of (row, 16-B chunk c) in a swizzled [rows][DP] image
-template <int DP>
+template <int DP, int SW = 0>
 __device__ __forceinline__ int swz(int row, int c) {
-  return row * (DP * 2) + ((c ^ (row & (DP / 8 - 1))) << 4);
+  return row * (DP * 2) + ((c ^ swz_x<DP, SW>(row)) << 4);
 }
 
 // DMA one tile (rows r0.., clamped to [0, nrows)) into a swizzled LDS image; the chunk
@@ -43,7 +57,7 @@ __device__ __forceinline__ int swz(int row, int c) {
 // ASM: issue through inline asm (lds_dma16) so the compiler's waitcnt pass does not put
 // vmcnt(0) before later ds_reads; the builtin form is kept where it measured faster (the
 // forward kernel, whose spilled address registers make every scratch reload a vmcnt wait).
-template <int DP, int ROWS, int NWV = FL_WAVES, bool ASM = false>
+template <int DP, int ROWS, int NWV = FL_WAVES, bool ASM = false, int SW = 0>
 __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w, int lane) {
   using C = FlashCfg<DP, ROWS, NWV>;
 #pragma unroll
@@ -51,7 +65,7 @@ __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_
     const int piece = w * C::PPW + i;
     const int row = piece * C::RPP + lane / C::NCH;
     const int pos = lane % C::NCH;
-    const int c = pos ^ (row & (C::NCH - 1));
+    const int c = pos ^ swz_x<DP, SW>(row);
     const int gr = min(r0 + row, nrows - 1);
     const bf16* g = src + (int64_t)gr * ld + c * 8;
     if constexpr (ASM)
@@ -125,14 +139,14 @@ __device__ __forceinline__ f32x16 mfma32(bf16x8 a, bf16x8 b, f32x16 c) {
 // 32x32x16 form of the transposing read: A[m = column c0 + (lane & 31)][k = 8hi + j] where
 // k <-> image row  rbase + 4hi + j (j < 4)  and  rbase + 8 + 4hi + (j - 4) (j >= 4), hi = lane >> 5
 // (the row order of a 32x32 accumulator's registers r = 8(j>>2) + ... within a 16-row step).
-template <int DP>
+template <int DP, int SW = 0>
 __device__ __forceinline__ bf16x8 tr_frag_perm32(const char* img, int rbase, int c0, int lane) {
   const int G = lane >> 4, hi = G >> 1, qq = (lane >> 2) & 3, pp = lane & 3;
   const int r0 = rbase + 4 * hi + qq;
   const int dcol = c0 + 16 * (G & 1) + 4 * pp;
   const int ch = dcol >> 3, off = (dcol & 7) * 2;
-  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP>(r0, ch) + off));
-  v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP>(r0 + 8, ch) + off));
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP, SW>(r0, ch) + off));
+  v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + swz<DP, SW>(r0 + 8, ch) + off));
   v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
   return __builtin_bit_cast(bf16x8, cat);
 }
