@@ -260,6 +260,18 @@ int s2h_mask_loss_finalize(int N, int64_t P, const float* stats, const float* pr
 int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
                       float inv_temp, const float* coef, float* dx, int64_t lddx, const float* gtot,
                       float* dious, hipStream_t st);
+/* BCECategoryLoss (losses.py:251-372, loss.type=bce): per-row stats[2*r..] = (sum of
+ * binary_cross_entropy_with_logits(x/T, t, pos_weight[r]), target sum); pos_weight may be NULL. */
+int s2h_bce_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                  float inv_temp, const float* pos_weight, float* stats, hipStream_t st);
+/* losses[0] += frame_scale * (mean (reduction 0) or sum (1) over the rows with target pixels);
+ * coef[N] are the backward coefficients. */
+int s2h_bce_finalize(int N, int64_t P, const float* stats, int reduction, float frame_scale, float* losses,
+                     float* coef, hipStream_t st);
+/* dx = gtot[0] * d(loss)/d(logits) (gtot: device scalar upstream gradient, NULL = 1). */
+int s2h_bce_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt, float inv_temp,
+                const float* pos_weight, const float* coef, const float* gtot, float* dx, int64_t lddx,
+                hipStream_t st);
 /* Evaluation counts of one frame (eval/eval.py:16-40 caculate_iou / _dice / _mae on the
  * binarised category-merged mask pred = logits > 0): counts[4n..4n+3] = |pred & gt|,
  * |pred | gt|, |pred|, |gt| as uint64 (zeroed by the call).  Validation only, no gradient. */

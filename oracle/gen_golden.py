@@ -39,6 +39,20 @@ CASES = {
     # Hiera-B+ structure (heads 2..16, head_dim 56, q-pool, global blocks 12/16/20) at a small resolution
     "bplus128_point_all": dict(size="base_plus", image_size=128, T=3, n_cat=4, n_obj=2, prompt="point",
                                trainable=ALL),
+    # 8 frames: the full memory bank (cond frame + 6 previous frames = all 7 maskmem_tpos_enc slots),
+    # object pointers from 8 frames and the non-cond bank prune (sam2model.py:365-377)
+    "bplus128_point_all_t8": dict(size="base_plus", image_size=128, T=8, n_cat=4, n_obj=3, prompt="point",
+                                  trainable=ALL),
+    # categories split into 2 and 3 connected components: the max / sigmoid-mass weighted merge
+    # over several objects (masks.py:53-213) and its gradient
+    "tiny256_point_all_multi": dict(size="tiny", image_size=256, T=4, n_cat=5, n_obj=3, parts=(2, 3),
+                                    prompt="point", trainable=ALL),
+    # memory-attention Lq = 256 (flash-attention size) in fp32 and under CPU bf16 autocast: the
+    # reference's own bf16 drift at the size where the bf16 kernels of the bench path run
+    "bplus256_point_all": dict(size="base_plus", image_size=256, T=4, n_cat=4, n_obj=3, prompt="point",
+                               trainable=ALL),
+    "bplus256_point_all_bf16": dict(size="base_plus", image_size=256, T=4, n_cat=4, n_obj=3, prompt="point",
+                                    trainable=ALL, autocast="bf16"),
 }
 FULL_GRAD_NUMEL = 4096
 
@@ -66,7 +80,7 @@ def run_case(name, c, seed=0, clip_idx=7):
     torch.manual_seed(0)
     model = H.build_reference_model(c["size"], c["image_size"], c["trainable"], c["prompt"], seed=seed)
     synth = H.product_file("data/synthetic.py")
-    clip = synth.make_clip(clip_idx, c["T"], c["image_size"], c["n_cat"], c["n_obj"])
+    clip = synth.make_clip(clip_idx, c["T"], c["image_size"], c["n_cat"], c["n_obj"], c.get("parts"))
     batch = reference_batch(clip)
     from sam2_video.model.losses import MultiStepMultiMasksAndIous, CORE_LOSS_KEY
     from sam2_video.utils import merge_object_results_to_category
@@ -75,13 +89,20 @@ def run_case(name, c, seed=0, clip_idx=7):
                                       supervise_all_iou=True, iou_use_l1_loss=True, pred_obj_scores=False,
                                       focal_gamma_obj_score=0.0, focal_alpha_obj_score=-1.0, logit_temperature=1.0)
     t0 = time.time()
-    # SAM2Model.forward (sam2model.py:153-179), restated to keep the per-object outputs
-    backbone_out = model.forward_image(batch.flat_img_batch)
-    feats = {f"fpn{i}": x.detach().clone() for i, x in enumerate(backbone_out["backbone_fpn"])}
-    backbone_out = model.prepare_prompt_inputs(backbone_out, batch)
-    stages = model.forward_tracking(backbone_out, batch)
-    outs = merge_object_results_to_category(stages, backbone_out["obj_to_cat"], backbone_out["num_categories"])
-    losses = crit(outs, batch.masks)
+    # SAM2Model.forward (sam2model.py:153-179), restated to keep the per-object outputs; under
+    # `autocast` the forward + loss run in torch.autocast("cpu", bfloat16) (the reference's
+    # trainer.precision bf16-mixed), the backward outside it as Lightning does
+    import contextlib
+    ac = (torch.autocast("cpu", dtype=torch.bfloat16) if c.get("autocast") == "bf16"
+          else contextlib.nullcontext())
+    with ac:
+        backbone_out = model.forward_image(batch.flat_img_batch)
+        feats = {f"fpn{i}": x.detach().float().clone() for i, x in enumerate(backbone_out["backbone_fpn"])}
+        backbone_out = model.prepare_prompt_inputs(backbone_out, batch)
+        stages = model.forward_tracking(backbone_out, batch)
+        outs = merge_object_results_to_category(stages, backbone_out["obj_to_cat"],
+                                                backbone_out["num_categories"])
+        losses = crit(outs, batch.masks)
     total = losses[CORE_LOSS_KEY]
     total.backward()
     dt = time.time() - t0
@@ -91,6 +112,8 @@ def run_case(name, c, seed=0, clip_idx=7):
     g["meta/image_size"] = torch.tensor(c["image_size"])
     g["meta/seed"] = torch.tensor(seed)
     g["meta/clip_idx"] = torch.tensor(clip_idx)
+    g["meta/parts"] = torch.tensor(list(c.get("parts") or []), dtype=torch.long)
+    g["meta/autocast"] = torch.tensor(1 if c.get("autocast") == "bf16" else 0)
     g["in/images_sum"] = clip["images"].double().sum()
     g["in/images_abs"] = clip["images"].double().abs().sum()
     g["in/masks_count"] = clip["masks"].sum(dim=(2, 3))
@@ -104,20 +127,20 @@ def run_case(name, c, seed=0, clip_idx=7):
         g[f"feat/{k}_sq"] = (v.double() ** 2).sum()
     g["feat/fpn_last"] = feats[f"fpn{len(feats) - 1}"]
     for t, st in enumerate(stages):
-        g[f"obj/{t}/low_res"] = st["pred_masks"].detach().clone()
-        g[f"obj/{t}/ious"] = st["multistep_pred_ious"][0].detach().clone()
-        g[f"obj/{t}/obj_score"] = st["multistep_object_score_logits"][0].detach().clone()
+        g[f"obj/{t}/low_res"] = st["pred_masks"].detach().float().clone()
+        g[f"obj/{t}/ious"] = st["multistep_pred_ious"][0].detach().float().clone()
+        g[f"obj/{t}/obj_score"] = st["multistep_object_score_logits"][0].detach().float().clone()
     for t, o in enumerate(outs):
-        hr = o["multistep_pred_multimasks_high_res"][0].detach()
-        g[f"cat/{t}/low_res"] = o["pred_masks"].detach().clone()
+        hr = o["multistep_pred_multimasks_high_res"][0].detach().float()
+        g[f"cat/{t}/low_res"] = o["pred_masks"].detach().float().clone()
         g[f"cat/{t}/high_res_sub"] = hr[:, :, ::8, ::8].clone()
         g[f"cat/{t}/high_res_sum"] = hr.double().sum()
         g[f"cat/{t}/high_res_sq"] = (hr.double() ** 2).sum()
-        g[f"cat/{t}/ious"] = o["multistep_pred_ious"][0].detach().clone()
-        g[f"cat/{t}/obj_score"] = o["multistep_object_score_logits"][0].detach().clone()
+        g[f"cat/{t}/ious"] = o["multistep_pred_ious"][0].detach().float().clone()
+        g[f"cat/{t}/obj_score"] = o["multistep_object_score_logits"][0].detach().float().clone()
     for k in ("loss_mask", "loss_dice", "loss_iou", "loss_class", CORE_LOSS_KEY):
         v = losses[k]
-        g[f"loss/{k}"] = v.detach().clone() if torch.is_tensor(v) else torch.tensor(float(v))
+        g[f"loss/{k}"] = v.detach().float().clone() if torch.is_tensor(v) else torch.tensor(float(v))
     none_grad = []
     for n, p in model.named_parameters():
         if not p.requires_grad:

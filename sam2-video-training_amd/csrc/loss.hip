@@ -144,6 +144,104 @@ extern "C" int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, 
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------- BCE category loss
+// BCECategoryLoss (losses.py:251-372): per frame, binary_cross_entropy_with_logits over the
+// categories with ground-truth pixels (logits / T, optional per-category pos_weight), mean (or
+// sum) reduction, averaged over frames.  bce = (1 - t) x + (1 + (pw - 1) t) softplus(-x).
+// stats[n] = {sum bce, sum t}
+__global__ __launch_bounds__(256) void bce_stats_kernel(int N, int64_t P, const float* x, int64_t ldx,
+                                                        const uint8_t* tgt, int64_t ldt, float inv_temp,
+                                                        const float* pos_weight, float* stats) {
+  const int n = blockIdx.y;
+  const int64_t chunk = (P + gridDim.x - 1) / gridDim.x;
+  const int64_t p0 = blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+  const float pw = pos_weight ? pos_weight[n] : 1.f;
+  float a0 = 0.f, a1 = 0.f;
+  for (int64_t p = p0 + threadIdx.x; p < p1; p += 256) {
+    const float xv = x[n * ldx + p] * inv_temp;
+    const float t = tgt[n * ldt + p] ? 1.f : 0.f;
+    const float lw = 1.f + (pw - 1.f) * t;
+    a0 += (1.f - t) * xv + lw * (log1pf(expf(-fabsf(xv))) + fmaxf(-xv, 0.f));
+    a1 += t;
+  }
+  __shared__ float red[4][2];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  a0 = wave_sum(a0);
+  a1 = wave_sum(a1);
+  if (lane == 0) { red[w][0] = a0; red[w][1] = a1; }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    atomicAdd(&stats[n * 2 + threadIdx.x], v);
+  }
+}
+extern "C" int s2h_bce_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                             float inv_temp, const float* pos_weight, float* stats, hipStream_t st) {
+  if (N <= 0) return 0;
+  s2h_zero_f32(stats, 1, (int64_t)N * 2, (int64_t)N * 2, st);
+  int chunks = (int)((P + 4095) / 4096);
+  if (chunks > 256) chunks = 256;
+  if (chunks < 1) chunks = 1;
+  hipLaunchKernelGGL(bce_stats_kernel, dim3(chunks, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
+                     pos_weight, stats);
+  return (int)hipGetLastError();
+}
+// losses[0] += frame_scale * frame loss; coef[n] = d(frame_scale * loss) / d(bce sum of row n).
+// reduction 0 = mean over the valid rows' elements (0/0 = NaN when no row is valid, as torch's
+// mean of an empty tensor), 1 = sum.
+__global__ void bce_finalize_kernel(int N, int64_t P, const float* stats, int reduction, float frame_scale,
+                                    float* losses, float* coef) {
+  if (threadIdx.x != 0) return;
+  int nv = 0;
+  float tot = 0.f;
+  for (int n = 0; n < N; ++n) {
+    if (stats[n * 2 + 1] > 0.f) { ++nv; tot += stats[n * 2]; }
+  }
+  const float den = reduction == 0 ? (float)nv * (float)P : 1.f;
+  const float c = nv > 0 ? frame_scale / den : 0.f;
+  for (int n = 0; n < N; ++n) coef[n] = stats[n * 2 + 1] > 0.f ? c : 0.f;
+  losses[0] += frame_scale * (tot / den);
+}
+extern "C" int s2h_bce_finalize(int N, int64_t P, const float* stats, int reduction, float frame_scale,
+                                float* losses, float* coef, hipStream_t st) {
+  hipLaunchKernelGGL(bce_finalize_kernel, dim3(1), dim3(64), 0, st, N, P, stats, reduction, frame_scale, losses,
+                     coef);
+  return (int)hipGetLastError();
+}
+// dx = gtot * coef[n] * inv_temp * ((1 - t) - (1 + (pw - 1) t) * sigmoid(-x))
+__global__ void bce_bwd_kernel(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                               float inv_temp, const float* pos_weight, const float* coef, const float* gtot,
+                               float* dx, int64_t lddx) {
+  const int64_t n_all = (int64_t)N * P;
+  const float gs = gtot ? gtot[0] : 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = i / P;
+    const int64_t p = i - (int64_t)n * P;
+    float g = 0.f;
+    const float c = coef[n];
+    if (c != 0.f) {
+      const float xv = x[n * ldx + p] * inv_temp;
+      const float t = tgt[n * ldt + p] ? 1.f : 0.f;
+      const float pw = pos_weight ? pos_weight[n] : 1.f;
+      const float lw = 1.f + (pw - 1.f) * t;
+      const float sneg = 1.f / (1.f + expf(xv));
+      g = c * inv_temp * ((1.f - t) - lw * sneg);
+    }
+    dx[n * lddx + p] = g * gs;
+  }
+}
+extern "C" int s2h_bce_bwd(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
+                           float inv_temp, const float* pos_weight, const float* coef, const float* gtot, float* dx,
+                           int64_t lddx, hipStream_t st) {
+  const int64_t n = (int64_t)N * P;
+  if (n <= 0) return 0;
+  int64_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  hipLaunchKernelGGL(bce_bwd_kernel, dim3((unsigned)b), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
+                     pos_weight, coef, gtot, dx, lddx);
+  return (int)hipGetLastError();
+}
+
 // ---------------------------------------------------------- category merge
 // cat_off[c]..cat_off[c+1] index into cat_obj (object ids of category c).
 __global__ void group_max_fwd_kernel(int Ncat, int64_t P, const int* cat_off, const int* cat_obj, const float* x,
@@ -157,7 +255,8 @@ __global__ void group_max_fwd_kernel(int Ncat, int64_t P, const int* cat_off, co
     for (int k = cat_off[c]; k < cat_off[c + 1]; ++k) {
       const int o = cat_obj[k];
       const float v = x[o * ldx + p];
-      if (best < 0 || v > m) { m = v; best = o; }
+      // first maximum wins ties; the first NaN wins outright (torch.max(dim) semantics)
+      if (best < 0 || v > m || (v != v && m == m)) { m = v; best = o; }
     }
     y[c * ldy + p] = m;
     if (arg) arg[i] = best;

@@ -17,8 +17,14 @@ import math
 import torch
 
 
-def make_clip(clip_idx: int, num_frames: int, image_size: int, n_cat: int, n_obj: int):
-    """Returns {"images": [T, 3, H, W] f32, "masks": [T, n_cat, H, W] bool}."""
+def make_clip(clip_idx: int, num_frames: int, image_size: int, n_cat: int, n_obj: int, parts=None):
+    """Returns {"images": [T, 3, H, W] f32, "masks": [T, n_cat, H, W] bool}.
+
+    `parts` (optional): component counts of categories 0..len(parts)-1.  A category with k > 1
+    components holds k smaller discs side by side in its cell (radius cell/(3k+1), spacing
+    cell/k: gaps wider than the 5x5 opening), so the frame-0 connected-component split
+    (masks.py:13-50) turns it into k tracked objects that the category merge (masks.py:53-213)
+    has to recombine."""
     H = W = image_size
     g = torch.Generator().manual_seed(int(clip_idx))
     images = torch.randn(num_frames, 3, H, W, generator=g, dtype=torch.float32)
@@ -28,11 +34,19 @@ def make_clip(clip_idx: int, num_frames: int, image_size: int, n_cat: int, n_obj
     ys = torch.arange(H, dtype=torch.float32).view(H, 1)
     xs = torch.arange(W, dtype=torch.float32).view(1, W)
     masks = torch.zeros(num_frames, n_cat, H, W, dtype=torch.bool)
+    parts = list(parts or [])
     for t in range(num_frames):
         for c in range(min(n_obj, n_cat)):
             cx = (c % grid + 0.5) * cell + t
             cy = (c // grid + 0.5) * cell + t
-            masks[t, c] = (xs - cx) ** 2 + (ys - cy) ** 2 <= r * r
+            k = parts[c] if c < len(parts) else 1
+            if k <= 1:
+                masks[t, c] = (xs - cx) ** 2 + (ys - cy) ** 2 <= r * r
+                continue
+            rk = cell / (3.0 * k + 1.0)
+            for j in range(k):
+                jx = cx + (j - (k - 1) / 2.0) * (cell / k)
+                masks[t, c] |= (xs - jx) ** 2 + (ys - cy) ** 2 <= rk * rk
     return {"images": images, "masks": masks}
 
 
@@ -59,5 +73,24 @@ def sam2_collate_fn(batch_list):
                                  metadata=meta, dict_key="video_batch", batch_size=[T])
 
 
-def synthetic_batch(clip_idx: int, num_frames: int, image_size: int, n_cat: int, n_obj: int):
-    return sam2_collate_fn([make_clip(clip_idx, num_frames, image_size, n_cat, n_obj)])
+def synthetic_batch(clip_idx: int, num_frames: int, image_size: int, n_cat: int, n_obj: int, parts=None):
+    return sam2_collate_fn([make_clip(clip_idx, num_frames, image_size, n_cat, n_obj, parts)])
+
+
+class SyntheticClipDataset:
+    """Map-style dataset of deterministic synthetic clips (clip index = offset + i), the stand-in
+    for the reference's COCODataset (dataset.py:305-343) when no annotation files are present.
+    Items are {"images", "masks"} dicts, collated by sam2_collate_fn."""
+
+    def __init__(self, num_clips: int, num_frames: int, image_size: int, n_cat: int, n_obj: int, offset: int = 0,
+                 parts=None):
+        self.num_clips, self.num_frames, self.image_size = int(num_clips), int(num_frames), int(image_size)
+        self.n_cat, self.n_obj, self.offset, self.parts = int(n_cat), int(n_obj), int(offset), parts
+
+    def __len__(self):
+        return self.num_clips
+
+    def __getitem__(self, i):
+        if not 0 <= i < self.num_clips:
+            raise IndexError(i)
+        return make_clip(self.offset + i, self.num_frames, self.image_size, self.n_cat, self.n_obj, self.parts)

@@ -67,6 +67,9 @@ SIGNATURES = {
     "s2h_mask_stats": [I, L, P, L, P, L, F, P, P],
     "s2h_mask_loss_finalize": [I, L, P, P, P, F, F, F, F, P, P, P],
     "s2h_mask_loss_bwd": [I, L, P, L, P, L, F, P, P, L, P, P, P],
+    "s2h_bce_stats": [I, L, P, L, P, L, F, P, P, P],
+    "s2h_bce_finalize": [I, L, P, I, F, P, P, P],
+    "s2h_bce_bwd": [I, L, P, L, P, L, F, P, P, P, P, L, P],
     "s2h_mask_eval_counts": [I, L, P, L, P, L, P, P],
     "s2h_group_max_fwd": [I, L, P, P, P, L, P, L, P, P],
     "s2h_group_max_bwd": [I, L, P, P, P, L, P, L, P],

@@ -361,3 +361,32 @@ class _FrameLoss(torch.autograd.Function):
 
 def frame_loss(logits, ious, tgt, valid, weights=(20.0, 1.0, 1.0), temperature=1.0):
     return _FrameLoss.apply(logits, ious, tgt, valid, tuple(float(w) for w in weights), 1.0 / float(temperature))
+
+
+class _BCEFrame(torch.autograd.Function):
+    """one frame of BCECategoryLoss (losses.py:306-366): BCE-with-logits over the categories with
+    ground truth, reduced and scaled by 1/num_frames; accumulates into `acc` [1] f32"""
+
+    @staticmethod
+    def forward(ctx, logits, tgt, pos_weight, inv_temp, reduction, frame_scale):
+        N = logits.shape[0]
+        x = logits.reshape(N, -1)
+        t = tgt.reshape(N, -1).view(torch.uint8)
+        stats = ops.bce_stats(x, t, inv_temp, pos_weight)
+        loss = torch.zeros(1, device=x.device)
+        coef = torch.empty(N, device=x.device)
+        ops.bce_finalize(stats, x.shape[1], reduction, frame_scale, loss, coef)
+        ctx.save_for_backward(x, t, coef, pos_weight)
+        ctx.inv_temp, ctx.shape = inv_temp, logits.shape
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        x, t, coef, pw = ctx.saved_tensors
+        dx = torch.empty_like(x)
+        ops.bce_bwd(x, t, ctx.inv_temp, pw, coef, dx, gtot=g.contiguous())
+        return dx.view(ctx.shape), None, None, None, None, None
+
+
+def bce_frame_loss(logits, tgt, pos_weight, temperature, reduction, frame_scale):
+    return _BCEFrame.apply(logits, tgt, pos_weight, 1.0 / float(temperature), int(reduction), float(frame_scale))

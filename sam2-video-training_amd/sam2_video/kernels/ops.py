@@ -424,6 +424,27 @@ def mask_loss_bwd(x, tgt, coef, inv_temp, dx, gtot=None, dious=None):
     return dx
 
 
+def bce_stats(x, tgt, inv_temp=1.0, pos_weight=None):
+    """x [N, P] f32 logits, tgt [N, P] uint8 -> stats [N, 2] (bce sum, target sum)"""
+    N, P = x.shape
+    stats = torch.empty(N, 2, device=x.device, dtype=torch.float32)
+    call("s2h_bce_stats", N, P, ptr(x), x.stride(0), ptr(tgt), tgt.stride(0), float(inv_temp), ptr(pos_weight),
+         ptr(stats), stream())
+    return stats
+
+
+def bce_finalize(stats, P, reduction, frame_scale, losses, coef):
+    call("s2h_bce_finalize", stats.shape[0], P, ptr(stats), int(reduction), float(frame_scale), ptr(losses),
+         ptr(coef), stream())
+
+
+def bce_bwd(x, tgt, inv_temp, pos_weight, coef, dx, gtot=None):
+    N, P = x.shape
+    call("s2h_bce_bwd", N, P, ptr(x), x.stride(0), ptr(tgt), tgt.stride(0), float(inv_temp), ptr(pos_weight),
+         ptr(coef), ptr(gtot), ptr(dx), dx.stride(0), stream())
+    return dx
+
+
 def group_max(x, cat_off, cat_obj, ncat, out, arg):
     P = x.shape[1]
     call("s2h_group_max_fwd", ncat, P, ptr(cat_off), ptr(cat_obj), ptr(x), x.stride(0), ptr(out), out.stride(0),

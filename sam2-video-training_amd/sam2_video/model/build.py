@@ -32,8 +32,22 @@ _TARGETS = {
 }
 
 
+# Lightning classes of the reference configs (best.yaml:13,22,99); Lightning is not installed here, so the
+# trainer resolves to this build's Lightning-API Trainer (training/trainer.py) unless it is importable
+_LIGHTNING = {
+    "lightning.pytorch.trainer.trainer.Trainer": "sam2_video.training.trainer.Trainer",
+    "lightning.pytorch.Trainer": "sam2_video.training.trainer.Trainer",
+    "lightning.Trainer": "sam2_video.training.trainer.Trainer",
+}
+
+
 def _resolve(target: str):
     path = _TARGETS.get(target, target)
+    if path in _LIGHTNING:
+        try:
+            importlib.import_module("lightning")
+        except ImportError:
+            path = _LIGHTNING[path]
     mod, name = path.rsplit(".", 1)
     return getattr(importlib.import_module(mod), name)
 
@@ -47,10 +61,13 @@ def _coerce(v):
     return v
 
 
-def instantiate(cfg, **override):
+def instantiate(cfg, _recursive_: bool = True, **override):
+    """hydra.utils.instantiate for `_target_` dicts; `_recursive_=False` passes nested sections
+    through as plain dicts (train.py:103-104 instantiates module / data_module that way)."""
     if isinstance(cfg, dict):
         if "_target_" in cfg:
-            kw = {k: instantiate(v) for k, v in cfg.items() if k != "_target_"}
+            rec = cfg.get("_recursive_", _recursive_)
+            kw = {k: (instantiate(v) if rec else v) for k, v in cfg.items() if k not in ("_target_", "_recursive_")}
             kw.update(override)
             return _resolve(cfg["_target_"])(**kw)
         return {k: instantiate(v) for k, v in cfg.items()}

@@ -15,7 +15,7 @@ import torch
 from torch import nn
 
 from ..kernels import functional as FN
-from ..kernels.functional_sam import frame_loss
+from ..kernels.functional_sam import bce_frame_loss, frame_loss
 
 CORE_LOSS_KEY = "total_loss"
 
@@ -55,6 +55,49 @@ class MultiStepMultiMasksAndIous(nn.Module):
 
 
 class BCECategoryLoss(nn.Module):
+    """losses.py:251-372: per frame, binary_cross_entropy_with_logits(logits / T, gt, pos_weight)
+    over the categories that have ground-truth pixels (category-level `pred_masks_high_res`,
+    else `pred_masks`), "mean" or "sum" reduction, averaged over frames.  One statistics kernel,
+    one finalize kernel and, in backward, one elementwise kernel per frame."""
+
     def __init__(self, pos_weight=None, reduction: str = "mean", logit_temperature: float = 1.0):
         super().__init__()
-        raise NotImplementedError("BCECategoryLoss (loss.type=bce) is not built yet in this MI355X build")
+        if isinstance(pos_weight, (list, tuple)):
+            pos_weight = torch.tensor(pos_weight, dtype=torch.float32)
+        self._pos_weight = pos_weight.float().reshape(-1) if isinstance(pos_weight, torch.Tensor) else None
+        if reduction not in ("mean", "sum"):
+            raise NotImplementedError("BCECategoryLoss reductions: mean | sum (the per-frame sum of a 'none' "
+                                      "reduction is not shape-stable in the reference either)")
+        self.reduction = reduction
+        if not (isinstance(logit_temperature, (int, float)) and logit_temperature > 0):
+            raise ValueError("logit_temperature must be a positive float")
+        self.logit_temperature = float(logit_temperature)
+
+    def forward(self, outs_batch: List[Dict], targets_batch: torch.Tensor) -> Dict[str, torch.Tensor]:
+        assert len(outs_batch) == len(targets_batch), (
+            f"Mismatched sequence lengths: outs={len(outs_batch)} vs targets={len(targets_batch)}")
+        num_frames = len(outs_batch)
+        acc = None
+        for outs, targets in zip(outs_batch, targets_batch):
+            logits = outs.get("pred_masks_high_res")
+            if logits is None:
+                logits = outs.get("pred_masks")
+            if logits is None:
+                raise KeyError("BCECategoryLoss expects 'pred_masks_high_res' or 'pred_masks' in outputs")
+            if logits.dim() == 4 and logits.shape[1] == 1:
+                logits = logits.squeeze(1)
+            elif logits.dim() != 3:
+                raise ValueError(f"Unexpected logits shape for BCECategoryLoss: {tuple(logits.shape)}")
+            if targets.dim() != 3:
+                raise ValueError(f"Unexpected target shape for BCECategoryLoss: {tuple(targets.shape)}")
+            pw = None
+            if self._pos_weight is not None:
+                if self._pos_weight.numel() != logits.shape[0]:
+                    raise ValueError(f"pos_weight length {self._pos_weight.numel()} does not match number of "
+                                     f"classes {logits.shape[0]}")
+                pw = self._pos_weight.to(logits.device)
+            lf = bce_frame_loss(logits.float().contiguous(), targets.contiguous(), pw, self.logit_temperature,
+                                0 if self.reduction == "mean" else 1, 1.0 / max(num_frames, 1))
+            acc = lf if acc is None else FN.add(acc, lf)
+        total = acc[0]
+        return {"loss_bce": total, CORE_LOSS_KEY: total}

@@ -74,11 +74,41 @@ class SAM2Model(SAM2Base):
         else:  # offline: deterministic synthetic weights keyed by parameter name
             self.load_state_dict({k: synth_tensor(k, v.shape, seed) for k, v in sd.items()}, strict=True)
 
+    @staticmethod
+    def strip_lightning_prefix(ck):
+        """Lightning .ckpt -> model state_dict: the `state_dict` entry with the `model.` prefix of
+        SAM2LightningModule.model removed (reference train.py:146-157)"""
+        sd = ck["state_dict"] if isinstance(ck, dict) and "state_dict" in ck else ck
+        if any(k.startswith("model.") for k in sd):
+            sd = {k[len("model."):]: v for k, v in sd.items() if k.startswith("model.")}
+        return sd
+
+    def load_lightning_checkpoint(self, path, strict: bool = True):
+        """weights of a Lightning checkpoint of SAM2LightningModule (Trainer.save_checkpoint or the
+        reference's ModelCheckpoint files); re-run load(device) afterwards if the arena exists"""
+        ck = torch.load(path, map_location="cpu", weights_only=True)
+        sd = self.strip_lightning_prefix(ck)
+        if self.arena is not None:  # parameters are arena views: copy in place
+            with torch.no_grad():
+                own = self.state_dict()
+                missing = [k for k in own if k not in sd]
+                if strict and missing:
+                    raise KeyError(f"checkpoint misses {len(missing)} keys, e.g. {missing[:3]}")
+                for k, v in sd.items():
+                    if k in own:
+                        own[k].copy_(v.to(own[k].device, own[k].dtype))
+            self.arena.refresh_shadow()
+            return self
+        self.load_state_dict(sd, strict=strict)
+        return self
+
     def _load_finetuned(self, path):
-        """sam2model.py:109-126"""
-        if path.count("all") > 0:
+        """sam2model.py:109-126 (an "all" path holds a full state dict; a Lightning .ckpt is
+        unwrapped as train.py:146-157 does)"""
+        if path.count("all") > 0 or path.endswith(".ckpt"):
             sd = torch.load(path, map_location="cpu", weights_only=True)
-            self.load_state_dict(sd if isinstance(sd, (dict, OrderedDict)) else sd.state_dict(), strict=False)
+            sd = sd if isinstance(sd, (dict, OrderedDict)) else sd.state_dict()
+            self.load_state_dict(self.strip_lightning_prefix(sd), strict=False)
         else:
             self.sam_mask_decoder.load_state_dict(torch.load(path, map_location="cpu", weights_only=True), strict=True)
             pe_path = path.replace(".torch", "_prompt_encoder.torch")

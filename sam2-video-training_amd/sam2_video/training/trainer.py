@@ -1,20 +1,38 @@
-"""SAM2LightningModule drop-in (reference sam2_video/training/trainer.py:28-322)
-and the fit loop that replaces Lightning's (Lightning is not a dependency here).
+"""SAM2LightningModule / SAM2LightningDataModule drop-ins (reference
+sam2_video/training/trainer.py:28-400) and a Lightning-API Trainer for them.
 
-Same constructor (model, loss, optimizer, scheduler, visualization config
-sections), same loss selection, gt_stride, training_step/validation_step
-signatures and logged keys.  `configure_optimizers` returns the arena AdamW
-(eps/amsgrad of the YAML are ignored exactly as the reference does,
-trainer.py:124-130) with the cosine-with-warmup schedule stepped per
-optimizer step.  The reference's per-step torch.cuda.synchronize() +
-empty_cache() (trainer.py:186-187) are host syncs with no effect on results and
-are omitted.  W&B GIF logging is out of scope.
+* `SAM2LightningModule(model, loss, optimizer, scheduler, visualization)`: same
+  constructor sections, loss selection (multi_step | bce), gt_stride,
+  training_step / validation_step signatures and logged keys.  It subclasses
+  `lightning.pytorch.LightningModule` when Lightning is importable, else
+  `nn.Module`.  `configure_optimizers` returns the arena AdamW (eps/amsgrad of
+  the YAML are ignored exactly as the reference does, trainer.py:124-130) with
+  the cosine-with-warmup schedule stepped per optimizer step.
+* `SAM2LightningDataModule(data, train_shuffle)`: DataLoaders of B == 1 clips
+  collated by `sam2_collate_fn` (trainer.py:325-400); COCO files when the data
+  section's paths exist, synthetic clips of the data section's shape otherwise.
+* `Trainer(**cfg.trainer)`: the `lightning.pytorch.Trainer` arguments the
+  reference configs set (best.yaml:98-113) -- max_epochs / max_steps,
+  accumulate_grad_batches, gradient_clip_val (0 / None = no clip, as Lightning),
+  precision, val_check_interval, num_sanity_val_steps, limit_*_batches -- and
+  `fit(module, datamodule)`.  `model/build.py` resolves the configs'
+  `_target_: lightning.pytorch.trainer.trainer.Trainer` to it when Lightning is
+  not installed (it is not in this image).
+* `StepRunner`: one micro-step of the fit loop on the device (captured HIP
+  graph per input signature), RCCL all-reduce + clip + AdamW at accumulation
+  boundaries.
+
+The reference's per-step torch.cuda.synchronize() + empty_cache()
+(trainer.py:186-187) are host syncs with no effect on results and are omitted.
+W&B GIF logging is out of scope.
 """
 from __future__ import annotations
 
+import math
+import os
 import time
 from types import SimpleNamespace
-from typing import Any, Dict, List
+from typing import Any, Dict, List, Optional
 
 import torch
 from torch import nn
@@ -25,6 +43,12 @@ from ..model.losses import CORE_LOSS_KEY, BCECategoryLoss, MultiStepMultiMasksAn
 from .ddp import ArenaGradReducer
 from .optim import ArenaAdamW, cosine_with_warmup
 
+try:  # the reference's base classes when Lightning is installed (it is not in this image)
+    import lightning.pytorch as _pl
+    _ModuleBase, _DataBase, HAVE_LIGHTNING = _pl.LightningModule, _pl.LightningDataModule, True
+except Exception:  # pragma: no cover - depends on the environment
+    _ModuleBase, _DataBase, HAVE_LIGHTNING = nn.Module, object, False
+
 
 def _ns(x):
     if isinstance(x, dict):
@@ -33,6 +57,8 @@ def _ns(x):
 
 
 def _get(ns, k, default=None):
+    if ns is None:
+        return default
     if isinstance(ns, dict):
         return ns.get(k, default)
     return getattr(ns, k, default)
@@ -41,64 +67,92 @@ def _get(ns, k, default=None):
 def _todict(x):
     if isinstance(x, SimpleNamespace):
         return {k: _todict(v) for k, v in vars(x).items()}
+    if hasattr(x, "items") and not isinstance(x, dict):  # OmegaConf DictConfig
+        return {k: _todict(v) for k, v in x.items()}
     return x
 
 
-class SAM2LightningModule(nn.Module):
+def precision_dtype(precision) -> str:
+    """Lightning `precision` -> compute dtype of the kernels.  "16"/"16-mixed" (fp16 AMP in the
+    reference configs, best.yaml:103) and "bf16*" run bf16 (same width; fp16 is not a CDNA4
+    training format here), "32*"/"64*" run the fp32 mode."""
+    p = str(precision if precision is not None else "bf16").lower()
+    return "fp32" if p.startswith("32") or p.startswith("64") else "bf16"
+
+
+class SAM2LightningModule(_ModuleBase):
     def __init__(self, model: Any, loss: Any, optimizer: Any, scheduler: Any, visualization: Any = None):
         super().__init__()
-        self.hparams = SimpleNamespace(model=model, loss=_ns(loss), optimizer=_ns(optimizer),
-                                       scheduler=_ns(scheduler), visualization=_ns(visualization or {}))
-        self.model = None
-        lt = _get(self.hparams.loss, "type", None)
-        if lt is not None and str(lt).lower() in {"bce", "bce_only", "ce_only"}:
-            self.criterion = BCECategoryLoss(pos_weight=_get(self.hparams.loss, "bce_pos_weight"),
-                                             reduction=_get(self.hparams.loss, "bce_reduction", "mean"),
-                                             logit_temperature=_get(self.hparams.loss, "bce_logit_temperature", 1.0))
+        cfg = SimpleNamespace(model=model, loss=_ns(_todict(loss)), optimizer=_ns(_todict(optimizer)),
+                              scheduler=_ns(_todict(scheduler)), visualization=_ns(_todict(visualization or {})))
+        if HAVE_LIGHTNING:  # pragma: no cover
+            self.save_hyperparameters(ignore=["model"] if isinstance(model, nn.Module) else None)
+            self.automatic_optimization = False  # the arena optimizer steps itself (training_step)
         else:
-            L = self.hparams.loss
+            self.hparams = cfg
+        self.cfg = cfg
+        self.model = None
+        L = cfg.loss
+        lt = _get(L, "type", None)
+        if lt is not None and str(lt).lower() in {"bce", "bce_only", "ce_only"}:
+            self.criterion = BCECategoryLoss(pos_weight=_get(L, "bce_pos_weight"),
+                                             reduction=_get(L, "bce_reduction", "mean"),
+                                             logit_temperature=_get(L, "bce_logit_temperature", 1.0))
+        else:
             self.criterion = MultiStepMultiMasksAndIous(
                 weight_dict=_todict(_get(L, "weight_dict")), supervise_all_iou=_get(L, "supervise_all_iou", False),
                 iou_use_l1_loss=_get(L, "iou_use_l1_loss", False), pred_obj_scores=_get(L, "pred_obj_scores", False),
                 focal_gamma_obj_score=_get(L, "focal_gamma_obj_score", 0.0),
                 focal_alpha_obj_score=_get(L, "focal_alpha_obj_score", -1.0),
                 logit_temperature=_get(L, "multistep_logit_temperature", 1.0))
-        self.loss_gt_stride = max(int(_get(self.hparams.loss, "gt_stride", 1)), 1)
-        self.logged: Dict[str, torch.Tensor] = {}
+        self.loss_gt_stride = max(int(_get(L, "gt_stride", 1)), 1)
+        self.logged: Dict[str, Any] = {}
         self.optimizer = None
         self.lr_at = None
-        self.reducer = None
+        self.gradient_clip_val = None  # set by the Trainer (Lightning's trainer.gradient_clip_val)
+        self.compute_dtype = None  # set by the Trainer from `precision`
+        self._runner = None
 
     # ------------------------------------------------------------ setup
     def setup(self, stage: str = "fit", device=None):
+        """trainer.py:101-115: instantiate the model section, load it on the device, train mode"""
         if stage == "fit":
             if self.model is None:
-                m = self.hparams.model
-                self.model = m if isinstance(m, nn.Module) else instantiate(_todict(m))
-            self.model.load(device or "cuda")
+                m = self.cfg.model
+                if isinstance(m, nn.Module):
+                    self.model = m
+                else:
+                    kw = {"compute_dtype": self.compute_dtype} if self.compute_dtype else {}
+                    self.model = instantiate(_todict(m), **kw)
+            if device is None:
+                device = "cuda"
+            self.model.load(device)
             self.model.train()
 
     def configure_optimizers(self, total_steps: int = 1) -> Dict[str, Any]:
-        o = self.hparams.optimizer
-        if str(_get(o, "type", "adamw")).lower() == "adamw":
-            opt = ArenaAdamW(self.model.arena, lr=_get(o, "lr", 1e-4), weight_decay=_get(o, "weight_decay", 0.01),
-                             betas=tuple(_get(o, "betas", (0.9, 0.999))), eps=1e-8,
-                             max_grad_norm=_get(o, "gradient_clip_val", 1.0))
-        else:
+        """trainer.py:117-177: AdamW(lr, weight_decay, betas) -- eps 1e-8 / amsgrad False whatever the
+        YAML says -- with get_cosine_schedule_with_warmup(total * warmup_factor, total), stepped per
+        optimizer step.  The clip is the Trainer's gradient_clip_val (Lightning's clip_grad_norm_)."""
+        o = self.cfg.optimizer
+        if str(_get(o, "type", "adamw")).lower() != "adamw":
             raise NotImplementedError("only AdamW (the reference configs' optimizer) is built")
+        opt = ArenaAdamW(self.model.arena, lr=_get(o, "lr", 1e-4), weight_decay=_get(o, "weight_decay", 0.01),
+                         betas=tuple(_get(o, "betas", (0.9, 0.999))), eps=1e-8,
+                         max_grad_norm=self.gradient_clip_val)
         self.optimizer = opt
         sched = None
-        if _get(self.hparams.scheduler, "enabled", True):
+        if _get(self.cfg.scheduler, "enabled", True):
             total = max(1, int(total_steps))
             warm = total * float(_get(o, "warmup_factor", 0.0))
             if warm >= total:
                 warm = max(0, total - 1)
-            self.lr_at = cosine_with_warmup(opt.lr, warm, total, float(_get(self.hparams.scheduler, "num_cycles", 0.5)))
+            self.lr_at = cosine_with_warmup(opt.lr, warm, total, float(_get(self.cfg.scheduler, "num_cycles", 0.5)))
             sched = {"scheduler": self.lr_at, "interval": "step", "frequency": 1}
         return {"optimizer": opt, "lr_scheduler": sched} if sched else {"optimizer": opt}
 
     # --------------------------------------------------------- forward
     def forward(self, batch):
+        """trainer.py:182-188"""
         return self.model(batch)
 
     def _apply_gt_stride(self, outs_per_frame, target_masks):
@@ -110,6 +164,8 @@ class SAM2LightningModule(nn.Module):
 
     def log(self, name, value, **kw):
         self.logged[name] = value.detach() if torch.is_tensor(value) else value
+        if HAVE_LIGHTNING and getattr(self, "_trainer", None) is not None:  # pragma: no cover
+            super().log(name, value, batch_size=1, **kw)
 
     def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
         """trainer.py:256-289"""
@@ -125,17 +181,36 @@ class SAM2LightningModule(nn.Module):
             self.log(f"train/{k}", v)
         if self.optimizer is not None:
             self.log("train/learning_rate", self.optimizer.param_groups[0]["lr"])
+        if HAVE_LIGHTNING and getattr(self, "_trainer", None) is not None:  # pragma: no cover
+            self._lightning_manual_step(total)
         return total
+
+    def _lightning_manual_step(self, total):  # pragma: no cover - Lightning is not installed here
+        """Under a real Lightning Trainer (manual optimization): backward into the gradient arena,
+        then clip + AdamW at accumulation boundaries with the trainer's settings."""
+        tr = self.trainer
+        if self._runner is None:
+            self.gradient_clip_val = tr.gradient_clip_val
+            self._runner = StepRunner(self, total_steps=max(1, int(tr.estimated_stepping_batches)),
+                                      accumulate_grad_batches=tr.accumulate_grad_batches, graph=False,
+                                      gradient_clip_val=tr.gradient_clip_val)
+        self.manual_backward(total)
+        self._runner.after_backward()
 
     @torch.no_grad()
     def validation_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
-        """trainer.py:291-322 (loss, no gradient tape) plus the reference's offline evaluation
-        metrics computed in the loop on every frame (eval/eval.py: IoU / Dice / MAE of the
-        category-merged binarised masks, averaged as get_video_scores does): val/iou,
-        val/dice, val/mae."""
-        outs_per_frame, _ = self.forward(batch)
-        outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
-        losses = self.criterion(outs, targets)
+        """trainer.py:291-322 (loss, no gradient tape) in eval mode (dropout off, as Lightning's
+        model.eval() before validation) plus the reference's offline evaluation metrics computed in
+        the loop on every frame (eval/eval.py: IoU / Dice / MAE of the category-merged binarised
+        masks, averaged as get_video_scores does): val/iou, val/dice, val/mae."""
+        was = self.model.training
+        self.model.eval()
+        try:
+            outs_per_frame, _ = self.forward(batch)
+            outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
+            losses = self.criterion(outs, targets)
+        finally:
+            self.model.train(was)
         self.log("val/total_loss", losses[CORE_LOSS_KEY])
         for k, v in losses.items():
             if k not in (CORE_LOSS_KEY, "logits"):
@@ -148,24 +223,34 @@ class SAM2LightningModule(nn.Module):
 
 
 class StepRunner:
-    """One optimizer step of the fit loop: zero grads -> training_step -> backward ->
-    (RCCL all-reduce) -> clip + AdamW (+ schedule).  Everything stays on the device.
+    """One micro-step of the fit loop: (zero the arena when a window starts) -> training_step ->
+    backward into the gradient arena, and at every `accumulate_grad_batches`-th micro-step: RCCL
+    all-reduce (N > 1) -> clip + AdamW (+ schedule).  Everything stays on the device.
 
-    graph=True captures zero-grad + forward + loss + backward of the step ONCE per input
-    signature (frame count, image size, category/object layout) into a HIP graph and replays
-    it: the ~6k kernel launches of a B+ 512^2 8-frame step cost one graph launch instead of
-    ~6k Python/ctypes launches (the step was host-bound).  Per step, only the host prompt stage
-    (connected components + clicks, sam2model.py:181-236), the copies of the new clip into the
-    graph's static input buffers, the dropout RNG offset and the all-reduce + optimizer run
-    eagerly.  Dropout masks still change every step: kernels fold the device-resident RNG
-    offset into their seeds (s2h_rng_bind)."""
+    Gradient accumulation follows Lightning: micro-step gradients are summed, the loss scale
+    1/accumulate (and the 1/world average of DDP) is folded into the optimizer's grad_scale, the
+    clip sees the scaled gradient, the schedule counts optimizer steps, and non-boundary
+    micro-steps issue no all-reduce (DDP no_sync).
+
+    graph=True captures forward + loss + backward of a micro-step ONCE per input signature
+    (frame count, image size, category/object layout) into a HIP graph and replays it: the ~5k
+    kernel launches of a B+ 512^2 8-frame step cost one graph launch instead of ~5k Python/ctypes
+    launches.  Per step only the host prompt stage (connected components + clicks,
+    sam2model.py:181-236), the copies of the new clip into the graph's static input buffers, the
+    dropout RNG offset and the boundary work (all-reduce, optimizer, zeroing) run eagerly.
+    Dropout masks still change every step: kernels fold the device-resident RNG offset into
+    their seeds (s2h_rng_bind)."""
 
     def __init__(self, module: SAM2LightningModule, total_steps: int = 1, distributed: bool = False,
-                 graph: bool = False):
+                 graph: bool = False, accumulate_grad_batches: int = 1, gradient_clip_val=None):
         self.module = module
+        if gradient_clip_val is not None:
+            module.gradient_clip_val = gradient_clip_val
         module.configure_optimizers(total_steps)
         self.reducer = ArenaGradReducer(module.model.arena.grad_region()) if distributed else None
-        self.global_step = 0
+        self.accumulate = max(1, int(accumulate_grad_batches or 1))
+        self.global_step = 0  # optimizer steps
+        self.micro_step = 0
         self.graph = graph
         self._graphs: Dict[Any, Dict[str, Any]] = {}
         self.before_capture = None  # optional callable, run right before a graph is captured
@@ -177,12 +262,11 @@ class StepRunner:
         # variation of the dropout masks comes from the device RNG offset alone, so an eager step
         # and a replay of the captured one use identical masks
         self.seed_base = FN._SEED[0]
+        module.model.arena.zero_grad()
 
     def _device_step(self, batch):
-        m = self.module
         self._fn.set_seed(self.seed_base)
-        m.model.arena.zero_grad()
-        loss = m.training_step(batch, self.global_step)
+        loss = self.module.training_step(batch, self.micro_step)
         loss.backward()
         return loss
 
@@ -198,12 +282,19 @@ class StepRunner:
             plan = dict(plan)
             plan["dev"] = model.upload_prompt_plan(plan, dev)
             static.prompt_plan = plan
+            # the eager warm-up accumulates into the gradient arena: keep what earlier micro-steps
+            # of this accumulation window left there
+            saved = model.arena.grad_region().clone() if self.micro_step % self.accumulate else None
             cur = torch.cuda.current_stream(dev)
             side = torch.cuda.Stream(dev)
             side.wait_stream(cur)
             with torch.cuda.stream(side):  # eager warm-up: fills every device-side table cache
                 self._device_step(static)
             cur.wait_stream(side)
+            if saved is not None:
+                model.arena.grad_region().copy_(saved)
+            else:
+                model.arena.zero_grad()
             if self.before_capture is not None:
                 self.before_capture()
             g = torch.cuda.CUDAGraph()
@@ -223,19 +314,30 @@ class StepRunner:
         self.module.last_outputs = ent["outputs"]
         return ent["loss"]
 
-    def __call__(self, batch):
+    def after_backward(self) -> bool:
+        """Counts the micro-step; at an accumulation boundary runs all-reduce + clip + AdamW (the
+        arena is zeroed when the next window starts).  Returns True when an optimizer step was
+        taken."""
         m = self.module
-        self.rng.fill_(self.global_step + 1)
-        loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
-        scale = 1.0
+        self.micro_step += 1
+        if self.micro_step % self.accumulate:
+            return False
+        scale = 1.0 / self.accumulate
         if self.reducer is not None:
             self.reducer.reduce()
-            scale = self.reducer.grad_scale
+            scale *= self.reducer.grad_scale
         lr = m.lr_at(self.global_step) if m.lr_at is not None else None
         m.optimizer.step(lr=lr, grad_scale=scale)
-        if m.optimizer is not None:
-            m.log("train/learning_rate", m.optimizer.param_groups[0]["lr"])
+        m.log("train/learning_rate", m.optimizer.param_groups[0]["lr"])
         self.global_step += 1
+        return True
+
+    def __call__(self, batch):
+        if self.micro_step % self.accumulate == 0:  # new accumulation window (zero_grad)
+            self.module.model.arena.zero_grad()
+        self.rng.fill_(self.micro_step + 1)
+        loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
+        self.after_backward()
         return loss
 
 
@@ -250,11 +352,174 @@ def _static_batch(batch, device):
     return out
 
 
+# ------------------------------------------------------------------ data module
+class SAM2LightningDataModule(_DataBase):
+    """trainer.py:325-400: B == 1 clip DataLoaders collated by sam2_collate_fn.  The data section
+    (configs/data/*.yaml: train_path, val_path, image_size, video_clip_length, stride,
+    num_workers, batch_size, num_categories) is read as the reference reads it; when the COCO
+    annotation files are not present the loaders yield deterministic synthetic clips of the same
+    shape (data/synthetic.py), `synthetic_clips` per split."""
+
+    def __init__(self, data: Any, train_shuffle: bool = True):
+        if _DataBase is not object:  # pragma: no cover
+            super().__init__()
+        self.data = _ns(_todict(data))
+        self.train_shuffle = train_shuffle
+        self.hparams = SimpleNamespace(data=self.data, train_shuffle=train_shuffle)
+        self.train_dataset = None
+        self.val_dataset = None
+
+    def _dataset(self, split):
+        d = self.data
+        path = _get(d, f"{split}_path")
+        if path and os.path.exists(str(path)):
+            from ..data.dataset import COCODataset
+            return COCODataset(config=d, coco_json_path=path)
+        from ..data.synthetic import SyntheticClipDataset
+        n_cat = int(_get(d, "num_categories", 13))
+        return SyntheticClipDataset(num_clips=int(_get(d, "synthetic_clips", 16 if split == "train" else 4)),
+                                    num_frames=int(_get(d, "video_clip_length", 8)),
+                                    image_size=int(_get(d, "image_size", 512)), n_cat=n_cat,
+                                    n_obj=int(_get(d, "synthetic_objects", n_cat)),
+                                    offset=0 if split == "train" else 100_000)
+
+    def setup(self, stage: str = "fit"):
+        if stage == "fit":
+            self.train_dataset = self._dataset("train")
+            self.val_dataset = self._dataset("val")
+
+    def _loader(self, ds, shuffle):
+        from torch.utils.data import DataLoader
+
+        from ..data.synthetic import sam2_collate_fn
+        if ds is None:
+            raise RuntimeError("dataset not initialized: call setup('fit') first")
+        return DataLoader(ds, batch_size=int(_get(self.data, "batch_size", 1)),
+                          num_workers=int(_get(self.data, "num_workers", 0)), shuffle=shuffle,
+                          pin_memory=torch.cuda.is_available(), collate_fn=sam2_collate_fn)
+
+    def train_dataloader(self):
+        return self._loader(self.train_dataset, self.train_shuffle)
+
+    def val_dataloader(self):
+        return self._loader(self.val_dataset, False)
+
+
+# ---------------------------------------------------------------------- trainer
+class Trainer:
+    """The `lightning.pytorch.Trainer` surface the reference configs use (best.yaml:98-113), driving
+    SAM2LightningModule through StepRunner.  Unknown Lightning arguments (logger, callbacks,
+    enable_progress_bar, ...) are accepted and ignored."""
+
+    def __init__(self, accelerator="auto", devices=1, precision=None, max_epochs=None, max_steps=-1,
+                 gradient_clip_val=None, accumulate_grad_batches=1, val_check_interval=1.0,
+                 num_sanity_val_steps=0, limit_train_batches=None, limit_val_batches=None,
+                 log_every_n_steps=50, strategy="auto", graph=True, default_root_dir=None, **unused):
+        self.precision = precision
+        self.devices = devices
+        self.strategy = strategy
+        self.max_epochs = max_epochs if max_epochs is not None else (1 if max_steps and max_steps > 0 else 1000)
+        self.max_steps = int(max_steps if max_steps is not None else -1)
+        self.gradient_clip_val = gradient_clip_val
+        self.accumulate_grad_batches = max(1, int(accumulate_grad_batches or 1))
+        self.val_check_interval = val_check_interval
+        self.num_sanity_val_steps = int(num_sanity_val_steps or 0)
+        self.limit_train_batches = limit_train_batches
+        self.limit_val_batches = limit_val_batches
+        self.log_every_n_steps = max(1, int(log_every_n_steps or 1))
+        self.graph = graph
+        self.default_root_dir = default_root_dir
+        self.history: List[Dict[str, float]] = []
+        self.val_history: List[Dict[str, float]] = []
+        self.global_step = 0
+        self.current_epoch = 0
+
+    @staticmethod
+    def _limit(n, lim):
+        if lim is None:
+            return n
+        if isinstance(lim, float) and lim <= 1.0:
+            return int(n * lim)
+        return min(n, int(lim))
+
+    def _validate(self, module, loader, device, n):
+        vals = []
+        for i, batch in enumerate(loader):
+            if i >= n:
+                break
+            module.validation_step(batch.to(device, non_blocking=True), i)
+            vals.append({k: float(v) for k, v in module.logged.items() if k.startswith("val/")})
+        if vals:
+            row = {k: sum(v[k] for v in vals) / len(vals) for k in vals[0]}
+            row["step"] = self.global_step
+            self.val_history.append(row)
+
+    def fit(self, module: SAM2LightningModule, datamodule=None, train_dataloaders=None, val_dataloaders=None):
+        from .ddp import init_from_env
+        rank, world, local = init_from_env("nccl")
+        device = torch.device("cuda", local)
+        if world == 1:
+            torch.cuda.set_device(device)
+        if module.compute_dtype is None and self.precision is not None:
+            module.compute_dtype = precision_dtype(self.precision)
+        if datamodule is not None:
+            datamodule.setup("fit")
+            train_dataloaders = datamodule.train_dataloader()
+            val_dataloaders = datamodule.val_dataloader()
+        module.trainer_ = self
+        module.setup("fit", device)
+        n_train = self._limit(len(train_dataloaders), self.limit_train_batches)
+        n_val = self._limit(len(val_dataloaders), self.limit_val_batches) if val_dataloaders is not None else 0
+        per_epoch = max(1, n_train // self.accumulate_grad_batches)
+        total = self.max_steps if self.max_steps > 0 else per_epoch * self.max_epochs
+        run = StepRunner(module, total, distributed=world > 1, graph=self.graph,
+                         accumulate_grad_batches=self.accumulate_grad_batches,
+                         gradient_clip_val=self.gradient_clip_val)
+        self.runner = run
+        if n_val and self.num_sanity_val_steps:
+            self._validate(module, val_dataloaders, device, min(n_val, self.num_sanity_val_steps))
+            self.val_history.clear()
+        vci = self.val_check_interval
+        val_every = (max(1, int(n_train * vci)) if isinstance(vci, float) and vci <= 1.0 else int(vci)) if n_val else 0
+        t0 = time.time()
+        done = False
+        for epoch in range(self.max_epochs):
+            self.current_epoch = epoch
+            for i, batch in enumerate(train_dataloaders):
+                if i >= n_train:
+                    break
+                before = run.global_step
+                run(batch.to(device, non_blocking=True))
+                self.global_step = run.global_step
+                if run.global_step != before and run.global_step % self.log_every_n_steps == 0:
+                    row = {k: float(v) for k, v in module.logged.items() if k.startswith("train/")}
+                    row["step"], row["epoch"], row["time_s"] = run.global_step, epoch, time.time() - t0
+                    self.history.append(row)
+                if val_every and (i + 1) % val_every == 0:
+                    self._validate(module, val_dataloaders, device, n_val)
+                if self.max_steps > 0 and run.global_step >= self.max_steps:
+                    done = True
+                    break
+            if done:
+                break
+        return self.history
+
+    def save_checkpoint(self, path, module: SAM2LightningModule):
+        """Lightning-layout checkpoint: state_dict with the `model.` prefix (the reference strips it
+        when it reloads, train.py:146-157) + optimizer state + counters."""
+        sd = {"model." + k: v.detach().cpu() for k, v in module.model.state_dict().items()}
+        torch.save({"state_dict": sd, "optimizer_states": [module.optimizer.state_dict()],
+                    "global_step": self.global_step, "epoch": self.current_epoch}, path)
+
+
 def fit(module: SAM2LightningModule, batches, max_steps: int, device="cuda", log_every: int = 1, distributed=False,
-        graph: bool = True):
-    """Minimal fit loop (max_steps optimizer steps over an iterable of BatchedVideoDatapoint)."""
+        graph: bool = True, accumulate_grad_batches: int = 1, gradient_clip_val: Optional[float] = 1.0):
+    """Minimal fit loop: `max_steps` micro-steps over an iterable of BatchedVideoDatapoint
+    (gradient_clip_val 1.0 = best.yaml's trainer section)."""
     module.setup("fit", device)
-    run = StepRunner(module, max_steps, distributed, graph=graph)
+    run = StepRunner(module, max(1, math.ceil(max_steps / max(1, accumulate_grad_batches))), distributed,
+                     graph=graph, accumulate_grad_batches=accumulate_grad_batches,
+                     gradient_clip_val=gradient_clip_val)
     hist: List[Dict[str, float]] = []
     t0 = time.time()
     for i, batch in enumerate(batches):

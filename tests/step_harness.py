@@ -13,7 +13,12 @@ CASES = {
     "tiny256_point_mem": ("tiny", "point", ["memory_attention", "memory_encoder"]),
     "tiny256_box_all": ("tiny", "box", ALL),
     "bplus128_point_all": ("base_plus", "point", ALL),
+    "bplus128_point_all_t8": ("base_plus", "point", ALL),
+    "tiny256_point_all_multi": ("tiny", "point", ALL),
+    "bplus256_point_all": ("base_plus", "point", ALL),
 }
+# reference steps under CPU bf16 autocast (oracle/gen_golden.py), with their fp32 twin
+BF16_CASES = {"bplus256_point_all_bf16": "bplus256_point_all"}
 
 
 def load_golden(name):
@@ -53,7 +58,8 @@ def golden_batch(g):
     T, S = int(g["meta/T"]), int(g["meta/image_size"])
     n_cat = g["in/masks_count"].shape[1]
     n_obj = int((g["in/masks_count"][0] > 0).sum())
-    return synthetic_batch(int(g["meta/clip_idx"]), T, S, n_cat, n_obj)
+    parts = g["meta/parts"].tolist() if "meta/parts" in g else None
+    return synthetic_batch(int(g["meta/clip_idx"]), T, S, n_cat, n_obj, parts)
 
 
 def grads_by_name(model):

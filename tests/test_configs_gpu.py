@@ -1,0 +1,123 @@
+"""The BASELINE.json configurations the bench and the scaling runs use, run on the GPU at their
+full size (the oracle cannot finish them in seconds, so these check size-independent
+properties):
+
+* config 2 (B+, 512^2, 8 frames, 13 objects, bf16 -- the bench workload): finite losses, the
+  captured HIP graph replayed 12 times (the regime where captured memset nodes once broke the
+  stream order) reproduces the eager step clip by clip, and the bf16 mode stays
+  close to the fp32 mode of the same build on the same clip;
+* config 3 (B+, 384^2, 10 frames, 7 objects): the 10-frame bank and the graph path;
+* gradient accumulation (accumulate_grad_batches) equals the summed micro-step gradients;
+* validation_step is deterministic (eval mode: dropout off).
+"""
+import math
+
+import pytest
+import torch
+
+from step_harness import ALL, mask_iou
+
+pytestmark = pytest.mark.gpu
+
+LOSS = {"type": "multi_step", "gt_stride": 1, "multistep_logit_temperature": 1.0,
+        "weight_dict": {"loss_mask": 20, "loss_dice": 1, "loss_iou": 1, "loss_class": 0},
+        "supervise_all_iou": True, "iou_use_l1_loss": True, "pred_obj_scores": False}
+
+
+def _module(size, S, dtype="bf16", dropout=None, lr=0.0, clip=1.0):
+    from sam2_video.kernels import functional as FN
+    from sam2_video.model.sam2model import SAM2Model
+    from sam2_video.training.trainer import SAM2LightningModule
+    FN.set_seed(4242)
+    model = SAM2Model(None, f"{size}@{S}", trainable_modules=ALL, compute_dtype=dtype)
+    if dropout is not None:
+        model.set_dropout(dropout)
+    opt = {"type": "AdamW", "lr": lr, "weight_decay": 0.01, "betas": [0.9, 0.999], "warmup_factor": 0.0}
+    module = SAM2LightningModule(model, LOSS, opt, {"enabled": False})
+    module.gradient_clip_val = clip
+    module.setup("fit", "cuda")
+    return module
+
+
+def _clips(idxs, T, S, n_cat, n_obj):
+    from sam2_video.data.synthetic import make_clip, sam2_collate_fn
+    return [sam2_collate_fn([make_clip(i, T, S, n_cat, n_obj)]).to("cuda") for i in idxs]
+
+
+def _losses(module, clips, graph):
+    from sam2_video.training.trainer import StepRunner
+    run = StepRunner(module, total_steps=len(clips), graph=graph)
+    out = [float(run(c).detach()) for c in clips]
+    torch.cuda.synchronize()
+    return out, run
+
+
+@pytest.mark.parametrize("cfg", [("base_plus", 512, 8, 13), ("base_plus", 384, 10, 7)], ids=["config2", "config3"])
+def test_config_graph_replays_match_eager(cfg):
+    """lr = 0 (fixed weights), dropout 0.1 as trained: 12 replays (config 2) / 4 (config 3) of the
+    captured step on different clips give the eager step's loss on each clip"""
+    size, S, T, O = cfg
+    n = 12 if S == 512 else 4
+    clips = _clips(range(50, 50 + n), T, S, O, O)
+    eager, _ = _losses(_module(size, S), clips, graph=False)
+    graphed, run = _losses(_module(size, S), clips, graph=True)
+    assert len(run._graphs) == 1
+    assert all(math.isfinite(x) for x in eager + graphed), (eager, graphed)
+    for a, b in zip(eager, graphed):
+        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (eager, graphed)
+
+
+def test_config2_bf16_close_to_fp32():
+    """bf16 vs fp32 mode of this build on one config-2 clip (dropout off): binarised masks agree
+    (IoU >= 0.97 per frame) and the loss within 2 % -- the size-independent counterpart of the
+    golden bf16 test at 256^2"""
+    from step_harness import run_step
+    clip = _clips([77], 8, 512, 13, 13)[0]
+    res = {}
+    for dt in ("fp32", "bf16"):
+        m = _module("base_plus", 512, dtype=dt, dropout=0.0)
+        stages, merged, losses, _ = run_step(m.model, clip)
+        res[dt] = ([s["pred_masks"].detach().float().cpu() for s in stages], float(losses["total_loss"]))
+        del m, stages, merged
+        torch.cuda.empty_cache()
+    ious = [mask_iou(a, b) for a, b in zip(res["fp32"][0], res["bf16"][0])]
+    errs = [(a - b).abs().max().item() for a, b in zip(res["fp32"][0], res["bf16"][0])]
+    print("per-frame IoU bf16 vs fp32", ious, "max |dlogit|", errs, "losses", res["fp32"][1], res["bf16"][1])
+    assert min(ious) >= 0.97, ious
+    assert abs(res["fp32"][1] - res["bf16"][1]) <= 0.02 * abs(res["fp32"][1])
+
+
+def test_gradient_accumulation_sums_micro_steps():
+    """accumulate_grad_batches = 2: the arena after two micro-steps equals the sum of the two
+    single-step gradients (fp32, dropout off), no optimizer step in between"""
+    from sam2_video.training.trainer import StepRunner
+    clips = _clips([5, 6], 3, 128, 4, 3)
+    single = []
+    for c in clips:
+        m = _module("tiny", 128, dtype="fp32", dropout=0.0)
+        run = StepRunner(m, total_steps=1, graph=False, accumulate_grad_batches=1)
+        m.optimizer.lr = 0.0
+        run(c)
+        single.append(m.model.arena.grad_region().detach().clone())
+    for graph in (False, True):
+        m = _module("tiny", 128, dtype="fp32", dropout=0.0)
+        run = StepRunner(m, total_steps=1, graph=graph, accumulate_grad_batches=2)
+        run(clips[0])
+        assert run.global_step == 0
+        run(clips[1])
+        assert run.global_step == 1
+        acc = m.model.arena.grad_region()
+        ref = single[0] + single[1]
+        assert (acc - ref).abs().max().item() <= 1e-5 * ref.abs().max().item(), graph
+
+
+def test_validation_step_is_deterministic():
+    """validation runs in eval mode (dropout off) and restores train mode"""
+    m = _module("tiny", 128, dtype="bf16")
+    clip = _clips([9], 3, 128, 4, 3)[0]
+    vals = []
+    for _ in range(2):
+        m.validation_step(clip)
+        vals.append({k: float(v) for k, v in m.logged.items() if k.startswith("val/")})
+    assert m.model.training
+    assert vals[0] == vals[1], vals

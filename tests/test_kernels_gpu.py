@@ -595,3 +595,105 @@ def test_act_dropout_bwd_fused(dtype, act):
     g = ops.dropout(dy, 0.1, 4321)
     ref = ops.act_bwd(pre, g, act) if act else g
     _close(got, ref, 1e-2 if dtype == torch.bfloat16 else 1e-6)
+
+
+@pytest.mark.parametrize("max_norm,grad_scale", [(1.0, 1.0), (1.0, 0.5), (0.1, 0.25), (0.0, 0.5)])
+def test_clip_adamw_matches_torch(max_norm, grad_scale):
+    """s2h_grad_norm + s2h_adamw (ArenaAdamW) == clip_grad_norm_ + torch.optim.AdamW on the
+    scaled gradient: grad_scale models the 1/world average after the SUM all-reduce (world 2 ->
+    0.5) and 1/accumulate_grad_batches; max_norm 0 = no clip (Lightning's gradient_clip_val 0)"""
+    ops = _ops()
+    torch.manual_seed(11)
+    n = 300_001
+    p = torch.randn(n, device=DEV)
+    pt = p.clone().requires_grad_(True)
+    opt = torch.optim.AdamW([pt], lr=1e-3, weight_decay=0.01, betas=(0.9, 0.999))
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    ws, out = torch.empty(1024, device=DEV), torch.zeros(2, device=DEV)
+    for step in range(1, 4):
+        g = torch.randn(n, device=DEV) * (3.0 if step == 2 else 0.01)  # step 2 clips, the others do not
+        pt.grad = g * grad_scale
+        if max_norm > 0:
+            torch.nn.utils.clip_grad_norm_([pt], max_norm)
+        opt.step()
+        ops.grad_norm(g, max_norm, ws, out, grad_scale)
+        ops.adamw(p, g, m, v, out, 1e-3, 0.9, 0.999, 1e-8, 0.01, step)
+        _close(out[0:1], (g * grad_scale).norm().view(1), 1e-5)
+    _close(p, pt.detach(), 1e-5)
+
+
+def test_category_merge_multi_object_matches_reference_formulas():
+    """merge_masks / merge_scores over categories of 1, 2 and 3 objects (a tie and a NaN included)
+    vs the reference's _grouped_max / _grouped_weighted_avg (masks.py:92-143) under autograd:
+    forward values and the gradients into the object logits and scores"""
+    from sam2_video.utils.masks import merge_object_results_to_category
+    torch.manual_seed(5)
+    obj_to_cat = [0, 1, 1, 2, 2, 2]
+    O, H = len(obj_to_cat), 24
+    logits = torch.randn(O, 1, H, H, device=DEV) * 3
+    logits[2, 0, 0, 0] = logits[1, 0, 0, 0]  # exact tie: the first object takes the gradient
+    ious = torch.rand(O, 1, device=DEV)
+    stage = {"pred_masks": logits, "pred_masks_high_res": logits, "multistep_pred_masks": logits,
+             "multistep_pred_masks_high_res": logits, "multistep_pred_multimasks": [logits],
+             "multistep_pred_multimasks_high_res": [logits], "multistep_pred_ious": [ious],
+             "multistep_object_score_logits": [ious], "point_inputs": None, "mask_inputs": None}
+    x = logits.clone().requires_grad_(True)
+    s = ious.clone().requires_grad_(True)
+    st = dict(stage, pred_masks_high_res=x, multistep_pred_multimasks_high_res=[x], multistep_pred_ious=[s])
+    out = merge_object_results_to_category([st], obj_to_cat, 3)[0]
+    hr, mi = out["multistep_pred_multimasks_high_res"][0], out["multistep_pred_ious"][0]
+    # reference formulas on the same inputs
+    xr = logits.clone().requires_grad_(True)
+    sr = ious.clone().requires_grad_(True)
+    groups = [[0], [1, 2], [3, 4, 5]]
+    w = torch.sigmoid(xr).sum(dim=(1, 2, 3))
+    hr_ref = torch.stack([xr[g].max(dim=0).values for g in groups])
+    mi_ref = torch.stack([(sr[g] * w[g].view(-1, 1)).sum(0) / w[g].sum() for g in groups])
+    _close(hr, hr_ref, 1e-6)
+    _close(mi, mi_ref, 1e-5)
+    gh = torch.randn_like(hr_ref)
+    gi = torch.randn_like(mi_ref)
+    ((hr * gh).sum() + (mi * gi).sum()).backward()
+    ((hr_ref * gh).sum() + (mi_ref * gi).sum()).backward()
+    _close(x.grad, xr.grad, 1e-4)
+    _close(s.grad, sr.grad, 1e-5)
+    # a NaN logit propagates through the max like torch.max (the kernel once dropped it)
+    from sam2_video.kernels.functional_sam import merge_masks
+    from sam2_video.utils.masks import CategoryGroups
+    xn = logits.clone()
+    xn[4, 0, 1, 1] = float("nan")
+    got = merge_masks(xn, CategoryGroups(obj_to_cat, 3, xn.device))
+    ref = torch.stack([xn[g].max(dim=0).values for g in groups])
+    assert torch.equal(torch.isnan(got), torch.isnan(ref)) and bool(torch.isnan(got[2, 0, 1, 1]))
+
+
+@pytest.mark.parametrize("reduction,pw,temp", [("mean", None, 1.0), ("mean", [0.5, 2.0, 1.0, 3.0], 0.7),
+                                               ("sum", None, 1.5)])
+def test_bce_category_loss_matches_reference_formula(reduction, pw, temp):
+    """BCECategoryLoss (losses.py:251-372) vs its torch formula: valid-category filter, logit
+    temperature, pos_weight, mean/sum reduction, average over frames; loss and d(logits)"""
+    import torch.nn.functional as F
+
+    from sam2_video.model.losses import BCECategoryLoss
+    torch.manual_seed(8)
+    T, C, H = 3, 4, 40
+    logits = torch.randn(T, C, 1, H, H, device=DEV) * 2
+    tgt = torch.rand(T, C, H, H, device=DEV) > 0.6
+    tgt[1, 2] = False  # a category without ground truth in frame 1
+    x = logits.clone().requires_grad_(True)
+    outs = [{"pred_masks_high_res": x[t]} for t in range(T)]
+    crit = BCECategoryLoss(pos_weight=pw, reduction=reduction, logit_temperature=temp)
+    got = crit(outs, tgt)
+    xr = logits.clone().requires_grad_(True)
+    tot = 0.0
+    for t in range(T):
+        valid = tgt[t].sum(dim=(1, 2)).bool()
+        lw = None if pw is None else torch.tensor(pw, device=DEV).view(-1, 1, 1)[valid]
+        tot = tot + F.binary_cross_entropy_with_logits(xr[t].squeeze(1)[valid] / temp, tgt[t][valid].float(),
+                                                       pos_weight=lw, reduction=reduction)
+    tot = tot / T
+    _close(got["total_loss"].view(1), tot.view(1), 1e-5)
+    assert torch.equal(got["loss_bce"], got["total_loss"])
+    got["total_loss"].backward()
+    tot.backward()
+    _close(x.grad, xr.grad, 1e-5)
