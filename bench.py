@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--trainable", default="all", choices=["all", "mem"])
     ap.add_argument("--dropout", type=float, default=None, help="override dropout p (default: config, 0.1)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
-    ap.add_argument("--cpu-frames", type=int, default=4, help="frames of the CPU baseline sample clip")
+    ap.add_argument("--cpu-frames", type=int, default=None,
+                    help="frames of the CPU baseline sample clip (default: the workload's own frame count)")
     ap.add_argument("--no-prof", action="store_true")
     ap.add_argument("--print-losses", action="store_true", help="diagnostic: print every step's loss (host syncs)")
     ap.add_argument("--no-graph", action="store_true",
@@ -130,25 +131,49 @@ def cpu_baseline(args):
     from sam2_video.model.configs import model_config
     from sam2_video.utils.init import synth_tensor
 
-    threads = min(16, os.cpu_count() or 1)
+    # the host's CPU share: OMP_NUM_THREADS (16 per GPU on the GPU box) when set, else every core
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
     torch.set_num_threads(threads)
+    frames = args.cpu_frames or args.frames
     cfg = model_config(args.size, args.image_size)
     trainable = ALL if args.trainable == "all" else ["memory_attention", "memory_encoder"]
     P = O.make_params(O.param_shapes(cfg), O.trainable_prefixes(trainable), synth_tensor, seed=0)
-    clip = make_clip(10_000, args.cpu_frames, args.image_size, args.objects, args.objects)
+    clip = make_clip(10_000, frames, args.image_size, args.objects, args.objects)
     model = O.OracleSAM2(cfg, P, dropout=0.0)
     t0 = time.time()
     stages, merged, aux = model.forward(clip["images"], clip["masks"])
     losses = O.multistep_loss(merged, clip["masks"])
     losses["total_loss"].backward()
     dt = time.time() - t0
-    return {"value": round(args.cpu_frames / dt, 4), "unit": "clip-frames/s", "cores": threads, "kind": "port",
-            "sample": f"1 clip x {args.cpu_frames} frames, {args.size} {args.image_size}^2, {args.objects} objects, "
-                      f"fp32 fwd+loss+bwd (oracle), {dt:.1f} s"}
+    return {"value": round(frames / dt, 4), "unit": "clip-frames/s", "cores": threads, "kind": "port",
+            "sample": f"1 clip x {frames} frames (the timed workload's clip), {args.size} {args.image_size}^2, "
+                      f"{args.objects} objects, fp32 fwd+loss+bwd (oracle, no optimizer step), {dt:.1f} s, "
+                      f"{threads} threads"}
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside torchrun: start N rank processes (one per GPU, RCCL over
+    127.0.0.1) before this parent touches the GPU, wait for all, exit with the worst status.
+    Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    codes = [p.wait() for p in procs]
+    return max(codes, key=abs)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
     from sam2_video.data.synthetic import make_clip, sam2_collate_fn
     from sam2_video.kernels import _lib
     from sam2_video.kernels import functional as FN
@@ -212,7 +237,8 @@ def main():
 
     loss_val = float(module.logged["train/total_loss"])  # last timed step
     if not math.isfinite(loss_val):
-        print(f"WARNING: non-finite training loss {loss_val} in the timed steps", file=sys.stderr)
+        print(f"ERROR: non-finite training loss {loss_val} in the timed steps", file=sys.stderr)
+        sys.exit(3)
     roof = None
     if not args.no_prof:
         if graph:

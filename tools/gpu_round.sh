@@ -1,8 +1,13 @@
-# one GPU call: gpu tests, then the bench with the kernel table (run via gpurun from the repo root)
+# one GPU call: gpu tests (all, report failures), smoke, then the bench with the kernel table
+# (run via gpurun from the repo root)
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/gpu_tests.log; exit 1; }
-tail -3 gpurun_out/gpu_tests.log
-timeout -k 10 300 python -u bench.py --kernel-table > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -30 gpurun_out/bench.err; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -q -rf --timeout 150 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+rc=$?
+tail -25 gpurun_out/gpu_tests.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "TESTS_ABORTED rc=$rc"; exit $rc; fi
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo SMOKE_FAILED; tail -20 gpurun_out/smoke.log; exit 1; }
+timeout -k 10 400 python -u bench.py --kernel-table > gpurun_out/bench.log 2> gpurun_out/bench.err || { echo BENCH_FAILED; tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.log
+exit $rc
