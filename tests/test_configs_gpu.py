@@ -120,4 +120,7 @@ def test_validation_step_is_deterministic():
         m.validation_step(clip)
         vals.append({k: float(v) for k, v in m.logged.items() if k.startswith("val/")})
     assert m.model.training
-    assert vals[0] == vals[1], vals
+    # equal up to the fp32 atomics of the loss reductions (summation order); dropout would
+    # move them by far more
+    for k in vals[0]:
+        assert abs(vals[0][k] - vals[1][k]) <= 1e-5 * max(1.0, abs(vals[0][k])), (k, vals)
