@@ -49,6 +49,9 @@ CASES = {
                                     prompt="point", trainable=ALL),
     # memory-attention Lq = 256 (flash-attention size) in fp32 and under CPU bf16 autocast: the
     # reference's own bf16 drift at the size where the bf16 kernels of the bench path run
+    # mask prompts (sam2model.py:215-217): frame 0 bypasses the SAM heads (_use_mask_as_output)
+    "tiny256_mask_all": dict(size="tiny", image_size=256, T=4, n_cat=5, n_obj=3, parts=(2,), prompt="mask",
+                             trainable=ALL),
     "bplus256_point_all": dict(size="base_plus", image_size=256, T=4, n_cat=4, n_obj=3, prompt="point",
                                trainable=ALL),
     "bplus256_point_all_bf16": dict(size="base_plus", image_size=256, T=4, n_cat=4, n_obj=3, prompt="point",

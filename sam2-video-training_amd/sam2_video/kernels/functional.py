@@ -30,6 +30,11 @@ def set_seed(s):
     _SEED[0] = int(s) & (2**64 - 1)
 
 
+def _compute_weight(mod):
+    """a Linear / Conv2d module's weight in the compute dtype as a [out, in*k*k] matrix"""
+    return mod.weight._s2h_compute.reshape(mod.weight.shape[0], -1)
+
+
 def _grad_of(p):
     return getattr(p, "_s2h_grad", None) if p is not None and p.requires_grad else None
 

@@ -39,7 +39,51 @@ def _bicubic_matrix_np(n_in: int, n_out: int):
     return M
 
 
+@lru_cache(maxsize=None)
+def _aa_bilinear_matrix_np(n_in: int, n_out: int):
+    """PyTorch's antialiased bilinear resize (F.interpolate(mode="bilinear", antialias=True,
+    align_corners=False), the _upsample_bilinear2d_aa weights) as a matrix [n_out, n_in]: a
+    triangle filter of half-width `scale` when downsampling, normalised per output pixel."""
+    scale = n_in / n_out
+    support = scale if scale >= 1.0 else 1.0
+    invscale = 1.0 / scale if scale >= 1.0 else 1.0
+    M = np.zeros((n_out, n_in), np.float64)
+    for i in range(n_out):
+        center = scale * (i + 0.5)
+        xmin = max(int(center - support + 0.5), 0)
+        xsize = min(int(center + support + 0.5), n_in) - xmin
+        ws = [max(0.0, 1.0 - abs((j + xmin - center + 0.5) * invscale)) for j in range(xsize)]
+        tot = sum(ws)
+        for j, wv in enumerate(ws):
+            M[i, xmin + j] = wv / tot if tot != 0 else wv
+    return M
+
+
 _DEV_CACHE = {}
+
+
+def aa_bilinear_matrix(n_in, n_out, device):
+    key = ("aa", n_in, n_out, str(device))
+    t = _DEV_CACHE.get(key)
+    if t is None:
+        t = torch.from_numpy(_aa_bilinear_matrix_np(n_in, n_out)).float().to(device)
+        _DEV_CACHE[key] = t
+    return t
+
+
+def aa_downsample(x, ho, wo):
+    """[N, hi, wi] f32 -> [N, ho, wo]: antialiased bilinear resize as two fp32 GEMMs with the
+    separable weight matrices (forward only: the mask-prompt output path, sam2_base.py:446-452)"""
+    N, hi, wi = x.shape
+    Ah, Aw = aa_bilinear_matrix(hi, ho, x.device), aa_bilinear_matrix(wi, wo, x.device)
+    Y1 = torch.empty(N * hi, wo, device=x.device)
+    # Y1 = X Aw^T  ([N*hi, wi] x [wi, wo])
+    ops.gemm(x.reshape(N * hi, wi), Aw, Y1, M=N * hi, N=wo, K=wi, lda_m=wi, lda_k=1, ldb_k=1, ldb_n=wi, ldc=wo)
+    out = torch.empty(N, ho, wo, device=x.device)
+    # out[n] = Ah Y1[n]  ([ho, hi] x [hi, wo])
+    ops.gemm(Ah, Y1, out, M=ho, N=wo, K=hi, lda_m=hi, lda_k=1, ldb_k=wo, ldb_n=1, ldc=wo, batch=N, sA=0,
+             sB=hi * wo, sC=ho * wo)
+    return out
 
 
 def bicubic_matrix(n_in, n_out, device):

@@ -80,7 +80,7 @@ class MaskDecoder(nn.Module):
         self.pred_obj_score_head = (MLP(transformer_dim, transformer_dim, 1, 3) if pred_obj_scores_mlp
                                     else Linear(transformer_dim, 1))
 
-    def forward(self, image_embeddings, h, w, image_pe_table, sparse, no_mask_embed, high_res_features):
+    def forward(self, image_embeddings, h, w, image_pe_table, sparse, no_mask_embed, high_res_features, dense=None):
         """image_embeddings [O, h*w, C]; sparse [O, Ns, C]; high_res_features (s0 [1|O, 4h, 4w, C/8],
         s1 [1|O, 2h, 2w, C/4]) -> (low-res mask logits [O, 4h*4w] compute dtype, iou [O, 1],
         mask token 0 [O, C], object score logits [O, 1] f32)"""
@@ -89,7 +89,10 @@ class MaskDecoder(nn.Module):
         dt = image_embeddings.dtype
         tokens = _DecoderTokens.apply(sparse, dt, self.obj_score_token.weight, self.iou_token.weight,
                                       self.mask_tokens.weight)
-        src = FN.add_bcast(image_embeddings, no_mask_embed.weight._s2h_compute.view(-1), bparam=no_mask_embed.weight)
+        if dense is None:  # no mask prompt: the no_mask_embed broadcast (prompt_encoder.py:196-200)
+            src = FN.add_bcast(image_embeddings, no_mask_embed.weight._s2h_compute.view(-1), bparam=no_mask_embed.weight)
+        else:  # mask-prompt dense embedding [O, h*w, C]
+            src = FN.add(image_embeddings, dense)
         hs, src = self.transformer(src, image_pe_table, tokens)
         iou_token_out = hs[:, 1].contiguous()
         mask_token0 = hs[:, 2].contiguous()

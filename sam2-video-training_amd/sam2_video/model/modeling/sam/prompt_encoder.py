@@ -12,6 +12,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ....kernels import ops
 from ....kernels.functional_sam import point_embed
 from ..layers import Conv2d, Embedding, Identity, LayerNorm2d
 from ..position_encoding import PositionEmbeddingRandom
@@ -53,3 +54,20 @@ class PromptEncoder(nn.Module):
     def sparse(self, pe_dev, labels_dev, dtype):
         """label embeddings added on the device -> [B, N, C] (differentiable in the embeddings)"""
         return point_embed(pe_dev, labels_dev, dtype, self.not_a_point_embed, self.point_embeddings)
+
+    @torch.no_grad()
+    def dense_from_mask(self, masks, dtype):
+        """_embed_masks (prompt_encoder.py:153-158) on NHWC masks [B, 4h, 4w, 1]: conv2x2/2 -> LN2d ->
+        GELU -> conv2x2/2 -> LN2d -> GELU -> conv1x1, as im2col GEMMs + row norms; returns the dense
+        embedding [B, h*w, C].  Forward only (the mask-prompt frame takes no gradient)."""
+        from ....kernels.functional import _compute_weight
+        x = ops.cast(masks.contiguous(), dtype) if masks.dtype != dtype else masks
+        B = x.shape[0]
+        c0, n1, _, c3, n4, _, c6 = self.mask_downscaling
+        for conv, norm in ((c0, n1), (c3, n4)):
+            col, Ho, Wo = ops.im2col(x.contiguous(), 2, 2, 2, 0)
+            y = ops.linear(col, _compute_weight(conv), conv.bias.detach())
+            y, _, _ = ops.layernorm_fwd(y, norm.weight.detach(), norm.bias.detach(), norm.eps)
+            x = ops.act_fwd(y, "gelu").view(B, Ho, Wo, -1)
+        y = ops.linear(x.reshape(-1, x.shape[-1]), _compute_weight(c6), c6.bias.detach())
+        return y.view(B, -1, self.embed_dim)

@@ -241,6 +241,37 @@ class SAM2Base(nn.Module):
             ptr = ops.gate_mix(ptr, score_flat, self.no_obj_ptr._s2h_compute.view(-1), scale_x=self.fixed_no_obj_ptr)
         return low, high, ious, ptr, score
 
+    @torch.no_grad()
+    def _use_mask_as_output(self, feat, masks, score, high_res, num_objects):
+        """sam2_base.py:436-486 (mask prompt on the conditioning frame): the object masks as output
+        logits (x20 - 10), antialiased bilinear /4 for the low-res, IoU prediction 1, and an object
+        pointer from the SAM heads run on the RAW backbone feature (no no_mem_embed) with
+        mask_downsample(mask) as the mask prompt; pointer gated by mask non-emptiness.  masks
+        [O, H, W] f32 on the device; score [O] = 20 * any(mask) - 10 (host-computed).  No
+        gradient reaches anything here (constant outputs, detached pointer)."""
+        from ...kernels.functional_sam import aa_downsample
+        O = num_objects
+        h = w = self.sam_image_embedding_size
+        H = self.image_size
+        dt = self.compute_dtype
+        high = ops.act_fwd(masks.reshape(O, H * H), None, scale=20.0, shift=-10.0)
+        low = aa_downsample(high.view(O, H, H), H // 4, H // 4).view(O, -1)
+        ious = torch.ones(O, 1, device=masks.device)
+        # mask_downsample: Conv2d(1, 1, 4, 4) as an im2col GEMM on the [O, H, W, 1] mask
+        m = ops.cast(masks.reshape(O, H, H, 1), dt) if dt != torch.float32 else masks.reshape(O, H, H, 1)
+        col, Ho, Wo = ops.im2col(m.contiguous(), 4, 4, 4, 0)
+        md = ops.linear(col, self.mask_downsample.compute_weight(), self.mask_downsample.compute_bias())
+        dense = self.sam_prompt_encoder.dense_from_mask(md.view(O, Ho, Wo, 1), dt)
+        pix = FN.expand_batch(feat.unsqueeze(0), O)
+        pe1, lab1 = self._mask_pad_prompt
+        sparse = self.sam_prompt_encoder.sparse(pe1, lab1, dt)
+        dense_pe = self.sam_prompt_encoder.dense_pe_table(pix.device, dt)
+        _, _, token0, _ = self.sam_mask_decoder(pix, h, w, dense_pe, sparse, self.sam_prompt_encoder.no_mask_embed,
+                                                high_res, dense=dense)
+        ptr = self.obj_ptr_proj(token0)
+        ptr = ops.gate_mix(ptr, score, self.no_obj_ptr._s2h_compute.view(-1), scale_x=self.fixed_no_obj_ptr)
+        return low, high, ious, ptr, score.view(O, 1)
+
     def _encode_new_memory(self, feat, high_res, score, num_objects):
         """sam2_base.py:715-769 (training): sigmoid(logits)*scale+bias -> memory encoder ->
         + no-object spatial embedding where the object is predicted absent."""

@@ -44,8 +44,6 @@ class SAM2Model(SAM2Base):
         self.config_path = config_path
         self.prompt_type = prompt_type
         assert prompt_type in ["point", "box", "mask"], f"prompt_type must be one of point/box/mask, got {prompt_type}"
-        if prompt_type == "mask":
-            raise NotImplementedError("mask prompts (use_mask_input_as_output_without_sam path) are not built yet")
         self.forward_backbone_per_frame_for_eval = forward_backbone_per_frame_for_eval
         self.num_pos_points = num_pos_points
         self.num_neg_points = num_neg_points
@@ -54,6 +52,9 @@ class SAM2Model(SAM2Base):
         cfg = load_model_config(config_path, image_size)
         kw = {k: instantiate(v) for k, v in cfg.items() if k != "_target_"}
         super().__init__(use_activation_checkpoint=use_activation_checkpoint, **kw)
+        if prompt_type == "mask" and not self.use_mask_input_as_output_without_sam:
+            raise NotImplementedError("mask prompts through the SAM heads (use_mask_input_as_output_without_sam "
+                                      "False) are not built; the SAM2.1 configs set it True")
         self.compute_dtype = DTYPES[compute_dtype]
         self.arena: Optional[ParamArena] = None
         self._load_weights(checkpoint_path, init_seed)
@@ -152,6 +153,9 @@ class SAM2Model(SAM2Base):
         for n, p in self.named_parameters():
             if not p.requires_grad:
                 continue
+            if self.prompt_type == "mask" and n == "no_mem_embed":
+                out.append(n)  # the mask-prompt frame bypasses it (sam2_base.py:796-806); no other frame adds it
+                continue
             if (n.startswith("memory_encoder.") or n in ("no_mem_pos_enc", "no_obj_ptr", "no_obj_embed_spatial")
                     or n.startswith("mask_downsample.") or n.startswith("sam_prompt_encoder.mask_downscaling.")
                     or n.startswith("sam_mask_decoder.pred_obj_score_head.") or n.startswith("obj_ptr_proj.")):
@@ -214,16 +218,24 @@ class SAM2Model(SAM2Base):
         hm = getattr(input, "host_masks0", None) if start_frame_idx == 0 else None
         masks0 = (hm if hm is not None else input.masks[start_frame_idx]).unsqueeze(1)
         obj_masks, obj_to_cat, num_categories = utils.cat_to_obj_mask(masks0)
+        O = len(obj_to_cat)
+        pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
+                                                        pad=True)
+        if self.prompt_type == "mask":
+            # the object masks are the prompt (sam2model.py:215-217); score = 20 * any(mask) - 10
+            # (sam2_base.py:473-477) is a host-side fact of the prompt
+            m = obj_masks.reshape(O, -1).float()
+            score = (m.amax(dim=1) > 0).float() * 20.0 - 10.0
+            return {"start_frame_idx": start_frame_idx, "obj_to_cat": obj_to_cat, "num_categories": num_categories,
+                    "points": None, "labels": None, "mask": True,
+                    "host": (obj_masks.reshape(O, *obj_masks.shape[-2:]).float(), score, pe1, lab1)}
         if self.prompt_type == "box":
             points, labels = utils.generate_box_prompt(obj_masks)
         else:
             points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
                                                          num_neg_points=self.num_neg_points,
                                                          include_center=self.include_center)
-        O = len(obj_to_cat)
         pe0, lab0 = self.sam_prompt_encoder.host_points(points, labels, pad=True)
-        pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
-                                                        pad=True)
         return {"start_frame_idx": start_frame_idx, "obj_to_cat": obj_to_cat, "num_categories": num_categories,
                 "points": points, "labels": labels, "host": (pe0, lab0, pe1, lab1)}
 
@@ -248,11 +260,17 @@ class SAM2Model(SAM2Base):
         backbone_out["num_frames"] = input.num_frames
         backbone_out["obj_to_cat"] = plan["obj_to_cat"]
         backbone_out["num_categories"] = plan["num_categories"]
-        backbone_out["prompt_cond"] = (dev[0], dev[1])
         backbone_out["prompt_pad"] = (dev[2], dev[3])
-        backbone_out["point_inputs_per_frame"] = {start_frame_idx: {"point_coords": plan["points"],
-                                                                    "point_labels": plan["labels"]}}
-        backbone_out["mask_inputs_per_frame"] = {}
+        if plan.get("mask"):
+            backbone_out["prompt_cond"] = None
+            backbone_out["mask_cond"] = (dev[0], dev[1])
+            backbone_out["point_inputs_per_frame"] = {}
+            backbone_out["mask_inputs_per_frame"] = {start_frame_idx: dev[0]}
+        else:
+            backbone_out["prompt_cond"] = (dev[0], dev[1])
+            backbone_out["point_inputs_per_frame"] = {start_frame_idx: {"point_coords": plan["points"],
+                                                                        "point_labels": plan["labels"]}}
+            backbone_out["mask_inputs_per_frame"] = {}
         return backbone_out
 
     def forward_tracking(self, backbone_out, input: BatchedVideoDatapoint, return_dict=False):
@@ -267,12 +285,22 @@ class SAM2Model(SAM2Base):
         O = len(backbone_out["obj_to_cat"])
         output_dict = {"cond_frame_outputs": {}, "non_cond_frame_outputs": {}}
         frames = []
+        mask_cond = backbone_out.get("mask_cond")
+        if mask_cond is not None:
+            if T <= 1 and self.training:
+                raise NotImplementedError("mask prompts on single-frame training clips go through the SAM heads "
+                                          "(sam2_base.py:796-800); not built")
+            self._mask_pad_prompt = backbone_out["prompt_pad"]
         for t in range(T):
             is_cond = t == 0
             feat_t = feats[t]
-            pix = self._prepare_memory_conditioned_features(t, is_cond, feat_t, pos, T, output_dict, O)
-            prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
-            low, high, ious, ptr, score = self._forward_sam_heads(pix, prompt, (s0[t:t + 1], s1[t:t + 1]), O)
+            if is_cond and mask_cond is not None:
+                low, high, ious, ptr, score = self._use_mask_as_output(feat_t, mask_cond[0], mask_cond[1],
+                                                                       (s0[t:t + 1], s1[t:t + 1]), O)
+            else:
+                pix = self._prepare_memory_conditioned_features(t, is_cond, feat_t, pos, T, output_dict, O)
+                prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
+                low, high, ious, ptr, score = self._forward_sam_heads(pix, prompt, (s0[t:t + 1], s1[t:t + 1]), O)
             mfeat, mpos = self._encode_new_memory(feat_t, high, score, O)
             entry = {"maskmem_features": mfeat, "maskmem_pos_enc": mpos, "obj_ptr": ptr}
             if is_cond:
@@ -285,8 +313,9 @@ class SAM2Model(SAM2Base):
             pin = backbone_out["point_inputs_per_frame"].get(t)
             low4 = low.view(O, 1, 4 * h, 4 * w)
             high4 = high.view(O, 1, self.image_size, self.image_size)
+            minp = backbone_out["mask_inputs_per_frame"].get(t)
             frames.append({
-                "point_inputs": pin, "mask_inputs": None,
+                "point_inputs": pin, "mask_inputs": minp,
                 "pred_masks": low4, "pred_masks_high_res": high4,
                 "multistep_pred_masks": low4, "multistep_pred_masks_high_res": high4,
                 "multistep_pred_multimasks": [low4], "multistep_pred_multimasks_high_res": [high4],

@@ -15,6 +15,7 @@ CASES = {
     "bplus128_point_all": ("base_plus", "point", ALL),
     "bplus128_point_all_t8": ("base_plus", "point", ALL),
     "tiny256_point_all_multi": ("tiny", "point", ALL),
+    "tiny256_mask_all": ("tiny", "mask", ALL),
     "bplus256_point_all": ("base_plus", "point", ALL),
 }
 # reference steps under CPU bf16 autocast (oracle/gen_golden.py), with their fp32 twin
