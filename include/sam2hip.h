@@ -56,6 +56,8 @@ int s2h_prof_read(int max, float* ms, int64_t* meta);
 /* ---------------------------------------------------------------- GEMM
  * C[b](m,n) = act(alpha * sum_k A[b](m,k) B[b](k,n) + bias) * cscale[n], dropout(p, seed),
  *             + R[b](m,n) + beta * C[b](m,n)
+ * (dropout element index drop_idx0 + (b*M + m)*N + n: a launch over frame f of a frame-stacked
+ *  activation passes f*M*N so the frame-batched backward regenerates the same mask)
  * A addressed as A[m*lda_m + k*lda_k] (one of lda_m, lda_k must be 1), B as
  * B[k*ldb_k + n*ldb_n] (one of ldb_k, ldb_n must be 1), batch strides sA/sB/sC.
  * dt_ab: S2H_F32 (fp32 MFMA, parity mode; dt_c must be F32) or S2H_BF16 (bf16 MFMA,
@@ -77,7 +79,7 @@ int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
              const float* bias, int bias_mode,
              const void* R, int64_t ldr, int64_t sR,
              void* X, int64_t ldx, int64_t sX, int aux_mode,
-             const float* cscale, float drop_p, uint64_t seed,
+             const float* cscale, float drop_p, uint64_t seed, uint64_t drop_idx0,
              float alpha, float beta, int act, hipStream_t stream);
 
 /* A/B switch (tests, benchmarks) for the bf16 GEMM tiling; returns the previous setting.
@@ -99,7 +101,8 @@ int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t
  * Fused multi-head attention, tensors [B, L, H, D] addressed through
  * (batch, head, row) strides with contiguous D; lse [B, H, Lq] fp32 (natural log).
  * Optional attention-probability dropout p_drop with a counter-based hash keyed by
- * `seed` (regenerated identically in the backward).  D in {32, 64, 96, 128, 256}
+ * `seed` (regenerated identically in the backward) over the element index
+ * idx0 + ((b*H + h)*Lq + q)*Lk + k.  D in {32, 64, 96, 128, 256}
  * for bf16, 32..256 (multiple of 4) for fp32.
  * Replaces F.scaled_dot_product_attention at hieradet.py:70 (windowed / global
  * Hiera attention), transformer.py:243 (two-way decoder attention) and
@@ -118,8 +121,8 @@ int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* k, int64_t skb, int64_t skh, int64_t skl,
                  const void* v, int64_t svb, int64_t svh, int64_t svl,
                  void* o, int64_t sob, int64_t soh, int64_t sol,
-                 float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
-                 hipStream_t st);
+                 float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws,
+                 int64_t ws_bytes, hipStream_t st);
 /* Backward of s2h_attn_fwd; di_ws: fp32 workspace [B*H*Lq].  bf16 with head_dim 128/256
  * and >= 128 query rows takes the flash path (dQ kernel with key-split fp32 partials in
  * `ws` of s2h_attn_bwd_ws_bytes(...) bytes, dK/dV kernel per 128-key block). */
@@ -133,8 +136,23 @@ int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
                  void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                  void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
-                 const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, void* ws,
-                 int64_t ws_bytes, hipStream_t st);
+                 const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0,
+                 void* ws, int64_t ws_bytes, hipStream_t st);
+/* Frame-batched flash backward (bf16, head_dim 128/256, Lq >= 128): nfr frames x bpf batches
+ * x H heads of the tracking loop in one launch per kernel -- Q / O / dO / dQ / lse uniform
+ * [nfr*bpf] batches, K / V / dK / dV packed per frame (frame f: bpf blocks of fr_lk[f] rows
+ * starting at row fr_krow[f]); frame f's dropout indices start at fr_idx0[f] (host arrays of
+ * nfr <= 32 entries).  The memory-attention backward of every frame at once
+ * (transformer.py:275-311 for frames 1..T-1, memory_attention.py:58-99). */
+/* 1 when s2h_flash_bwd_frames takes (dt, Lq, head_dim); 0 = run the frames one by one. */
+int s2h_flash_bwd_ok(int dt, int Lq, int D);
+int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk, const int64_t* fr_krow,
+                         const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                         const void* k, int64_t skh, int64_t skl, const void* v, int64_t svh, int64_t svl,
+                         const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout, int64_t sgb,
+                         int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk,
+                         int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh, int64_t sdvl, const float* lse,
+                         float* di_ws, float scale, float p_drop, uint64_t seed, hipStream_t st);
 
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:
@@ -169,13 +187,14 @@ int s2h_act_fwd(int dt, int64_t n, const void* x, int act, float scale, float sh
 int s2h_act_bwd(int dt, int64_t n, const void* x, const void* dy, int act, void* dx, int accum, hipStream_t st);
 /* dtype conversion (fp32 <-> bf16; sam2_base.py:391-399 `.float()` of the logits). */
 int s2h_cast(int dt_in, int dt_out, int64_t n, const void* x, void* y, hipStream_t st);
-/* out = a + dropout(b) (b may be NULL: out = dropout(a)); nn.Dropout at
+/* out = a + dropout(b) (b may be NULL: out = dropout(a)), element index idx0 + i; nn.Dropout at
  * memory_attention.py:40-48 and the post-attention / FFN dropouts. */
-int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out, hipStream_t st);
+int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, uint64_t idx0, void* out,
+                hipStream_t st);
 /* dx = act'(x_pre) * keep(i) / (1 - p) * dy in one pass: the backward of a Linear epilogue's
  * act -> dropout (memory_attention.py:95-98); x_pre NULL = no activation. */
 int s2h_act_dropout_bwd(int dt, int64_t n, const void* x_pre, const void* dy, int act, float p, uint64_t seed,
-                        void* dx, hipStream_t st);
+                        uint64_t idx0, void* dx, hipStream_t st);
 /* Axial rotary embedding of the first `nrot` rows of each batch (cos/sin tables
  * [period, D/2], row r uses entry r % period; inverse = 1 applies the transpose
  * rotation for the backward).  Replaces apply_rotary_enc (position_encoding.py:212-239)

@@ -27,6 +27,7 @@ struct AttnArgs {
   float p_drop;
   uint64_t seed;
   const uint64_t* seed_off;
+  uint64_t idx0;  // dropout element-index offset (frame slot of a frame-stacked batch)
 };
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
@@ -37,7 +38,7 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D);
 int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                   const void* k, int64_t skb, int64_t skh, int64_t skl, const void* v, int64_t svb, int64_t svh,
                   int64_t svl, void* o, int64_t sob, int64_t soh, int64_t sol, float* lse, float scale, float p_drop,
-                  uint64_t seed, void* ws, int64_t ws_bytes, hipStream_t st);
+                  uint64_t seed, uint64_t idx0, void* ws, int64_t ws_bytes, hipStream_t st);
 
 int s2h_flash_bwd_eligible(int dt, int Lq, int D);
 int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D);
@@ -46,7 +47,8 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sq
                   int64_t svl, const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout, int64_t sgb,
                   int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk, int64_t sdkb,
                   int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl, const float* lse,
-                  float* di_ws, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes, hipStream_t st);
+                  float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws, int64_t ws_bytes,
+                  hipStream_t st);
 
 // Workspace the backward wants (key-split dQ partials of the flash path); 0 = none.
 extern "C" int64_t s2h_attn_bwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D) {
@@ -192,7 +194,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
         rs[r] += p;
         if (drop) {
           const int qi = qw + (lane >> 4) * 4 + r;
-          uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+          uint64_t idx = a.idx0 + ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
           p = s2h_keep(a.seed, idx, thresh) ? p * inv_keep : 0.f;
         }
         Pw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p);
@@ -321,7 +323,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
         float p = (key < a.Lk && qi < a.Lq) ? exp2f(s[r] * sl2 - lse2[r]) : 0.f;
         float g = dp[r];
         if (drop) {
-          uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+          uint64_t idx = a.idx0 + ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
           g = s2h_keep(a.seed, idx, thresh) ? g * inv_keep : 0.f;
         }
         Sw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p * (g - di[r]));
@@ -432,7 +434,7 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
         float p = valid ? exp2f(s[r] * sl2 - lse_s[qc]) : 0.f;
         float pd = p, g = dp[r];
         if (drop) {
-          uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+          uint64_t idx = a.idx0 + ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
           bool keep = valid && s2h_keep(a.seed, idx, thresh);
           pd = keep ? p * inv_keep : 0.f;
           g = keep ? g * inv_keep : 0.f;
@@ -569,7 +571,7 @@ __global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
           rs[r] += p;
           if (drop) {
             const int qi = (lane >> 4) * 4 + r;
-            const uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
+            const uint64_t idx = a.idx0 + ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key;
             p = s2h_keep(a.seed, idx, thresh) ? p * inv_keep : 0.f;
           }
           Pw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p);
@@ -689,7 +691,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
           const float p = (krow < a.Lk && qi < a.Lq) ? exp2f(s[r] * sl2 - lse2[r]) : 0.f;
           float g = dp[r];
           if (drop) {
-            const uint64_t idx = ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + krow;
+            const uint64_t idx = a.idx0 + ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + krow;
             g = s2h_keep(a.seed, idx, thresh) ? g * inv_keep : 0.f;
           }
           Sw[((lane >> 4) * 4 + r) * PS + j * 16 + (lane & 15)] = from_f32<T>(p * (g - di[r]));
@@ -797,7 +799,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
           const float p = valid ? exp2f(s[r] * sl2 - lse_s[qc]) : 0.f;
           float pd = p, g = dp[r];
           if (drop) {
-            const uint64_t idx = ((uint64_t)bh * a.Lq + qrow) * (uint64_t)a.Lk + key;
+            const uint64_t idx = a.idx0 + ((uint64_t)bh * a.Lq + qrow) * (uint64_t)a.Lk + key;
             const bool keep = valid && s2h_keep(a.seed, idx, thresh);
             pd = keep ? p * inv_keep : 0.f;
             g = keep ? g * inv_keep : 0.f;
@@ -912,8 +914,8 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                             const void* k, int64_t skb, int64_t skh, int64_t skl,
                             const void* v, int64_t svb, int64_t svh, int64_t svl,
                             void* o, int64_t sob, int64_t soh, int64_t sol,
-                            float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
-                            hipStream_t st) {
+                            float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws,
+                            int64_t ws_bytes, hipStream_t st) {
   if (B * H <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
@@ -922,7 +924,7 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
   if (s2h_flash_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol)) {
     const int slot = s2h_prof_begin(st, 1, (int64_t)B * H, Lq, Lk, D, 2);
     const int rc = s2h_flash_fwd(B, H, Lq, Lk, D, q, sqb, sqh, sql, k, skb, skh, skl, v, svb, svh, svl, o, sob, soh,
-                                 sol, lse, scale, p_drop, seed, ws, ws_bytes, st);
+                                 sol, lse, scale, p_drop, seed, idx0, ws, ws_bytes, st);
     s2h_prof_end(slot, st);
     return rc;
   }
@@ -933,6 +935,7 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.v = v; a.svb = svb; a.svh = svh; a.svl = svl;
   a.o = o; a.sob = sob; a.soh = soh; a.sol = sol;
   a.lse = lse; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
+  a.idx0 = idx0;
   return dt == S2H_BF16 ? attn_dispatch<bf16, true>(a, st) : attn_dispatch<float, true>(a, st);
 }
 
@@ -945,8 +948,8 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                             void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
                             void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                             void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
-                            const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, void* ws,
-                            int64_t ws_bytes, hipStream_t st) {
+                            const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                            uint64_t idx0, void* ws, int64_t ws_bytes, hipStream_t st) {
   if (B * H <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
@@ -958,7 +961,7 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
     const int slot = s2h_prof_begin(st, 2, (int64_t)B * H, Lq, Lk, D, 2);
     const int rc = s2h_flash_bwd(B, H, Lq, Lk, D, q, sqb, sqh, sql, k, skb, skh, skl, v, svb, svh, svl, o, sob, soh,
                                  sol, dout, sgb, sgh, sgl, dq, sdqb, sdqh, sdql, dk, sdkb, sdkh, sdkl, dv, sdvb, sdvh,
-                                 sdvl, lse, di_ws, scale, p_drop, seed, ws, ws_bytes, st);
+                                 sdvl, lse, di_ws, scale, p_drop, seed, idx0, ws, ws_bytes, st);
     s2h_prof_end(slot, st);
     return rc;
   }
@@ -973,5 +976,6 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.dk = dk; a.sdkb = sdkb; a.sdkh = sdkh; a.sdkl = sdkl;
   a.dv = dv; a.sdvb = sdvb; a.sdvh = sdvh; a.sdvl = sdvl;
   a.lse = (float*)lse; a.di = di_ws; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
+  a.idx0 = idx0;
   return dt == S2H_BF16 ? attn_dispatch<bf16, false>(a, st) : attn_dispatch<float, false>(a, st);
 }

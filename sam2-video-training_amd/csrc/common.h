@@ -4,6 +4,9 @@
 // activations: `float` (fp32-parity mode, f32-input MFMA 16x16x4) or `__bf16`
 // (performance mode, bf16 MFMA 16x16x32).  Accumulation is always fp32.
 #pragma once
+
+// frames one frame-batched launch can cover (the tracking loop's frames, T <= 32)
+#define S2H_MAX_FRAMES 32
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 

@@ -109,20 +109,20 @@ extern "C" int s2h_act_bwd(int dt, int64_t n, const void* x, const void* dy, int
 // mask is the forward's counter hash of the flat output index.  x_pre may be null (no act).
 template <typename T>
 __global__ void act_dropout_bwd_kernel(int64_t n, const void* x, const void* dy, int act, float p, uint64_t seed,
-                                       const uint64_t* seed_off, void* dx) {
+                                       const uint64_t* seed_off, uint64_t idx0, void* dx) {
   seed = s2h_seed(seed, seed_off);
   const uint32_t thresh = (uint32_t)(p * 4294967296.0);
   const float inv = p > 0.f ? 1.f / (1.f - p) : 1.f;
   GRID_STRIDE(i, n) {
-    float v = (p > 0.f && !s2h_keep(seed, (uint64_t)i, thresh)) ? 0.f : to_f32(((const T*)dy)[i]) * inv;
+    float v = (p > 0.f && !s2h_keep(seed, idx0 + (uint64_t)i, thresh)) ? 0.f : to_f32(((const T*)dy)[i]) * inv;
     if (x) v *= act_grad(to_f32(((const T*)x)[i]), act);
     ((T*)dx)[i] = from_f32<T>(v);
   }
 }
 extern "C" int s2h_act_dropout_bwd(int dt, int64_t n, const void* x_pre, const void* dy, int act, float p,
-                                   uint64_t seed, void* dx, hipStream_t st) {
+                                   uint64_t seed, uint64_t idx0, void* dx, hipStream_t st) {
   if (n <= 0) return 0;
-  DISPATCH_T(dt, act_dropout_bwd_kernel, ew_grid(n), n, x_pre, dy, act, p, seed, s2h_rng_offset_ptr(), dx);
+  DISPATCH_T(dt, act_dropout_bwd_kernel, ew_grid(n), n, x_pre, dy, act, p, seed, s2h_rng_offset_ptr(), idx0, dx);
   return (int)hipGetLastError();
 }
 
@@ -147,20 +147,20 @@ extern "C" int s2h_cast(int dt_in, int dt_out, int64_t n, const void* x, void* y
 // mode 0: out = a + keep(i)*b/(1-p)     mode 1: out = keep(i)*b/(1-p)   (also the backward)
 template <typename T>
 __global__ void dropout_kernel(int64_t n, const void* a, const void* b, float p, uint64_t seed, const uint64_t* seed_off,
-                               void* out) {
+                               uint64_t idx0, void* out) {
   seed = s2h_seed(seed, seed_off);
   const uint32_t thresh = (uint32_t)(p * 4294967296.0);
   const float inv = 1.f / (1.f - p);
   GRID_STRIDE(i, n) {
-    float v = s2h_keep(seed, (uint64_t)i, thresh) ? to_f32(((const T*)b)[i]) * inv : 0.f;
+    float v = s2h_keep(seed, idx0 + (uint64_t)i, thresh) ? to_f32(((const T*)b)[i]) * inv : 0.f;
     if (a) v += to_f32(((const T*)a)[i]);
     ((T*)out)[i] = from_f32<T>(v);
   }
 }
-extern "C" int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, void* out,
-                           hipStream_t st) {
+extern "C" int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64_t seed, uint64_t idx0,
+                           void* out, hipStream_t st) {
   if (n <= 0) return 0;
-  DISPATCH_T(dt, dropout_kernel, ew_grid(n), n, a, b, p, seed, s2h_rng_offset_ptr(), out);
+  DISPATCH_T(dt, dropout_kernel, ew_grid(n), n, a, b, p, seed, s2h_rng_offset_ptr(), idx0, out);
   return (int)hipGetLastError();
 }
 

@@ -32,6 +32,7 @@ struct FlashArgs {
   float* lse;
   float sl2;  // scale * log2(e)
   float p_drop; uint32_t thresh; float inv_keep; uint64_t seed; const uint64_t* seed_off;
+  uint64_t idx0;  // dropout element-index offset (this launch's frame slot in a frame-stacked batch)
   int splits, tiles_per_split;
   float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
   float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
@@ -78,7 +79,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
-  const uint64_t drow = ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
+  const uint64_t drow = a.idx0 + ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
   const int qq = (lane >> 2) & 3, pp = lane & 3;  // transposing-read lane roles
 
   for (int it = 0; it < nt; ++it) {
@@ -306,9 +307,10 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
                   const void* k, int64_t skb, int64_t skh, int64_t skl,
                   const void* v, int64_t svb, int64_t svh, int64_t svl,
                   void* o, int64_t sob, int64_t soh, int64_t sol,
-                  float* lse, float scale, float p_drop, uint64_t seed, void* ws, int64_t ws_bytes,
+                  float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws, int64_t ws_bytes,
                   hipStream_t st) {
   FlashArgs a = {};
+  a.idx0 = idx0;
   a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
   a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;

@@ -15,6 +15,9 @@
 //          dV^T += dO^T P_drop and dK^T += Q^T dS (dO^T / Q^T by transposing reads).
 #include "flash_common.h"
 
+int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
+void s2h_prof_end(int slot, hipStream_t st);
+
 struct FlashBwdArgs {
   int BH, H, Lq, Lk;
   const bf16* q; int64_t sqb, sqh, sql;
@@ -33,7 +36,45 @@ struct FlashBwdArgs {
   float* ws_dq;  // [splits][BH*Lq][DP] fp32 partial dQ (splits > 1)
   int kv_splits, kv_tiles_per_split;  // dK/dV kernel: query range split over workgroups
   float* ws_dkv;  // [kv_splits][BH*Lk][2][DP] fp32 partial (dK, dV) (kv_splits > 1)
+  uint64_t idx0;  // dropout element-index offset (single-frame launches)
+  // Frame table (nfr > 0): the batch is nfr frames x bpf batches, Q / O / dO / dQ / LSE uniform,
+  // K / V / dK / dV PACKED per frame: batch bl of frame f has fr_lk[f] keys starting at row
+  // fr_krow[f] + bl * fr_lk[f]; dropout indices of frame f start at fr_idx0[f] (the offsets its
+  // forward launch used).  One launch covers the frame-batched backward of every frame.
+  int nfr, bpf;
+  int fr_lk[S2H_MAX_FRAMES];
+  int64_t fr_krow[S2H_MAX_FRAMES];
+  uint64_t fr_idx0[S2H_MAX_FRAMES];
 };
+
+// K / V / dK / dV bases, key count and dropout index base (query 0) of batch-head bh
+struct KvFrame {
+  const bf16* k; const bf16* v; bf16* dk; bf16* dv;
+  int Lk;
+  uint64_t drow0;
+};
+__device__ __forceinline__ KvFrame kv_frame(const FlashBwdArgs& a, int bh) {
+  const int b = bh / a.H, h = bh % a.H;
+  KvFrame r;
+  if (a.nfr > 0) {
+    const int f = b / a.bpf, bl = b - f * a.bpf;
+    r.Lk = a.fr_lk[f];
+    const int64_t row = a.fr_krow[f] + (int64_t)bl * r.Lk;
+    r.k = a.k + row * a.skl + h * a.skh;
+    r.v = a.v + row * a.svl + h * a.svh;
+    r.dk = a.dk + row * a.sdkl + h * a.sdkh;
+    r.dv = a.dv + row * a.sdvl + h * a.sdvh;
+    r.drow0 = a.fr_idx0[f] + (uint64_t)(bl * a.H + h) * (uint64_t)a.Lq * (uint64_t)r.Lk;
+  } else {
+    r.Lk = a.Lk;
+    r.k = a.k + b * a.skb + h * a.skh;
+    r.v = a.v + b * a.svb + h * a.svh;
+    r.dk = a.dk + b * a.sdkb + h * a.sdkh;
+    r.dv = a.dv + b * a.sdvb + h * a.sdvh;
+    r.drow0 = a.idx0 + (uint64_t)bh * (uint64_t)a.Lq * (uint64_t)a.Lk;
+  }
+  return r;
+}
 
 // ------------------------------------------------------------------ Di
 template <int DP>
@@ -68,15 +109,17 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   const int q = blockIdx.x * FL_QB + w * 16 + ql;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
-  const bf16* K = a.k + b * a.skb + h * a.skh;
-  const bf16* V = a.v + b * a.svb + h * a.svh;
-  const int ntiles_all = (a.Lk + C::KT - 1) / C::KT;
+  const KvFrame fr = kv_frame(a, bh);
+  const bf16* K = fr.k;
+  const bf16* V = fr.v;
+  const int Lk = fr.Lk;
+  const int ntiles_all = (Lk + C::KT - 1) / C::KT;
   const int t0 = split * a.tiles_per_split;
   const int nt = min(ntiles_all, t0 + a.tiles_per_split) - t0;
 
   if (nt > 0) {
-    dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
-    dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane);
+    dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane);
   }
   const bool qv = q < a.Lq;
   bf16x8 qf[C::NT], gf[C::NT];
@@ -93,7 +136,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   f32x4 acc[C::ND];  // dQ^T: row d = 16*db + 4g + r, column q
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const uint64_t drow = ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
+  const uint64_t drow = fr.drow0 + (uint64_t)q * (uint64_t)Lk;
 
   for (int it = 0; it < nt; ++it) {
     const int k0 = (t0 + it) * C::KT;
@@ -101,8 +144,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     char* Vb = Kb + C::TILEB;
     if (it + 1 < nt) {
       char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
-      dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane);
+      dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane);
       wait_vmcnt<2 * C::PPW>();
     } else {
       wait_vmcnt<0>();
@@ -123,7 +166,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
         dp[kb] = mfma16(vf, gf[t], dp[kb]);
       }
     }
-    const bool full = k0 + C::KT <= a.Lk;
+    const bool full = k0 + C::KT <= Lk;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       bool kp[4] = {true, true, true, true};
@@ -139,7 +182,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool valid = full || (k0 + kb * 16 + 4 * g + r < a.Lk);
+        const bool valid = full || (k0 + kb * 16 + 4 * g + r < Lk);
         const float p = valid ? __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2) : 0.f;
         const float dpd = kp[r] ? dp[kb][r] * a.inv_keep : 0.f;
         s[kb][r] = p * (dpd - di);  // dS (scale applied at the end)
@@ -203,11 +246,13 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int key = blockIdx.x * FL_QB + w * 16 + kl;  // this lane's key (B-operand column)
-  const bool kv = key < a.Lk;
+  const KvFrame fr = kv_frame(a, bh);
+  if ((int)blockIdx.x * FL_QB >= fr.Lk) return;  // frame-table launch: past this frame's keys
+  const bool kv = key < fr.Lk;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
-  const bf16* K = a.k + b * a.skb + h * a.skh;
-  const bf16* V = a.v + b * a.svb + h * a.svh;
+  const bf16* K = fr.k;
+  const bf16* V = fr.v;
   const int nt = (a.Lq + C::KT - 1) / C::KT;
 
   dma_tile<DP, 32, FL_WAVES, true>(smem, Q, a.sql, 0, a.Lq, w, lane);
@@ -284,7 +329,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
         const int qi = q0 + 16 * qb + 4 * g + r;
         const float p = __builtin_amdgcn_exp2f(s[qb][r] * a.sl2 - lt[r] * FL_LOG2E);
         bool keep = true;
-        if (a.p_drop > 0.f) keep = s2h_keep(a.seed, ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key, a.thresh);
+        if (a.p_drop > 0.f) keep = s2h_keep(a.seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
         const float pd = keep ? p * a.inv_keep : 0.f;
         const float dpd = keep ? dp[qb][r] * a.inv_keep : 0.f;
         pdb[4 * qb + r] = (bf16)pd;
@@ -301,8 +346,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   }
 
   if (!kv) return;
-  bf16* DK = a.dk + b * a.sdkb + h * a.sdkh + (int64_t)key * a.sdkl;
-  bf16* DV = a.dv + b * a.sdvb + h * a.sdvh + (int64_t)key * a.sdvl;
+  bf16* DK = fr.dk + (int64_t)key * a.sdkl;
+  bf16* DV = fr.dv + (int64_t)key * a.sdvl;
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) {
     bf16 tk[4], tv[4];
@@ -337,11 +382,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, kl = lane & 31;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int key = blockIdx.x * (NWV * 32) + w * 32 + kl;
-  const bool kv = key < a.Lk;
+  const KvFrame fr = kv_frame(a, bh);
+  if ((int)blockIdx.x * (NWV * 32) >= fr.Lk) return;  // frame-table launch: past this frame's keys
+  const bool kv = key < fr.Lk;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
-  const bf16* K = a.k + b * a.skb + h * a.skh;
-  const bf16* V = a.v + b * a.svb + h * a.svh;
+  const bf16* K = fr.k;
+  const bf16* V = fr.v;
   // query tiles [qt0, qt0 + nt) of this workgroup (kv_splits > 1: partial dK / dV)
   const int nt_all = (a.Lq + QT - 1) / QT;
   const int qt0 = blockIdx.z * a.kv_tiles_per_split;
@@ -356,12 +403,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     const float* src = (lane < 32 ? LSE : DI) + qi;
     lds_dma4(src, stage + 2 * C::TILEB + w * 256);
   };
-  dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), a.Lk, w, lane);
+  dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), fr.Lk, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
   bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
-  const int64_t vkey = min(key, a.Lk - 1);
+  const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
   for (int t = 0; t < NT; ++t) vf[t] = *(const bf16x8*)(V + vkey * a.svl + 16 * t + 8 * hi);
   __builtin_amdgcn_s_waitcnt(0xF70);  // retire the V loads in the compiler's bookkeeping (see dq)
@@ -406,7 +453,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       const float lse_r = rows[ql], di_r = rows[32 + ql];
       const float p = qi < a.Lq ? __builtin_amdgcn_exp2f(s[r] * a.sl2 - lse_r * FL_LOG2E) : 0.f;
       bool keep = true;
-      if (a.p_drop > 0.f) keep = s2h_keep(a.seed, ((uint64_t)bh * a.Lq + qi) * (uint64_t)a.Lk + key, a.thresh);
+      if (a.p_drop > 0.f) keep = s2h_keep(a.seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
       const float pd = keep ? p * a.inv_keep : 0.f;
       const float dpd = keep ? dp[r] * a.inv_keep : 0.f;
       pdb[r >> 3][r & 7] = (bf16)pd;
@@ -426,7 +473,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
 
   if (!kv) return;
   if (a.kv_splits > 1) {  // fp32 partials, summed (and scaled, cast) by flash_bwd_dkv_combine_kernel
-    float* W = a.ws_dkv + (((int64_t)blockIdx.z * a.BH + bh) * a.Lk + key) * 2 * DP;
+    float* W = a.ws_dkv + (((int64_t)blockIdx.z * a.BH + bh) * a.Lk + key) * 2 * DP;  // single-frame only
 #pragma unroll
     for (int d = 0; d < ND; ++d)
 #pragma unroll
@@ -437,8 +484,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       }
     return;
   }
-  bf16* DK = a.dk + b * a.sdkb + h * a.sdkh + (int64_t)key * a.sdkl;
-  bf16* DV = a.dv + b * a.sdvb + h * a.sdvh + (int64_t)key * a.sdvl;
+  bf16* DK = fr.dk + (int64_t)key * a.sdkl;
+  bf16* DV = fr.dv + (int64_t)key * a.sdvl;
 #pragma unroll
   for (int d = 0; d < ND; ++d)
 #pragma unroll
@@ -543,9 +590,10 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
                   void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
                   void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                   void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
-                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, void* ws,
+                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws,
                   int64_t ws_bytes, hipStream_t st) {
   FlashBwdArgs a = {};
+  a.idx0 = idx0;
   a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
   a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;
@@ -580,3 +628,54 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
 int s2h_flash_bwd_eligible(int dt, int Lq, int D);
 int s2h_flash_eligible(int dt, int Lq, int D);
 int s2h_flash_bwd_eligible(int dt, int Lq, int D) { return s2h_flash_eligible(dt, Lq, D) && (D == 128 || D == 256); }
+
+// Frame-batched backward: nfr frames x bpf batches x H heads in ONE launch per kernel.  Q / O /
+// dO / dQ / LSE are [nfr * bpf] uniform batches (batch stride sqb ...); K / V / dK / dV are
+// packed per frame (frame f: bpf blocks of fr_lk[f] rows from row fr_krow[f]; row stride skl,
+// head stride skh); dropout indices of frame f start at fr_idx0[f].  nfr * bpf * (Lq / 128)
+// query blocks fill the chip without key or query splits, so no fp32 partials or combines.
+extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk, const int64_t* fr_krow,
+                                    const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                                    const void* k, int64_t skh, int64_t skl, const void* v, int64_t svh, int64_t svl,
+                                    const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout,
+                                    int64_t sgb, int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh,
+                                    int64_t sdql, void* dk, int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh,
+                                    int64_t sdvl, const float* lse, float* di_ws, float scale, float p_drop,
+                                    uint64_t seed, hipStream_t st) {
+  if (nfr <= 0 || bpf <= 0 || H <= 0 || Lq <= 0) return 0;
+  if (nfr > S2H_MAX_FRAMES || !(D == 128 || D == 256) || Lq < 128) return (int)hipErrorInvalidValue;
+  FlashBwdArgs a = {};
+  a.nfr = nfr; a.bpf = bpf;
+  int lk_max = 0;
+  for (int f = 0; f < nfr; ++f) {
+    if (fr_lk[f] <= 0) return (int)hipErrorInvalidValue;
+    a.fr_lk[f] = fr_lk[f]; a.fr_krow[f] = fr_krow[f]; a.fr_idx0[f] = fr_idx0[f];
+    lk_max = std::max(lk_max, fr_lk[f]);
+  }
+  a.BH = nfr * bpf * H; a.H = H; a.Lq = Lq; a.Lk = lk_max;
+  a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
+  a.k = (const bf16*)k; a.skh = skh; a.skl = skl;
+  a.v = (const bf16*)v; a.svh = svh; a.svl = svl;
+  a.o = (const bf16*)o; a.sob = sob; a.soh = soh; a.sol = sol;
+  a.g = (const bf16*)dout; a.sgb = sgb; a.sgh = sgh; a.sgl = sgl;
+  a.dq = (bf16*)dq; a.sdqb = sdqb; a.sdqh = sdqh; a.sdql = sdql;
+  a.dk = (bf16*)dk; a.sdkh = sdkh; a.sdkl = sdkl;
+  a.dv = (bf16*)dv; a.sdvh = sdvh; a.sdvl = sdvl;
+  a.lse = lse; a.di = di_ws;
+  a.scale = scale; a.sl2 = scale * FL_LOG2E;
+  a.p_drop = p_drop;
+  a.thresh = (uint32_t)(p_drop * 4294967296.0);
+  a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed;
+  a.seed_off = s2h_rng_offset_ptr();
+  a.splits = 1; a.tiles_per_split = (lk_max + 63) / 64;
+  a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32;
+  const int slot = s2h_prof_begin(st, 2, (int64_t)a.BH, Lq, lk_max, D, 3);
+  const int rc = D == 256 ? flash_bwd_launch<256>(a, st) : flash_bwd_launch<128>(a, st);
+  s2h_prof_end(slot, st);
+  return rc;
+}
+
+// the frame-batched backward's domain for the host (bf16, head_dim 128 / 256, >= 128 query
+// rows, flash path not switched off by s2h_attn_config)
+extern "C" int s2h_flash_bwd_ok(int dt, int Lq, int D) { return s2h_flash_bwd_eligible(dt, Lq, D); }

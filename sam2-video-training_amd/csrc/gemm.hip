@@ -21,6 +21,7 @@ struct GemmArgs {
   int aux_mode;
   const float* cscale;        // optional per-column scale applied after the activation
   float drop_p; uint64_t seed; const uint64_t* seed_off; // optional dropout after the activation (index = row*N + col)
+  uint64_t drop_idx0;  // dropout element-index offset (frame slot of a frame-stacked activation)
   float alpha, beta; int act;
   int vecA, vecB;
 };
@@ -147,7 +148,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
           else v = apply_act(v, p.act);
           if (p.cscale) v *= p.cscale[col];
           if (p.drop_p > 0.f) {
-            const uint64_t idx = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
+            const uint64_t idx = p.drop_idx0 + (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col;
             v = s2h_keep(p.seed, idx, (uint32_t)(p.drop_p * 4294967296.0)) ? v / (1.f - p.drop_p) : 0.f;
           }
           if (R) v += to_f32(R[(int64_t)row * p.ldr + col]);
@@ -187,7 +188,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
                         const float* bias, int bias_mode,
                         const void* R, int64_t ldr, int64_t sR,
                         void* X, int64_t ldx, int64_t sX, int aux_mode,
-                        const float* cscale, float drop_p, uint64_t seed,
+                        const float* cscale, float drop_p, uint64_t seed, uint64_t drop_idx0,
                         float alpha, float beta, int act, hipStream_t stream) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   if (!(lda_k == 1 || lda_m == 1) || !(ldb_k == 1 || ldb_n == 1)) return (int)hipErrorInvalidValue;
@@ -201,6 +202,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   a.R = R; a.ldr = ldr; a.sR = sR;
   a.X = X; a.ldx = ldx; a.sX = sX; a.aux_mode = X ? aux_mode : 0;
   a.cscale = cscale; a.drop_p = drop_p; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
+  a.drop_idx0 = drop_idx0;
   a.alpha = alpha; a.beta = beta; a.act = act;
   const int esz = dt_ab == S2H_BF16 ? 2 : 4;
   const int vec = 16 / esz;
@@ -229,6 +231,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   b.R = R; b.ldr = ldr; b.sR = sR;
   b.X = X; b.ldx = ldx; b.sX = sX; b.aux_mode = a.aux_mode;
   b.cscale = cscale; b.drop_p = drop_p; b.seed = seed; b.seed_off = s2h_rng_offset_ptr();
+  b.drop_idx0 = drop_idx0;
   b.alpha = alpha; b.beta = beta; b.act = act;
   b.vecA = a.vecA; b.vecB = a.vecB;
   b.out_f32 = dt_c == S2H_F32;
@@ -252,7 +255,7 @@ extern "C" int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* 
   if (!accumulate && db) s2h_zero_f32(db, 1, N, N, stream);
   if (dt == S2H_F32) {
     int rc = s2h_gemm(S2H_F32, S2H_F32, 1, N, K, (int)rows, dy, 1, lddy, 0, x, ldx, 1, 0, dw, lddw, 0, nullptr, 0,
-                      nullptr, 0, 0, nullptr, 0, 0, 0, nullptr, 0.f, 0, 1.f, accumulate ? 1.f : 0.f, 0, stream);
+                      nullptr, 0, 0, nullptr, 0, 0, 0, nullptr, 0.f, 0, 0, 1.f, accumulate ? 1.f : 0.f, 0, stream);
     if (rc || !db) return rc;
     return s2h_colsum(dt, rows, N, dy, lddy, db, 1, stream);
   }

@@ -12,7 +12,7 @@ struct GemmArgs16 {
   void* X; int64_t ldx, sX;
   int aux_mode;
   const float* cscale;
-  float drop_p; uint64_t seed; const uint64_t* seed_off;
+  float drop_p; uint64_t seed; const uint64_t* seed_off; uint64_t drop_idx0;
   float alpha, beta; int act;
   int vecA, vecB;
   int splits, kchunk;  // split-K: blockIdx.z = batch * splits + split

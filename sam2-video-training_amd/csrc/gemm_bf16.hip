@@ -154,7 +154,7 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
   if (p.drop_p > 0.f) {
     const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
     const float inv_keep = 1.f / (1.f - p.drop_p);
-    const uint64_t idx0 = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
+    const uint64_t idx0 = p.drop_idx0 + (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
     bool k[4];
     if ((idx0 & 1) == 0) {
       s2h_keep_pair(p.seed, idx0 >> 1, thresh, k[0], k[1]);
@@ -277,7 +277,7 @@ __device__ __forceinline__ void epilogue8(const GemmArgs16& p, int bz, int row, 
   if (p.drop_p > 0.f) {
     const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
     const float inv_keep = 1.f / (1.f - p.drop_p);
-    const uint64_t idx0 = (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
+    const uint64_t idx0 = p.drop_idx0 + (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
     bool k[8];
     if ((idx0 & 1) == 0) {
 #pragma unroll

@@ -27,17 +27,22 @@ F = c_float
 SIGNATURES = {
     "s2h_version": [],
     "s2h_rng_bind": [P],
-    "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, F, F, I, P],
+    "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, c_uint64,
+                 F, F, I, P],
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],
     "s2h_attn_bwd_ws_bytes": [I, I, I, I, I, I],
-    "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, P, L, P],
+    "s2h_attn_fwd": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, F, F, c_uint64, c_uint64, P, L,
+                     P],
     "s2h_attn_bwd": [I, I, I, I, I, I,
                      P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
                      P, L, L, L, P, L, L, L, P, L, L, L,
-                     P, P, F, F, c_uint64, P, L, P],
+                     P, P, F, F, c_uint64, c_uint64, P, L, P],
+    "s2h_flash_bwd_ok": [I, I, I],
+    "s2h_flash_bwd_frames": [I, I, I, I, I, P, P, P, P, L, L, L, P, L, L, P, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
+                             P, L, L, P, L, L, P, P, F, F, c_uint64, P],
     "s2h_layernorm_fwd": [I, I, I, P, L, P, L, I, P, P, P, F, P, L, P, P, P],
     "s2h_layernorm_bwd_ws_bytes": [I, I, I],
     "s2h_layernorm_bwd": [I, I, I, P, L, P, L, P, P, P, P, L, I, P, L, P, P, P, P],
@@ -46,8 +51,8 @@ SIGNATURES = {
     "s2h_act_fwd": [I, L, P, I, F, F, P, P],
     "s2h_act_bwd": [I, L, P, P, I, P, I, P],
     "s2h_cast": [I, I, L, P, P, P],
-    "s2h_dropout": [I, L, P, P, F, c_uint64, P, P],
-    "s2h_act_dropout_bwd": [I, L, P, P, I, F, c_uint64, P, P],
+    "s2h_dropout": [I, L, P, P, F, c_uint64, c_uint64, P, P],
+    "s2h_act_dropout_bwd": [I, L, P, P, I, F, c_uint64, c_uint64, P, P],
     "s2h_rope": [I, L, I, I, P, L, L, P, L, L, P, P, I, I, P],
     "s2h_maxpool2_fwd": [I, I, I, I, I, P, L, P, P],
     "s2h_maxpool2_bwd": [I, I, I, I, I, P, L, P, P, L, P],

@@ -1,0 +1,930 @@
+"""Frame-batched backward of the tracking loop.
+
+The tracking loop (reference sam2model.py:266-401) is sequential in the forward -- frame t reads
+the memory bank written by frames < t -- but its backward is not: the bank entries and object
+pointers are detached (sam2model.py:340-358), so every frame's graph ends at the bank and the
+frames' backwards are independent.  Running them one frame at a time (autograd) leaves every
+GEMM at 13 objects x 1024 tokens and every flash-attention backward at 13 batches: latency-bound
+launches far below the MFMA roofline.
+
+A FrameTape records the per-frame ops of one program (the memory attention of frames 1..T-1, or
+the SAM heads of frames 0..T-1).  Every frame runs the SAME op sequence; op k's outputs at frame
+f are written straight into slot f of a [F, ...] buffer (or, for the memory-bank-sized tensors
+whose row count grows with the frame, into frame f's rows of a packed buffer), so everything the
+backward needs is already stacked.  The backward walks the ops once in reverse and runs each op
+over all frames: one dgrad GEMM, one weight-gradient GEMM, one LayerNorm backward, one flash
+backward (s2h_flash_bwd_frames, packed per-frame K/V) per op instead of F of each.
+
+Dropout stays mask-identical to the per-frame forward: a dropout site draws one seed and frame
+f's launch offsets its element indices by the elements of frames < f (the kernels' idx0), so the
+stacked backward regenerates exactly the forward's masks.
+
+While a tape is recording, the sam2_video.kernels.functional ops dispatch here (`active()`); the
+module code is shared with the autograd path.  Test infrastructure compares both paths
+(tests/test_frametape_gpu.py).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import torch
+
+from . import ops
+
+_ACTIVE: List[Optional["FrameTape"]] = [None]
+
+
+def active() -> Optional["FrameTape"]:
+    """the recording tape, when the op runs with autograd enabled (no_grad regions of the
+    tracking loop -- object pointers, memory encoder -- run the plain kernels)"""
+    t = _ACTIVE[0]
+    return t if (t is not None and torch.is_grad_enabled()) else None
+
+
+class recording:
+    """context: the FN ops record into `tape` for its current frame"""
+
+    def __init__(self, tape):
+        self.tape = tape
+
+    def __enter__(self):
+        self.prev = _ACTIVE[0]
+        _ACTIVE[0] = self.tape
+        return self.tape
+
+    def __exit__(self, *exc):
+        _ACTIVE[0] = self.prev
+
+
+def _grad_of(p):
+    return getattr(p, "_s2h_grad", None) if p is not None and p.requires_grad else None
+
+
+# ------------------------------------------------------------------------- storage
+class Store:
+    """A value's frame-stacked storage: uniform [F, *shape] or packed (frame f's rows at
+    offsets[f] of a flat [total] buffer; the per-frame element count scales with the frame's
+    memory rows)."""
+
+    def __init__(self, tape, shape, dtype, scale=None):
+        self.shape0 = tuple(shape)
+        self.dtype = dtype
+        F = tape.F
+        n0 = math.prod(shape)
+        if scale is None:  # uniform
+            self.numels = [n0] * F
+            self.buf = torch.empty(F * n0, device=tape.device, dtype=dtype)
+        else:  # element count of frame f = n0 * scale[f] / scale[0]
+            assert all(n0 * s % scale[0] == 0 for s in scale)
+            self.numels = [n0 * s // scale[0] for s in scale]
+            self.buf = torch.empty(sum(self.numels), device=tape.device, dtype=dtype)
+        self.offsets = [0]
+        for n in self.numels[:-1]:
+            self.offsets.append(self.offsets[-1] + n)
+        self.uniform = scale is None
+        self.scale = scale
+        if scale is not None:  # the varying dim: the one of size scale[0] (memory rows), unique
+            hits = [i for i, d in enumerate(self.shape0) if d == scale[0]]
+            assert len(hits) == 1, f"ambiguous memory-row dim in {self.shape0} (rows {scale[0]})"
+            self.vdim = hits[0]
+
+    def frame_shape(self, f):
+        if self.uniform:
+            return self.shape0
+        sh = list(self.shape0)
+        sh[self.vdim] = self.scale[f]
+        return tuple(sh)
+
+    def frame(self, f):
+        return self.buf[self.offsets[f]:self.offsets[f] + self.numels[f]].view(self.frame_shape(f))
+
+    def stacked(self, lead=None):
+        """uniform: [F, *shape] (or [F * shape[0], *shape[1:]] with lead='merge'); packed: flat"""
+        if not self.uniform:
+            return self.buf
+        F = len(self.numels)
+        if lead == "merge":
+            return self.buf.view(F * self.shape0[0], *self.shape0[1:])
+        return self.buf.view(F, *self.shape0)
+
+
+class Op:
+    __slots__ = ("kind", "idx", "ins", "outs", "attrs", "fattrs", "saved", "needs", "bw")
+
+    def __init__(self, kind, ins, outs, attrs, bw):
+        self.kind = kind
+        self.idx = -1
+        self.ins = ins      # input value ids (None = constant / param-only)
+        self.outs = outs    # output value ids
+        self.attrs = attrs  # frame-invariant attributes
+        self.fattrs = {}    # per-frame attribute lists
+        self.saved = {}     # name -> value id / Store / per-frame list
+        self.needs = None
+        self.bw = bw
+
+
+class FrameTape:
+    def __init__(self, nframes: int, device, mem_rows: Optional[List[int]] = None, name: str = ""):
+        self.F = int(nframes)
+        self.device = device
+        self.name = name
+        self.mem_rows = list(mem_rows) if mem_rows is not None else None
+        self.ops: List[Op] = []
+        self.f = -1
+        self.k = 0
+        self.stores: Dict[object, Store] = {}   # value id -> Store
+        self.requires: Dict[object, bool] = {}  # value id -> needs grad
+        self.ptr2vid: Dict[int, object] = {}    # current frame: data_ptr -> value id
+        self.inputs: Dict[str, object] = {}     # declared grad-carrying frame inputs
+        self._seeds: Dict[int, int] = {}
+
+    # ------------------------------------------------------------ frames
+    def begin_frame(self):
+        self.f += 1
+        assert self.f < self.F, f"tape {self.name}: more frames than declared ({self.F})"
+        self.k = 0
+        self.ptr2vid = {}
+
+    def end_frame(self):
+        assert self.k == len(self.ops), f"tape {self.name}: frame {self.f} ran {self.k} ops, frame 0 {len(self.ops)}"
+
+    # ------------------------------------------------------------ values
+    def _register(self, vid, t):
+        self.ptr2vid[t.data_ptr()] = vid
+
+    def vid(self, t):
+        """value id of a tensor produced by this frame's ops (None = constant)"""
+        if t is None:
+            return None
+        v = self.ptr2vid.get(t.data_ptr())
+        if v is None and self.f == 0:
+            self._check_const(t)
+        return v
+
+    def _check_const(self, t):
+        # a constant must not alias tape storage (a view the tape did not record)
+        p0, p1 = t.data_ptr(), t.data_ptr() + t.numel() * t.element_size()
+        for st in self.stores.values():
+            b0 = st.buf.data_ptr()
+            b1 = b0 + st.buf.numel() * st.buf.element_size()
+            if p0 < b1 and b0 < p1:
+                raise RuntimeError(f"tape {self.name}: tensor aliases tape storage but is not a recorded value "
+                                   f"(slice / copy outside the FN ops?)")
+
+    def input(self, name, t, requires_grad=True):
+        """declare a grad-carrying per-frame input (e.g. the backbone feature of this frame): its
+        frame values are stacked (copied) so the backward can return [F, ...] gradients"""
+        vid = ("in", name)
+        if self.f == 0:
+            self.stores[vid] = Store(self, t.shape, t.dtype)
+            self.requires[vid] = requires_grad
+            self.inputs[name] = vid
+        slot = self.stores[vid].frame(self.f)
+        slot.copy_(t.detach())
+        self._register(vid, slot)
+        return slot
+
+    def varlen_slot(self, name, shape, dtype):
+        """a packed per-frame buffer for a constant whose row count follows the memory rows (the
+        assembled memory bank): written by the caller, read by the ops as a value"""
+        vid = ("const", name)
+        if self.f == 0:
+            self.stores[vid] = Store(self, shape, dtype, scale=self.mem_rows)
+            self.requires[vid] = False
+        slot = self.stores[vid].frame(self.f)
+        assert tuple(slot.shape) == tuple(shape), (slot.shape, shape)
+        self._register(vid, slot)
+        return slot
+
+    def _varlen_scale(self, *ts):
+        for t in ts:
+            v = self.vid(t) if t is not None else None
+            if v is not None and not self.stores[v].uniform:
+                return self.stores[v].scale
+        return None
+
+    def _out(self, j, shape, dtype, scale=None):
+        """output j of the current op at this frame (allocated on frame 0)"""
+        vid = (self.k, j)
+        if self.f == 0:
+            self.stores[vid] = Store(self, shape, dtype, scale=scale)
+        slot = self.stores[vid].frame(self.f)
+        assert tuple(slot.shape) == tuple(shape), (self.name, self.k, slot.shape, shape)
+        self._register(vid, slot)
+        return vid, slot
+
+    def _aux(self, name, shape, dtype, scale=None):
+        """frame-stacked saved buffer of the current op (not a value)"""
+        key = ("aux", self.k, name)
+        if self.f == 0:
+            self.stores[key] = Store(self, shape, dtype, scale=scale)
+        return self.stores[key].frame(self.f)
+
+    def _begin(self, kind, ins, bw, attrs=None):
+        """start op `kind` at the current frame; returns (op, is_first_frame)"""
+        if self.f == 0:
+            op = Op(kind, [self.vid(t) if torch.is_tensor(t) else None for t in ins], [], attrs or {}, bw)
+            op.needs = [v is not None and self.requires.get(v, False) for v in op.ins]
+            op.idx = len(self.ops)
+            self.ops.append(op)
+            return op, True
+        op = self.ops[self.k]
+        assert op.kind == kind, f"tape {self.name}: frame {self.f} op {self.k} is {kind}, frame 0 had {op.kind}"
+        got = [self.vid(t) if torch.is_tensor(t) else None for t in ins]
+        assert got == op.ins, f"tape {self.name}: op {self.k} ({kind}) inputs differ between frames"
+        return op, False
+
+    def _finish(self, op, outs_vids, req):
+        if self.f == 0:
+            op.outs = outs_vids
+            for v in outs_vids:
+                self.requires[v] = req
+        self.k += 1
+
+    def _seed(self):
+        from .functional import next_seed
+        if self.f == 0:
+            s = next_seed()
+            self._seeds[self.k] = s
+            return s
+        return self._seeds[self.k]
+
+    def _fattr(self, op, name, value):
+        lst = op.fattrs.setdefault(name, [])
+        assert len(lst) == self.f
+        lst.append(value)
+
+    def _idx0(self, op, numel):
+        """dropout element offset of this frame: elements of all earlier frames of the site"""
+        lst = op.fattrs.setdefault("idx0", [])
+        n = op.fattrs.setdefault("numel", [])
+        assert len(lst) == self.f
+        lst.append(0 if self.f == 0 else lst[-1] + n[-1])
+        n.append(numel)
+        return lst[-1]
+
+    def _req(self, op, params=()):
+        return any(op.needs) or any(p is not None and p.requires_grad and _grad_of(p) is not None for p in params)
+
+    # ------------------------------------------------------------ backward
+    def backward(self, out_grads: Dict[object, torch.Tensor]):
+        """out_grads: value id -> stacked gradient.  Returns {input name: stacked gradient}."""
+        G = dict(out_grads)
+        owned = set()
+
+        def acc(vid, g):
+            if vid is None or g is None:
+                return
+            if vid not in G:
+                G[vid] = g
+                return
+            if vid in owned:
+                ops.add(G[vid], g, out=G[vid])
+            else:
+                G[vid] = ops.add(G[vid], g)
+                owned.add(vid)
+
+        for k in range(len(self.ops) - 1, -1, -1):
+            op = self.ops[k]
+            gys = [G.pop(v, None) for v in op.outs]
+            if all(g is None for g in gys):
+                continue
+            gins = op.bw(self, op, gys)
+            for v, need, g in zip(op.ins, op.needs, gins):
+                if need:
+                    acc(v, g)
+        return {name: G.get(vid) for name, vid in self.inputs.items()}
+
+    def out_vid(self, t):
+        """value id of a recorded output (to seed the backward)"""
+        return self.ptr2vid[t.data_ptr()]
+
+    def st(self, vid) -> Store:
+        return self.stores[vid]
+
+
+# =============================================================================== ops
+# Each op: forward at the current frame (writes slots) + batched backward over all frames.
+
+def _flat(st: Store, width):
+    """stacked storage as [rows, width]"""
+    return st.buf.view(-1, width)
+
+
+def _empty_like_store(tape, st: Store, dtype=None):
+    return torch.empty(st.buf.numel(), device=st.buf.device, dtype=dtype or st.dtype)
+
+
+# ---------------------------------------------------------------- linear
+def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0):
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("linear", [x, residual], _linear_bw, {"mod": mod, "act": act, "p": float(drop_p)})
+    if first and tape.vid(x) is None:
+        raise RuntimeError("tape linear: input must be a recorded value or declared input")
+    w = mod.compute_weight()
+    b = mod.compute_bias()
+    N = w.shape[0]
+    scale = tape._varlen_scale(x)
+    shape = (*x.shape[:-1], N)
+    vid, out = tape._out(0, shape, x.dtype, scale)
+    pre = tape._aux("pre", shape, x.dtype, scale) if act else None
+    seed = tape._seed() if drop_p > 0 else 0
+    idx0 = tape._idx0(op, out.numel())
+    ops.linear(x, w, b, act=act, out=out, pre=pre, residual=residual, drop_p=drop_p, seed=seed, drop_idx0=idx0)
+    if first:
+        op.attrs["seed"] = seed
+        op.attrs["K"] = x.shape[-1]
+    tape._finish(op, [vid], tape._req(op, (mod.weight, mod.bias)))
+    return out
+
+
+def _linear_bw(tape, op, gys):
+    (gy,) = gys
+    mod, act, p = op.attrs["mod"], op.attrs["act"], op.attrs["p"]
+    N, K = mod.compute_weight().shape
+    gy2 = gy.view(-1, N)
+    if p > 0:
+        pre = tape.stores[("aux", op.idx, "pre")] if act else None
+        dpre = ops.act_dropout_bwd(_flat(pre, N) if act else None, gy2, act, p, op.attrs["seed"])
+    elif act:
+        pre = tape.stores[("aux", op.idx, "pre")]
+        dpre = ops.act_bwd(_flat(pre, N), gy2, act)
+    else:
+        dpre = gy2
+    x2 = _flat(tape.st(op.ins[0]), K)
+    gw, gb = mod.grad_views()
+    if gw is not None:
+        ops.linear_wgrad(dpre, x2, gw.view(gw.shape[0], -1), db=gb)
+    elif gb is not None:
+        ops.colsum(dpre, gb)
+    dx = ops.linear_dgrad(dpre, mod.compute_weight()).view(-1) if op.needs[0] else None
+    dres = gy if op.needs[1] else None
+    return [dx, dres]
+
+
+# ---------------------------------------------------------------- layer norms
+def layer_norm(tape: FrameTape, x, mod, eps, add=None):
+    """LN(x) or (LN(x + add), x + add)"""
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("ln", [x, add], _ln_bw, {"mod": mod, "eps": eps, "add": add is not None})
+    rows = x.numel() // x.shape[-1]
+    vid, y = tape._out(0, x.shape, x.dtype)
+    outs = [vid]
+    xsum = None
+    if add is not None:
+        vid2, xsum = tape._out(1, x.shape, x.dtype)
+        outs.append(vid2)
+    mean = tape._aux("mean", (rows,), torch.float32)
+    rstd = tape._aux("rstd", (rows,), torch.float32)
+    call_ln_fwd(x, mod, eps, y, mean, rstd, add, xsum)
+    tape._finish(op, outs, tape._req(op, (mod.weight, mod.bias)))
+    return (y, xsum) if add is not None else y
+
+
+def call_ln_fwd(x, mod, eps, y, mean, rstd, add, xsum):
+    from ._lib import call
+    C = x.shape[-1]
+    rows = x.numel() // C
+    call("s2h_layernorm_fwd", ops.dt(x), rows, C, ops.ptr(x), C, ops.ptr(add), C, 0, ops.ptr(xsum),
+         ops.ptr(mod.weight.detach()), ops.ptr(mod.bias.detach()), float(eps), ops.ptr(y), C, ops.ptr(mean),
+         ops.ptr(rstd), ops.stream())
+
+
+def _ln_bw(tape, op, gys):
+    gy = gys[0]
+    gxsum = gys[1] if len(gys) > 1 else None
+    mod = op.attrs["mod"]
+    k = op.idx
+    C = mod.weight.shape[0]
+    src = tape.st(op.outs[1]) if op.attrs["add"] else tape.st(op.ins[0])
+    x2 = _flat(src, C)
+    mean = tape.stores[("aux", k, "mean")].buf
+    rstd = tape.stores[("aux", k, "rstd")].buf
+    if gy is None:
+        gy = torch.zeros_like(src.buf)
+    dx = ops.layernorm_bwd(x2, gy.view(-1, C), mod.weight.detach(), mean, rstd,
+                           dres=gxsum.contiguous().view(-1, C) if gxsum is not None else None,
+                           dgamma=_grad_of(mod.weight), dbeta=_grad_of(mod.bias))
+    dx = dx.view(-1)
+    return [dx, dx if op.attrs["add"] else None]
+
+
+# ---------------------------------------------------------------- attention
+def attention(tape: FrameTape, q, k, v, scale, p_drop):
+    """q [B, Lq, H, D], k / v [B, Lk, H, D] views of recorded values (contiguous per value)"""
+    op, first = tape._begin("attn", [q, k, v], _attn_bw, {"scale": scale, "p": p_drop})
+    B, Lq, H, D = q.shape
+    Lk = k.shape[1]
+    vid, o = tape._out(0, (B, Lq, H, D), q.dtype)
+    lse = tape._aux("lse", (B, H, Lq), torch.float32)
+    seed = tape._seed() if p_drop > 0 else 0
+    idx0 = tape._idx0(op, B * H * Lq * Lk)
+    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0)
+    tape._fattr(op, "Lk", Lk)
+    if first:
+        op.attrs.update(seed=seed, B=B, Lq=Lq, H=H, D=D, qshape=tuple(q.shape))
+    tape._finish(op, [vid], any(op.needs))
+    return o
+
+
+def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_buf, dv_buf):
+    """one frame-table flash launch, or a per-frame loop of the generic kernels"""
+    a = op.attrs
+    F, B, Lq, H, D = tape.F, a["B"], a["Lq"], a["H"], a["D"]
+    lks = op.fattrs["Lk"]
+    krow = [0]
+    for f in range(F - 1):
+        krow.append(krow[-1] + B * lks[f])
+    k_rows, v_rows, dk_rows, dv_rows = kview
+    if ops.flash_bwd_eligible(q_all):
+        ops.flash_bwd_frames(F, B, lks, krow, op.fattrs["idx0"], q_all, k_rows, v_rows, o_all, go, lse, dq,
+                             dk_rows, dv_rows, a["scale"], a["p"], a["seed"])
+        return
+    for f in range(F):
+        sl = slice(f * B, (f + 1) * B)
+        r0, r1 = krow[f], krow[f] + B * lks[f]
+        ops.attn_bwd(q_all[sl], k_rows[r0:r1].view(B, lks[f], H, D), v_rows[r0:r1].view(B, lks[f], H, D), o_all[sl],
+                     go[sl], lse[sl], dq[sl], dk_rows[r0:r1].view(B, lks[f], H, D),
+                     dv_rows[r0:r1].view(B, lks[f], H, D), a["scale"], a["p"], a["seed"], idx0=op.fattrs["idx0"][f])
+
+
+def _attn_bw(tape, op, gys):
+    (go,) = gys
+    a = op.attrs
+    F, B, Lq, H, D = tape.F, a["B"], a["Lq"], a["H"], a["D"]
+    k_idx = op.idx
+    q_st, k_st, v_st = (tape.st(v) for v in op.ins)
+    q_all = q_st.buf.view(F * B, Lq, H, D)
+    o_all = tape.st(op.outs[0]).buf.view(F * B, Lq, H, D)
+    go = go.contiguous().view(F * B, Lq, H, D)
+    lse = tape.stores[("aux", k_idx, "lse")].buf.view(F * B, H, Lq)
+    dq = torch.empty_like(q_all)
+    dk = torch.empty(k_st.buf.numel(), device=go.device, dtype=go.dtype)
+    dv = torch.empty(v_st.buf.numel(), device=go.device, dtype=go.dtype)
+    rows = lambda t: t.view(-1, H, D)  # noqa: E731
+    _attn_frames_bwd(tape, op, q_all, k_st, v_st, (rows(k_st.buf), rows(v_st.buf), rows(dk), rows(dv)), o_all, go,
+                     lse, dq, dk, dv)
+    return [dq.view(-1), dk, dv]
+
+
+def qkv_attention(tape: FrameTape, qkv, scale, p_drop, rope):
+    """self-attention on a packed [B, L, 3, H, d] projection (optional RoPE on q and k)"""
+    op, first = tape._begin("qkv_attn", [qkv], _qkv_bw, {"scale": scale, "p": p_drop, "rope": rope})
+    B, L, _, H, D = qkv.shape
+    q, k, v = qkv[:, :, 0], qkv[:, :, 1], qkv[:, :, 2]
+    if rope is not None:
+        cos, sin, period = rope
+        qk = tape._aux("qk", (B, L, 2, H, D), qkv.dtype)
+        _rope_into(q, qk[:, :, 0], L, cos, sin, period)
+        _rope_into(k, qk[:, :, 1], L, cos, sin, period)
+        q, k = qk[:, :, 0], qk[:, :, 1]
+    vid, o = tape._out(0, (B, L, H, D), qkv.dtype)
+    lse = tape._aux("lse", (B, H, L), torch.float32)
+    seed = tape._seed() if p_drop > 0 else 0
+    idx0 = tape._idx0(op, B * H * L * L)
+    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0)
+    tape._fattr(op, "Lk", L)
+    if first:
+        op.attrs.update(seed=seed, B=B, Lq=L, H=H, D=D)
+    tape._finish(op, [vid], any(op.needs))
+    return o
+
+
+def _rope_into(x, y, nrot, cos, sin, period, inverse=False):
+    """rotate rows < nrot of x [B, L, H, D] (strided) into y [B, L, H, D] (strided)"""
+    from ._lib import call
+    B, L, H, D = x.shape
+    assert H == 1 or (x.stride(2) == D and y.stride(2) == D)
+    call("s2h_rope", ops.dt(x), B, int(nrot), H * D, ops.ptr(x), x.stride(0), x.stride(1), ops.ptr(y), y.stride(0),
+         y.stride(1), ops.ptr(cos), ops.ptr(sin), int(period), int(inverse), ops.stream())
+
+
+def _qkv_bw(tape, op, gys):
+    (go,) = gys
+    a = op.attrs
+    F, B, L, H, D = tape.F, a["B"], a["Lq"], a["H"], a["D"]
+    k_idx = op.idx
+    qkv_all = tape.st(op.ins[0]).buf.view(F * B, L, 3, H, D)
+    rope = a["rope"]
+    if rope is not None:
+        qk_all = tape.stores[("aux", k_idx, "qk")].buf.view(F * B, L, 2, H, D)
+        q_all, k_all = qk_all[:, :, 0], qk_all[:, :, 1]
+    else:
+        q_all, k_all = qkv_all[:, :, 0], qkv_all[:, :, 1]
+    v_all = qkv_all[:, :, 2]
+    o_all = tape.st(op.outs[0]).buf.view(F * B, L, H, D)
+    lse = tape.stores[("aux", k_idx, "lse")].buf.view(F * B, H, L)
+    dqkv = torch.empty(qkv_all.shape, device=go.device, dtype=go.dtype)
+    dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
+    go = go.contiguous().view(F * B, L, H, D)
+    def rows(t):  # [F*B, L, H, D] slice of a packed projection -> [F*B*L, H, D] rows (uniform row stride)
+        assert t.stride(0) == L * t.stride(1)
+        return torch.as_strided(t, (F * B * L, H, D), (t.stride(1), t.stride(2), 1), t.storage_offset())
+    _attn_frames_bwd(tape, op, q_all, None, None, (rows(k_all), rows(v_all), rows(dk), rows(dv)), o_all, go, lse,
+                     dq, None, None)
+    if rope is not None:
+        cos, sin, period = rope
+        for g in (dq, dk):
+            _rope_into(g, g, L, cos, sin, period, inverse=True)
+    return [dqkv.view(-1)]
+
+
+# ---------------------------------------------------------------- RoPE
+def rope(tape: FrameTape, x, nrot, cos, sin, period):
+    """x [Bt, L, D]: rotate rows < nrot (per frame: the memory rows of the frame), copy the rest"""
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("rope", [x], _rope_bw, {"cos": cos, "sin": sin, "period": period})
+    scale = tape._varlen_scale(x)
+    vid, y = tape._out(0, x.shape, x.dtype, scale)
+    if nrot < x.shape[1]:
+        y[:, nrot:].copy_(x[:, nrot:])
+    ops.rope(x, y, nrot, cos, sin, period)
+    tape._fattr(op, "nrot", int(nrot))
+    tape._fattr(op, "shape", tuple(x.shape))
+    tape._finish(op, [vid], any(op.needs))
+    return y
+
+
+def _rope_bw(tape, op, gys):
+    (gy,) = gys
+    a = op.attrs
+    out_st = tape.st(op.outs[0])
+    dx = torch.empty_like(gy)
+    shapes, nrots = op.fattrs["shape"], op.fattrs["nrot"]
+    if out_st.uniform and len(set(nrots)) == 1:
+        Bt, L, D = shapes[0]
+        g3 = gy.view(-1, L, D)
+        d3 = dx.view(-1, L, D)
+        if nrots[0] < L:
+            d3[:, nrots[0]:].copy_(g3[:, nrots[0]:])
+        ops.rope(g3, d3, nrots[0], a["cos"], a["sin"], a["period"], inverse=True)
+        return [dx]
+    for f in range(tape.F):
+        o, n = out_st.offsets[f], out_st.numels[f]
+        g3 = gy[o:o + n].view(shapes[f])
+        d3 = dx[o:o + n].view(shapes[f])
+        nr = nrots[f]
+        if nr < shapes[f][1]:
+            d3[:, nr:].copy_(g3[:, nr:])
+        ops.rope(g3, d3, nr, a["cos"], a["sin"], a["period"], inverse=True)
+    return [dx]
+
+
+# ---------------------------------------------------------------- elementwise
+def add(tape: FrameTape, a, b, alpha, beta):
+    a = a if a.is_contiguous() else a.contiguous()
+    b = b if b.is_contiguous() else b.contiguous()
+    op, first = tape._begin("add", [a, b], _add_bw, {"alpha": alpha, "beta": beta})
+    scale = tape._varlen_scale(a, b)
+    vid, out = tape._out(0, a.shape, a.dtype, scale)
+    ops.add(a, b, out=out, alpha=alpha, beta=beta)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _scaled(g, s):
+    return g if s == 1.0 else ops.add(g, None, alpha=s)
+
+
+def _add_bw(tape, op, gys):
+    (g,) = gys
+    return [_scaled(g, op.attrs["alpha"]) if op.needs[0] else None,
+            _scaled(g, op.attrs["beta"]) if op.needs[1] else None]
+
+
+def add_bcast(tape: FrameTape, a, b, alpha, beta, shape, bparam):
+    """out[o, ...] = alpha a[o, ...] + beta b[...]; b is a constant table, a parameter's compute
+    copy (bparam) or a recorded value (the memory positional table)"""
+    a = a if (a is None or a.is_contiguous()) else a.contiguous()
+    b = b.contiguous()
+    op, first = tape._begin("add_bcast", [a, b], _add_bcast_bw, {"alpha": alpha, "beta": beta, "bparam": bparam})
+    scale = tape._varlen_scale(a, b)
+    oshape = a.shape if a is not None else shape
+    vid, out = tape._out(0, oshape, b.dtype, scale)
+    ops.add_bcast(a, b, out=out, alpha=alpha, beta=beta)
+    tape._fattr(op, "inner", b.numel())
+    tape._fattr(op, "outer", out.numel() // b.numel())
+    tape._finish(op, [vid], tape._req(op, (bparam,)))
+    return out
+
+
+def _add_bcast_bw(tape, op, gys):
+    (g,) = gys
+    a = op.attrs
+    da = _scaled(g, a["alpha"]) if op.needs[0] else None
+    db = None
+    inners, outers = op.fattrs["inner"], op.fattrs["outer"]
+    if a["bparam"] is not None:
+        gb = _grad_of(a["bparam"])
+        if gb is not None:
+            inner = inners[0]
+            tmp = None
+            if a["beta"] != 1.0:
+                tmp = torch.zeros(inner, device=g.device, dtype=torch.float32)
+                ops.colsum(g.view(-1, inner), tmp)
+                ops.add(gb.view(-1), tmp, beta=a["beta"], out=gb.view(-1))
+            else:
+                ops.colsum(g.view(-1, inner), gb.view(-1), accumulate=True)
+    elif op.needs[1]:
+        bst = tape.st(op.ins[1])
+        db = torch.empty(bst.buf.numel(), device=g.device, dtype=g.dtype)
+        go = 0
+        for f in range(tape.F):
+            n_in, n_out = inners[f], inners[f] * outers[f]
+            ops.sum_outer(g[go:go + n_out].view(outers[f], n_in), db[bst.offsets[f]:bst.offsets[f] + n_in])
+            go += n_out
+        if a["beta"] != 1.0:
+            db = ops.add(db, None, alpha=a["beta"])
+    return [da, db]
+
+
+def act(tape: FrameTape, x, a):
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("act", [x], _act_bw, {"act": a})
+    vid, out = tape._out(0, x.shape, x.dtype)
+    ops.act_fwd(x, a, out=out)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _act_bw(tape, op, gys):
+    (g,) = gys
+    return [ops.act_bwd(tape.st(op.ins[0]).buf, g.contiguous().view(-1), op.attrs["act"])]
+
+
+def cast(tape: FrameTape, x, dtype):
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("cast", [x], _cast_bw, {"src": x.dtype})
+    vid, out = tape._out(0, x.shape, dtype)
+    ops.cast(x, dtype, out=out)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _cast_bw(tape, op, gys):
+    (g,) = gys
+    return [ops.cast(g.contiguous().view(-1), op.attrs["src"])]
+
+
+def expand_batch(tape: FrameTape, x, O):
+    """[1, ...] -> [O, ...] materialised broadcast (grad = sum over O)"""
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("expand", [x], _expand_bw, {"O": O})
+    vid, out = tape._out(0, (O, *x.shape[1:]), x.dtype)
+    ops.add_bcast(None, x, out=out)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _expand_bw(tape, op, gys):
+    (g,) = gys
+    O = op.attrs["O"]
+    inner = tape.st(op.ins[0]).numels[0]
+    d = torch.empty(tape.F * inner, device=g.device, dtype=g.dtype)
+    g3 = g.view(tape.F, O, inner)
+    for f in range(tape.F):
+        ops.sum_outer(g3[f], d[f * inner:(f + 1) * inner])
+    return [d]
+
+
+def row_gate(tape: FrameTape, x, gate, fill):
+    """x[r] if gate[r] > 0 else fill; gate [R] f32 per-frame constant (no gradient)"""
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("row_gate", [x], _row_gate_bw, {"fill": fill})
+    vid, out = tape._out(0, x.shape, x.dtype)
+    gsave = tape._aux("gate", gate.shape, gate.dtype)
+    gsave.copy_(gate)
+    ops.row_gate(x, gate, fill, out=out)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _row_gate_bw(tape, op, gys):
+    (g,) = gys
+    gate = tape.stores[("aux", op.idx, "gate")].buf
+    R = gate.numel()
+    return [ops.row_gate(g.contiguous().view(R, -1), gate, 0.0, backward=True).view(-1)]
+
+
+def bilinear(tape: FrameTape, x, ho, wo):
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("bilinear", [x], _bilinear_bw, {"hw": tuple(x.shape[-2:])})
+    vid, out = tape._out(0, (*x.shape[:-2], ho, wo), x.dtype)
+    ops.bilinear(x, ho, wo, out=out)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _bilinear_bw(tape, op, gys):
+    (g,) = gys
+    hi, wi = op.attrs["hw"]
+    out_shape = tape.st(op.outs[0]).shape0
+    g3 = g.contiguous().view(-1, out_shape[-2], out_shape[-1])
+    return [ops.bilinear_bwd(g3, hi, wi).view(-1)]
+
+
+def select_token(tape: FrameTape, x, i):
+    """x [B, N, C] -> x[:, i] (contiguous copy)"""
+    op, first = tape._begin("select", [x], _select_bw, {"i": i, "shape": tuple(x.shape)})
+    B, N, C = x.shape
+    vid, out = tape._out(0, (B, C), x.dtype)
+    out.copy_(x[:, i])
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _select_bw(tape, op, gys):
+    (g,) = gys
+    B, N, C = op.attrs["shape"]
+    d = torch.zeros(tape.F * B, N, C, device=g.device, dtype=g.dtype)
+    d[:, op.attrs["i"]].copy_(g.view(tape.F * B, C))
+    return [d.view(-1)]
+
+
+# ---------------------------------------------------------------- SAM pieces
+def conv_transpose2x2(tape: FrameTape, x, mod, add=None):
+    """ConvTranspose2d(2, 2) + bias (+ add broadcast over the batch when it has batch 1)"""
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("convt", [x, add], _convt_bw, {"mod": mod})
+    B, H, W, Ci = x.shape
+    Co = mod.out_ch
+    w = mod.compute_weight()
+    Y = tape._aux("Y", (B * H * W, 4 * Co), x.dtype)
+    ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
+             ldc=4 * Co)
+    vid, out = tape._out(0, (B, 2 * H, 2 * W, Co), x.dtype)
+    ops.convt2_scatter(Y, B, H, W, Co, bias=mod.bias.detach(), add=None, out=out)
+    if add is not None:
+        add = add.contiguous()
+        if add.shape[0] == B:
+            ops.add(out, add, out=out)
+        else:
+            ops.add_bcast(out, add, out=out)
+    if first:
+        op.attrs.update(B=B, H=H, W=W, Ci=Ci, Co=Co, bcast=add is not None and add.shape[0] != B)
+    tape._finish(op, [vid], tape._req(op, (mod.weight, mod.bias)))
+    return out
+
+
+def _convt_bw(tape, op, gys):
+    (g,) = gys
+    a = op.attrs
+    mod, F = a["mod"], tape.F
+    B, H, W, Ci, Co = a["B"], a["H"], a["W"], a["Ci"], a["Co"]
+    g = g.contiguous()
+    dY = ops.convt2_gather(g.view(F * B, 2 * H, 2 * W, Co), F * B, H, W, Co)
+    gw, gb = _grad_of(mod.weight), _grad_of(mod.bias)
+    x2 = _flat(tape.st(op.ins[0]), Ci)
+    R = F * B * H * W
+    if gw is not None:
+        ops.gemm(x2, dY, gw.view(Ci, 4 * Co), M=Ci, N=4 * Co, K=R, lda_m=1, lda_k=Ci, ldb_k=4 * Co, ldb_n=1,
+                 ldc=4 * Co, beta=1.0)
+    if gb is not None:
+        ops.colsum(g.view(-1, Co), gb)
+    dx = None
+    if op.needs[0]:
+        dx = torch.empty(R * Ci, device=g.device, dtype=g.dtype)
+        ops.gemm(dY, mod.compute_weight(), dx.view(R, Ci), M=R, N=Ci, K=4 * Co, lda_m=4 * Co, lda_k=1, ldb_k=1,
+                 ldb_n=4 * Co, ldc=Ci)
+    dadd = None
+    if op.needs[1]:
+        if a["bcast"]:
+            inner = 4 * H * W * Co
+            dadd = torch.empty(F * inner, device=g.device, dtype=g.dtype)
+            g3 = g.view(F, B, inner)
+            for f in range(F):
+                ops.sum_outer(g3[f], dadd[f * inner:(f + 1) * inner])
+        else:
+            dadd = g.view(-1)
+    return [dx, dadd]
+
+
+def hyper_mask(tape: FrameTape, hyper, up):
+    """masks[o, p] = sum_c hyper[o, c] up[o, p, c]"""
+    hyper = hyper if hyper.is_contiguous() else hyper.contiguous()
+    op, first = tape._begin("hyper", [hyper, up], _hyper_bw, {})
+    O, P, C = up.shape
+    vid, out = tape._out(0, (O, P), up.dtype)
+    ops.bmm(hyper.view(O, 1, C), up, out.view(O, 1, P), trans_b=True)
+    if first:
+        op.attrs.update(O=O, P=P, C=C)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _hyper_bw(tape, op, gys):
+    (g,) = gys
+    F, O, P, C = tape.F, op.attrs["O"], op.attrs["P"], op.attrs["C"]
+    h3 = tape.st(op.ins[0]).buf.view(F * O, 1, C)
+    up = tape.st(op.ins[1]).buf.view(F * O, P, C)
+    g3 = g.contiguous().view(F * O, 1, P)
+    dh = dup = None
+    if op.needs[0]:
+        dh32 = torch.empty(F * O, 1, C, device=g.device, dtype=torch.float32)
+        ops.bmm(g3, up, dh32)
+        dh = ops.cast(dh32, up.dtype).view(-1)
+    if op.needs[1]:
+        dup = torch.empty(F * O, P, C, device=g.device, dtype=up.dtype)
+        ops.gemm(g3, h3, dup, M=P, N=C, K=1, lda_m=1, lda_k=P, ldb_k=C, ldb_n=1, ldc=C, batch=F * O, sA=P, sB=C,
+                 sC=P * C)
+        dup = dup.view(-1)
+    return [dh, dup]
+
+
+def point_embed(tape: FrameTape, pe, labels, dtype, tables):
+    """PromptEncoder point embeddings (per-frame constant clicks + learned label embeddings)"""
+    op, first = tape._begin("point_embed", [], _point_embed_bw, {"tables": tables})
+    R, D = pe.shape[0] * pe.shape[1], pe.shape[2]
+    table = torch.cat([p._s2h_compute.reshape(1, -1) for p in tables], 0).contiguous() if first else \
+        op.attrs["table"]
+    vid, out = tape._out(0, pe.shape, dtype)
+    ops.point_embed(pe.reshape(R, D), labels.reshape(R), table, out.view(R, D))
+    lab = tape._aux("labels", (R,), labels.dtype)
+    lab.copy_(labels.reshape(R))
+    if first:
+        op.attrs["table"] = table
+        op.attrs["D"] = D
+    tape._finish(op, [vid], any(_grad_of(p) is not None for p in tables))
+    return out
+
+
+def _point_embed_bw(tape, op, gys):
+    (g,) = gys
+    D = op.attrs["D"]
+    labels = tape.stores[("aux", op.idx, "labels")].buf
+    dtable = torch.zeros(len(op.attrs["tables"]), D, device=g.device)
+    ops.point_embed_bwd(labels, g.contiguous().view(-1, D), dtable)
+    for i, p in enumerate(op.attrs["tables"]):
+        gp = _grad_of(p)
+        if gp is not None:
+            ops.add(gp.view(-1), dtable[i], out=gp.view(-1))
+    return []
+
+
+def decoder_tokens(tape: FrameTape, sparse, dtype, params):
+    """cat(obj_score_token, iou_token, mask_tokens) over objects + the sparse prompt rows"""
+    op, first = tape._begin("tokens", [sparse], _tokens_bw, {"params": params})
+    O, Ns, C = sparse.shape
+    head = torch.cat([p._s2h_compute.reshape(-1, C) for p in params], 0) if first else op.attrs["head"]
+    nh = head.shape[0]
+    vid, out = tape._out(0, (O, nh + Ns, C), dtype)
+    out[:, :nh].copy_(head.unsqueeze(0).expand(O, -1, -1))
+    out[:, nh:].copy_(sparse)
+    if first:
+        op.attrs.update(head=head, nh=nh, Ns=Ns, C=C, O=O)
+    tape._finish(op, [vid], any(op.needs) or any(_grad_of(p) is not None for p in params))
+    return out
+
+
+def _tokens_bw(tape, op, gys):
+    (g,) = gys
+    a = op.attrs
+    F, O, nh, Ns, C = tape.F, a["O"], a["nh"], a["Ns"], a["C"]
+    g3 = g.contiguous().view(F * O, nh + Ns, C)
+    r = 0
+    for p in a["params"]:
+        gp = _grad_of(p)
+        n = p.numel() // C
+        if gp is not None:
+            for j in range(n):
+                ops.colsum(g3[:, r + j], gp.view(-1, C)[j], accumulate=True)
+        r += n
+    dsp = g3[:, nh:].contiguous().view(-1) if op.needs[0] else None
+    return [dsp]
+
+
+def memory_pos(tape: FrameTape, tpos_p, obj_pos, spatial_pos, tpos_idx, L, dtype):
+    """memory positional table of this frame (sam2_base.py:597-674): spatial pos +
+    maskmem_tpos_enc[tpos_idx[j]] per memory slot, then the object-pointer rows (constant)"""
+    op, first = tape._begin("memory_pos", [], _mpos_bw, {"tpos_p": tpos_p, "L": L})
+    n = len(tpos_idx)
+    Dm = spatial_pos.shape[-1]
+    M = n * L + (obj_pos.shape[0] if obj_pos is not None else 0)
+    tpos = tpos_p._s2h_compute.reshape(-1, Dm)
+    if tpos.dtype != dtype:
+        tpos = ops.cast(tpos.contiguous(), dtype)
+    vid, out = tape._out(0, (M, Dm), dtype, tape.mem_rows)
+    for j, ti in enumerate(tpos_idx):
+        ops.add_bcast(spatial_pos, tpos[ti], out=out[j * L:(j + 1) * L])
+    if obj_pos is not None:
+        out[n * L:].copy_(obj_pos)
+    tape._fattr(op, "tpos_idx", list(tpos_idx))
+    tape._finish(op, [vid], _grad_of(tpos_p) is not None)
+    return out
+
+
+def _mpos_bw(tape, op, gys):
+    (g,) = gys
+    gt = _grad_of(op.attrs["tpos_p"])
+    if gt is None:
+        return []
+    st = tape.st(op.outs[0])
+    L = op.attrs["L"]
+    Dm = st.shape0[-1]
+    gt2 = gt.view(-1, Dm)
+    for f in range(tape.F):
+        gf = g[st.offsets[f]:st.offsets[f] + st.numels[f]].view(-1, Dm)
+        for j, ti in enumerate(op.fattrs["tpos_idx"][f]):
+            ops.colsum(gf[j * L:(j + 1) * L], gt2[ti], accumulate=True)
+    return []

@@ -16,6 +16,7 @@ import math
 
 import torch
 
+from . import frametape as _ft
 from . import ops
 
 _SEED = [0x5EED]
@@ -74,6 +75,9 @@ class _Linear(torch.autograd.Function):
 def linear(x, mod, act=None, residual=None, drop_p=0.0):
     """drop(act(x @ W^T + b)) (+ residual).  `mod` provides compute_weight(), compute_bias(),
     grad_views() and `weight`/`bias` anchors (Parameters) for the autograd tape."""
+    T = _ft.active()
+    if T is not None:
+        return _ft.linear(T, x, mod, act, residual, float(drop_p))
     return _Linear.apply(x.contiguous(), mod.weight, mod.bias, mod, act, residual, float(drop_p))
 
 
@@ -112,11 +116,17 @@ class _LayerNorm(torch.autograd.Function):
 
 
 def layer_norm(x, mod, eps):
+    T = _ft.active()
+    if T is not None:
+        return _ft.layer_norm(T, x, mod, eps)
     return _LayerNorm.apply(x.contiguous(), mod.weight, mod.bias, mod, eps, None, False)
 
 
 def add_layer_norm(x, add, mod, eps):
     """returns (LN(x + add), x + add) -- fused residual add + norm"""
+    T = _ft.active()
+    if T is not None:
+        return _ft.layer_norm(T, x, mod, eps, add=add if add.is_contiguous() else add.contiguous())
     return _LayerNorm.apply(x.contiguous(), mod.weight, mod.bias, mod, eps, add.contiguous(), False)
 
 
@@ -148,6 +158,9 @@ def attention(q, k, v, scale=None, p_drop=0.0):
     """softmax(scale q k^T) v over [B, L, H, D] views (head dim contiguous)."""
     if scale is None:
         scale = 1.0 / math.sqrt(q.shape[-1])
+    T = _ft.active()
+    if T is not None:
+        return _ft.attention(T, q, k, v, float(scale), float(p_drop))
     return _Attention.apply(q, k, v, float(scale), float(p_drop))
 
 
@@ -200,6 +213,9 @@ def qkv_attention(qkv, scale=None, p_drop=0.0, rope=None):
     period) rotates q and k (every row) first."""
     if scale is None:
         scale = 1.0 / math.sqrt(qkv.shape[-1])
+    T = _ft.active()
+    if T is not None:
+        return _ft.qkv_attention(T, qkv, float(scale), float(p_drop), rope)
     return _QKVAttention.apply(qkv, float(scale), float(p_drop), rope)
 
 
@@ -228,6 +244,9 @@ class _Rope(torch.autograd.Function):
 
 
 def rope(x, nrot, cos, sin, period):
+    T = _ft.active()
+    if T is not None:
+        return _ft.rope(T, x, int(nrot), cos, sin, int(period))
     return _Rope.apply(x.contiguous(), int(nrot), cos, sin, int(period))
 
 
@@ -247,6 +266,9 @@ class _Add(torch.autograd.Function):
 
 
 def add(a, b, alpha=1.0, beta=1.0):
+    T = _ft.active()
+    if T is not None:
+        return _ft.add(T, a, b, float(alpha), float(beta))
     return _Add.apply(a, b, float(alpha), float(beta))
 
 
@@ -290,6 +312,9 @@ class _AddBcast(torch.autograd.Function):
 def add_bcast(a, b, alpha=1.0, beta=1.0, shape=None, bparam=None):
     """a + beta*b with b broadcast over leading dims.  If `bparam` (a Parameter) is given,
     b is its compute copy and its gradient goes to the arena."""
+    T = _ft.active()
+    if T is not None:
+        return _ft.add_bcast(T, a, b, float(alpha), float(beta), shape, bparam)
     return _AddBcast.apply(a, b, float(alpha), float(beta), shape, bparam)
 
 
@@ -307,6 +332,9 @@ class _Act(torch.autograd.Function):
 
 
 def act(x, a):
+    T = _ft.active()
+    if T is not None:
+        return _ft.act(T, x, a)
     return _Act.apply(x, a)
 
 
@@ -411,6 +439,9 @@ class _Bilinear(torch.autograd.Function):
 
 def bilinear(x, ho, wo):
     """[N, hi, wi] f32 -> [N, ho, wo] bilinear (align_corners=False)"""
+    T = _ft.active()
+    if T is not None:
+        return _ft.bilinear(T, x, int(ho), int(wo))
     return _Bilinear.apply(x, int(ho), int(wo))
 
 
@@ -428,6 +459,9 @@ class _RowGate(torch.autograd.Function):
 
 def row_gate(x, gate, fill):
     """x[r] if gate[r] > 0 else fill (gate is a non-differentiable f32 [R])"""
+    T = _ft.active()
+    if T is not None:
+        return _ft.row_gate(T, x, gate, float(fill))
     return _RowGate.apply(x, gate, float(fill))
 
 
@@ -445,6 +479,9 @@ class _Cast(torch.autograd.Function):
 def cast(x, dtype):
     if x.dtype == dtype:
         return x
+    T = _ft.active()
+    if T is not None:
+        return _ft.cast(T, x, dtype)
     return _Cast.apply(x, dtype)
 
 
@@ -467,4 +504,28 @@ class _SumOuter(torch.autograd.Function):
 
 def expand_batch(x, O):
     """[1, ...] -> [O, ...] materialised broadcast (grad = sum over O)"""
+    T = _ft.active()
+    if T is not None:
+        return _ft.expand_batch(T, x, int(O))
     return _SumOuter.apply(x, int(O))
+
+
+class _SelectToken(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, i):
+        ctx.shape, ctx.i = x.shape, i
+        return x[:, i].contiguous()
+
+    @staticmethod
+    def backward(ctx, g):
+        d = torch.zeros(ctx.shape, device=g.device, dtype=g.dtype)
+        d[:, ctx.i].copy_(g)
+        return d, None
+
+
+def select_token(x, i):
+    """x [B, N, C] -> x[:, i] as a contiguous [B, C] (the decoder's output-token reads)"""
+    T = _ft.active()
+    if T is not None:
+        return _ft.select_token(T, x, int(i))
+    return _SelectToken.apply(x, int(i))

@@ -10,6 +10,7 @@ from functools import lru_cache
 import numpy as np
 import torch
 
+from . import frametape as _ft
 from . import ops
 from .functional import _grad_of
 
@@ -196,6 +197,9 @@ class _ConvT2(torch.autograd.Function):
 
 
 def conv_transpose2x2(x, mod, add=None):
+    T = _ft.active()
+    if T is not None:
+        return _ft.conv_transpose2x2(T, x, mod, add)
     return _ConvT2.apply(x, mod.weight, mod.bias, mod, add)
 
 
@@ -233,6 +237,9 @@ class _HyperMask(torch.autograd.Function):
 
 
 def hyper_mask(hyper, up):
+    T = _ft.active()
+    if T is not None:
+        return _ft.hyper_mask(T, hyper, up)
     return _HyperMask.apply(hyper, up)
 
 
@@ -269,6 +276,9 @@ class _PointEmbed(torch.autograd.Function):
 
 def point_embed(pe, labels, dtype, not_a_point, point_embeddings):
     tabs = [not_a_point.weight] + [e.weight for e in point_embeddings]
+    T = _ft.active()
+    if T is not None:
+        return _ft.point_embed(T, pe, labels, dtype, tabs)
     return _PointEmbed.apply(pe, labels, dtype, *tabs)
 
 
@@ -310,6 +320,9 @@ class _MemoryPos(torch.autograd.Function):
 
 
 def memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype):
+    T = _ft.active()
+    if T is not None:
+        return _ft.memory_pos(T, tpos_param, obj_pos, spatial_pos, list(tpos_idx), int(L), dtype)
     return _MemoryPos.apply(tpos_param, obj_pos, spatial_pos, list(tpos_idx), int(L), dtype)
 
 

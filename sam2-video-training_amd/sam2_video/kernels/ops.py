@@ -59,14 +59,15 @@ def rng_offset(device):
 # ----------------------------------------------------------------- GEMM
 def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB=0, sC=0,
          bias=None, bias_mode=1, residual=None, ldr=0, sR=0, aux=None, ldx=0, sX=0, aux_mode=0,
-         cscale=None, drop_p=0.0, seed=0, alpha=1.0, beta=0.0, act=0):
+         cscale=None, drop_p=0.0, seed=0, alpha=1.0, beta=0.0, act=0, drop_idx0=0):
     _dev(a, b, c, bias, residual, aux)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
     call("s2h_gemm", dt(a), dt(c), batch, M, N, K,
          ptr(a), lda_m, lda_k, sA, ptr(b), ldb_k, ldb_n, sB, ptr(c), ldc, sC,
          ptr(bias), bias_mode, ptr(residual), ldr, sR, ptr(aux), ldx, sX, aux_mode,
-         ptr(cscale), float(drop_p), int(seed) & (2**64 - 1), float(alpha), float(beta), int(act), stream())
+         ptr(cscale), float(drop_p), int(seed) & (2**64 - 1), int(drop_idx0), float(alpha), float(beta), int(act),
+         stream())
     return c
 
 
@@ -76,7 +77,7 @@ def _rows(x):
 
 
 def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dtype=None, cscale=None,
-           drop_p=0.0, seed=0):
+           drop_p=0.0, seed=0, drop_idx0=0):
     """out = drop(act(x @ w^T + bias) * cscale) (+ residual); optionally stores the pre-activation in `pre`."""
     x2 = x.reshape(-1, x.shape[-1])
     M, K = x2.shape
@@ -89,7 +90,7 @@ def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dty
     p2 = pre.view(-1, N) if pre is not None else None
     gemm(x2, w, o2, M=M, N=N, K=K, lda_m=x2.stride(0), lda_k=1, ldb_k=1, ldb_n=K, ldc=N,
          bias=bias, residual=r2, ldr=N, aux=p2, ldx=N, aux_mode=1 if pre is not None else 0, act=ACT[act],
-         cscale=cscale, drop_p=drop_p, seed=seed)
+         cscale=cscale, drop_p=drop_p, seed=seed, drop_idx0=drop_idx0)
     return out
 
 
@@ -145,7 +146,7 @@ def _bhl(t):
     return t.stride(0), t.stride(2), t.stride(1)
 
 
-def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0):
+def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0, idx0=0):
     """q [B, Lq, H, D], k/v [B, Lk, H, D] (any strides, D contiguous) -> o [B, Lq, H, D], lse [B, H, Lq] f32"""
     _dev(q, k, v, o, lse)
     B, Lq, H, D = q.shape
@@ -153,12 +154,12 @@ def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0):
     nws = lib().s2h_attn_fwd_ws_bytes(dt(q), B, H, Lq, Lk, D)
     ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
     call("s2h_attn_fwd", dt(q), B, H, Lq, Lk, D, ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v),
-         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), ptr(ws), int(nws),
-         stream())
+         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0), ptr(ws),
+         int(nws), stream())
     return o, lse
 
 
-def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0):
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0, idx0=0):
     _dev(q, k, v, o, do, lse, dq, dk, dv)
     B, Lq, H, D = q.shape
     Lk = k.shape[1]
@@ -168,7 +169,38 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0):
     call("s2h_attn_bwd", dt(q), B, H, Lq, Lk, D,
          ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
          ptr(dq), *_bhl(dq), ptr(dk), *_bhl(dk), ptr(dv), *_bhl(dv),
-         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), ptr(ws), int(nws), stream())
+         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0), ptr(ws), int(nws),
+         stream())
+    return dq, dk, dv
+
+
+def flash_bwd_eligible(q):
+    """the frame-batched flash backward's domain (bf16, head_dim 128 / 256, >= 128 query rows,
+    flash path enabled): q [B, Lq, H, D]"""
+    return bool(lib().s2h_flash_bwd_ok(dt(q), q.shape[1], q.shape[-1]))
+
+
+def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, scale, p_drop, seed):
+    """Frame-batched flash backward (s2h_flash_bwd_frames): q/o/do/dq [nfr*bpf, Lq, H, D] views,
+    k/v/dk/dv PACKED [rows, H, D] views (frame f: bpf blocks of lk[f] rows from row krow[f]),
+    lse [nfr*bpf, H, Lq]; frame f's dropout indices start at idx0[f]."""
+    import ctypes
+    _dev(q, k, v, o, do, lse, dq, dk, dv)
+    B, Lq, H, D = q.shape
+    assert B == nfr * bpf and len(lk) == nfr == len(krow) == len(idx0)
+    di = torch.empty(B * H * Lq, device=q.device, dtype=torch.float32)
+    alk = (ctypes.c_int * nfr)(*[int(x) for x in lk])
+    akr = (ctypes.c_int64 * nfr)(*[int(x) for x in krow])
+    aix = (ctypes.c_uint64 * nfr)(*[int(x) & (2**64 - 1) for x in idx0])
+
+    def hl(t):  # (head, row) strides of a packed [rows, H, D] view
+        assert t.stride(-1) == 1
+        return t.stride(1), t.stride(0)
+    call("s2h_flash_bwd_frames", nfr, bpf, H, Lq, D, ctypes.cast(alk, ctypes.c_void_p).value,
+         ctypes.cast(akr, ctypes.c_void_p).value, ctypes.cast(aix, ctypes.c_void_p).value,
+         ptr(q), *_bhl(q), ptr(k), *hl(k), ptr(v), *hl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
+         ptr(dq), *_bhl(dq), ptr(dk), *hl(dk), ptr(dv), *hl(dv), ptr(lse), ptr(di), float(scale), float(p_drop),
+         int(seed) & (2**64 - 1), stream())
     return dq, dk, dv
 
 
@@ -230,12 +262,12 @@ def act_fwd(x, act, out=None, scale=1.0, shift=0.0):
     return out
 
 
-def act_dropout_bwd(x_pre, dy, act, p, seed, dx=None):
+def act_dropout_bwd(x_pre, dy, act, p, seed, dx=None, idx0=0):
     """dx = act'(x_pre) * dropout_mask(seed) / (1 - p) * dy (one pass; x_pre None = no act)"""
     if dx is None:
         dx = torch.empty_like(dy)
     call("s2h_act_dropout_bwd", dt(dy), dy.numel(), ptr(x_pre), ptr(dy), ACT[act], float(p), int(seed) & (2**64 - 1),
-         ptr(dx), stream())
+         int(idx0), ptr(dx), stream())
     return dx
 
 
@@ -253,11 +285,12 @@ def cast(x, dtype, out=None):
     return out
 
 
-def dropout(b, p, seed, a=None, out=None):
+def dropout(b, p, seed, a=None, out=None, idx0=0):
     """out = (a +) keep*b/(1-p) with the counter-hash mask of (seed, flat index)"""
     if out is None:
         out = torch.empty_like(b)
-    call("s2h_dropout", dt(b), b.numel(), ptr(a), ptr(b), float(p), int(seed) & (2**64 - 1), ptr(out), stream())
+    call("s2h_dropout", dt(b), b.numel(), ptr(a), ptr(b), float(p), int(seed) & (2**64 - 1), int(idx0), ptr(out),
+         stream())
     return out
 
 

@@ -13,6 +13,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from ....kernels import frametape as _ft
 from ....kernels import functional as FN
 from ....kernels import ops
 from ....kernels.functional_sam import conv_transpose2x2, hyper_mask
@@ -87,15 +88,17 @@ class MaskDecoder(nn.Module):
         O = image_embeddings.shape[0]
         C = self.transformer_dim
         dt = image_embeddings.dtype
-        tokens = _DecoderTokens.apply(sparse, dt, self.obj_score_token.weight, self.iou_token.weight,
-                                      self.mask_tokens.weight)
+        tparams = (self.obj_score_token.weight, self.iou_token.weight, self.mask_tokens.weight)
+        T = _ft.active()
+        tokens = (_ft.decoder_tokens(T, sparse, dt, tparams) if T is not None
+                  else _DecoderTokens.apply(sparse, dt, *tparams))
         if dense is None:  # no mask prompt: the no_mask_embed broadcast (prompt_encoder.py:196-200)
             src = FN.add_bcast(image_embeddings, no_mask_embed.weight._s2h_compute.view(-1), bparam=no_mask_embed.weight)
         else:  # mask-prompt dense embedding [O, h*w, C]
             src = FN.add(image_embeddings, dense)
         hs, src = self.transformer(src, image_pe_table, tokens)
-        iou_token_out = hs[:, 1].contiguous()
-        mask_token0 = hs[:, 2].contiguous()
+        iou_token_out = FN.select_token(hs, 1)
+        mask_token0 = FN.select_token(hs, 2)
         feat_s0, feat_s1 = high_res_features
         dc1, ln1, _, dc2, _ = self.output_upscaling
         u = conv_transpose2x2(src.view(O, h, w, C), dc1, add=feat_s1)
@@ -105,7 +108,7 @@ class MaskDecoder(nn.Module):
         hyper0 = self.output_hypernetworks_mlps[0](mask_token0)
         masks = hyper_mask(hyper0, u.view(O, -1, C // 8))
         iou_pred = self.iou_prediction_head(iou_token_out)
-        iou0 = FN.cast(iou_pred[:, 0:1].contiguous(), torch.float32)
+        iou0 = FN.cast(FN.select_token(iou_pred.unsqueeze(-1), 0), torch.float32)
         with torch.no_grad():
             score = self.pred_obj_score_head(hs[:, 0].detach().contiguous())
             score = ops.cast(score, torch.float32) if score.dtype != torch.float32 else score

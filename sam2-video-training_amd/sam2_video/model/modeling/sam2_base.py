@@ -170,52 +170,82 @@ class SAM2Base(nn.Module):
         op = self.obj_ptr_tpos_proj(pe)  # [n_ptr, mem_dim]
         return op.repeat_interleave(self.hidden_dim // self.mem_dim, dim=0)
 
+    def _memory_selection(self, frame_idx, num_frames, cond_keys, non_cond_keys, track_in_reverse=False):
+        """which bank entries frame `frame_idx` attends to (sam2_base.py:549-647, training order):
+        [(t_pos, frame)] spatial memories (conditioning frame first, then t-1, t-2, ...) and
+        [(pos, frame)] object pointers -- frame ids only, so the row count of every frame's memory
+        is known before the loop runs (the frame-batched backward packs by it)"""
+        assert len(cond_keys) > 0 and self.max_cond_frames_in_attn == -1
+        mems = [(0, t) for t in cond_keys]
+        stride = 1 if self.training else self.memory_temporal_stride_for_eval
+        for t_pos in range(1, self.num_maskmem):
+            t_rel = self.num_maskmem - t_pos
+            if t_rel == 1:
+                prev = frame_idx - t_rel if not track_in_reverse else frame_idx + t_rel
+            elif not track_in_reverse:
+                prev = ((frame_idx - 2) // stride) * stride - (t_rel - 2) * stride
+            else:
+                prev = -(-(frame_idx + 2) // stride) * stride + (t_rel - 2) * stride
+            if prev in non_cond_keys:
+                mems.append((t_pos, prev))
+        max_ptr = min(num_frames, self.max_obj_ptrs_in_encoder)
+        sign = -1 if track_in_reverse else 1
+        ptrs = [((frame_idx - t) * sign if self.use_signed_tpos_enc_to_obj_ptrs else abs(frame_idx - t), t)
+                for t in cond_keys]
+        for t_diff in range(1, max_ptr):
+            t = frame_idx + t_diff if track_in_reverse else frame_idx - t_diff
+            if t < 0 or (num_frames is not None and t >= num_frames):
+                break
+            if t in non_cond_keys:
+                ptrs.append((t_diff, t))
+        return mems, ptrs, max_ptr
+
+    def _bank_rows(self, num_frames, L, C):
+        """memory rows M_t of frames 1..T-1 (spatial L per memory frame + C/mem_dim tokens per
+        object pointer), simulating the bank write / prune of forward_tracking"""
+        cond, non_cond, rows = [0], [], []
+        for t in range(1, num_frames):
+            mems, ptrs, _ = self._memory_selection(t, num_frames, cond, set(non_cond))
+            rows.append(len(mems) * L + len(ptrs) * (C // self.mem_dim))
+            non_cond.append(t)
+            while len(non_cond) > max(self.num_maskmem - 1, 0):
+                non_cond.pop(0)
+        return rows
+
     def _prepare_memory_conditioned_features(self, frame_idx, is_init_cond_frame, feat, pos, num_frames,
-                                             output_dict, num_objects, track_in_reverse=False):
-        """sam2_base.py:524-713 (training order).  feat/pos: [L, C] of this frame; returns [O, L, C]."""
+                                             output_dict, num_objects, track_in_reverse=False, tape=None):
+        """sam2_base.py:524-713 (training order).  feat/pos: [L, C] of this frame; returns [O, L, C].
+        With a recording `tape` the assembled memory goes into the tape's packed per-frame buffer."""
         L, C = feat.shape
         if is_init_cond_frame:
             x = FN.add_bcast(feat, self.no_mem_embed._s2h_compute.view(-1), bparam=self.no_mem_embed)
             return FN.expand_batch(x.unsqueeze(0), num_objects)
         cond = output_dict["cond_frame_outputs"]
         non_cond = output_dict["non_cond_frame_outputs"]
-        assert len(cond) > 0 and self.max_cond_frames_in_attn == -1
-        t_pos_and_prevs = [(0, out) for out in cond.values()]
-        stride = 1 if self.training else self.memory_temporal_stride_for_eval
-        for t_pos in range(1, self.num_maskmem):
-            t_rel = self.num_maskmem - t_pos
-            if t_rel == 1:
-                prev_frame_idx = frame_idx - t_rel if not track_in_reverse else frame_idx + t_rel
-            elif not track_in_reverse:
-                prev_frame_idx = ((frame_idx - 2) // stride) * stride - (t_rel - 2) * stride
-            else:
-                prev_frame_idx = -(-(frame_idx + 2) // stride) * stride + (t_rel - 2) * stride
-            t_pos_and_prevs.append((t_pos, non_cond.get(prev_frame_idx, None)))
-        feats, tpos_idx = [], []
-        spatial_pos = None
-        for t_pos, prev in t_pos_and_prevs:
-            if prev is None:
-                continue
-            feats.append(prev["maskmem_features"].reshape(num_objects, -1, self.mem_dim))
-            spatial_pos = prev["maskmem_pos_enc"]
-            tpos_idx.append(self.num_maskmem - t_pos - 1)
-        # object pointers (:613-677)
-        max_ptr = min(num_frames, self.max_obj_ptrs_in_encoder)
-        sign = -1 if track_in_reverse else 1
-        pos_and_ptrs = [((frame_idx - t) * sign if self.use_signed_tpos_enc_to_obj_ptrs else abs(frame_idx - t),
-                         out["obj_ptr"]) for t, out in cond.items()]
-        for t_diff in range(1, max_ptr):
-            t = frame_idx + t_diff if track_in_reverse else frame_idx - t_diff
-            if t < 0 or (num_frames is not None and t >= num_frames):
-                break
-            out = non_cond.get(t, None)
-            if out is not None:
-                pos_and_ptrs.append((t_diff, out["obj_ptr"]))
-        pos_list, ptrs = zip(*pos_and_ptrs)
+        mems, ptr_sel, max_ptr = self._memory_selection(frame_idx, num_frames, list(cond), set(non_cond),
+                                                        track_in_reverse)
+        bank = lambda t: cond[t] if t in cond else non_cond[t]  # noqa: E731
+        feats = [bank(t)["maskmem_features"].reshape(num_objects, -1, self.mem_dim) for _, t in mems]
+        spatial_pos = bank(mems[-1][1])["maskmem_pos_enc"]
+        tpos_idx = [self.num_maskmem - t_pos - 1 for t_pos, _ in mems]
+        pos_list = [p for p, _ in ptr_sel]
+        ptrs = [bank(t)["obj_ptr"] for _, t in ptr_sel]
         n_ptr_tok = len(ptrs) * (C // self.mem_dim)
         ptr_tokens = torch.stack(ptrs, dim=1).reshape(num_objects, n_ptr_tok, self.mem_dim)
-        obj_pos = self._obj_pos_table(list(pos_list), max_ptr, feat.dtype, feat.device)
-        memory = torch.cat(feats + [ptr_tokens], dim=1)
+        if tape is not None:
+            if self.obj_ptr_tpos_proj.weight.requires_grad:
+                raise NotImplementedError("frame-batched backward with a trainable obj_ptr_tpos_proj")
+            with torch.no_grad():
+                obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device)
+            M = sum(f.shape[1] for f in feats) + n_ptr_tok
+            memory = tape.varlen_slot("memory", (num_objects, M, self.mem_dim), feat.dtype)
+            r = 0
+            for f in feats + [ptr_tokens]:
+                memory[:, r:r + f.shape[1]].copy_(f)
+                r += f.shape[1]
+        else:
+            obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device)
+            memory = torch.cat(feats + [ptr_tokens], dim=1)
         mpos = FN_memory_pos(self.maskmem_tpos_enc, obj_pos, spatial_pos, tpos_idx, spatial_pos.shape[0], feat.dtype)
         return self.memory_attention(feat, pos, memory, mpos, num_obj_ptr_tokens=n_ptr_tok, num_objects=num_objects)
 

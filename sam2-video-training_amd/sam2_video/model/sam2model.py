@@ -56,6 +56,9 @@ class SAM2Model(SAM2Base):
             raise NotImplementedError("mask prompts through the SAM heads (use_mask_input_as_output_without_sam "
                                       "False) are not built; the SAM2.1 configs set it True")
         self.compute_dtype = DTYPES[compute_dtype]
+        # training steps run the tracking loop's backward frame-batched (model/tracking.py);
+        # False = per-frame autograd (the reference's graph shape; A/B and tests)
+        self.frame_batched = os.environ.get("S2H_FRAME_BATCHED", "1") != "0"
         self.arena: Optional[ParamArena] = None
         self._load_weights(checkpoint_path, init_seed)
         if fintuned_model_path is not None:
@@ -291,12 +294,21 @@ class SAM2Model(SAM2Base):
                 raise NotImplementedError("mask prompts on single-frame training clips go through the SAM heads "
                                           "(sam2_base.py:796-800); not built")
             self._mask_pad_prompt = backbone_out["prompt_pad"]
+        tracker = None
+        if self.frame_batched and self.training and torch.is_grad_enabled() and not return_dict:
+            from .tracking import FrameTracker
+            tracker = FrameTracker(self, T, O, feats, s0, s1, mask_cond is not None)
         for t in range(T):
             is_cond = t == 0
             feat_t = feats[t]
             if is_cond and mask_cond is not None:
                 low, high, ious, ptr, score = self._use_mask_as_output(feat_t, mask_cond[0], mask_cond[1],
                                                                        (s0[t:t + 1], s1[t:t + 1]), O)
+            elif tracker is not None:
+                prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
+                pix = tracker.memory_conditioned(t, feat_t.detach(), pos, output_dict)
+                low, high, ious, ptr, score = tracker.sam_heads(t, pix, prompt, s0[t:t + 1].detach(),
+                                                                s1[t:t + 1].detach())
             else:
                 pix = self._prepare_memory_conditioned_features(t, is_cond, feat_t, pos, T, output_dict, O)
                 prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
@@ -324,4 +336,12 @@ class SAM2Model(SAM2Base):
             })
         if return_dict:
             return output_dict
+        if tracker is not None:  # one autograd node for the whole loop (frame-batched backward)
+            hi = tracker.finish()
+            for t, fr in enumerate(frames):
+                if t in hi:
+                    high4 = hi[t][0].view(O, 1, self.image_size, self.image_size)
+                    fr["pred_masks_high_res"] = fr["multistep_pred_masks_high_res"] = high4
+                    fr["multistep_pred_multimasks_high_res"] = [high4]
+                    fr["multistep_pred_ious"] = [hi[t][1]]
         return frames

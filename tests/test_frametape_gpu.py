@@ -1,0 +1,103 @@
+"""Frame-batched backward of the tracking loop (kernels/frametape.py, model/tracking.py) against
+the per-frame autograd path of the same build: the forward runs the same kernels in the same
+order (dropout off), so outputs agree to the bit and gradients up to summation order; plus the
+frame-table flash backward kernel against per-frame launches (dropout on, same masks)."""
+import math
+
+import pytest
+import torch
+
+from step_harness import CASES, build_model, golden_batch, grads_by_name, load_golden, run_step
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(name, dtype):
+    g = load_golden(name)
+    size, prompt, trainable = CASES[name]
+    out = []
+    for batched in (False, True):
+        m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype=dtype, seed=int(g["meta/seed"]))
+        m.frame_batched = batched
+        batch = golden_batch(g).to("cuda")
+        stages, merged, losses, _ = run_step(m, batch)
+        out.append(([s["pred_masks"].detach().float().cpu() for s in stages],
+                    {k: float(v) for k, v in losses.items() if torch.is_tensor(v)}, grads_by_name(m)))
+        del m
+    return out
+
+
+@pytest.mark.parametrize("name", ["tiny256_point_all", "tiny256_point_mem", "bplus128_point_all_t8",
+                                  "tiny256_mask_all", "tiny256_point_all_multi"])
+def test_frame_batched_equals_per_frame_fp32(name):
+    (la, lsa, ga), (lb, lsb, gb) = _pair(name, "fp32")
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b)
+    for k in lsa:
+        assert abs(lsa[k] - lsb[k]) <= 1e-6 * max(1.0, abs(lsa[k])), (k, lsa[k], lsb[k])
+    assert sorted(ga) == sorted(gb)
+    bad = []
+    for n in ga:
+        ref = ga[n].double()
+        err = (gb[n].double() - ref).abs().max().item()
+        if err > 1e-5 * ref.abs().max().item() + 1e-9:
+            bad.append((n, err, ref.abs().max().item()))
+    assert not bad, bad[:8]
+
+
+def test_frame_batched_equals_per_frame_bf16():
+    """bf16 at B+ 256^2 (flash forward, frame-table flash backward, LDS-DMA GEMMs), dropout off:
+    same forward bits; gradients within bf16 rounding of the per-frame path"""
+    (la, lsa, ga), (lb, lsb, gb) = _pair("bplus256_point_all", "bf16")
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b)
+    assert abs(lsa["total_loss"] - lsb["total_loss"]) <= 1e-6 * abs(lsa["total_loss"])
+    num = sum(float((gb[n].double() - ga[n].double()).norm() ** 2) for n in ga)
+    den = sum(float(ga[n].double().norm() ** 2) for n in ga)
+    rel = math.sqrt(num / den)
+    print("global relative gradient difference batched vs per-frame (bf16):", rel)
+    assert rel <= 2e-2, rel
+
+
+@pytest.mark.parametrize("p_drop", [0.0, 0.1])
+def test_flash_bwd_frames_matches_per_frame(p_drop):
+    """s2h_flash_bwd_frames over 3 frames with packed K/V of 1028 / 2056 / 3084 keys vs one
+    s2h_attn_bwd per frame with the same seed and index offsets"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(0)
+    B, Lq, H, D = 5, 256, 1, 256
+    lks = [1028, 2056, 3084]
+    F = len(lks)
+    dt = torch.bfloat16
+    q = (torch.randn(F * B, Lq, H, D, device="cuda") * 0.5).to(dt)
+    do = torch.randn(F * B, Lq, H, D, device="cuda").to(dt)
+    rows = sum(B * lk for lk in lks)
+    k = (torch.randn(rows, H, D, device="cuda") * 0.5).to(dt)
+    v = torch.randn(rows, H, D, device="cuda").to(dt)
+    scale = 1.0 / math.sqrt(D)
+    seed = 12345
+    o = torch.empty_like(q)
+    lse = torch.empty(F * B, H, Lq, device="cuda")
+    krow, idx0, r, n = [], [], 0, 0
+    for f, lk in enumerate(lks):
+        krow.append(r)
+        idx0.append(n)
+        sl = slice(f * B, (f + 1) * B)
+        ops.attn_fwd(q[sl], k[r:r + B * lk].view(B, lk, H, D), v[r:r + B * lk].view(B, lk, H, D), o[sl], lse[sl],
+                     scale, p_drop, seed, idx0=n)
+        r += B * lk
+        n += B * H * Lq * lk
+    dq_ref, dk_ref, dv_ref = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    for f, lk in enumerate(lks):
+        sl = slice(f * B, (f + 1) * B)
+        r0, r1 = krow[f], krow[f] + B * lk
+        ops.attn_bwd(q[sl], k[r0:r1].view(B, lk, H, D), v[r0:r1].view(B, lk, H, D), o[sl], do[sl], lse[sl], dq_ref[sl],
+                     dk_ref[r0:r1].view(B, lk, H, D), dv_ref[r0:r1].view(B, lk, H, D), scale, p_drop, seed,
+                     idx0=idx0[f])
+    dq, dk, dv = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    assert ops.flash_bwd_eligible(q)
+    ops.flash_bwd_frames(F, B, lks, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, scale, p_drop, seed)
+    torch.cuda.synchronize()
+    for a, b in ((dq, dq_ref), (dk, dk_ref), (dv, dv_ref)):
+        err = (a.float() - b.float()).abs().max().item()
+        assert err <= 2e-2 * b.float().abs().max().item(), err
