@@ -297,7 +297,9 @@ class SAM2Model(SAM2Base):
         tracker = None
         if self.frame_batched and self.training and torch.is_grad_enabled() and not return_dict:
             from .tracking import FrameTracker
-            tracker = FrameTracker(self, T, O, feats, s0, s1, mask_cond is not None)
+            pshape = [tuple(backbone_out["prompt_cond"][0].shape) if (t == 0 and mask_cond is None)
+                      else tuple(backbone_out["prompt_pad"][0].shape) for t in range(T)]
+            tracker = FrameTracker(self, T, O, feats, s0, s1, mask_cond is not None, pshape)
         for t in range(T):
             is_cond = t == 0
             feat_t = feats[t]

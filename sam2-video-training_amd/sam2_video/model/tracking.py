@@ -20,7 +20,10 @@ from ..kernels.frametape import FrameTape, recording
 
 
 class FrameTracker:
-    def __init__(self, model, T, O, feats, s0, s1, mask_mode):
+    """prompt_shapes: per frame, the shape of its sparse prompt (frames whose SAM heads see a
+    different prompt size -- a box prompt on frame 0 -- record into a tape of their own)"""
+
+    def __init__(self, model, T, O, feats, s0, s1, mask_mode, prompt_shapes=None):
         self.m = model
         self.T, self.O = T, O
         self.feats, self.s0, self.s1 = feats, s0, s1
@@ -31,7 +34,18 @@ class FrameTracker:
         self.dec_frames = [t for t in range(T) if not (t == 0 and mask_mode)]
         self.ma = (FrameTape(T - 1, dev, mem_rows=model._bank_rows(T, L, C), name="memory_attention")
                    if T > 1 else None)
-        self.dec = FrameTape(len(self.dec_frames), dev, name="sam_heads")
+        # SAM-heads tapes, one per prompt shape (frames in order)
+        groups = {}
+        for t in self.dec_frames:
+            key = tuple(prompt_shapes[t]) if prompt_shapes is not None else ()
+            groups.setdefault(key, []).append(t)
+        self.decs = []  # [(tape, frames)]
+        self.dec_of = {}  # t -> (group index, position)
+        for gi, frames in enumerate(groups.values()):
+            self.decs.append((FrameTape(len(frames), dev, name=f"sam_heads{gi}"), frames))
+            for j, t in enumerate(frames):
+                self.dec_of[t] = (gi, j)
+        self.vids = [None] * len(self.decs)
         self.pix0 = None
         self.outs = {}  # t -> (high, ious)
 
@@ -53,7 +67,8 @@ class FrameTracker:
         return pix
 
     def sam_heads(self, t, pix, prompt, s0t, s1t):
-        tp = self.dec
+        gi, _ = self.dec_of[t]
+        tp = self.decs[gi][0]
         tp.begin_frame()
         with recording(tp):
             p_in = tp.input("pix", pix)
@@ -61,7 +76,7 @@ class FrameTracker:
             s1_in = tp.input("s1", s1t, requires_grad=self.s1.requires_grad)
             low, high, ious, ptr, score = self.m._forward_sam_heads(p_in, prompt, (s0_in, s1_in), self.O)
             if tp.f == 0:
-                self.vid_high, self.vid_ious = tp.out_vid(high), tp.out_vid(ious)
+                self.vids[gi] = (tp.out_vid(high), tp.out_vid(ious))
         tp.end_frame()
         self.outs[t] = (high, ious)
         return low, high, ious, ptr, score
@@ -87,47 +102,61 @@ class FrameTracker:
 
     def backward(self, grads):
         T, O, L, C = self.T, self.O, self.L, self.C
-        dec = self.dec
-        F = dec.F
-        hs, is_ = dec.st(self.vid_high), dec.st(self.vid_ious)
-        gh = torch.empty(hs.buf.numel(), device=hs.buf.device, dtype=hs.dtype)
-        gi = torch.empty(is_.buf.numel(), device=is_.buf.device, dtype=is_.dtype)
-        for j in range(F):
-            for g, st, dst in ((grads[2 * j], hs, gh), (grads[2 * j + 1], is_, gi)):
-                d = dst[st.offsets[j]:st.offsets[j] + st.numels[j]]
-                if g is None:
-                    d.zero_()
-                else:
-                    d.copy_(g.reshape(-1))
-        din = dec.backward({self.vid_high: gh, self.vid_ious: gi})
-        dt_ = self.feats.dtype
-        dfeats = ds0 = ds1 = None
-        dpix = din.get("pix")
-        if self.feats.requires_grad:
-            dfeats = torch.zeros(T, L, C, device=gh.device, dtype=dt_)
         pix_n = O * L * C
-        if dpix is not None:
-            first = 0
-            if not self.mask_mode:  # frame 0: pix0 = expand(feat0 + no_mem_embed)
-                d0 = dpix[:pix_n].view(O, L * C)
-                if dfeats is not None:
-                    ops.sum_outer(d0, dfeats[0].view(-1))
-                gm = FN._grad_of(self.m.no_mem_embed)
-                if gm is not None:
-                    ops.colsum(d0.reshape(O * L, C), gm.view(-1), accumulate=True)
-                first = 1
-            if self.ma is not None:
-                dma = self.ma.backward({self.ma_out: dpix[first * pix_n:]})
-                if dfeats is not None and dma.get("feat") is not None:
-                    ops.add(dma["feat"], None, out=dfeats[1:].reshape(-1))
-        nd = len(self.dec_frames)
+        gpos = {t: j for j, t in enumerate(self.dec_frames)}  # position of frame t in `grads`
+        dev = self.feats.device
+        dpix = {}  # t -> flat d(pix) (views into the tapes' stacked gradients)
+        dhr = {"s0": {}, "s1": {}}
+        for gi, (tp, frames) in enumerate(self.decs):
+            vh, vi = self.vids[gi]
+            hs, is_ = tp.st(vh), tp.st(vi)
+            gh = torch.empty(hs.buf.numel(), device=dev, dtype=hs.dtype)
+            gio = torch.empty(is_.buf.numel(), device=dev, dtype=is_.dtype)
+            for j, t in enumerate(frames):
+                for g, st, dst in ((grads[2 * gpos[t]], hs, gh), (grads[2 * gpos[t] + 1], is_, gio)):
+                    d = dst[st.offsets[j]:st.offsets[j] + st.numels[j]]
+                    if g is None:
+                        d.zero_()
+                    else:
+                        d.copy_(g.reshape(-1))
+            din = tp.backward({vh: gh, vi: gio})
+            for j, t in enumerate(frames):
+                if din.get("pix") is not None:
+                    dpix[t] = din["pix"][j * pix_n:(j + 1) * pix_n]
+                for key in ("s0", "s1"):
+                    g = din.get(key)
+                    if g is not None:
+                        per = g.numel() // len(frames)
+                        dhr[key][t] = g[j * per:(j + 1) * per]
+        dfeats = ds0 = ds1 = None
+        if self.feats.requires_grad:
+            dfeats = torch.zeros(T, L, C, device=dev, dtype=self.feats.dtype)
+        if 0 in dpix and not self.mask_mode:  # frame 0: pix0 = expand(feat0 + no_mem_embed)
+            d0 = dpix[0].view(O, L * C)
+            if dfeats is not None:
+                ops.sum_outer(d0, dfeats[0].view(-1))
+            gm = FN._grad_of(self.m.no_mem_embed)
+            if gm is not None:
+                ops.colsum(d0.reshape(O * L, C), gm.view(-1), accumulate=True)
+        if self.ma is not None and all(t in dpix for t in range(1, T)):
+            # frames 1..T-1 stacked in order for the memory-attention tape (one copy unless a
+            # single SAM-heads tape already holds them contiguously)
+            g1 = dpix[1]
+            es = g1.element_size()
+            if all(dpix[t].data_ptr() == g1.data_ptr() + (t - 1) * pix_n * es for t in range(1, T)):
+                gma = torch.as_strided(g1, ((T - 1) * pix_n,), (1,))
+            else:
+                gma = torch.cat([dpix[t] for t in range(1, T)])
+            dma = self.ma.backward({self.ma_out: gma})
+            if dfeats is not None and dma.get("feat") is not None:
+                ops.add(dma["feat"], None, out=dfeats[1:].reshape(-1))
         for key, src in (("s0", self.s0), ("s1", self.s1)):
-            g = din.get(key)
-            if g is None or not src.requires_grad:
+            if not src.requires_grad or not dhr[key]:
                 continue
-            full = torch.zeros(src.shape, device=g.device, dtype=src.dtype)
+            full = torch.zeros(src.shape, device=dev, dtype=src.dtype)
             per = full[0].numel()
-            full.view(T, per)[self.dec_frames[0]:].copy_(g.view(nd, per))  # dec frames: 0..T-1 or 1..T-1
+            for t, g in dhr[key].items():
+                full.view(T, per)[t].copy_(g)
             if key == "s0":
                 ds0 = full
             else:

@@ -36,11 +36,14 @@ def test_frame_batched_equals_per_frame_fp32(name):
     for k in lsa:
         assert abs(lsa[k] - lsb[k]) <= 1e-6 * max(1.0, abs(lsa[k])), (k, lsa[k], lsb[k])
     assert sorted(ga) == sorted(gb)
+    # per parameter, relative to its own scale -- with a floor at 1e-6 of the largest gradient of
+    # the step for the attention key biases, whose exact gradient is 0 (softmax shift invariance)
+    gmax = max(float(g.abs().max()) for g in ga.values())
     bad = []
     for n in ga:
         ref = ga[n].double()
         err = (gb[n].double() - ref).abs().max().item()
-        if err > 1e-5 * ref.abs().max().item() + 1e-9:
+        if err > 1e-5 * ref.abs().max().item() + 1e-6 * gmax:
             bad.append((n, err, ref.abs().max().item()))
     assert not bad, bad[:8]
 
