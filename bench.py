@@ -56,31 +56,56 @@ def parse():
     return ap.parse_args()
 
 
-def attention_roofline(records):
-    """records: (ms, [BH, Lq, Lk, D, esize]) of every attention-forward launch in the timed region.
-    Dominant kernel = the memory-attention cross attention (head_dim 256, Lk > Lq)."""
-    sel = [(ms, m) for ms, m in records if m[3] == 256 and m[2] > m[1]]
-    if not sel:
-        return None
-    flops = sum(4.0 * m[0] * m[1] * m[2] * m[3] for _, m in sel)
-    ms = sum(t for t, _ in sel)
-    n = len(sel)
-    if ms <= 0.0:
-        return None
-    achieved = flops / (ms * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(achieved / PEAK_BF16_TFLOPS, 4), "traffic": None,
-            "kernel": "flash_fwd_kernel<256> (memory-attention cross-attention, bf16)",
-            "launches": n, "avg_launch_ms": round(ms / n, 4),
-            "flops_per_launch_avg": flops / n}
+# algorithmic flops per profiler record (SURVEY.md §8(d) counting: attention backward = 2 x forward,
+# the QK^T recompute of the flash backward is not counted)
+def record_flops(kind, m):
+    if kind == 4:
+        b, M, N, K = m[1:5]
+        return 2.0 * b * M * N * K
+    bh, lq, lk, d = m[1:5]
+    return (4.0 if kind == 1 else 8.0) * bh * lq * lk * d
 
 
-def pmc_traffic():
-    """HBM bytes per launch of the roofline kernel from the latest committed rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes (profiles/*_flash_fwd_pmc.json, written by the recipe in
-    tools/gpu_prof.sh; counters cannot be collected inside this timed run)."""
+FAMILY = {1: "attention forward (flash_fwd / attn_fwd kernels)",
+          2: "attention backward (flash_bwd di/dq/dkv kernels, frame-batched; attn_bwd kernels)",
+          4: "GEMM (gemm16g / gemm kernels: projections, FFN, convs, dgrad, wgrad)"}
+
+
+def family_roofline(recs, nsteps=1):
+    """per-family totals of the profiled step(s) (every GEMM / attention launch bracketed by HIP
+    events on its own stream; per-step figures = totals / nsteps) and the dominant family (most
+    kernel time) as the roofline line"""
+    fam = {}
+    for ms, m in recs:
+        f = fam.setdefault(m[0], {"ms": 0.0, "flops": 0.0, "launches": 0})
+        f["ms"] += ms
+        f["flops"] += record_flops(m[0], m)
+        f["launches"] += 1
+    if not fam:
+        return None
+    table = {}
+    for k, f in fam.items():
+        ach = f["flops"] / (f["ms"] * 1e-3) / 1e12 if f["ms"] > 0 else 0.0
+        table[FAMILY[k].split(" (")[0]] = {"ms_per_step": round(f["ms"] / nsteps, 3),
+                                          "tflop_per_step": round(f["flops"] / nsteps / 1e12, 4),
+                                          "achieved": round(ach, 1), "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                                          "launches_per_step": f["launches"] // nsteps}
+    k = max(fam, key=lambda kk: fam[kk]["ms"])
+    f = fam[k]
+    ach = f["flops"] / (f["ms"] * 1e-3) / 1e12
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": FAMILY[k],
+            "launches": f["launches"], "avg_launch_ms": round(f["ms"] / f["launches"], 4),
+            "flops_per_launch_avg": f["flops"] / f["launches"], "families": table, "_kind": k}
+
+
+def pmc_traffic(kind):
+    """HBM bytes per launch of the dominant family from the newest committed rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes (profiles/*_<family>_pmc.json, tools/pmc_family.py; counters
+    cannot be collected inside this timed run)"""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_flash_fwd_pmc.json")))
+    tag = {1: "attn_fwd", 2: "attn_bwd", 4: "gemm"}[kind]
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{tag}_pmc.json")))
     if not files:
         return None, None
     d = json.load(open(files[-1]))
@@ -214,7 +239,8 @@ def main():
             print(f"step {k} loss {float(loss):.5f}", file=sys.stderr)
     torch.cuda.synchronize()
     if not args.no_prof and not graph:
-        _lib.call("s2h_prof_enable", 8192)
+        _lib.call("s2h_prof_enable", 16384)
+        _lib.call("s2h_prof_select", 7)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -245,7 +271,8 @@ def main():
             # HIP events cannot time kernels inside a replayed graph (ROCm 7.2 rejects external
             # event nodes in capture): time the same kernels in one eager step right after the
             # timed region, each launch bracketed by events on its own stream
-            _lib.call("s2h_prof_enable", 8192)
+            _lib.call("s2h_prof_enable", 16384)
+            _lib.call("s2h_prof_select", 7)
             runner.graph = False
             runner(batches[-1])
             runner.graph = True
@@ -253,27 +280,18 @@ def main():
             print(f"profiled eager step loss {float(module.logged['train/total_loss']):.5f}", file=sys.stderr)
         recs = read_prof(_lib)
         _lib.call("s2h_prof_enable", 0)
-        roof = attention_roofline([(ms, m[1:]) for ms, m in recs if m[0] == 1])
+        roof = family_roofline([(ms, m) for ms, m in recs], 1 if graph else args.steps)
         if roof is not None:
-            roof["traffic"], src = pmc_traffic()
+            kind = roof.pop("_kind")
+            roof["traffic"], src = pmc_traffic(kind)
             if src:
-                roof["traffic_unit"] = "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE)"
+                roof["traffic_unit"] = "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE), same launch mix"
                 roof["traffic_source"] = src
             roof["timing"] = ("HIP events per launch, one eager step after the timed graph replays" if graph
                               else "HIP events per launch over the timed region")
-        if args.kernel_table:
-            # one extra (untimed) step with every GEMM / attention launch recorded
-            _lib.call("s2h_prof_enable", 16384)
-            _lib.call("s2h_prof_select", 7)
-            runner.graph = False  # one eager step: every launch bracketed by its own events
-            runner(batches[-1])
-            runner.graph = graph
-            torch.cuda.synchronize()
-            table = kernel_table(read_prof(_lib))
-            _lib.call("s2h_prof_enable", 0)
-            _lib.call("s2h_prof_select", 1)
-            if rank == 0:
-                print(table, file=sys.stderr, flush=True)
+        if args.kernel_table and rank == 0:
+            print(kernel_table(recs), file=sys.stderr, flush=True)
+        _lib.call("s2h_prof_select", 1)
 
     frames = args.frames * args.steps * world
     value = frames / elapsed

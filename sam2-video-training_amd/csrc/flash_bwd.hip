@@ -670,7 +670,10 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
   a.seed_off = s2h_rng_offset_ptr();
   a.splits = 1; a.tiles_per_split = (lk_max + 63) / 64;
   a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32;
-  const int slot = s2h_prof_begin(st, 2, (int64_t)a.BH, Lq, lk_max, D, 3);
+  // profiler record: per-frame batch-heads and the keys summed over frames (flops = 10 * m0 m1 m2 m3)
+  int64_t lk_sum = 0;
+  for (int f = 0; f < nfr; ++f) lk_sum += fr_lk[f];
+  const int slot = s2h_prof_begin(st, 2, (int64_t)bpf * H, Lq, lk_sum, D, 3);
   const int rc = D == 256 ? flash_bwd_launch<256>(a, st) : flash_bwd_launch<128>(a, st);
   s2h_prof_end(slot, st);
   return rc;

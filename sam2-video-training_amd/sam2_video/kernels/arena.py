@@ -32,9 +32,17 @@ def _align(n):
 
 class ParamArena:
     def __init__(self, named_params: Sequence, grad_names: Iterable[str], compute_dtype, device,
-                 groups: Sequence[Sequence[str]] = ()):
+                 groups: Sequence[Sequence[str]] = (), tail_prefixes: Sequence[str] = ()):
+        """tail_prefixes: gradient-receiving parameters under these name prefixes go to the END of
+        the gradient region (their gradients are completed last in the backward -- the image
+        encoder's -- so the rest of the region can be all-reduced while they are computed);
+        `grad_split` is the offset where they start."""
         grad_names = set(grad_names)
         params = dict(named_params)
+        tail = tuple(tail_prefixes)
+        if tail:  # stable partition of the gradient-receiving names: tail prefixes last
+            named_params = ([(n, p) for n, p in named_params if not (n in grad_names and n.startswith(tail))]
+                            + [(n, p) for n, p in named_params if n in grad_names and n.startswith(tail)])
         order: List[str] = []
         seen = set()
         # grad-receiving params first (contiguous gradient region), grouped names kept adjacent
@@ -66,6 +74,8 @@ class ParamArena:
                 n_grad = off
         self.total = _align(off)
         self.n_grad = _align(n_grad)
+        tails = [self.offsets[n] for n in order if n in grad_names and tail and n.startswith(tail)]
+        self.grad_split = min(tails) if tails else self.n_grad
         self.device = device
         self.compute_dtype = compute_dtype
         self.data = torch.zeros(self.total, dtype=torch.float32, device=device)

@@ -441,6 +441,13 @@ def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_
         ops.flash_bwd_frames(F, B, lks, krow, op.fattrs["idx0"], q_all, k_rows, v_rows, o_all, go, lse, dq,
                              dk_rows, dv_rows, a["scale"], a["p"], a["seed"])
         return
+    if len(set(lks)) == 1:
+        # uniform key count: the frames ARE one [F*B] batch (frame f's dropout indices start at
+        # f*B*H*Lq*Lk, where its forward put them)
+        Lk = lks[0]
+        ops.attn_bwd(q_all, k_rows.view(F * B, Lk, H, D), v_rows.view(F * B, Lk, H, D), o_all, go, lse, dq,
+                     dk_rows.view(F * B, Lk, H, D), dv_rows.view(F * B, Lk, H, D), a["scale"], a["p"], a["seed"])
+        return
     for f in range(F):
         sl = slice(f * B, (f + 1) * B)
         r0, r1 = krow[f], krow[f] + B * lks[f]

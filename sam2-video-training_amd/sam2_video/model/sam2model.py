@@ -179,7 +179,8 @@ class SAM2Model(SAM2Base):
         groups = []
         for i, layer in enumerate(self.memory_attention.layers):
             groups += layer.arena_groups(f"memory_attention.layers.{i}")
-        self.arena = ParamArena(named, grad_names, self.compute_dtype, device, groups=groups)
+        self.arena = ParamArena(named, grad_names, self.compute_dtype, device, groups=groups,
+                                tail_prefixes=("image_encoder.",))
         for m in self.modules():
             if hasattr(m, "bind_arena"):
                 m.bind_arena(self.arena)
@@ -208,6 +209,10 @@ class SAM2Model(SAM2Base):
         if self.arena is None:
             raise RuntimeError("call SAM2Model.load(device) before forward")
         backbone_out = self.forward_image(input.flat_img_batch)
+        # the backbone outputs the tracking loop reads: the split point of a two-phase backward
+        # (StepRunner overlaps the gradient all-reduce of everything after them with the image
+        # encoder's backward)
+        self.last_backbone_outputs = [t for t in backbone_out["backbone_fpn"] if t.requires_grad]
         backbone_out = self.prepare_prompt_inputs(backbone_out, input)
         stages = self.forward_tracking(backbone_out, input)
         out = merge_object_results_to_category(stages, backbone_out["obj_to_cat"], backbone_out["num_categories"])

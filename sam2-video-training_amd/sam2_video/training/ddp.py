@@ -19,13 +19,21 @@ import torch.distributed as dist
 
 
 class ArenaGradReducer:
-    def __init__(self, grad: torch.Tensor, group=None, bucket_bytes: int = 64 << 20):
+    """`split`: offset of the gradients completed last (the image encoder's, arena tail); the
+    region before it can be reduced (reduce_range(0, split, async_op=True)) while they are still
+    being computed -- the overlap of the all-reduce with the backward."""
+
+    def __init__(self, grad: torch.Tensor, group=None, bucket_bytes: int = 64 << 20, split: int = None):
         self.grad = grad
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         n = grad.numel()
-        per = max(1, bucket_bytes // grad.element_size())
-        self.buckets = [grad[i:i + per] for i in range(0, n, per)]
+        self.split = n if split is None else max(0, min(int(split), n))
+        self.per = max(1, bucket_bytes // grad.element_size())
+        self.buckets = self._buckets(0, n)
+
+    def _buckets(self, lo, hi):
+        return [self.grad[i:min(i + self.per, hi)] for i in range(lo, hi, self.per)]
 
     @property
     def grad_scale(self) -> float:
@@ -36,6 +44,16 @@ class ArenaGradReducer:
         if self.world == 1:
             return []
         works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op) for b in self.buckets]
+        return works if async_op else []
+
+    def reduce_range(self, lo, hi, async_op: bool = True):
+        """SUM all-reduce of grad[lo:hi] in buckets; async: returns the works (collectives are
+        ordered after the work already queued on the current stream, run beside what is queued
+        after them, and work.wait() makes the current stream wait for them)"""
+        if self.world == 1 or hi <= lo:
+            return []
+        works = [dist.all_reduce(b, op=dist.ReduceOp.SUM, group=self.group, async_op=async_op)
+                 for b in self._buckets(lo, hi)]
         return works if async_op else []
 
 

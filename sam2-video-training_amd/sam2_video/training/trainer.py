@@ -242,12 +242,19 @@ class StepRunner:
     their seeds (s2h_rng_bind)."""
 
     def __init__(self, module: SAM2LightningModule, total_steps: int = 1, distributed: bool = False,
-                 graph: bool = False, accumulate_grad_batches: int = 1, gradient_clip_val=None):
+                 graph: bool = False, accumulate_grad_batches: int = 1, gradient_clip_val=None,
+                 split_backward: Optional[bool] = None):
         self.module = module
         if gradient_clip_val is not None:
             module.gradient_clip_val = gradient_clip_val
         module.configure_optimizers(total_steps)
-        self.reducer = ArenaGradReducer(module.model.arena.grad_region()) if distributed else None
+        arena = module.model.arena
+        self.reducer = ArenaGradReducer(arena.grad_region(), split=arena.grad_split) if distributed else None
+        # overlap: a two-phase backward -- (1) loss -> backbone outputs (the frame-batched
+        # tracking backward completes every gradient except the image encoder's), (2) the image
+        # encoder's backward -- with the all-reduce of the completed region issued between them
+        split_ok = getattr(module.model, "frame_batched", False) and arena.grad_split < arena.n_grad
+        self.overlap = bool(split_ok and (distributed if split_backward is None else split_backward))
         self.accumulate = max(1, int(accumulate_grad_batches or 1))
         self.global_step = 0  # optimizer steps
         self.micro_step = 0
@@ -262,13 +269,28 @@ class StepRunner:
         # variation of the dropout masks comes from the device RNG offset alone, so an eager step
         # and a replay of the captured one use identical masks
         self.seed_base = FN._SEED[0]
+        self._pending = None
+        self._replay2 = None
         module.model.arena.zero_grad()
 
     def _device_step(self, batch):
+        """forward + loss + backward (phase 1 only when overlapping; _phase2 finishes it)"""
         self._fn.set_seed(self.seed_base)
         loss = self.module.training_step(batch, self.micro_step)
-        loss.backward()
+        bb = getattr(self.module.model, "last_backbone_outputs", None) if self.overlap else None
+        if bb:
+            grads = torch.autograd.grad(loss, bb, allow_unused=True)
+            self._pending = [(t, g) for t, g in zip(bb, grads) if g is not None]
+        else:
+            self._pending = None
+            loss.backward()
         return loss
+
+    def _phase2(self):
+        pend = self._pending
+        self._pending = None
+        if pend:
+            torch.autograd.backward([t for t, _ in pend], [g for _, g in pend])
 
     def _graphed_step(self, batch):
         model = self.module.model
@@ -290,6 +312,7 @@ class StepRunner:
             side.wait_stream(cur)
             with torch.cuda.stream(side):  # eager warm-up: fills every device-side table cache
                 self._device_step(static)
+                self._phase2()
             cur.wait_stream(side)
             if saved is not None:
                 model.arena.grad_region().copy_(saved)
@@ -300,8 +323,13 @@ class StepRunner:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 loss = self._device_step(static)
-            ent = self._graphs[key] = {"graph": g, "batch": static, "loss": loss, "logged": dict(self.module.logged),
-                                       "outputs": self.module.last_outputs}
+            g2 = None
+            if self._pending is not None:  # the image encoder's backward as a second graph
+                g2 = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g2, pool=g.pool()):
+                    self._phase2()
+            ent = self._graphs[key] = {"graph": g, "graph2": g2, "batch": static, "loss": loss,
+                                       "logged": dict(self.module.logged), "outputs": self.module.last_outputs}
         else:
             st = ent["batch"]
             st.img_batch.copy_(batch.img_batch, non_blocking=True)
@@ -310,21 +338,23 @@ class StepRunner:
             model.upload_prompt_plan(plan, dev, out=st.prompt_plan["dev"])
             st.prompt_plan.update({k: plan[k] for k in ("points", "labels")})
         ent["graph"].replay()
+        self._replay2 = ent["graph2"]
         self.module.logged = dict(ent["logged"])
         self.module.last_outputs = ent["outputs"]
         return ent["loss"]
 
-    def after_backward(self) -> bool:
-        """Counts the micro-step; at an accumulation boundary runs all-reduce + clip + AdamW (the
-        arena is zeroed when the next window starts).  Returns True when an optimizer step was
-        taken."""
+    def after_backward(self, reduced: bool = False) -> bool:
+        """Counts the micro-step; at an accumulation boundary runs all-reduce (unless `reduced`:
+        __call__ already overlapped it with the backward) + clip + AdamW (the arena is zeroed when
+        the next window starts).  Returns True when an optimizer step was taken."""
         m = self.module
         self.micro_step += 1
         if self.micro_step % self.accumulate:
             return False
         scale = 1.0 / self.accumulate
         if self.reducer is not None:
-            self.reducer.reduce()
+            if not reduced:
+                self.reducer.reduce()
             scale *= self.reducer.grad_scale
         lr = m.lr_at(self.global_step) if m.lr_at is not None else None
         m.optimizer.step(lr=lr, grad_scale=scale)
@@ -336,8 +366,24 @@ class StepRunner:
         if self.micro_step % self.accumulate == 0:  # new accumulation window (zero_grad)
             self.module.model.arena.zero_grad()
         self.rng.fill_(self.micro_step + 1)
+        self._replay2 = None
         loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
-        self.after_backward()
+        boundary = (self.micro_step + 1) % self.accumulate == 0
+        works = []
+        if self.overlap and boundary and self.reducer is not None:
+            # the tracking gradients are complete: reduce them beside the image encoder's backward
+            works += self.reducer.reduce_range(0, self.reducer.split)
+        if self._replay2 is not None:
+            self._replay2.replay()
+        else:
+            self._phase2()
+        reduced = False
+        if self.overlap and boundary and self.reducer is not None:
+            works += self.reducer.reduce_range(self.reducer.split, self.reducer.grad.numel())
+            for w in works:
+                w.wait()
+            reduced = True
+        self.after_backward(reduced=reduced)
         return loss
 
 

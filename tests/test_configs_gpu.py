@@ -124,3 +124,25 @@ def test_validation_step_is_deterministic():
     # move them by far more
     for k in vals[0]:
         assert abs(vals[0][k] - vals[1][k]) <= 1e-5 * max(1.0, abs(vals[0][k])), (k, vals)
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_split_backward_equals_single_backward(graph):
+    """the two-phase backward of the DDP overlap (tracking gradients first, then the image
+    encoder's as a second graph) leaves the same gradient arena as one backward; the image
+    encoder's gradients sit at the arena tail (grad_split)"""
+    from sam2_video.training.trainer import StepRunner
+    clips = _clips([3, 4], 3, 256, 4, 3)
+    res = []
+    for split in (False, True):
+        m = _module("base_plus", 256, dtype="fp32", dropout=0.0)
+        arena = m.model.arena
+        names = [n for n in arena.grad_names if arena.offsets[n] >= arena.grad_split]
+        assert names and all(n.startswith("image_encoder.") for n in names)
+        run = StepRunner(m, total_steps=2, graph=graph, split_backward=split)
+        assert run.overlap == split
+        for c in clips:
+            run(c)
+        res.append(arena.grad_region().detach().clone())
+    a, b = res
+    assert (a - b).abs().max().item() <= 1e-5 * a.abs().max().item()
