@@ -121,8 +121,13 @@ int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* k, int64_t skb, int64_t skh, int64_t skl,
                  const void* v, int64_t svb, int64_t svh, int64_t svl,
                  void* o, int64_t sob, int64_t soh, int64_t sol,
-                 float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws,
-                 int64_t ws_bytes, hipStream_t st);
+                 float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, uint32_t* keep,
+                 void* ws, int64_t ws_bytes, hipStream_t st);
+/* Dropout keep bitmap (`keep`, nullable, p_drop > 0 only): the flash forward at head_dim 256
+ * also writes each element's keep flag -- bit (k & 31) of word [(b*H + h) * Lq + q] * kw + k/32,
+ * kw = 2 * ceil(Lk / 64); s2h_attn_keep_words(...) words -- and the backward reads it instead
+ * of re-hashing.  A non-NULL keep on a launch that does not take that path is an error. */
+int64_t s2h_attn_keep_words(int B, int H, int Lq, int Lk);
 /* Backward of s2h_attn_fwd; di_ws: fp32 workspace [B*H*Lq].  bf16 with head_dim 128/256
  * and >= 128 query rows takes the flash path (dQ kernel with key-split fp32 partials in
  * `ws` of s2h_attn_bwd_ws_bytes(...) bytes, dK/dV kernel per 128-key block). */
@@ -137,12 +142,13 @@ int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                  void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0,
-                 void* ws, int64_t ws_bytes, hipStream_t st);
+                 const uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st);
 /* Frame-batched flash backward (bf16, head_dim 128/256, Lq >= 128): nfr frames x bpf batches
  * x H heads of the tracking loop in one launch per kernel -- Q / O / dO / dQ / lse uniform
  * [nfr*bpf] batches, K / V / dK / dV packed per frame (frame f: bpf blocks of fr_lk[f] rows
  * starting at row fr_krow[f]); frame f's dropout indices start at fr_idx0[f] (host arrays of
- * nfr <= 32 entries).  The memory-attention backward of every frame at once
+ * nfr <= 32 entries); keep (nullable) = the frames' forward keep bitmaps, frame f's from word
+ * fr_koff[f].  The memory-attention backward of every frame at once
  * (transformer.py:275-311 for frames 1..T-1, memory_attention.py:58-99). */
 /* 1 when s2h_flash_bwd_frames takes (dt, Lq, head_dim); 0 = run the frames one by one. */
 int s2h_flash_bwd_ok(int dt, int Lq, int D);
@@ -152,7 +158,8 @@ int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_l
                          const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout, int64_t sgb,
                          int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk,
                          int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh, int64_t sdvl, const float* lse,
-                         float* di_ws, float scale, float p_drop, uint64_t seed, hipStream_t st);
+                         float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
+                         const int64_t* fr_koff, hipStream_t st);
 
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:

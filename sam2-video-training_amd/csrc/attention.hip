@@ -38,7 +38,7 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D);
 int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                   const void* k, int64_t skb, int64_t skh, int64_t skl, const void* v, int64_t svb, int64_t svh,
                   int64_t svl, void* o, int64_t sob, int64_t soh, int64_t sol, float* lse, float scale, float p_drop,
-                  uint64_t seed, uint64_t idx0, void* ws, int64_t ws_bytes, hipStream_t st);
+                  uint64_t seed, uint64_t idx0, uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st);
 
 int s2h_flash_bwd_eligible(int dt, int Lq, int D);
 int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D);
@@ -47,8 +47,14 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D, const void* q, int64_t sq
                   int64_t svl, const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout, int64_t sgb,
                   int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk, int64_t sdkb,
                   int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl, const float* lse,
-                  float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws, int64_t ws_bytes,
-                  hipStream_t st);
+                  float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0, const uint32_t* keep, void* ws,
+                  int64_t ws_bytes, hipStream_t st);
+
+// 32-bit words of the dropout keep bitmap of one attention launch (flash path, head_dim 256):
+// B*H*Lq rows of 2 * ceil(Lk / 64) words.
+extern "C" int64_t s2h_attn_keep_words(int B, int H, int Lq, int Lk) {
+  return (int64_t)B * H * Lq * 2 * ((Lk + 63) / 64);
+}
 
 // Workspace the backward wants (key-split dQ partials of the flash path); 0 = none.
 extern "C" int64_t s2h_attn_bwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D) {
@@ -914,17 +920,20 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                             const void* k, int64_t skb, int64_t skh, int64_t skl,
                             const void* v, int64_t svb, int64_t svh, int64_t svl,
                             void* o, int64_t sob, int64_t soh, int64_t sol,
-                            float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws,
-                            int64_t ws_bytes, hipStream_t st) {
+                            float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, uint32_t* keep,
+                            void* ws, int64_t ws_bytes, hipStream_t st) {
   if (B * H <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
       !attn_aligned(dt, D, v, svb, svh, svl))
     return (int)hipErrorInvalidValue;
-  if (s2h_flash_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol)) {
+  const bool flash = s2h_flash_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol);
+  // a keep bitmap is written by the flash path only, for the head-dim-256 backward that reads it
+  if (keep && p_drop > 0.f && (!flash || D != 256)) return (int)hipErrorInvalidValue;
+  if (flash) {
     const int slot = s2h_prof_begin(st, 1, (int64_t)B * H, Lq, Lk, D, 2);
     const int rc = s2h_flash_fwd(B, H, Lq, Lk, D, q, sqb, sqh, sql, k, skb, skh, skl, v, svb, svh, svl, o, sob, soh,
-                                 sol, lse, scale, p_drop, seed, idx0, ws, ws_bytes, st);
+                                 sol, lse, scale, p_drop, seed, idx0, keep, ws, ws_bytes, st);
     s2h_prof_end(slot, st);
     return rc;
   }
@@ -949,19 +958,21 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                             void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                             void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
                             const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
-                            uint64_t idx0, void* ws, int64_t ws_bytes, hipStream_t st) {
+                            uint64_t idx0, const uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st) {
   if (B * H <= 0 || Lq <= 0) return 0;
   if (Lk <= 0 || D <= 0 || D > 256) return (int)hipErrorInvalidValue;
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
       !attn_aligned(dt, D, v, svb, svh, svl) || !attn_aligned(dt, D, dout, sgb, sgh, sgl))
     return (int)hipErrorInvalidValue;
-  if (s2h_flash_bwd_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol) &&
-      attn_aligned(dt, D, dq, sdqb, sdqh, sdql) && attn_aligned(dt, D, dk, sdkb, sdkh, sdkl) &&
-      attn_aligned(dt, D, dv, sdvb, sdvh, sdvl)) {
+  const bool flash = s2h_flash_bwd_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol) &&
+                     attn_aligned(dt, D, dq, sdqb, sdqh, sdql) && attn_aligned(dt, D, dk, sdkb, sdkh, sdkl) &&
+                     attn_aligned(dt, D, dv, sdvb, sdvh, sdvl);
+  if (keep && p_drop > 0.f && (!flash || D != 256)) return (int)hipErrorInvalidValue;
+  if (flash) {
     const int slot = s2h_prof_begin(st, 2, (int64_t)B * H, Lq, Lk, D, 2);
     const int rc = s2h_flash_bwd(B, H, Lq, Lk, D, q, sqb, sqh, sql, k, skb, skh, skl, v, svb, svh, svl, o, sob, soh,
                                  sol, dout, sgb, sgh, sgl, dq, sdqb, sdqh, sdql, dk, sdkb, sdkh, sdkl, dv, sdvb, sdvh,
-                                 sdvl, lse, di_ws, scale, p_drop, seed, idx0, ws, ws_bytes, st);
+                                 sdvl, lse, di_ws, scale, p_drop, seed, idx0, keep, ws, ws_bytes, st);
     s2h_prof_end(slot, st);
     return rc;
   }

@@ -33,6 +33,10 @@ struct FlashArgs {
   float sl2;  // scale * log2(e)
   float p_drop; uint32_t thresh; float inv_keep; uint64_t seed; const uint64_t* seed_off;
   uint64_t idx0;  // dropout element-index offset (this launch's frame slot in a frame-stacked batch)
+  // keep bitmap (nullable): bit (k & 31) of word keep[(bh * Lq + q) * kw + k / 32] = this launch's
+  // dropout keep flag of (q, k); kw = 2 * ceil(Lk / 64).  The backward reads it instead of
+  // re-hashing (flash_bwd.hip).
+  uint32_t* keep; int kw;
   int splits, tiles_per_split;
   float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
   float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
@@ -150,6 +154,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
       }
     if (a.p_drop > 0.f) {
       // the 4 keys of a (kb) block are consecutive: two hashes per block when pairs align
+      uint32_t kbits[2] = {0u, 0u};  // this lane's keep flags: bit 16kb + 4g + e of the tile's 64 keys
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
@@ -163,6 +168,16 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[kb][e] = kp[e] ? s[kb][e] * a.inv_keep : 0.f;
+        kbits[kb >> 1] |= ((uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3))
+                          << (16 * (kb & 1) + 4 * g);
+      }
+      if (a.keep) {  // OR the 4 key groups of the query row, one 8-B store per row and tile
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          kbits[h2] |= (uint32_t)__shfl_xor((int)kbits[h2], 16);
+          kbits[h2] |= (uint32_t)__shfl_xor((int)kbits[h2], 32);
+        }
+        if (g == 0 && q < a.Lq) *(uint2*)(a.keep + ((int64_t)bh * a.Lq + q) * a.kw + (k0 >> 5)) = uint2{kbits[0], kbits[1]};
       }
     }
     rs += __shfl_xor(rs, 16);
@@ -307,10 +322,12 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
                   const void* k, int64_t skb, int64_t skh, int64_t skl,
                   const void* v, int64_t svb, int64_t svh, int64_t svl,
                   void* o, int64_t sob, int64_t soh, int64_t sol,
-                  float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws, int64_t ws_bytes,
-                  hipStream_t st) {
+                  float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, uint32_t* keep, void* ws,
+                  int64_t ws_bytes, hipStream_t st) {
   FlashArgs a = {};
   a.idx0 = idx0;
+  a.keep = p_drop > 0.f ? keep : nullptr;
+  a.kw = 2 * ((Lk + 63) / 64);
   a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
   a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;

@@ -37,6 +37,9 @@ struct FlashBwdArgs {
   int kv_splits, kv_tiles_per_split;  // dK/dV kernel: query range split over workgroups
   float* ws_dkv;  // [kv_splits][BH*Lk][2][DP] fp32 partial (dK, dV) (kv_splits > 1)
   uint64_t idx0;  // dropout element-index offset (single-frame launches)
+  // dropout keep bitmap of the forward (nullable; flash.hip layout: bit (k & 31) of word
+  // [(bh * Lq + q) * kw + k / 32]); read instead of re-hashing every element
+  const uint32_t* keep; int kw;
   // Frame table (nfr > 0): the batch is nfr frames x bpf batches, Q / O / dO / dQ / LSE uniform,
   // K / V / dK / dV PACKED per frame: batch bl of frame f has fr_lk[f] keys starting at row
   // fr_krow[f] + bl * fr_lk[f]; dropout indices of frame f start at fr_idx0[f] (the offsets its
@@ -45,26 +48,38 @@ struct FlashBwdArgs {
   int fr_lk[S2H_MAX_FRAMES];
   int64_t fr_krow[S2H_MAX_FRAMES];
   uint64_t fr_idx0[S2H_MAX_FRAMES];
+  int64_t fr_koff[S2H_MAX_FRAMES];  // word offset of frame f's keep bitmap
 };
+
+// The frame table is read straight from the kernarg segment (scalar loads): indexing the by-value
+// argument's arrays with a runtime frame made the compiler copy the whole struct (1.3 KB) into
+// per-lane scratch at every kernel start.
+typedef __attribute__((address_space(4))) const FlashBwdArgs KFlashBwdArgs;
+__device__ __forceinline__ KFlashBwdArgs* kargs() { return (KFlashBwdArgs*)__builtin_amdgcn_kernarg_segment_ptr(); }
 
 // K / V / dK / dV bases, key count and dropout index base (query 0) of batch-head bh
 struct KvFrame {
   const bf16* k; const bf16* v; bf16* dk; bf16* dv;
   int Lk;
   uint64_t drow0;
+  const uint32_t* keep;  // keep bitmap of query 0 of this batch-head (nullptr: hash)
+  int kw;                // its words per query row
 };
 __device__ __forceinline__ KvFrame kv_frame(const FlashBwdArgs& a, int bh) {
   const int b = bh / a.H, h = bh % a.H;
   KvFrame r;
   if (a.nfr > 0) {
     const int f = b / a.bpf, bl = b - f * a.bpf;
-    r.Lk = a.fr_lk[f];
-    const int64_t row = a.fr_krow[f] + (int64_t)bl * r.Lk;
+    KFlashBwdArgs* ka = kargs();
+    r.Lk = ka->fr_lk[f];
+    const int64_t row = ka->fr_krow[f] + (int64_t)bl * r.Lk;
     r.k = a.k + row * a.skl + h * a.skh;
     r.v = a.v + row * a.svl + h * a.svh;
     r.dk = a.dk + row * a.sdkl + h * a.sdkh;
     r.dv = a.dv + row * a.sdvl + h * a.sdvh;
-    r.drow0 = a.fr_idx0[f] + (uint64_t)(bl * a.H + h) * (uint64_t)a.Lq * (uint64_t)r.Lk;
+    r.drow0 = ka->fr_idx0[f] + (uint64_t)(bl * a.H + h) * (uint64_t)a.Lq * (uint64_t)r.Lk;
+    r.kw = 2 * ((r.Lk + 63) / 64);
+    r.keep = a.keep ? a.keep + ka->fr_koff[f] + (int64_t)(bl * a.H + h) * a.Lq * r.kw : nullptr;
   } else {
     r.Lk = a.Lk;
     r.k = a.k + b * a.skb + h * a.skh;
@@ -72,6 +87,8 @@ __device__ __forceinline__ KvFrame kv_frame(const FlashBwdArgs& a, int bh) {
     r.dk = a.dk + b * a.sdkb + h * a.sdkh;
     r.dv = a.dv + b * a.sdvb + h * a.sdvh;
     r.drow0 = a.idx0 + (uint64_t)bh * (uint64_t)a.Lq * (uint64_t)a.Lk;
+    r.kw = a.kw;
+    r.keep = a.keep ? a.keep + (int64_t)bh * a.Lq * a.kw : nullptr;
   }
   return r;
 }
@@ -102,7 +119,8 @@ template <int DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
   if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using C = FlashCfg<DP, 64>;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][K | V]
+  // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB + 2 * FL_WAVES * 256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int split = blockIdx.z;
@@ -116,10 +134,18 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   const int ntiles_all = (Lk + C::KT - 1) / C::KT;
   const int t0 = split * a.tiles_per_split;
   const int nt = min(ntiles_all, t0 + a.tiles_per_split) - t0;
+  // keep words of this wave's 16 queries for the 64 keys of a tile: lane 2i + j (< 32) fetches
+  // word j of query i (lanes 32..63 repeat them); LDS holds them as one uint2 per query
+  const bool bits = fr.keep != nullptr && a.p_drop > 0.f;
+  const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min((int)blockIdx.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
+                               : nullptr;
+  char* bits_lds = smem + 2 * 2 * C::TILEB + w * 256;
+  auto dma_bits = [&](int stage, int k0) { lds_dma4(KEEPQ + (k0 >> 5) + (lane & 1), bits_lds + stage * FL_WAVES * 256); };
 
   if (nt > 0) {
     dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane);
     dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane);
+    if (bits) dma_bits(0, t0 * C::KT);
   }
   const bool qv = q < a.Lq;
   bf16x8 qf[C::NT], gf[C::NT];
@@ -146,7 +172,12 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
       dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane);
       dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane);
-      wait_vmcnt<2 * C::PPW>();
+      if (bits) {
+        dma_bits((it + 1) & 1, k0 + C::KT);
+        wait_vmcnt<2 * C::PPW + 1>();
+      } else {
+        wait_vmcnt<2 * C::PPW>();
+      }
     } else {
       wait_vmcnt<0>();
     }
@@ -167,10 +198,20 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       }
     }
     const bool full = k0 + C::KT <= Lk;
+    uint32_t kwords[2] = {0u, 0u};
+    if (bits) {
+      const uint2 t2 = *(const uint2*)(bits_lds + (it & 1) * FL_WAVES * 256 + ql * 8);
+      kwords[0] = t2.x;
+      kwords[1] = t2.y;
+    }
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       bool kp[4] = {true, true, true, true};
-      if (a.p_drop > 0.f) {
+      if (bits) {
+        const uint32_t wd = kwords[kb >> 1] >> (16 * (kb & 1) + 4 * g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) kp[e] = (wd >> e) & 1u;
+      } else if (a.p_drop > 0.f) {
         const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
         if ((e0 & 1) == 0) {
           s2h_keep_pair(a.seed, e0 >> 1, a.thresh, kp[0], kp[1]);
@@ -375,7 +416,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   // own copy of the row constants).  K lives in LDS (read as the B operand of S = Q K^T),
   // V in registers: both in registers would leave too few for the rest at 512 per lane.
   using CK = FlashCfg<DP, NWV * 32, NWV>;
-  constexpr int STAGE = 2 * C::TILEB + NWV * 256;
+  constexpr int STAGE = 2 * C::TILEB + NWV * 512;  // + per wave [lse | Di | keep words (x2)]
   __shared__ __attribute__((aligned(1024))) char smem[CK::TILEB + 2 * STAGE];
   char* Kblk = smem;
   char* stages = smem + CK::TILEB;
@@ -401,12 +442,20 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   auto dma_rows = [&](char* stage, int q0) {
     const int qi = min(q0 + (lane & 31), a.Lq - 1);
     const float* src = (lane < 32 ? LSE : DI) + qi;
-    lds_dma4(src, stage + 2 * C::TILEB + w * 256);
+    lds_dma4(src, stage + 2 * C::TILEB + w * 512);
+  };
+  // keep words of this wave's 32 keys (word key / 32) for the 32 queries of a tile (lanes 32..63
+  // repeat lanes 0..31)
+  const bool bits = fr.keep != nullptr && a.p_drop > 0.f;
+  const uint32_t* KEEPW = bits ? fr.keep + min((int)blockIdx.x * NWV + w, fr.kw - 1) : nullptr;
+  auto dma_bits = [&](char* stage, int q0) {
+    lds_dma4(KEEPW + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * fr.kw, stage + 2 * C::TILEB + w * 512 + 256);
   };
   dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), fr.Lk, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
+  if (bits) dma_bits(stages, qbase);
   bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
@@ -423,13 +472,19 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     const int q0 = qbase + it * QT;
     char* Qb = stages + (it & 1) * STAGE;
     char* Gb = Qb + C::TILEB;
-    const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 256);  // [lse(32) | Di(32)]
+    const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 512);  // [lse(32) | Di(32) | keep(32)]
+    const uint32_t* kwd = (const uint32_t*)(rows + 64);
     if (it + 1 < nt) {
       char* Qn = stages + ((it + 1) & 1) * STAGE;
       dma_tile<DP, QT, NWV, true, 1>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
       dma_tile<DP, QT, NWV, true, 1>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
       dma_rows(Qn, q0 + QT);
-      wait_vmcnt<2 * C::PPW + 1>();
+      if (bits) {
+        dma_bits(Qn, q0 + QT);
+        wait_vmcnt<2 * C::PPW + 2>();
+      } else {
+        wait_vmcnt<2 * C::PPW + 1>();
+      }
     } else {
       wait_vmcnt<0>();
     }
@@ -453,11 +508,13 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       const float lse_r = rows[ql], di_r = rows[32 + ql];
       const float p = qi < a.Lq ? __builtin_amdgcn_exp2f(s[r] * a.sl2 - lse_r * FL_LOG2E) : 0.f;
       bool keep = true;
-      if (a.p_drop > 0.f) keep = s2h_keep(a.seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
-      const float pd = keep ? p * a.inv_keep : 0.f;
-      const float dpd = keep ? dp[r] * a.inv_keep : 0.f;
-      pdb[r >> 3][r & 7] = (bf16)pd;
-      dsb[r >> 3][r & 7] = (bf16)(p * (dpd - di_r));
+      if (bits) keep = (kwd[ql] >> kl) & 1u;
+      else if (a.p_drop > 0.f) keep = s2h_keep(a.seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
+      // dV accumulates the kept P unscaled (x 1/keep at the store); dS = P (keep dP / keep_p - Di)
+      const float pk = keep ? p : 0.f;
+      const float dpd = keep ? dp[r] : 0.f;
+      pdb[r >> 3][r & 7] = (bf16)pk;
+      dsb[r >> 3][r & 7] = (bf16)(p * fmaf(dpd, a.inv_keep, -di_r));
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -480,7 +537,8 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       for (int G4 = 0; G4 < 4; ++G4) {
         const int d0 = 32 * d + 8 * G4 + 4 * hi;
         *(float4*)(W + d0) = float4{dk[d][4 * G4], dk[d][4 * G4 + 1], dk[d][4 * G4 + 2], dk[d][4 * G4 + 3]};
-        *(float4*)(W + DP + d0) = float4{dv[d][4 * G4], dv[d][4 * G4 + 1], dv[d][4 * G4 + 2], dv[d][4 * G4 + 3]};
+        *(float4*)(W + DP + d0) = float4{dv[d][4 * G4] * a.inv_keep, dv[d][4 * G4 + 1] * a.inv_keep,
+                                         dv[d][4 * G4 + 2] * a.inv_keep, dv[d][4 * G4 + 3] * a.inv_keep};
       }
     return;
   }
@@ -494,7 +552,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         tk[e] = (bf16)(dk[d][4 * G4 + e] * a.scale);
-        tv[e] = (bf16)dv[d][4 * G4 + e];
+        tv[e] = (bf16)(dv[d][4 * G4 + e] * a.inv_keep);
       }
       const int d0 = 32 * d + 8 * G4 + 4 * hi;
       *(uint2*)(DK + d0) = *(const uint2*)tk;
@@ -590,10 +648,13 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
                   void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql,
                   void* dk, int64_t sdkb, int64_t sdkh, int64_t sdkl,
                   void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
-                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0, void* ws,
-                  int64_t ws_bytes, hipStream_t st) {
+                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0,
+                  const uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st) {
   FlashBwdArgs a = {};
   a.idx0 = idx0;
+  if (keep && D != 256) return (int)hipErrorInvalidValue;  // the head-dim-256 kernels read the bitmap
+  a.keep = keep;
+  a.kw = 2 * ((Lk + 63) / 64);
   a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
   a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;
@@ -632,7 +693,9 @@ int s2h_flash_bwd_eligible(int dt, int Lq, int D) { return s2h_flash_eligible(dt
 // Frame-batched backward: nfr frames x bpf batches x H heads in ONE launch per kernel.  Q / O /
 // dO / dQ / LSE are [nfr * bpf] uniform batches (batch stride sqb ...); K / V / dK / dV are
 // packed per frame (frame f: bpf blocks of fr_lk[f] rows from row fr_krow[f]; row stride skl,
-// head stride skh); dropout indices of frame f start at fr_idx0[f].  nfr * bpf * (Lq / 128)
+// head stride skh); dropout indices of frame f start at fr_idx0[f]; keep (nullable) holds frame
+// f's forward keep bitmap from word fr_koff[f] (flash.hip layout: bpf * H * Lq rows of
+// 2 * ceil(fr_lk[f] / 64) words).  nfr * bpf * (Lq / 128)
 // query blocks fill the chip without key or query splits, so no fp32 partials or combines.
 extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk, const int64_t* fr_krow,
                                     const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
@@ -641,15 +704,18 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
                                     int64_t sgb, int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh,
                                     int64_t sdql, void* dk, int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh,
                                     int64_t sdvl, const float* lse, float* di_ws, float scale, float p_drop,
-                                    uint64_t seed, hipStream_t st) {
+                                    uint64_t seed, const uint32_t* keep, const int64_t* fr_koff, hipStream_t st) {
   if (nfr <= 0 || bpf <= 0 || H <= 0 || Lq <= 0) return 0;
   if (nfr > S2H_MAX_FRAMES || !(D == 128 || D == 256) || Lq < 128) return (int)hipErrorInvalidValue;
+  if (keep && (D != 256 || fr_koff == nullptr)) return (int)hipErrorInvalidValue;
   FlashBwdArgs a = {};
   a.nfr = nfr; a.bpf = bpf;
+  a.keep = keep;
   int lk_max = 0;
   for (int f = 0; f < nfr; ++f) {
     if (fr_lk[f] <= 0) return (int)hipErrorInvalidValue;
     a.fr_lk[f] = fr_lk[f]; a.fr_krow[f] = fr_krow[f]; a.fr_idx0[f] = fr_idx0[f];
+    a.fr_koff[f] = keep ? fr_koff[f] : 0;
     lk_max = std::max(lk_max, fr_lk[f]);
   }
   a.BH = nfr * bpf * H; a.H = H; a.Lq = Lq; a.Lk = lk_max;

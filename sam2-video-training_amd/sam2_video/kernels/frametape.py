@@ -109,6 +109,20 @@ class Store:
         return self.buf.view(F, *self.shape0)
 
 
+class FlatStore:
+    """a saved per-frame buffer of explicit per-frame element counts (flat, frame f from offsets[f])"""
+
+    def __init__(self, tape, numels, dtype):
+        self.numels = [int(n) for n in numels]
+        self.offsets = [0]
+        for n in self.numels[:-1]:
+            self.offsets.append(self.offsets[-1] + n)
+        self.buf = torch.empty(sum(self.numels), device=tape.device, dtype=dtype)
+
+    def frame(self, f):
+        return self.buf[self.offsets[f]:self.offsets[f] + self.numels[f]]
+
+
 class Op:
     __slots__ = ("kind", "idx", "ins", "outs", "attrs", "fattrs", "saved", "needs", "bw")
 
@@ -220,6 +234,24 @@ class FrameTape:
         if self.f == 0:
             self.stores[key] = Store(self, shape, dtype, scale=scale)
         return self.stores[key].frame(self.f)
+
+    def _aux_flat(self, name, numels, dtype):
+        """frame-stacked saved flat buffer of the current op with per-frame sizes `numels` (all frames)"""
+        key = ("aux", self.k, name)
+        if self.f == 0:
+            self.stores[key] = FlatStore(self, numels, dtype)
+        return self.stores[key].frame(self.f)
+
+    def _keep_bits(self, q, Lk, kvid, p_drop):
+        """dropout keep bitmap slot of this frame's attention (None: the kernels re-hash), sized for
+        every frame's key count (packed per frame when the key value `kvid` follows the memory rows)"""
+        if not ops.keep_bits_ok(q, p_drop):
+            return None
+        B, Lq, H, _ = q.shape
+        st = self.stores.get(kvid) if kvid is not None else None
+        scale = st.scale if st is not None and not st.uniform else None
+        lks = [Lk] * self.F if scale is None else [Lk * sc // scale[self.f] for sc in scale]
+        return self._aux_flat("keep", [ops.keep_words(B, H, Lq, lk) for lk in lks], torch.int32)
 
     def _begin(self, kind, ins, bw, attrs=None):
         """start op `kind` at the current frame; returns (op, is_first_frame)"""
@@ -420,10 +452,11 @@ def attention(tape: FrameTape, q, k, v, scale, p_drop):
     lse = tape._aux("lse", (B, H, Lq), torch.float32)
     seed = tape._seed() if p_drop > 0 else 0
     idx0 = tape._idx0(op, B * H * Lq * Lk)
-    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0)
+    keep = tape._keep_bits(q, Lk, op.ins[1], p_drop)
+    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0, keep=keep)
     tape._fattr(op, "Lk", Lk)
     if first:
-        op.attrs.update(seed=seed, B=B, Lq=Lq, H=H, D=D, qshape=tuple(q.shape))
+        op.attrs.update(seed=seed, B=B, Lq=Lq, H=H, D=D, qshape=tuple(q.shape), keep=keep is not None)
     tape._finish(op, [vid], any(op.needs))
     return o
 
@@ -437,10 +470,13 @@ def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_
     for f in range(F - 1):
         krow.append(krow[-1] + B * lks[f])
     k_rows, v_rows, dk_rows, dv_rows = kview
+    ks = tape.stores[("aux", op.idx, "keep")] if a.get("keep") else None
     if ops.flash_bwd_eligible(q_all):
         ops.flash_bwd_frames(F, B, lks, krow, op.fattrs["idx0"], q_all, k_rows, v_rows, o_all, go, lse, dq,
-                             dk_rows, dv_rows, a["scale"], a["p"], a["seed"])
+                             dk_rows, dv_rows, a["scale"], a["p"], a["seed"], keep=ks.buf if ks else None,
+                             koff=ks.offsets if ks else None)
         return
+    assert ks is None, "keep bitmap written but the flash backward is not eligible"
     if len(set(lks)) == 1:
         # uniform key count: the frames ARE one [F*B] batch (frame f's dropout indices start at
         # f*B*H*Lq*Lk, where its forward put them)
@@ -490,10 +526,11 @@ def qkv_attention(tape: FrameTape, qkv, scale, p_drop, rope):
     lse = tape._aux("lse", (B, H, L), torch.float32)
     seed = tape._seed() if p_drop > 0 else 0
     idx0 = tape._idx0(op, B * H * L * L)
-    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0)
+    keep = tape._keep_bits(q, L, None, p_drop)
+    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0, keep=keep)
     tape._fattr(op, "Lk", L)
     if first:
-        op.attrs.update(seed=seed, B=B, Lq=L, H=H, D=D)
+        op.attrs.update(seed=seed, B=B, Lq=L, H=H, D=D, keep=keep is not None)
     tape._finish(op, [vid], any(op.needs))
     return o
 

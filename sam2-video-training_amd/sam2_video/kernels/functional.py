@@ -131,6 +131,15 @@ def add_layer_norm(x, add, mod, eps):
 
 
 # ------------------------------------------------------------- attention
+def _keep_buffer(ctx, q, Lk, p_drop, nin):
+    """dropout keep bitmap of a training attention on the flash path (the backward reads it
+    instead of re-hashing every element); None otherwise"""
+    if not any(ctx.needs_input_grad[:nin]) or not ops.keep_bits_ok(q, p_drop):
+        return None
+    B, Lq, H, _ = q.shape
+    return torch.empty(ops.keep_words(B, H, Lq, Lk), device=q.device, dtype=torch.int32)
+
+
 class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, scale, p_drop):
@@ -138,8 +147,9 @@ class _Attention(torch.autograd.Function):
         o = torch.empty(B, Lq, H, D, device=q.device, dtype=q.dtype)
         lse = torch.empty(B, H, Lq, device=q.device, dtype=torch.float32)
         seed = next_seed() if p_drop > 0 else 0
-        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed)
-        ctx.scale, ctx.p, ctx.seed = scale, p_drop, seed
+        keep = _keep_buffer(ctx, q, k.shape[1], p_drop, 3)
+        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, keep=keep)
+        ctx.scale, ctx.p, ctx.seed, ctx.keep = scale, p_drop, seed, keep
         ctx.save_for_backward(q, k, v, o, lse)
         return o
 
@@ -150,7 +160,8 @@ class _Attention(torch.autograd.Function):
         dq = torch.empty(q.shape, device=q.device, dtype=q.dtype)
         dk = torch.empty(k.shape, device=k.device, dtype=k.dtype)
         dv = torch.empty(v.shape, device=v.device, dtype=v.dtype)
-        ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed)
+        ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed, keep=ctx.keep)
+        ctx.keep = None
         return dq, dk, dv, None, None
 
 
@@ -186,8 +197,9 @@ class _QKVAttention(torch.autograd.Function):
         o = torch.empty(B, L, H, D, device=qkv.device, dtype=qkv.dtype)
         lse = torch.empty(B, H, L, device=qkv.device, dtype=torch.float32)
         seed = next_seed() if p_drop > 0 else 0
-        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed)
-        ctx.scale, ctx.p, ctx.seed, ctx.rope = scale, p_drop, seed, rope
+        keep = _keep_buffer(ctx, q, L, p_drop, 1)
+        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, keep=keep)
+        ctx.scale, ctx.p, ctx.seed, ctx.rope, ctx.keep = scale, p_drop, seed, rope, keep
         ctx.save_for_backward(qkv, qk if rope is not None else qkv, o, lse)
         return o
 
@@ -199,7 +211,8 @@ class _QKVAttention(torch.autograd.Function):
         v = qkv[:, :, 2]
         dqkv = torch.empty(qkv.shape, device=qkv.device, dtype=qkv.dtype)
         dq, dk, dv = dqkv[:, :, 0], dqkv[:, :, 1], dqkv[:, :, 2]
-        ops.attn_bwd(q, k, v, o, do.contiguous(), lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed)
+        ops.attn_bwd(q, k, v, o, do.contiguous(), lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed, keep=ctx.keep)
+        ctx.keep = None
         if ctx.rope is not None:
             cos, sin, period = ctx.rope
             for g in (dq, dk):

@@ -146,20 +146,39 @@ def _bhl(t):
     return t.stride(0), t.stride(2), t.stride(1)
 
 
-def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0, idx0=0):
-    """q [B, Lq, H, D], k/v [B, Lk, H, D] (any strides, D contiguous) -> o [B, Lq, H, D], lse [B, H, Lq] f32"""
+def keep_bits_ok(q, p_drop):
+    """the flash forward writes (and the flash backward reads) a dropout keep bitmap for this
+    attention: dropout on, bf16 head_dim 256 flash path"""
+    return p_drop > 0 and q.shape[-1] == 256 and flash_bwd_eligible(q)
+
+
+def keep_words(B, H, Lq, Lk):
+    """int32 words of one launch's keep bitmap (s2h_attn_keep_words)"""
+    return B * H * Lq * 2 * ((Lk + 63) // 64)
+
+
+def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0, idx0=0, keep=None):
+    """q [B, Lq, H, D], k/v [B, Lk, H, D] (any strides, D contiguous) -> o [B, Lq, H, D], lse [B, H, Lq] f32;
+    keep: optional int32 [keep_words(...)] receiving the dropout keep bitmap (keep_bits_ok)"""
     _dev(q, k, v, o, lse)
     B, Lq, H, D = q.shape
     Lk = k.shape[1]
     nws = lib().s2h_attn_fwd_ws_bytes(dt(q), B, H, Lq, Lk, D)
     ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
     call("s2h_attn_fwd", dt(q), B, H, Lq, Lk, D, ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v),
-         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0), ptr(ws),
-         int(nws), stream())
+         ptr(o), *_bhl(o), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0),
+         _keep_ptr(keep, B, H, Lq, Lk), ptr(ws), int(nws), stream())
     return o, lse
 
 
-def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0, idx0=0):
+def _keep_ptr(keep, B, H, Lq, Lk):
+    if keep is None:
+        return None
+    assert keep.dtype == torch.int32 and keep.is_contiguous() and keep.numel() >= keep_words(B, H, Lq, Lk)
+    return ptr(keep)
+
+
+def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0, idx0=0, keep=None):
     _dev(q, k, v, o, do, lse, dq, dk, dv)
     B, Lq, H, D = q.shape
     Lk = k.shape[1]
@@ -169,8 +188,8 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0, idx0=0)
     call("s2h_attn_bwd", dt(q), B, H, Lq, Lk, D,
          ptr(q), *_bhl(q), ptr(k), *_bhl(k), ptr(v), *_bhl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
          ptr(dq), *_bhl(dq), ptr(dk), *_bhl(dk), ptr(dv), *_bhl(dv),
-         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0), ptr(ws), int(nws),
-         stream())
+         ptr(lse), ptr(di), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0),
+         _keep_ptr(keep, B, H, Lq, Lk), ptr(ws), int(nws), stream())
     return dq, dk, dv
 
 
@@ -180,10 +199,12 @@ def flash_bwd_eligible(q):
     return bool(lib().s2h_flash_bwd_ok(dt(q), q.shape[1], q.shape[-1]))
 
 
-def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, scale, p_drop, seed):
+def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, scale, p_drop, seed, keep=None,
+                     koff=None):
     """Frame-batched flash backward (s2h_flash_bwd_frames): q/o/do/dq [nfr*bpf, Lq, H, D] views,
     k/v/dk/dv PACKED [rows, H, D] views (frame f: bpf blocks of lk[f] rows from row krow[f]),
-    lse [nfr*bpf, H, Lq]; frame f's dropout indices start at idx0[f]."""
+    lse [nfr*bpf, H, Lq]; frame f's dropout indices start at idx0[f]; keep (optional int32) holds
+    frame f's forward keep bitmap from word koff[f]."""
     import ctypes
     _dev(q, k, v, o, do, lse, dq, dk, dv)
     B, Lq, H, D = q.shape
@@ -192,6 +213,12 @@ def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, 
     alk = (ctypes.c_int * nfr)(*[int(x) for x in lk])
     akr = (ctypes.c_int64 * nfr)(*[int(x) for x in krow])
     aix = (ctypes.c_uint64 * nfr)(*[int(x) & (2**64 - 1) for x in idx0])
+    kp = None
+    if keep is not None:
+        assert keep.dtype == torch.int32 and len(koff) == nfr
+        assert all(int(koff[f]) + keep_words(bpf, H, Lq, lk[f]) <= keep.numel() for f in range(nfr))
+        ako = (ctypes.c_int64 * nfr)(*[int(x) for x in koff])
+        kp = ptr(keep)
 
     def hl(t):  # (head, row) strides of a packed [rows, H, D] view
         assert t.stride(-1) == 1
@@ -200,7 +227,7 @@ def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, 
          ctypes.cast(akr, ctypes.c_void_p).value, ctypes.cast(aix, ctypes.c_void_p).value,
          ptr(q), *_bhl(q), ptr(k), *hl(k), ptr(v), *hl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
          ptr(dq), *_bhl(dq), ptr(dk), *hl(dk), ptr(dv), *hl(dv), ptr(lse), ptr(di), float(scale), float(p_drop),
-         int(seed) & (2**64 - 1), stream())
+         int(seed) & (2**64 - 1), kp, ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None, stream())
     return dq, dk, dv
 
 

@@ -4,6 +4,7 @@ order (dropout off), so outputs agree to the bit and gradients up to summation o
 frame-table flash backward kernel against per-frame launches (dropout on, same masks)."""
 import math
 
+import numpy as np
 import pytest
 import torch
 
@@ -104,3 +105,67 @@ def test_flash_bwd_frames_matches_per_frame(p_drop):
     for a, b in ((dq, dq_ref), (dk, dk_ref), (dv, dv_ref)):
         err = (a.float() - b.float()).abs().max().item()
         assert err <= 2e-2 * b.float().abs().max().item(), err
+
+
+def test_keep_bitmap_backward_equals_rehash():
+    """the flash forward's dropout keep bitmap (s2h_attn_fwd keep) read by the backward gives the
+    same gradients, bit for bit, as re-hashing every element: single launches (Lk not a multiple
+    of 64) and the frame-table launch over packed per-frame bitmaps"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(1)
+    B, Lq, H, D, p, seed = 3, 256, 1, 256, 0.1, 777
+    lks = [1028, 300, 2056]
+    F = len(lks)
+    dt = torch.bfloat16
+    q = (torch.randn(F * B, Lq, H, D, device="cuda") * 0.5).to(dt)
+    do = torch.randn(F * B, Lq, H, D, device="cuda").to(dt)
+    rows = sum(B * lk for lk in lks)
+    k = (torch.randn(rows, H, D, device="cuda") * 0.5).to(dt)
+    v = torch.randn(rows, H, D, device="cuda").to(dt)
+    scale = 1.0 / math.sqrt(D)
+    assert ops.keep_bits_ok(q, p)
+    nw = [ops.keep_words(B, H, Lq, lk) for lk in lks]
+    koff = [sum(nw[:f]) for f in range(F)]
+    keep = torch.full((sum(nw),), -1, device="cuda", dtype=torch.int32)
+    o, o2 = torch.empty_like(q), torch.empty_like(q)
+    lse, lse2 = torch.empty(F * B, H, Lq, device="cuda"), torch.empty(F * B, H, Lq, device="cuda")
+    krow, idx0, r, n = [], [], 0, 0
+    for f, lk in enumerate(lks):
+        krow.append(r)
+        idx0.append(n)
+        sl = slice(f * B, (f + 1) * B)
+        kf, vf = k[r:r + B * lk].view(B, lk, H, D), v[r:r + B * lk].view(B, lk, H, D)
+        ops.attn_fwd(q[sl], kf, vf, o[sl], lse[sl], scale, p, seed, idx0=n, keep=keep[koff[f]:koff[f] + nw[f]])
+        ops.attn_fwd(q[sl], kf, vf, o2[sl], lse2[sl], scale, p, seed, idx0=n)
+        r += B * lk
+        n += B * H * Lq * lk
+    torch.cuda.synchronize()
+    assert torch.equal(o, o2) and torch.equal(lse, lse2)
+    # kept fraction over valid keys ~ 1 - p
+    for f, lk in enumerate(lks):
+        words = keep[koff[f]:koff[f] + nw[f]].view(B * H * Lq, -1).cpu().numpy().view("uint32")
+        bits = ((words[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(B * H * Lq, -1)[:, :lk]
+        assert abs(bits.mean() - (1 - p)) < 0.01, bits.mean()
+    # single launches: bitmap vs re-hash
+    for f, lk in enumerate(lks):
+        sl = slice(f * B, (f + 1) * B)
+        r0, r1 = krow[f], krow[f] + B * lk
+        kf, vf = k[r0:r1].view(B, lk, H, D), v[r0:r1].view(B, lk, H, D)
+        outs = []
+        for kp in (keep[koff[f]:koff[f] + nw[f]], None):
+            g = (torch.empty_like(q[sl]), torch.empty_like(kf), torch.empty_like(vf))
+            ops.attn_bwd(q[sl], kf, vf, o[sl], do[sl], lse[sl], *g, scale, p, seed, idx0=idx0[f], keep=kp)
+            outs.append(g)
+        torch.cuda.synchronize()
+        for a, b in zip(*outs):
+            assert torch.equal(a, b), f"frame {f}: {(a.float() - b.float()).abs().max().item()}"
+    # frame table: bitmap vs re-hash
+    outs = []
+    for kp in (keep, None):
+        g = (torch.empty_like(q), torch.empty_like(k), torch.empty_like(v))
+        ops.flash_bwd_frames(F, B, lks, krow, idx0, q, k, v, o, do, lse, *g, scale, p, seed, keep=kp,
+                             koff=koff if kp is not None else None)
+        outs.append(g)
+    torch.cuda.synchronize()
+    for a, b in zip(*outs):
+        assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
