@@ -202,6 +202,10 @@ int s2h_dropout(int dt, int64_t n, const void* a, const void* b, float p, uint64
  * act -> dropout (memory_attention.py:95-98); x_pre NULL = no activation. */
 int s2h_act_dropout_bwd(int dt, int64_t n, const void* x_pre, const void* dy, int act, float p, uint64_t seed,
                         uint64_t idx0, void* dx, hipStream_t st);
+/* dx = scale * [y > 0] * dy: the backward of ReLU (-> dropout, scale = 1/(1-p)) from the layer's
+ * output y, which is positive exactly where the pre-activation was and the element was kept
+ * (memory_attention.py:95-98 linear1 + ReLU + dropout; no pre-activation stored, no re-hash). */
+int s2h_relu_mask_bwd(int dt, int64_t n, const void* y, const void* dy, float scale, void* dx, hipStream_t st);
 /* Axial rotary embedding of the first `nrot` rows of each batch (cos/sin tables
  * [period, D/2], row r uses entry r % period; inverse = 1 applies the transpose
  * rotation for the backward).  Replaces apply_rotary_enc (position_encoding.py:212-239)

@@ -54,6 +54,7 @@ SIGNATURES = {
     "s2h_cast": [I, I, L, P, P, P],
     "s2h_dropout": [I, L, P, P, F, c_uint64, c_uint64, P, P],
     "s2h_act_dropout_bwd": [I, L, P, P, I, F, c_uint64, c_uint64, P, P],
+    "s2h_relu_mask_bwd": [I, L, P, P, F, P, P],
     "s2h_rope": [I, L, I, I, P, L, L, P, L, L, P, P, I, I, P],
     "s2h_maxpool2_fwd": [I, I, I, I, I, P, L, P, P],
     "s2h_maxpool2_bwd": [I, I, I, I, I, P, L, P, P, L, P],

@@ -25,6 +25,7 @@ module code is shared with the autograd path.  Test infrastructure compares both
 """
 from __future__ import annotations
 
+import collections
 import math
 from typing import Dict, List, Optional
 
@@ -304,6 +305,10 @@ class FrameTape:
         """out_grads: value id -> stacked gradient.  Returns {input name: stacked gradient}."""
         G = dict(out_grads)
         owned = set()
+        self.producer = {v: op for op in self.ops for v in op.outs}
+        self.nuse = collections.Counter(v for op in self.ops for v in op.ins if v is not None)
+        self.premasked = set()
+        self.seeded = set(out_grads)
 
         def acc(vid, g):
             if vid is None or g is None:
@@ -351,7 +356,11 @@ def _empty_like_store(tape, st: Store, dtype=None):
 # ---------------------------------------------------------------- linear
 def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0):
     x = x if x.is_contiguous() else x.contiguous()
-    op, first = tape._begin("linear", [x, residual], _linear_bw, {"mod": mod, "act": act, "p": float(drop_p)})
+    # ReLU without residual: the backward masks with the output (> 0 exactly where the
+    # pre-activation was positive and the element kept), so no pre-activation is stored
+    relu_out = act == "relu" and residual is None
+    op, first = tape._begin("linear", [x, residual], _linear_bw,
+                            {"mod": mod, "act": act, "p": float(drop_p), "relu_out": relu_out})
     if first and tape.vid(x) is None:
         raise RuntimeError("tape linear: input must be a recorded value or declared input")
     w = mod.compute_weight()
@@ -360,7 +369,7 @@ def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0):
     scale = tape._varlen_scale(x)
     shape = (*x.shape[:-1], N)
     vid, out = tape._out(0, shape, x.dtype, scale)
-    pre = tape._aux("pre", shape, x.dtype, scale) if act else None
+    pre = tape._aux("pre", shape, x.dtype, scale) if act and not relu_out else None
     seed = tape._seed() if drop_p > 0 else 0
     idx0 = tape._idx0(op, out.numel())
     ops.linear(x, w, b, act=act, out=out, pre=pre, residual=residual, drop_p=drop_p, seed=seed, drop_idx0=idx0)
@@ -376,7 +385,11 @@ def _linear_bw(tape, op, gys):
     mod, act, p = op.attrs["mod"], op.attrs["act"], op.attrs["p"]
     N, K = mod.compute_weight().shape
     gy2 = gy.view(-1, N)
-    if p > 0:
+    if op.outs[0] in tape.premasked:  # the consumer's dgrad already applied ReLU' and 1/keep
+        dpre = gy2
+    elif op.attrs["relu_out"]:
+        dpre = ops.relu_mask_bwd(_flat(tape.st(op.outs[0]), N), gy2, 1.0 / (1.0 - p))
+    elif p > 0:
         pre = tape.stores[("aux", op.idx, "pre")] if act else None
         dpre = ops.act_dropout_bwd(_flat(pre, N) if act else None, gy2, act, p, op.attrs["seed"])
     elif act:
@@ -390,7 +403,17 @@ def _linear_bw(tape, op, gys):
         ops.linear_wgrad(dpre, x2, gw.view(gw.shape[0], -1), db=gb)
     elif gb is not None:
         ops.colsum(dpre, gb)
-    dx = ops.linear_dgrad(dpre, mod.compute_weight()).view(-1) if op.needs[0] else None
+    dx = None
+    if op.needs[0]:
+        prod = tape.producer.get(op.ins[0])
+        if prod is not None and prod.kind == "linear" and prod.attrs["relu_out"] and tape.nuse[op.ins[0]] == 1 \
+                and op.ins[0] not in tape.seeded:
+            # sole consumer of a ReLU (-> dropout) linear: its mask and 1/keep fused into this dgrad
+            pp = prod.attrs["p"]
+            dx = ops.linear_dgrad(dpre, mod.compute_weight(), pre=x2, act="relu", alpha=1.0 / (1.0 - pp)).view(-1)
+            tape.premasked.add(op.ins[0])
+        else:
+            dx = ops.linear_dgrad(dpre, mod.compute_weight()).view(-1)
     dres = gy if op.needs[1] else None
     return [dx, dres]
 

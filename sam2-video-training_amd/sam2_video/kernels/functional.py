@@ -46,12 +46,14 @@ class _Linear(torch.autograd.Function):
     def forward(ctx, x, wp, bp, mod, act, residual, drop_p):
         w = mod.compute_weight()
         b = mod.compute_bias()
-        pre = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype) if act else None
+        # ReLU without residual: the backward masks with the output itself (no pre-activation)
+        relu_out = act == "relu" and residual is None
+        pre = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype) if act and not relu_out else None
         seed = next_seed() if drop_p > 0 else 0
         out = ops.linear(x, w, b, act=act, pre=pre, residual=residual, drop_p=drop_p, seed=seed)
-        ctx.mod, ctx.act, ctx.drop_p, ctx.seed = mod, act, drop_p, seed
+        ctx.mod, ctx.act, ctx.drop_p, ctx.seed, ctx.relu_out = mod, act, drop_p, seed, relu_out
         ctx.has_res = residual is not None
-        ctx.save_for_backward(x, pre)
+        ctx.save_for_backward(x, out if relu_out else pre)
         return out
 
     @staticmethod
@@ -59,7 +61,9 @@ class _Linear(torch.autograd.Function):
         x, pre = ctx.saved_tensors
         mod = ctx.mod
         dy = dy.contiguous()
-        if ctx.drop_p > 0:
+        if ctx.relu_out:
+            dpre = ops.relu_mask_bwd(pre, dy, 1.0 / (1.0 - ctx.drop_p))
+        elif ctx.drop_p > 0:
             dpre = ops.act_dropout_bwd(pre if ctx.act else None, dy, ctx.act, ctx.drop_p, ctx.seed)
         else:
             dpre = ops.act_bwd(pre, dy, ctx.act) if ctx.act else dy

@@ -94,8 +94,9 @@ def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dty
     return out
 
 
-def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None):
-    """dx = dy @ w   (optionally * act'(pre) elementwise, fusing the previous layer's activation grad)."""
+def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0):
+    """dx = alpha * dy @ w   (optionally * act'(pre) elementwise, fusing the previous layer's
+    activation grad; for ReLU `pre` may be the previous layer's output, and alpha its 1/keep)."""
     dy2 = dy.reshape(-1, dy.shape[-1])
     M, N = dy2.shape
     K = w.shape[1]
@@ -105,7 +106,7 @@ def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None):
     p2 = pre.reshape(-1, K) if pre is not None else None
     gemm(dy2, w, d2, M=M, N=K, K=N, lda_m=dy2.stride(0), lda_k=1, ldb_k=K, ldb_n=1, ldc=K,
          aux=p2, ldx=K, aux_mode=2 if pre is not None else 0, act=ACT[act] if pre is not None else 0,
-         beta=1.0 if accumulate else 0.0)
+         alpha=alpha, beta=1.0 if accumulate else 0.0)
     return dx
 
 
@@ -295,6 +296,15 @@ def act_dropout_bwd(x_pre, dy, act, p, seed, dx=None, idx0=0):
         dx = torch.empty_like(dy)
     call("s2h_act_dropout_bwd", dt(dy), dy.numel(), ptr(x_pre), ptr(dy), ACT[act], float(p), int(seed) & (2**64 - 1),
          int(idx0), ptr(dx), stream())
+    return dx
+
+
+def relu_mask_bwd(y, dy, scale=1.0, dx=None):
+    """dx = scale * [y > 0] * dy -- ReLU (-> dropout) backward from the layer output y"""
+    assert y.is_contiguous() and dy.is_contiguous() and y.numel() == dy.numel() and y.dtype == dy.dtype
+    if dx is None:
+        dx = torch.empty_like(dy)
+    call("s2h_relu_mask_bwd", dt(dy), dy.numel(), ptr(y), ptr(dy), float(scale), ptr(dx), stream())
     return dx
 
 

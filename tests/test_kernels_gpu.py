@@ -597,6 +597,32 @@ def test_act_dropout_bwd_fused(dtype, act):
     _close(got, ref, 1e-2 if dtype == torch.bfloat16 else 1e-6)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_relu_mask_bwd_from_output(dtype, p):
+    """ReLU -> dropout backward from the layer OUTPUT (s2h_relu_mask_bwd, and fused into the next
+    layer's dgrad epilogue with alpha = 1/keep) == the pre-activation + re-hash backward
+    (s2h_act_dropout_bwd) of the same linear epilogue"""
+    ops = _ops()
+    torch.manual_seed(5)
+    M, K, N, N2 = 1000, 64, 136, 48
+    x = torch.randn(M, K, device=DEV).to(dtype)
+    w = (torch.randn(N, K, device=DEV) * 0.2).to(dtype)
+    b = torch.randn(N, device=DEV) * 0.1
+    pre = torch.empty(M, N, device=DEV, dtype=dtype)
+    out = ops.linear(x, w, b, act="relu", pre=pre, drop_p=p, seed=99)
+    dy = torch.randn(M, N, device=DEV).to(dtype)
+    ref = ops.act_dropout_bwd(pre, dy, "relu", p, 99) if p > 0 else ops.act_bwd(pre, dy, "relu")
+    got = ops.relu_mask_bwd(out, dy, 1.0 / (1.0 - p))
+    _close(got, ref, 1e-6 if dtype == torch.float32 else 1e-2)
+    # fused into the consumer's dgrad: dh = (dz @ w2) masked by out > 0, times 1/keep
+    w2 = (torch.randn(N2, N, device=DEV) * 0.2).to(dtype)
+    dz = torch.randn(M, N2, device=DEV).to(dtype)
+    fused = ops.linear_dgrad(dz, w2, pre=out, act="relu", alpha=1.0 / (1.0 - p))
+    plain = ops.relu_mask_bwd(out, ops.linear_dgrad(dz, w2), 1.0 / (1.0 - p))
+    _close(fused, plain, 1e-5 if dtype == torch.float32 else 2e-2)
+
+
 @pytest.mark.parametrize("max_norm,grad_scale", [(1.0, 1.0), (1.0, 0.5), (0.1, 0.25), (0.0, 0.5)])
 def test_clip_adamw_matches_torch(max_norm, grad_scale):
     """s2h_grad_norm + s2h_adamw (ArenaAdamW) == clip_grad_norm_ + torch.optim.AdamW on the
