@@ -114,10 +114,14 @@ __global__ __launch_bounds__(256) void flash_bwd_di_kernel(FlashBwdArgs a) {
   if (lane == 0) a.di[row] = s;
 }
 
+// dropout handling of the backward kernels (a template parameter: a runtime test per element
+// made the compiler branch around every element's exp2 / hash, SALU + exec churn in the loop)
+enum { DROP_NONE = 0, DROP_BITS = 1, DROP_HASH = 2 };
+
 // ------------------------------------------------------------------ dQ
-template <int DP>
+template <int DP, int DROP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
-  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
+  const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   using C = FlashCfg<DP, 64>;
   // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB + 2 * FL_WAVES * 256];
@@ -136,7 +140,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   const int nt = min(ntiles_all, t0 + a.tiles_per_split) - t0;
   // keep words of this wave's 16 queries for the 64 keys of a tile: lane 2i + j (< 32) fetches
   // word j of query i (lanes 32..63 repeat them); LDS holds them as one uint2 per query
-  const bool bits = fr.keep != nullptr && a.p_drop > 0.f;
+  constexpr bool bits = DROP == DROP_BITS;
   const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min((int)blockIdx.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
                                : nullptr;
   char* bits_lds = smem + 2 * 2 * C::TILEB + w * 256;
@@ -145,7 +149,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   if (nt > 0) {
     dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane);
     dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane);
-    if (bits) dma_bits(0, t0 * C::KT);
+    if constexpr (bits) dma_bits(0, t0 * C::KT);
   }
   const bool qv = q < a.Lq;
   bf16x8 qf[C::NT], gf[C::NT];
@@ -172,7 +176,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
       dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane);
       dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane);
-      if (bits) {
+      if constexpr (bits) {
         dma_bits((it + 1) & 1, k0 + C::KT);
         wait_vmcnt<2 * C::PPW + 1>();
       } else {
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     }
     const bool full = k0 + C::KT <= Lk;
     uint32_t kwords[2] = {0u, 0u};
-    if (bits) {
+    if constexpr (bits) {
       const uint2 t2 = *(const uint2*)(bits_lds + (it & 1) * FL_WAVES * 256 + ql * 8);
       kwords[0] = t2.x;
       kwords[1] = t2.y;
@@ -207,26 +211,30 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       bool kp[4] = {true, true, true, true};
-      if (bits) {
+      if constexpr (bits) {
         const uint32_t wd = kwords[kb >> 1] >> (16 * (kb & 1) + 4 * g);
 #pragma unroll
         for (int e = 0; e < 4; ++e) kp[e] = (wd >> e) & 1u;
-      } else if (a.p_drop > 0.f) {
+      } else if constexpr (DROP == DROP_HASH) {
         const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
         if ((e0 & 1) == 0) {
-          s2h_keep_pair(a.seed, e0 >> 1, a.thresh, kp[0], kp[1]);
-          s2h_keep_pair(a.seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
+          s2h_keep_pair(seed, e0 >> 1, a.thresh, kp[0], kp[1]);
+          s2h_keep_pair(seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
         } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(a.seed, e0 + e, a.thresh);
+          for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(seed, e0 + e, a.thresh);
         }
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool valid = full || (k0 + kb * 16 + 4 * g + r < Lk);
-        const float p = valid ? __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2) : 0.f;
-        const float dpd = kp[r] ? dp[kb][r] * a.inv_keep : 0.f;
-        s[kb][r] = p * (dpd - di);  // dS (scale applied at the end)
+        float p = __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2);
+        if (!full) p = (k0 + kb * 16 + 4 * g + r < Lk) ? p : 0.f;  // wave-uniform test, then a select
+        if constexpr (DROP == DROP_NONE) {
+          s[kb][r] = p * (dp[kb][r] - di);  // dS (scale applied at the end)
+        } else {
+          const float dpd = kp[r] ? dp[kb][r] : 0.f;
+          s[kb][r] = p * fmaf(dpd, a.inv_keep, -di);
+        }
       }
     }
     bf16x8 dsb[2];
@@ -406,9 +414,9 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
 // (128) + S, dP registers beyond 256 per wave, so this form runs one wave per SIMD with
 // the 512-register file: 4 waves x 32 keys on v_mfma_f32_32x32x16_bf16 (also half the LDS
 // operand traffic per FLOP), dK^T / dV^T in 2 x 128 accumulator registers.
-template <int DP>
+template <int DP, int DROP>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a) {
-  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
+  const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   constexpr int NWV = 4, QT = 32;
   using C = FlashCfg<DP, QT, NWV>;
   constexpr int NT = DP / 16, ND = DP / 32;
@@ -446,7 +454,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   };
   // keep words of this wave's 32 keys (word key / 32) for the 32 queries of a tile (lanes 32..63
   // repeat lanes 0..31)
-  const bool bits = fr.keep != nullptr && a.p_drop > 0.f;
+  constexpr bool bits = DROP == DROP_BITS;
   const uint32_t* KEEPW = bits ? fr.keep + min((int)blockIdx.x * NWV + w, fr.kw - 1) : nullptr;
   auto dma_bits = [&](char* stage, int q0) {
     lds_dma4(KEEPW + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * fr.kw, stage + 2 * C::TILEB + w * 512 + 256);
@@ -455,7 +463,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
-  if (bits) dma_bits(stages, qbase);
+  if constexpr (bits) dma_bits(stages, qbase);
   bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
@@ -479,7 +487,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       dma_tile<DP, QT, NWV, true, 1>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
       dma_tile<DP, QT, NWV, true, 1>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
       dma_rows(Qn, q0 + QT);
-      if (bits) {
+      if constexpr (bits) {
         dma_bits(Qn, q0 + QT);
         wait_vmcnt<2 * C::PPW + 2>();
       } else {
@@ -501,20 +509,27 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the fragment prefetch depth
     }
     bf16x8 pdb[2], dsb[2];  // 16-query steps c: k index 8hi + j <-> r = 8c + j
+    const bool qfull = q0 + QT <= a.Lq;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int ql = 8 * (r >> 2) + 4 * hi + (r & 3);
       const int qi = q0 + ql;
       const float lse_r = rows[ql], di_r = rows[32 + ql];
-      const float p = qi < a.Lq ? __builtin_amdgcn_exp2f(s[r] * a.sl2 - lse_r * FL_LOG2E) : 0.f;
-      bool keep = true;
-      if (bits) keep = (kwd[ql] >> kl) & 1u;
-      else if (a.p_drop > 0.f) keep = s2h_keep(a.seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
-      // dV accumulates the kept P unscaled (x 1/keep at the store); dS = P (keep dP / keep_p - Di)
-      const float pk = keep ? p : 0.f;
-      const float dpd = keep ? dp[r] : 0.f;
-      pdb[r >> 3][r & 7] = (bf16)pk;
-      dsb[r >> 3][r & 7] = (bf16)(p * fmaf(dpd, a.inv_keep, -di_r));
+      float p = __builtin_amdgcn_exp2f(fmaf(s[r], a.sl2, -lse_r * FL_LOG2E));
+      if (!qfull) p = qi < a.Lq ? p : 0.f;  // wave-uniform test, then a select
+      if constexpr (DROP == DROP_NONE) {
+        pdb[r >> 3][r & 7] = (bf16)p;
+        dsb[r >> 3][r & 7] = (bf16)(p * (dp[r] - di_r));
+      } else {
+        bool keep;
+        if constexpr (bits) keep = (kwd[ql] >> kl) & 1u;
+        else keep = s2h_keep(seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
+        // dV accumulates the kept P unscaled (x 1/keep at the store); dS = P (keep dP / keep_p - Di)
+        const float pk = keep ? p : 0.f;
+        const float dpd = keep ? dp[r] : 0.f;
+        pdb[r >> 3][r & 7] = (bf16)pk;
+        dsb[r >> 3][r & 7] = (bf16)(p * fmaf(dpd, a.inv_keep, -di_r));
+      }
     }
 #pragma unroll
     for (int c = 0; c < 2; ++c)
@@ -622,13 +637,19 @@ template <int DP>
 static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.BH * a.Lq;
   hipLaunchKernelGGL((flash_bwd_di_kernel<DP>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
-  hipLaunchKernelGGL((flash_bwd_dq_kernel<DP>), dim3((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits), dim3(FL_WAVES * 64),
-                     0, st, a);
+  const int drop = a.p_drop <= 0.f ? DROP_NONE : (a.keep ? DROP_BITS : DROP_HASH);
+  const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits);
+  if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH>), gq, dim3(FL_WAVES * 64), 0, st, a);
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_bwd_dq_combine_kernel<DP>), dim3((unsigned)((rows * DP / 4 + 255) / 256)), dim3(256), 0,
                        st, a);
   if constexpr (DP == 256) {
-    hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP>), dim3((a.Lk + 127) / 128, a.BH, a.kv_splits), dim3(256), 0, st, a);
+    const dim3 gk((a.Lk + 127) / 128, a.BH, a.kv_splits);
+    if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE>), gk, dim3(256), 0, st, a);
+    else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS>), gk, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH>), gk, dim3(256), 0, st, a);
     if (a.kv_splits > 1) {
       const int64_t n4 = (int64_t)a.BH * a.Lk * 2 * DP / 4;
       hipLaunchKernelGGL((flash_bwd_dkv_combine_kernel<DP>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
