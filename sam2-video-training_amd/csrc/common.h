@@ -97,6 +97,12 @@ __device__ __forceinline__ uint32_t s2h_hash_pair(uint64_t seed, uint64_t pair) 
   const uint32_t key = s2h_mix32((uint32_t)seed ^ 0x5bd1e995u) ^ (uint32_t)(seed >> 32);
   return s2h_mix32(((uint32_t)pair + (uint32_t)(pair >> 32) * 0x9E3779B9u) ^ key);
 }
+// the two halves of s2h_hash_pair, for kernels that hoist the seed key and the high word:
+// s2h_hash_pair(seed, pair) == s2h_hash_mixed(s2h_hash_key(seed), lo(pair) + hi(pair) * 0x9E3779B9)
+__device__ __forceinline__ uint32_t s2h_hash_key(uint64_t seed) {
+  return s2h_mix32((uint32_t)seed ^ 0x5bd1e995u) ^ (uint32_t)(seed >> 32);
+}
+__device__ __forceinline__ uint32_t s2h_hash_mixed(uint32_t key, uint32_t x) { return s2h_mix32(x ^ key); }
 // thresh = p * 2^32 (the 16 high bits are used)
 __device__ __forceinline__ bool s2h_keep(uint64_t seed, uint64_t idx, uint32_t thresh) {
   const uint32_t h = s2h_hash_pair(seed, idx >> 1);

@@ -37,14 +37,19 @@ struct FlashArgs {
   // dropout keep flag of (q, k); kw = 2 * ceil(Lk / 64).  The backward reads it instead of
   // re-hashing (flash_bwd.hip).
   uint32_t* keep; int kw;
+  int pair_ok;  // idx0 and Lk even: every element pair (2i, 2i + 1) of a 4-key group shares one hash
   int splits, tiles_per_split;
   float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
   float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
 };
 
-template <int DP>
+// dropout: none / counter hash / counter hash + keep bitmap store (template: no per-tile tests)
+enum { FDROP_NONE = 0, FDROP_HASH = 1, FDROP_BITS = 2 };
+
+template <int DP, int DROP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
-  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
+  const uint32_t hkey = DROP != FDROP_NONE ? s2h_hash_key(s2h_seed(a.seed, a.seed_off)) : 0u;
+  const uint32_t t16 = a.thresh >> 16;
   using C = FlashCfg<DP>;
   using I = PadImg<DP>;  // padded K / V images (affine read addresses, no swizzle)
   // one LDS array: [2 stages][K tile | V tile]
@@ -152,26 +157,35 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mref);
         rs += s[kb][r];
       }
-    if (a.p_drop > 0.f) {
-      // the 4 keys of a (kb) block are consecutive: two hashes per block when pairs align
+    if constexpr (DROP != FDROP_NONE) {
       uint32_t kbits[2] = {0u, 0u};  // this lane's keep flags: bit 16kb + 4g + e of the tile's 64 keys
+      // the 4 keys of a (kb) block are consecutive: two hashes per block when pairs align
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) {
         const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
         bool kp[4];
         if ((e0 & 1) == 0) {
-          s2h_keep_pair(a.seed, e0 >> 1, a.thresh, kp[0], kp[1]);
-          s2h_keep_pair(a.seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
+          const uint64_t pr = e0 >> 1;
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const uint32_t hsh = s2h_hash_mixed(hkey, (uint32_t)(pr + j) + (uint32_t)((pr + j) >> 32) * 0x9E3779B9u);
+            kp[2 * j] = (hsh & 0xFFFFu) >= t16;
+            kp[2 * j + 1] = (hsh >> 16) >= t16;
+          }
         } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(a.seed, e0 + e, a.thresh);
+          for (int e = 0; e < 4; ++e) {
+            const uint64_t pr = (e0 + e) >> 1;
+            const uint32_t hsh = s2h_hash_mixed(hkey, (uint32_t)pr + (uint32_t)(pr >> 32) * 0x9E3779B9u);
+            kp[e] = (((e0 + e) & 1) ? (hsh >> 16) : (hsh & 0xFFFFu)) >= t16;
+          }
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[kb][e] = kp[e] ? s[kb][e] * a.inv_keep : 0.f;
         kbits[kb >> 1] |= ((uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3))
                           << (16 * (kb & 1) + 4 * g);
       }
-      if (a.keep) {  // OR the 4 key groups of the query row, one 8-B store per row and tile
+      if constexpr (DROP == FDROP_BITS) {  // OR the 4 key groups of the query row, one 8-B store per row and tile
 #pragma unroll
         for (int h2 = 0; h2 < 2; ++h2) {
           kbits[h2] |= (uint32_t)__shfl_xor((int)kbits[h2], 16);
@@ -310,7 +324,9 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
 template <int DP>
 static int flash_launch(FlashArgs& a, hipStream_t st) {
   dim3 grid((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits);
-  hipLaunchKernelGGL((flash_fwd_kernel<DP>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  if (a.p_drop <= 0.f) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  else if (a.keep) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  else hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH>), grid, dim3(FL_WAVES * 64), 0, st, a);
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_combine_kernel<DP>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0, st,
                        a);
@@ -328,6 +344,7 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
   a.idx0 = idx0;
   a.keep = p_drop > 0.f ? keep : nullptr;
   a.kw = 2 * ((Lk + 63) / 64);
+  a.pair_ok = ((idx0 | (uint64_t)Lk) & 1) == 0;
   a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
   a.q = (const bf16*)q; a.sqb = sqb; a.sqh = sqh; a.sql = sql;
   a.k = (const bf16*)k; a.skb = skb; a.skh = skh; a.skl = skl;
