@@ -25,6 +25,7 @@ void s2h_prof_end(int slot, hipStream_t st);
 
 struct FlashArgs {
   int BH, H, Lq, Lk;
+  int D;  // head dim (<= DP; DP = 64 pads e.g. Hiera's 56: zero Q columns, unstored O columns)
   const bf16* q; int64_t sqb, sqh, sql;
   const bf16* k; int64_t skb, skh, skl;
   const bf16* v; int64_t svb, svh, svl;
@@ -67,8 +68,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   const int nt = t1 - t0;
 
   if (nt > 0) {
-    dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane);
-    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane);
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane, a.D);
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane, a.D);
   }
   const int npw = I::pieces(w);
 
@@ -76,7 +77,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   bf16x8 qf[C::NT];
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) {
-    if (q < a.Lq) qf[t] = *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g);
+    if (q < a.Lq && 32 * t + 8 * g < a.D) qf[t] = *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g);
     else qf[t] = bf16x8{};
   }
   // compiler-visible vmcnt(0): retires the Q loads in the compiler's own bookkeeping too;
@@ -98,8 +99,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     char* Vb = Kb + I::TILEB;
     if (it + 1 < nt) {
       char* Kn = smem + ((it + 1) & 1) * 2 * I::TILEB;
-      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane);
-      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane);
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane, a.D);
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane, a.D);
       // this wave's pieces of tile `it` have landed once all but the 2*npw just issued retired
       wait_vmcnt_pieces<2, I::PPW_LO>(npw);
     } else {
@@ -236,7 +237,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
       bf16 t4[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) t4[e] = (bf16)(o[d][e] * inv);
-      *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
+      if (16 * d + 4 * g < a.D) *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
     }
     if (g == 0) a.lse[(int64_t)bh * a.Lq + q] = (m + log2f(l)) * FL_LN2;
   } else {
@@ -278,7 +279,8 @@ __global__ __launch_bounds__(256) void flash_combine_kernel(FlashArgs a) {
   const float inv = L > 0.f ? 1.f / L : 0.f;
   bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
 #pragma unroll
-  for (int j = 0; j < PER; ++j) O[lane * PER + j] = (bf16)(acc[j] * inv);
+  for (int j = 0; j < PER; ++j)
+    if (lane * PER + j < a.D) O[lane * PER + j] = (bf16)(acc[j] * inv);
   if (lane == 0) a.lse[rowg] = (Mr + log2f(L)) * FL_LN2;
 }
 
@@ -309,16 +311,19 @@ extern "C" int s2h_attn_config(int flash_enable) {
   return prev;
 }
 
-// eligible: bf16, head_dim exactly 64 / 128 / 256, >= 128 query rows, 16-B aligned rows
+// eligible: bf16, head_dim 128 / 256 or 32..64 in steps of 8 (padded to a 64 image), >= 128
+// query rows, 16-B aligned rows
 int s2h_flash_eligible(int dt, int Lq, int D) {
-  return g_flash_enabled && dt == S2H_BF16 && (D == 64 || D == 128 || D == 256) && Lq >= 128;
+  const bool dok = D == 128 || D == 256 || (D >= 32 && D <= 64 && D % 8 == 0);
+  return g_flash_enabled && dt == S2H_BF16 && dok && Lq >= 128;
 }
 
 int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
   int splits, tps;
   flash_plan(B * H, Lq, Lk, splits, tps);
   if (splits <= 1) return 0;
-  return (int64_t)splits * B * H * Lq * (D + 2) * 4;
+  const int DPd = D <= 64 ? 64 : D;  // padded image width
+  return (int64_t)splits * B * H * Lq * (DPd + 2) * 4;
 }
 
 template <int DP>
@@ -342,6 +347,7 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
                   int64_t ws_bytes, hipStream_t st) {
   FlashArgs a = {};
   a.idx0 = idx0;
+  a.D = D;
   a.keep = p_drop > 0.f ? keep : nullptr;
   a.kw = 2 * ((Lk + 63) / 64);
   a.pair_ok = ((idx0 | (uint64_t)Lk) & 1) == 0;
@@ -357,16 +363,17 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed;
   a.seed_off = s2h_rng_offset_ptr();
+  const int DPd = D <= 64 ? 64 : D;  // padded image width of the partials
   flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
-  const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (D + 2) * 4 : 0;
+  const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (DPd + 2) * 4 : 0;
   if (need > ws_bytes || (need > 0 && ws == nullptr)) {  // no workspace: one split
     a.splits = 1;
     a.tiles_per_split = (Lk + 63) / 64;
   } else if (a.splits > 1) {
     a.ws_o = (float*)ws;
-    a.ws_ml = a.ws_o + (int64_t)a.splits * a.BH * Lq * D;
+    a.ws_ml = a.ws_o + (int64_t)a.splits * a.BH * Lq * DPd;
   }
   if (D == 256) return flash_launch<256>(a, st);
   if (D == 128) return flash_launch<128>(a, st);
-  return flash_launch<64>(a, st);
+  return flash_launch<64>(a, st);  // D <= 64 (s2h_flash_eligible)
 }

@@ -20,6 +20,7 @@ void s2h_prof_end(int slot, hipStream_t st);
 
 struct FlashBwdArgs {
   int BH, H, Lq, Lk;
+  int D;  // head dim (<= DP: head dims <= 64 run in a 64 image, zero operand columns past D)
   const bf16* q; int64_t sqb, sqh, sql;
   const bf16* k; int64_t skb, skh, skl;
   const bf16* v; int64_t svb, svh, svl;
@@ -103,7 +104,7 @@ __global__ __launch_bounds__(256) void flash_bwd_di_kernel(FlashBwdArgs a) {
   const bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
   const bf16* G = a.g + b * a.sgb + h * a.sgh + (int64_t)q * a.sgl;
   float s = 0.f;
-  for (int d = lane * 4; d < DP; d += 256) {
+  for (int d = lane * 4; d < a.D; d += 256) {
     const uint2 ou = *(const uint2*)(O + d), gu = *(const uint2*)(G + d);
     const bf16* ob = (const bf16*)&ou;
     const bf16* gb = (const bf16*)&gu;
@@ -147,16 +148,17 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   auto dma_bits = [&](int stage, int k0) { lds_dma4(KEEPQ + (k0 >> 5) + (lane & 1), bits_lds + stage * FL_WAVES * 256); };
 
   if (nt > 0) {
-    dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane);
-    dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane);
+    dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane, a.D);
+    dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane, a.D);
     if constexpr (bits) dma_bits(0, t0 * C::KT);
   }
   const bool qv = q < a.Lq;
   bf16x8 qf[C::NT], gf[C::NT];
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) {
-    qf[t] = qv ? *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g) : bf16x8{};
-    gf[t] = qv ? *(const bf16x8*)(G + (int64_t)q * a.sgl + 32 * t + 8 * g) : bf16x8{};
+    const bool ok = qv && 32 * t + 8 * g < a.D;  // zero past the head dim
+    qf[t] = ok ? *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g) : bf16x8{};
+    gf[t] = ok ? *(const bf16x8*)(G + (int64_t)q * a.sgl + 32 * t + 8 * g) : bf16x8{};
   }
   const float lse2 = qv ? a.lse[(int64_t)bh * a.Lq + q] * FL_LOG2E : 0.f;
   const float di = qv ? a.di[(int64_t)bh * a.Lq + q] : 0.f;
@@ -174,8 +176,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     char* Vb = Kb + C::TILEB;
     if (it + 1 < nt) {
       char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane);
-      dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane);
+      dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane, a.D);
+      dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane, a.D);
       if constexpr (bits) {
         dma_bits((it + 1) & 1, k0 + C::KT);
         wait_vmcnt<2 * C::PPW + 1>();
@@ -257,6 +259,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     bf16* DQ = a.dq + b * a.sdqb + h * a.sdqh + (int64_t)q * a.sdql;
 #pragma unroll
     for (int d = 0; d < C::ND; ++d) {
+      if (16 * d + 4 * g >= a.D) continue;
       bf16 t4[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) t4[e] = (bf16)(acc[d][e] * a.scale);
@@ -281,16 +284,21 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_combine_kernel(FlashBwdArgs 
     const float4 t = *(const float4*)(a.ws_dq + sp * rows * DP + i);
     s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
   }
+  if (d >= a.D) return;
   const int bh = row / a.Lq, q = row % a.Lq, b = bh / a.H, h = bh % a.H;
   bf16 t4[4] = {(bf16)(s.x * a.scale), (bf16)(s.y * a.scale), (bf16)(s.z * a.scale), (bf16)(s.w * a.scale)};
   *(uint2*)(a.dq + b * a.sdqb + h * a.sdqh + (int64_t)q * a.sdql + d) = *(const uint2*)t4;
 }
 
 // ------------------------------------------------------------------ dK / dV
-template <int DP>
+// head_dim 128, or <= 64 padded to a 64 image (Hiera, hieradet.py:56-81): 8 waves x 16 keys, K / V
+// fragments in registers; Q / dO tiles of QT queries (64 for the 64 image: a 32-row tile would be
+// half a DMA piece per wave) consumed in 32-query halves.
+template <int DP, int DROP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBwdArgs a) {
-  if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
-  using C = FlashCfg<DP, 32>;  // 32-query tiles
+  const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
+  constexpr int QT = DP == 64 ? 64 : 32;
+  using C = FlashCfg<DP, QT>;
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][Q | dO]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
@@ -302,16 +310,19 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
   const bf16* K = fr.k;
   const bf16* V = fr.v;
-  const int nt = (a.Lq + C::KT - 1) / C::KT;
+  const int nt = (a.Lq + QT - 1) / QT;
 
-  dma_tile<DP, 32, FL_WAVES, true>(smem, Q, a.sql, 0, a.Lq, w, lane);
-  dma_tile<DP, 32, FL_WAVES, true>(smem + C::TILEB, G, a.sgl, 0, a.Lq, w, lane);
-  bf16x8 kf[C::NT], vf[C::NT];  // B operands: K^T / V^T [k = d][n = key]
+  dma_tile<DP, QT, FL_WAVES, true>(smem, Q, a.sql, 0, a.Lq, w, lane, a.D);
+  dma_tile<DP, QT, FL_WAVES, true>(smem + C::TILEB, G, a.sgl, 0, a.Lq, w, lane, a.D);
+  bf16x8 kf[C::NT], vf[C::NT];  // B operands: K^T / V^T [k = d][n = key]; zero past the head dim
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) {
-    kf[t] = kv ? *(const bf16x8*)(K + (int64_t)key * a.skl + 32 * t + 8 * g) : bf16x8{};
-    vf[t] = kv ? *(const bf16x8*)(V + (int64_t)key * a.svl + 32 * t + 8 * g) : bf16x8{};
+    const bool ok = kv && 32 * t + 8 * g < a.D;
+    kf[t] = ok ? *(const bf16x8*)(K + (int64_t)key * a.skl + 32 * t + 8 * g) : bf16x8{};
+    vf[t] = ok ? *(const bf16x8*)(V + (int64_t)key * a.svl + 32 * t + 8 * g) : bf16x8{};
   }
+  // compiler-visible vmcnt(0) for the fragment loads (see the dQ kernel)
+  __builtin_amdgcn_s_waitcnt(0xF70);
   f32x4 dk[C::ND], dv[C::ND];  // dK^T / dV^T: row d = 16*db + 4g + r, column key
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) {
@@ -322,13 +333,13 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   const float* DI = a.di + (int64_t)bh * a.Lq;
 
   for (int it = 0; it < nt; ++it) {
-    const int q0 = it * C::KT;
+    const int q0 = it * QT;
     char* Qb = smem + (it & 1) * 2 * C::TILEB;
     char* Gb = Qb + C::TILEB;
-    // this tile's queries of this lane: q0 + 16*qb + 4g + r  (qb = 0, 1; r = 0..3)
-    float4 lse4[2], di4[2];
+    // this tile's queries of this lane: q0 + 32*hf + 16*qb + 4g + r  (hf < QT/32; qb = 0, 1; r = 0..3)
+    float4 lse4[QT / 16], di4[QT / 16];
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < QT / 16; ++qb) {
       const int qr = q0 + 16 * qb + 4 * g;
       if (qr + 3 < a.Lq && (a.Lq & 3) == 0) {
         lse4[qb] = *(const float4*)(LSE + qr);
@@ -346,49 +357,57 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
     }
     if (it + 1 < nt) {
       char* Qn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 32, FL_WAVES, true>(Qn, Q, a.sql, q0 + C::KT, a.Lq, w, lane);
-      dma_tile<DP, 32, FL_WAVES, true>(Qn + C::TILEB, G, a.sgl, q0 + C::KT, a.Lq, w, lane);
+      dma_tile<DP, QT, FL_WAVES, true>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane, a.D);
+      dma_tile<DP, QT, FL_WAVES, true>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane, a.D);
       wait_vmcnt<2 * C::PPW>();
     } else {
       wait_vmcnt<0>();
     }
     wg_barrier();
 
-    f32x4 s[2], dp[2];  // S / dP: row q = 16*qb + 4g + r, column key
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      s[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      dp[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int row = qb * 16 + kl;
+    for (int hf = 0; hf < QT / 32; ++hf) {
+      f32x4 s[2], dp[2];  // S / dP: row q = 32*hf + 16*qb + 4g + r, column key
 #pragma unroll
-      for (int t = 0; t < C::NT; ++t) {
-        const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP>(row, 4 * t + g));
-        s[qb] = mfma16(qa, kf[t], s[qb]);
-        const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP>(row, 4 * t + g));
-        dp[qb] = mfma16(ga, vf[t], dp[qb]);
+      for (int qb = 0; qb < 2; ++qb) {
+        s[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        dp[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int row = 32 * hf + qb * 16 + kl;
+#pragma unroll
+        for (int t = 0; t < C::NT; ++t) {
+          const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP>(row, 4 * t + g));
+          s[qb] = mfma16(qa, kf[t], s[qb]);
+          const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP>(row, 4 * t + g));
+          dp[qb] = mfma16(ga, vf[t], dp[qb]);
+        }
       }
-    }
-    bf16x8 pdb, dsb;  // B operands over the 32 queries: k index 8g + j <-> q 16(j>>2) + 4g + (j&3)
+      bf16x8 pdb, dsb;  // B operands over 32 queries: k index 8g + j <-> q 16(j>>2) + 4g + (j&3)
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const float lt[4] = {lse4[qb].x, lse4[qb].y, lse4[qb].z, lse4[qb].w};
-      const float dt[4] = {di4[qb].x, di4[qb].y, di4[qb].z, di4[qb].w};
+      for (int qb = 0; qb < 2; ++qb) {
+        const float4 l4 = lse4[2 * hf + qb], d4 = di4[2 * hf + qb];
+        const float lt[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dt[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int qi = q0 + 16 * qb + 4 * g + r;
-        const float p = __builtin_amdgcn_exp2f(s[qb][r] * a.sl2 - lt[r] * FL_LOG2E);
-        bool keep = true;
-        if (a.p_drop > 0.f) keep = s2h_keep(a.seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
-        const float pd = keep ? p * a.inv_keep : 0.f;
-        const float dpd = keep ? dp[qb][r] * a.inv_keep : 0.f;
-        pdb[4 * qb + r] = (bf16)pd;
-        dsb[4 * qb + r] = (bf16)(p * (dpd - dt[r]));
+        for (int r = 0; r < 4; ++r) {
+          const float p = __builtin_amdgcn_exp2f(s[qb][r] * a.sl2 - lt[r] * FL_LOG2E);
+          if constexpr (DROP == DROP_NONE) {
+            pdb[4 * qb + r] = (bf16)p;
+            dsb[4 * qb + r] = (bf16)(p * (dp[qb][r] - dt[r]));
+          } else {
+            const int qi = q0 + 32 * hf + 16 * qb + 4 * g + r;
+            const bool keep = s2h_keep(seed, fr.drow0 + (uint64_t)qi * (uint64_t)fr.Lk + key, a.thresh);
+            const float pd = keep ? p * a.inv_keep : 0.f;
+            const float dpd = keep ? dp[qb][r] * a.inv_keep : 0.f;
+            pdb[4 * qb + r] = (bf16)pd;
+            dsb[4 * qb + r] = (bf16)(p * (dpd - dt[r]));
+          }
+        }
       }
-    }
 #pragma unroll
-    for (int d = 0; d < C::ND; ++d) {
-      dv[d] = mfma16(tr_frag_perm<DP>(Gb, 0, 16 * d, lane), pdb, dv[d]);
-      dk[d] = mfma16(tr_frag_perm<DP>(Qb, 0, 16 * d, lane), dsb, dk[d]);
+      for (int d = 0; d < C::ND; ++d) {
+        dv[d] = mfma16(tr_frag_perm<DP>(Gb, 32 * hf, 16 * d, lane), pdb, dv[d]);
+        dk[d] = mfma16(tr_frag_perm<DP>(Qb, 32 * hf, 16 * d, lane), dsb, dk[d]);
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wg_barrier();
@@ -399,6 +418,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   bf16* DV = fr.dv + (int64_t)key * a.sdvl;
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) {
+    if (16 * d + 4 * g >= a.D) continue;
     bf16 tk[4], tv[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -623,7 +643,8 @@ static void flash_bwd_ws_layout(int BH, int Lq, int Lk, int D, int64_t& dq_bytes
   int splits, tps, kvs, ktps;
   flash_bwd_plan(BH, Lq, Lk, splits, tps);
   flash_bwd_kv_plan(BH, Lq, Lk, kvs, ktps);
-  dq_bytes = splits > 1 ? (int64_t)splits * BH * Lq * D * 4 : 0;
+  const int DPd = D <= 64 ? 64 : D;  // padded image width of the dQ partials
+  dq_bytes = splits > 1 ? (int64_t)splits * BH * Lq * DPd * 4 : 0;
   dkv_bytes = (D == 256 && kvs > 1) ? (int64_t)kvs * BH * Lk * 2 * D * 4 : 0;
 }
 
@@ -654,9 +675,11 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
       const int64_t n4 = (int64_t)a.BH * a.Lk * 2 * DP / 4;
       hipLaunchKernelGGL((flash_bwd_dkv_combine_kernel<DP>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
     }
-  } else
-    hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP>), dim3((a.Lk + FL_QB - 1) / FL_QB, a.BH), dim3(FL_WAVES * 64), 0, st,
-                       a);
+  } else {
+    const dim3 gk((a.Lk + FL_QB - 1) / FL_QB, a.BH);
+    if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP, DROP_NONE>), gk, dim3(FL_WAVES * 64), 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP, DROP_HASH>), gk, dim3(FL_WAVES * 64), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -673,6 +696,7 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
                   const uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st) {
   FlashBwdArgs a = {};
   a.idx0 = idx0;
+  a.D = D;
   if (keep && D != 256) return (int)hipErrorInvalidValue;  // the head-dim-256 kernels read the bitmap
   a.keep = keep;
   a.kw = 2 * ((Lk + 63) / 64);
@@ -703,13 +727,15 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
   if (dkv_bytes > 0) a.ws_dkv = (float*)((char*)ws + dq_bytes);
   else { a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32; }
   if (D == 256) return flash_bwd_launch<256>(a, st);
-  return flash_bwd_launch<128>(a, st);
+  if (D == 128) return flash_bwd_launch<128>(a, st);
+  return flash_bwd_launch<64>(a, st);  // D <= 64: padded image
 }
 
-// eligible: bf16, head_dim 128 / 256 (32-query DMA tiles need >= 8 KiB), >= 128 query rows
+// eligible: the flash forward's domain (bf16, head_dim 128 / 256 or 32..64 padded to 64, >= 128
+// query rows)
 int s2h_flash_bwd_eligible(int dt, int Lq, int D);
 int s2h_flash_eligible(int dt, int Lq, int D);
-int s2h_flash_bwd_eligible(int dt, int Lq, int D) { return s2h_flash_eligible(dt, Lq, D) && (D == 128 || D == 256); }
+int s2h_flash_bwd_eligible(int dt, int Lq, int D) { return s2h_flash_eligible(dt, Lq, D); }
 
 // Frame-batched backward: nfr frames x bpf batches x H heads in ONE launch per kernel.  Q / O /
 // dO / dQ / LSE are [nfr * bpf] uniform batches (batch stride sqb ...); K / V / dK / dV are
@@ -727,9 +753,10 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
                                     int64_t sdvl, const float* lse, float* di_ws, float scale, float p_drop,
                                     uint64_t seed, const uint32_t* keep, const int64_t* fr_koff, hipStream_t st) {
   if (nfr <= 0 || bpf <= 0 || H <= 0 || Lq <= 0) return 0;
-  if (nfr > S2H_MAX_FRAMES || !(D == 128 || D == 256) || Lq < 128) return (int)hipErrorInvalidValue;
+  if (nfr > S2H_MAX_FRAMES || !s2h_flash_bwd_eligible(S2H_BF16, Lq, D)) return (int)hipErrorInvalidValue;
   if (keep && (D != 256 || fr_koff == nullptr)) return (int)hipErrorInvalidValue;
   FlashBwdArgs a = {};
+  a.D = D;
   a.nfr = nfr; a.bpf = bpf;
   a.keep = keep;
   int lk_max = 0;
@@ -761,7 +788,8 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
   int64_t lk_sum = 0;
   for (int f = 0; f < nfr; ++f) lk_sum += fr_lk[f];
   const int slot = s2h_prof_begin(st, 2, (int64_t)bpf * H, Lq, lk_sum, D, 3);
-  const int rc = D == 256 ? flash_bwd_launch<256>(a, st) : flash_bwd_launch<128>(a, st);
+  const int rc = D == 256 ? flash_bwd_launch<256>(a, st) : D == 128 ? flash_bwd_launch<128>(a, st)
+                                                                    : flash_bwd_launch<64>(a, st);
   s2h_prof_end(slot, st);
   return rc;
 }

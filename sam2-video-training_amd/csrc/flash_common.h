@@ -57,8 +57,11 @@ __device__ __forceinline__ int swz(int row, int c) {
 // ASM: issue through inline asm (lds_dma16) so the compiler's waitcnt pass does not put
 // vmcnt(0) before later ds_reads; the builtin form is kept where it measured faster (the
 // forward kernel, whose spilled address registers make every scratch reload a vmcnt wait).
+// dvalid < DP (head dims padded to DP, e.g. Hiera's 56 in a 64 image): chunks at or past dvalid
+// re-read chunk 0 of the row -- finite values the kernels cancel (zero operand columns) or never store
 template <int DP, int ROWS, int NWV = FL_WAVES, bool ASM = false, int SW = 0>
-__device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w, int lane) {
+__device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w, int lane,
+                                         int dvalid = DP) {
   using C = FlashCfg<DP, ROWS, NWV>;
 #pragma unroll
   for (int i = 0; i < C::PPW; ++i) {
@@ -67,7 +70,7 @@ __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_
     const int pos = lane % C::NCH;
     const int c = pos ^ swz_x<DP, SW>(row);
     const int gr = min(r0 + row, nrows - 1);
-    const bf16* g = src + (int64_t)gr * ld + c * 8;
+    const bf16* g = src + (int64_t)gr * ld + (c * 8 < dvalid ? c * 8 : 0);
     if constexpr (ASM)
       lds_dma16(g, lds_tile + piece * 1024);
     else
@@ -97,7 +100,7 @@ struct PadImg {
 
 template <int DP, int ROWS = 64, int NWV = FL_WAVES, bool ASM = false>
 __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w,
-                                             int lane) {
+                                             int lane, int dvalid = DP) {
   using I = PadImg<DP, ROWS, NWV>;
 #pragma unroll
   for (int i = 0; i < I::PPW_LO + (I::NHI ? 1 : 0); ++i) {
@@ -106,7 +109,7 @@ __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, in
     const int slot = piece * 64 + lane;
     const int row = slot / I::SPR, c = slot % I::SPR;
     const int gr = min(r0 + row, nrows - 1);
-    const bf16* g = src + (int64_t)gr * ld + (c < DP / 8 ? c * 8 : 0);
+    const bf16* g = src + (int64_t)gr * ld + (c < DP / 8 && c * 8 < dvalid ? c * 8 : 0);
     if constexpr (ASM)
       lds_dma16(g, lds_tile + piece * 1024);
     else

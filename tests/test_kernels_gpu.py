@@ -199,9 +199,13 @@ def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
 
 
 @pytest.mark.parametrize("B,H,Lq,Lk,D", [(13, 1, 1024, 7196, 256), (13, 1, 1024, 1024, 256), (2, 2, 1024, 1028, 128),
-                                         (2, 4, 300, 77, 64), (1, 1, 1000, 1031, 256), (3, 1, 128, 40, 256)])
+                                         (2, 4, 300, 77, 64), (1, 1, 1000, 1031, 256), (3, 1, 128, 40, 256),
+                                         # Hiera head dim 56 (and 40) in the padded 64 image
+                                         (2, 2, 196, 196, 56), (1, 8, 1024, 1024, 56), (3, 2, 130, 300, 40),
+                                         (2, 4, 256, 200, 64)])
 def test_flash_forward_matches_reference(B, H, Lq, Lk, D):
-    """bf16 long-sequence path (flash.hip): key-split partials + combine, ragged tails."""
+    """bf16 long-sequence path (flash.hip, flash_bwd.hip): key-split partials + combine, ragged
+    tails, head dims <= 64 padded to the 64 image."""
     ops = _ops()
     torch.manual_seed(4)
     q = torch.randn(B, Lq, H, D, device=DEV).to(torch.bfloat16)
@@ -723,3 +727,28 @@ def test_bce_category_loss_matches_reference_formula(reduction, pw, temp):
     got["total_loss"].backward()
     tot.backward()
     _close(x.grad, xr.grad, 1e-5)
+
+
+def test_flash_strided_qkv_head56_fwd_bwd():
+    """Hiera's fused [B, L, 3, H, 56] projection through the padded-64 flash path: q / k / v read
+    in place, gradients written in place into one dqkv buffer (the QKV attention layout)"""
+    ops = _ops()
+    torch.manual_seed(8)
+    B, L, H, d = 3, 196, 2, 56
+    qkv = (torch.randn(B, L, 3, H, d, device=DEV) * 0.7).to(torch.bfloat16)
+    q, k, v = qkv.unbind(2)
+    o = torch.empty(B, L, H, d, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, d ** -0.5)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ro, rl = _ref_attn(qr, kr, vr, d ** -0.5)
+    _close(o, ro, 2e-2)
+    _close(lse, rl, 1e-3)
+    do = torch.randn_like(o)
+    ro.backward(do.float())
+    dqkv = torch.full((B, L, 3, H, d), float("nan"), device=DEV, dtype=torch.bfloat16)
+    dq, dk, dv = dqkv.unbind(2)
+    ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, d ** -0.5)
+    _close(dq, qr.grad, 4e-2)
+    _close(dk, kr.grad, 4e-2)
+    _close(dv, vr.grad, 4e-2)

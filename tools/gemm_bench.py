@@ -17,11 +17,14 @@ from sam2_video.kernels import ops  # noqa: E402
 # (M, N, K, kind): fwd = x[M,K] @ w[N,K]^T ; dgrad = dy[M,K] @ w[K,N] ; wgrad = dy[K,M]^T @ x[K,N] (fp32 out)
 SHAPES = [
     (13312, 2048, 256, "fwd"), (13312, 256, 2048, "fwd"), (13312, 768, 256, "fwd"), (13312, 256, 256, "fwd"),
-    (13312, 2048, 256, "dgrad"), (13312, 256, 2048, "dgrad"),
-    (2048, 256, 13312, "wgrad"), (256, 256, 13312, "wgrad"), (256, 2048, 13312, "wgrad"),
+    (13312, 128, 256, "fwd"), (13312, 1024, 256, "fwd"),
+    (93184, 2048, 256, "dgrad"), (93184, 256, 2048, "dgrad"), (93184, 256, 256, "dgrad"),
+    (2048, 256, 93184, "wgrad"), (256, 256, 93184, "wgrad"), (256, 2048, 93184, "wgrad"), (256, 64, 374192, "wgrad"),
+    (1792, 448, 8192, "wgrad"), (448, 1792, 8192, "wgrad"),
     (8192, 1792, 448, "fwd"), (8192, 448, 1792, "fwd"), (14112, 1344, 448, "fwd"),
-    (131072, 448, 112, "fwd"), (131072, 112, 448, "dgrad"), (448, 112, 131072, "wgrad"),
-    (93548, 256, 64, "fwd"), (4096, 4096, 4096, "fwd"),
+    (131072, 448, 112, "fwd"), (93548, 256, 64, "fwd"),
+    (104, 256, 2048, "fwd"), (104, 256, 256, "fwd"), (104, 2048, 256, "fwd"), (13, 256, 256, "fwd"),
+    (4096, 4096, 4096, "fwd"),
 ]
 
 

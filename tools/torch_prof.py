@@ -40,7 +40,7 @@ def main():
         runner(batch)
     torch.cuda.synchronize()
     from torch.profiler import ProfilerActivity, profile
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True, record_shapes=True) as prof:
         runner(batch)
         torch.cuda.synchronize()
     ka = prof.key_averages()
@@ -48,6 +48,12 @@ def main():
     # call sites of the torch copies / fills / adds / cats
     want = ("aten::copy_", "aten::fill_", "aten::add_", "aten::add", "aten::cat", "aten::zero_", "aten::clone",
             "aten::contiguous", "aten::index", "aten::mul", "aten::stack")
+    # forward ops by autograd sequence number (a backward node's ops carry the forward op's number)
+    fwd_by_seq = {}
+    for ev in prof.events():
+        sq = getattr(ev, "sequence_nr", -1)
+        if sq is not None and sq >= 0 and ev.stack and not ev.name.startswith("autograd::"):
+            fwd_by_seq.setdefault(sq, ev)
     sites = {}
     for ev in prof.events():
         if ev.name not in want:
@@ -56,7 +62,21 @@ def main():
         if dev <= 0:
             continue
         stack = [s for s in (ev.stack or []) if "sam2_video" in s or "tests" in s or "bench" in s]
-        key = (ev.name, " <- ".join(stack[:3]) if stack else "(no python frame)")
+        if stack:
+            where = " <- ".join(stack[:3])
+        else:  # backward-engine ops have no Python frame: name the enclosing ops instead
+            chain, p, fwd = [], ev.cpu_parent, None
+            while p is not None and len(chain) < 4:
+                chain.append(p.name)
+                sq = getattr(p, "sequence_nr", -1)
+                if fwd is None and sq is not None and sq >= 0 and sq in fwd_by_seq:
+                    fwd = fwd_by_seq[sq]
+                p = p.cpu_parent
+            where = "parents: " + " < ".join(chain[:2]) if chain else "(no python frame)"
+            if fwd is not None:
+                fst = [s for s in fwd.stack if "sam2_video" in s or "tests" in s]
+                where += " | fwd " + fwd.name + " @ " + " <- ".join(fst[:3])
+        key = (ev.name, where)
         v = sites.setdefault(key, [0, 0.0])
         v[0] += 1
         v[1] += dev
