@@ -85,6 +85,48 @@ def linear(x, mod, act=None, residual=None, drop_p=0.0):
     return _Linear.apply(x.contiguous(), mod.weight, mod.bias, mod, act, residual, float(drop_p))
 
 
+class _MLP2(torch.autograd.Function):
+    """fc2(act(fc1(x))) (+ residual) as one node: the backward applies act'(pre) in fc2's dgrad
+    epilogue (no separate activation-gradient pass, no d(hidden) round trip through HBM)."""
+
+    @staticmethod
+    def forward(ctx, x, w1p, b1p, w2p, b2p, fc1, fc2, act, residual):
+        w1, w2 = fc1.compute_weight(), fc2.compute_weight()
+        pre = torch.empty(*x.shape[:-1], w1.shape[0], device=x.device, dtype=x.dtype)
+        hid = ops.linear(x, w1, fc1.compute_bias(), act=act, pre=pre)
+        out = ops.linear(hid, w2, fc2.compute_bias(), residual=residual)
+        ctx.fc1, ctx.fc2, ctx.act, ctx.has_res = fc1, fc2, act, residual is not None
+        ctx.save_for_backward(x, pre, hid)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, pre, hid = ctx.saved_tensors
+        dy = dy.contiguous()
+        fc1, fc2 = ctx.fc1, ctx.fc2
+        gw2, gb2 = fc2.grad_views()
+        if gw2 is not None:
+            ops.linear_wgrad(dy, hid, gw2.view(gw2.shape[0], -1), db=gb2)
+        elif gb2 is not None:
+            ops.colsum(dy, gb2)
+        dpre = ops.linear_dgrad(dy, fc2.compute_weight(), pre=pre, act=ctx.act)
+        gw1, gb1 = fc1.grad_views()
+        if gw1 is not None:
+            ops.linear_wgrad(dpre, x, gw1.view(gw1.shape[0], -1), db=gb1)
+        elif gb1 is not None:
+            ops.colsum(dpre, gb1)
+        dx = ops.linear_dgrad(dpre, fc1.compute_weight()) if ctx.needs_input_grad[0] else None
+        return dx, None, None, None, None, None, None, None, (dy if ctx.has_res else None)
+
+
+def mlp2(x, fc1, fc2, act, residual=None):
+    """fc2(act(fc1(x))) (+ residual) -- two-layer MLP (hieradet.py:87-91 MultiScaleBlock.mlp)"""
+    T = _ft.active()
+    if T is not None:
+        return linear(linear(x, fc1, act=act), fc2, residual=residual)
+    return _MLP2.apply(x.contiguous(), fc1.weight, fc1.bias, fc2.weight, fc2.bias, fc1, fc2, act, residual)
+
+
 # ------------------------------------------------------------- LayerNorm
 class _LayerNorm(torch.autograd.Function):
     @staticmethod

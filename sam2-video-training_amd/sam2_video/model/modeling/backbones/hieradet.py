@@ -84,10 +84,10 @@ class MultiScaleBlock(nn.Module):
         if self.window_size > 0:
             y = FN.window_unpartition(y, ws, B, H, W)
         h, x = FN.add_layer_norm(shortcut, y, self.norm2, self.norm2.eps)
-        h = self.mlp.layers[0](h, act="gelu")
+        fc1, fc2 = self.mlp.layers[0], self.mlp.layers[1]
         if next_norm is None:
-            return self.mlp.layers[1](h, residual=x)
-        t, x = FN.add_layer_norm(x, self.mlp.layers[1](h), next_norm, next_norm.eps)
+            return FN.mlp2(h, fc1, fc2, "gelu", residual=x)
+        t, x = FN.add_layer_norm(x, FN.mlp2(h, fc1, fc2, "gelu"), next_norm, next_norm.eps)
         return x, t
 
 
