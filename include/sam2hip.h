@@ -145,8 +145,8 @@ int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0,
                  const uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st);
 /* Frame-batched flash backward (the flash domain: bf16, head_dim 32..64 / 128 / 256, Lq >= 128):
- * nfr frames x bpf batches * x H heads of the tracking loop in one launch per kernel -- Q / O / dO / dQ / lse uniform
- * [nfr*bpf] batches, K / V / dK / dV packed per frame (frame f: bpf blocks of fr_lk[f] rows
+ * nfr frames x bpf batches x H heads of the tracking loop in one launch per kernel -- Q / O / dO /
+ * dQ / lse uniform [nfr*bpf] batches, K / V / dK / dV packed per frame (frame f: bpf blocks of fr_lk[f] rows
  * starting at row fr_krow[f]); frame f's dropout indices start at fr_idx0[f] (host arrays of
  * nfr <= 32 entries); keep (nullable) = the frames' forward keep bitmaps, frame f's from word
  * fr_koff[f].  The memory-attention backward of every frame at once
