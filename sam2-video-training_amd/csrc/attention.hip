@@ -910,6 +910,10 @@ static int attn_dispatch(const AttnArgs& a, hipStream_t st) {
   return (int)hipErrorInvalidValue;
 }
 
+// the flash kernels address their LDS-DMA operands with 32-bit element offsets from the
+// (batch, head) base: rows x row stride must stay below 2^31 elements
+static bool flash_span_ok(int64_t rows, int64_t stride) { return rows * (stride < 0 ? -stride : stride) < (1ll << 31); }
+
 static bool attn_aligned(int dt, int D, const void* p, int64_t s1, int64_t s2, int64_t s3) {
   const int vec = dt == S2H_BF16 ? 8 : 4;
   return ((uintptr_t)p % 16 == 0) && D % vec == 0 && s1 % vec == 0 && s2 % vec == 0 && s3 % vec == 0;
@@ -927,7 +931,8 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
   if (!attn_aligned(dt, D, q, sqb, sqh, sql) || !attn_aligned(dt, D, k, skb, skh, skl) ||
       !attn_aligned(dt, D, v, svb, svh, svl))
     return (int)hipErrorInvalidValue;
-  const bool flash = s2h_flash_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol);
+  const bool flash = s2h_flash_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol) &&
+                     flash_span_ok(Lk, skl) && flash_span_ok(Lk, svl);
   // a keep bitmap is written by the flash path only, for the head-dim-256 backward that reads it
   if (keep && p_drop > 0.f && (!flash || D != 256)) return (int)hipErrorInvalidValue;
   if (flash) {
@@ -966,7 +971,8 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
     return (int)hipErrorInvalidValue;
   const bool flash = s2h_flash_bwd_eligible(dt, Lq, D) && attn_aligned(dt, D, o, sob, soh, sol) &&
                      attn_aligned(dt, D, dq, sdqb, sdqh, sdql) && attn_aligned(dt, D, dk, sdkb, sdkh, sdkl) &&
-                     attn_aligned(dt, D, dv, sdvb, sdvh, sdvl);
+                     attn_aligned(dt, D, dv, sdvb, sdvh, sdvl) && flash_span_ok(Lk, skl) &&
+                     flash_span_ok(Lk, svl) && flash_span_ok(Lq, sql) && flash_span_ok(Lq, sgl);
   if (keep && p_drop > 0.f && (!flash || D != 256)) return (int)hipErrorInvalidValue;
   if (flash) {
     const int slot = s2h_prof_begin(st, 2, (int64_t)B * H, Lq, Lk, D, 2);

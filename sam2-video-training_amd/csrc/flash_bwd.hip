@@ -760,8 +760,9 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
   a.nfr = nfr; a.bpf = bpf;
   a.keep = keep;
   int lk_max = 0;
+  if ((int64_t)Lq * std::max(sql, sgl) >= (1ll << 31)) return (int)hipErrorInvalidValue;  // 32-bit DMA offsets
   for (int f = 0; f < nfr; ++f) {
-    if (fr_lk[f] <= 0) return (int)hipErrorInvalidValue;
+    if (fr_lk[f] <= 0 || (int64_t)fr_lk[f] * std::max(skl, svl) >= (1ll << 31)) return (int)hipErrorInvalidValue;
     a.fr_lk[f] = fr_lk[f]; a.fr_krow[f] = fr_krow[f]; a.fr_idx0[f] = fr_idx0[f];
     a.fr_koff[f] = keep ? fr_koff[f] : 0;
     lk_max = std::max(lk_max, fr_lk[f]);

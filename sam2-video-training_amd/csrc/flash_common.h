@@ -70,7 +70,7 @@ __device__ __forceinline__ void dma_tile(char* lds_tile, const bf16* src, int64_
     const int pos = lane % C::NCH;
     const int c = pos ^ swz_x<DP, SW>(row);
     const int gr = min(r0 + row, nrows - 1);
-    const bf16* g = src + (int64_t)gr * ld + (c * 8 < dvalid ? c * 8 : 0);
+    const bf16* g = src + (gr * (int)ld + (c * 8 < dvalid ? c * 8 : 0));  // 32-bit offsets (host-checked)
     if constexpr (ASM)
       lds_dma16(g, lds_tile + piece * 1024);
     else
@@ -109,7 +109,7 @@ __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, in
     const int slot = piece * 64 + lane;
     const int row = slot / I::SPR, c = slot % I::SPR;
     const int gr = min(r0 + row, nrows - 1);
-    const bf16* g = src + (int64_t)gr * ld + (c < DP / 8 && c * 8 < dvalid ? c * 8 : 0);
+    const bf16* g = src + (gr * (int)ld + (c < DP / 8 && c * 8 < dvalid ? c * 8 : 0));  // 32-bit offsets
     if constexpr (ASM)
       lds_dma16(g, lds_tile + piece * 1024);
     else

@@ -458,14 +458,16 @@ struct GImg {
       const int irow = piece * (1024 / RB) + lane / LPR;  // image row
       const int c = swz(irow, lane % LPR);                 // logical 16-B chunk held at this slot
       const bf16* src;
+      // 32-bit element offsets: gemm_glds_ok keeps operands past 2^31 elements on the
+      // register-staged kernel (a 64-bit multiply per piece was a third of the step's VALU here)
       if (KC) {
         const int r = min(row0 + irow, nrows - 1);
         const int k = k0 + 8 * c < kend ? k0 + 8 * c : k0;
-        src = base + (int64_t)r * ld_row + k;
+        src = base + (r * (int)ld_row + k);
       } else {
         const int k = min(k0 + irow, kend - 1);
         const int r = row0 + 8 * c < nrows ? row0 + 8 * c : row0;
-        src = base + (int64_t)k * ld_k + r;
+        src = base + (k * (int)ld_k + r);
       }
       lds_dma16(src, img + piece * 1024);
     }
@@ -676,8 +678,12 @@ static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
   const int64_t lda = akc ? a.lda_m : a.lda_k, ldb = bkc ? a.ldb_n : a.ldb_k;
   const int aext = akc ? a.K : a.M, bext = bkc ? a.K : a.N;  // contiguous extents
+  // per-batch operand extents addressed with 32-bit element offsets in GImg::dma
+  const int64_t aspan = akc ? (int64_t)a.M * lda : (int64_t)a.K * lda;
+  const int64_t bspan = bkc ? (int64_t)a.N * ldb : (int64_t)a.K * ldb;
   return al(a.A) && al(a.B) && lda % 8 == 0 && ldb % 8 == 0 && aext % 8 == 0 && bext % 8 == 0 &&
-         (batch == 1 || (a.sA % 8 == 0 && a.sB % 8 == 0)) && a.K > 0;
+         (batch == 1 || (a.sA % 8 == 0 && a.sB % 8 == 0)) && a.K > 0 && aspan < (1ll << 31) &&
+         bspan < (1ll << 31);
 }
 
 // split-K decision + output-group alignment for a BM x BN tiling
