@@ -56,9 +56,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   // one LDS array: [2 stages][K tile | V tile]
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * I::TILEB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int split = blockIdx.z;
-  const int q = blockIdx.x * FL_QB + w * 16 + ql;  // this lane's query row
+  const WgIdx wi = wg_xcd_order();
+  if (wi.y >= a.BH) return;  // grid padding
+  const int bh = wi.y, b = bh / a.H, h = bh % a.H;
+  const int split = wi.z;
+  const int q = wi.x * FL_QB + w * 16 + ql;  // this lane's query row
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* K = a.k + b * a.skb + h * a.skh;
   const bf16* V = a.v + b * a.svb + h * a.svh;
@@ -328,7 +330,7 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
 
 template <int DP>
 static int flash_launch(FlashArgs& a, hipStream_t st) {
-  dim3 grid((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits);
+  dim3 grid((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
   if (a.p_drop <= 0.f) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE>), grid, dim3(FL_WAVES * 64), 0, st, a);
   else if (a.keep) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS>), grid, dim3(FL_WAVES * 64), 0, st, a);
   else hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH>), grid, dim3(FL_WAVES * 64), 0, st, a);

@@ -127,9 +127,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB + 2 * FL_WAVES * 256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int split = blockIdx.z;
-  const int q = blockIdx.x * FL_QB + w * 16 + ql;
+  const WgIdx wi = wg_xcd_order();
+  if (wi.y >= a.BH) return;  // grid padding
+  const int bh = wi.y, b = bh / a.H, h = bh % a.H;
+  const int split = wi.z;
+  const int q = wi.x * FL_QB + w * 16 + ql;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
   const KvFrame fr = kv_frame(a, bh);
@@ -142,7 +144,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   // keep words of this wave's 16 queries for the 64 keys of a tile: lane 2i + j (< 32) fetches
   // word j of query i (lanes 32..63 repeat them); LDS holds them as one uint2 per query
   constexpr bool bits = DROP == DROP_BITS;
-  const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min((int)blockIdx.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
+  const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min(wi.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
                                : nullptr;
   char* bits_lds = smem + 2 * 2 * C::TILEB + w * 256;
   auto dma_bits = [&](int stage, int k0) { lds_dma4(KEEPQ + (k0 >> 5) + (lane & 1), bits_lds + stage * FL_WAVES * 256); };
@@ -301,10 +303,12 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
   using C = FlashCfg<DP, QT>;
   __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB];  // [stage][Q | dO]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int key = blockIdx.x * FL_QB + w * 16 + kl;  // this lane's key (B-operand column)
+  const WgIdx wi = wg_xcd_order();
+  if (wi.y >= a.BH) return;  // grid padding
+  const int bh = wi.y, b = bh / a.H, h = bh % a.H;
+  const int key = wi.x * FL_QB + w * 16 + kl;  // this lane's key (B-operand column)
   const KvFrame fr = kv_frame(a, bh);
-  if ((int)blockIdx.x * FL_QB >= fr.Lk) return;  // frame-table launch: past this frame's keys
+  if (wi.x * FL_QB >= fr.Lk) return;  // frame-table launch: past this frame's keys
   const bool kv = key < fr.Lk;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
@@ -449,10 +453,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   char* Kblk = smem;
   char* stages = smem + CK::TILEB;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, kl = lane & 31;
-  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
-  const int key = blockIdx.x * (NWV * 32) + w * 32 + kl;
+  const WgIdx wi = wg_xcd_order();
+  if (wi.y >= a.BH) return;  // grid padding
+  const int bh = wi.y, b = bh / a.H, h = bh % a.H;
+  const int key = wi.x * (NWV * 32) + w * 32 + kl;
   const KvFrame fr = kv_frame(a, bh);
-  if ((int)blockIdx.x * (NWV * 32) >= fr.Lk) return;  // frame-table launch: past this frame's keys
+  if (wi.x * (NWV * 32) >= fr.Lk) return;  // frame-table launch: past this frame's keys
   const bool kv = key < fr.Lk;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* G = a.g + b * a.sgb + h * a.sgh;
@@ -460,7 +466,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   const bf16* V = fr.v;
   // query tiles [qt0, qt0 + nt) of this workgroup (kv_splits > 1: partial dK / dV)
   const int nt_all = (a.Lq + QT - 1) / QT;
-  const int qt0 = blockIdx.z * a.kv_tiles_per_split;
+  const int qt0 = wi.z * a.kv_tiles_per_split;
   const int nt = max(0, min(nt_all, qt0 + a.kv_tiles_per_split) - qt0);
   const int qbase = qt0 * QT;
 
@@ -475,11 +481,11 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   // keep words of this wave's 32 keys (word key / 32) for the 32 queries of a tile (lanes 32..63
   // repeat lanes 0..31)
   constexpr bool bits = DROP == DROP_BITS;
-  const uint32_t* KEEPW = bits ? fr.keep + min((int)blockIdx.x * NWV + w, fr.kw - 1) : nullptr;
+  const uint32_t* KEEPW = bits ? fr.keep + min(wi.x * NWV + w, fr.kw - 1) : nullptr;
   auto dma_bits = [&](char* stage, int q0) {
     lds_dma4(KEEPW + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * fr.kw, stage + 2 * C::TILEB + w * 512 + 256);
   };
-  dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, blockIdx.x * (NWV * 32), fr.Lk, w, lane);
+  dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, wi.x * (NWV * 32), fr.Lk, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
@@ -565,7 +571,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
 
   if (!kv) return;
   if (a.kv_splits > 1) {  // fp32 partials, summed (and scaled, cast) by flash_bwd_dkv_combine_kernel
-    float* W = a.ws_dkv + (((int64_t)blockIdx.z * a.BH + bh) * a.Lk + key) * 2 * DP;  // single-frame only
+    float* W = a.ws_dkv + (((int64_t)wi.z * a.BH + bh) * a.Lk + key) * 2 * DP;  // single-frame only
 #pragma unroll
     for (int d = 0; d < ND; ++d)
 #pragma unroll
@@ -659,7 +665,7 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.BH * a.Lq;
   hipLaunchKernelGGL((flash_bwd_di_kernel<DP>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
   const int drop = a.p_drop <= 0.f ? DROP_NONE : (a.keep ? DROP_BITS : DROP_HASH);
-  const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, a.BH, a.splits);
+  const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
   if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE>), gq, dim3(FL_WAVES * 64), 0, st, a);
   else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS>), gq, dim3(FL_WAVES * 64), 0, st, a);
   else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH>), gq, dim3(FL_WAVES * 64), 0, st, a);
@@ -667,7 +673,7 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((flash_bwd_dq_combine_kernel<DP>), dim3((unsigned)((rows * DP / 4 + 255) / 256)), dim3(256), 0,
                        st, a);
   if constexpr (DP == 256) {
-    const dim3 gk((a.Lk + 127) / 128, a.BH, a.kv_splits);
+    const dim3 gk((a.Lk + 127) / 128, pad_bh8(a.BH), a.kv_splits);
     if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE>), gk, dim3(256), 0, st, a);
     else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS>), gk, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH>), gk, dim3(256), 0, st, a);
@@ -676,7 +682,7 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
       hipLaunchKernelGGL((flash_bwd_dkv_combine_kernel<DP>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
     }
   } else {
-    const dim3 gk((a.Lk + FL_QB - 1) / FL_QB, a.BH);
+    const dim3 gk((a.Lk + FL_QB - 1) / FL_QB, pad_bh8(a.BH));
     if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP, DROP_NONE>), gk, dim3(FL_WAVES * 64), 0, st, a);
     else hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP, DROP_HASH>), gk, dim3(FL_WAVES * 64), 0, st, a);
   }

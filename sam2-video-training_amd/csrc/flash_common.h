@@ -118,6 +118,24 @@ __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, in
   }
 }
 
+// XCD-aware work order: workgroup `id` (x fastest) runs on XCD id % 8, so round-robin placed the
+// workgroups that re-read one (batch, head)'s operands -- the query blocks of a forward / dQ
+// launch, the key blocks of a dK/dV launch -- on 8 different L2s.  Here XCD j runs every x (and z)
+// of the batch-heads y = j, j + 8, ... in order: they share its L2, and consecutive batch-heads
+// (different frames of a frame-table launch, different key counts) still spread over all XCDs.
+// The host pads gridDim.y to a multiple of 8 (pad_bh8); workgroups with y >= BH return at once.
+struct WgIdx {
+  int x, y, z;
+};
+__device__ __forceinline__ WgIdx wg_xcd_order() {
+  const int gx = gridDim.x, gy8 = gridDim.y / 8;
+  const int id = blockIdx.x + gx * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int xcd = id % 8, m = id / 8;
+  const int x = m % gx, t = m / gx;
+  return WgIdx{x, (t % gy8) * 8 + xcd, t / gy8};
+}
+static inline unsigned pad_bh8(int bh) { return (unsigned)((bh + 7) / 8 * 8); }
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
