@@ -68,12 +68,17 @@ class Store:
     offsets[f] of a flat [total] buffer; the per-frame element count scales with the frame's
     memory rows)."""
 
-    def __init__(self, tape, shape, dtype, scale=None):
+    def __init__(self, tape, shape, dtype, scale=None, alias=None):
         self.shape0 = tuple(shape)
         self.dtype = dtype
         F = tape.F
         n0 = math.prod(shape)
-        if scale is None:  # uniform
+        self.aliased = alias is not None
+        if alias is not None:  # uniform storage the caller already holds
+            assert scale is None and alias.numel() == F * n0 and alias.dtype == dtype
+            self.numels = [n0] * F
+            self.buf = alias
+        elif scale is None:  # uniform
             self.numels = [n0] * F
             self.buf = torch.empty(F * n0, device=tape.device, dtype=dtype)
         else:  # element count of frame f = n0 * scale[f] / scale[0]
@@ -108,6 +113,18 @@ class Store:
         if lead == "merge":
             return self.buf.view(F * self.shape0[0], *self.shape0[1:])
         return self.buf.view(F, *self.shape0)
+
+
+def _alias_rows(stacked, F, t):
+    """flat view of frames [first, first + F) of a frame-stacked tensor, when contiguous"""
+    if stacked is None:
+        return None
+    src, first = stacked
+    if src.dtype != t.dtype or not src.is_contiguous() or first + F > src.shape[0]:
+        return None
+    if src[first].numel() != t.numel():
+        return None
+    return src[first:first + F].reshape(-1)
 
 
 class FlatStore:
@@ -187,16 +204,23 @@ class FrameTape:
                 raise RuntimeError(f"tape {self.name}: tensor aliases tape storage but is not a recorded value "
                                    f"(slice / copy outside the FN ops?)")
 
-    def input(self, name, t, requires_grad=True):
+    def input(self, name, t, requires_grad=True, stacked=None):
         """declare a grad-carrying per-frame input (e.g. the backbone feature of this frame): its
-        frame values are stacked (copied) so the backward can return [F, ...] gradients"""
+        frame values are stacked (copied) so the backward can return [F, ...] gradients.
+        stacked = (tensor, first): the caller's values already ARE frame-stacked -- this tape's
+        frame f is tensor[first + f] (contiguous) -- and the store aliases them (no copy)."""
         vid = ("in", name)
         if self.f == 0:
-            self.stores[vid] = Store(self, t.shape, t.dtype)
+            st = Store(self, t.shape, t.dtype, alias=_alias_rows(stacked, self.F, t))
+            self.stores[vid] = st
             self.requires[vid] = requires_grad
             self.inputs[name] = vid
-        slot = self.stores[vid].frame(self.f)
-        slot.copy_(t.detach())
+        st = self.stores[vid]
+        slot = st.frame(self.f)
+        if st.aliased:
+            assert slot.data_ptr() == t.data_ptr(), f"tape {self.name}: input {name} is not the stacked frame"
+        else:
+            slot.copy_(t.detach())
         self._register(vid, slot)
         return slot
 

@@ -267,6 +267,48 @@ class _QKVAttention(torch.autograd.Function):
         return dqkv, None, None, None
 
 
+class _PoolQKVAttention(torch.autograd.Function):
+    """Hiera query-pooling attention (hieradet.py:56-81 with q_pool): q = 2x2 max-pool of the q
+    third of the fused qkv [B, H, W, 3d] projection, k / v read in place.  The backward writes dk,
+    dv and the max-pool scatter of dq into ONE dqkv buffer (separate select / slice inputs made
+    autograd zero-fill a qkv-sized buffer per slice and add them)."""
+
+    @staticmethod
+    def forward(ctx, qkv, nh):
+        B, H, W, d3 = qkv.shape
+        d = d3 // 3
+        hd = d // nh
+        q = ops.maxpool2(qkv[..., :d]).view(B, (H // 2) * (W // 2), nh, hd)
+        qkv5 = qkv.view(B, H * W, 3, nh, hd)
+        o = torch.empty(q.shape, device=qkv.device, dtype=qkv.dtype)
+        lse = torch.empty(B, nh, q.shape[1], device=qkv.device, dtype=torch.float32)
+        scale = 1.0 / math.sqrt(hd)
+        ops.attn_fwd(q, qkv5[:, :, 1], qkv5[:, :, 2], o, lse, scale)
+        ctx.nh, ctx.scale = nh, scale
+        ctx.save_for_backward(qkv, q, o, lse)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        qkv, q, o, lse = ctx.saved_tensors
+        B, H, W, d3 = qkv.shape
+        d = d3 // 3
+        qkv5 = qkv.view(B, H * W, 3, ctx.nh, d // ctx.nh)
+        dqkv = torch.empty_like(qkv)
+        dqkv5 = dqkv.view(qkv5.shape)
+        dq = torch.empty_like(q)
+        ops.attn_bwd(q, qkv5[:, :, 1], qkv5[:, :, 2], o, do.contiguous(), lse, dq, dqkv5[:, :, 1], dqkv5[:, :, 2],
+                     ctx.scale)
+        ops.maxpool2_bwd(qkv[..., :d], dq.view(B, H // 2, W // 2, d), dqkv[..., :d])
+        return dqkv, None
+
+
+def pooled_qkv_attention(qkv, num_heads):
+    """attention of the 2x2-max-pooled q third of a fused [B, H, W, 3d] projection against its full
+    k / v (Hiera's stage-transition blocks) -> [B, H/2 * W/2, heads, d / heads]"""
+    return _PoolQKVAttention.apply(qkv, num_heads)
+
+
 def qkv_attention(qkv, scale=None, p_drop=0.0, rope=None):
     """softmax(scale q k^T) v with q, k, v = qkv[:, :, 0/1/2] ([B, L, 3, H, d]); rope = (cos, sin,
     period) rotates q and k (every row) first."""

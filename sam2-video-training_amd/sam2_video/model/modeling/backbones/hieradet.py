@@ -35,12 +35,9 @@ class MultiScaleAttention(nn.Module):
         d, nh = self.dim_out, self.num_heads
         qkv = self.qkv(x)  # [B, H, W, 3d]
         qkv5 = qkv.view(B, H * W, 3, nh, d // nh)
-        if self.q_pool:
-            k, v = qkv5[:, :, 1], qkv5[:, :, 2]
-            q = FN.maxpool2(qkv[..., :d])  # pooled straight out of the fused qkv (pixel stride 3d)
+        if self.q_pool:  # q pooled straight out of the fused qkv; one dqkv in the backward
+            o = FN.pooled_qkv_attention(qkv, nh)
             H, W = H // 2, W // 2
-            q = q.view(B, H * W, nh, d // nh)
-            o = FN.attention(q, k, v)
         else:
             o = FN.qkv_attention(qkv5)  # one packed dqkv in the backward
         return self.proj(o.reshape(B, H, W, d))

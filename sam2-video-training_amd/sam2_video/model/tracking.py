@@ -59,7 +59,7 @@ class FrameTracker:
         tp = self.ma
         tp.begin_frame()
         with recording(tp):
-            f_in = tp.input("feat", feat_t, requires_grad=self.feats.requires_grad)
+            f_in = tp.input("feat", feat_t, requires_grad=self.feats.requires_grad, stacked=(self.feats.detach(), 1))
             pix = m._prepare_memory_conditioned_features(t, False, f_in, pos, self.T, output_dict, self.O, tape=tp)
             if tp.f == 0:
                 self.ma_out = tp.out_vid(pix)
@@ -68,12 +68,16 @@ class FrameTracker:
 
     def sam_heads(self, t, pix, prompt, s0t, s1t):
         gi, _ = self.dec_of[t]
-        tp = self.decs[gi][0]
+        tp, frames = self.decs[gi]
+        # the high-res features of consecutive frames are already stacked: alias, do not copy
+        run = frames == list(range(frames[0], frames[0] + len(frames)))
         tp.begin_frame()
         with recording(tp):
             p_in = tp.input("pix", pix)
-            s0_in = tp.input("s0", s0t, requires_grad=self.s0.requires_grad)
-            s1_in = tp.input("s1", s1t, requires_grad=self.s1.requires_grad)
+            s0_in = tp.input("s0", s0t, requires_grad=self.s0.requires_grad,
+                             stacked=(self.s0.detach(), frames[0]) if run else None)
+            s1_in = tp.input("s1", s1t, requires_grad=self.s1.requires_grad,
+                             stacked=(self.s1.detach(), frames[0]) if run else None)
             low, high, ious, ptr, score = self.m._forward_sam_heads(p_in, prompt, (s0_in, s1_in), self.O)
             if tp.f == 0:
                 self.vids[gi] = (tp.out_vid(high), tp.out_vid(ious))
