@@ -243,20 +243,35 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 }
 
 // ------------------------------------------------- backward: Di = rowsum(dO*O)
+// 2^lpr_log2 lanes per row (the fewest that cover D with 16-B vectors when `vec`), so short head
+// dims (the decoder's 16 over 852k rows) do not launch one wave per row
 template <typename T>
-__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+__global__ __launch_bounds__(256) void attn_bwd_pre_kernel(AttnArgs a, int lpr_log2, int vec) {
+  constexpr int V = 16 / sizeof(T);
+  const int lpr = 1 << lpr_log2;
+  const int64_t row = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> lpr_log2;
+  const int sub = threadIdx.x & (lpr - 1);
   const int64_t nrows = (int64_t)a.B * a.H * a.Lq;
-  if (row >= nrows) return;
-  const int qi = row % a.Lq;
-  const int bh = row / a.Lq, b = bh / a.H, h = bh % a.H;
-  const T* dO = (const T*)a.o + b * a.sob + h * a.soh + (int64_t)qi * a.sol;
-  const T* O = (const T*)a.fo + b * a.sfb + h * a.sfh + (int64_t)qi * a.sfl;
   float acc = 0.f;
-  for (int d = lane; d < a.D; d += 64) acc += to_f32(dO[d]) * to_f32(O[d]);
-  acc = wave_sum(acc);
-  if (lane == 0) a.di[row] = acc;
+  if (row < nrows) {
+    const int qi = row % a.Lq;
+    const int bh = row / a.Lq, b = bh / a.H, h = bh % a.H;
+    const T* dO = (const T*)a.o + b * a.sob + h * a.soh + (int64_t)qi * a.sol;
+    const T* O = (const T*)a.fo + b * a.sfb + h * a.sfh + (int64_t)qi * a.sfl;
+    if (vec) {
+      for (int d = sub * V; d < a.D; d += lpr * V) {
+        const uint4 gu = *(const uint4*)(dO + d), ou = *(const uint4*)(O + d);
+        const T* gb = (const T*)&gu;
+        const T* ob = (const T*)&ou;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc += to_f32(gb[e]) * to_f32(ob[e]);
+      }
+    } else {
+      for (int d = sub; d < a.D; d += lpr) acc += to_f32(dO[d]) * to_f32(O[d]);
+    }
+  }
+  for (int off = lpr >> 1; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+  if (row < nrows && sub == 0) a.di[row] = acc;
 }
 
 // ------------------------------------------------------- backward: dQ
@@ -879,7 +894,18 @@ template <typename T, int DP>
 static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.B * a.H * a.Lq;
   const int slot = s2h_prof_begin(st, 2, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
-  hipLaunchKernelGGL((attn_bwd_pre_kernel<T>), dim3((rows + 3) / 4), dim3(256), 0, st, a);
+  {
+    constexpr int V = 16 / sizeof(T);
+    auto al = [](const void* p, int64_t s1, int64_t s2, int64_t s3) {
+      return (uintptr_t)p % 16 == 0 && s1 % V == 0 && s2 % V == 0 && s3 % V == 0;
+    };
+    const int vec = a.D % V == 0 && al(a.o, a.sob, a.soh, a.sol) && al(a.fo, a.sfb, a.sfh, a.sfl);
+    const int per = vec ? (a.D + V - 1) / V : a.D;  // loads per row
+    int lg = 0;
+    while ((1 << lg) < per && lg < 6) ++lg;
+    const int64_t threads = rows << lg;
+    hipLaunchKernelGGL((attn_bwd_pre_kernel<T>), dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, a, lg, vec);
+  }
   dim3 gq((a.Lq + 63) / 64, a.B * a.H);
   bool done_dq = false, done_dkv = false;
   if constexpr (DP <= 64) {
