@@ -35,8 +35,8 @@ ALL = ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder", "p
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--size", default="base_plus")
     ap.add_argument("--image-size", type=int, default=512)
     ap.add_argument("--frames", type=int, default=8)
