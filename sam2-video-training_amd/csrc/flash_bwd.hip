@@ -124,8 +124,9 @@ template <int DP, int DROP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   using C = FlashCfg<DP, 64>;
+  using I = PadImg<DP>;  // padded K / V images (the forward's: conflict-free b128 and transposing reads)
   // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * C::TILEB + 2 * FL_WAVES * 256];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * I::TILEB + 2 * FL_WAVES * 256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
@@ -146,12 +147,13 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   constexpr bool bits = DROP == DROP_BITS;
   const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min(wi.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
                                : nullptr;
-  char* bits_lds = smem + 2 * 2 * C::TILEB + w * 256;
+  char* bits_lds = smem + 2 * 2 * I::TILEB + w * 256;
+  const int npw = I::pieces(w);
   auto dma_bits = [&](int stage, int k0) { lds_dma4(KEEPQ + (k0 >> 5) + (lane & 1), bits_lds + stage * FL_WAVES * 256); };
 
   if (nt > 0) {
-    dma_tile<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane, a.D);
-    dma_tile<DP, 64, FL_WAVES, true>(smem + C::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane, a.D);
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane, a.D);
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane, a.D);
     if constexpr (bits) dma_bits(0, t0 * C::KT);
   }
   const bool qv = q < a.Lq;
@@ -174,17 +176,19 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
 
   for (int it = 0; it < nt; ++it) {
     const int k0 = (t0 + it) * C::KT;
-    char* Kb = smem + (it & 1) * 2 * C::TILEB;
-    char* Vb = Kb + C::TILEB;
+    char* Kb = smem + (it & 1) * 2 * I::TILEB;
+    char* Vb = Kb + I::TILEB;
     if (it + 1 < nt) {
-      char* Kn = smem + ((it + 1) & 1) * 2 * C::TILEB;
-      dma_tile<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane, a.D);
-      dma_tile<DP, 64, FL_WAVES, true>(Kn + C::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane, a.D);
+      char* Kn = smem + ((it + 1) & 1) * 2 * I::TILEB;
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane, a.D);
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane, a.D);
+      // this wave's pieces of tile `it` have landed once all but the ones just issued retired
       if constexpr (bits) {
         dma_bits((it + 1) & 1, k0 + C::KT);
-        wait_vmcnt<2 * C::PPW + 1>();
+        if (npw > I::PPW_LO) wait_vmcnt<2 * (I::PPW_LO + 1) + 1>();
+        else wait_vmcnt<2 * I::PPW_LO + 1>();
       } else {
-        wait_vmcnt<2 * C::PPW>();
+        wait_vmcnt_pieces<2, I::PPW_LO>(npw);
       }
     } else {
       wait_vmcnt<0>();
@@ -199,9 +203,9 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       const int row = kb * 16 + ql;
 #pragma unroll
       for (int t = 0; t < C::NT; ++t) {
-        const bf16x8 kf = *(const bf16x8*)(Kb + swz<DP>(row, 4 * t + g));
+        const bf16x8 kf = *(const bf16x8*)(Kb + row * I::ROWB + 16 * (4 * t + g));
         s[kb] = mfma16(kf, qf[t], s[kb]);
-        const bf16x8 vf = *(const bf16x8*)(Vb + swz<DP>(row, 4 * t + g));
+        const bf16x8 vf = *(const bf16x8*)(Vb + row * I::ROWB + 16 * (4 * t + g));
         dp[kb] = mfma16(vf, gf[t], dp[kb]);
       }
     }
@@ -250,7 +254,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int d = 0; d < C::ND; ++d) acc[d] = mfma16(tr_frag_perm<DP>(Kb, 32 * c, 16 * d, lane), dsb[c], acc[d]);
+      for (int d = 0; d < C::ND; ++d) acc[d] = mfma16(tr_frag_pad<I::ROWB>(Kb, 32 * c, 16 * d, lane), dsb[c], acc[d]);
 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wg_barrier();

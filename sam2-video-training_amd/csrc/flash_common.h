@@ -98,6 +98,20 @@ struct PadImg {
   __device__ static __forceinline__ int pieces(int w) { return PPW_LO + (w < NHI ? 1 : 0); }
 };
 
+// Transposing fragment read from a padded image (PadImg row pitch): A[m = column c0 + (lane & 15)]
+// [k = 8g + j] with k <-> image row rbase + 4g + j (j < 4) and rbase + 16 + 4g + (j - 4) (j >= 4)
+// -- tr_frag_perm's layout, conflict-free on the padded pitch.
+template <int ROWB>
+__device__ __forceinline__ bf16x8 tr_frag_pad(const char* img, int rbase, int c0, int lane) {
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int r0 = rbase + 4 * g + qq;
+  const int dcol = c0 + 4 * pp;
+  v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + r0 * ROWB + 2 * dcol));
+  v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(img + (r0 + 16) * ROWB + 2 * dcol));
+  v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, cat);
+}
+
 template <int DP, int ROWS = 64, int NWV = FL_WAVES, bool ASM = false>
 __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, int64_t ld, int r0, int nrows, int w,
                                              int lane, int dvalid = DP) {
