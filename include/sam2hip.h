@@ -107,8 +107,8 @@ int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t
  * Replaces F.scaled_dot_product_attention at hieradet.py:70 (windowed / global
  * Hiera attention), transformer.py:243 (two-way decoder attention) and
  * transformer.py:306 (memory-attention RoPE self / cross attention).
- * bf16 with head_dim 128/256, or 32..64 in steps of 8 (run in a zero-padded 64 image: Hiera's 56),
- * and >= 128 query rows takes the flash path
+ * bf16 with head_dim 256, or 32..128 in steps of 8 (run in a zero-padded 64 / 128 image: Hiera-B+'s
+ * 56, Hiera-L's 72), and >= 128 query rows takes the flash path
  * (16x16x32 MFMA, LDS-DMA K/V ring, key range split over workgroups): it wants a
  * device workspace of s2h_attn_fwd_ws_bytes(...) bytes (ws = NULL / too small
  * just disables the key split). */
@@ -144,7 +144,7 @@ int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
                  void* dv, int64_t sdvb, int64_t sdvh, int64_t sdvl,
                  const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, uint64_t idx0,
                  const uint32_t* keep, void* ws, int64_t ws_bytes, hipStream_t st);
-/* Frame-batched flash backward (the flash domain: bf16, head_dim 32..64 / 128 / 256, Lq >= 128):
+/* Frame-batched flash backward (the flash domain: bf16, head_dim 32..128 / 256, Lq >= 128):
  * nfr frames x bpf batches x H heads of the tracking loop in one launch per kernel -- Q / O / dO /
  * dQ / lse uniform [nfr*bpf] batches, K / V / dK / dV packed per frame (frame f: bpf blocks of fr_lk[f] rows
  * starting at row fr_krow[f]); frame f's dropout indices start at fr_idx0[f] (host arrays of

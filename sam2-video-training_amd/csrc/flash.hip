@@ -313,10 +313,10 @@ extern "C" int s2h_attn_config(int flash_enable) {
   return prev;
 }
 
-// eligible: bf16, head_dim 128 / 256 or 32..64 in steps of 8 (padded to a 64 image), >= 128
-// query rows, 16-B aligned rows
+// eligible: bf16, head_dim 256 or 32..128 in steps of 8 (padded to a 64 / 128 image: Hiera-B+'s
+// 56, Hiera-L's 72), >= 128 query rows, 16-B aligned rows
 int s2h_flash_eligible(int dt, int Lq, int D) {
-  const bool dok = D == 128 || D == 256 || (D >= 32 && D <= 64 && D % 8 == 0);
+  const bool dok = D == 256 || (D >= 32 && D <= 128 && D % 8 == 0);
   return g_flash_enabled && dt == S2H_BF16 && dok && Lq >= 128;
 }
 
@@ -324,7 +324,7 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
   int splits, tps;
   flash_plan(B * H, Lq, Lk, splits, tps);
   if (splits <= 1) return 0;
-  const int DPd = D <= 64 ? 64 : D;  // padded image width
+  const int DPd = flash_dp(D);  // padded image width
   return (int64_t)splits * B * H * Lq * (DPd + 2) * 4;
 }
 
@@ -365,7 +365,7 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed;
   a.seed_off = s2h_rng_offset_ptr();
-  const int DPd = D <= 64 ? 64 : D;  // padded image width of the partials
+  const int DPd = flash_dp(D);  // padded image width of the partials
   flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
   const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (DPd + 2) * 4 : 0;
   if (need > ws_bytes || (need > 0 && ws == nullptr)) {  // no workspace: one split
@@ -376,6 +376,6 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
     a.ws_ml = a.ws_o + (int64_t)a.splits * a.BH * Lq * DPd;
   }
   if (D == 256) return flash_launch<256>(a, st);
-  if (D == 128) return flash_launch<128>(a, st);
-  return flash_launch<64>(a, st);  // D <= 64 (s2h_flash_eligible)
+  if (D > 64) return flash_launch<128>(a, st);  // 72..128 (s2h_flash_eligible)
+  return flash_launch<64>(a, st);               // 32..64
 }

@@ -297,7 +297,8 @@ __global__ __launch_bounds__(256) void flash_bwd_dq_combine_kernel(FlashBwdArgs 
 }
 
 // ------------------------------------------------------------------ dK / dV
-// head_dim 128, or <= 64 padded to a 64 image (Hiera, hieradet.py:56-81): 8 waves x 16 keys, K / V
+// head_dim 72..128 in a 128 image, or 32..64 in a 64 image (Hiera, hieradet.py:56-81; B+ 56, L 72):
+// 8 waves x 16 keys, K / V
 // fragments in registers; Q / dO tiles of QT queries (64 for the 64 image: a 32-row tile would be
 // half a DMA piece per wave) consumed in 32-query halves.
 template <int DP, int DROP>
@@ -653,7 +654,7 @@ static void flash_bwd_ws_layout(int BH, int Lq, int Lk, int D, int64_t& dq_bytes
   int splits, tps, kvs, ktps;
   flash_bwd_plan(BH, Lq, Lk, splits, tps);
   flash_bwd_kv_plan(BH, Lq, Lk, kvs, ktps);
-  const int DPd = D <= 64 ? 64 : D;  // padded image width of the dQ partials
+  const int DPd = flash_dp(D);  // padded image width of the dQ partials
   dq_bytes = splits > 1 ? (int64_t)splits * BH * Lq * DPd * 4 : 0;
   dkv_bytes = (D == 256 && kvs > 1) ? (int64_t)kvs * BH * Lk * 2 * D * 4 : 0;
 }
@@ -737,11 +738,11 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
   if (dkv_bytes > 0) a.ws_dkv = (float*)((char*)ws + dq_bytes);
   else { a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32; }
   if (D == 256) return flash_bwd_launch<256>(a, st);
-  if (D == 128) return flash_bwd_launch<128>(a, st);
-  return flash_bwd_launch<64>(a, st);  // D <= 64: padded image
+  if (D > 64) return flash_bwd_launch<128>(a, st);  // 72..128: padded 128 image
+  return flash_bwd_launch<64>(a, st);               // 32..64: padded 64 image
 }
 
-// eligible: the flash forward's domain (bf16, head_dim 128 / 256 or 32..64 padded to 64, >= 128
+// eligible: the flash forward's domain (bf16, head_dim 256 or 32..128 padded to 64 / 128, >= 128
 // query rows)
 int s2h_flash_bwd_eligible(int dt, int Lq, int D);
 int s2h_flash_eligible(int dt, int Lq, int D);
@@ -799,12 +800,12 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
   int64_t lk_sum = 0;
   for (int f = 0; f < nfr; ++f) lk_sum += fr_lk[f];
   const int slot = s2h_prof_begin(st, 2, (int64_t)bpf * H, Lq, lk_sum, D, 3);
-  const int rc = D == 256 ? flash_bwd_launch<256>(a, st) : D == 128 ? flash_bwd_launch<128>(a, st)
-                                                                    : flash_bwd_launch<64>(a, st);
+  const int rc = D == 256 ? flash_bwd_launch<256>(a, st) : D > 64 ? flash_bwd_launch<128>(a, st)
+                                                                  : flash_bwd_launch<64>(a, st);
   s2h_prof_end(slot, st);
   return rc;
 }
 
-// the frame-batched backward's domain for the host (bf16, head_dim 128 / 256, >= 128 query
+// the frame-batched backward's domain for the host (bf16, head_dim 256 or 32..128, >= 128 query
 // rows, flash path not switched off by s2h_attn_config)
 extern "C" int s2h_flash_bwd_ok(int dt, int Lq, int D) { return s2h_flash_bwd_eligible(dt, Lq, D); }

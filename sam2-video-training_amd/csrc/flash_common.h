@@ -149,6 +149,8 @@ __device__ __forceinline__ WgIdx wg_xcd_order() {
   return WgIdx{x, (t % gy8) * 8 + xcd, t / gy8};
 }
 static inline unsigned pad_bh8(int bh) { return (unsigned)((bh + 7) / 8 * 8); }
+// LDS image width of a head dim: 32..64 -> 64, 72..128 -> 128 (zero-extended columns), 256
+static inline int flash_dp(int D) { return D <= 64 ? 64 : D <= 128 ? 128 : D; }
 
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {

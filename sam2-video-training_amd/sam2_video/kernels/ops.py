@@ -195,7 +195,7 @@ def attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale, p_drop=0.0, seed=0, idx0=0,
 
 
 def flash_bwd_eligible(q):
-    """the frame-batched flash backward's domain (bf16, head_dim 128 / 256, >= 128 query rows,
+    """the frame-batched flash backward's domain (bf16, head_dim 32..128 / 256, >= 128 query rows,
     flash path enabled): q [B, Lq, H, D]"""
     return bool(lib().s2h_flash_bwd_ok(dt(q), q.shape[1], q.shape[-1]))
 

@@ -7,6 +7,8 @@ properties):
   stream order) reproduces the eager step clip by clip, and the bf16 mode stays
   close to the fp32 mode of the same build on the same clip;
 * config 3 (B+, 384^2, 10 frames, 7 objects): the 10-frame bank and the graph path;
+* config 4 (Hiera-L, 1024^2, 8 frames; 13 objects): head dim 72 on the padded-128 flash path,
+  4096-token memory attention over a 7-frame bank (28k keys), the graph path;
 * gradient accumulation (accumulate_grad_batches) equals the summed micro-step gradients;
 * validation_step is deterministic (eval mode: dropout off).
 """
@@ -52,12 +54,13 @@ def _losses(module, clips, graph):
     return out, run
 
 
-@pytest.mark.parametrize("cfg", [("base_plus", 512, 8, 13), ("base_plus", 384, 10, 7)], ids=["config2", "config3"])
+@pytest.mark.parametrize("cfg", [("base_plus", 512, 8, 13), ("base_plus", 384, 10, 7), ("large", 1024, 8, 13)],
+                         ids=["config2", "config3", "config4"])
 def test_config_graph_replays_match_eager(cfg):
-    """lr = 0 (fixed weights), dropout 0.1 as trained: 12 replays (config 2) / 4 (config 3) of the
-    captured step on different clips give the eager step's loss on each clip"""
+    """lr = 0 (fixed weights), dropout 0.1 as trained: 12 replays (config 2) / 4 (config 3) / 2
+    (config 4) of the captured step on different clips give the eager step's loss on each clip"""
     size, S, T, O = cfg
-    n = 12 if S == 512 else 4
+    n = {512: 12, 384: 4, 1024: 2}[S]
     clips = _clips(range(50, 50 + n), T, S, O, O)
     eager, _ = _losses(_module(size, S), clips, graph=False)
     graphed, run = _losses(_module(size, S), clips, graph=True)
@@ -146,3 +149,25 @@ def test_split_backward_equals_single_backward(graph):
         res.append(arena.grad_region().detach().clone())
     a, b = res
     assert (a - b).abs().max().item() <= 1e-5 * a.abs().max().item()
+
+
+def test_lightning_checkpoint_resumes_on_device(tmp_path):
+    """after a trained step, Trainer.save_checkpoint -> load_lightning_checkpoint into a fresh
+    arena-backed model gives the trained weights (fp32 master copies and the bf16 shadow) and the
+    same validation outputs on a clip (reference train.py:146-157 reloads checkpoints this way)"""
+    from sam2_video.training.trainer import StepRunner, Trainer
+    clip = _clips([21], 3, 128, 4, 3)[0]
+    src = _module("tiny", 128, lr=1e-3)
+    StepRunner(src, total_steps=1, graph=False)(clip)
+    path = str(tmp_path / "last.ckpt")
+    Trainer(max_steps=1).save_checkpoint(path, src)
+    dst = _module("tiny", 128)
+    dst.model.load_lightning_checkpoint(path)
+    a, b = src.model.state_dict(), dst.model.state_dict()
+    assert all(torch.equal(a[k], b[k]) for k in a)
+    vals = []
+    for m in (src, dst):
+        m.validation_step(clip)
+        vals.append({k: float(v) for k, v in m.logged.items() if k.startswith("val/")})
+    for k in vals[0]:
+        assert abs(vals[0][k] - vals[1][k]) <= 1e-5 * max(1.0, abs(vals[0][k])), (k, vals)

@@ -202,7 +202,10 @@ def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
                                          (2, 4, 300, 77, 64), (1, 1, 1000, 1031, 256), (3, 1, 128, 40, 256),
                                          # Hiera head dim 56 (and 40) in the padded 64 image
                                          (2, 2, 196, 196, 56), (1, 8, 1024, 1024, 56), (3, 2, 130, 300, 40),
-                                         (2, 4, 256, 200, 64)])
+                                         (2, 4, 256, 200, 64),
+                                         # Hiera-L head dim 72 (and 96, 120) in the padded 128 image
+                                         (2, 2, 256, 256, 72), (1, 4, 4096, 4096, 72), (1, 2, 300, 700, 96),
+                                         (2, 1, 130, 200, 120)])
 def test_flash_forward_matches_reference(B, H, Lq, Lk, D):
     """bf16 long-sequence path (flash.hip, flash_bwd.hip): key-split partials + combine, ragged
     tails, head dims <= 64 padded to the 64 image."""
@@ -729,12 +732,14 @@ def test_bce_category_loss_matches_reference_formula(reduction, pw, temp):
     _close(x.grad, xr.grad, 1e-5)
 
 
-def test_flash_strided_qkv_head56_fwd_bwd():
-    """Hiera's fused [B, L, 3, H, 56] projection through the padded-64 flash path: q / k / v read
-    in place, gradients written in place into one dqkv buffer (the QKV attention layout)"""
+@pytest.mark.parametrize("d", [56, 72])
+def test_flash_strided_qkv_padded_head_fwd_bwd(d):
+    """Hiera's fused [B, L, 3, H, d] projection (B+ 56, L 72) through the padded 64 / 128 flash
+    path: q / k / v read in place, gradients written in place into one dqkv buffer (the QKV
+    attention layout)"""
     ops = _ops()
     torch.manual_seed(8)
-    B, L, H, d = 3, 196, 2, 56
+    B, L, H = 3, 196, 2
     qkv = (torch.randn(B, L, 3, H, d, device=DEV) * 0.7).to(torch.bfloat16)
     q, k, v = qkv.unbind(2)
     o = torch.empty(B, L, H, d, device=DEV, dtype=torch.bfloat16)

@@ -91,6 +91,35 @@ def test_lightning_checkpoint_prefix_strip(tmp_path):
     assert SAM2Model.strip_lightning_prefix({"a": 1}) == {"a": 1}
 
 
+def test_lightning_checkpoint_round_trip(tmp_path):
+    """Trainer.save_checkpoint writes the Lightning layout (`state_dict` with the `model.` prefix,
+    optimizer states, counters); load_lightning_checkpoint and the fintuned_model_path branch
+    (reference sam2model.py:109-126 with train.py:146-157's unwrapping) restore every tensor of a
+    differently initialised model exactly"""
+    from sam2_video.model.sam2model import SAM2Model
+    from sam2_video.training.trainer import Trainer
+    src = SAM2Model(None, "tiny@128", trainable_modules=["memory_attention"], init_seed=3)
+    opt_state = {"step": 7, "lr": 1e-4}
+    module = SimpleNamespace(model=src, optimizer=SimpleNamespace(state_dict=lambda: opt_state))
+    tr = Trainer(max_steps=1)
+    path = str(tmp_path / "last.ckpt")
+    tr.save_checkpoint(path, module)
+    ck = torch.load(path, map_location="cpu", weights_only=True)
+    assert all(k.startswith("model.") for k in ck["state_dict"]) and ck["optimizer_states"] == [opt_state]
+    want = src.state_dict()
+    dst = SAM2Model(None, "tiny@128", trainable_modules=["memory_attention"], init_seed=11)
+    assert any(not torch.equal(want[k], v) for k, v in dst.state_dict().items())
+    dst.load_lightning_checkpoint(path)
+    assert all(torch.equal(want[k], v) for k, v in dst.state_dict().items())
+    ft = SAM2Model(None, "tiny@128", fintuned_model_path=path, trainable_modules=["memory_attention"], init_seed=11)
+    assert all(torch.equal(want[k], v) for k, v in ft.state_dict().items())
+    # a checkpoint missing a tensor is refused under strict loading
+    del ck["state_dict"]["model.no_mem_embed"]
+    torch.save(ck, path)
+    with pytest.raises(RuntimeError):
+        SAM2Model(None, "tiny@128", init_seed=11).load_lightning_checkpoint(path)
+
+
 def test_synthetic_clip_dataset_and_parts():
     from sam2_video.data.synthetic import SyntheticClipDataset, make_clip
     from sam2_video.utils.masks import cat_to_obj_mask
