@@ -16,6 +16,12 @@ def _ops():
     return ops
 
 
+def _cpu_conv(fn, x, w, b, **kw):
+    """fp32 torch convolution evaluated on the host (the references never go through MIOpen's
+    GPU solvers: its conv-transpose solver faulted on a fresh box), returned on x's device."""
+    return fn(x.float().cpu(), w.float().cpu(), None if b is None else b.float().cpu(), **kw).to(x.device)
+
+
 def _close(a, b, tol):
     a = a.float()
     b = b.float()
@@ -408,12 +414,12 @@ def test_im2col_conv_matches_torch():
     b = torch.randn(8, device=DEV)
     col, Ho, Wo = ops.im2col(x, 7, 7, 4, 3)
     y = ops.linear(col, w.reshape(8, -1), b).view(2, Ho, Wo, 8)
-    ref = torch.nn.functional.conv2d(x.permute(0, 3, 1, 2), w, b, stride=4, padding=3).permute(0, 2, 3, 1)
+    ref = _cpu_conv(torch.nn.functional.conv2d, x.permute(0, 3, 1, 2), w, b, stride=4, padding=3).permute(0, 2, 3, 1)
     _close(y, ref, 2e-5)
     wd = torch.randn(6, 1, 7, 7, device=DEV)
     xd = torch.randn(2, 9, 9, 6, device=DEV)
     yd = ops.dwconv(xd, wd, b[:6], 3)
-    ref = torch.nn.functional.conv2d(xd.permute(0, 3, 1, 2), wd, b[:6], padding=3, groups=6).permute(0, 2, 3, 1)
+    ref = _cpu_conv(torch.nn.functional.conv2d, xd.permute(0, 3, 1, 2), wd, b[:6], padding=3, groups=6).permute(0, 2, 3, 1)
     _close(yd, ref, 2e-5)
 
 
@@ -426,7 +432,7 @@ def test_dwconv_vectorised(dtype, tol, B, H, W, C):
     w = torch.randn(C, 1, 7, 7, device=DEV)
     b = torch.randn(C, device=DEV)
     y = ops.dwconv(x, w, b, 3)
-    ref = torch.nn.functional.conv2d(x.float().permute(0, 3, 1, 2), w, b, padding=3, groups=C).permute(0, 2, 3, 1)
+    ref = _cpu_conv(torch.nn.functional.conv2d, x.float().permute(0, 3, 1, 2), w, b, padding=3, groups=C).permute(0, 2, 3, 1)
     _close(y, ref, tol)
 
 
@@ -440,7 +446,7 @@ def test_convt2():
     x2 = x.reshape(-1, Ci)
     ops.gemm(x2, w, Y, M=B * H * W, N=Co * 4, K=Ci, lda_m=Ci, lda_k=1, ldb_k=Co * 4, ldb_n=1, ldc=Co * 4)
     out = ops.convt2_scatter(Y, B, H, W, Co, bias=b)
-    ref = torch.nn.functional.conv_transpose2d(x.permute(0, 3, 1, 2), w, b, stride=2).permute(0, 2, 3, 1)
+    ref = _cpu_conv(torch.nn.functional.conv_transpose2d, x.permute(0, 3, 1, 2), w, b, stride=2).permute(0, 2, 3, 1)
     _close(out, ref, 2e-5)
     dY = ops.convt2_gather(out, B, H, W, Co)
     Y2 = torch.empty_like(Y)
@@ -576,7 +582,7 @@ def test_mask_down_stage(dtype, tol, cin, cout, H):
     be = torch.randn(cout, device=DEV) * 0.1
 
     def ref(xin):
-        y = torch.nn.functional.conv2d(xin.permute(0, 3, 1, 2), w, b, stride=2, padding=1)
+        y = _cpu_conv(torch.nn.functional.conv2d, xin.permute(0, 3, 1, 2), w, b, stride=2, padding=1)
         y = torch.nn.functional.layer_norm(y.permute(0, 2, 3, 1), (cout,), g, be, 1e-6)
         return torch.nn.functional.gelu(y)
 
