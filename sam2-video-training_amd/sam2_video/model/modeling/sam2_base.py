@@ -190,8 +190,12 @@ class SAM2Base(nn.Module):
                 mems.append((t_pos, prev))
         max_ptr = min(num_frames, self.max_obj_ptrs_in_encoder)
         sign = -1 if track_in_reverse else 1
+        # eval: only conditioning frames on the tracked side of this frame contribute pointers
+        # (only_obj_ptrs_in_the_past_for_eval, sam2_base.py:618-625)
+        ptr_cond = [t for t in cond_keys if self.training or not self.only_obj_ptrs_in_the_past_for_eval
+                    or (t >= frame_idx if track_in_reverse else t <= frame_idx)]
         ptrs = [((frame_idx - t) * sign if self.use_signed_tpos_enc_to_obj_ptrs else abs(frame_idx - t), t)
-                for t in cond_keys]
+                for t in ptr_cond]
         for t_diff in range(1, max_ptr):
             t = frame_idx + t_diff if track_in_reverse else frame_idx - t_diff
             if t < 0 or (num_frames is not None and t >= num_frames):
@@ -231,6 +235,8 @@ class SAM2Base(nn.Module):
         pos_list = [p for p, _ in ptr_sel]
         ptrs = [bank(t)["obj_ptr"] for _, t in ptr_sel]
         n_ptr_tok = len(ptrs) * (C // self.mem_dim)
+        if not ptrs:  # eval, tracking away from every conditioning frame (sam2_base.py:677)
+            raise NotImplementedError("memory attention without object-pointer tokens")
         ptr_tokens = torch.stack(ptrs, dim=1).reshape(num_objects, n_ptr_tok, self.mem_dim)
         if tape is not None:
             if self.obj_ptr_tpos_proj.weight.requires_grad:
@@ -250,9 +256,11 @@ class SAM2Base(nn.Module):
         return self.memory_attention(feat, pos, memory, mpos, num_obj_ptr_tokens=n_ptr_tok, num_objects=num_objects)
 
     # ------------------------------------------------------------ heads
-    def _forward_sam_heads(self, pix, prompt, high_res, num_objects):
+    def _forward_sam_heads(self, pix, prompt, high_res, num_objects, dense=None):
         """sam2_base.py:262-434 (single mask).  pix [O, L, C]; prompt (pe [O, N, C] f32, labels [O, N]
-        int32) on the device; high_res (s0, s1) NHWC (batch 1 = broadcast over objects)."""
+        int32) on the device; high_res (s0, s1) NHWC (batch 1 = broadcast over objects); `dense` an
+        optional mask-prompt embedding [O, L, C] (prompt_encoder._embed_masks, the predictor's
+        refinement clicks) in place of no_mask_embed."""
         O = num_objects
         h = w = self.sam_image_embedding_size
         dt = pix.dtype
@@ -260,7 +268,8 @@ class SAM2Base(nn.Module):
         sparse = self.sam_prompt_encoder.sparse(pe_dev, lab_dev, dt)
         dense_pe = self.sam_prompt_encoder.dense_pe_table(pix.device, dt)
         masks, ious, token0, score = self.sam_mask_decoder(pix, h, w, dense_pe, sparse,
-                                                           self.sam_prompt_encoder.no_mask_embed, high_res)
+                                                           self.sam_prompt_encoder.no_mask_embed, high_res,
+                                                           **({"dense": dense} if dense is not None else {}))
         score_flat = score.view(-1).contiguous()
         low = FN.cast(masks, torch.float32)
         low = FN.row_gate(low, score_flat, NO_OBJ_SCORE)
