@@ -97,6 +97,35 @@ int s2h_gemm_config(int cfg);
 int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t lddy, const void* x,
                      int64_t ldx, float* dw, int64_t lddw, float* db, int accumulate, hipStream_t stream);
 
+/* ---------------------------------------------------------------- MX-fp8 (BASELINE config 5)
+ * No reference counterpart: the reference trains in fp32 / bf16 autocast only
+ * (trainer.py:256-289 under Lightning `precision`); this is the fp8 variant of the projection
+ * and FFN GEMMs the north_star asks for (`s2h_gemm` replaces nn.Linear in hieradet.py:56-91,
+ * memory_attention.py:58-99, transformer.py:137-311).  OCP MX v1.0 MXFP8-E4M3: 32-element
+ * blocks along the reduction dimension, one E8M0 scale each.
+ *
+ * s2h_mx8_quant: element (r, c) of X (bf16 / fp32) at X[r*ld_row + c*ld_col], r < rows, c < cols,
+ * blocks along c.  Q [rows][ldq] u8 e4m3 (ldq >= cols rounded up to 128, ldq % 16 == 0, Q 16-B
+ * aligned; columns cols..ldq-1 of the first round-up written as zeros); S [ceil(cols/128)][lds]
+ * int32 scale words (lds >= rows): byte b of word (kt, r) = E8M0 scale of block 4kt+b of row r.
+ * ld_row == 1 selects the row-walking lane order (a transposed source). */
+int s2h_mx8_quant(int rows, int cols, int dt_x, const void* X, int64_t ld_row, int64_t ld_col, uint8_t* Q,
+                  int64_t ldq, int32_t* S, int64_t lds, hipStream_t stream);
+
+/* C[M, N] = epilogue(alpha * A B^T) for MX-fp8 A [M, K] (Q lda, scales SA, row stride lsa >= M)
+ * and B [N, K] (ldb, SB, lsb >= N) as s2h_mx8_quant writes them; K is the logical depth (both
+ * operands zero-padded to a multiple of 128).  Epilogue as s2h_gemm with bias per column:
+ * act (aux_mode 1 stores the pre-activation to X, 2 multiplies by act'(X)), dropout, residual R,
+ * beta.  C bf16 (dt_c 1) or fp32 (0). */
+int s2h_gemm_mx8(int M, int N, int K, const uint8_t* A, int64_t lda, const int32_t* SA, int64_t lsa,
+                 const uint8_t* B, int64_t ldb, const int32_t* SB, int64_t lsb, void* C, int dt_c, int64_t ldc,
+                 const float* bias, const void* R, int64_t ldr, void* X, int64_t ldx, int aux_mode, float drop_p,
+                 uint64_t seed, uint64_t drop_idx0, float alpha, float beta, int act, hipStream_t stream);
+
+/* MX-fp8 GEMM tiling override for measurements: 0 automatic, 1 64x64, 2 128x64, 3 128x128;
+ * returns the previous value. */
+int s2h_mx8_config(int cfg);
+
 /* ---------------------------------------------------------------- attention
  * Fused multi-head attention, tensors [B, L, H, D] addressed through
  * (batch, head, row) strides with contiguous D; lse [B, H, Lq] fp32 (natural log).

@@ -11,9 +11,7 @@
 // transposed reads).  K is split over workgroups (fp32 atomic accumulate into
 // the output) when the output tile count cannot fill the 256 CUs -- the weight
 // gradients reduce over 10^4-10^5 rows into a few hundred KB.
-#include <type_traits>
-
-#include "gemm16.h"
+#include "gemm_epi.h"
 
 typedef short v4i16 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
@@ -81,245 +79,6 @@ struct Stage16 {
     return tr_frag(lds + ks * LDS_LD + row0, LDS_LD, lane);
   }
 };
-
-// Finishes outputs (row, col0..col0+3) of batch bz from the fp32 accumulators v4.
-// Every epilogue option is tested ONCE per 4-column group (uniform scalar branches around
-// 4-wide straight-line code), never per element: per-element option tests made the epilogue
-// SALU-bound (~1.7k SALU + 1.2k VALU instructions per wave for 32 MFMAs at K = 64).
-// `bcol` holds the lane's 4 column biases (loaded once per tile by the caller).
-__device__ __forceinline__ uint2 ld4_bf16(const bf16* ptr, bool full) {
-  if (full) return *(const uint2*)ptr;
-  return make_uint2(0, 0);
-}
-__device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4, const float* bcol) {
-  float v[4] = {v4.x, v4.y, v4.z, v4.w};
-  const int nval = p.N - col0;
-  if (nval <= 0) return;
-  const bool full = nval >= 4 && p.vecC;
-  if (p.splits > 1) {  // split-K: fp32 atomic accumulate (beta handled on the host side)
-    float* C = (float*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
-#pragma unroll
-    for (int e = 0; e < 4; ++e)
-      if (e < nval) atomicAdd(C + e, p.alpha * v[e]);
-    return;
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) v[e] = p.alpha * v[e] + bcol[e];
-  if (p.bias_mode == 2) {
-    const float br = p.bias[row];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] += br;
-  }
-  if (p.aux_mode == 1) {  // store the pre-activation
-    bf16* X = (bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0;
-    if (full && p.ldx % 4 == 0) {
-      bf16 t[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) t[e] = (bf16)v[e];
-      *(uint2*)X = *(const uint2*)t;
-    } else {
-      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) X[e] = (bf16)v[e];
-    }
-  }
-  if (p.aux_mode == 2) {  // multiply by act'(pre-activation)
-    const bf16* X = (const bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0;
-    float xs[4];
-    if (full && p.ldx % 4 == 0) {
-      const uint2 r = *(const uint2*)X;
-      const bf16* rb = (const bf16*)&r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xs[e] = (float)rb[e];
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) xs[e] = e < nval ? (float)X[e] : 0.f;
-    }
-    if (p.act == S2H_ACT_RELU) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = xs[e] > 0.f ? v[e] : 0.f;
-    } else if (p.act != S2H_ACT_NONE) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] *= act_grad(xs[e], p.act);
-    }
-  } else if (p.act == S2H_ACT_RELU) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-  } else if (p.act != S2H_ACT_NONE) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
-  }
-  if (p.cscale) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] *= e < nval ? p.cscale[col0 + e] : 0.f;
-  }
-  if (p.drop_p > 0.f) {
-    const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
-    const float inv_keep = 1.f / (1.f - p.drop_p);
-    const uint64_t idx0 = p.drop_idx0 + (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
-    bool k[4];
-    if ((idx0 & 1) == 0) {
-      s2h_keep_pair(p.seed, idx0 >> 1, thresh, k[0], k[1]);
-      s2h_keep_pair(p.seed, (idx0 >> 1) + 1, thresh, k[2], k[3]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) k[e] = s2h_keep(p.seed, idx0 + e, thresh);
-    }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
-  }
-  if (p.R) {
-    const bf16* R = (const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0;
-    if (full && p.ldr % 4 == 0) {
-      const uint2 r = *(const uint2*)R;
-      const bf16* rb = (const bf16*)&r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += (float)rb[e];
-    } else {
-      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) v[e] += (float)R[e];
-    }
-  }
-  const int64_t co = (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
-  if (p.out_f32) {
-    float* C = (float*)p.C + co;
-    if (full) {
-      float4 o = {v[0], v[1], v[2], v[3]};
-      if (p.beta != 0.f) {
-        const float4 c = *(const float4*)C;
-        o.x += p.beta * c.x; o.y += p.beta * c.y; o.z += p.beta * c.z; o.w += p.beta * c.w;
-      }
-      *(float4*)C = o;
-    } else {
-      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) C[e] = v[e] + (p.beta != 0.f ? p.beta * C[e] : 0.f);
-    }
-  } else {
-    bf16* C = (bf16*)p.C + co;
-    if (full) {
-      bf16 o[4];
-      if (p.beta != 0.f) {
-        const uint2 c = *(const uint2*)C;
-        const bf16* cb = (const bf16*)&c;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16)(v[e] + p.beta * (float)cb[e]);
-      } else {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (bf16)v[e];
-      }
-      *(uint2*)C = *(const uint2*)o;
-    } else {
-      _Pragma("unroll") for (int e = 0; e < 4; ++e) if (e < nval) C[e] = (bf16)(v[e] + (p.beta != 0.f ? p.beta * (float)C[e] : 0.f));
-    }
-  }
-}
-
-// 8 consecutive bf16 outputs (row, col0..col0+7) with one 16-B access per operand -- the
-// store-issue-bound tail of a GEMM costs per instruction, not per byte (the 4-column form
-// issues twice the stores).  Requires (checked by the caller) 8 valid columns, no split-K, a
-// bf16 output and vec8 bit 0; X / R fall back to two 8-B accesses when their bit is clear.
-__device__ __forceinline__ void ld8_bf16(const bf16* ptr, bool wide, float* out) {
-  if (wide) {
-    const uint4 r = *(const uint4*)ptr;
-    const bf16* rb = (const bf16*)&r;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) out[e] = (float)rb[e];
-  } else {
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const uint2 r = *(const uint2*)(ptr + 4 * h);
-      const bf16* rb = (const bf16*)&r;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) out[4 * h + e] = (float)rb[e];
-    }
-  }
-}
-__device__ __forceinline__ void st8_bf16(bf16* ptr, bool wide, const float* v) {
-  bf16 t[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) t[e] = (bf16)v[e];
-  if (wide) {
-    *(uint4*)ptr = *(const uint4*)t;
-  } else {
-    *(uint2*)ptr = *(const uint2*)t;
-    *(uint2*)(ptr + 4) = *(const uint2*)(t + 4);
-  }
-}
-__device__ __forceinline__ void epilogue8(const GemmArgs16& p, int bz, int row, int col0, const float* vin,
-                                          const float* bcol) {
-  float v[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = p.alpha * vin[e] + bcol[e];
-  if (p.bias_mode == 2) {
-    const float br = p.bias[row];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += br;
-  }
-  const bool wx = (p.vec8 & 2) != 0, wr = (p.vec8 & 4) != 0;
-  if (p.aux_mode == 1) st8_bf16((bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0, wx, v);
-  if (p.aux_mode == 2) {
-    float xs[8];
-    ld8_bf16((const bf16*)p.X + (int64_t)bz * p.sX + (int64_t)row * p.ldx + col0, wx, xs);
-    if (p.act == S2H_ACT_RELU) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = xs[e] > 0.f ? v[e] : 0.f;
-    } else if (p.act != S2H_ACT_NONE) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] *= act_grad(xs[e], p.act);
-    }
-  } else if (p.act == S2H_ACT_RELU) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
-  } else if (p.act != S2H_ACT_NONE) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act);
-  }
-  if (p.cscale) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] *= p.cscale[col0 + e];
-  }
-  if (p.drop_p > 0.f) {
-    const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
-    const float inv_keep = 1.f / (1.f - p.drop_p);
-    const uint64_t idx0 = p.drop_idx0 + (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
-    bool k[8];
-    if ((idx0 & 1) == 0) {
-#pragma unroll
-      for (int h = 0; h < 4; ++h) s2h_keep_pair(p.seed, (idx0 >> 1) + h, thresh, k[2 * h], k[2 * h + 1]);
-    } else {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) k[e] = s2h_keep(p.seed, idx0 + e, thresh);
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
-  }
-  if (p.R) {
-    float rs[8];
-    ld8_bf16((const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0, wr, rs);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += rs[e];
-  }
-  bf16* C = (bf16*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
-  if (p.beta != 0.f) {
-    float cs[8];
-    ld8_bf16(C, true, cs);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] += p.beta * cs[e];
-  }
-  st8_bf16(C, true, v);
-}
-
-// compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
-template <int B, int E, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) {
-    f(std::integral_constant<int, B>{});
-    static_for<B + 1, E>(f);
-  }
-}
-
-// the lane's 4 column biases (zeros when the bias is absent or per row)
-template <int V = 4>
-__device__ __forceinline__ void load_bcol(const GemmArgs16& p, int col0, float* bcol) {
-#pragma unroll
-  for (int e = 0; e < V; ++e) bcol[e] = (p.splits == 1 && p.bias_mode == 1 && col0 + e < p.N) ? p.bias[col0 + e] : 0.f;
-}
 
 template <int BM, int BN, bool AKC, bool BKC>
 __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
@@ -520,69 +279,6 @@ struct GemmShape {
   static constexpr int MINB = NS * STAGE_BYTES <= 80 * 1024 ? 2 : 1;  // workgroups per CU the LDS allows
 };
 
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// Epilogue of one wave's WM x WN accumulator block through a wave-private LDS slab `ep`
-// (16 x (WN + 4) fp32): per 16-row slab, stage the accumulators, then every lane finishes 4
-// consecutive columns of a row (epilogue4) with 8-/16-byte stores -- rows of a
-// wave-instruction are 128-B column runs.  The slab is private to the wave, so no workgroup
-// barrier: LDS operations of one wave retire in order.  (A register-direct variant with
-// swapped MFMA operands -- 4 consecutive columns per lane, no staging -- measured 1.5-2.6x
-// slower: its stores scatter 16 rows x 32 B per instruction, and split-K atomics likewise.)
-template <int WM, int WN, int MI, int NI>
-__device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[MI][NI], float* ep, int bz, int mw,
-                                              int nw, int lane) {
-  constexpr int EPLD = WN + 4;
-  float bcol[4], bcol8[8];
-  load_bcol(p, nw + 4 * (lane % (WN / 4)), bcol);
-  load_bcol<8>(p, nw + 8 * (lane % (WN / 8 > 0 ? WN / 8 : 1)), bcol8);
-  // compile-time slab index (a rolled loop would index acc dynamically -> scratch)
-  static_for<0, MI>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
-    __builtin_amdgcn_wave_barrier();
-    if (p.splits > 1) {
-      // split-K: one row per instruction, consecutive lanes on consecutive columns (256 B)
-      float* C = (float*)p.C + (int64_t)bz * p.sC;
-      constexpr int RPI = 64 / WN;  // rows per instruction
-      const int col = nw + lane % WN;
-      for (int rr = lane / WN; rr < 16; rr += RPI) {
-        const int row = mw + i * 16 + rr;
-        if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
-      }
-    } else if (WN % 32 == 0 && (p.vec8 & 1) && nw + WN <= p.N) {
-      // 8 columns per lane, one 16-B store each (the wave's column block is entirely valid)
-      constexpr int CPR = WN / 8, RPP = 64 / CPR;
-      const int c8 = lane % CPR, rg = lane / CPR;
-      for (int ps = 0; ps < 16 / RPP; ++ps) {
-        const int rl = rg + ps * RPP;
-        const float4 lo = *(const float4*)&ep[rl * EPLD + 8 * c8];
-        const float4 hi = *(const float4*)&ep[rl * EPLD + 8 * c8 + 4];
-        const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        const int row = mw + i * 16 + rl;
-        if (row < p.M && !(p.dbg & 1)) epilogue8(p, bz, row, nw + 8 * c8, v8, bcol8);
-      }
-    } else {
-      constexpr int CPR = WN / 4, RPP = 64 / CPR;
-      const int c4 = lane % CPR, rg = lane / CPR;
-      for (int ps = 0; ps < 16 / RPP; ++ps) {
-        const int rl = rg + ps * RPP;
-        const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
-        const int row = mw + i * 16 + rl;
-        if (row < p.M && !(p.dbg & 1)) epilogue4(p, bz, row, nw + 4 * c4, v4, bcol);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  });
-}
-
 template <int BM, int BN, int WGM, int WGN, int NS, int BK, bool AKC, bool BKC>
 __global__ __launch_bounds__((GemmShape<BM, BN, WGM, WGN, NS, BK>::NT), (GemmShape<BM, BN, WGM, WGN, NS, BK>::MINB))
 void gemm16g_kernel(GemmArgs16 p) {
@@ -709,14 +405,7 @@ static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st
       }
     }
   }
-  // 4-column output groups: 16-B (f32) / 8-B (bf16) aligned
-  a.vecC = ((uintptr_t)a.C % (a.out_f32 ? 16 : 8) == 0) && a.ldc % 4 == 0 && (batch == 1 || a.sC % 4 == 0);
-  // 8-column groups with one 16-B access per operand (bf16: base 16-B aligned, strides % 8)
-  auto ok8 = [&](const void* ptr, int64_t ld, int64_t sb) {
-    return ptr && (uintptr_t)ptr % 16 == 0 && ld % 8 == 0 && (batch == 1 || sb % 8 == 0);
-  };
-  a.vec8 = (!a.out_f32 && ok8(a.C, a.ldc, a.sC) ? 1 : 0) | (ok8(a.X, a.ldx, a.sX) ? 2 : 0) |
-           (ok8(a.R, a.ldr, a.sR) ? 4 : 0);
+  gemm_plan_vec(a, batch);
 }
 
 template <int BM, int BN, int WGM, int WGN, int NS, int BK = 64>

@@ -126,6 +126,91 @@ def linear_wgrad(dy, x, dw, accumulate=True, db=None):
     return dw
 
 
+# ----------------------------------------------------------------- MX-fp8 (config 5)
+class MX8:
+    """An MX-fp8 (OCP MXFP8-E4M3) operand as s2h_mx8_quant writes it: `q` [rows, Kp] uint8 e4m3
+    codes (Kp = k rounded up to 128, zero padded), `s` [Kp / 128, rows] int32 scale words (byte b
+    of word (kt, r) = E8M0 exponent of the 32-block 4kt + b of row r), `k` the logical depth."""
+    __slots__ = ("q", "s", "k")
+
+    def __init__(self, q, s, k):
+        self.q, self.s, self.k = q, s, k
+
+    @property
+    def rows(self):
+        return self.q.shape[0]
+
+
+def mx8_empty(rows, k, device):
+    kp = (k + 127) // 128 * 128
+    return MX8(torch.empty(rows, kp, dtype=torch.uint8, device=device),
+               torch.empty(kp // 128, rows, dtype=torch.int32, device=device), k)
+
+
+def mx8_quant(x, out=None, transpose=False):
+    """MX-fp8 of the rows of 2-D `x` [rows, cols] (blocks along cols, cols contiguous), or with
+    transpose=True of x^T ([cols, rows] -> blocks along x's rows: the dgrad operand of a weight)."""
+    _dev(x)
+    assert x.dim() == 2
+    if transpose:
+        assert x.stride(0) == 1 or x.is_contiguous()
+        rows, cols = x.shape[1], x.shape[0]
+        ld_row, ld_col = x.stride(1), x.stride(0)
+    else:
+        assert x.stride(1) == 1
+        rows, cols = x.shape
+        ld_row, ld_col = x.stride(0), 1
+    if out is None:
+        out = mx8_empty(rows, cols, x.device)
+    assert out.q.shape[0] == rows and out.k == cols and out.s.shape[1] >= rows
+    call("s2h_mx8_quant", rows, cols, dt(x), ptr(x), ld_row, ld_col, ptr(out.q), out.q.stride(0), ptr(out.s),
+         out.s.stride(0), stream())
+    return out
+
+
+def gemm_mx8(a: MX8, b: MX8, c, *, bias=None, residual=None, aux=None, aux_mode=0, act=0, drop_p=0.0, seed=0,
+             drop_idx0=0, alpha=1.0, beta=0.0):
+    """c[M, N] = epilogue(alpha * A B^T) for MX-fp8 A [M, K] and B [N, K] (s2h_gemm_mx8)"""
+    assert a.k == b.k and c.dim() == 2 and c.stride(1) == 1
+    M, N = a.rows, b.rows
+    assert c.shape == (M, N)
+    _dev(a.q, b.q, c, bias, residual, aux)
+    call("s2h_gemm_mx8", M, N, a.k, ptr(a.q), a.q.stride(0), ptr(a.s), a.s.stride(0), ptr(b.q), b.q.stride(0),
+         ptr(b.s), b.s.stride(0), ptr(c), dt(c), c.stride(0), ptr(bias), ptr(residual),
+         residual.stride(0) if residual is not None else 0, ptr(aux), aux.stride(0) if aux is not None else 0,
+         aux_mode if aux is not None else 0, float(drop_p), int(seed) & (2**64 - 1), int(drop_idx0), float(alpha),
+         float(beta), int(act), stream())
+    return c
+
+
+def linear_mx8(x, w8: MX8, bias=None, act=None, out=None, pre=None, residual=None, drop_p=0.0, seed=0, drop_idx0=0):
+    """ops.linear with MX-fp8 operands: x (bf16) quantised here, w8 = the weight's MX-fp8 copy."""
+    x2 = x.reshape(-1, x.shape[-1])
+    N = w8.rows
+    assert x2.shape[1] == w8.k
+    if out is None:
+        out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+    xq = mx8_quant(x2 if x2.stride(1) == 1 else x2.contiguous())
+    gemm_mx8(xq, w8, out.view(-1, N), bias=bias, residual=residual.reshape(-1, N) if residual is not None else None,
+             aux=pre.view(-1, N) if pre is not None else None, aux_mode=1 if pre is not None else 0, act=ACT[act],
+             drop_p=drop_p, seed=seed, drop_idx0=drop_idx0)
+    return out
+
+
+def linear_dgrad_mx8(dy, wt8: MX8, dx=None, accumulate=False, pre=None, act=None, alpha=1.0):
+    """ops.linear_dgrad with MX-fp8 operands: dy quantised along its N, wt8 = MX-fp8 of W^T [K, N]."""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    K = wt8.rows
+    assert dy2.shape[1] == wt8.k
+    if dx is None:
+        dx = torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=dy.dtype)
+    dq = mx8_quant(dy2 if dy2.stride(1) == 1 else dy2.contiguous())
+    gemm_mx8(dq, wt8, dx.view(-1, K), aux=pre.reshape(-1, K) if pre is not None else None,
+             aux_mode=2 if pre is not None else 0, act=ACT[act] if pre is not None else 0, alpha=alpha,
+             beta=1.0 if accumulate else 0.0)
+    return dx
+
+
 def bmm(a, b, out, *, trans_b=False, alpha=1.0, beta=0.0):
     """Batched out[i] = a[i] @ b[i] (or b[i]^T): a [Bt, M, K], b [Bt, K, N] / [Bt, N, K]."""
     Bt, M, K = a.shape
