@@ -26,6 +26,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 PEAK_BF16_TFLOPS = 2500.0  # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip-level parameters)
+PEAK_FP8_TFLOPS = 5000.0  # dense block-scaled fp8 MFMA (same table; the MX-fp8 GEMM family is priced on it)
 # algorithmic fwd+bwd TFLOP per clip-frame: config 2 all-trainable
 # 13.75 TF / 8 frames, `mem` 11.14 TF / 8 frames
 STEP_TF_PER_FRAME = {("base_plus", 512, 8, 13, "all"): 13.75 / 8, ("base_plus", 512, 8, 13, "mem"): 11.14 / 8}
@@ -41,7 +42,10 @@ def parse():
     ap.add_argument("--image-size", type=int, default=512)
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--objects", type=int, default=13)
-    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--dtype", default="bf16", help="bf16 | fp32 | fp8 (MX-fp8 projections / FFN, kernels/fp8.py)")
+    ap.add_argument("--config", type=int, default=2, choices=[2, 5],
+                    help="BASELINE config preset: 2 = B+ 512^2 8 frames bf16 (the headline), "
+                         "5 = B+ 512^2 16 frames MX-fp8 (long-memory stress)")
     ap.add_argument("--trainable", default="all", choices=["all", "mem"])
     ap.add_argument("--dropout", type=float, default=None, help="override dropout p (default: config, 0.1)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="time the CPU oracle on rank 0 at N=1")
@@ -53,7 +57,10 @@ def parse():
                     help="launch every kernel from Python each step instead of replaying the captured HIP graph")
     ap.add_argument("--kernel-table", action="store_true",
                     help="after timing, profile one extra step and print per-shape GEMM/attention TF/s to stderr")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.config == 5:
+        args.frames, args.dtype = 16, "fp8"
+    return args
 
 
 # algorithmic flops per profiler record (SURVEY.md §8(d) counting: attention backward = 2 x forward,
@@ -66,7 +73,8 @@ def record_flops(kind, m):
     return (4.0 if kind == 1 else 8.0) * bh * lq * lk * d
 
 
-FAMILY = {1: "attention forward (flash_fwd / attn_fwd kernels)",
+FAMILY = {40: "MX-fp8 GEMM (gemm_mx8: forward and dgrad of the projections / FFN, config 5)",
+          1: "attention forward (flash_fwd / attn_fwd kernels)",
           2: "attention backward (flash_bwd di/dq/dkv kernels, frame-batched; attn_bwd kernels)",
           4: "GEMM (gemm16g / gemm kernels: projections, FFN, convs, dgrad, wgrad)"}
 
@@ -77,24 +85,26 @@ def family_roofline(recs, nsteps=1):
     kernel time) as the roofline line"""
     fam = {}
     for ms, m in recs:
-        f = fam.setdefault(m[0], {"ms": 0.0, "flops": 0.0, "launches": 0})
+        k = 40 if m[0] == 4 and (m[5] & 8) else m[0]  # layout flag 8: MX-fp8 operands
+        f = fam.setdefault(k, {"ms": 0.0, "flops": 0.0, "launches": 0})
         f["ms"] += ms
         f["flops"] += record_flops(m[0], m)
         f["launches"] += 1
     if not fam:
         return None
     table = {}
+    peak = lambda kk: PEAK_FP8_TFLOPS if kk == 40 else PEAK_BF16_TFLOPS  # noqa: E731
     for k, f in fam.items():
         ach = f["flops"] / (f["ms"] * 1e-3) / 1e12 if f["ms"] > 0 else 0.0
         table[FAMILY[k].split(" (")[0]] = {"ms_per_step": round(f["ms"] / nsteps, 3),
                                           "tflop_per_step": round(f["flops"] / nsteps / 1e12, 4),
-                                          "achieved": round(ach, 1), "frac": round(ach / PEAK_BF16_TFLOPS, 4),
+                                          "achieved": round(ach, 1), "frac": round(ach / peak(k), 4),
                                           "launches_per_step": f["launches"] // nsteps}
     k = max(fam, key=lambda kk: fam[kk]["ms"])
     f = fam[k]
     ach = f["flops"] / (f["ms"] * 1e-3) / 1e12
-    return {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_BF16_TFLOPS, "unit": "TFLOP/s",
-            "frac": round(ach / PEAK_BF16_TFLOPS, 4), "traffic": None, "kernel": FAMILY[k],
+    return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak(k), "unit": "TFLOP/s",
+            "frac": round(ach / peak(k), 4), "traffic": None, "kernel": FAMILY[k],
             "launches": f["launches"], "avg_launch_ms": round(f["ms"] / f["launches"], 4),
             "flops_per_launch_avg": f["flops"] / f["launches"], "families": table, "_kind": k}
 
@@ -104,7 +114,7 @@ def pmc_traffic(kind):
     FETCH_SIZE / WRITE_SIZE passes (profiles/*_<family>_pmc.json, tools/pmc_family.py; counters
     cannot be collected inside this timed run)"""
     import glob
-    tag = {1: "attn_fwd", 2: "attn_bwd", 4: "gemm"}[kind]
+    tag = {1: "attn_fwd", 2: "attn_bwd", 4: "gemm", 40: "gemm_mx8"}[kind]
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{tag}_pmc.json")))
     if not files:
         return None, None
@@ -129,7 +139,8 @@ def kernel_table(recs):
         kind = m[0]
         if kind == 4:
             b, M, N, K, lay = m[1:]
-            key = ("gemm", f"b{b} {M}x{N}x{K} {'AB'[0] if lay & 2 else 'a'}{'B' if lay & 1 else 'b'}")
+            key = ("gemm_mx8" if lay & 8 else "gemm",
+                   f"b{b} {M}x{N}x{K} {'AB'[0] if lay & 2 else 'a'}{'B' if lay & 1 else 'b'}")
             fl = 2.0 * b * M * N * K
         else:
             bh, lq, lk, d, _ = m[1:]
@@ -315,7 +326,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": args.dtype,
+        "dtype": args.dtype if args.dtype != "fp8" else "fp8 (MX e4m3 fwd + dgrad of projections / FFN) + bf16",
         "data": "synthetic (N(0,1) images, drifting disc masks; deterministic synthetic weights, no checkpoint)",
         "config": {"workload": f"SAM2 video fine-tuning step, sam2.1_hiera_{args.size}, {args.image_size}^2, "
                                f"{args.frames} frames, {args.objects} objects, trainable={args.trainable}",

@@ -123,6 +123,7 @@ int s2h_gemm_mx8(int M, int N, int K, const uint8_t* A, int64_t lda, const int32
                  uint64_t seed, uint64_t drop_idx0, float alpha, float beta, int act, hipStream_t stream);
 
 /* MX-fp8 GEMM tiling override for measurements: 0 automatic, 1 64x64, 2 128x64, 3 128x128;
+ * bits 8+ measurement-only ablations (1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA);
  * returns the previous value. */
 int s2h_mx8_config(int cfg);
 

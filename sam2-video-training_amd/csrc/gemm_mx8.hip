@@ -185,9 +185,12 @@ __global__ __launch_bounds__(256, (2 * 128 * (BM + BN) <= 80 * 1024 ? 2 : 1)) vo
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  const bool dma_on = !(p.e.dbg & 4);
   if (nk > 0) {
-    IA::dma(smem, p.A, lda, m0, 0, M, w, lane);
-    IB::dma(smem + IA::BYTES, p.B, ldb, n0, 0, N, w, lane);
+    if (dma_on) {
+      IA::dma(smem, p.A, lda, m0, 0, M, w, lane);
+      IB::dma(smem + IA::BYTES, p.B, ldb, n0, 0, N, w, lane);
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i) sa_n[i] = p.SA[arow[i]];
 #pragma unroll
@@ -206,13 +209,16 @@ __global__ __launch_bounds__(256, (2 * 128 * (BM + BN) <= 80 * 1024 ? 2 : 1)) vo
     for (int j = 0; j < NI; ++j) scb[j] = (sb_n[j] >> sh) & 0xff;
     if (kt + 1 < nk) {  // next stage into the buffer step kt-1 read; runs under this step's MFMAs
       char* na = smem + ((kt + 1) & 1) * STAGE;
-      IA::dma(na, p.A, lda, m0, (kt + 1) * 128, M, w, lane);
-      IB::dma(na + IA::BYTES, p.B, ldb, n0, (kt + 1) * 128, N, w, lane);
+      if (dma_on) {
+        IA::dma(na, p.A, lda, m0, (kt + 1) * 128, M, w, lane);
+        IB::dma(na + IA::BYTES, p.B, ldb, n0, (kt + 1) * 128, N, w, lane);
+      }
 #pragma unroll
       for (int i = 0; i < MI; ++i) sa_n[i] = p.SA[(int64_t)(kt + 1) * p.lsa + arow[i]];
 #pragma unroll
       for (int j = 0; j < NI; ++j) sb_n[j] = p.SB[(int64_t)(kt + 1) * p.lsb + brow[j]];
     }
+    if (p.e.dbg & 2) continue;
     v8i32 a[MI], b[NI];
 #pragma unroll
     for (int i = 0; i < MI; ++i) a[i] = IA::frag(sa, wm * WM + i * 16, lane);
@@ -231,9 +237,11 @@ __global__ __launch_bounds__(256, (2 * 128 * (BM + BN) <= 80 * 1024 ? 2 : 1)) vo
 }
 
 static int g_mx8_cfg = 0;  // 0 automatic, 1: 64x64, 2: 128x64, 3: 128x128
+static int g_mx8_dbg = 0;  // measurement-only ablations (bits 8+): as GemmArgs16::dbg
 extern "C" int s2h_mx8_config(int cfg) {
-  const int prev = g_mx8_cfg;
-  g_mx8_cfg = cfg;
+  const int prev = g_mx8_cfg | (g_mx8_dbg << 8);
+  g_mx8_cfg = cfg & 0xff;
+  g_mx8_dbg = cfg >> 8;
   return prev;
 }
 
@@ -267,7 +275,7 @@ extern "C" int s2h_gemm_mx8(int M, int N, int K, const uint8_t* A, int64_t lda, 
   e.splits = 1; e.kchunk = K;
   e.out_f32 = dt_c == S2H_F32;
   e.rowsum = nullptr;
-  e.dbg = 0;
+  e.dbg = g_mx8_dbg;
   gemm_plan_vec(e, 1);
   a.A = A; a.lda = lda; a.SA = SA; a.lsa = lsa;
   a.B = B; a.ldb = ldb; a.SB = SB; a.lsb = lsb;
@@ -275,9 +283,11 @@ extern "C" int s2h_gemm_mx8(int M, int N, int K, const uint8_t* A, int64_t lda, 
   const int slot = s2h_prof_begin(st, 4, 1, M, N, K, 8 + 2 + 1);  // layout flag 8: MX-fp8 operands
   int cfg = g_mx8_cfg;
   if (!cfg) {
+    // graph-replay timings of the config-5 shapes (tools/mx8_bench.py): 128x64 wins everywhere
+    // but on long K (16384x448x1792: 128x128 23.5 us vs 28.5) and on small grids (64x64)
     const long t128 = (long)((M + 127) / 128) * ((N + 127) / 128);
     const long t128x64 = (long)((M + 127) / 128) * ((N + 63) / 64);
-    cfg = t128 >= 512 ? 3 : (t128x64 >= 512 ? 2 : 1);
+    cfg = (K >= 1024 && t128 >= 256) ? 3 : (t128x64 >= 256 ? 2 : 1);
   }
   if (cfg == 3) launch_mx8<128, 128>(a, st);
   else if (cfg == 2) launch_mx8<128, 64>(a, st);

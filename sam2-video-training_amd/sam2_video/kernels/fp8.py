@@ -1,0 +1,116 @@
+"""MX-fp8 compute mode (BASELINE config 5: `compute_dtype="fp8"`, Lightning precision "fp8").
+
+Recipe: the projection and FFN Linear layers of the image encoder trunk and the memory attention
+run their forward GEMM and their input-gradient
+(dgrad) GEMM on MX-fp8 operands (OCP MXFP8-E4M3, 32-element blocks along the reduction
+dimension, csrc/gemm_mx8.hip): Y = Q(X) Q(W)^T, dX = Q(dY) Q(W^T)^T.  The weight gradients stay
+bf16 (dW = dY^T X over 10^4-10^5 token rows from the saved bf16 activations, fp32 accumulate),
+as do activations between kernels, attention, norms, losses, the fp32 master weights and AdamW.
+
+Weight operands are quantised from the bf16 shadow once per forward (`new_step`, called at the
+top of SAM2Model.forward, so a captured step graph re-quantises on every replay after AdamW
+moved the weights): the forward operand Q(W) [N, Kp] on first forward use, the dgrad operand
+Q(W^T) [K, Np] on first backward use.  Activation and gradient operands are quantised right
+before each GEMM (one bf16 read, one fp8 write).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+_STATE = {"gen": 0}
+
+# module name prefixes whose Linear layers take the MX-fp8 path.  The mask decoder's two-way
+# transformer stays bf16: a negligible share of the flops (<= 8 tokens x 4096 keys per object)
+# and the most quantisation-sensitive layers of the step (tools/fp8_drift.py at B+ 256^2 against
+# the fp32 mode: two-way in fp8 -> mask IoU 0.95-0.97, memory attention -> 0.988-0.995,
+# trunk -> 0.954-0.963; bf16 everywhere -> 0.992-0.995)
+FP8_PREFIXES = ("image_encoder.trunk.", "memory_attention.")
+MIN_IN_FEATURES = 128  # narrower inputs would be mostly padding in a 128-deep MX step
+# input-gradient GEMMs on MX-fp8 too (False: forward only, dgrad in bf16)
+DGRAD = {"on": True}
+
+
+def new_step():
+    _STATE["gen"] += 1
+
+
+def mark_modules(model):
+    """flag the fp8-eligible Linear layers of `model` (SAM2Model.load with compute_dtype fp8)"""
+    from ..model.modeling.layers import Linear
+    n = 0
+    for name, m in model.named_modules():
+        if type(m) is Linear and name.startswith(FP8_PREFIXES) and m.in_features >= MIN_IN_FEATURES \
+                and m.out_features >= 64:
+            m._s2h_fp8 = True
+            n += 1
+    return n
+
+
+def _eligible(mod):
+    f = getattr(mod, "_s2h_fp8", None)
+    if f is None:
+        members = getattr(mod, "members", None)  # FusedLinear: all members flagged
+        f = bool(members) and all(getattr(m, "_s2h_fp8", False) for m in members)
+    return f
+
+
+class _Entry:
+    __slots__ = ("fwd", "t", "gen_f", "gen_t")
+
+    def __init__(self):
+        self.fwd = self.t = None
+        self.gen_f = self.gen_t = -1
+
+
+def _entry(mod):
+    e = getattr(mod, "_s2h_fp8_entry", None)
+    if e is None:
+        e = _Entry()
+        mod._s2h_fp8_entry = e
+    return e
+
+
+def weight(mod):
+    """MX-fp8 forward operand Q(W) [N, Kp] of `mod` for this step, or None (bf16 path)"""
+    if not _eligible(mod):
+        return None
+    e = _entry(mod)
+    if e.gen_f != _STATE["gen"]:
+        w = mod.compute_weight()
+        if e.fwd is None:
+            e.fwd = ops.mx8_empty(w.shape[0], w.shape[1], w.device)
+        ops.mx8_quant(w, out=e.fwd)
+        e.gen_f = _STATE["gen"]
+    return e.fwd
+
+
+def weight_t(mod):
+    """MX-fp8 dgrad operand Q(W^T) [K, Np] of `mod` for this step, or None"""
+    if not _eligible(mod):
+        return None
+    e = _entry(mod)
+    if e.gen_t != _STATE["gen"]:
+        w = mod.compute_weight()
+        if e.t is None:
+            e.t = ops.mx8_empty(w.shape[1], w.shape[0], w.device)
+        ops.mx8_quant(w, out=e.t, transpose=True)
+        e.gen_t = _STATE["gen"]
+    return e.t
+
+
+def linear(x, mod, w, bias, **kw):
+    """forward GEMM of a Linear: MX-fp8 when `mod` is eligible, else the bf16 kernel"""
+    w8 = weight(mod) if x.dtype != torch.float32 else None
+    if w8 is not None:
+        return ops.linear_mx8(x, w8, bias, **kw)
+    return ops.linear(x, w, bias, **kw)
+
+
+def linear_dgrad(dy, mod, **kw):
+    """input-gradient GEMM of a Linear: MX-fp8 when `mod` is eligible, else the bf16 kernel"""
+    wt8 = weight_t(mod) if dy.dtype != torch.float32 and DGRAD["on"] else None
+    if wt8 is not None:
+        return ops.linear_dgrad_mx8(dy, wt8, **kw)
+    return ops.linear_dgrad(dy, mod.compute_weight(), **kw)

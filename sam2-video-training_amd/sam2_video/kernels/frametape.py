@@ -31,6 +31,7 @@ from typing import Dict, List, Optional
 
 import torch
 
+from . import fp8 as _fp8
 from . import ops
 
 _ACTIVE: List[Optional["FrameTape"]] = [None]
@@ -396,7 +397,7 @@ def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0):
     pre = tape._aux("pre", shape, x.dtype, scale) if act and not relu_out else None
     seed = tape._seed() if drop_p > 0 else 0
     idx0 = tape._idx0(op, out.numel())
-    ops.linear(x, w, b, act=act, out=out, pre=pre, residual=residual, drop_p=drop_p, seed=seed, drop_idx0=idx0)
+    _fp8.linear(x, mod, w, b, act=act, out=out, pre=pre, residual=residual, drop_p=drop_p, seed=seed, drop_idx0=idx0)
     if first:
         op.attrs["seed"] = seed
         op.attrs["K"] = x.shape[-1]
@@ -434,10 +435,10 @@ def _linear_bw(tape, op, gys):
                 and op.ins[0] not in tape.seeded:
             # sole consumer of a ReLU (-> dropout) linear: its mask and 1/keep fused into this dgrad
             pp = prod.attrs["p"]
-            dx = ops.linear_dgrad(dpre, mod.compute_weight(), pre=x2, act="relu", alpha=1.0 / (1.0 - pp)).view(-1)
+            dx = _fp8.linear_dgrad(dpre, mod, pre=x2, act="relu", alpha=1.0 / (1.0 - pp)).view(-1)
             tape.premasked.add(op.ins[0])
         else:
-            dx = ops.linear_dgrad(dpre, mod.compute_weight()).view(-1)
+            dx = _fp8.linear_dgrad(dpre, mod).view(-1)
     dres = gy if op.needs[1] else None
     return [dx, dres]
 

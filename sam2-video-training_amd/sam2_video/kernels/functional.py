@@ -16,6 +16,7 @@ import math
 
 import torch
 
+from . import fp8 as _fp8
 from . import frametape as _ft
 from . import ops
 
@@ -50,7 +51,7 @@ class _Linear(torch.autograd.Function):
         relu_out = act == "relu" and residual is None
         pre = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype) if act and not relu_out else None
         seed = next_seed() if drop_p > 0 else 0
-        out = ops.linear(x, w, b, act=act, pre=pre, residual=residual, drop_p=drop_p, seed=seed)
+        out = _fp8.linear(x, mod, w, b, act=act, pre=pre, residual=residual, drop_p=drop_p, seed=seed)
         ctx.mod, ctx.act, ctx.drop_p, ctx.seed, ctx.relu_out = mod, act, drop_p, seed, relu_out
         ctx.has_res = residual is not None
         ctx.save_for_backward(x, out if relu_out else pre)
@@ -72,7 +73,7 @@ class _Linear(torch.autograd.Function):
             ops.linear_wgrad(dpre, x, gw.view(gw.shape[0], -1), db=gb)
         elif gb is not None:
             ops.colsum(dpre, gb)
-        dx = ops.linear_dgrad(dpre, mod.compute_weight()) if ctx.needs_input_grad[0] else None
+        dx = _fp8.linear_dgrad(dpre, mod) if ctx.needs_input_grad[0] else None
         return dx, None, None, None, None, (dy if ctx.has_res else None), None
 
 
@@ -93,8 +94,8 @@ class _MLP2(torch.autograd.Function):
     def forward(ctx, x, w1p, b1p, w2p, b2p, fc1, fc2, act, residual):
         w1, w2 = fc1.compute_weight(), fc2.compute_weight()
         pre = torch.empty(*x.shape[:-1], w1.shape[0], device=x.device, dtype=x.dtype)
-        hid = ops.linear(x, w1, fc1.compute_bias(), act=act, pre=pre)
-        out = ops.linear(hid, w2, fc2.compute_bias(), residual=residual)
+        hid = _fp8.linear(x, fc1, w1, fc1.compute_bias(), act=act, pre=pre)
+        out = _fp8.linear(hid, fc2, w2, fc2.compute_bias(), residual=residual)
         ctx.fc1, ctx.fc2, ctx.act, ctx.has_res = fc1, fc2, act, residual is not None
         ctx.save_for_backward(x, pre, hid)
         return out
@@ -109,13 +110,13 @@ class _MLP2(torch.autograd.Function):
             ops.linear_wgrad(dy, hid, gw2.view(gw2.shape[0], -1), db=gb2)
         elif gb2 is not None:
             ops.colsum(dy, gb2)
-        dpre = ops.linear_dgrad(dy, fc2.compute_weight(), pre=pre, act=ctx.act)
+        dpre = _fp8.linear_dgrad(dy, fc2, pre=pre, act=ctx.act)
         gw1, gb1 = fc1.grad_views()
         if gw1 is not None:
             ops.linear_wgrad(dpre, x, gw1.view(gw1.shape[0], -1), db=gb1)
         elif gb1 is not None:
             ops.colsum(dpre, gb1)
-        dx = ops.linear_dgrad(dpre, fc1.compute_weight()) if ctx.needs_input_grad[0] else None
+        dx = _fp8.linear_dgrad(dpre, fc1) if ctx.needs_input_grad[0] else None
         return dx, None, None, None, None, None, None, None, (dy if ctx.has_res else None)
 
 

@@ -23,6 +23,7 @@ from torch import nn
 
 from .. import utils
 from ..data.data_utils import BatchedVideoDatapoint
+from ..kernels import fp8
 from ..kernels.arena import ParamArena
 from ..utils.init import synth_tensor
 from ..utils.masks import merge_object_results_to_category
@@ -30,7 +31,9 @@ from .build import instantiate, load_model_config
 from .modeling.sam2_base import SAM2Base
 
 DTYPES = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": torch.float32, "float32": torch.float32,
-          torch.bfloat16: torch.bfloat16, torch.float32: torch.float32}
+          torch.bfloat16: torch.bfloat16, torch.float32: torch.float32,
+          # MX-fp8 projections / FFN (kernels/fp8.py) over bf16 activations and shadow weights
+          "fp8": torch.bfloat16, "mxfp8": torch.bfloat16}
 
 
 class SAM2Model(SAM2Base):
@@ -56,6 +59,7 @@ class SAM2Model(SAM2Base):
             raise NotImplementedError("mask prompts through the SAM heads (use_mask_input_as_output_without_sam "
                                       "False) are not built; the SAM2.1 configs set it True")
         self.compute_dtype = DTYPES[compute_dtype]
+        self.fp8 = compute_dtype in ("fp8", "mxfp8")
         # training steps run the tracking loop's backward frame-batched (model/tracking.py);
         # False = per-frame autograd (the reference's graph shape; A/B and tests)
         self.frame_batched = os.environ.get("S2H_FRAME_BATCHED", "1") != "0"
@@ -184,6 +188,8 @@ class SAM2Model(SAM2Base):
         for m in self.modules():
             if hasattr(m, "bind_arena"):
                 m.bind_arena(self.arena)
+        if self.fp8:
+            fp8.mark_modules(self)
         return self
 
     def set_dropout(self, p: float):
@@ -208,6 +214,8 @@ class SAM2Model(SAM2Base):
         """sam2model.py:153-179"""
         if self.arena is None:
             raise RuntimeError("call SAM2Model.load(device) before forward")
+        if self.fp8:
+            fp8.new_step()  # weights moved since the last forward: re-quantise on first use
         backbone_out = self.forward_image(input.flat_img_batch)
         # the backbone outputs the tracking loop reads: the split point of a two-phase backward
         # (StepRunner overlaps the gradient all-reduce of everything after them with the image

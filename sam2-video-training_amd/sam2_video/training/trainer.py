@@ -75,8 +75,11 @@ def _todict(x):
 def precision_dtype(precision) -> str:
     """Lightning `precision` -> compute dtype of the kernels.  "16"/"16-mixed" (fp16 AMP in the
     reference configs, best.yaml:103) and "bf16*" run bf16 (same width; fp16 is not a CDNA4
-    training format here), "32*"/"64*" run the fp32 mode."""
+    training format here), "32*"/"64*" run the fp32 mode, "fp8" / "transformer-engine" the MX-fp8
+    mode."""
     p = str(precision if precision is not None else "bf16").lower()
+    if p.startswith("fp8") or p.startswith("mxfp8") or p == "transformer-engine":
+        return "fp8"  # MX-fp8 projections / FFN (BASELINE config 5, kernels/fp8.py)
     return "fp32" if p.startswith("32") or p.startswith("64") else "bf16"
 
 
