@@ -436,7 +436,8 @@ static int launch16_regs(GemmArgs16& a, int batch, hipStream_t st) {
 // LDS-DMA tilings (s2h_gemm_config selects one for A/B measurements; 0 = automatic)
 enum GemmCfg {
   CFG_AUTO = 0, CFG_64 = 1, CFG_128 = 2, CFG_128_NS3 = 3, CFG_256x128 = 4, CFG_256 = 5, CFG_128x256 = 6,
-  CFG_128x64 = 7, CFG_64x128 = 8, CFG_64_NS3 = 9, CFG_64_K32_NS4 = 10
+  CFG_128x64 = 7, CFG_64x128 = 8, CFG_64_NS3 = 9, CFG_64_K32_NS4 = 10, CFG_128x64_K32_NS3 = 11,
+  CFG_128x64_K32_NS4 = 12, CFG_128x64_NS3 = 13
 };
 static int g_gemm_cfg = CFG_AUTO;
 static int g_gemm_dbg = 0;
@@ -462,6 +463,10 @@ static int pick_cfg(const GemmArgs16& a, int batch) {
   if (a.M >= 1024 && a.N >= 1024 && a.K >= 1024 && t256 >= 128) return CFG_256;
   const long t128x64 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64) * batch;
   const bool split = a.out_f32 && a.K >= 1024 && t128x64 < 512;  // plan_splits' split-K regime
+  // shallow K (<= 256) on large grids: 32-deep stages, 3-deep ring (tools/epi_bench.py graph
+  // replays: 131072x448x112 70 -> 58 us, 32768x672x224 35 -> 28, 93184x2048x256 222 -> 216;
+  // below ~2k tiles or at K >= 448 the 64-deep 2-stage form stays ahead)
+  if (!split && a.K <= 256 && t128x64 >= 2048) return CFG_128x64_K32_NS3;
   if (split ? t128x64 >= 64 : t128x64 >= 1024) return CFG_128x64;
   return CFG_64;
 }
@@ -485,6 +490,9 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
     case CFG_64x128: return launch_glds<64, 128, 2, 2, 2>(a, batch, st);
     case CFG_64_NS3: return launch_glds<64, 64, 2, 2, 3>(a, batch, st);
     case CFG_64_K32_NS4: return launch_glds<64, 64, 2, 2, 4, 32>(a, batch, st);
+    case CFG_128x64_K32_NS3: return launch_glds<128, 64, 2, 2, 3, 32>(a, batch, st);
+    case CFG_128x64_K32_NS4: return launch_glds<128, 64, 2, 2, 4, 32>(a, batch, st);
+    case CFG_128x64_NS3: return launch_glds<128, 64, 2, 2, 3>(a, batch, st);
     default: return launch_glds<128, 128, 2, 2, 2>(a, batch, st);
   }
 }
