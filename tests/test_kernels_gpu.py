@@ -763,3 +763,43 @@ def test_flash_strided_qkv_padded_head_fwd_bwd(d):
     _close(dq, qr.grad, 4e-2)
     _close(dk, kr.grad, 4e-2)
     _close(dv, vr.grad, 4e-2)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_elementwise_vector_forms_match_scalar(dtype):
+    """16-B vector kernels (add, broadcast add, act fwd / bwd, dropout, act + dropout backward)
+    give bit-identical results to the scalar kernels (selected by 2-byte-misaligned views) and
+    match torch on the plain ops; odd dropout index offsets take the per-element hash path"""
+    ops = _ops()
+    torch.manual_seed(11)
+    R, C = 999, 264
+    n = R * C
+
+    def pair():  # the same values aligned (vector path) and misaligned (scalar path)
+        buf = torch.randn(n + 1, device=DEV).to(dtype)
+        al = torch.empty(n, device=DEV, dtype=dtype)
+        al.copy_(buf[1:])
+        return al, buf[1:]
+
+    (a, a_), (b, b_) = pair(), pair()
+    assert a.data_ptr() % 16 == 0 and a_.data_ptr() % 16 != 0
+    out_ = torch.empty(n + 1, device=DEV, dtype=dtype)[1:]
+    for alpha, beta in ((1.0, 1.0), (0.5, -2.0)):
+        v = ops.add(a, b, alpha=alpha, beta=beta)
+        s = ops.add(a_, b_, out=out_, alpha=alpha, beta=beta)
+        assert torch.equal(v, s)
+        _close(v, (alpha * a.float() + beta * b.float()).to(dtype), 1e-2 if dtype == torch.bfloat16 else 1e-6)
+    tab, tab_ = pair()
+    for period in (1, 7):
+        v = ops.add_bcast(a.view(R, C), tab[: period * C], b_period=period, alpha=0.7, beta=1.3)
+        s = ops.add_bcast(a_.view(R, C), tab_[: period * C], out=out_.view(R, C), b_period=period, alpha=0.7, beta=1.3)
+        assert torch.equal(v.reshape(-1), s.reshape(-1)), period
+        ref = 0.7 * a.float().view(R, C) + 1.3 * tab[: period * C].float().view(period, C).repeat(R // period + 1, 1)[:R]
+        _close(v.view(R, C), ref.to(dtype), 2e-2 if dtype == torch.bfloat16 else 1e-5)
+    for act in ("relu", "gelu"):
+        assert torch.equal(ops.act_fwd(a, act), ops.act_fwd(a_, act, out=out_))
+        assert torch.equal(ops.act_bwd(a, b, act), ops.act_bwd(a_, b_, act, dx=out_))
+    for idx0 in (0, 3):
+        assert torch.equal(ops.dropout(b, 0.1, 77, idx0=idx0), ops.dropout(b_, 0.1, 77, out=out_, idx0=idx0))
+        assert torch.equal(ops.act_dropout_bwd(a, b, "gelu", 0.1, 77, idx0=idx0),
+                           ops.act_dropout_bwd(a_, b_, "gelu", 0.1, 77, dx=out_, idx0=idx0))
