@@ -443,20 +443,23 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
 // (128) + S, dP registers beyond 256 per wave, so this form runs one wave per SIMD with
 // the 512-register file: 4 waves x 32 keys on v_mfma_f32_32x32x16_bf16 (also half the LDS
 // operand traffic per FLOP), dK^T / dV^T in 2 x 128 accumulator registers.
-template <int DP, int DROP>
+// KREG: K fragments held in registers like V (64 more VGPRs, no K block in LDS): the S / dP
+// phase re-read the constant K block from LDS every 32-query tile -- a third of that phase's
+// LDS traffic, and the phase is LDS-bandwidth-bound (4 waves x 48 b128 reads against 32 MFMAs).
+template <int DP, int DROP, bool KREG = true>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a) {
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   constexpr int NWV = 4, QT = 32;
   using C = FlashCfg<DP, QT, NWV>;
   constexpr int NT = DP / 16, ND = DP / 32;
-  // [K block: 128 keys][stage][Q | dO] + [stage][wave][lse(32) | Di(32)] (each wave DMAs its
-  // own copy of the row constants).  K lives in LDS (read as the B operand of S = Q K^T),
-  // V in registers: both in registers would leave too few for the rest at 512 per lane.
+  // [K block: 128 keys (!KREG)][stage][Q | dO] + [stage][wave][lse(32) | Di(32)] (each wave DMAs
+  // its own copy of the row constants).  V (and with KREG, K) live in registers.
   using CK = FlashCfg<DP, NWV * 32, NWV>;
   constexpr int STAGE = 2 * C::TILEB + NWV * 512;  // + per wave [lse | Di | keep words (x2)]
-  __shared__ __attribute__((aligned(1024))) char smem[CK::TILEB + 2 * STAGE];
+  constexpr int KBLK = KREG ? 0 : CK::TILEB;
+  __shared__ __attribute__((aligned(1024))) char smem[KBLK + 2 * STAGE];
   char* Kblk = smem;
-  char* stages = smem + CK::TILEB;
+  char* stages = smem + KBLK;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, kl = lane & 31;
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
@@ -490,7 +493,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   auto dma_bits = [&](char* stage, int q0) {
     lds_dma4(KEEPW + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * fr.kw, stage + 2 * C::TILEB + w * 512 + 256);
   };
-  dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, wi.x * (NWV * 32), fr.Lk, w, lane);
+  if constexpr (!KREG) dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, wi.x * (NWV * 32), fr.Lk, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
@@ -499,7 +502,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
   for (int t = 0; t < NT; ++t) vf[t] = *(const bf16x8*)(V + vkey * a.svl + 16 * t + 8 * hi);
-  __builtin_amdgcn_s_waitcnt(0xF70);  // retire the V loads in the compiler's bookkeeping (see dq)
+  bf16x8 kf[KREG ? NT : 1];  // B operand K^T of S = Q K^T: [k = d = 16t + 8hi + j][n = key]
+  if constexpr (KREG) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t) kf[t] = *(const bf16x8*)(K + vkey * a.skl + 16 * t + 8 * hi);
+  }
+  __builtin_amdgcn_s_waitcnt(0xF70);  // retire the V (K) loads in the compiler's bookkeeping (see dq)
   const int krow = w * 32 + kl;  // this lane's key row in the K block
   f32x16 dk[ND], dv[ND];  // dK^T / dV^T: row d = 32*db + 8(r>>2) + 4hi + (r&3), column key
 #pragma unroll
@@ -533,8 +541,12 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
       const bf16x8 qa = *(const bf16x8*)(Qb + swz<DP, 1>(kl, 2 * t + hi));
-      const bf16x8 kb = *(const bf16x8*)(Kblk + swz<DP, 1>(krow, 2 * t + hi));
-      s = mfma32(qa, kb, s);
+      if constexpr (KREG) {
+        s = mfma32(qa, kf[t], s);
+      } else {
+        const bf16x8 kb = *(const bf16x8*)(Kblk + swz<DP, 1>(krow, 2 * t + hi));
+        s = mfma32(qa, kb, s);
+      }
       const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP, 1>(kl, 2 * t + hi));
       dp = mfma32(ga, vf[t], dp);
       if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the fragment prefetch depth

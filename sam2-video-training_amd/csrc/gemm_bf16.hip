@@ -393,7 +393,9 @@ static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st
     int s = (768 + tiles - 1) / tiles;
     int maxs = a.K / 512;
     if (s > maxs) s = maxs;
-    if (s > 64) s = 64;
+    // up to 256 splits: the memory K / V projection weight gradients (256 x 64 over 374k rows)
+    // have 2-4 output tiles, which 64 splits left at half a wave of workgroups
+    if (s > 256) s = 256;
     if (s > 1) {
       a.splits = s;
       a.kchunk = ((a.K + s - 1) / s + 63) / 64 * 64;

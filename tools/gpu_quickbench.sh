@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_mx8_gpu.py tests/test_parity_gpu.py -x -q -rf --timeout 150 --timeout-method thread > gpurun_out/qb_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests/test_kernels_gpu.py tests/test_mx8_gpu.py tests/test_parity_gpu.py tests/test_frametape_gpu.py -x -q -rf --timeout 150 --timeout-method thread > gpurun_out/qb_tests.log 2>&1
 rc=$?
 tail -3 gpurun_out/qb_tests.log
 [ $rc -eq 0 ] || { tail -40 gpurun_out/qb_tests.log; exit $rc; }
