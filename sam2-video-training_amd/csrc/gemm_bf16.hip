@@ -468,7 +468,10 @@ static int pick_cfg(const GemmArgs16& a, int batch) {
   // shallow K (<= 256) on large grids: 32-deep stages, 3-deep ring (tools/epi_bench.py graph
   // replays: 131072x448x112 70 -> 58 us, 32768x672x224 35 -> 28, 93184x2048x256 222 -> 216;
   // below ~2k tiles or at K >= 448 the 64-deep 2-stage form stays ahead)
-  if (!split && a.K <= 256 && t128x64 >= 2048) return CFG_128x64_K32_NS3;
+  // (tools/dgrad_bench.py: the same holds for narrow outputs up to K = 1024 -- dgrad 32768x224
+  // over K = 672: 29.2 -> 24.4 us, 131072x112 over K = 448: 43.9 -> 40.3)
+  if (!split && t128x64 >= 1024 && (a.K <= 256 ? t128x64 >= 2048 : (a.N <= 256 && a.K <= 1024)))
+    return CFG_128x64_K32_NS3;
   if (split ? t128x64 >= 64 : t128x64 >= 1024) return CFG_128x64;
   return CFG_64;
 }

@@ -34,7 +34,7 @@ def main():
                 "supervise_all_iou": True, "iou_use_l1_loss": True}
     module = SAM2LightningModule(model, loss_cfg, {"type": "AdamW", "lr": 4e-6}, {"enabled": False})
     module.setup("fit", "cuda")
-    runner = StepRunner(module, 10)
+    runner = StepRunner(module, 10, graph=False)  # eager: the profiler sees each launch and its call site
     batch = sam2_collate_fn([make_clip(0, a.frames, a.image_size, a.objects, a.objects)]).to("cuda")
     for _ in range(2):
         runner(batch)
