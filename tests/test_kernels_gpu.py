@@ -803,3 +803,4 @@ def test_elementwise_vector_forms_match_scalar(dtype):
         assert torch.equal(ops.dropout(b, 0.1, 77, idx0=idx0), ops.dropout(b_, 0.1, 77, out=out_, idx0=idx0))
         assert torch.equal(ops.act_dropout_bwd(a, b, "gelu", 0.1, 77, idx0=idx0),
                            ops.act_dropout_bwd(a_, b_, "gelu", 0.1, 77, dx=out_, idx0=idx0))
+

@@ -25,9 +25,8 @@ def main():
         b = torch.zeros(N, device="cuda")
         out = torch.empty(M, N, device="cuda", dtype=bf)
         row = f"{M}x{N}x{K:<6} MB out {M * N * 2 / 1e6:6.1f} |"
-        for cfg, cn in ((0, "auto"), (1, "64"), (9, "64ns3"), (10, "64k32ns4"), (7, "128x64"), (11, "128x64k32ns3"),
-                        (12, "128x64k32ns4"), (13, "128x64ns3")):
-            for dbg, nm in ((0, "nt"), (1, "nostore")):
+        for cfg, cn in ((0, "auto"), (1, "64"), (7, "128x64"), (11, "128x64k32ns3")):
+            for dbg, nm in ((0, "nt"),):
                 _lib.lib().s2h_gemm_config(cfg | (dbg << 8))
                 t = graph_time(lambda: ops.linear(x, w, b, out=out))
                 row += f" {cn}/{nm} {t:5.1f}"
@@ -35,7 +34,7 @@ def main():
         _lib.lib().s2h_gemm_config(0)
         if K >= 128:
             x8, w8 = ops.mx8_quant(x), ops.mx8_quant(w)
-            for dbg, nm in ((0, "nt"), (1, "nostore")):
+            for dbg, nm in ((0, "nt"),):
                 _lib.lib().s2h_mx8_config(dbg << 8)
                 t = graph_time(lambda: ops.gemm_mx8(x8, w8, out, bias=b))
                 row += f" mx8/{nm} {t:5.1f}"
