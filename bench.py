@@ -115,7 +115,12 @@ def pmc_traffic(kind):
     cannot be collected inside this timed run)"""
     import glob
     tag = {1: "attn_fwd", 2: "attn_bwd", 4: "gemm", 40: "gemm_mx8"}[kind]
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{tag}_pmc.json")))
+    import re
+
+    def order(f):  # r<round>_v<version>: numeric, so r02_v16 is newer than r02_v6
+        m = re.search(r"r(\d+)_v(\d+)_", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{tag}_pmc.json")), key=order)
     if not files:
         return None, None
     d = json.load(open(files[-1]))

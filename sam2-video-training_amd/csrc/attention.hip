@@ -113,6 +113,30 @@ __device__ __forceinline__ typename Mfma<T>::frag frag_global(const T* base, int
   return MF::zero();
 }
 
+// bf16 B-operand fragment (k = k0 .. k0+31, n = n0 .. n0+15) read from a NATURAL [k][n] LDS
+// image with transposing LDS reads (ds_read_b64_tr_b16, two per fragment): replaces the
+// transposed tile copies (lds_load_rows_t: eight 2-byte LDS stores per 16-B vector) of V in the
+// forward, K in dQ and Q / dO in dK / dV.  ld (elements) and n0 keep every read 8-B aligned.
+typedef short attn_v4i16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8 tr_bfrag(const bf16* img, int ld, int k0, int n0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  const bf16* a0 = img + (k0 + 8 * g + q) * ld + n0 + 4 * p;
+  const bf16* a1 = a0 + 4 * ld;
+  typedef __attribute__((address_space(3))) attn_v4i16 lds_v4;
+  const attn_v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a0);
+  const attn_v4i16 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a1);
+  typedef short v8i16 __attribute__((ext_vector_type(8)));
+  const v8i16 c = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8, c);
+}
+template <typename T> __device__ __forceinline__ typename Mfma<T>::frag tr_or_load(const T* nat, int ldn, const T* tr, int ldt,
+                                                                                    int k0, int n0, int lane) {
+  // B operand B[k][n] for k = k0 + 8(lane >> 4) + j, n = n0 + (lane & 15): bf16 from the natural
+  // image, fp32 from the transposed copy (one element per lane)
+  if constexpr (sizeof(T) == 2) return tr_bfrag(nat, ldn, k0, n0, lane);
+  else return Mfma<T>::load(&tr[(n0 + (lane & 15)) * ldt + k0 + (lane >> 4) * Mfma<T>::KPL]);
+}
+
 // ------------------------------------------------------------------ forward
 template <typename T, int DP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
@@ -122,10 +146,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int KS = DP + VEC, VS = BKEY + VEC, PS = BKEY + VEC;
   constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16;
-  __shared__ __attribute__((aligned(16))) T smem[BKEY * KS + DP * VS + 4 * 16 * PS];
+  constexpr bool TRR = sizeof(T) == 2;  // bf16: V natural, read transposed
+  constexpr int VBUF = TRR ? BKEY * KS : DP * VS;
+  __shared__ __attribute__((aligned(16))) T smem[BKEY * KS + VBUF + 4 * 16 * PS];
   T* Ks = smem;
-  T* Vt = Ks + BKEY * KS;
-  T* Ps = Vt + DP * VS;
+  T* Vt = Ks + BKEY * KS;  // [key][d] (bf16) or [d][key] (fp32)
+  T* Ps = Vt + VBUF;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
@@ -156,7 +182,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     const int k0 = kt * BKEY;
     __syncthreads();
     lds_load_rows<T, BKEY, DP, KS, 256>(Ks, K, a.skl, k0, a.Lk, a.D, tid);
-    lds_load_rows_t<T, BKEY, DP, VS, 256>(Vt, V, a.svl, k0, a.Lk, a.D, tid);
+    if constexpr (TRR) lds_load_rows<T, BKEY, DP, KS, 256>(Vt, V, a.svl, k0, a.Lk, a.D, tid);
+    else lds_load_rows_t<T, BKEY, DP, VS, 256>(Vt, V, a.svl, k0, a.Lk, a.D, tid);
     __syncthreads();
 
     f32x4 s[NB];
@@ -221,7 +248,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     for (int d = 0; d < ND; ++d)
 #pragma unroll
       for (int t = 0; t < NPF; ++t) {
-        typename MF::frag bv = MF::load(&Vt[(d * 16 + (lane & 15)) * VS + t * MF::KSTEP + (lane >> 4) * MF::KPL]);
+        typename MF::frag bv = tr_or_load<T>(Vt, KS, Vt, VS, t * MF::KSTEP, d * 16, lane);
         o[d] = MF::mma(pf[t], bv, o[d]);
       }
   }
@@ -283,11 +310,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
   constexpr int VEC = 16 / sizeof(T);
   constexpr int KS = DP + VEC, TS = BKEY + VEC, PS = BKEY + VEC;
   constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16;
-  __shared__ __attribute__((aligned(16))) T smem[2 * BKEY * KS + DP * TS + 4 * 16 * PS];
+  constexpr bool TRR = sizeof(T) == 2;  // bf16: K^T fragments by transposing reads of Ks
+  constexpr int KTBUF = TRR ? 0 : DP * TS;
+  __shared__ __attribute__((aligned(16))) T smem[2 * BKEY * KS + KTBUF + 4 * 16 * PS];
   T* Ks = smem;
   T* Vs = Ks + BKEY * KS;
   T* Kt = Vs + BKEY * KS;
-  T* Ss = Kt + DP * TS;
+  T* Ss = Kt + KTBUF;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
@@ -326,7 +355,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     __syncthreads();
     lds_load_rows<T, BKEY, DP, KS, 256>(Ks, K, a.skl, k0, a.Lk, a.D, tid);
     lds_load_rows<T, BKEY, DP, KS, 256>(Vs, V, a.svl, k0, a.Lk, a.D, tid);
-    lds_load_rows_t<T, BKEY, DP, TS, 256>(Kt, K, a.skl, k0, a.Lk, a.D, tid);
+    if constexpr (!TRR) lds_load_rows_t<T, BKEY, DP, TS, 256>(Kt, K, a.skl, k0, a.Lk, a.D, tid);
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -359,7 +388,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(AttnArgs a) {
     for (int d = 0; d < ND; ++d)
 #pragma unroll
       for (int t = 0; t < NPF; ++t)
-        dq[d] = MF::mma(sf[t], MF::load(&Kt[(d * 16 + (lane & 15)) * TS + t * MF::KSTEP + (lane >> 4) * MF::KPL]), dq[d]);
+        dq[d] = MF::mma(sf[t], tr_or_load<T>(Ks, KS, Kt, TS, t * MF::KSTEP, d * 16, lane), dq[d]);
   }
   T* dQ = (T*)a.dq + b * a.sdqb + h * a.sdqh;
 #pragma unroll
@@ -385,15 +414,17 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
   constexpr int VEC = 16 / sizeof(T);
   constexpr int KS = DP + VEC, QS = BQ + VEC;
   constexpr int NKF = DP / MF::KSTEP, NB = BQ / 16, ND = DP / 16, NPF = BQ / MF::KSTEP;
-  __shared__ __attribute__((aligned(16))) T smem[2 * NW * 16 * KS + 2 * BQ * KS + 2 * DP * QS + 2 * NW * 16 * QS];
+  constexpr bool TRR = sizeof(T) == 2;  // bf16: Q^T / dO^T fragments by transposing reads of Qs / Gs
+  constexpr int TBUF = TRR ? 0 : DP * QS;
+  __shared__ __attribute__((aligned(16))) T smem[2 * NW * 16 * KS + 2 * BQ * KS + 2 * TBUF + 2 * NW * 16 * QS];
   __shared__ float stat[2 * BQ];
   T* Kn = smem;
   T* Vn = Kn + NW * 16 * KS;
   T* Qs = Vn + NW * 16 * KS;
   T* Gs = Qs + BQ * KS;
   T* Qt = Gs + BQ * KS;
-  T* Gt = Qt + DP * QS;
-  T* Pb = Gt + DP * QS;
+  T* Gt = Qt + TBUF;
+  T* Pb = Gt + TBUF;
   T* Sb = Pb + NW * 16 * QS;
   float* lse_s = stat;
   float* di_s = stat + BQ;
@@ -428,8 +459,10 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
     __syncthreads();
     lds_load_rows<T, BQ, DP, KS, NT>(Qs, Q, a.sql, q0, a.Lq, a.D, tid);
     lds_load_rows<T, BQ, DP, KS, NT>(Gs, dO, a.sol, q0, a.Lq, a.D, tid);
-    lds_load_rows_t<T, BQ, DP, QS, NT>(Qt, Q, a.sql, q0, a.Lq, a.D, tid);
-    lds_load_rows_t<T, BQ, DP, QS, NT>(Gt, dO, a.sol, q0, a.Lq, a.D, tid);
+    if constexpr (!TRR) {
+      lds_load_rows_t<T, BQ, DP, QS, NT>(Qt, Q, a.sql, q0, a.Lq, a.D, tid);
+      lds_load_rows_t<T, BQ, DP, QS, NT>(Gt, dO, a.sol, q0, a.Lq, a.D, tid);
+    }
     for (int i = tid; i < BQ; i += NT) {
       const int qi = q0 + i;
       lse_s[i] = qi < a.Lq ? a.lse[(int64_t)bh * a.Lq + qi] * LOG2E : 0.f;
@@ -476,9 +509,8 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
     for (int d = 0; d < ND; ++d)
 #pragma unroll
       for (int t = 0; t < NPF; ++t) {
-        const int o = (d * 16 + (lane & 15)) * QS + t * MF::KSTEP + (lane >> 4) * MF::KPL;
-        dv[d] = MF::mma(pf[t], MF::load(&Gt[o]), dv[d]);
-        dk[d] = MF::mma(sf[t], MF::load(&Qt[o]), dk[d]);
+        dv[d] = MF::mma(pf[t], tr_or_load<T>(Gs, KS, Gt, QS, t * MF::KSTEP, d * 16, lane), dv[d]);
+        dk[d] = MF::mma(sf[t], tr_or_load<T>(Qs, KS, Qt, QS, t * MF::KSTEP, d * 16, lane), dk[d]);
       }
   }
   T* dK = (T*)a.dk + b * a.sdkb + h * a.sdkh;
