@@ -31,7 +31,20 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--drop", type=float, default=0.1)
+    ap.add_argument("--targets", default="", help="comma list of flash-forward key-split targets (workgroups) to sweep")
     a = ap.parse_args()
+    if a.targets:
+        from sam2_video.kernels._lib import lib
+        for t in a.targets.split(","):
+            lib().s2h_attn_config(1 | (int(t) << 8))
+            print(f"key-split target {t}:", end=" ")
+            run(a)
+        lib().s2h_attn_config(1)
+        return
+    run(a)
+
+
+def run(a):
     torch.manual_seed(0)
     B, Lq, H, D = 13, 1024, 1, 256
     sc = 1 / math.sqrt(D)
