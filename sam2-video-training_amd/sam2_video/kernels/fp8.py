@@ -1,9 +1,10 @@
 """MX-fp8 compute mode (BASELINE config 5: `compute_dtype="fp8"`, Lightning precision "fp8").
 
-Recipe: the projection and FFN Linear layers of the image encoder trunk and the memory attention
-run their forward GEMM and their input-gradient
-(dgrad) GEMM on MX-fp8 operands (OCP MXFP8-E4M3, 32-element blocks along the reduction
-dimension, csrc/gemm_mx8.hip): Y = Q(X) Q(W)^T, dX = Q(dY) Q(W^T)^T.  The weight gradients stay
+Recipe: among the projection and FFN Linear layers of the image encoder trunk and the memory
+attention, the widening GEMMs run on MX-fp8 operands (OCP MXFP8-E4M3, 32-element blocks along the
+reduction dimension, csrc/gemm_mx8.hip): the forward of layers with in < out (Hiera qkv and MLP
+fc1, the FFN's linear1): Y = Q(X) Q(W)^T, and the input gradient of layers with out < in (MLP
+fc2, linear2): dX = Q(dY) Q(W^T)^T -- see `_pays`.  The weight gradients stay
 bf16 (dW = dY^T X over 10^4-10^5 token rows from the saved bf16 activations, fp32 accumulate),
 as do activations between kernels, attention, norms, losses, the fp32 master weights and AdamW.
 
@@ -100,17 +101,29 @@ def weight_t(mod):
     return e.t
 
 
+def _pays(k_reduce, n_out):
+    """MX-fp8 only where the quantiser pass over the activation operand ([rows, k_reduce]: one
+    bf16 read + one fp8 write) is cheaper than what the faster GEMM saves.  The step's GEMMs are
+    short-K and store-bound, so the saving is a fraction of the OUTPUT traffic ([rows, n_out]):
+    widening layers (k < n: Hiera qkv / MLP fc1, memory-attention FFN linear1, and the dgrads of
+    the narrowing layers) pay; K = N projections break even and narrowing layers (MLP fc2, FFN
+    linear2 forward over a 4x-wide input) lose -- rocprofv3 of config 5 with every projection on
+    MX-fp8: the quantiser passes took 8.5 ms per step, more than the MX GEMMs saved."""
+    return k_reduce < n_out
+
+
 def linear(x, mod, w, bias, **kw):
-    """forward GEMM of a Linear: MX-fp8 when `mod` is eligible, else the bf16 kernel"""
-    w8 = weight(mod) if x.dtype != torch.float32 else None
+    """forward GEMM of a Linear: MX-fp8 when `mod` is eligible (and it pays), else the bf16 kernel"""
+    w8 = weight(mod) if x.dtype != torch.float32 and _pays(w.shape[1], w.shape[0]) else None
     if w8 is not None:
         return ops.linear_mx8(x, w8, bias, **kw)
     return ops.linear(x, w, bias, **kw)
 
 
 def linear_dgrad(dy, mod, **kw):
-    """input-gradient GEMM of a Linear: MX-fp8 when `mod` is eligible, else the bf16 kernel"""
-    wt8 = weight_t(mod) if dy.dtype != torch.float32 and DGRAD["on"] else None
+    """input-gradient GEMM of a Linear: MX-fp8 when `mod` is eligible (and it pays), else the bf16 kernel"""
+    n_out, k_in = mod.out_features, mod.in_features
+    wt8 = weight_t(mod) if dy.dtype != torch.float32 and DGRAD["on"] and _pays(n_out, k_in) else None
     if wt8 is not None:
         return ops.linear_dgrad_mx8(dy, wt8, **kw)
     return ops.linear_dgrad(dy, mod.compute_weight(), **kw)
