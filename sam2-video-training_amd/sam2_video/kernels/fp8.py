@@ -122,8 +122,9 @@ def linear(x, mod, w, bias, **kw):
 
 def linear_dgrad(dy, mod, **kw):
     """input-gradient GEMM of a Linear: MX-fp8 when `mod` is eligible (and it pays), else the bf16 kernel"""
-    n_out, k_in = mod.out_features, mod.in_features
-    wt8 = weight_t(mod) if dy.dtype != torch.float32 and DGRAD["on"] and _pays(n_out, k_in) else None
+    wt8 = None
+    if dy.dtype != torch.float32 and DGRAD["on"] and _eligible(mod) and _pays(mod.out_features, mod.in_features):
+        wt8 = weight_t(mod)
     if wt8 is not None:
         return ops.linear_dgrad_mx8(dy, wt8, **kw)
     return ops.linear_dgrad(dy, mod.compute_weight(), **kw)

@@ -5,9 +5,9 @@ with respect to the reference); it is checked against this build's bf16 mode on 
 and weights, and against itself between eager steps and captured-graph replays:
 
 * the fp8 step stays close to the bf16 step (dropout off, random-init weights): binarised masks
-  IoU >= 0.92 per frame, loss within 8 %, gradient arena cosine >= 0.95 (measured at B+ 256^2:
-  IoU 0.95-0.96, loss +6 %, cosine 0.977 -- e4m3's 3 mantissa bits through 24 trunk blocks; the
-  bf16 mode of the same build is at IoU 0.992-0.995 against fp32, tools/fp8_drift.py);
+  IoU >= 0.95 per frame, loss within 3 %, gradient arena cosine >= 0.97 (measured at B+ 256^2:
+  IoU 0.972-0.978, loss +0.5 %, cosine 0.985; the bf16 mode of the same build is at IoU
+  0.992-0.995 against fp32, tools/fp8_drift.py);
 * the step really runs the MX-fp8 GEMM (in-library launch profiler records with the MX-fp8
   layout flag) for the projections / FFN of the trunk and the memory attention;
 * config 5 itself (B+, 512^2, 16 frames, 13 objects): finite losses, and graph replays reproduce
@@ -38,9 +38,9 @@ def test_fp8_step_close_to_bf16():
     g16, g8 = res["bf16"][2], res["fp8"][2]
     cos = float((g16 * g8).sum() / (g16.norm() * g8.norm()))
     print("fp8 vs bf16: per-frame IoU", ious, "losses", res["bf16"][1], res["fp8"][1], "grad cosine", cos)
-    assert min(ious) >= 0.92, ious
-    assert abs(res["bf16"][1] - res["fp8"][1]) <= 0.08 * abs(res["bf16"][1])
-    assert cos >= 0.95, cos
+    assert min(ious) >= 0.95, ious
+    assert abs(res["bf16"][1] - res["fp8"][1]) <= 0.03 * abs(res["bf16"][1])
+    assert cos >= 0.97, cos
 
 
 def test_fp8_step_runs_mx8_gemms():
