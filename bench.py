@@ -73,6 +73,20 @@ def record_flops(kind, m):
     return (4.0 if kind == 1 else 8.0) * bh * lq * lk * d
 
 
+def record_bytes(kind, m):
+    """algorithmic HBM bytes of one launch: every operand read once, every output written once
+    (GEMM: bf16 A, B, C -- fp32 C for weight gradients (layout 4), 1-B A / B for MX-fp8 (layout
+    flag 8); attention: Q, K, V, O (+ dO, dQ, dK, dV in the backward), bf16)"""
+    if kind == 4:
+        b, M, N, K, lay = m[1:6]
+        ab = 1 if lay & 8 else 2
+        cb = 4 if lay == 4 else 2
+        return float(b) * (ab * (M * K + N * K) + cb * M * N)
+    bh, lq, lk, d = m[1:5]
+    per = 2.0 * (2 * bh * lq * d + 2 * bh * lk * d)
+    return per if kind == 1 else 2.0 * per
+
+
 FAMILY = {40: "MX-fp8 GEMM (gemm_mx8: forward and dgrad of the projections / FFN, config 5)",
           1: "attention forward (flash_fwd / attn_fwd kernels)",
           2: "attention backward (flash_bwd di/dq/dkv kernels, frame-batched; attn_bwd kernels)",
@@ -86,9 +100,10 @@ def family_roofline(recs, nsteps=1):
     fam = {}
     for ms, m in recs:
         k = 40 if m[0] == 4 and (m[5] & 8) else m[0]  # layout flag 8: MX-fp8 operands
-        f = fam.setdefault(k, {"ms": 0.0, "flops": 0.0, "launches": 0})
+        f = fam.setdefault(k, {"ms": 0.0, "flops": 0.0, "launches": 0, "bytes": 0.0})
         f["ms"] += ms
         f["flops"] += record_flops(m[0], m)
+        f["bytes"] += record_bytes(m[0], m)
         f["launches"] += 1
     if not fam:
         return None
@@ -106,7 +121,9 @@ def family_roofline(recs, nsteps=1):
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": peak(k), "unit": "TFLOP/s",
             "frac": round(ach / peak(k), 4), "traffic": None, "kernel": FAMILY[k],
             "launches": f["launches"], "avg_launch_ms": round(f["ms"] / f["launches"], 4),
-            "flops_per_launch_avg": f["flops"] / f["launches"], "families": table, "_kind": k}
+            "flops_per_launch_avg": f["flops"] / f["launches"],
+            # compare with `traffic` (PMC HBM bytes per launch of the same family)
+            "alg_bytes_per_launch": round(f["bytes"] / f["launches"]), "families": table, "_kind": k}
 
 
 def pmc_traffic(kind):
