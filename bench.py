@@ -239,10 +239,14 @@ def main():
     from sam2_video.training.ddp import init_from_env, shard_clips
     from sam2_video.training.trainer import SAM2LightningModule, StepRunner
 
-    rank, world, local = init_from_env("nccl")
-    if world == 1:
-        torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # S2H_DIST_BACKEND=gloo: rehearsal of the N > 1 path with several ranks sharing the GPUs there
+    # are (rank -> GPU local % count), e.g. 2 ranks on a 1-GPU box; the scaling runs use RCCL
+    backend = os.environ.get("S2H_DIST_BACKEND", "nccl")
+    rank, world, local = init_from_env(backend)
+    dev = local if backend == "nccl" else local % max(1, torch.cuda.device_count())
+    if world == 1 or backend != "nccl":
+        torch.cuda.set_device(dev)
+    device = torch.device("cuda", dev)
     FN.set_seed(1234 + rank)
     trainable = ALL if args.trainable == "all" else ["memory_attention", "memory_encoder"]
     model = SAM2Model(None, f"{args.size}@{args.image_size}", trainable_modules=trainable, compute_dtype=args.dtype)
