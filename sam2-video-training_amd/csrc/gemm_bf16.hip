@@ -465,6 +465,10 @@ static int pick_cfg(const GemmArgs16& a, int batch) {
   if (a.M >= 1024 && a.N >= 1024 && a.K >= 1024 && t256 >= 128) return CFG_256;
   const long t128x64 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64) * batch;
   const bool split = a.out_f32 && a.K >= 1024 && t128x64 < 512;  // plan_splits' split-K regime
+  // deep K on large grids: 128x128 (tools/epi_bench.py: 93184x256x2048 175 -> 139 us; below
+  // 512 of its tiles the 128x64 form stays ahead, e.g. 8192x448x1792 24 vs 29 us)
+  const long t128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch;
+  if (!split && a.K >= 1024 && t128 >= 512) return CFG_128;
   // shallow K (<= 256) on large grids: 32-deep stages, 3-deep ring (tools/epi_bench.py graph
   // replays: 131072x448x112 70 -> 58 us, 32768x672x224 35 -> 28, 93184x2048x256 222 -> 216;
   // below ~2k tiles or at K >= 448 the 64-deep 2-stage form stays ahead)

@@ -13,9 +13,9 @@ from gemm_graph_bench import graph_time  # noqa: E402
 from sam2_video.kernels import _lib, ops  # noqa: E402
 
 # (rows M, layer out N, layer in K): dX [M, K] = dY [M, N] W [N, K]
-SHAPES = [(93184, 256, 2048), (93184, 256, 256), (93184, 256, 768), (131072, 448, 112), (32768, 672, 224),
+SHAPES = [(93184, 2048, 256), (8192, 1792, 448), (93184, 256, 2048), (93184, 256, 256), (93184, 256, 768), (131072, 448, 112), (32768, 672, 224),
           (8192, 448, 1792), (13312, 256, 256), (106496, 256, 64)]
-CFGS = ((0, "auto"), (1, "64"), (7, "128x64"), (11, "128x64k32ns3"), (2, "128"))
+CFGS = ((7, "128x64"), (0, "auto"), (1, "64"), (11, "128x64k32ns3"), (2, "128"))
 
 
 def main():

@@ -25,7 +25,8 @@ def main():
         b = torch.zeros(N, device="cuda")
         out = torch.empty(M, N, device="cuda", dtype=bf)
         row = f"{M}x{N}x{K:<6} MB out {M * N * 2 / 1e6:6.1f} |"
-        for cfg, cn in ((0, "auto"), (1, "64"), (7, "128x64"), (11, "128x64k32ns3")):
+        for cfg, cn in ((0, "auto"), (1, "64"), (7, "128x64"), (11, "128x64k32ns3"), (2, "128"), (4, "256x128"),
+                        (5, "256")):
             for dbg, nm in ((0, "nt"),):
                 _lib.lib().s2h_gemm_config(cfg | (dbg << 8))
                 t = graph_time(lambda: ops.linear(x, w, b, out=out))
