@@ -3,7 +3,7 @@
 //
 // P is recomputed from Q, K and the forward's LSE; dropout masks are regenerated from the
 // same counter hash.  Three kernels, no atomics:
-//   * Di = rowsum(dO * O)                                 (one wave per query row)
+//   * Di = rowsum(dO * O)                                 (inside the dQ kernel)
 //   * dQ:  per 128-query block, K / V tiles streamed by LDS-DMA exactly like the forward;
 //          S^T = K Q^T and dP^T = V dO^T keep the query on the lane, so P, dS are
 //          lane-local; dQ^T += K^T dS^T with K^T fragments from transposing LDS reads.
@@ -94,27 +94,6 @@ __device__ __forceinline__ KvFrame kv_frame(const FlashBwdArgs& a, int bh) {
   return r;
 }
 
-// ------------------------------------------------------------------ Di
-template <int DP>
-__global__ __launch_bounds__(256) void flash_bwd_di_kernel(FlashBwdArgs a) {
-  const int lane = threadIdx.x & 63;
-  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (row >= (int64_t)a.BH * a.Lq) return;
-  const int bh = row / a.Lq, q = row % a.Lq, b = bh / a.H, h = bh % a.H;
-  const bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
-  const bf16* G = a.g + b * a.sgb + h * a.sgh + (int64_t)q * a.sgl;
-  float s = 0.f;
-  for (int d = lane * 4; d < a.D; d += 256) {
-    const uint2 ou = *(const uint2*)(O + d), gu = *(const uint2*)(G + d);
-    const bf16* ob = (const bf16*)&ou;
-    const bf16* gb = (const bf16*)&gu;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) s += (float)ob[e] * (float)gb[e];
-  }
-  s = wave_sum(s);
-  if (lane == 0) a.di[row] = s;
-}
-
 // dropout handling of the backward kernels (a template parameter: a runtime test per element
 // made the compiler branch around every element's exp2 / hash, SALU + exec churn in the loop)
 enum { DROP_NONE = 0, DROP_BITS = 1, DROP_HASH = 2 };
@@ -165,10 +144,27 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     gf[t] = ok ? *(const bf16x8*)(G + (int64_t)q * a.sgl + 32 * t + 8 * g) : bf16x8{};
   }
   const float lse2 = qv ? a.lse[(int64_t)bh * a.Lq + q] * FL_LOG2E : 0.f;
-  const float di = qv ? a.di[(int64_t)bh * a.Lq + q] : 0.f;
+  // Di = rowsum(dO * O) of this lane's query from the dO fragments already in registers and the
+  // matching O fragments, reduced over the 4 lanes (g) of the query: replaces a separate
+  // one-wave-per-row pass over O and dO.  Split 0 stores it for the dK/dV kernel that follows.
+  float di = 0.f;
+  {
+    const bf16* O = a.o + b * a.sob + h * a.soh;
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) {
+      if (qv && 32 * t + 8 * g < a.D) {
+        const bf16x8 of = *(const bf16x8*)(O + (int64_t)q * a.sol + 32 * t + 8 * g);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) di += (float)gf[t][j] * (float)of[j];
+      }
+    }
+    di += __shfl_xor(di, 16, 64);
+    di += __shfl_xor(di, 32, 64);
+  }
   // compiler-visible vmcnt(0): the compiler's own bookkeeping retires these loads here instead
   // of waiting vmcnt(0) inside the key loop (which would also drain the asm K/V prefetch)
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
+  if (split == 0 && g == 0 && qv) a.di[(int64_t)bh * a.Lq + q] = di;
   f32x4 acc[C::ND];  // dQ^T: row d = 16*db + 4g + r, column q
 #pragma unroll
   for (int d = 0; d < C::ND; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -680,7 +676,7 @@ int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D) {
 template <int DP>
 static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.BH * a.Lq;
-  hipLaunchKernelGGL((flash_bwd_di_kernel<DP>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+  // Di = rowsum(dO * O) is computed by the dQ kernel and stored for the dK / dV kernel
   const int drop = a.p_drop <= 0.f ? DROP_NONE : (a.keep ? DROP_BITS : DROP_HASH);
   const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
   if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE>), gq, dim3(FL_WAVES * 64), 0, st, a);
