@@ -56,6 +56,25 @@ CASES = {
                                trainable=ALL),
     "bplus256_point_all_bf16": dict(size="base_plus", image_size=256, T=4, n_cat=4, n_obj=3, prompt="point",
                                     trainable=ALL, autocast="bf16"),
+    # the loss knobs of the reference's experiments, applied as SAM2LightningModule.training_step
+    # does: gt_stride 4 (trainer.py:190-203, sweeps/temp0.7+final_sweeps.yaml:5) with the
+    # multi-step loss at logit temperature 0.7 (losses.py:166, configs/dice_loss_only.yaml:62)
+    "bplus128_t8_gts4_temp07": dict(size="base_plus", image_size=128, T=8, n_cat=4, n_obj=3, prompt="point",
+                                    trainable=ALL, loss=dict(kind="multistep", temperature=0.7, gt_stride=4)),
+    # BCECategoryLoss (losses.py:251-372): 4 of 13 categories valid, temperature 0.7, mean
+    "tiny256_point_all_bce": dict(size="tiny", image_size=256, T=4, n_cat=13, n_obj=4, prompt="point",
+                                  trainable=ALL, loss=dict(kind="bce", temperature=0.7, reduction="mean")),
+    # BCE with a per-category pos_weight (every category valid: the reference indexes pos_weight by
+    # the valid set after checking its length against it, losses.py:348-363) and sum reduction
+    "tiny256_bce_posw_sum": dict(size="tiny", image_size=256, T=3, n_cat=3, n_obj=3, prompt="point",
+                                 trainable=ALL, loss=dict(kind="bce", temperature=1.0, reduction="sum",
+                                                          pos_weight=[2.0, 0.5, 1.5])),
+    # 8 frames at memory-attention Lq = 256 in fp32 and CPU bf16 autocast: the deep bank (7 memory
+    # frames) and the frame-table flash backward over 7 frames, bf16 against the reference's bf16
+    "bplus256_point_all_t8": dict(size="base_plus", image_size=256, T=8, n_cat=4, n_obj=3, prompt="point",
+                                  trainable=ALL),
+    "bplus256_point_all_t8_bf16": dict(size="base_plus", image_size=256, T=8, n_cat=4, n_obj=3, prompt="point",
+                                       trainable=ALL, autocast="bf16"),
 }
 FULL_GRAD_NUMEL = 4096
 
@@ -85,12 +104,20 @@ def run_case(name, c, seed=0, clip_idx=7):
     synth = H.product_file("data/synthetic.py")
     clip = synth.make_clip(clip_idx, c["T"], c["image_size"], c["n_cat"], c["n_obj"], c.get("parts"))
     batch = reference_batch(clip)
-    from sam2_video.model.losses import MultiStepMultiMasksAndIous, CORE_LOSS_KEY
+    from sam2_video.model.losses import BCECategoryLoss, MultiStepMultiMasksAndIous, CORE_LOSS_KEY
     from sam2_video.utils import merge_object_results_to_category
 
-    crit = MultiStepMultiMasksAndIous(weight_dict={"loss_mask": 20, "loss_dice": 1, "loss_iou": 1, "loss_class": 0},
-                                      supervise_all_iou=True, iou_use_l1_loss=True, pred_obj_scores=False,
-                                      focal_gamma_obj_score=0.0, focal_alpha_obj_score=-1.0, logit_temperature=1.0)
+    lc = c.get("loss", {})
+    if lc.get("kind") == "bce":
+        crit = BCECategoryLoss(pos_weight=lc.get("pos_weight"), reduction=lc.get("reduction", "mean"),
+                               logit_temperature=lc.get("temperature", 1.0))
+    else:
+        crit = MultiStepMultiMasksAndIous(weight_dict={"loss_mask": 20, "loss_dice": 1, "loss_iou": 1,
+                                                       "loss_class": 0},
+                                          supervise_all_iou=True, iou_use_l1_loss=True, pred_obj_scores=False,
+                                          focal_gamma_obj_score=0.0, focal_alpha_obj_score=-1.0,
+                                          logit_temperature=lc.get("temperature", 1.0))
+    gt_stride = int(lc.get("gt_stride", 1))
     t0 = time.time()
     # SAM2Model.forward (sam2model.py:153-179), restated to keep the per-object outputs; under
     # `autocast` the forward + loss run in torch.autocast("cpu", bfloat16) (the reference's
@@ -105,7 +132,12 @@ def run_case(name, c, seed=0, clip_idx=7):
         stages = model.forward_tracking(backbone_out, batch)
         outs = merge_object_results_to_category(stages, backbone_out["obj_to_cat"],
                                                 backbone_out["num_categories"])
-        losses = crit(outs, batch.masks)
+        # SAM2LightningModule._apply_gt_stride (trainer.py:190-203), restated: Lightning is absent
+        if gt_stride > 1:
+            idxs = list(range(0, len(outs), gt_stride))
+            losses = crit([outs[i] for i in idxs], batch.masks[idxs])
+        else:
+            losses = crit(outs, batch.masks)
     total = losses[CORE_LOSS_KEY]
     total.backward()
     dt = time.time() - t0
@@ -117,6 +149,12 @@ def run_case(name, c, seed=0, clip_idx=7):
     g["meta/clip_idx"] = torch.tensor(clip_idx)
     g["meta/parts"] = torch.tensor(list(c.get("parts") or []), dtype=torch.long)
     g["meta/autocast"] = torch.tensor(1 if c.get("autocast") == "bf16" else 0)
+    g["meta/loss_kind"] = lc.get("kind", "multistep")
+    g["meta/temperature"] = torch.tensor(float(lc.get("temperature", 1.0)))
+    g["meta/gt_stride"] = torch.tensor(gt_stride)
+    g["meta/reduction"] = lc.get("reduction", "mean")
+    if lc.get("pos_weight") is not None:
+        g["meta/pos_weight"] = torch.tensor(lc["pos_weight"], dtype=torch.float32)
     g["in/images_sum"] = clip["images"].double().sum()
     g["in/images_abs"] = clip["images"].double().abs().sum()
     g["in/masks_count"] = clip["masks"].sum(dim=(2, 3))
@@ -141,7 +179,7 @@ def run_case(name, c, seed=0, clip_idx=7):
         g[f"cat/{t}/high_res_sq"] = (hr.double() ** 2).sum()
         g[f"cat/{t}/ious"] = o["multistep_pred_ious"][0].detach().float().clone()
         g[f"cat/{t}/obj_score"] = o["multistep_object_score_logits"][0].detach().float().clone()
-    for k in ("loss_mask", "loss_dice", "loss_iou", "loss_class", CORE_LOSS_KEY):
+    for k in [k for k in losses if k != "logits"]:
         v = losses[k]
         g[f"loss/{k}"] = v.detach().float().clone() if torch.is_tensor(v) else torch.tensor(float(v))
     none_grad = []

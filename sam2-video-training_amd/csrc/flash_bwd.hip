@@ -702,6 +702,11 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// the dQ kernel reads O (for Di = rowsum(dO * O)) with 16-B loads: base and strides 16-B aligned
+static bool flash_bwd_o_aligned(const void* o, int64_t sob, int64_t soh, int64_t sol) {
+  return ((uintptr_t)o & 15) == 0 && (sob & 7) == 0 && (soh & 7) == 0 && (sol & 7) == 0;
+}
+
 int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
                   const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                   const void* k, int64_t skb, int64_t skh, int64_t skl,
@@ -717,6 +722,7 @@ int s2h_flash_bwd(int B, int H, int Lq, int Lk, int D,
   a.idx0 = idx0;
   a.D = D;
   if (keep && D != 256) return (int)hipErrorInvalidValue;  // the head-dim-256 kernels read the bitmap
+  if (!flash_bwd_o_aligned(o, sob, soh, sol)) return (int)hipErrorInvalidValue;
   a.keep = keep;
   a.kw = 2 * ((Lk + 63) / 64);
   a.BH = B * H; a.H = H; a.Lq = Lq; a.Lk = Lk;
@@ -774,6 +780,7 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
   if (nfr <= 0 || bpf <= 0 || H <= 0 || Lq <= 0) return 0;
   if (nfr > S2H_MAX_FRAMES || !s2h_flash_bwd_eligible(S2H_BF16, Lq, D)) return (int)hipErrorInvalidValue;
   if (keep && (D != 256 || fr_koff == nullptr)) return (int)hipErrorInvalidValue;
+  if (!flash_bwd_o_aligned(o, sob, soh, sol)) return (int)hipErrorInvalidValue;
   FlashBwdArgs a = {};
   a.D = D;
   a.nfr = nfr; a.bpf = bpf;

@@ -73,14 +73,21 @@ class SAM2Model(SAM2Base):
 
     # ----------------------------------------------------------- weights
     def _load_weights(self, checkpoint_path, seed):
+        """A SAM2.1 checkpoint (`{"model": state_dict}`, as upstream build_sam2 loads it, strict) or,
+        with checkpoint_path None only, deterministic synthetic weights keyed by parameter name (no
+        checkpoints exist offline).  A path that does not exist raises, as upstream build_sam2 does
+        (reference sam2model.py:80-82) -- a mistyped path never trains from random weights."""
         sd = self.state_dict()
-        if checkpoint_path and os.path.exists(str(checkpoint_path)):
-            ck = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
-            if isinstance(ck, dict) and "model" in ck:
-                ck = ck["model"]
-            self.load_state_dict(ck, strict=True)
-        else:  # offline: deterministic synthetic weights keyed by parameter name
+        if checkpoint_path is None:
             self.load_state_dict({k: synth_tensor(k, v.shape, seed) for k, v in sd.items()}, strict=True)
+            return
+        if not os.path.isfile(str(checkpoint_path)):
+            raise FileNotFoundError(f"SAM2 checkpoint not found: {checkpoint_path} (pass checkpoint_path=None "
+                                    "for deterministic synthetic weights)")
+        ck = torch.load(checkpoint_path, map_location="cpu", weights_only=True)
+        if isinstance(ck, dict) and "model" in ck:
+            ck = ck["model"]
+        self.load_state_dict(ck, strict=True)
 
     @staticmethod
     def strip_lightning_prefix(ck):

@@ -142,7 +142,13 @@ class FrameTracker:
             gm = FN._grad_of(self.m.no_mem_embed)
             if gm is not None:
                 ops.colsum(d0.reshape(O * L, C), gm.view(-1), accumulate=True)
-        if self.ma is not None and all(t in dpix for t in range(1, T)):
+        have = [t in dpix for t in range(1, T)]
+        if self.ma is not None and any(have) and not all(have):
+            # every SAM-heads tape returns its pix gradient (zeros for unsupervised frames), so a
+            # partial set means a broken tape -- never drop the memory-attention backward silently
+            raise RuntimeError(f"memory-attention backward: pix gradients for frames "
+                               f"{[t for t, h in zip(range(1, T), have) if h]} only (expected 1..{T - 1})")
+        if self.ma is not None and have and all(have):
             # frames 1..T-1 stacked in order for the memory-attention tape (one copy unless a
             # single SAM-heads tape already holds them contiguously)
             g1 = dpix[1]

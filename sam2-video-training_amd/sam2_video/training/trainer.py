@@ -118,7 +118,8 @@ class SAM2LightningModule(_ModuleBase):
 
     # ------------------------------------------------------------ setup
     def setup(self, stage: str = "fit", device=None):
-        """trainer.py:101-115: instantiate the model section, load it on the device, train mode"""
+        """trainer.py:101-115: instantiate the model section, load it on the device (the current
+        CUDA device -- the rank's own under DDP -- when none is given), train mode"""
         if stage == "fit":
             if self.model is None:
                 m = self.cfg.model
@@ -128,14 +129,20 @@ class SAM2LightningModule(_ModuleBase):
                     kw = {"compute_dtype": self.compute_dtype} if self.compute_dtype else {}
                     self.model = instantiate(_todict(m), **kw)
             if device is None:
-                device = "cuda"
+                device = torch.device("cuda", torch.cuda.current_device())
             self.model.load(device)
             self.model.train()
 
-    def configure_optimizers(self, total_steps: int = 1) -> Dict[str, Any]:
+    def configure_optimizers(self, total_steps: Optional[int] = None) -> Optional[Dict[str, Any]]:
         """trainer.py:117-177: AdamW(lr, weight_decay, betas) -- eps 1e-8 / amsgrad False whatever the
         YAML says -- with get_cosine_schedule_with_warmup(total * warmup_factor, total), stepped per
-        optimizer step.  The clip is the Trainer's gradient_clip_val (Lightning's clip_grad_norm_)."""
+        optimizer step.  The clip is the Trainer's gradient_clip_val (Lightning's clip_grad_norm_).
+        Called by Lightning itself (no argument, a trainer attached) it returns None: the arena
+        optimizer is not a torch.optim.Optimizer over `param.grad`; the manual-optimization runner
+        builds it on the first training_step."""
+        if total_steps is None and self._attached_trainer() is not None:
+            return None
+        total_steps = 1 if total_steps is None else total_steps
         o = self.cfg.optimizer
         if str(_get(o, "type", "adamw")).lower() != "adamw":
             raise NotImplementedError("only AdamW (the reference configs' optimizer) is built")
@@ -167,11 +174,17 @@ class SAM2LightningModule(_ModuleBase):
 
     def log(self, name, value, **kw):
         self.logged[name] = value.detach() if torch.is_tensor(value) else value
-        if HAVE_LIGHTNING and getattr(self, "_trainer", None) is not None:  # pragma: no cover
+        if HAVE_LIGHTNING and self._attached_trainer() is not None:  # pragma: no cover
             super().log(name, value, batch_size=1, **kw)
 
     def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
-        """trainer.py:256-289"""
+        """trainer.py:256-289.  Under a Lightning trainer (manual optimization, see
+        `_lightning_runner`) it also runs the backward into the gradient arena and, at accumulation
+        boundaries, the all-reduce + clip + AdamW -- the work Lightning's automatic optimization
+        and DDP wrapper would do on `param.grad`, which this build never fills."""
+        runner = self._lightning_runner()
+        if runner is not None:
+            runner.begin_micro_step()
         outs_per_frame, obj_to_cat = self.forward(batch)
         self.last_outputs = outs_per_frame
         outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
@@ -184,21 +197,36 @@ class SAM2LightningModule(_ModuleBase):
             self.log(f"train/{k}", v)
         if self.optimizer is not None:
             self.log("train/learning_rate", self.optimizer.param_groups[0]["lr"])
-        if HAVE_LIGHTNING and getattr(self, "_trainer", None) is not None:  # pragma: no cover
-            self._lightning_manual_step(total)
+        if runner is not None:
+            if hasattr(self, "manual_backward"):  # pragma: no cover - LightningModule only
+                self.manual_backward(total)
+            else:
+                total.backward()
+            runner.after_backward()
         return total
 
-    def _lightning_manual_step(self, total):  # pragma: no cover - Lightning is not installed here
-        """Under a real Lightning Trainer (manual optimization): backward into the gradient arena,
-        then clip + AdamW at accumulation boundaries with the trainer's settings."""
-        tr = self.trainer
+    def _attached_trainer(self):
+        """the Lightning trainer driving this module (LightningModule._trainer), if any; this
+        build's own Trainer drives StepRunner directly and does not attach itself"""
+        return getattr(self, "_trainer", None)
+
+    def _lightning_runner(self):
+        """Manual-optimization runner for a Lightning trainer, built on the first training_step:
+        accumulation and clip from the trainer's settings, the schedule over its
+        estimated_stepping_batches, and the arena all-reduce whenever the process group has more
+        than one rank (Lightning `strategy=ddp` must not wrap the module in
+        DistributedDataParallel -- no parameter has a .grad -- use `arena_ddp_strategy()`)."""
+        tr = self._attached_trainer()
+        if tr is None:
+            return None
         if self._runner is None:
-            self.gradient_clip_val = tr.gradient_clip_val
-            self._runner = StepRunner(self, total_steps=max(1, int(tr.estimated_stepping_batches)),
-                                      accumulate_grad_batches=tr.accumulate_grad_batches, graph=False,
-                                      gradient_clip_val=tr.gradient_clip_val)
-        self.manual_backward(total)
-        self._runner.after_backward()
+            import torch.distributed as dist
+            distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+            self._runner = StepRunner(self, total_steps=max(1, int(getattr(tr, "estimated_stepping_batches", 1))),
+                                      accumulate_grad_batches=getattr(tr, "accumulate_grad_batches", 1),
+                                      graph=False, gradient_clip_val=getattr(tr, "gradient_clip_val", None),
+                                      distributed=distributed)
+        return self._runner
 
     @torch.no_grad()
     def validation_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
@@ -346,6 +374,22 @@ class StepRunner:
         self.module.last_outputs = ent["outputs"]
         return ent["loss"]
 
+    def begin_micro_step(self):
+        """zero the gradient arena when an accumulation window starts (Lightning's zero_grad) and
+        draw fresh dropout masks (the device RNG offset); shared by __call__ and the Lightning path"""
+        if self.micro_step % self.accumulate == 0:
+            self.module.model.arena.zero_grad()
+        self.rng.fill_(self.micro_step + 1)
+        self._fn.set_seed(self.seed_base)
+
+    def flush(self) -> bool:
+        """close a partial accumulation window (Lightning steps the optimizer on an epoch's last
+        batch even when fewer than accumulate_grad_batches micro-steps were taken)"""
+        if self.micro_step % self.accumulate == 0:
+            return False
+        self.micro_step += self.accumulate - self.micro_step % self.accumulate - 1
+        return self.after_backward()
+
     def after_backward(self, reduced: bool = False) -> bool:
         """Counts the micro-step; at an accumulation boundary runs all-reduce (unless `reduced`:
         __call__ already overlapped it with the backward) + clip + AdamW (the arena is zeroed when
@@ -366,9 +410,7 @@ class StepRunner:
         return True
 
     def __call__(self, batch):
-        if self.micro_step % self.accumulate == 0:  # new accumulation window (zero_grad)
-            self.module.model.arena.zero_grad()
-        self.rng.fill_(self.micro_step + 1)
+        self.begin_micro_step()
         self._replay2 = None
         loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
         boundary = (self.micro_step + 1) % self.accumulate == 0
@@ -438,13 +480,22 @@ class SAM2LightningDataModule(_DataBase):
             self.val_dataset = self._dataset("val")
 
     def _loader(self, ds, shuffle):
-        from torch.utils.data import DataLoader
+        """B == 1 clip loader; with more than one rank in the process group the clips are sharded
+        by a DistributedSampler (what Lightning injects under strategy=ddp): every rank trains on
+        its own clips, the Trainer calls sampler.set_epoch each epoch"""
+        import torch.distributed as dist
+        from torch.utils.data import DataLoader, DistributedSampler
 
         from ..data.synthetic import sam2_collate_fn
         if ds is None:
             raise RuntimeError("dataset not initialized: call setup('fit') first")
+        sampler = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            sampler = DistributedSampler(ds, num_replicas=dist.get_world_size(), rank=dist.get_rank(),
+                                         shuffle=shuffle)
         return DataLoader(ds, batch_size=int(_get(self.data, "batch_size", 1)),
-                          num_workers=int(_get(self.data, "num_workers", 0)), shuffle=shuffle,
+                          num_workers=int(_get(self.data, "num_workers", 0)),
+                          shuffle=shuffle if sampler is None else False, sampler=sampler,
                           pin_memory=torch.cuda.is_available(), collate_fn=sam2_collate_fn)
 
     def train_dataloader(self):
@@ -464,6 +515,12 @@ class Trainer:
                  gradient_clip_val=None, accumulate_grad_batches=1, val_check_interval=1.0,
                  num_sanity_val_steps=0, limit_train_batches=None, limit_val_batches=None,
                  log_every_n_steps=50, strategy="auto", graph=True, default_root_dir=None, **unused):
+        if str(accelerator).lower() == "cpu":
+            # the reference's config 1 (overfit.yaml, trainer.accelerator=cpu): this build's step is
+            # HIP kernels only -- refuse rather than run on the GPU behind the caller's back
+            raise ValueError("accelerator='cpu' is not supported: the sam2_video step runs as HIP kernels on an "
+                             "MI355X (use accelerator='gpu' / 'auto')")
+        self.accelerator = accelerator
         self.precision = precision
         self.devices = devices
         self.strategy = strategy
@@ -519,7 +576,8 @@ class Trainer:
         module.setup("fit", device)
         n_train = self._limit(len(train_dataloaders), self.limit_train_batches)
         n_val = self._limit(len(val_dataloaders), self.limit_val_batches) if val_dataloaders is not None else 0
-        per_epoch = max(1, n_train // self.accumulate_grad_batches)
+        # Lightning's estimated_stepping_batches: a partial last window is an optimizer step too
+        per_epoch = max(1, math.ceil(n_train / self.accumulate_grad_batches))
         total = self.max_steps if self.max_steps > 0 else per_epoch * self.max_epochs
         run = StepRunner(module, total, distributed=world > 1, graph=self.graph,
                          accumulate_grad_batches=self.accumulate_grad_batches,
@@ -534,6 +592,9 @@ class Trainer:
         done = False
         for epoch in range(self.max_epochs):
             self.current_epoch = epoch
+            sampler = getattr(train_dataloaders, "sampler", None)
+            if hasattr(sampler, "set_epoch"):
+                sampler.set_epoch(epoch)
             for i, batch in enumerate(train_dataloaders):
                 if i >= n_train:
                     break
@@ -551,11 +612,17 @@ class Trainer:
                     break
             if done:
                 break
+            if run.flush():  # the epoch's last, partial accumulation window
+                self.global_step = run.global_step
         return self.history
 
     def save_checkpoint(self, path, module: SAM2LightningModule):
         """Lightning-layout checkpoint: state_dict with the `model.` prefix (the reference strips it
-        when it reloads, train.py:146-157) + optimizer state + counters."""
+        when it reloads, train.py:146-157) + optimizer state + counters.  Written by global rank 0
+        only (Lightning's rank-zero checkpointing); the parameters are identical on every rank."""
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_rank() != 0:
+            return
         sd = {"model." + k: v.detach().cpu() for k, v in module.model.state_dict().items()}
         torch.save({"state_dict": sd, "optimizer_states": [module.optimizer.state_dict()],
                     "global_step": self.global_step, "epoch": self.current_epoch}, path)

@@ -765,6 +765,42 @@ def test_flash_strided_qkv_padded_head_fwd_bwd(d):
     _close(dv, vr.grad, 4e-2)
 
 
+def test_flash_bwd_strided_o_and_misaligned_o_refused():
+    """the flash dQ kernel reads O (Di fusion) with 16-B loads: O as a strided view into a wider
+    buffer (16-B aligned base and strides) gives the contiguous-O gradients bit for bit; an O whose
+    base is only 8-B aligned goes to the generic kernel through s2h_attn_bwd, and is refused with
+    hipErrorInvalidValue by the frame-batched flash entry point instead of faulting"""
+    ops = _ops()
+    from sam2_video.kernels._lib import HipKernelError
+    torch.manual_seed(9)
+    B, L, H, D = 2, 256, 1, 256
+    q, k, v = ((torch.randn(B, L, H, D, device=DEV) * 0.5).to(torch.bfloat16) for _ in range(3))
+    o = torch.empty(B, L, H, D, device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, H, L, device=DEV)
+    ops.attn_fwd(q, k, v, o, lse, D ** -0.5)
+    do = torch.randn_like(o)
+    grads = [torch.empty_like(q) for _ in range(3)]
+    ops.attn_bwd(q, k, v, o, do, lse, *grads, D ** -0.5)
+    wide = torch.zeros(B, L, H, D + 16, device=DEV, dtype=torch.bfloat16)
+    ow = wide[..., 8:8 + D]
+    ow.copy_(o)
+    g2 = [torch.empty_like(q) for _ in range(3)]
+    ops.attn_bwd(q, k, v, ow, do, lse, *g2, D ** -0.5)
+    for a, b in zip(grads, g2):
+        assert torch.equal(a, b)
+    om = wide[..., 4:4 + D]
+    om.copy_(o)
+    g3 = [torch.empty_like(q) for _ in range(3)]
+    ops.attn_bwd(q, k, v, om, do, lse, *g3, D ** -0.5)  # generic kernel
+    for a, b in zip(grads, g3):
+        _close(b, a.float(), 4e-2)
+    kp, vp = k.reshape(B * L, H, D), v.reshape(B * L, H, D)
+    with pytest.raises(HipKernelError):
+        ops.flash_bwd_frames(1, B, [L], [0], [0], q, kp, vp, om, do, lse, torch.empty_like(q),
+                             torch.empty_like(kp), torch.empty_like(vp), D ** -0.5, 0.0, 0)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_elementwise_vector_forms_match_scalar(dtype):
     """16-B vector kernels (add, broadcast add, act fwd / bwd, dropout, act + dropout backward)
