@@ -192,6 +192,35 @@ int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_l
                          float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
                          const int64_t* fr_koff, hipStream_t st);
 
+/* V-fold of the memory-attention cross-attention (RoPEAttention, transformer.py:275-311, with
+ * kv_in_dim 64: memory_attention.py:66-81, sam2.1_hiera_t.yaml:49-58).  Its values are a projection
+ * of the 64-channel memory bank M, V = M Wv^T + bv, so with D = dropout(softmax(scale q k^T))
+ * (the dropped, normalised probabilities) attention(q, k, V) = u' [Wv | bv]^T where
+ * u' = [D M | rowsum(D) | 0 x 7] (72 columns).  Single head, q / k head_dim 256, bf16, Lq >= 128.
+ * s2h_attn_fwd_vfold: q [B, Lq, 256], k [B, Lk, 256] (RoPE applied), mem [B, Lk, 64] -> u [B, Lq,
+ * sul >= 72], lse [B, Lq]; strides (batch, row) in elements, 16-B aligned rows; ws of
+ * s2h_attn_fwd_vfold_ws_bytes bytes enables the key split; keep: as s2h_attn_fwd (B, H = 1).
+ * Replaces v_proj(memory) + the SDPA of the cross-attention (transformer.py:296-307). */
+int64_t s2h_attn_fwd_vfold_ws_bytes(int B, int Lq, int Lk);
+int s2h_attn_fwd_vfold(int B, int Lq, int Lk, const void* q, int64_t sqb, int64_t sql, const void* k, int64_t skb,
+                       int64_t skl, const void* mem, int64_t smb, int64_t sml, void* u, int64_t sub, int64_t sul,
+                       float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, uint32_t* keep, void* ws,
+                       int64_t ws_bytes, hipStream_t st);
+/* Frame-batched backward of s2h_attn_fwd_vfold (layout as s2h_flash_bwd_frames, H = 1): du = the
+ * gradient of u' (dO [Wv | bv | 0], 72 columns), dq, dk; no value gradient (the memory bank is
+ * detached, sam2model.py:345-358).  di_ws: fp32 [nfr * bpf * Lq]. */
+int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
+                               const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql, const void* k,
+                               int64_t skl, const void* mem, int64_t sml, const void* u, int64_t sub, int64_t sul,
+                               const void* du, int64_t sgb, int64_t sgl, void* dq, int64_t sdqb, int64_t sdql, void* dk,
+                               int64_t sdkl, const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                               const uint32_t* keep, const int64_t* fr_koff, hipStream_t st);
+/* [Wv | bv | 0] as a bf16 [N, ld] matrix (ld >= K + 1) from the bf16 weight [N, K] and the fp32 bias,
+ * and its fp32 gradient g [N, ld] scattered back: gwv [N, K] += g[:, :K], gbv [N] += g[:, K]
+ * (either nullable).  The value projection's parameters of the folded cross-attention. */
+int s2h_vfold_weight(int N, int K, int ld, const void* wv, const float* bv, void* out, hipStream_t st);
+int s2h_vfold_grad(int N, int K, int ld, const float* g, float* gwv, float* gbv, hipStream_t st);
+
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:
  * xsum = x + badd (badd broadcast over rows when b_bcast), y = LN(xsum) * gamma + beta;

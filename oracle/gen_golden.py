@@ -73,6 +73,9 @@ CASES = {
     # frames) and the frame-table flash backward over 7 frames, bf16 against the reference's bf16
     "bplus256_point_all_t8": dict(size="base_plus", image_size=256, T=8, n_cat=4, n_obj=3, prompt="point",
                                   trainable=ALL),
+    # Hiera-L trunk (stages [2, 6, 36, 4], window_spec [8, 4, 16, 8], global blocks 23 / 33 / 43, head
+    # dim 72, BASELINE config 4's model) at a small resolution
+    "large128_point_all": dict(size="large", image_size=128, T=3, n_cat=4, n_obj=2, prompt="point", trainable=ALL),
     "bplus256_point_all_t8_bf16": dict(size="base_plus", image_size=256, T=8, n_cat=4, n_obj=3, prompt="point",
                                        trainable=ALL, autocast="bf16"),
 }

@@ -1099,3 +1099,43 @@ void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t 
   if (b > 4096) b = 4096;
   hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)b), dim3(256), 0, st, p, rows, cols, ld);
 }
+
+// ------------------------------------------------------------------ V-fold value projection
+// [Wv | bv | 0] (bf16 [N, ld], ld >= K + 8): the value projection's weight with its bias as an
+// extra input column, the B operand of u' [rows, K + 8] x [Wv | bv | 0]^T (flash.hip V-fold).
+// wv is the compute-dtype (bf16) weight [N, K], bv the fp32 bias [N].
+__global__ __launch_bounds__(256) void vfold_weight_kernel(int N, int K, int ld, const bf16* wv, const float* bv,
+                                                           bf16* out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)N * ld) return;
+  const int n = (int)(i / ld), k = (int)(i % ld);
+  out[i] = k < K ? wv[(int64_t)n * K + k] : (k == K ? (bf16)bv[n] : (bf16)0.f);
+}
+extern "C" int s2h_vfold_weight(int N, int K, int ld, const void* wv, const float* bv, void* out, hipStream_t st) {
+  if (N <= 0) return 0;
+  if (ld < K + 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(vfold_weight_kernel, dim3((unsigned)(((int64_t)N * ld + 255) / 256)), dim3(256), 0, st, N, K, ld,
+                     (const bf16*)wv, bv, (bf16*)out);
+  return (int)hipGetLastError();
+}
+
+// the weight gradient of [Wv | bv | 0] (fp32 [N, ld]) scattered back: gwv [N, K] += g[:, :K],
+// gbv [N] += g[:, K] (either may be null: frozen)
+__global__ __launch_bounds__(256) void vfold_grad_kernel(int N, int K, int ld, const float* g, float* gwv, float* gbv) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)N * (K + 1)) return;
+  const int n = (int)(i / (K + 1)), k = (int)(i % (K + 1));
+  const float v = g[(int64_t)n * ld + k];
+  if (k < K) {
+    if (gwv) gwv[(int64_t)n * K + k] += v;
+  } else if (gbv) {
+    gbv[n] += v;
+  }
+}
+extern "C" int s2h_vfold_grad(int N, int K, int ld, const float* g, float* gwv, float* gbv, hipStream_t st) {
+  if (N <= 0) return 0;
+  if (ld < K + 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(vfold_grad_kernel, dim3((unsigned)(((int64_t)N * (K + 1) + 255) / 256)), dim3(256), 0, st, N, K,
+                     ld, g, gwv, gbv);
+  return (int)hipGetLastError();
+}

@@ -18,6 +18,13 @@
 //   * Too few query rows to fill 256 CUs (13 objects x 1024 rows = 104 query blocks) ->
 //     the key range is split over workgroups; partial (O, m, l) go to a workspace and a
 //     combine kernel merges them (flash-decoding style).
+//   * V-fold (DV != DP, s2h_attn_fwd_vfold): the memory-attention cross-attention's values are a
+//     projection of the 64-channel memory bank, V = M Wv^T + bv (memory_attention.py:66-81,
+//     kv_in_dim 64).  With D = P_drop / l the dropped, normalised probabilities,
+//     D V = (D M) Wv^T + rowsum(D) bv: the kernel streams M (64 wide) instead of V (256 wide) and
+//     writes u' = [D M | rowsum(D) | 0 x 7] (72 columns); one [rows x 72] x [72 x 256] GEMM with
+//     [Wv | bv] finishes O.  P V costs a quarter of its MFMAs and V tiles a quarter of their bytes;
+//     the V projection of the whole bank (up to 7196 x 13 rows per frame and layer) disappears.
 #include "flash_common.h"
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
@@ -47,14 +54,23 @@ struct FlashArgs {
 // dropout: none / counter hash / counter hash + keep bitmap store (template: no per-tile tests)
 enum { FDROP_NONE = 0, FDROP_HASH = 1, FDROP_BITS = 2 };
 
-template <int DP, int DROP>
+// columns of the V-fold output row u' = [D M (DV) | rowsum(D) | 0 x 7]
+#define FL_VFOLD_COLS(DV) ((DV) + 8)
+// partial-row scalars in the key-split workspace: (m, l) or, V-fold, (m, l, rowsum(D), -)
+#define FL_MLW(FOLD) ((FOLD) ? 4 : 2)
+
+template <int DP, int DROP, int DV = DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
+  constexpr bool FOLD = DV != DP;
   const uint32_t hkey = DROP != FDROP_NONE ? s2h_hash_key(s2h_seed(a.seed, a.seed_off)) : 0u;
   const uint32_t t16 = a.thresh >> 16;
   using C = FlashCfg<DP>;
-  using I = PadImg<DP>;  // padded K / V images (affine read addresses, no swizzle)
+  using I = PadImg<DP>;   // padded K image (affine read addresses, no swizzle)
+  using IV = PadImg<DV>;  // padded V image (V-fold: the 64-channel memory rows)
+  constexpr int NDV = DV / 16;
+  constexpr int STG = I::TILEB + IV::TILEB;
   // one LDS array: [2 stages][K tile | V tile]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * I::TILEB];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
@@ -71,9 +87,9 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
 
   if (nt > 0) {
     dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, a.Lk, w, lane, a.D);
-    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane, a.D);
+    dma_tile_pad<DV, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane, FOLD ? DV : a.D);
   }
-  const int npw = I::pieces(w);
+  const int npw = I::pieces(w), npv = IV::pieces(w);
 
   // Q^T fragments (B operand of K Q^T): lane -> query q, d = 32t + 8g + j
   bf16x8 qf[C::NT];
@@ -87,24 +103,25 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   // the first MFMA of every tile -- which also drains the (asm, invisible) K/V prefetch
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 
-  f32x4 o[C::ND];  // O^T: row d = 16*db + 4g + r, column q
+  f32x4 o[NDV];  // O^T: row d = 16*db + 4g + r, column q
 #pragma unroll
-  for (int d = 0; d < C::ND; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int d = 0; d < NDV; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m = -INFINITY, l = 0.f;
+  float rd = 0.f;  // V-fold with dropout: running rowsum of the dropped probabilities (scaled like l)
   const uint64_t drow = a.idx0 + ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
   const int qq = (lane >> 2) & 3, pp = lane & 3;  // transposing-read lane roles
 
   for (int it = 0; it < nt; ++it) {
     const int kt = t0 + it;
     const int k0 = kt * C::KT;
-    char* Kb = smem + (it & 1) * 2 * I::TILEB;
+    char* Kb = smem + (it & 1) * STG;
     char* Vb = Kb + I::TILEB;
     if (it + 1 < nt) {
-      char* Kn = smem + ((it + 1) & 1) * 2 * I::TILEB;
+      char* Kn = smem + ((it + 1) & 1) * STG;
       dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane, a.D);
-      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane, a.D);
-      // this wave's pieces of tile `it` have landed once all but the 2*npw just issued retired
-      wait_vmcnt_pieces<2, I::PPW_LO>(npw);
+      dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane, FOLD ? DV : a.D);
+      // this wave's pieces of tile `it` have landed once all but the npw + npv just issued retired
+      wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
     } else {
       wait_vmcnt<0>();
     }
@@ -160,6 +177,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mref);
         rs += s[kb][r];
       }
+    float rdt = 0.f;  // V-fold: this tile's dropped-probability sum (lane part)
     if constexpr (DROP != FDROP_NONE) {
       uint32_t kbits[2] = {0u, 0u};  // this lane's keep flags: bit 16kb + 4g + e of the tile's 64 keys
       // the 4 keys of a (kb) block are consecutive: two hashes per block when pairs align
@@ -185,6 +203,10 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         }
 #pragma unroll
         for (int e = 0; e < 4; ++e) s[kb][e] = kp[e] ? s[kb][e] * a.inv_keep : 0.f;
+        if constexpr (FOLD) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) rdt += s[kb][e];
+        }
         kbits[kb >> 1] |= ((uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3))
                           << (16 * (kb & 1) + 4 * g);
       }
@@ -200,9 +222,14 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     rs += __shfl_xor(rs, 16);
     rs += __shfl_xor(rs, 32);
     l = l * alpha + rs;
+    if constexpr (FOLD && DROP != FDROP_NONE) {
+      rdt += __shfl_xor(rdt, 16);
+      rdt += __shfl_xor(rdt, 32);
+      rd = rd * alpha + rdt;
+    }
     if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
-      for (int d = 0; d < C::ND; ++d) o[d] *= alpha;
+      for (int d = 0; d < NDV; ++d) o[d] *= alpha;
     }
     // P^T as the B operand: 32-key step c, k index 8g + j <-> key 32c + 16(j>>2) + 4g + (j&3)
     bf16x8 pb[2];
@@ -216,10 +243,10 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     for (int c = 0; c < 2; ++c) {
       const int r0 = 32 * c + 4 * g + qq;
 #pragma unroll
-      for (int d = 0; d < C::ND; ++d) {
+      for (int d = 0; d < NDV; ++d) {
         const int dcol = 16 * d + 4 * pp;  // first of the 4 d this lane addresses
-        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + r0 * I::ROWB + 2 * dcol));
-        v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + (r0 + 16) * I::ROWB + 2 * dcol));
+        v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + r0 * IV::ROWB + 2 * dcol));
+        v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + (r0 + 16) * IV::ROWB + 2 * dcol));
         v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
         o[d] = mfma16(__builtin_bit_cast(bf16x8, cat), pb[c], o[d]);
       }
@@ -235,54 +262,70 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
     const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-    for (int d = 0; d < C::ND; ++d) {
+    for (int d = 0; d < NDV; ++d) {
       bf16 t4[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) t4[e] = (bf16)(o[d][e] * inv);
-      if (16 * d + 4 * g < a.D) *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
+      if (FOLD || 16 * d + 4 * g < a.D) *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
+    }
+    if constexpr (FOLD) {  // rowsum(D): exactly 1 without dropout (l is the sum of the same p)
+      if (g == 0) {
+        bf16 t8[8] = {};
+        t8[0] = (bf16)(DROP == FDROP_NONE ? (l > 0.f ? 1.f : 0.f) : rd * inv);
+        *(uint4*)(O + DV) = *(const uint4*)t8;
+      }
     }
     if (g == 0) a.lse[(int64_t)bh * a.Lq + q] = (m + log2f(l)) * FL_LN2;
   } else {
     const int64_t row = (int64_t)split * a.BH * a.Lq + (int64_t)bh * a.Lq + q;
-    float* W = a.ws_o + row * DP;
+    float* W = a.ws_o + row * DV;
 #pragma unroll
-    for (int d = 0; d < C::ND; ++d) *(float4*)(W + 16 * d + 4 * g) = float4{o[d][0], o[d][1], o[d][2], o[d][3]};
+    for (int d = 0; d < NDV; ++d) *(float4*)(W + 16 * d + 4 * g) = float4{o[d][0], o[d][1], o[d][2], o[d][3]};
     if (g == 0) {
-      a.ws_ml[2 * row] = m;
-      a.ws_ml[2 * row + 1] = l;
+      a.ws_ml[FL_MLW(FOLD) * row] = m;
+      a.ws_ml[FL_MLW(FOLD) * row + 1] = l;
+      if constexpr (FOLD) a.ws_ml[FL_MLW(FOLD) * row + 2] = DROP == FDROP_NONE ? l : rd;
     }
   }
 }
 
 // Merge the key-split partials: one wave per query row, DP/64 columns per lane.
-template <int DP>
+// V-fold (DV != DP): the partials carry rowsum(D) beside (m, l), merged like l; the output row is
+// u' = [DV columns | rowsum(D) / L | 0 x 7].
+template <int DP, int DV = DP>
 __global__ __launch_bounds__(256) void flash_combine_kernel(FlashArgs a) {
+  constexpr bool FOLD = DV != DP;
+  constexpr int MLW = FL_MLW(FOLD);
   const int lane = threadIdx.x & 63;
   const int64_t rowg = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);  // bh*Lq + q
   if (rowg >= (int64_t)a.BH * a.Lq) return;
   const int bh = rowg / a.Lq, q = rowg % a.Lq, b = bh / a.H, h = bh % a.H;
   const int64_t stride = (int64_t)a.BH * a.Lq;
   float M = -INFINITY;
-  for (int s = 0; s < a.splits; ++s) M = fmaxf(M, a.ws_ml[2 * (s * stride + rowg)]);
+  for (int s = 0; s < a.splits; ++s) M = fmaxf(M, a.ws_ml[MLW * (s * stride + rowg)]);
   const float Mr = M == -INFINITY ? 0.f : M;
-  float L = 0.f;
-  constexpr int PER = DP / 64;
+  float L = 0.f, R = 0.f;
+  constexpr int PER = DV / 64;
   float acc[PER];
 #pragma unroll
   for (int j = 0; j < PER; ++j) acc[j] = 0.f;
   for (int s = 0; s < a.splits; ++s) {
     const int64_t r = s * stride + rowg;
-    const float ms = a.ws_ml[2 * r], ls = a.ws_ml[2 * r + 1];
+    const float ms = a.ws_ml[MLW * r], ls = a.ws_ml[MLW * r + 1];
     const float f = ms == -INFINITY ? 0.f : exp2f(ms - Mr);
     L += ls * f;
+    if constexpr (FOLD) R += a.ws_ml[MLW * r + 2] * f;
 #pragma unroll
-    for (int j = 0; j < PER; ++j) acc[j] += f * a.ws_o[r * DP + lane * PER + j];
+    for (int j = 0; j < PER; ++j) acc[j] += f * a.ws_o[r * DV + lane * PER + j];
   }
   const float inv = L > 0.f ? 1.f / L : 0.f;
   bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
 #pragma unroll
   for (int j = 0; j < PER; ++j)
-    if (lane * PER + j < a.D) O[lane * PER + j] = (bf16)(acc[j] * inv);
+    if (FOLD || lane * PER + j < a.D) O[lane * PER + j] = (bf16)(acc[j] * inv);
+  if constexpr (FOLD) {
+    if (lane < 8) O[DV + lane] = (bf16)(lane == 0 ? R * inv : 0.f);
+  }
   if (lane == 0) a.lse[rowg] = (Mr + log2f(L)) * FL_LN2;
 }
 
@@ -328,15 +371,15 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
   return (int64_t)splits * B * H * Lq * (DPd + 2) * 4;
 }
 
-template <int DP>
+template <int DP, int DV = DP>
 static int flash_launch(FlashArgs& a, hipStream_t st) {
   dim3 grid((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
-  if (a.p_drop <= 0.f) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE>), grid, dim3(FL_WAVES * 64), 0, st, a);
-  else if (a.keep) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS>), grid, dim3(FL_WAVES * 64), 0, st, a);
-  else hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  if (a.p_drop <= 0.f) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  else if (a.keep) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  else hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV>), grid, dim3(FL_WAVES * 64), 0, st, a);
   if (a.splits > 1)
-    hipLaunchKernelGGL((flash_combine_kernel<DP>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0, st,
-                       a);
+    hipLaunchKernelGGL((flash_combine_kernel<DP, DV>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0,
+                       st, a);
   return (int)hipGetLastError();
 }
 
@@ -378,4 +421,66 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
   if (D == 256) return flash_launch<256>(a, st);
   if (D > 64) return flash_launch<128>(a, st);  // 72..128 (s2h_flash_eligible)
   return flash_launch<64>(a, st);               // 32..64
+}
+
+// ---------------------------------------------------------------------------- V-fold
+// Memory-attention cross-attention with the value projection folded out (header comment):
+// q [B, Lq, 256], k [B, Lk, 256] (RoPE applied), m [B, Lk, 64] (the memory bank rows, the
+// value projection's INPUT), single head -> u [B, Lq, >= 72]: u[:, :, 0:64] = D m,
+// u[:, :, 64] = rowsum(D), u[:, :, 65:72] = 0, lse [B, Lq].  Strides in elements, (batch, row).
+#define VF_D 256
+#define VF_DV 64
+
+extern "C" int64_t s2h_attn_fwd_vfold_ws_bytes(int B, int Lq, int Lk) {
+  int splits, tps;
+  flash_plan(B, Lq, Lk, splits, tps);
+  if (splits <= 1) return 0;
+  return (int64_t)splits * B * Lq * (VF_DV + FL_MLW(true)) * 4;
+}
+
+static bool vf_rows_ok(const void* p, int64_t sb, int64_t sl) {
+  return ((uintptr_t)p & 15) == 0 && (sb & 7) == 0 && (sl & 7) == 0;
+}
+
+extern "C" int s2h_attn_fwd_vfold(int B, int Lq, int Lk, const void* q, int64_t sqb, int64_t sql, const void* k, int64_t skb,
+                       int64_t skl, const void* mem, int64_t smb, int64_t sml, void* u, int64_t sub, int64_t sul,
+                       float* lse, float scale, float p_drop, uint64_t seed, uint64_t idx0, uint32_t* keep, void* ws,
+                       int64_t ws_bytes, hipStream_t st) {
+  if (B <= 0 || Lq <= 0) return 0;
+  if (Lk <= 0 || !s2h_flash_eligible(S2H_BF16, Lq, VF_D) || sul < FL_VFOLD_COLS(VF_DV)) return (int)hipErrorInvalidValue;
+  if (!vf_rows_ok(q, sqb, sql) || !vf_rows_ok(k, skb, skl) || !vf_rows_ok(mem, smb, sml) || !vf_rows_ok(u, sub, sul))
+    return (int)hipErrorInvalidValue;
+  if ((int64_t)Lk * std::max(skl, sml) >= (1ll << 31)) return (int)hipErrorInvalidValue;  // 32-bit DMA offsets
+  FlashArgs a = {};
+  a.idx0 = idx0;
+  a.D = VF_D;
+  a.keep = p_drop > 0.f ? keep : nullptr;
+  a.kw = 2 * ((Lk + 63) / 64);
+  a.pair_ok = ((idx0 | (uint64_t)Lk) & 1) == 0;
+  a.BH = B; a.H = 1; a.Lq = Lq; a.Lk = Lk;
+  a.q = (const bf16*)q; a.sqb = sqb; a.sqh = 0; a.sql = sql;
+  a.k = (const bf16*)k; a.skb = skb; a.skh = 0; a.skl = skl;
+  a.v = (const bf16*)mem; a.svb = smb; a.svh = 0; a.svl = sml;
+  a.o = (bf16*)u; a.sob = sub; a.soh = 0; a.sol = sul;
+  a.lse = lse;
+  a.sl2 = scale * FL_LOG2E;
+  a.p_drop = p_drop;
+  a.thresh = (uint32_t)(p_drop * 4294967296.0);
+  a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed;
+  a.seed_off = s2h_rng_offset_ptr();
+  flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
+  const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (VF_DV + FL_MLW(true)) * 4 : 0;
+  if (need > ws_bytes || (need > 0 && ws == nullptr)) {
+    a.splits = 1;
+    a.tiles_per_split = (Lk + 63) / 64;
+  } else if (a.splits > 1) {
+    a.ws_o = (float*)ws;
+    a.ws_ml = a.ws_o + (int64_t)a.splits * a.BH * Lq * VF_DV;
+  }
+  // profiler record: m4 = 1000 + DV marks the folded value width (bench.py prices 2 (D + DV) per pair)
+  const int slot = s2h_prof_begin(st, 1, (int64_t)B, Lq, Lk, VF_D, 1000 + VF_DV);
+  const int rc = flash_launch<VF_D, VF_DV>(a, st);
+  s2h_prof_end(slot, st);
+  return rc;
 }

@@ -13,6 +13,11 @@
 //          Q / dO tiles of 32 queries streamed by LDS-DMA; S = Q K^T and dP = dO V^T keep
 //          the key on the lane, so P_drop and dS are already the B operands of
 //          dV^T += dO^T P_drop and dK^T += Q^T dS (dO^T / Q^T by transposing reads).
+// V-fold (DV != DP, s2h_flash_bwd_frames_vfold; the forward's flash.hip header): the memory bank M
+// (64 wide) stands in for V = M Wv^T + bv and the upstream gradient arrives as
+// du' = dO [Wv | bv] = [dO Wv | dO . bv] (72 columns): dD = du M^T + dr (dr = du'[:, 64]),
+// Di = rowsum(dO * O) = du . u + dr * rowsum(D) from u' = [D M | rowsum(D)].  No dV: the bank is
+// detached (sam2model.py:345-358) and the value projection's weight gradient is dO^T u'.
 #include "flash_common.h"
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
@@ -99,13 +104,17 @@ __device__ __forceinline__ KvFrame kv_frame(const FlashBwdArgs& a, int bh) {
 enum { DROP_NONE = 0, DROP_BITS = 1, DROP_HASH = 2 };
 
 // ------------------------------------------------------------------ dQ
-template <int DP, int DROP>
+template <int DP, int DROP, int DV = DP>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
+  constexpr bool FOLD = DV != DP;
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   using C = FlashCfg<DP, 64>;
-  using I = PadImg<DP>;  // padded K / V images (the forward's: conflict-free b128 and transposing reads)
+  using I = PadImg<DP>;   // padded K image (the forward's: conflict-free b128 and transposing reads)
+  using IV = PadImg<DV>;  // padded V image (V-fold: memory rows)
+  constexpr int NTV = DV / 32;  // 32-deep d steps of dP
+  constexpr int STG = I::TILEB + IV::TILEB;
   // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * 2 * I::TILEB + 2 * FL_WAVES * 256];
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + 2 * FL_WAVES * 256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
@@ -126,23 +135,29 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   constexpr bool bits = DROP == DROP_BITS;
   const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min(wi.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
                                : nullptr;
-  char* bits_lds = smem + 2 * 2 * I::TILEB + w * 256;
-  const int npw = I::pieces(w);
+  char* bits_lds = smem + 2 * STG + w * 256;
+  const int npw = I::pieces(w), npv = IV::pieces(w);
   auto dma_bits = [&](int stage, int k0) { lds_dma4(KEEPQ + (k0 >> 5) + (lane & 1), bits_lds + stage * FL_WAVES * 256); };
 
   if (nt > 0) {
     dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane, a.D);
-    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane, a.D);
+    dma_tile_pad<DV, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane, FOLD ? DV : a.D);
     if constexpr (bits) dma_bits(0, t0 * C::KT);
   }
   const bool qv = q < a.Lq;
-  bf16x8 qf[C::NT], gf[C::NT];
+  bf16x8 qf[C::NT], gf[NTV];
 #pragma unroll
   for (int t = 0; t < C::NT; ++t) {
     const bool ok = qv && 32 * t + 8 * g < a.D;  // zero past the head dim
     qf[t] = ok ? *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g) : bf16x8{};
+  }
+#pragma unroll
+  for (int t = 0; t < NTV; ++t) {
+    const bool ok = qv && (FOLD || 32 * t + 8 * g < a.D);
     gf[t] = ok ? *(const bf16x8*)(G + (int64_t)q * a.sgl + 32 * t + 8 * g) : bf16x8{};
   }
+  // V-fold: dr = du'[q, DV] (dO . bv), constant over the keys of the row
+  const float dr = FOLD && qv ? (float)G[(int64_t)q * a.sgl + DV] : 0.f;
   const float lse2 = qv ? a.lse[(int64_t)bh * a.Lq + q] * FL_LOG2E : 0.f;
   // Di = rowsum(dO * O) of this lane's query from the dO fragments already in registers and the
   // matching O fragments, reduced over the 4 lanes (g) of the query: replaces a separate
@@ -151,8 +166,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   {
     const bf16* O = a.o + b * a.sob + h * a.soh;
 #pragma unroll
-    for (int t = 0; t < C::NT; ++t) {
-      if (qv && 32 * t + 8 * g < a.D) {
+    for (int t = 0; t < NTV; ++t) {
+      if (qv && (FOLD || 32 * t + 8 * g < a.D)) {
         const bf16x8 of = *(const bf16x8*)(O + (int64_t)q * a.sol + 32 * t + 8 * g);
 #pragma unroll
         for (int j = 0; j < 8; ++j) di += (float)gf[t][j] * (float)of[j];
@@ -160,6 +175,9 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     }
     di += __shfl_xor(di, 16, 64);
     di += __shfl_xor(di, 32, 64);
+    if constexpr (FOLD) {  // + dr * rowsum(D)
+      if (qv) di += dr * (float)O[(int64_t)q * a.sol + DV];
+    }
   }
   // compiler-visible vmcnt(0): the compiler's own bookkeeping retires these loads here instead
   // of waiting vmcnt(0) inside the key loop (which would also drain the asm K/V prefetch)
@@ -172,19 +190,18 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
 
   for (int it = 0; it < nt; ++it) {
     const int k0 = (t0 + it) * C::KT;
-    char* Kb = smem + (it & 1) * 2 * I::TILEB;
+    char* Kb = smem + (it & 1) * STG;
     char* Vb = Kb + I::TILEB;
     if (it + 1 < nt) {
-      char* Kn = smem + ((it + 1) & 1) * 2 * I::TILEB;
+      char* Kn = smem + ((it + 1) & 1) * STG;
       dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane, a.D);
-      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane, a.D);
+      dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane, FOLD ? DV : a.D);
       // this wave's pieces of tile `it` have landed once all but the ones just issued retired
       if constexpr (bits) {
         dma_bits((it + 1) & 1, k0 + C::KT);
-        if (npw > I::PPW_LO) wait_vmcnt<2 * (I::PPW_LO + 1) + 1>();
-        else wait_vmcnt<2 * I::PPW_LO + 1>();
+        wait_kv_pieces<I::PPW_LO + 1, IV::PPW_LO>(npw + 1, npv);
       } else {
-        wait_vmcnt_pieces<2, I::PPW_LO>(npw);
+        wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
       }
     } else {
       wait_vmcnt<0>();
@@ -201,8 +218,10 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       for (int t = 0; t < C::NT; ++t) {
         const bf16x8 kf = *(const bf16x8*)(Kb + row * I::ROWB + 16 * (4 * t + g));
         s[kb] = mfma16(kf, qf[t], s[kb]);
-        const bf16x8 vf = *(const bf16x8*)(Vb + row * I::ROWB + 16 * (4 * t + g));
-        dp[kb] = mfma16(vf, gf[t], dp[kb]);
+        if (t < NTV) {
+          const bf16x8 vf = *(const bf16x8*)(Vb + row * IV::ROWB + 16 * (4 * t + g));
+          dp[kb] = mfma16(vf, gf[t], dp[kb]);
+        }
       }
     }
     const bool full = k0 + C::KT <= Lk;
@@ -233,10 +252,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       for (int r = 0; r < 4; ++r) {
         float p = __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2);
         if (!full) p = (k0 + kb * 16 + 4 * g + r < Lk) ? p : 0.f;  // wave-uniform test, then a select
+        const float dpr = FOLD ? dp[kb][r] + dr : dp[kb][r];
         if constexpr (DROP == DROP_NONE) {
-          s[kb][r] = p * (dp[kb][r] - di);  // dS (scale applied at the end)
+          s[kb][r] = p * (dpr - di);  // dS (scale applied at the end)
         } else {
-          const float dpd = kp[r] ? dp[kb][r] : 0.f;
+          const float dpd = kp[r] ? dpr : 0.f;
           s[kb][r] = p * fmaf(dpd, a.inv_keep, -di);
         }
       }
@@ -442,16 +462,20 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
 // KREG: K fragments held in registers like V (64 more VGPRs, no K block in LDS): the S / dP
 // phase re-read the constant K block from LDS every 32-query tile -- a third of that phase's
 // LDS traffic, and the phase is LDS-bandwidth-bound (4 waves x 48 b128 reads against 32 MFMAs).
-template <int DP, int DROP, bool KREG = true>
+template <int DP, int DROP, bool KREG = true, int DV = DP>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a) {
+  constexpr bool FOLD = DV != DP;  // V-fold: dO tile = du' (DV wide + dr), no dV
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   constexpr int NWV = 4, QT = 32;
   using C = FlashCfg<DP, QT, NWV>;
-  constexpr int NT = DP / 16, ND = DP / 32;
+  using CG = FlashCfg<DV, QT, NWV>;  // dO (du') tile
+  constexpr int SWG = DV >= 128 ? 1 : 0;
+  constexpr int NT = DP / 16, ND = DP / 32, NTV = DV / 16;
   // [K block: 128 keys (!KREG)][stage][Q | dO] + [stage][wave][lse(32) | Di(32)] (each wave DMAs
   // its own copy of the row constants).  V (and with KREG, K) live in registers.
   using CK = FlashCfg<DP, NWV * 32, NWV>;
-  constexpr int STAGE = 2 * C::TILEB + NWV * 512;  // + per wave [lse | Di | keep words (x2)]
+  constexpr int RWB = FOLD ? 768 : 512;  // per wave [lse | Di | keep words (x2) | dr words (x2, V-fold)]
+  constexpr int STAGE = C::TILEB + CG::TILEB + NWV * RWB;
   constexpr int KBLK = KREG ? 0 : CK::TILEB;
   __shared__ __attribute__((aligned(1024))) char smem[KBLK + 2 * STAGE];
   char* Kblk = smem;
@@ -480,24 +504,29 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   auto dma_rows = [&](char* stage, int q0) {
     const int qi = min(q0 + (lane & 31), a.Lq - 1);
     const float* src = (lane < 32 ? LSE : DI) + qi;
-    lds_dma4(src, stage + 2 * C::TILEB + w * 512);
+    lds_dma4(src, stage + C::TILEB + CG::TILEB + w * RWB);
   };
   // keep words of this wave's 32 keys (word key / 32) for the 32 queries of a tile (lanes 32..63
   // repeat lanes 0..31)
   constexpr bool bits = DROP == DROP_BITS;
   const uint32_t* KEEPW = bits ? fr.keep + min(wi.x * NWV + w, fr.kw - 1) : nullptr;
   auto dma_bits = [&](char* stage, int q0) {
-    lds_dma4(KEEPW + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * fr.kw, stage + 2 * C::TILEB + w * 512 + 256);
+    lds_dma4(KEEPW + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * fr.kw, stage + C::TILEB + CG::TILEB + w * RWB + 256);
+  };
+  // V-fold: dr of the tile's 32 queries = du'[q, DV] (bf16, read as the word of columns DV, DV + 1)
+  auto dma_dr = [&](char* stage, int q0) {
+    lds_dma4(G + (int64_t)min(q0 + (lane & 31), a.Lq - 1) * a.sgl + DV, stage + C::TILEB + CG::TILEB + w * RWB + 512);
   };
   if constexpr (!KREG) dma_tile<DP, NWV * 32, NWV, true, 1>(Kblk, K, a.skl, wi.x * (NWV * 32), fr.Lk, w, lane);
   dma_tile<DP, QT, NWV, true, 1>(stages, Q, a.sql, qbase, a.Lq, w, lane);
-  dma_tile<DP, QT, NWV, true, 1>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
+  dma_tile<DV, QT, NWV, true, SWG>(stages + C::TILEB, G, a.sgl, qbase, a.Lq, w, lane);
   dma_rows(stages, qbase);
   if constexpr (bits) dma_bits(stages, qbase);
-  bf16x8 vf[NT];  // B operand V^T: [k = d = 16t + 8hi + j][n = key]
+  if constexpr (FOLD) dma_dr(stages, qbase);
+  bf16x8 vf[NTV];  // B operand V^T (V-fold: M^T): [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
-  for (int t = 0; t < NT; ++t) vf[t] = *(const bf16x8*)(V + vkey * a.svl + 16 * t + 8 * hi);
+  for (int t = 0; t < NTV; ++t) vf[t] = *(const bf16x8*)(V + vkey * a.svl + 16 * t + 8 * hi);
   bf16x8 kf[KREG ? NT : 1];  // B operand K^T of S = Q K^T: [k = d = 16t + 8hi + j][n = key]
   if constexpr (KREG) {
 #pragma unroll
@@ -505,29 +534,28 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   }
   __builtin_amdgcn_s_waitcnt(0xF70);  // retire the V (K) loads in the compiler's bookkeeping (see dq)
   const int krow = w * 32 + kl;  // this lane's key row in the K block
-  f32x16 dk[ND], dv[ND];  // dK^T / dV^T: row d = 32*db + 8(r>>2) + 4hi + (r&3), column key
+  constexpr int NDV = FOLD ? 1 : ND;
+  f32x16 dk[ND], dv[NDV];  // dK^T / dV^T: row d = 32*db + 8(r>>2) + 4hi + (r&3), column key
 #pragma unroll
-  for (int d = 0; d < ND; ++d) {
-    dk[d] = f32x16{};
-    dv[d] = f32x16{};
-  }
+  for (int d = 0; d < ND; ++d) dk[d] = f32x16{};
+#pragma unroll
+  for (int d = 0; d < NDV; ++d) dv[d] = f32x16{};
   for (int it = 0; it < nt; ++it) {
     const int q0 = qbase + it * QT;
     char* Qb = stages + (it & 1) * STAGE;
     char* Gb = Qb + C::TILEB;
-    const float* rows = (const float*)(Qb + 2 * C::TILEB + w * 512);  // [lse(32) | Di(32) | keep(32)]
+    // [lse(32) | Di(32) | keep(32) | - | dr words(32) | -]
+    const float* rows = (const float*)(Qb + C::TILEB + CG::TILEB + w * RWB);
     const uint32_t* kwd = (const uint32_t*)(rows + 64);
+    const uint32_t* drw = (const uint32_t*)(rows + 128);
     if (it + 1 < nt) {
       char* Qn = stages + ((it + 1) & 1) * STAGE;
       dma_tile<DP, QT, NWV, true, 1>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
-      dma_tile<DP, QT, NWV, true, 1>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
+      dma_tile<DV, QT, NWV, true, SWG>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
       dma_rows(Qn, q0 + QT);
-      if constexpr (bits) {
-        dma_bits(Qn, q0 + QT);
-        wait_vmcnt<2 * C::PPW + 2>();
-      } else {
-        wait_vmcnt<2 * C::PPW + 1>();
-      }
+      if constexpr (bits) dma_bits(Qn, q0 + QT);
+      if constexpr (FOLD) dma_dr(Qn, q0 + QT);
+      wait_vmcnt<C::PPW + CG::PPW + 1 + (bits ? 1 : 0) + (FOLD ? 1 : 0)>();
     } else {
       wait_vmcnt<0>();
     }
@@ -543,8 +571,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
         const bf16x8 kb = *(const bf16x8*)(Kblk + swz<DP, 1>(krow, 2 * t + hi));
         s = mfma32(qa, kb, s);
       }
-      const bf16x8 ga = *(const bf16x8*)(Gb + swz<DP, 1>(kl, 2 * t + hi));
-      dp = mfma32(ga, vf[t], dp);
+      if (t < NTV) {
+        const bf16x8 ga = *(const bf16x8*)(Gb + swz<DV, SWG>(kl, 2 * t + hi));
+        dp = mfma32(ga, vf[t], dp);
+      }
       if ((t & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound the fragment prefetch depth
     }
     bf16x8 pdb[2], dsb[2];  // 16-query steps c: k index 8hi + j <-> r = 8c + j
@@ -556,6 +586,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       const float lse_r = rows[ql], di_r = rows[32 + ql];
       float p = __builtin_amdgcn_exp2f(fmaf(s[r], a.sl2, -lse_r * FL_LOG2E));
       if (!qfull) p = qi < a.Lq ? p : 0.f;  // wave-uniform test, then a select
+      if constexpr (FOLD) dp[r] += __uint_as_float(drw[ql] << 16);  // + dr (bf16 in the low half)
       if constexpr (DROP == DROP_NONE) {
         pdb[r >> 3][r & 7] = (bf16)p;
         dsb[r >> 3][r & 7] = (bf16)(p * (dp[r] - di_r));
@@ -574,7 +605,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int d = 0; d < ND; ++d) {
-        dv[d] = mfma32(tr_frag_perm32<DP, 1>(Gb, 16 * c, 32 * d, lane), pdb[c], dv[d]);
+        if constexpr (!FOLD) dv[d] = mfma32(tr_frag_perm32<DP, 1>(Gb, 16 * c, 32 * d, lane), pdb[c], dv[d]);
         dk[d] = mfma32(tr_frag_perm32<DP, 1>(Qb, 16 * c, 32 * d, lane), dsb[c], dk[d]);
         if (d & 1) __builtin_amdgcn_sched_barrier(0);
       }
@@ -583,7 +614,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   }
 
   if (!kv) return;
-  if (a.kv_splits > 1) {  // fp32 partials, summed (and scaled, cast) by flash_bwd_dkv_combine_kernel
+  if (!FOLD && a.kv_splits > 1) {  // fp32 partials, summed (and scaled, cast) by flash_bwd_dkv_combine_kernel
     float* W = a.ws_dkv + (((int64_t)wi.z * a.BH + bh) * a.Lk + key) * 2 * DP;  // single-frame only
 #pragma unroll
     for (int d = 0; d < ND; ++d)
@@ -591,26 +622,28 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
       for (int G4 = 0; G4 < 4; ++G4) {
         const int d0 = 32 * d + 8 * G4 + 4 * hi;
         *(float4*)(W + d0) = float4{dk[d][4 * G4], dk[d][4 * G4 + 1], dk[d][4 * G4 + 2], dk[d][4 * G4 + 3]};
-        *(float4*)(W + DP + d0) = float4{dv[d][4 * G4] * a.inv_keep, dv[d][4 * G4 + 1] * a.inv_keep,
-                                         dv[d][4 * G4 + 2] * a.inv_keep, dv[d][4 * G4 + 3] * a.inv_keep};
+        const int dvd = FOLD ? 0 : d;
+        *(float4*)(W + DP + d0) = float4{dv[dvd][4 * G4] * a.inv_keep, dv[dvd][4 * G4 + 1] * a.inv_keep,
+                                         dv[dvd][4 * G4 + 2] * a.inv_keep, dv[dvd][4 * G4 + 3] * a.inv_keep};
       }
     return;
   }
   bf16* DK = fr.dk + (int64_t)key * a.sdkl;
-  bf16* DV = fr.dv + (int64_t)key * a.sdvl;
+  bf16* DVp = FOLD ? nullptr : fr.dv + (int64_t)key * a.sdvl;
 #pragma unroll
   for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int G4 = 0; G4 < 4; ++G4) {
       bf16 tk[4], tv[4];
+      const int dvd = FOLD ? 0 : d;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         tk[e] = (bf16)(dk[d][4 * G4 + e] * a.scale);
-        tv[e] = (bf16)(dv[d][4 * G4 + e] * a.inv_keep);
+        tv[e] = (bf16)(dv[dvd][4 * G4 + e] * a.inv_keep);
       }
       const int d0 = 32 * d + 8 * G4 + 4 * hi;
       *(uint2*)(DK + d0) = *(const uint2*)tk;
-      *(uint2*)(DV + d0) = *(const uint2*)tv;
+      if constexpr (!FOLD) *(uint2*)(DVp + d0) = *(const uint2*)tv;
     }
 }
 
@@ -673,28 +706,28 @@ int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D) {
   return dq_bytes + dkv_bytes;
 }
 
-template <int DP>
+template <int DP, int DV = DP>
 static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.BH * a.Lq;
   // Di = rowsum(dO * O) is computed by the dQ kernel and stored for the dK / dV kernel
   const int drop = a.p_drop <= 0.f ? DROP_NONE : (a.keep ? DROP_BITS : DROP_HASH);
   const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
-  if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE>), gq, dim3(FL_WAVES * 64), 0, st, a);
-  else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS>), gq, dim3(FL_WAVES * 64), 0, st, a);
-  else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_bwd_dq_combine_kernel<DP>), dim3((unsigned)((rows * DP / 4 + 255) / 256)), dim3(256), 0,
                        st, a);
   if constexpr (DP == 256) {
     const dim3 gk((a.Lk + 127) / 128, pad_bh8(a.BH), a.kv_splits);
-    if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE>), gk, dim3(256), 0, st, a);
-    else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS>), gk, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH>), gk, dim3(256), 0, st, a);
-    if (a.kv_splits > 1) {
+    if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV>), gk, dim3(256), 0, st, a);
+    else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV>), gk, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH, true, DV>), gk, dim3(256), 0, st, a);
+    if (DV == DP && a.kv_splits > 1) {
       const int64_t n4 = (int64_t)a.BH * a.Lk * 2 * DP / 4;
       hipLaunchKernelGGL((flash_bwd_dkv_combine_kernel<DP>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
     }
-  } else {
+  } else if constexpr (DV == DP) {
     const dim3 gk((a.Lk + FL_QB - 1) / FL_QB, pad_bh8(a.BH));
     if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP, DROP_NONE>), gk, dim3(FL_WAVES * 64), 0, st, a);
     else hipLaunchKernelGGL((flash_bwd_dkv_kernel<DP, DROP_HASH>), gk, dim3(FL_WAVES * 64), 0, st, a);
@@ -824,3 +857,64 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
 // the frame-batched backward's domain for the host (bf16, head_dim 256 or 32..128, >= 128 query
 // rows, flash path not switched off by s2h_attn_config)
 extern "C" int s2h_flash_bwd_ok(int dt, int Lq, int D) { return s2h_flash_bwd_eligible(dt, Lq, D); }
+
+// V-fold frame-batched backward (header comment; the forward is s2h_attn_fwd_vfold): single head,
+// q / u / du / dq [nfr * bpf, Lq, ...] uniform (batch, row strides), k / m / dk PACKED per frame
+// like s2h_flash_bwd_frames (row strides), u / du rows of >= 72 columns; no dV (the memory is
+// detached).  Di is computed by the dQ kernel into di_ws [nfr * bpf * Lq].
+extern "C" int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
+                                          const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql,
+                                          const void* k, int64_t skl, const void* mem, int64_t sml, const void* u,
+                                          int64_t sub, int64_t sul, const void* du, int64_t sgb, int64_t sgl, void* dq,
+                                          int64_t sdqb, int64_t sdql, void* dk, int64_t sdkl, const float* lse,
+                                          float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
+                                          const int64_t* fr_koff, hipStream_t st) {
+  constexpr int D = 256, DV = 64;
+  if (nfr <= 0 || bpf <= 0 || Lq <= 0) return 0;
+  if (nfr > S2H_MAX_FRAMES || !s2h_flash_bwd_eligible(S2H_BF16, Lq, D)) return (int)hipErrorInvalidValue;
+  if (keep && fr_koff == nullptr) return (int)hipErrorInvalidValue;
+  if (sul < DV + 8 || sgl < DV + 8) return (int)hipErrorInvalidValue;
+  auto rows_ok = [](const void* p, int64_t sb, int64_t sl) {
+    return ((uintptr_t)p & 15) == 0 && (sb & 7) == 0 && (sl & 7) == 0;
+  };
+  if (!rows_ok(q, sqb, sql) || !rows_ok(k, 0, skl) || !rows_ok(mem, 0, sml) || !rows_ok(u, sub, sul) ||
+      !rows_ok(du, sgb, sgl) || !rows_ok(dq, sdqb, sdql) || !rows_ok(dk, 0, sdkl))
+    return (int)hipErrorInvalidValue;
+  FlashBwdArgs a = {};
+  a.D = D;
+  a.nfr = nfr; a.bpf = bpf;
+  a.keep = keep;
+  int lk_max = 0;
+  if ((int64_t)Lq * std::max(sql, sgl) >= (1ll << 31)) return (int)hipErrorInvalidValue;  // 32-bit DMA offsets
+  for (int f = 0; f < nfr; ++f) {
+    if (fr_lk[f] <= 0 || (int64_t)fr_lk[f] * std::max(skl, sml) >= (1ll << 31)) return (int)hipErrorInvalidValue;
+    a.fr_lk[f] = fr_lk[f]; a.fr_krow[f] = fr_krow[f]; a.fr_idx0[f] = fr_idx0[f];
+    a.fr_koff[f] = keep ? fr_koff[f] : 0;
+    lk_max = std::max(lk_max, fr_lk[f]);
+  }
+  a.BH = nfr * bpf; a.H = 1; a.Lq = Lq; a.Lk = lk_max;
+  a.q = (const bf16*)q; a.sqb = sqb; a.sqh = 0; a.sql = sql;
+  a.k = (const bf16*)k; a.skh = 0; a.skl = skl;
+  a.v = (const bf16*)mem; a.svh = 0; a.svl = sml;
+  a.o = (const bf16*)u; a.sob = sub; a.soh = 0; a.sol = sul;
+  a.g = (const bf16*)du; a.sgb = sgb; a.sgh = 0; a.sgl = sgl;
+  a.dq = (bf16*)dq; a.sdqb = sdqb; a.sdqh = 0; a.sdql = sdql;
+  a.dk = (bf16*)dk; a.sdkh = 0; a.sdkl = sdkl;
+  a.dv = nullptr;
+  a.lse = lse; a.di = di_ws;
+  a.scale = scale; a.sl2 = scale * FL_LOG2E;
+  a.p_drop = p_drop;
+  a.thresh = (uint32_t)(p_drop * 4294967296.0);
+  a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
+  a.seed = seed;
+  a.seed_off = s2h_rng_offset_ptr();
+  a.splits = 1; a.tiles_per_split = (lk_max + 63) / 64;
+  a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32;
+  int64_t lk_sum = 0;
+  for (int f = 0; f < nfr; ++f) lk_sum += fr_lk[f];
+  // profiler record: m4 = 1000 + DV (bench.py prices 2 (2 D + DV) per pair: dP over DV, dQ, dK)
+  const int slot = s2h_prof_begin(st, 2, (int64_t)bpf, Lq, lk_sum, D, 1000 + DV);
+  const int rc = flash_bwd_launch<D, DV>(a, st);
+  s2h_prof_end(slot, st);
+  return rc;
+}

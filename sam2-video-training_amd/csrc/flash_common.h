@@ -164,6 +164,19 @@ __device__ __forceinline__ void wait_vmcnt_pieces(int n) {
   else wait_vmcnt<M * LO>();
 }
 
+// vmcnt wait that leaves the K and V pieces of the next tile in flight (nk in {LOK, LOK + 1},
+// nv in {LOV, LOV + 1}, wave-uniform)
+template <int LOK, int LOV>
+__device__ __forceinline__ void wait_kv_pieces(int nk, int nv) {
+  if (nk > LOK) {
+    if (nv > LOV) wait_vmcnt<LOK + LOV + 2>();
+    else wait_vmcnt<LOK + LOV + 1>();
+  } else {
+    if (nv > LOV) wait_vmcnt<LOK + LOV + 1>();
+    else wait_vmcnt<LOK + LOV>();
+  }
+}
+
 __device__ __forceinline__ void wg_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");

@@ -47,6 +47,12 @@ SIGNATURES = {
     "s2h_flash_bwd_ok": [I, I, I],
     "s2h_flash_bwd_frames": [I, I, I, I, I, P, P, P, P, L, L, L, P, L, L, P, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
                              P, L, L, P, L, L, P, P, F, F, c_uint64, P, P, P],
+    "s2h_attn_fwd_vfold_ws_bytes": [I, I, I],
+    "s2h_attn_fwd_vfold": [I, I, I, P, L, L, P, L, L, P, L, L, P, L, L, P, F, F, c_uint64, c_uint64, P, P, L, P],
+    "s2h_flash_bwd_frames_vfold": [I, I, I, P, P, P, P, L, L, P, L, P, L, P, L, L, P, L, L, P, L, L, P, L, P, P, F, F,
+                                   c_uint64, P, P, P],
+    "s2h_vfold_weight": [I, I, I, P, P, P, P],
+    "s2h_vfold_grad": [I, I, I, P, P, P, P],
     "s2h_layernorm_fwd": [I, I, I, P, L, P, L, I, P, P, P, F, P, L, P, P, P],
     "s2h_layernorm_bwd_ws_bytes": [I, I, I],
     "s2h_layernorm_bwd": [I, I, I, P, L, P, L, P, P, P, P, L, I, P, L, P, P, P, P],
@@ -104,6 +110,7 @@ _LIB = None
 
 # entry points that do not return a hipError_t
 RESTYPES = {"s2h_attn_fwd_ws_bytes": c_int64, "s2h_attn_bwd_ws_bytes": c_int64, "s2h_attn_keep_words": c_int64,
+            "s2h_attn_fwd_vfold_ws_bytes": c_int64,
             "s2h_layernorm_bwd_ws_bytes": c_int64}
 
 

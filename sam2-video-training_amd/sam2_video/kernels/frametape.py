@@ -423,8 +423,11 @@ def _linear_bw(tape, op, gys):
     else:
         dpre = gy2
     x2 = _flat(tape.st(op.ins[0]), K)
+    wgrad = getattr(mod, "wgrad", None)
     gw, gb = mod.grad_views()
-    if gw is not None:
+    if wgrad is not None:  # a derived weight (functional.VFoldProj) scatters its own gradient
+        wgrad(dpre, x2)
+    elif gw is not None:
         ops.linear_wgrad(dpre, x2, gw.view(gw.shape[0], -1), db=gb)
     elif gb is not None:
         ops.colsum(dpre, gb)
@@ -557,6 +560,47 @@ def _attn_bw(tape, op, gys):
     _attn_frames_bwd(tape, op, q_all, k_st, v_st, (rows(k_st.buf), rows(v_st.buf), rows(dk), rows(dv)), o_all, go,
                      lse, dq, dk, dv)
     return [dq.view(-1), dk, dv]
+
+
+def attention_vfold(tape: FrameTape, q, k, mem, scale, p_drop):
+    """the folded cross-attention (functional.attention_vfold): q [B, Lq, 1, 256], k [B, Lk, 1, 256],
+    mem [B, Lk, 1, 64] views of recorded values -> u' [B, Lq, 1, 72]"""
+    op, first = tape._begin("attn_vfold", [q, k, mem], _attn_vfold_bw, {"scale": scale, "p": p_drop})
+    B, Lq = q.shape[0], q.shape[1]
+    Lk = k.shape[1]
+    vid, u = tape._out(0, (B, Lq, 1, ops.VFOLD_COLS), q.dtype)
+    lse = tape._aux("lse", (B, 1, Lq), torch.float32)
+    seed = tape._seed() if p_drop > 0 else 0
+    idx0 = tape._idx0(op, B * Lq * Lk)
+    keep = tape._keep_bits(q, Lk, op.ins[1], p_drop)
+    ops.attn_fwd_vfold(q, k, mem, u, lse, scale, p_drop, seed, idx0=idx0, keep=keep)
+    tape._fattr(op, "Lk", Lk)
+    if first:
+        op.attrs.update(seed=seed, B=B, Lq=Lq, D=q.shape[-1], keep=keep is not None)
+    tape._finish(op, [vid], any(op.needs))
+    return u
+
+
+def _attn_vfold_bw(tape, op, gys):
+    (gu,) = gys
+    a = op.attrs
+    F, B, Lq, D = tape.F, a["B"], a["Lq"], a["D"]
+    q_st, k_st, m_st = (tape.st(v) for v in op.ins)
+    q_all = q_st.buf.view(F * B, Lq, 1, D)
+    u_all = tape.st(op.outs[0]).buf.view(F * B, Lq, 1, ops.VFOLD_COLS)
+    gu = gu.contiguous().view(F * B, Lq, 1, ops.VFOLD_COLS)
+    lse = tape.stores[("aux", op.idx, "lse")].buf.view(F * B, 1, Lq)
+    dq = torch.empty_like(q_all)
+    dk = torch.empty(k_st.buf.numel(), device=gu.device, dtype=gu.dtype)
+    lks = op.fattrs["Lk"]
+    krow = [0]
+    for f in range(F - 1):
+        krow.append(krow[-1] + B * lks[f])
+    ks = tape.stores[("aux", op.idx, "keep")] if a.get("keep") else None
+    ops.flash_bwd_frames_vfold(F, B, lks, krow, op.fattrs["idx0"], q_all, k_st.buf.view(-1, 1, D),
+                               m_st.buf.view(-1, 1, ops.VFOLD_DV), u_all, gu, lse, dq, dk.view(-1, 1, D), a["scale"],
+                               a["p"], a["seed"], keep=ks.buf if ks else None, koff=ks.offsets if ks else None)
+    return [dq.view(-1), dk, None]
 
 
 def qkv_attention(tape: FrameTape, qkv, scale, p_drop, rope):

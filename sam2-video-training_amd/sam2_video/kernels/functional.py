@@ -32,6 +32,16 @@ def set_seed(s):
     _SEED[0] = int(s) & (2**64 - 1)
 
 
+# weight generation: bumped once per step (SAM2Model.forward_image); weights derived from the
+# arena (the folded value projection) are rebuilt on their first use in a new generation -- inside
+# the step, so a captured graph rebuilds them on every replay
+_GEN = [0]
+
+
+def new_step():
+    _GEN[0] += 1
+
+
 def _compute_weight(mod):
     """a Linear / Conv2d module's weight in the compute dtype as a [out, in*k*k] matrix"""
     return mod.weight._s2h_compute.reshape(mod.weight.shape[0], -1)
@@ -68,8 +78,11 @@ class _Linear(torch.autograd.Function):
             dpre = ops.act_dropout_bwd(pre if ctx.act else None, dy, ctx.act, ctx.drop_p, ctx.seed)
         else:
             dpre = ops.act_bwd(pre, dy, ctx.act) if ctx.act else dy
+        wgrad = getattr(mod, "wgrad", None)
         gw, gb = mod.grad_views()
-        if gw is not None:
+        if wgrad is not None:
+            wgrad(dpre, x)
+        elif gw is not None:
             ops.linear_wgrad(dpre, x, gw.view(gw.shape[0], -1), db=gb)
         elif gb is not None:
             ops.colsum(dpre, gb)
@@ -210,6 +223,93 @@ class _Attention(torch.autograd.Function):
         ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, ctx.scale, ctx.p, ctx.seed, keep=ctx.keep)
         ctx.keep = None
         return dq, dk, dv, None, None
+
+
+class VFoldProj:
+    """The value projection of a folded cross-attention (ops.attn_fwd_vfold) as the weight of ONE
+    GEMM: O = u' [Wv | bv | 0]^T over u' = [D M | rowsum(D) | 0] (72 columns), which equals
+    D (M Wv^T + bv) -- the reference's v_proj followed by the attention's P V
+    (transformer.py:296-307).  The [N, 72] bf16 weight is rebuilt from the arena on first use in
+    each step (new_step); its fp32 gradient dO^T u' is scattered back into the Linear's own weight
+    and bias gradients (`wgrad`, called by the linear backward in place of grad_views)."""
+
+    def __init__(self, lin):
+        self.lin = lin
+        self.weight, self.bias = lin.weight, lin.bias  # autograd anchors (the Linear's parameters)
+        self.out_features, self.in_features = lin.out_features, ops.VFOLD_COLS
+        self._w = None
+        self._g = None
+        self._gen = -1
+
+    def compute_weight(self):
+        if self._gen != _GEN[0]:
+            self._w = ops.vfold_weight(self.lin.compute_weight(), self.lin.bias.detach(), out=self._w)
+            self._gen = _GEN[0]
+        return self._w
+
+    def compute_bias(self):
+        return None
+
+    def grad_views(self):
+        return None, None
+
+    def wgrad(self, dy, x):
+        gw, gb = _grad_of(self.lin.weight), _grad_of(self.lin.bias)
+        if gw is None and gb is None:
+            return
+        if self._g is None:
+            self._g = torch.empty(self.out_features, self.in_features, device=dy.device, dtype=torch.float32)
+        ops.linear_wgrad(dy, x, self._g, accumulate=False)
+        ops.vfold_grad(self._g, gw, gb)
+
+
+def vfold_enabled():
+    """S2H_VFOLD=0 keeps the unfolded value projection + attention (A/B measurements)"""
+    import os
+    return os.environ.get("S2H_VFOLD", "1") != "0"
+
+
+class _AttentionVFold(torch.autograd.Function):
+    """u' = [D M | rowsum(D) | 0] of the folded cross-attention (ops.attn_fwd_vfold); backward:
+    the frame-batched V-fold flash backward with one frame.  The memory M is detached (no dM)."""
+
+    @staticmethod
+    def forward(ctx, q, k, mem, scale, p_drop):
+        B, Lq = q.shape[0], q.shape[1]
+        Lk = k.shape[1]
+        u = torch.empty(B, Lq, 1, ops.VFOLD_COLS, device=q.device, dtype=q.dtype)
+        lse = torch.empty(B, 1, Lq, device=q.device, dtype=torch.float32)
+        seed = next_seed() if p_drop > 0 else 0
+        keep = _keep_buffer(ctx, q, Lk, p_drop, 2)
+        ops.attn_fwd_vfold(q, k, mem, u, lse, scale, p_drop, seed, keep=keep)
+        ctx.scale, ctx.p, ctx.seed, ctx.keep = scale, p_drop, seed, keep
+        ctx.save_for_backward(q, k, mem, u, lse)
+        return u
+
+    @staticmethod
+    def backward(ctx, du):
+        q, k, mem, u, lse = ctx.saved_tensors
+        B, Lq, _, D = q.shape
+        Lk = k.shape[1]
+        dq = torch.empty(q.shape, device=q.device, dtype=q.dtype)
+        dk = torch.empty(B * Lk, 1, D, device=k.device, dtype=k.dtype)
+        ops.flash_bwd_frames_vfold(1, B, [Lk], [0], [0], q, k.reshape(B * Lk, 1, D), mem.reshape(B * Lk, 1, -1), u,
+                                   du.contiguous(), lse, dq, dk, ctx.scale, ctx.p, ctx.seed, keep=ctx.keep,
+                                   koff=[0] if ctx.keep is not None else None)
+        ctx.keep = None
+        return dq, dk.view(k.shape), None, None, None
+
+
+def attention_vfold(q, k, mem, scale=None, p_drop=0.0):
+    """u' = [D mem | rowsum(D) | 0] with D = dropout(softmax(scale q k^T)): q [B, Lq, 1, 256], k
+    [B, Lk, 1, 256], mem [B, Lk, 1, 64] -> [B, Lq, 1, 72] (the folded cross-attention; VFoldProj
+    finishes it)"""
+    if scale is None:
+        scale = 1.0 / math.sqrt(q.shape[-1])
+    T = _ft.active()
+    if T is not None:
+        return _ft.attention_vfold(T, q, k, mem, float(scale), float(p_drop))
+    return _AttentionVFold.apply(q, k.contiguous(), mem.contiguous(), float(scale), float(p_drop))
 
 
 def attention(q, k, v, scale=None, p_drop=0.0):

@@ -257,6 +257,84 @@ def attn_fwd(q, k, v, o, lse, scale, p_drop=0.0, seed=0, idx0=0, keep=None):
     return o, lse
 
 
+VFOLD_DV, VFOLD_COLS = 64, 72  # memory channels; columns of u' = [D M | rowsum(D) | 0 x 7]
+
+
+def vfold_ok(q, mem):
+    """the folded cross-attention's domain: bf16, one head of dim 256 (q [B, Lq, 1, 256]), 64-channel
+    memory, flash-eligible query count"""
+    return (q.dtype == torch.bfloat16 and q.shape[-1] == 256 and q.shape[-2] == 1 and mem.shape[-1] == VFOLD_DV
+            and bool(lib().s2h_flash_bwd_ok(BF16, q.shape[1], 256)))
+
+
+def _brs(t):
+    """(batch, row) strides of a [B, L, (1,) C] view with contiguous channels"""
+    assert t.stride(-1) == 1
+    return t.stride(0), t.stride(1)
+
+
+def attn_fwd_vfold(q, k, mem, u, lse, scale, p_drop=0.0, seed=0, idx0=0, keep=None):
+    """q [B, Lq, 1, 256], k [B, Lk, 1, 256], mem [B, Lk, 1, 64] -> u [B, Lq, 1, 72] (u' = [D mem |
+    rowsum(D) | 0]), lse [B, 1, Lq] (s2h_attn_fwd_vfold); keep as attn_fwd"""
+    _dev(q, k, mem, u, lse)
+    B, Lq = q.shape[0], q.shape[1]
+    Lk = k.shape[1]
+    nws = lib().s2h_attn_fwd_vfold_ws_bytes(B, Lq, Lk)
+    ws = torch.empty(nws, device=q.device, dtype=torch.uint8) if nws > 0 else None
+    call("s2h_attn_fwd_vfold", B, Lq, Lk, ptr(q), *_brs(q), ptr(k), *_brs(k), ptr(mem), *_brs(mem), ptr(u),
+         *_brs(u), ptr(lse), float(scale), float(p_drop), int(seed) & (2**64 - 1), int(idx0),
+         _keep_ptr(keep, B, 1, Lq, Lk), ptr(ws), int(nws), stream())
+    return u, lse
+
+
+def flash_bwd_frames_vfold(nfr, bpf, lk, krow, idx0, q, k, mem, u, du, lse, dq, dk, scale, p_drop, seed, keep=None,
+                           koff=None):
+    """Frame-batched backward of attn_fwd_vfold (s2h_flash_bwd_frames_vfold): q / u / du / dq
+    [nfr*bpf, Lq, 1, C] views, k / mem / dk PACKED [rows, 1, C] (frame f: bpf blocks of lk[f] rows
+    from row krow[f]); keep / koff as flash_bwd_frames"""
+    import ctypes
+    _dev(q, k, mem, u, du, lse, dq, dk)
+    B, Lq = q.shape[0], q.shape[1]
+    assert B == nfr * bpf and len(lk) == nfr == len(krow) == len(idx0)
+    di = torch.empty(B * Lq, device=q.device, dtype=torch.float32)
+    alk = (ctypes.c_int * nfr)(*[int(x) for x in lk])
+    akr = (ctypes.c_int64 * nfr)(*[int(x) for x in krow])
+    aix = (ctypes.c_uint64 * nfr)(*[int(x) & (2**64 - 1) for x in idx0])
+    kp = ako = None
+    if keep is not None:
+        assert keep.dtype == torch.int32 and len(koff) == nfr
+        assert all(int(koff[f]) + keep_words(bpf, 1, Lq, lk[f]) <= keep.numel() for f in range(nfr))
+        ako = (ctypes.c_int64 * nfr)(*[int(x) for x in koff])
+        kp = ptr(keep)
+
+    def rs(t):  # row stride of a packed [rows, 1, C] view
+        assert t.stride(-1) == 1
+        return t.stride(0)
+    call("s2h_flash_bwd_frames_vfold", nfr, bpf, Lq, ctypes.cast(alk, ctypes.c_void_p).value,
+         ctypes.cast(akr, ctypes.c_void_p).value, ctypes.cast(aix, ctypes.c_void_p).value,
+         ptr(q), *_brs(q), ptr(k), rs(k), ptr(mem), rs(mem), ptr(u), *_brs(u), ptr(du), *_brs(du),
+         ptr(dq), *_brs(dq), ptr(dk), rs(dk), ptr(lse), ptr(di), float(scale), float(p_drop),
+         int(seed) & (2**64 - 1), kp, ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None, stream())
+    return dq, dk
+
+
+def vfold_weight(wv, bv, out=None):
+    """[Wv | bv | 0] bf16 [N, 72] from the bf16 weight [N, 64] and the fp32 bias [N]"""
+    N, K = wv.shape
+    if out is None:
+        out = torch.empty(N, VFOLD_COLS, device=wv.device, dtype=torch.bfloat16)
+    assert wv.dtype == torch.bfloat16 and wv.is_contiguous() and bv.dtype == torch.float32 and out.is_contiguous()
+    call("s2h_vfold_weight", N, K, out.shape[1], ptr(wv), ptr(bv), ptr(out), stream())
+    return out
+
+
+def vfold_grad(g, gwv, gbv):
+    """gwv [N, K] += g[:, :K], gbv [N] += g[:, K] (g fp32 [N, ld])"""
+    N, ld = g.shape
+    K = gwv.shape[1] if gwv is not None else VFOLD_DV
+    call("s2h_vfold_grad", N, K, ld, ptr(g), ptr(gwv), ptr(gbv), stream())
+
+
 def _keep_ptr(keep, B, H, Lq, Lk):
     if keep is None:
         return None

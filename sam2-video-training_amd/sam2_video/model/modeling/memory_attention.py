@@ -4,7 +4,9 @@ Per layer: LN1 -> fused q/k/v GEMM (arena-adjacent weights) -> RoPE(q, k) ->
 flash attention -> out-proj GEMM with dropout + residual in the epilogue;
 LN2 -> q GEMM + RoPE, k GEMM on (memory + memory_pos) + RoPE on the spatial
 rows (table repeated per memory frame, object-pointer rows excluded), v GEMM on
-memory -> flash attention over Lk = n_frames*L + 4*n_ptr -> out-proj (+res);
+memory -> flash attention over Lk = n_frames*L + 4*n_ptr -> out-proj (+res) -- in bf16 the value
+projection is folded into the attention (RoPEAttention.attend_mem: the 64-wide memory is the
+attention's value, [Wv | bv] one GEMM after it);
 LN3 -> linear1 (ReLU + dropout in the epilogue) -> linear2 (+dropout, +res).
 """
 from __future__ import annotations
@@ -74,7 +76,7 @@ class MemoryAttentionLayer(nn.Module):
         ca = self.cross_attn_image
         q = ca.rope_q(ca.q_proj(t), L)
         k = ca.rope_k(ca.k_proj(mem_k), L, num_k_exclude_rope)
-        y = ca.attend(q, k, ca.v_proj(mem_v), out_drop=p)
+        y = ca.attend_mem(q, k, mem_v, out_drop=p)
         t, x = FN.add_layer_norm(x, y, self.norm3, self.norm3.eps)
         y = self.linear2(self.linear1(t, act="relu", drop_p=p), drop_p=p)
         t, x = FN.add_layer_norm(x, y, next_norm, next_norm.eps)
@@ -104,8 +106,7 @@ class MemoryAttentionLayer(nn.Module):
         t2 = self.norm2(tgt)
         q = ca.rope_q(ca.q_proj(t2), L)
         k = ca.rope_k(ca.k_proj(mem_k), L, num_k_exclude_rope)
-        v = ca.v_proj(mem_v)
-        tgt = ca.attend(q, k, v, residual=tgt, out_drop=p)
+        tgt = ca.attend_mem(q, k, mem_v, residual=tgt, out_drop=p)
         # feed-forward (:95-98)
         t2 = self.norm3(tgt)
         h = self.linear1(t2, act="relu", drop_p=p)

@@ -139,6 +139,7 @@ class SAM2Base(nn.Module):
         """sam2_base.py:488-506.  img_batch [T, 3, H, W] fp32 (NCHW, as the reference).
         Returns NHWC features: backbone_fpn levels [T, h_i, w_i, C_i] (levels 0/1 projected by
         conv_s0 / conv_s1), vision_pos_enc tables [h_i*w_i, 256]."""
+        FN.new_step()  # arena-derived weights (the folded value projections) are rebuilt on first use
         dtype = self.compute_dtype
         x = img_batch.permute(0, 2, 3, 1).contiguous()
         x = ops.cast(x, dtype) if dtype != torch.float32 else x

@@ -17,6 +17,8 @@ CASES = {
     "tiny256_point_all_multi": ("tiny", "point", ALL),
     "tiny256_mask_all": ("tiny", "mask", ALL),
     "bplus256_point_all": ("base_plus", "point", ALL),
+    # Hiera-L trunk (BASELINE config 4's model): stages [2, 6, 36, 4], head dim 72
+    "large128_point_all": ("large", "point", ALL),
 }
 # reference steps under CPU bf16 autocast (oracle/gen_golden.py), with their fp32 twin
 BF16_CASES = {"bplus256_point_all_bf16": "bplus256_point_all"}

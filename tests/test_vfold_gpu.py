@@ -1,0 +1,184 @@
+"""The folded memory cross-attention (flash.hip / flash_bwd.hip V-fold, kernels/functional.py
+VFoldProj): attention(q, k, M Wv^T + bv) computed as [D M | rowsum(D)] [Wv | bv]^T
+(transformer.py:275-311 with memory_attention.py:66-81's kv_in_dim 64).  Checked against a torch
+fp32 reference of the unfolded op, against the unfolded flash kernels on the same dropout
+masks, the frame-table backward against one launch per frame, and the V-fold module path
+against the unfolded one in a bf16 training step."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ops():
+    from sam2_video.kernels import ops
+    return ops
+
+
+def _close(a, b, tol, what=""):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    scale = b.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"{what}: max err {err:.3e} vs scale {scale:.3e} (tol {tol})"
+
+
+def _inputs(B, Lq, Lk, seed):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    bf = torch.bfloat16
+    q = (torch.randn(B, Lq, 1, 256, generator=g) * 0.5).to(DEV, bf)
+    k = (torch.randn(B, Lk, 1, 256, generator=g) * 0.5).to(DEV, bf)
+    m = torch.randn(B, Lk, 1, 64, generator=g).to(DEV, bf)
+    wv = (torch.randn(256, 64, generator=g) * 0.1).to(DEV, bf)
+    bv = (torch.randn(256, generator=g) * 0.5).to(DEV)
+    return q, k, m, wv, bv
+
+
+@pytest.mark.parametrize("B,Lq,Lk", [(3, 256, 600), (2, 128, 64), (13, 1024, 2056)])
+def test_vfold_matches_unfolded_attention_fp32_reference(B, Lq, Lk):
+    """u' [Wv | bv]^T == softmax(scale q k^T)(M Wv^T + bv) (fp32 torch, bf16 tolerance), forward
+    with and without the key split, and the backward's dq / dk against autograd; u'[:, :, 64] = 1
+    and the pad columns 0 without dropout"""
+    ops = _ops()
+    q, k, m, wv, bv = _inputs(B, Lq, Lk, 1)
+    scale = 256 ** -0.5
+    u = torch.full((B, Lq, 1, 72), float("nan"), device=DEV, dtype=torch.bfloat16)
+    lse = torch.empty(B, 1, Lq, device=DEV)
+    ops.attn_fwd_vfold(q, k, m, u, lse, scale)
+    assert torch.all(u[..., 64] == 1) and torch.all(u[..., 65:] == 0)
+    w72 = ops.vfold_weight(wv, bv)
+    assert torch.equal(w72[:, :64], wv) and torch.equal(w72[:, 64], bv.to(torch.bfloat16))
+    assert torch.all(w72[:, 65:] == 0)
+    o = u.float()[:, :, 0] @ w72.float().t()
+    qr, kr = (t.float()[:, :, 0].clone().requires_grad_(True) for t in (q, k))
+    v = m.float()[:, :, 0] @ wv.float().t() + bv
+    s = (qr @ kr.transpose(1, 2)) * scale
+    ref = s.softmax(-1) @ v
+    _close(o, ref, 2e-2, "o")
+    _close(lse[:, 0], torch.logsumexp(s, -1), 1e-3, "lse")
+    do = torch.randn(B, Lq, 256, device=DEV)
+    ref.backward(do)
+    du = (do.to(torch.bfloat16).float() @ w72.float()).to(torch.bfloat16).view(B, Lq, 1, 72)
+    dq = torch.empty_like(q)
+    dk = torch.empty(B * Lk, 1, 256, device=DEV, dtype=torch.bfloat16)
+    ops.flash_bwd_frames_vfold(1, B, [Lk], [0], [0], q, k.reshape(B * Lk, 1, 256), m.reshape(B * Lk, 1, 64), u, du,
+                               lse, dq, dk, scale, 0.0, 0)
+    _close(dq[:, :, 0], qr.grad, 4e-2, "dq")
+    _close(dk.view(B, Lk, 256), kr.grad, 4e-2, "dk")
+    # value-projection weight gradient from u' (dO^T u') == the unfolded dV^T M + bias gradient
+    p = s.softmax(-1).detach()
+    dv = p.transpose(1, 2) @ do
+    dwv_ref = torch.einsum("bkn,bkc->nc", dv, m.float()[:, :, 0])
+    dbv_ref = dv.sum((0, 1))
+    g72 = torch.einsum("bqn,bqc->nc", do.to(torch.bfloat16).float(), u.float()[:, :, 0])
+    _close(g72[:, :64], dwv_ref, 2e-2, "dWv")
+    _close(g72[:, 64], dbv_ref, 2e-2, "dbv")
+
+
+def test_vfold_dropout_matches_unfolded_flash_kernels():
+    """with dropout the fold and the unfolded flash kernels draw the same keep masks (same seed,
+    element indices, keep bitmap): forward outputs, dq and dk agree to bf16 rounding, and
+    rowsum(D) (u'[:, :, 64]) carries the dropped mass"""
+    ops = _ops()
+    B, Lq, Lk, p_drop, seed = 4, 256, 1100, 0.1, 77
+    q, k, m, wv, bv = _inputs(B, Lq, Lk, 2)
+    scale = 256 ** -0.5
+    w72 = ops.vfold_weight(wv, bv)
+    v = (m.float()[:, :, 0] @ wv.float().t() + bv).to(torch.bfloat16).view(B, Lk, 1, 256)
+    keep_a = torch.zeros(ops.keep_words(B, 1, Lq, Lk), device=DEV, dtype=torch.int32)
+    keep_b = torch.zeros_like(keep_a)
+    o_ref = torch.empty(B, Lq, 1, 256, device=DEV, dtype=torch.bfloat16)
+    lse_a = torch.empty(B, 1, Lq, device=DEV)
+    ops.attn_fwd(q, k, v, o_ref, lse_a, scale, p_drop, seed, keep=keep_a)
+    u = torch.empty(B, Lq, 1, 72, device=DEV, dtype=torch.bfloat16)
+    lse_b = torch.empty(B, 1, Lq, device=DEV)
+    ops.attn_fwd_vfold(q, k, m, u, lse_b, scale, p_drop, seed, keep=keep_b)
+    assert torch.equal(keep_a, keep_b)
+    torch.testing.assert_close(lse_a, lse_b, atol=1e-5, rtol=1e-5)
+    o = u.float()[:, :, 0] @ w72.float().t()
+    _close(o, o_ref.float()[:, :, 0], 2e-2, "o (dropout)")
+    r = u.float()[:, :, 0, 64]
+    assert (r - 1).abs().max() > 1e-3 and (r - 1).abs().mean() < 0.1  # dropped mass, around 1
+    do = torch.randn(B, Lq, 1, 256, device=DEV).to(torch.bfloat16)
+    dq_a, dk_a, dv_a = torch.empty_like(q), torch.empty_like(k), torch.empty_like(v)
+    ops.attn_bwd(q, k, v, o_ref, do, lse_a, dq_a, dk_a, dv_a, scale, p_drop, seed, keep=keep_a)
+    du = (do.float()[:, :, 0] @ w72.float()).to(torch.bfloat16).view(B, Lq, 1, 72)
+    dq_b = torch.empty_like(q)
+    dk_b = torch.empty(B * Lk, 1, 256, device=DEV, dtype=torch.bfloat16)
+    ops.flash_bwd_frames_vfold(1, B, [Lk], [0], [0], q, k.reshape(B * Lk, 1, 256), m.reshape(B * Lk, 1, 64), u, du,
+                               lse_b, dq_b, dk_b, scale, p_drop, seed, keep=keep_b, koff=[0])
+    _close(dq_b, dq_a, 5e-2, "dq (dropout)")
+    _close(dk_b.view_as(k), dk_a, 5e-2, "dk (dropout)")
+
+
+def test_vfold_frame_table_backward_equals_per_frame_launches():
+    """the frame-table V-fold backward (packed K / M of 3 frames with different key counts, dropout
+    idx0 per frame) equals one single-frame launch per frame bit for bit"""
+    ops = _ops()
+    B, Lq, p_drop, seed = 2, 128, 0.1, 5
+    lks = [300, 620, 1028]
+    fr = [_inputs(B, Lq, lk, 10 + i) for i, lk in enumerate(lks)]
+    scale = 256 ** -0.5
+    idx0, koff, acc_e, acc_w = [], [], 0, 0
+    us, lses, keeps = [], [], []
+    for (q, k, m, _, _), lk in zip(fr, lks):
+        idx0.append(acc_e)
+        koff.append(acc_w)
+        u = torch.empty(B, Lq, 1, 72, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B, 1, Lq, device=DEV)
+        keep = torch.zeros(ops.keep_words(B, 1, Lq, lk), device=DEV, dtype=torch.int32)
+        ops.attn_fwd_vfold(q, k, m, u, lse, scale, p_drop, seed, idx0=acc_e, keep=keep)
+        us.append(u)
+        lses.append(lse)
+        keeps.append(keep)
+        acc_e += B * Lq * lk
+        acc_w += keep.numel()
+    dus = [torch.randn(B, Lq, 1, 72, device=DEV).to(torch.bfloat16) for _ in lks]
+    singles = []
+    for i, ((q, k, m, _, _), lk) in enumerate(zip(fr, lks)):
+        dq = torch.empty_like(q)
+        dk = torch.empty(B * lk, 1, 256, device=DEV, dtype=torch.bfloat16)
+        ops.flash_bwd_frames_vfold(1, B, [lk], [0], [idx0[i]], q, k.reshape(-1, 1, 256), m.reshape(-1, 1, 64), us[i],
+                                   dus[i], lses[i], dq, dk, scale, p_drop, seed, keep=keeps[i], koff=[0])
+        singles.append((dq, dk))
+    q_all = torch.cat([f[0] for f in fr])
+    k_all = torch.cat([f[1].reshape(-1, 1, 256) for f in fr])
+    m_all = torch.cat([f[2].reshape(-1, 1, 64) for f in fr])
+    krow = [0, B * lks[0], B * (lks[0] + lks[1])]
+    dq = torch.empty_like(q_all)
+    dk = torch.empty_like(k_all)
+    ops.flash_bwd_frames_vfold(3, B, lks, krow, idx0, q_all, k_all, m_all, torch.cat(us), torch.cat(dus),
+                               torch.cat(lses), dq, dk, scale, p_drop, seed, keep=torch.cat(keeps), koff=koff)
+    for i, (dq1, dk1) in enumerate(singles):
+        assert torch.equal(dq[i * B:(i + 1) * B], dq1)
+        assert torch.equal(dk[krow[i]:krow[i] + B * lks[i]], dk1)
+
+
+def test_vfold_step_matches_unfolded_step_bf16(monkeypatch):
+    """a bf16 B+ 256^2 training step with the fold (default) against the same step with
+    S2H_VFOLD=0 (v_proj GEMM + unfolded flash attention), dropout off: per-object mask logits and
+    every gradient within bf16 drift, the value projections' gradients included"""
+    from step_harness import build_model, golden_batch, grads_by_name, load_golden, mask_iou, run_step
+    g = load_golden("bplus256_point_all")
+    batch = golden_batch(g).to(DEV)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("S2H_VFOLD", flag)
+        model = build_model("base_plus", 256, ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder",
+                                               "prompt_encoder"], "point", dtype="bf16")
+        stages, merged, losses, _ = run_step(model, batch)
+        res[flag] = ([s["pred_masks"].detach().float().cpu() for s in stages], float(losses["total_loss"]),
+                     grads_by_name(model))
+    (m0, l0, g0), (m1, l1, g1) = res["0"], res["1"]
+    for a, b in zip(m0, m1):
+        assert mask_iou(a, b) >= 0.98
+        _close(a, b, 0.05)
+    assert abs(l0 - l1) <= 0.01 * abs(l0)
+    names = [n for n in g0 if ".cross_attn_image.v_proj." in n or ".cross_attn_image.k_proj.weight" in n]
+    assert len(names) == 12
+    for n in names:
+        cos = torch.nn.functional.cosine_similarity(g0[n].flatten(), g1[n].flatten(), dim=0).item()
+        assert cos >= 0.98, (n, cos)
+    flat0 = torch.cat([v.flatten() for v in g0.values()])
+    flat1 = torch.cat([v.flatten() for v in g1.values()])
+    assert torch.nn.functional.cosine_similarity(flat0, flat1, dim=0).item() >= 0.99
