@@ -221,6 +221,16 @@ int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* fr_lk, const
 int s2h_vfold_weight(int N, int K, int ld, const void* wv, const float* bv, void* out, hipStream_t st);
 int s2h_vfold_grad(int N, int K, int ld, const float* g, float* gwv, float* gbv, hipStream_t st);
 
+/* bf16 Linear whose output is rotated by the axial RoPE in the GEMM epilogue: Y = A W^T + bias
+ * (A [M, K], W [N, K] rows K-contiguous), then in every block of L rows the rows r < nrot are
+ * rotated in (2i, 2i+1) column pairs for columns c < ncol with table row r % period and column
+ * (c % dh) / 2 (cosv / sinv [period, dh / 2] fp32, as s2h_rope).  Replaces q_proj / k_proj +
+ * apply_rotary_enc (transformer.py:275-311, position_encoding.py:212-239) and the fused
+ * q / k / v projection of the memory self-attention with q and k rotated (ncol = 2 x 256). */
+int s2h_linear_rope(int M, int N, int K, const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
+                    void* Y, int64_t ldy, const float* cosv, const float* sinv, int L, int nrot, int period, int ncol,
+                    int dh, hipStream_t stream);
+
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:
  * xsum = x + badd (badd broadcast over rows when b_bcast), y = LN(xsum) * gamma + beta;

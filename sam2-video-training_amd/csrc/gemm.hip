@@ -222,7 +222,7 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
     s2h_prof_end(slot, stream);
     return rc;
   }
-  GemmArgs16 b;
+  GemmArgs16 b = {};
   b.M = a.M; b.N = a.N; b.K = a.K;
   b.A = (const bf16*)A; b.lda_m = lda_m; b.lda_k = lda_k; b.sA = sA;
   b.B = (const bf16*)B; b.ldb_k = ldb_k; b.ldb_n = ldb_n; b.sB = sB;
@@ -237,6 +237,34 @@ extern "C" int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
   b.out_f32 = dt_c == S2H_F32;
   b.rowsum = nullptr;
   rc = s2h_gemm_bf16(b, batch, stream);
+  s2h_prof_end(slot, stream);
+  return rc;
+}
+
+// Linear + axial RoPE of its output in one launch (bf16): Y[b] = A[b] W^T + bias, then rows
+// r < nrot of every block of L rows rotated in (2i, 2i+1) pairs of the columns c < ncol with table
+// row (r % period) and column (c % dh) / 2 -- the memory attention's q / k projections followed by
+// apply_rotary_enc (transformer.py:275-311), and the fused q/k/v projection with q and k rotated.
+extern "C" int s2h_linear_rope(int M, int N, int K, const void* A, int64_t lda, const void* W, int64_t ldw,
+                               const float* bias, void* Y, int64_t ldy, const float* cosv, const float* sinv, int L,
+                               int nrot, int period, int ncol, int dh, hipStream_t stream) {
+  if (M <= 0 || N <= 0) return 0;
+  if (K <= 0 || L <= 0 || period <= 0 || dh <= 0 || dh % 8 || ncol % 8 || nrot < 0 || nrot > L || !cosv || !sinv)
+    return (int)hipErrorInvalidValue;
+  const int slot = s2h_prof_begin(stream, 4, 1, M, N, K, 2 + 1 + 4);
+  GemmArgs16 b = {};
+  b.M = M; b.N = N; b.K = K;
+  b.A = (const bf16*)A; b.lda_m = lda; b.lda_k = 1;
+  b.B = (const bf16*)W; b.ldb_k = 1; b.ldb_n = ldw;
+  b.C = Y; b.ldc = ldy;
+  b.bias = bias; b.bias_mode = bias ? 1 : 0;
+  b.seed_off = s2h_rng_offset_ptr();
+  b.alpha = 1.f;
+  b.vecA = aligned16(A) && lda % 8 == 0;
+  b.vecB = aligned16(W) && ldw % 8 == 0;
+  b.rope_cos = cosv; b.rope_sin = sinv;
+  b.rope_L = L; b.rope_nrot = nrot; b.rope_period = period; b.rope_ncol = ncol; b.rope_dh = dh;
+  const int rc = s2h_gemm_bf16(b, 1, stream);
   s2h_prof_end(slot, stream);
   return rc;
 }

@@ -20,6 +20,12 @@ struct GemmArgs16 {
   int vecC;  // 4-column output groups are vector-aligned
   int vec8;  // 8-column groups take 16-B accesses: bit 0 C (bf16 out), bit 1 X, bit 2 R
   float* rowsum;  // optional: rowsum[b*M + m] += sum_k A[b](m, k)  (fused bias gradient)
+  // optional axial RoPE of the output (memory-attention q / k projections, transformer.py:275-311):
+  // row r (within batch bz) is rotated when (r % rope_L) < rope_nrot, with table row
+  // (r % rope_L) % rope_period; columns c < rope_ncol are rotated in pairs (2i, 2i+1) with the
+  // tables' column (c % rope_dh) / 2.  rope_cos == nullptr: no rotation.
+  const float* rope_cos; const float* rope_sin;
+  int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
   int dbg;        // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
 };
 

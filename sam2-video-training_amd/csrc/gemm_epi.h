@@ -31,6 +31,23 @@ __device__ __forceinline__ uint2 ld4_bf16(const bf16* ptr, bool full) {
   if (full) return *(const uint2*)ptr;
   return make_uint2(0, 0);
 }
+// axial RoPE of NV consecutive output columns (col0 even) of `row` (GemmArgs16 rope_* fields)
+template <int NV>
+__device__ __forceinline__ void rope_cols(const GemmArgs16& p, int row, int col0, float* v) {
+  if (p.rope_cos == nullptr || col0 >= p.rope_ncol) return;
+  const int l = row % p.rope_L;
+  if (l >= p.rope_nrot) return;
+  const int half = p.rope_dh / 2;
+  const int t = (l % p.rope_period) * half + (col0 % p.rope_dh) / 2;
+#pragma unroll
+  for (int j = 0; j < NV / 2; ++j) {
+    const float co = p.rope_cos[t + j], si = p.rope_sin[t + j];
+    const float x0 = v[2 * j], x1 = v[2 * j + 1];
+    v[2 * j] = x0 * co - x1 * si;
+    v[2 * j + 1] = x0 * si + x1 * co;
+  }
+}
+
 __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4, const float* bcol) {
   float v[4] = {v4.x, v4.y, v4.z, v4.w};
   const int nval = p.N - col0;
@@ -87,6 +104,7 @@ __device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, 
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], p.act);
   }
+  rope_cols<4>(p, row, col0, v);
   if (p.cscale) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] *= e < nval ? p.cscale[col0 + e] : 0.f;
@@ -210,6 +228,7 @@ __device__ __forceinline__ void epilogue8(const GemmArgs16& p, int bz, int row, 
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], p.act);
   }
+  rope_cols<8>(p, row, col0, v);
   if (p.cscale) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] *= p.cscale[col0 + e];

@@ -30,6 +30,7 @@ SIGNATURES = {
     "s2h_gemm": [I, I, I, I, I, I, P, L, L, L, P, L, L, L, P, L, L, P, I, P, L, L, P, L, L, I, P, F, c_uint64, c_uint64,
                  F, F, I, P],
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
+    "s2h_linear_rope": [I, I, I, P, L, P, L, P, P, L, P, P, I, I, I, I, I, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],

@@ -120,6 +120,17 @@ def linear(x, mod, w, bias, **kw):
     return ops.linear(x, w, bias, **kw)
 
 
+def linear_rope(x, mod, w, bias, rope, out=None):
+    """forward GEMM of a Linear whose output is rotated by RoPE (ops.rope_blocks layout): MX-fp8
+    GEMM + in-place rotation when `mod` is eligible, else the bf16 GEMM with the rotation fused"""
+    w8 = weight(mod) if x.dtype != torch.float32 and _pays(w.shape[1], w.shape[0]) else None
+    if w8 is not None:
+        out = ops.linear_mx8(x, w8, bias, out=out)
+        ops.rope_blocks(out.view(-1, out.shape[-1]), rope)
+        return out
+    return ops.linear_rope(x, w, bias, rope, out=out)
+
+
 def linear_dgrad(dy, mod, **kw):
     """input-gradient GEMM of a Linear: MX-fp8 when `mod` is eligible (and it pays), else the bf16 kernel"""
     wt8 = None

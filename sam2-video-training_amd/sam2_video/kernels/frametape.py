@@ -379,13 +379,14 @@ def _empty_like_store(tape, st: Store, dtype=None):
 
 
 # ---------------------------------------------------------------- linear
-def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0):
+def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0, rope=None):
     x = x if x.is_contiguous() else x.contiguous()
     # ReLU without residual: the backward masks with the output (> 0 exactly where the
     # pre-activation was positive and the element kept), so no pre-activation is stored
     relu_out = act == "relu" and residual is None
     op, first = tape._begin("linear", [x, residual], _linear_bw,
-                            {"mod": mod, "act": act, "p": float(drop_p), "relu_out": relu_out})
+                            {"mod": mod, "act": act, "p": float(drop_p), "relu_out": relu_out,
+                             "rope": rope is not None})
     if first and tape.vid(x) is None:
         raise RuntimeError("tape linear: input must be a recorded value or declared input")
     w = mod.compute_weight()
@@ -397,7 +398,13 @@ def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0):
     pre = tape._aux("pre", shape, x.dtype, scale) if act and not relu_out else None
     seed = tape._seed() if drop_p > 0 else 0
     idx0 = tape._idx0(op, out.numel())
-    _fp8.linear(x, mod, w, b, act=act, out=out, pre=pre, residual=residual, drop_p=drop_p, seed=seed, drop_idx0=idx0)
+    if rope is not None:  # RoPE of the output in the GEMM epilogue; per-frame (L, nrot) for the backward
+        assert act is None and residual is None and drop_p == 0
+        _fp8.linear_rope(x, mod, w, b, rope, out=out)
+        tape._fattr(op, "rope", rope)
+    else:
+        _fp8.linear(x, mod, w, b, act=act, out=out, pre=pre, residual=residual, drop_p=drop_p, seed=seed,
+                    drop_idx0=idx0)
     if first:
         op.attrs["seed"] = seed
         op.attrs["K"] = x.shape[-1]
@@ -410,6 +417,14 @@ def _linear_bw(tape, op, gys):
     mod, act, p = op.attrs["mod"], op.attrs["act"], op.attrs["p"]
     N, K = mod.compute_weight().shape
     gy2 = gy.view(-1, N)
+    if op.attrs.get("rope"):  # rotate the output gradient back (in place: the attention's fresh dq / dk)
+        ropes = op.fattrs["rope"]
+        if all(r[2:] == ropes[0][2:] for r in ropes):
+            ops.rope_blocks(gy2, ropes[0], inverse=True)
+        else:
+            st = tape.st(op.outs[0])
+            for f, r in enumerate(ropes):
+                ops.rope_blocks(gy[st.offsets[f]:st.offsets[f] + st.numels[f]].view(-1, N), r, inverse=True)
     if op.outs[0] in tape.premasked:  # the consumer's dgrad already applied ReLU' and 1/keep
         dpre = gy2
     elif op.attrs["relu_out"]:

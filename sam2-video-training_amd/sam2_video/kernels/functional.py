@@ -54,9 +54,16 @@ def _grad_of(p):
 # ---------------------------------------------------------------- Linear
 class _Linear(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, wp, bp, mod, act, residual, drop_p):
+    def forward(ctx, x, wp, bp, mod, act, residual, drop_p, rope=None):
         w = mod.compute_weight()
         b = mod.compute_bias()
+        ctx.rope = rope
+        if rope is not None:  # RoPE of the output in the GEMM epilogue (no act / residual / dropout)
+            assert act is None and residual is None and drop_p == 0
+            out = _fp8.linear_rope(x, mod, w, b, rope)
+            ctx.mod, ctx.act, ctx.drop_p, ctx.seed, ctx.relu_out, ctx.has_res = mod, None, 0.0, 0, False, False
+            ctx.save_for_backward(x, None)
+            return out
         # ReLU without residual: the backward masks with the output itself (no pre-activation)
         relu_out = act == "relu" and residual is None
         pre = torch.empty(*x.shape[:-1], w.shape[0], device=x.device, dtype=x.dtype) if act and not relu_out else None
@@ -72,6 +79,8 @@ class _Linear(torch.autograd.Function):
         x, pre = ctx.saved_tensors
         mod = ctx.mod
         dy = dy.contiguous()
+        if ctx.rope is not None:  # the gradient of the rotated output, rotated back (in place)
+            ops.rope_blocks(dy.view(-1, dy.shape[-1]), ctx.rope, inverse=True)
         if ctx.relu_out:
             dpre = ops.relu_mask_bwd(pre, dy, 1.0 / (1.0 - ctx.drop_p))
         elif ctx.drop_p > 0:
@@ -87,16 +96,18 @@ class _Linear(torch.autograd.Function):
         elif gb is not None:
             ops.colsum(dpre, gb)
         dx = _fp8.linear_dgrad(dpre, mod) if ctx.needs_input_grad[0] else None
-        return dx, None, None, None, None, (dy if ctx.has_res else None), None
+        return dx, None, None, None, None, (dy if ctx.has_res else None), None, None
 
 
-def linear(x, mod, act=None, residual=None, drop_p=0.0):
+def linear(x, mod, act=None, residual=None, drop_p=0.0, rope=None):
     """drop(act(x @ W^T + b)) (+ residual).  `mod` provides compute_weight(), compute_bias(),
-    grad_views() and `weight`/`bias` anchors (Parameters) for the autograd tape."""
+    grad_views() and `weight`/`bias` anchors (Parameters) for the autograd tape.  rope = (cos, sin,
+    L, nrot, period, ncol, dh): the output rotated by the axial RoPE in the GEMM epilogue
+    (ops.rope_blocks layout; no act / residual / dropout)."""
     T = _ft.active()
     if T is not None:
-        return _ft.linear(T, x, mod, act, residual, float(drop_p))
-    return _Linear.apply(x.contiguous(), mod.weight, mod.bias, mod, act, residual, float(drop_p))
+        return _ft.linear(T, x, mod, act, residual, float(drop_p), rope=rope)
+    return _Linear.apply(x.contiguous(), mod.weight, mod.bias, mod, act, residual, float(drop_p), rope)
 
 
 class _MLP2(torch.autograd.Function):

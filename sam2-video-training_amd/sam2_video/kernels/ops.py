@@ -94,6 +94,41 @@ def linear(x, w, bias=None, act=None, out=None, pre=None, residual=None, out_dty
     return out
 
 
+def rope_blocks(y2, rp, inverse=False):
+    """in place axial RoPE of a [rows, N] matrix (C contiguous): rp = (cos, sin, L, nrot, period,
+    ncol, dh) rotates, in every block of L rows, the rows < nrot in the columns < ncol (dh-wide
+    heads, pairs (2i, 2i + 1))"""
+    cos, sin, L, nrot, period, ncol, dh = rp
+    rows, N = y2.shape
+    assert rows % L == 0 and y2.stride(1) == 1
+    ld = y2.stride(0)
+    for c0 in range(0, ncol, dh):
+        v = torch.as_strided(y2, (rows // L, L, dh), (L * ld, ld, 1), y2.storage_offset() + c0)
+        rope(v, v, nrot, cos, sin, period, inverse)
+    return y2
+
+
+def linear_rope(x, w, bias, rp, out=None):
+    """out = RoPE(x @ w^T + bias) (rope_blocks' layout): one GEMM with the rotation in its epilogue
+    in bf16 (s2h_linear_rope), GEMM + in-place rotation in fp32"""
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N = w.shape[0]
+    assert w.shape[1] == K and w.is_contiguous()
+    if out is None:
+        out = torch.empty(*x.shape[:-1], N, device=x.device, dtype=x.dtype)
+    o2 = out.view(-1, N)
+    cos, sin, L, nrot, period, ncol, dh = rp
+    if x.dtype == torch.bfloat16 and x2.stride(1) == 1:
+        _dev(x2, w, o2, bias)
+        call("s2h_linear_rope", M, N, K, ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(bias), ptr(o2), N, ptr(cos),
+             ptr(sin), int(L), int(nrot), int(period), int(ncol), int(dh), stream())
+        return out
+    linear(x, w, bias, out=out)
+    rope_blocks(o2, rp)
+    return out
+
+
 def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0):
     """dx = alpha * dy @ w   (optionally * act'(pre) elementwise, fusing the previous layer's
     activation grad; for ReLU `pre` may be the previous layer's output, and alpha its 1/keep)."""

@@ -68,9 +68,9 @@ class FusedLinear:
         return (self.arena.group_view(self.wn, "grad").view(self.out_features, self.in_features),
                 self.arena.group_view(self.bn, "grad"))
 
-    def __call__(self, x, act=None, residual=None, drop_p=0.0):
+    def __call__(self, x, act=None, residual=None, drop_p=0.0, rope=None):
         if self.packed:
-            return FN.linear(x, self, act=act, residual=residual, drop_p=drop_p)
+            return FN.linear(x, self, act=act, residual=residual, drop_p=drop_p, rope=rope)
         return None
 
 

@@ -1,9 +1,9 @@
 """Memory attention (reference memory_attention.py:17-169), batch-first [O, L, C].
 
-Per layer: LN1 -> fused q/k/v GEMM (arena-adjacent weights) -> RoPE(q, k) ->
+Per layer: LN1 -> fused q/k/v GEMM (arena-adjacent weights, RoPE(q, k) in its epilogue) ->
 flash attention -> out-proj GEMM with dropout + residual in the epilogue;
-LN2 -> q GEMM + RoPE, k GEMM on (memory + memory_pos) + RoPE on the spatial
-rows (table repeated per memory frame, object-pointer rows excluded), v GEMM on
+LN2 -> q GEMM (+ RoPE in the epilogue), k GEMM on (memory + memory_pos) with RoPE in the
+epilogue on the spatial rows (table repeated per memory frame, object-pointer rows excluded), v GEMM on
 memory -> flash attention over Lk = n_frames*L + 4*n_ptr -> out-proj (+res) -- in bf16 the value
 projection is folded into the attention (RoPEAttention.attend_mem: the 64-wide memory is the
 attention's value, [Wv | bv] one GEMM after it);
@@ -64,18 +64,19 @@ class MemoryAttentionLayer(nn.Module):
         p = self._drop()
         sa = self.self_attn
         if self._fused_qkv is not None and sa.num_heads == 1:
-            qkv = self._fused_qkv(t)
-            cos, sin = sa.tables(L, qkv.device)
-            o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p(), rope=(cos, sin, L))
+            # one q/k/v GEMM with q and k rotated in its epilogue
+            cos, sin = sa.tables(L, t.device)
+            qkv = self._fused_qkv(t, rope=(cos, sin, L, L, L, 2 * C, C))
+            o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p())
             y = sa.out_proj(o.reshape(qkv.shape[0], L, C), drop_p=p)
         else:
-            q = sa.rope_q(sa.q_proj(t), L)
-            k = sa.rope_k(sa.k_proj(t), L)
+            q = sa.proj_q(t, L)
+            k = sa.proj_k(t, L)
             y = sa.attend(q, k, sa.v_proj(t), out_drop=p)
         t, x = FN.add_layer_norm(x, y, self.norm2, self.norm2.eps)
         ca = self.cross_attn_image
-        q = ca.rope_q(ca.q_proj(t), L)
-        k = ca.rope_k(ca.k_proj(mem_k), L, num_k_exclude_rope)
+        q = ca.proj_q(t, L)
+        k = ca.proj_k(mem_k, L, num_k_exclude_rope)
         y = ca.attend_mem(q, k, mem_v, out_drop=p)
         t, x = FN.add_layer_norm(x, y, self.norm3, self.norm3.eps)
         y = self.linear2(self.linear1(t, act="relu", drop_p=p), drop_p=p)
@@ -90,22 +91,20 @@ class MemoryAttentionLayer(nn.Module):
         sa = self.self_attn
         t2 = self.norm1(tgt)
         if self._fused_qkv is not None and sa.num_heads == 1:
-            # one packed q/k/v GEMM; RoPE + attention read it in place and the backward returns
-            # one packed gradient (FN.qkv_attention)
-            qkv = self._fused_qkv(t2)
-            cos, sin = sa.tables(L, qkv.device)
-            o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p(), rope=(cos, sin, L))
+            # one packed q/k/v GEMM with q and k rotated in its epilogue; the attention reads it in
+            # place and the backward returns one packed gradient (FN.qkv_attention)
+            cos, sin = sa.tables(L, t2.device)
+            qkv = self._fused_qkv(t2, rope=(cos, sin, L, L, L, 2 * C, C))
+            o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p())
             tgt = sa.out_proj(o.reshape(qkv.shape[0], L, C), residual=tgt, drop_p=p)
         else:
-            q, k, v = sa.q_proj(t2), sa.k_proj(t2), sa.v_proj(t2)
-            q = sa.rope_q(q, L)
-            k = sa.rope_k(k, L)
+            q, k, v = sa.proj_q(t2, L), sa.proj_k(t2, L), sa.v_proj(t2)
             tgt = sa.attend(q, k, v, residual=tgt, out_drop=p)
         # cross-attention to the memory bank (:66-81)
         ca = self.cross_attn_image
         t2 = self.norm2(tgt)
-        q = ca.rope_q(ca.q_proj(t2), L)
-        k = ca.rope_k(ca.k_proj(mem_k), L, num_k_exclude_rope)
+        q = ca.proj_q(t2, L)
+        k = ca.proj_k(mem_k, L, num_k_exclude_rope)
         tgt = ca.attend_mem(q, k, mem_v, residual=tgt, out_drop=p)
         # feed-forward (:95-98)
         t2 = self.norm3(tgt)

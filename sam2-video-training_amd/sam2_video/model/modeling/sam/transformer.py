@@ -88,6 +88,22 @@ class RoPEAttention(Attention):
         cos, sin = self.tables(Lq, q.device)
         return FN.rope(q, Lq, cos, sin, Lq)
 
+    def proj_q(self, x, Lq):
+        """rope_q(q_proj(x)) as one GEMM with the rotation in its epilogue"""
+        cos, sin = self.tables(Lq, x.device)
+        L = x.shape[1]
+        return FN.linear(x, self.q_proj, rope=(cos, sin, L, L, Lq, self.internal_dim, self.head_dim))
+
+    def proj_k(self, x, Lq, num_k_exclude_rope=0):
+        """rope_k(k_proj(x), Lq, num_k_exclude_rope) as one GEMM with the rotation in its epilogue
+        (the last num_k_exclude_rope rows -- object-pointer tokens -- unrotated)"""
+        Lk = x.shape[1]
+        nr = Lk - num_k_exclude_rope
+        if nr != Lq:
+            assert self.rope_k_repeat
+        cos, sin = self.tables(Lq, x.device)
+        return FN.linear(x, self.k_proj, rope=(cos, sin, Lk, nr, Lq, self.internal_dim, self.head_dim))
+
     def rope_k(self, k, Lq, num_k_exclude_rope=0):
         nr = k.shape[1] - num_k_exclude_rope
         if nr != Lq:
@@ -97,8 +113,8 @@ class RoPEAttention(Attention):
 
     def forward(self, q, k, v, num_k_exclude_rope=0, residual=None, out_drop=0.0):
         Lq = q.shape[1]
-        qp = self.rope_q(self.q_proj(q), Lq)
-        kp = self.rope_k(self.k_proj(k), Lq, num_k_exclude_rope)
+        qp = self.proj_q(q, Lq)
+        kp = self.proj_k(k, Lq, num_k_exclude_rope)
         return self.attend(qp, kp, self.v_proj(v), residual=residual, out_drop=out_drop)
 
 

@@ -840,3 +840,34 @@ def test_elementwise_vector_forms_match_scalar(dtype):
         assert torch.equal(ops.act_dropout_bwd(a, b, "gelu", 0.1, 77, idx0=idx0),
                            ops.act_dropout_bwd(a_, b_, "gelu", 0.1, 77, dx=out_, idx0=idx0))
 
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("Bt,L,nrot,N,ncol,dh", [(3, 256, 256, 256, 256, 256), (2, 1028 + 8, 1028, 256, 256, 256),
+                                                  (2, 256, 256, 768, 512, 256), (4, 64, 48, 128, 128, 32)])
+def test_linear_rope_matches_linear_then_rope(dtype, Bt, L, nrot, N, ncol, dh):
+    """s2h_linear_rope (RoPE in the GEMM epilogue: q / k projections, the fused q/k/v projection
+    with q and k rotated, key rows past nrot -- object-pointer tokens -- left alone) against the
+    torch fp32 product followed by the reference's complex-pair rotation (position_encoding.py:
+    212-239, table row r % period); and rope_blocks(inverse) undoes it"""
+    ops = _ops()
+    from sam2_video.model.modeling.position_encoding import axial_rope_table
+    torch.manual_seed(3)
+    period = 64 if dh == 32 else 256
+    side = int(period ** 0.5)
+    cos, sin = axial_rope_table(dh, side, side, 10000.0, DEV)
+    K = 64 if N == 256 and L > 1000 else 256
+    x = (torch.randn(Bt, L, K, device=DEV) * 0.5).to(dtype)
+    w = (torch.randn(N, K, device=DEV) * 0.05).to(dtype)
+    b = torch.randn(N, device=DEV)
+    y = ops.linear_rope(x, w, b, (cos, sin, L, nrot, period, ncol, dh))
+    ref = (x.float() @ w.float().t() + b).view(Bt, L, N).clone()
+    cc = torch.complex(cos, sin)  # [period, dh / 2]
+    for c0 in range(0, ncol, dh):
+        blk = ref[:, :nrot, c0:c0 + dh].reshape(Bt, nrot, dh // 2, 2)
+        z = torch.view_as_complex(blk.contiguous()) * cc[torch.arange(nrot, device=DEV) % period]
+        ref[:, :nrot, c0:c0 + dh] = torch.view_as_real(z).reshape(Bt, nrot, dh)
+    _close(y, ref, 2e-2 if dtype == torch.bfloat16 else 1e-5)
+    back = y.clone().view(-1, N)
+    ops.rope_blocks(back, (cos, sin, L, nrot, period, ncol, dh), inverse=True)
+    _close(back.view(Bt, L, N), (x.float() @ w.float().t() + b), 3e-2 if dtype == torch.bfloat16 else 1e-5)
