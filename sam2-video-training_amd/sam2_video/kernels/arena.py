@@ -32,15 +32,25 @@ def _align(n):
 
 class ParamArena:
     def __init__(self, named_params: Sequence, grad_names: Iterable[str], compute_dtype, device,
-                 groups: Sequence[Sequence[str]] = (), tail_prefixes: Sequence[str] = ()):
+                 groups: Sequence[Sequence[str]] = (), tail_prefixes: Sequence[str] = (), tail_rank=None):
         """tail_prefixes: gradient-receiving parameters under these name prefixes go to the END of
         the gradient region (their gradients are completed last in the backward -- the image
         encoder's -- so the rest of the region can be all-reduced while they are computed);
-        `grad_split` is the offset where they start."""
+        `grad_split` is the offset where they start.  tail_rank (name -> int or None) instead puts
+        the ranked gradient-receiving parameters at the end in rank order (the order the staged
+        backward completes them); `grad_cuts` = [start of each rank's range ..., n_grad]."""
         grad_names = set(grad_names)
         params = dict(named_params)
         tail = tuple(tail_prefixes)
-        if tail:  # stable partition of the gradient-receiving names: tail prefixes last
+        ranks = {}
+        if tail_rank is not None:
+            ranks = {n: tail_rank(n) for n, _ in named_params if n in grad_names}
+            ranks = {n: r for n, r in ranks.items() if r is not None}
+            head = [(n, p) for n, p in named_params if n not in ranks]
+            tailp = sorted([(n, p) for n, p in named_params if n in ranks], key=lambda np_: ranks[np_[0]])
+            named_params = head + tailp
+            tail = tuple(ranks)  # exact names (str.startswith accepts a tuple)
+        elif tail:  # stable partition of the gradient-receiving names: tail prefixes last
             named_params = ([(n, p) for n, p in named_params if not (n in grad_names and n.startswith(tail))]
                             + [(n, p) for n, p in named_params if n in grad_names and n.startswith(tail)])
         order: List[str] = []
@@ -74,8 +84,23 @@ class ParamArena:
                 n_grad = off
         self.total = _align(off)
         self.n_grad = _align(n_grad)
-        tails = [self.offsets[n] for n in order if n in grad_names and tail and n.startswith(tail)]
+        if ranks:
+            tails = [self.offsets[n] for n in order if n in ranks]
+        else:
+            tails = [self.offsets[n] for n in order if n in grad_names and tail and n.startswith(tail)]
         self.grad_split = min(tails) if tails else self.n_grad
+        # start offset of every rank's range (empty ranks start where the next one does) + n_grad
+        self.grad_cuts = [self.grad_split, self.n_grad]
+        if ranks:
+            top = max(ranks.values())
+            starts = {}
+            for n in order:
+                if n in ranks:
+                    starts.setdefault(ranks[n], self.offsets[n])
+            cuts = [self.n_grad] * (top + 2)
+            for r in range(top, -1, -1):
+                cuts[r] = starts.get(r, cuts[r + 1])
+            self.grad_cuts = cuts
         self.device = device
         self.compute_dtype = compute_dtype
         self.data = torch.zeros(self.total, dtype=torch.float32, device=device)

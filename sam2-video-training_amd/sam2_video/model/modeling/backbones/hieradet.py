@@ -155,4 +155,7 @@ class Hiera(nn.Module):
                 x, t = blk(x, t, next_norm=self.blocks[i + 1].norm1)
             if is_out:
                 outputs.append(x)
+        # the stage outputs: the cut points of the staged backbone backward
+        # (SAM2Model.backbone_backward_segments)
+        self.last_outputs = outputs if torch.is_grad_enabled() else []
         return outputs

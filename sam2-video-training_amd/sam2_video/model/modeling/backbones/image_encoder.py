@@ -7,6 +7,7 @@ from __future__ import annotations
 
 from typing import List, Optional
 
+import torch
 from torch import nn
 
 from ....kernels import functional as FN
@@ -59,7 +60,13 @@ class ImageEncoder(nn.Module):
         assert self.trunk.channel_list == self.neck.backbone_channel_list
 
     def forward(self, sample_nhwc):
-        features, pos = self.neck(self.trunk(sample_nhwc))
+        xs = self.trunk(sample_nhwc)
+        # the neck reads aliases of the stage outputs: autograd nodes of their own, so a backward
+        # from the backbone outputs can stop at the neck's inputs (the staged backbone backward,
+        # SAM2Model.backbone_backward_segments); no data is copied
+        xs = [x.view_as(x) for x in xs] if torch.is_grad_enabled() else xs
+        self.last_neck_inputs = xs if torch.is_grad_enabled() else []
+        features, pos = self.neck(xs)
         if self.scalp > 0:
             features, pos = features[: -self.scalp], pos[: -self.scalp]
         return {"vision_features": features[-1], "vision_pos_enc": pos, "backbone_fpn": features}

@@ -23,7 +23,7 @@ from torch import nn
 
 from .. import utils
 from ..data.data_utils import BatchedVideoDatapoint
-from ..kernels import fp8
+from ..kernels import fp8, ops
 from ..kernels.arena import ParamArena
 from ..utils.init import synth_tensor
 from ..utils.masks import merge_object_results_to_category
@@ -191,13 +191,73 @@ class SAM2Model(SAM2Base):
         for i, layer in enumerate(self.memory_attention.layers):
             groups += layer.arena_groups(f"memory_attention.layers.{i}")
         self.arena = ParamArena(named, grad_names, self.compute_dtype, device, groups=groups,
-                                tail_prefixes=("image_encoder.",))
+                                tail_rank=self._backbone_grad_rank())
         for m in self.modules():
             if hasattr(m, "bind_arena"):
                 m.bind_arena(self.arena)
         if self.fp8:
             fp8.mark_modules(self)
         return self
+
+    def _backbone_grad_rank(self):
+        """Order of the arena's tail: the parameters whose gradients the backbone backward (phase 2
+        of StepRunner's overlapped backward) completes, by the segment that completes them -- 0:
+        conv_s0 / conv_s1 (applied to the backbone outputs in forward_image) and the FPN neck, then
+        the Hiera stages last to first (1 = the last stage), patch / position embedding with the
+        first stage.  Everything else (the tracking loop's parameters) precedes them."""
+        ends = list(self.image_encoder.trunk.stage_ends)
+        nst = len(ends)
+
+        def rank(n):
+            if n.startswith(("sam_mask_decoder.conv_s0.", "sam_mask_decoder.conv_s1.", "image_encoder.neck.")):
+                return 0
+            if n.startswith("image_encoder.trunk.blocks."):
+                i = int(n.split(".")[3])
+                return nst - next(s for s, e in enumerate(ends) if i <= e)
+            if n.startswith("image_encoder."):
+                return nst
+            return None
+        return rank
+
+    def backbone_backward_segments(self, pending):
+        """Phase 2 of the overlapped backward as segments: [(closure, rank)], run in order; after
+        segment k every gradient of arena rank k (_backbone_grad_rank) is complete.  `pending` =
+        [(backbone output, its gradient)] from phase 1.  Segment 0 runs the backward from the backbone
+        outputs through conv_s0 / conv_s1 and the neck to the neck's inputs (aliases of the Hiera
+        stage outputs, ImageEncoder.forward, so it stops there); segment k >= 1 runs stage nst - k
+        from its output -- gradient = the neck's + the next stage's -- to the previous stage's output
+        (the first stage to the image)."""
+        enc = self.image_encoder
+        stages = list(getattr(enc.trunk, "last_outputs", []))
+        taps = list(getattr(enc, "last_neck_inputs", []))
+        outs = [t for t, _ in pending]
+        grads = [g for _, g in pending]
+        nst = len(enc.trunk.stage_ends)
+        if len(stages) != nst or len(taps) != nst or not all(x.requires_grad for x in stages):
+            # frozen trunk: conv_s0 / conv_s1 (and the neck) only, one segment
+            return [(lambda: torch.autograd.backward(outs, grads), 0)]
+        gs = {}
+
+        def seg0():
+            for i, g in enumerate(torch.autograd.grad(outs, taps, grads, allow_unused=True)):
+                gs[i] = g
+
+        def seg_stage(i):
+            def run():
+                g = gs.pop(i, None)
+                if g is None:
+                    return
+                if i == 0:
+                    torch.autograd.backward([stages[0]], [g])
+                    return
+                (gprev,) = torch.autograd.grad([stages[i]], [stages[i - 1]], [g], allow_unused=True)
+                if gprev is not None:
+                    if gs.get(i - 1) is None:
+                        gs[i - 1] = gprev
+                    else:
+                        ops.add(gs[i - 1], gprev, out=gs[i - 1])
+            return run
+        return [(seg0, 0)] + [(seg_stage(nst - k), k) for k in range(1, nst + 1)]
 
     def set_dropout(self, p: float):
         """override every dropout probability (p=0 gives the deterministic parity mode)"""

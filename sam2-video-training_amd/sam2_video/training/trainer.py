@@ -282,8 +282,11 @@ class StepRunner:
         arena = module.model.arena
         self.reducer = ArenaGradReducer(arena.grad_region(), split=arena.grad_split) if distributed else None
         # overlap: a two-phase backward -- (1) loss -> backbone outputs (the frame-batched
-        # tracking backward completes every gradient except the image encoder's), (2) the image
-        # encoder's backward -- with the all-reduce of the completed region issued between them
+        # tracking backward completes every gradient except the backbone's), (2) the backbone's
+        # backward in segments (SAM2Model.backbone_backward_segments: conv_s0/s1 + neck, then the
+        # Hiera stages last to first) -- with the all-reduce of every completed arena range
+        # (arena.grad_cuts) issued as soon as its segment ends, beside the following segments
+        self.cuts = list(getattr(arena, "grad_cuts", [arena.grad_split, arena.n_grad]))
         split_ok = getattr(module.model, "frame_batched", False) and arena.grad_split < arena.n_grad
         self.overlap = bool(split_ok and (distributed if split_backward is None else split_backward))
         self.accumulate = max(1, int(accumulate_grad_batches or 1))
@@ -301,7 +304,7 @@ class StepRunner:
         # and a replay of the captured one use identical masks
         self.seed_base = FN._SEED[0]
         self._pending = None
-        self._replay2 = None
+        self._segs = None
         module.model.arena.zero_grad()
 
     def _device_step(self, batch):
@@ -317,11 +320,20 @@ class StepRunner:
             loss.backward()
         return loss
 
-    def _phase2(self):
+    def _segments(self):
+        """the pending phase-2 backward as [(closure, arena rank)] (consumes the pending state)"""
         pend = self._pending
         self._pending = None
-        if pend:
-            torch.autograd.backward([t for t, _ in pend], [g for _, g in pend])
+        if not pend:
+            return []
+        segs = getattr(self.module.model, "backbone_backward_segments", None)
+        if segs is None:
+            return [(lambda: torch.autograd.backward([t for t, _ in pend], [g for _, g in pend]), 0)]
+        return segs(pend)
+
+    def _phase2(self):
+        for run, _ in self._segments():
+            run()
 
     def _graphed_step(self, batch):
         model = self.module.model
@@ -354,12 +366,13 @@ class StepRunner:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 loss = self._device_step(static)
-            g2 = None
-            if self._pending is not None:  # the image encoder's backward as a second graph
-                g2 = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g2, pool=g.pool()):
-                    self._phase2()
-            ent = self._graphs[key] = {"graph": g, "graph2": g2, "batch": static, "loss": loss,
+            segs = []
+            for run, rank in self._segments():  # the backbone's backward: one graph per segment
+                gk = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(gk, pool=g.pool()):
+                    run()
+                segs.append((gk.replay, rank, gk))
+            ent = self._graphs[key] = {"graph": g, "segs": segs, "batch": static, "loss": loss,
                                        "logged": dict(self.module.logged), "outputs": self.module.last_outputs}
         else:
             st = ent["batch"]
@@ -369,7 +382,7 @@ class StepRunner:
             model.upload_prompt_plan(plan, dev, out=st.prompt_plan["dev"])
             st.prompt_plan.update({k: plan[k] for k in ("points", "labels")})
         ent["graph"].replay()
-        self._replay2 = ent["graph2"]
+        self._segs = [(rep, rank) for rep, rank, _ in ent["segs"]]
         self.module.logged = dict(ent["logged"])
         self.module.last_outputs = ent["outputs"]
         return ent["loss"]
@@ -411,24 +424,27 @@ class StepRunner:
 
     def __call__(self, batch):
         self.begin_micro_step()
-        self._replay2 = None
+        self._segs = None
         loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
-        boundary = (self.micro_step + 1) % self.accumulate == 0
+        if self._segs is None:
+            self._segs = self._segments()
+        reduce = self.overlap and self.reducer is not None and (self.micro_step + 1) % self.accumulate == 0
         works = []
-        if self.overlap and boundary and self.reducer is not None:
-            # the tracking gradients are complete: reduce them beside the image encoder's backward
-            works += self.reducer.reduce_range(0, self.reducer.split)
-        if self._replay2 is not None:
-            self._replay2.replay()
-        else:
-            self._phase2()
-        reduced = False
-        if self.overlap and boundary and self.reducer is not None:
-            works += self.reducer.reduce_range(self.reducer.split, self.reducer.grad.numel())
+        if reduce:
+            # the tracking gradients are complete: reduce them beside the backbone's backward
+            works += self.reducer.reduce_range(0, self.cuts[0])
+        done = 0  # arena ranks reduced so far
+        for run, rank in self._segs:
+            run()
+            if reduce:  # this segment's range is complete: reduce it beside the next segments
+                works += self.reducer.reduce_range(self.cuts[done], self.cuts[rank + 1])
+                done = rank + 1
+        self._segs = None
+        if reduce:
+            works += self.reducer.reduce_range(self.cuts[done], self.reducer.grad.numel())
             for w in works:
                 w.wait()
-            reduced = True
-        self.after_backward(reduced=reduced)
+        self.after_backward(reduced=reduce)
         return loss
 
 

@@ -68,12 +68,14 @@ def _worker_overlap(rank, world, port, q):
     try:
         init_from_env("gloo")
         n, split = 50_003, 20_001
+        cuts = [split, 23_000, 23_000, 41_517, n]  # staged backbone ranges (one empty), StepRunner.cuts
         torch.manual_seed(rank)
         g = torch.randn(n) * (rank + 1)
         mine = g.clone()
         red = ArenaGradReducer(g, bucket_bytes=64 << 10, split=split)
         works = red.reduce_range(0, red.split)  # issued before the tail is "computed"
-        works += red.reduce_range(red.split, n)
+        for lo, hi in zip(cuts, cuts[1:]):  # one range per completed backward segment
+            works += red.reduce_range(lo, hi)
         for w in works:
             w.wait()
         allg = [torch.zeros(n) for _ in range(world)]

@@ -324,3 +324,36 @@ def test_data_module_shards_clips_across_ranks():
     idx = [list(iter(DistributedSampler(ds, num_replicas=2, rank=r, shuffle=True, seed=0))) for r in range(2)]
     assert not (set(idx[0]) & set(idx[1]) - {idx[0][-1], idx[1][-1]})  # only the padding repeats
     assert set(idx[0]) | set(idx[1]) == set(range(7))
+
+
+def test_arena_tail_ranks_follow_the_staged_backbone_backward():
+    """the gradient arena ends with the parameters the staged backbone backward completes, in the
+    order it completes them (SAM2Model._backbone_grad_rank): conv_s0 / conv_s1 and the neck (rank 0
+    -- conv_s0 / s1 act on the backbone outputs, so their gradients are finished by phase 2, not
+    phase 1), then the Hiera stages last to first, patch / position embedding with stage 1;
+    grad_cuts are the rank boundaries"""
+    from sam2_video.kernels.arena import ParamArena
+    from sam2_video.model.sam2model import SAM2Model
+    ALL = ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder", "prompt_encoder"]
+    m = SAM2Model(None, "tiny@128", trainable_modules=ALL)
+    rank = m._backbone_grad_rank()
+    never = set(m.never_grad_parameter_names())
+    named = list(m.named_parameters())
+    grad_names = [n for n, p in named if p.requires_grad and n not in never]
+    a = ParamArena(named, grad_names, torch.float32, torch.device("cpu"), tail_rank=rank)
+    nst = len(m.image_encoder.trunk.stage_ends)
+    assert len(a.grad_cuts) == nst + 2 and a.grad_cuts[0] == a.grad_split and a.grad_cuts[-1] == a.n_grad
+    assert all(x <= y for x, y in zip(a.grad_cuts, a.grad_cuts[1:]))
+    by_off = sorted((a.offsets[n], n) for n in a.grad_names)
+    ranks = [rank(n) for _, n in by_off if a.offsets[n] >= a.grad_split]
+    assert None not in ranks and ranks == sorted(ranks)
+    assert all(rank(n) is None for _, n in by_off if a.offsets[n] < a.grad_split)
+    assert rank("sam_mask_decoder.conv_s0.weight") == 0 and rank("image_encoder.neck.convs.0.conv.weight") == 0
+    last_block = m.image_encoder.trunk.stage_ends[-1]
+    assert rank(f"image_encoder.trunk.blocks.{last_block}.mlp.layers.0.weight") == 1
+    assert rank("image_encoder.trunk.blocks.0.norm1.weight") == nst == rank("image_encoder.trunk.patch_embed.proj.weight")
+    for r in range(nst + 1):  # each rank's parameters lie inside its cut range
+        for _, n in by_off:
+            if rank(n) == r:
+                assert a.grad_cuts[r] <= a.offsets[n] < a.grad_cuts[r + 1], (n, r)
+    assert rank("memory_attention.layers.0.linear1.weight") is None
