@@ -64,12 +64,17 @@ def parse():
 
 
 # algorithmic flops per profiler record (SURVEY.md §8(d) counting: attention backward = 2 x forward,
-# the QK^T recompute of the flash backward is not counted)
+# the QK^T recompute of the flash backward is not counted).  V-fold records (m[5] = 1000 + DV: the
+# memory cross-attention with its 64-wide value, flash.hip) are priced at the work the fold
+# performs: forward 2 (D + DV) per (query, key), backward 2 (2 D + DV) (dP over DV, dQ, dK; no dV)
 def record_flops(kind, m):
     if kind == 4:
         b, M, N, K = m[1:5]
         return 2.0 * b * M * N * K
     bh, lq, lk, d = m[1:5]
+    if m[5] >= 1000:
+        dv = m[5] - 1000
+        return 2.0 * bh * lq * lk * ((d + dv) if kind == 1 else (2 * d + dv))
     return (4.0 if kind == 1 else 8.0) * bh * lq * lk * d
 
 
@@ -83,6 +88,10 @@ def record_bytes(kind, m):
         cb = 4 if lay == 4 else 2
         return float(b) * (ab * (M * K + N * K) + cb * M * N)
     bh, lq, lk, d = m[1:5]
+    if m[5] >= 1000:  # V-fold: q, k (d wide), memory and u' (dv / dv + 8 wide); backward + dO', dQ, dK
+        dv = m[5] - 1000
+        fwd = 2.0 * bh * (lq * d + lk * d + lk * dv + lq * (dv + 8))
+        return fwd if kind == 1 else 2.0 * fwd
     per = 2.0 * (2 * bh * lq * d + 2 * bh * lk * d)
     return per if kind == 1 else 2.0 * per
 
@@ -165,9 +174,14 @@ def kernel_table(recs):
                    f"b{b} {M}x{N}x{K} {'AB'[0] if lay & 2 else 'a'}{'B' if lay & 1 else 'b'}")
             fl = 2.0 * b * M * N * K
         else:
-            bh, lq, lk, d, _ = m[1:]
-            key = ("attn_fwd" if kind == 1 else "attn_bwd", f"bh{bh} {lq}x{lk} d{d}")
-            fl = (4.0 if kind == 1 else 10.0) * bh * lq * lk * d
+            bh, lq, lk, d, tag = m[1:]
+            if tag >= 1000:  # V-fold (executed work incl. the backward's QK^T recompute)
+                dv = tag - 1000
+                key = ("attn_fwd" if kind == 1 else "attn_bwd", f"bh{bh} {lq}x{lk} d{d} vfold{dv}")
+                fl = 2.0 * bh * lq * lk * ((d + dv) if kind == 1 else (3 * d + dv))
+            else:
+                key = ("attn_fwd" if kind == 1 else "attn_bwd", f"bh{bh} {lq}x{lk} d{d}")
+                fl = (4.0 if kind == 1 else 10.0) * bh * lq * lk * d
         a = agg.setdefault(key, [0, 0.0, 0.0])
         a[0] += 1
         a[1] += ms
