@@ -131,9 +131,10 @@ def test_validation_step_is_deterministic():
 
 @pytest.mark.parametrize("graph", [False, True])
 def test_split_backward_equals_single_backward(graph):
-    """the two-phase backward of the DDP overlap (tracking gradients first, then the image
-    encoder's as a second graph) leaves the same gradient arena as one backward; the image
-    encoder's gradients sit at the arena tail (grad_split)"""
+    """the staged backward of the DDP overlap (tracking gradients first, then the backbone's in
+    segments -- conv_s0 / conv_s1 + neck, Hiera stages last to first -- one graph each) leaves the
+    same gradient arena as one backward; the backbone's gradients sit at the arena tail
+    (grad_split), conv_s0 / conv_s1 with them"""
     from sam2_video.training.trainer import StepRunner
     clips = _clips([3, 4], 3, 256, 4, 3)
     res = []
@@ -141,7 +142,9 @@ def test_split_backward_equals_single_backward(graph):
         m = _module("base_plus", 256, dtype="fp32", dropout=0.0)
         arena = m.model.arena
         names = [n for n in arena.grad_names if arena.offsets[n] >= arena.grad_split]
-        assert names and all(n.startswith("image_encoder.") for n in names)
+        assert names and all(n.startswith(("image_encoder.", "sam_mask_decoder.conv_s0.", "sam_mask_decoder.conv_s1."))
+                             for n in names)
+        assert any(n.startswith("sam_mask_decoder.conv_s0.") for n in names)
         run = StepRunner(m, total_steps=2, graph=graph, split_backward=split)
         assert run.overlap == split
         for c in clips:
