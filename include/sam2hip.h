@@ -406,6 +406,23 @@ int s2h_grad_norm(int64_t n, const float* g, float* partial_ws, float max_norm, 
 int s2h_adamw(int64_t n, float* p, const float* g, float* m, float* v, const float* clip, float lr,
               float beta1, float beta2, float eps, float wd, int step, void* bf16_shadow, hipStream_t st);
 
+/* ---------------------------------------------------------------- prompt stage (host CPU code)
+ * The per-step host work of prepare_prompt_inputs (sam2model.py:181-236) on frame 0, native and
+ * multi-threaded (one thread per category, `threads` at most); no device calls.
+ * s2h_prompt_objects replaces cat_to_obj_mask + find_connected_components (masks.py:13-50, the
+ * cv2 5x5-ellipse opening + 8-connected components): N category masks [N, H, W] of 0/1 bytes ->
+ * objects numbered category-major, raster order of first pixel within a category; obj_cat[o],
+ * stats[o * 7 ..] = (count, sum_y, sum_x, y_min, y_max, x_min, x_max), optional lab[N, H, W] =
+ * 1 + object index (0 background).  Returns 0, 2 with *n_obj = the count needed when it
+ * exceeds max_obj, 1 on bad arguments.
+ * s2h_prompt_object_masks: lab -> float object masks [n_obj, H, W] (cat_to_obj_mask's output).
+ * s2h_mask_moments: the same 7 moments of B whole masks [B, H, W] -- the centre-of-mass click of
+ * generate_point_prompt (prompts.py:13-75) and the corners of generate_box_prompt (prompts.py:78-97). */
+int s2h_prompt_objects(int N, int H, int W, const uint8_t* masks, int max_obj, int* n_obj, int32_t* obj_cat,
+                       int64_t* stats, int32_t* lab, int threads);
+int s2h_prompt_object_masks(int N, int H, int W, const int32_t* lab, int n_obj, float* out, int threads);
+int s2h_mask_moments(int B, int H, int W, const uint8_t* masks, int64_t* stats, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -300,6 +300,18 @@ class SAM2Model(SAM2Base):
         result as input."""
         hm = getattr(input, "host_masks0", None) if start_frame_idx == 0 else None
         masks0 = (hm if hm is not None else input.masks[start_frame_idx]).unsqueeze(1)
+        center_only = (self.prompt_type == "point" and self.num_pos_points == 1 and self.num_neg_points == 0
+                       and self.include_center)
+        if center_only or self.prompt_type == "box":
+            # the clicks need only the objects' moments: no object masks are materialised
+            from ..utils.masks import object_moments
+            from ..utils.prompts import box_prompt_from_moments, center_prompt_from_moments
+            cats, st, _ = object_moments(masks0[:, 0])
+            if len(cats) == 0:
+                raise ValueError("cat_to_obj_mask: no objects found in category masks (fail-fast)")
+            obj_to_cat, num_categories, O = cats.tolist(), int(masks0.shape[0]), len(cats)
+            points, labels = (center_prompt_from_moments if center_only else box_prompt_from_moments)(st)
+            return self._point_plan(start_frame_idx, obj_to_cat, num_categories, points, labels)
         obj_masks, obj_to_cat, num_categories = utils.cat_to_obj_mask(masks0)
         O = len(obj_to_cat)
         pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
@@ -312,13 +324,16 @@ class SAM2Model(SAM2Base):
             return {"start_frame_idx": start_frame_idx, "obj_to_cat": obj_to_cat, "num_categories": num_categories,
                     "points": None, "labels": None, "mask": True,
                     "host": (obj_masks.reshape(O, *obj_masks.shape[-2:]).float(), score, pe1, lab1)}
-        if self.prompt_type == "box":
-            points, labels = utils.generate_box_prompt(obj_masks)
-        else:
-            points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
-                                                         num_neg_points=self.num_neg_points,
-                                                         include_center=self.include_center)
+        points, labels = utils.generate_point_prompt(obj_masks, num_pos_points=self.num_pos_points,
+                                                     num_neg_points=self.num_neg_points,
+                                                     include_center=self.include_center)
+        return self._point_plan(start_frame_idx, obj_to_cat, num_categories, points, labels)
+
+    def _point_plan(self, start_frame_idx, obj_to_cat, num_categories, points, labels):
+        O = len(obj_to_cat)
         pe0, lab0 = self.sam_prompt_encoder.host_points(points, labels, pad=True)
+        pe1, lab1 = self.sam_prompt_encoder.host_points(torch.zeros(O, 1, 2), -torch.ones(O, 1, dtype=torch.int32),
+                                                        pad=True)
         return {"start_frame_idx": start_frame_idx, "obj_to_cat": obj_to_cat, "num_categories": num_categories,
                 "points": points, "labels": labels, "host": (pe0, lab0, pe1, lab1)}
 

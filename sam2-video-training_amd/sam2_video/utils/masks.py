@@ -2,48 +2,95 @@
 
 * find_connected_components / cat_to_obj_mask (masks.py:13-50): host-side, once
   per clip on frame 0 -- the 5x5 ellipse opening (erode with +inf border,
-  dilate with -inf border) and 8-connected labelling in raster order, restated
-  on scipy.ndimage (cv2 is not a dependency of this build).
+  dilate with -inf border) and 8-connected labelling in raster order -- in the
+  library's native host code (csrc/prompts_host.cpp: separable byte passes and a
+  union-find labelling, one thread per category).  `object_moments` gives the
+  objects' categories and moments without materialising their masks (the point
+  and box prompts need only those).
 * merge_object_results_to_category (masks.py:53-213): on the device -- pixelwise
   max over a category's objects for mask logits, sigmoid-mass weighted mean for
   IoU / object-score predictions (differentiable in the weights too).
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import Any, Dict, List, Tuple
 
 import numpy as np
 import torch
-from scipy import ndimage
 
-_ELLIPSE5 = np.ones((5, 5), bool)
-_ELLIPSE5[0, [0, 1, 3, 4]] = False
-_ELLIPSE5[4, [0, 1, 3, 4]] = False
+N_STATS = 7  # count, sum_y, sum_x, y_min, y_max, x_min, x_max
+_THREADS = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else 4))
+
+
+def _u8(m) -> np.ndarray:
+    """0/1 bytes, C-contiguous, of a bool / numeric mask (tensor or array)"""
+    if isinstance(m, torch.Tensor):
+        m = m.detach().cpu()
+        m = (m if m.dtype == torch.bool else m > 0).numpy()
+    else:
+        m = np.asarray(m)
+        m = m if m.dtype == np.bool_ else m > 0
+    return np.ascontiguousarray(m).view(np.uint8)
+
+
+def object_moments(cat_masks, want_labels: bool = False):
+    """N category masks [N, H, W] -> (obj_cat int32 [O], stats int64 [O, 7], labels int32
+    [N, H, W] or None): the objects of cat_to_obj_mask (opening + 8-connected components,
+    category-major, raster order) and their moments."""
+    from ..kernels import _lib
+    m = _u8(cat_masks)
+    N, H, W = m.shape
+    lab = np.empty((N, H, W), np.int32) if want_labels else None
+    cap = 64
+    while True:
+        n = ctypes.c_int(0)
+        cats = np.empty(cap, np.int32)
+        stats = np.empty((cap, N_STATS), np.int64)
+        rc = _lib.lib().s2h_prompt_objects(N, H, W, m.ctypes.data, cap, ctypes.byref(n), cats.ctypes.data,
+                                           stats.ctypes.data, lab.ctypes.data if lab is not None else None, _THREADS)
+        if rc == 2:
+            cap = n.value
+            continue
+        if rc != 0:
+            raise ValueError(f"s2h_prompt_objects: bad arguments (rc {rc}) for masks of shape {m.shape}")
+        return cats[:n.value], stats[:n.value], lab
+
+
+def object_masks(labels: np.ndarray, n_obj: int) -> torch.Tensor:
+    """labels of object_moments -> float object masks [O, H, W]"""
+    from ..kernels import _lib
+    N, H, W = labels.shape
+    out = torch.empty(n_obj, H, W, dtype=torch.float32)
+    _lib.call("s2h_prompt_object_masks", N, H, W, labels.ctypes.data, n_obj, out.data_ptr(), _THREADS)
+    return out
+
+
+def mask_moments(masks) -> np.ndarray:
+    """B whole masks [B, H, W] -> int64 [B, 7] moments (no opening)"""
+    from ..kernels import _lib
+    m = _u8(masks)
+    B, H, W = m.shape
+    stats = np.empty((B, N_STATS), np.int64)
+    _lib.call("s2h_mask_moments", B, H, W, m.ctypes.data, stats.ctypes.data, _THREADS)
+    return stats
 
 
 def find_connected_components(mask: torch.Tensor) -> List[torch.Tensor]:
-    m = mask.detach().cpu().numpy().astype(bool)
-    m = ndimage.binary_erosion(m, structure=_ELLIPSE5, border_value=1)
-    m = ndimage.binary_dilation(m, structure=_ELLIPSE5, border_value=0)
-    lab, n = ndimage.label(m, structure=np.ones((3, 3), int))
-    return [torch.from_numpy((lab == i).astype(np.float32)) for i in range(1, n + 1)]
+    """masks.py:13-28: the opened mask's 8-connected components, raster order, as float masks"""
+    m = _u8(mask)
+    _, stats, lab = object_moments(m[None], want_labels=True)
+    return list(object_masks(lab, len(stats)).unbind(0))
 
 
 def cat_to_obj_mask(cat_frame_masks: torch.Tensor) -> Tuple[torch.Tensor, List[int], int]:
     """[N, 1, H, W] category masks -> ([O, 1, H, W] float object masks (host), obj_to_cat, N)"""
     N = int(cat_frame_masks.shape[0])
-    cm = cat_frame_masks.detach().cpu()
-    obj_to_cat, objs = [], []
-    for c in range(N):
-        m = cm[c][0] > 0
-        if not bool(m.any()):
-            continue
-        for comp in find_connected_components(m):
-            objs.append(comp)
-            obj_to_cat.append(c)
-    if not objs:
+    cats, stats, lab = object_moments(_u8(cat_frame_masks)[:, 0], want_labels=True)
+    if len(cats) == 0:
         raise ValueError("cat_to_obj_mask: no objects found in category masks (fail-fast)")
-    return torch.stack(objs).unsqueeze(1), obj_to_cat, N
+    return object_masks(lab, len(cats)).unsqueeze(1), cats.tolist(), N
 
 
 _GROUP_CACHE = {}
