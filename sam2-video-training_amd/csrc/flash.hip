@@ -347,8 +347,11 @@ static void flash_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
 }
 
 static int g_flash_enabled = 1;
+// bits 1+ of the flash switch select older kernel variants for A/B runs (flash_bwd.hip)
+int s2h_flash_variant() { return g_flash_enabled >> 1; }
 
-// A/B switch for tests and benchmarks: 0 routes every attention to the generic kernels.
+// A/B switch for tests and benchmarks: 0 routes every attention to the generic kernels;
+// 3 keeps the flash path with the one-wave-per-SIMD V-fold dK kernel (flash_bwd_dkv32_kernel).
 extern "C" int s2h_attn_config(int flash_enable) {
   const int prev = g_flash_enabled | (g_flash_fwd_target << 8);
   g_flash_enabled = flash_enable & 0xff;

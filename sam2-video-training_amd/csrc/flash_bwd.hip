@@ -18,9 +18,12 @@
 // du' = dO [Wv | bv] = [dO Wv | dO . bv] (72 columns): dD = du M^T + dr (dr = du'[:, 64]),
 // Di = rowsum(dO * O) = du . u + dr * rowsum(D) from u' = [D M | rowsum(D)].  No dV: the bank is
 // detached (sam2model.py:345-358) and the value projection's weight gradient is dO^T u'.
+#include <type_traits>
+
 #include "flash_common.h"
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
+int s2h_flash_variant();  // flash.hip: A/B selection of older kernels
 void s2h_prof_end(int slot, hipStream_t st);
 
 struct FlashBwdArgs {
@@ -647,6 +650,173 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     }
 }
 
+// ------------------------------------------------------------------ dK of the V-fold, two waves per SIMD
+// The V-fold backward has no dV and a 64-wide value (the memory bank M), so a 16-key wave holds
+// K^T fragments (32 VGPRs), M^T fragments (8) and its dK^T accumulators (64): 8 waves x 16 keys run
+// two waves per SIMD (<= 256 VGPRs) and each wave's softmax / dropout VALU issues under its partner's
+// MFMAs.  (flash_bwd_dkv32_kernel<256, DROP, true, 64>, one wave per SIMD on 32x32x16, measured
+// 15 % MFMA-busy at 13.7 VALU per MFMA: its 512-register allocation moved S / dP through the
+// accumulator file every tile and each swizzled fragment read was waited for alone.)
+// Per 32-query tile and wave: S = Q K^T (16 MFMA), dP = du M^T (4), dK^T += Q^T dS (16).  Q and du
+// tiles sit in padded images (one base register + immediate offsets for every fragment, conflict-
+// free b128 and transposing reads); the row constants (lse, Di, dr = du'[:, 64], keep words
+// [word][query]) are DMA'd beside them so a lane reads its 4 consecutive queries with one b128.
+// DMA instructions per stage and wave: w0 Q x3; w1..5 Q x2 + du x1; w6 Q x2 + lse|Di; w7 Q x2 + dr
+// (+ 2 keep-word pieces with the bitmap).
+template <int DROP>
+__global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
+  static_assert(DROP != DROP_HASH, "the V-fold forward always writes the keep bitmap");
+  constexpr int DP = 256, DV = 64, QT = 32, NW = 8;
+  using IQ = PadImg<DP, QT, NW>;  // 32 rows x 544 B, 17 pieces
+  using IG = PadImg<DV, QT, 1>;   // 32 rows x 160 B, 5 pieces (waves 1..5 take one each)
+  constexpr int RB_LSE = 0, RB_DI = 128, RB_DR = 256, RB_KEEP = 384;  // row block: + keep [4 words][32 q]
+  constexpr int RB = 384 + 512;
+  constexpr int STAGE = IQ::TILEB + IG::TILEB + RB;
+  constexpr bool bits = DROP == DROP_BITS;
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
+  const WgIdx wi = wg_xcd_order();
+  if (wi.y >= a.BH) return;  // grid padding
+  const int bh = wi.y, b = bh / a.H, h = bh % a.H;
+  const KvFrame fr = kv_frame(a, bh);
+  if (wi.x * (NW * 16) >= fr.Lk) return;  // frame-table launch: past this frame's keys
+  const int key = wi.x * (NW * 16) + w * 16 + kl;
+  const bool kv = key < fr.Lk;
+  const bf16* Q = a.q + b * a.sqb + h * a.sqh;
+  const bf16* G = a.g + b * a.sgb + h * a.sgh;
+  const float* LSE = a.lse + (int64_t)bh * a.Lq;
+  const float* DI = a.di + (int64_t)bh * a.Lq;
+  const int nt = (a.Lq + QT - 1) / QT;
+  const int Lq1 = a.Lq - 1;
+
+  auto issue = [&](char* st, int q0) {
+    // Q pieces w, w + 8 (and 16 on wave 0)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      if (i == 2 && w != 0) break;  // wave-uniform
+      const int piece = i == 2 ? 16 : w + 8 * i;
+      const int slot = piece * 64 + lane;
+      const int row = slot / IQ::SPR, c = slot % IQ::SPR;
+      lds_dma16(Q + (min(q0 + row, Lq1) * (int)a.sql + (c < DP / 8 ? 8 * c : 0)), st + piece * 1024);
+    }
+    char* rb = st + IQ::TILEB + IG::TILEB;
+    if (w >= 1 && w <= 5) {  // du' piece w - 1 (64 value columns; dr comes with the row block)
+      const int piece = w - 1;
+      const int slot = piece * 64 + lane;
+      const int row = slot / IG::SPR, c = slot % IG::SPR;
+      lds_dma16(G + (min(q0 + row, Lq1) * (int)a.sgl + (c < DV / 8 ? 8 * c : 0)), st + IQ::TILEB + piece * 1024);
+    } else if (w == 6) {  // lanes 0..31 lse, 32..63 Di
+      const int qi = min(q0 + (lane & 31), Lq1);
+      lds_dma4((lane < 32 ? LSE : DI) + qi, rb + RB_LSE);
+    } else if (w == 7) {
+      // dr = du'[q, DV] (bf16 in the low half of the word); lanes 32..63 repeat 0..31
+      lds_dma4(G + (min(q0 + (lane & 31), Lq1) * (int)a.sgl + DV), rb + RB_DR);
+      if constexpr (bits) {  // keep words (key / 32) of the block's 128 keys: [word][query]
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int word = min(wi.x * 4 + 2 * j + (lane >> 5), fr.kw - 1);
+          lds_dma4(fr.keep + (int64_t)min(q0 + (lane & 31), Lq1) * fr.kw + word, rb + RB_KEEP + j * 256);
+        }
+      }
+    }
+  };
+  // vmcnt that leaves this wave's DMAs of the next stage in flight
+  auto wait_stage = [&]() {
+    if (bits && w == 7) wait_vmcnt<5>();
+    else wait_vmcnt<3>();
+  };
+
+  issue(smem, 0);
+  bf16x8 kf[DP / 32], vf[DV / 32];  // B operands K^T / M^T: [k = d = 32t + 8g + j][n = key]
+  const int64_t vkey = min(key, fr.Lk - 1);
+#pragma unroll
+  for (int t = 0; t < DP / 32; ++t) kf[t] = *(const bf16x8*)(fr.k + vkey * a.skl + 32 * t + 8 * g);
+#pragma unroll
+  for (int t = 0; t < DV / 32; ++t) vf[t] = *(const bf16x8*)(fr.v + vkey * a.svl + 32 * t + 8 * g);
+  __builtin_amdgcn_s_waitcnt(0xF70);  // retire the fragment loads in the compiler's bookkeeping
+  f32x4 dk[DP / 16];  // dK^T: row d = 16 db + 4g + r, column key
+#pragma unroll
+  for (int d = 0; d < DP / 16; ++d) dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kword = (w & 1) * 16 + kl;  // this lane's bit in its keep word
+  const int kwsel = w >> 1;             // which of the block's 4 words
+
+  for (int it = 0; it < nt; ++it) {
+    const int q0 = it * QT;
+    char* st = smem + (it & 1) * STAGE;
+    if (it + 1 < nt) {
+      issue(smem + ((it + 1) & 1) * STAGE, q0 + QT);
+      wait_stage();
+    } else {
+      wait_vmcnt<0>();
+    }
+    wg_barrier();
+    const char* Qi = st;
+    const char* Gi = st + IQ::TILEB;
+    const char* rb = st + IQ::TILEB + IG::TILEB;
+
+    f32x4 s[2], dp[2];  // row q = 16 qb + 4g + r, column key
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      s[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dp[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const char* qrow = Qi + (16 * qb + kl) * IQ::ROWB + 16 * g;
+      const char* grow = Gi + (16 * qb + kl) * IG::ROWB + 16 * g;
+#pragma unroll
+      for (int t = 0; t < DP / 32; ++t) s[qb] = mfma16(*(const bf16x8*)(qrow + 64 * t), kf[t], s[qb]);
+#pragma unroll
+      for (int t = 0; t < DV / 32; ++t) dp[qb] = mfma16(*(const bf16x8*)(grow + 64 * t), vf[t], dp[qb]);
+    }
+    bf16x8 dsb;  // B operand over 32 queries: k index 8g + j <-> q 16(j >> 2) + 4g + (j & 3)
+    // the query-tail test as a separate code path (an in-line `if` became per-element selects)
+    auto softmax = [&](auto tail) {
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      const int qo = 16 * qb + 4 * g;
+      const float4 l4 = *(const float4*)(rb + RB_LSE + 4 * qo);
+      const float4 d4 = *(const float4*)(rb + RB_DI + 4 * qo);
+      const uint4 r4 = *(const uint4*)(rb + RB_DR + 4 * qo);
+      uint4 k4 = uint4{0u, 0u, 0u, 0u};
+      if constexpr (bits) k4 = *(const uint4*)(rb + RB_KEEP + kwsel * 128 + 4 * qo);
+      const float lt[4] = {l4.x, l4.y, l4.z, l4.w};
+      const float dt[4] = {d4.x, d4.y, d4.z, d4.w};
+      const uint32_t rt[4] = {r4.x, r4.y, r4.z, r4.w};
+      const uint32_t kt[4] = {k4.x, k4.y, k4.z, k4.w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float p = __builtin_amdgcn_exp2f(fmaf(s[qb][r], a.sl2, -lt[r] * FL_LOG2E));
+        if constexpr (decltype(tail)::value) p = q0 + qo + r < a.Lq ? p : 0.f;
+        const float dpr = dp[qb][r] + __uint_as_float(rt[r] << 16);
+        float dsv;
+        if constexpr (bits) {
+          const float dpd = (kt[r] >> kword) & 1u ? dpr : 0.f;
+          dsv = p * fmaf(dpd, a.inv_keep, -dt[r]);
+        } else {
+          dsv = p * (dpr - dt[r]);
+        }
+        dsb[4 * qb + r] = (bf16)dsv;
+      }
+    }
+    };
+    if (q0 + QT <= a.Lq) softmax(std::false_type{});
+    else softmax(std::true_type{});
+    // dK^T += Q^T dS (Q^T fragments by transposing reads of the padded Q image)
+#pragma unroll
+    for (int d = 0; d < DP / 16; ++d) dk[d] = mfma16(tr_frag_pad<IQ::ROWB>(Qi, 0, 16 * d, lane), dsb, dk[d]);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wg_barrier();
+  }
+
+  if (!kv) return;
+  bf16* DK = fr.dk + (int64_t)key * a.sdkl;
+#pragma unroll
+  for (int d = 0; d < DP / 16; ++d) {
+    bf16 t4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) t4[e] = (bf16)(dk[d][e] * a.scale);
+    *(uint2*)(DK + 16 * d + 4 * g) = *(const uint2*)t4;
+  }
+}
+
 // dK = scale * sum_s partial_dK[s], dV = sum_s partial_dV[s]; 4 consecutive d per thread
 template <int DP>
 __global__ __launch_bounds__(256) void flash_bwd_dkv_combine_kernel(FlashBwdArgs a) {
@@ -720,6 +890,13 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
                        st, a);
   if constexpr (DP == 256) {
     const dim3 gk((a.Lk + 127) / 128, pad_bh8(a.BH), a.kv_splits);
+    if constexpr (DV == 64) {  // V-fold: dK only, two waves per SIMD (variant 1: the 32x32 kernel below)
+      if (drop != DROP_HASH && a.kv_splits == 1 && (s2h_flash_variant() & 1) == 0) {
+        if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkf_kernel<DROP_NONE>), gk, dim3(512), 0, st, a);
+        else hipLaunchKernelGGL((flash_bwd_dkf_kernel<DROP_BITS>), gk, dim3(512), 0, st, a);
+        return (int)hipGetLastError();
+      }
+    }
     if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV>), gk, dim3(256), 0, st, a);
     else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV>), gk, dim3(256), 0, st, a);
     else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH, true, DV>), gk, dim3(256), 0, st, a);

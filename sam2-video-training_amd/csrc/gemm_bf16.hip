@@ -204,8 +204,16 @@ struct GImg {
 
   // K-contiguous: chunk ^= (row >> 1) mod CPR -- conflict-free ds_read_b128 fragments for
   // both 128-B (BK 64) and 64-B (BK 32) image rows (checked against the b128 lane groups)
+  // Row-contiguous: a transposing fragment read's 32-lane half covers image rows k = 8g + q
+  // (g = 0, 1; q = 0..3) x two 16-B chunks, so the XOR must separate k and k + 8 as well:
+  //   256-/512-B rows (one row per bank row): chunk ^= 2 (k & 3) | 8 ((k >> 3) & 1)
+  //   128-B rows (two rows per bank row, k & 1 picks the half): chunk ^= 2 ((k >> 1) & 1) | 4 ((k >> 3) & 1)
+  // (the round-2 form 2 (k & 3) mapped k and k + 8 onto the same banks: PMC 1.65 conflict cycles
+  // per LDS instruction on the weight-gradient tiles)
   __device__ static __forceinline__ int swz(int r, int c) {
-    return KC ? (c ^ ((r >> 1) & (CPR - 1))) : (c ^ (2 * (r & 3)));
+    if constexpr (KC) return c ^ ((r >> 1) & (CPR - 1));
+    if constexpr (RB >= 256) return c ^ ((2 * (r & 3)) | (8 * ((r >> 3) & 1)));
+    return c ^ ((2 * ((r >> 1) & 1)) | (4 * ((r >> 3) & 1)));
   }
   // DMA rows/k of the tile at (row0, k0); rows >= nrows / k >= kend are clamped to valid
   // addresses (garbage rows are never stored; the K tail is zeroed in LDS afterwards)

@@ -182,3 +182,52 @@ def test_vfold_step_matches_unfolded_step_bf16(monkeypatch):
     flat0 = torch.cat([v.flatten() for v in g0.values()])
     flat1 = torch.cat([v.flatten() for v in g1.values()])
     assert torch.nn.functional.cosine_similarity(flat0, flat1, dim=0).item() >= 0.99
+
+
+@pytest.mark.parametrize("Lq,lks,p_drop", [(200, [300, 700], 0.1), (256, [1028, 129], 0.0)])
+def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
+    """the two-waves-per-SIMD V-fold dK kernel (flash_bwd_dkf_kernel, default) against the
+    one-wave-per-SIMD 32x32 kernel it replaced (s2h_attn_config(3)) on the same frame table: dK
+    equal to fp32-summation-order rounding (query tails, key tails, keep bitmap on and off); dQ is
+    the same kernel in both and must be bit-identical"""
+    from sam2_video.kernels._lib import lib
+    ops = _ops()
+    B, seed = 3, 21
+    fr = [_inputs(B, Lq, lk, 30 + i) for i, lk in enumerate(lks)]
+    scale = 256 ** -0.5
+    idx0, koff, acc_e, acc_w, us, lses, keeps = [], [], 0, 0, [], [], []
+    for (q, k, m, _, _), lk in zip(fr, lks):
+        idx0.append(acc_e)
+        koff.append(acc_w)
+        u = torch.empty(B, Lq, 1, 72, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B, 1, Lq, device=DEV)
+        keep = torch.zeros(ops.keep_words(B, 1, Lq, lk), device=DEV, dtype=torch.int32)
+        ops.attn_fwd_vfold(q, k, m, u, lse, scale, p_drop, seed, idx0=acc_e, keep=keep if p_drop > 0 else None)
+        us.append(u)
+        lses.append(lse)
+        keeps.append(keep)
+        acc_e += B * Lq * lk
+        acc_w += keep.numel()
+    du = torch.cat([torch.randn(B, Lq, 1, 72, device=DEV).to(torch.bfloat16) for _ in lks])
+    q_all = torch.cat([f[0] for f in fr])
+    k_all = torch.cat([f[1].reshape(-1, 1, 256) for f in fr])
+    m_all = torch.cat([f[2].reshape(-1, 1, 64) for f in fr])
+    krow = [0, B * lks[0]]
+    out = {}
+    prev = lib().s2h_attn_config(1)
+    try:
+        for variant in (1, 3):
+            lib().s2h_attn_config(variant)
+            dq = torch.empty_like(q_all)
+            dk = torch.full_like(k_all, float("nan"))
+            ops.flash_bwd_frames_vfold(2, B, lks, krow, idx0, q_all, k_all, m_all, torch.cat(us), du,
+                                       torch.cat(lses), dq, dk, scale, p_drop, seed,
+                                       keep=torch.cat(keeps) if p_drop > 0 else None,
+                                       koff=koff if p_drop > 0 else None)
+            torch.cuda.synchronize()
+            out[variant] = (dq, dk)
+    finally:
+        lib().s2h_attn_config(prev)
+    assert torch.equal(out[1][0], out[3][0])
+    assert not torch.isnan(out[1][1]).any()
+    _close(out[1][1], out[3][1], 1e-2, "dk two-wave vs one-wave")
