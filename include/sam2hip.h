@@ -85,10 +85,16 @@ int s2h_gemm(int dt_ab, int dt_c, int batch, int M, int N, int K,
 /* A/B switch (tests, benchmarks) for the bf16 GEMM tiling; returns the previous setting.
  * 0 = automatic by shape, -1 = register-staged kernel, LDS-DMA tilings: 1 = 64x64,
  * 2 = 128x128, 3 = 128x128 with a 3-deep ring, 4 = 256x128, 5 = 256x256, 6 = 128x256,
- * 7 = 128x64, 8 = 64x128, 9 = 64x64 with a 3-deep ring;
+ * 7 = 128x64, 8 = 64x128, 9 = 64x64 with a 3-deep ring, 10 = 64x64 32-deep 4-deep ring,
+ * 11 / 12 / 13 = 128x64 32-deep 3- / 4-deep ring and 64-deep 3-deep ring, 14 / 15 = 256x128 on 4 waves
+ * (32-deep 3-deep ring / 64-deep 2-deep), 16 = 128x128 32-deep 3-deep ring, 17 = 256x64 on 4 waves;
  * bits 8+ are measurement-only ablations of the LDS-DMA kernel (results are wrong):
  * 256 = skip the epilogue stores, 512 = skip the MFMAs. */
 int s2h_gemm_config(int cfg);
+
+/* A/B knob (tests, benchmarks): workgroups a split-K weight-gradient GEMM aims at (default 768;
+ * t <= 0 leaves it unchanged); returns the previous value. */
+int s2h_gemm_split_target(int t);
 
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),

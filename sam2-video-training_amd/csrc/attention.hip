@@ -543,8 +543,17 @@ __global__ __launch_bounds__(AttnCfg<T>::NW_DKV * 64) void attn_bwd_dkv_kernel(A
 // are safe.  K / Q rows feed the MFMA B operand straight from global (16-B loads); only
 // the operands that need a transposed (key-major or query-major) fragment go through
 // wave-private LDS.
-template <typename T, int DP>
-__global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
+// sum of the NW waves' partials of one element (stride = floats per wave's partial block)
+template <int NW>
+__device__ __forceinline__ float mrg_sum(const float* p, int stride) {
+  float s = 0.f;
+#pragma unroll
+  for (int u = 0; u < NW; ++u) s += p[u * stride];
+  return s;
+}
+
+template <typename T, int DP, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void attn_fwd_fewq_kernel(AttnArgs a) {
   if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using MF = Mfma<T>;
   constexpr int BKEY = 64;
@@ -552,8 +561,8 @@ __global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
   constexpr int VS = BKEY + VEC, PS = BKEY + VEC;
   constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16, NPF = BKEY / MF::KSTEP;
   constexpr int WL = DP * VS + 16 * PS;  // wave-private LDS elements
-  __shared__ __attribute__((aligned(16))) T smem[4 * WL];
-  __shared__ float mrg[4][16][DP + 2];
+  __shared__ __attribute__((aligned(16))) T smem[NW * WL];
+  __shared__ float mrg[NW][16][DP + 2];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
@@ -579,8 +588,8 @@ __global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
   for (int r = 0; r < 4; ++r) { m[r] = -INFINITY; l[r] = 0.f; }
 
   const int nkt = (a.Lk + BKEY - 1) / BKEY;
-  for (int it = 0; it < (nkt + 3) / 4; ++it) {
-    const int kt = it * 4 + w;
+  for (int it = 0; it < (nkt + NW - 1) / NW; ++it) {
+    const int kt = it * NW + w;
     const int k0 = kt * BKEY;
     if (kt < nkt) {
       lds_load_rows_t<T, BKEY, DP, VS, 64>(Vt, V, a.svl, k0, a.Lk, a.D, lane);
@@ -661,15 +670,15 @@ __global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
   }
   __syncthreads();
   T* O = (T*)a.o + b * a.sob + h * a.soh;
-  for (int e = tid; e < 16 * DP; e += 256) {
+  for (int e = tid; e < 16 * DP; e += NW * 64) {
     const int row = e / DP, col = e % DP;
     if (row >= a.Lq) continue;
     float M = -INFINITY;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) M = fmaxf(M, mrg[u][row][DP]);
+    for (int u = 0; u < NW; ++u) M = fmaxf(M, mrg[u][row][DP]);
     float L = 0.f, acc = 0.f;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < NW; ++u) {
       const float f = exp2f(mrg[u][row][DP] - M);  // waves without keys: m = -inf -> 0
       L += mrg[u][row][DP + 1] * f;
       acc += mrg[u][row][col] * f;
@@ -679,8 +688,8 @@ __global__ __launch_bounds__(256) void attn_fwd_fewq_kernel(AttnArgs a) {
   }
 }
 
-template <typename T, int DP>
-__global__ __launch_bounds__(256) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
+template <typename T, int DP, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
   if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using MF = Mfma<T>;
   constexpr int BKEY = 64;
@@ -688,8 +697,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
   constexpr int TS = BKEY + VEC, PS = BKEY + VEC;
   constexpr int NQF = DP / MF::KSTEP, NB = BKEY / 16, ND = DP / 16, NPF = BKEY / MF::KSTEP;
   constexpr int WL = DP * TS + 16 * PS;
-  __shared__ __attribute__((aligned(16))) T smem[4 * WL];
-  __shared__ float mrg[4][16][DP + 1];
+  __shared__ __attribute__((aligned(16))) T smem[NW * WL];
+  __shared__ float mrg[NW][16][DP + 1];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
@@ -723,8 +732,8 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
   for (int d = 0; d < ND; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nkt = (a.Lk + BKEY - 1) / BKEY;
-  for (int it = 0; it < (nkt + 3) / 4; ++it) {
-    const int kt = it * 4 + w;
+  for (int it = 0; it < (nkt + NW - 1) / NW; ++it) {
+    const int kt = it * NW + w;
     const int k0 = kt * BKEY;
     if (kt < nkt) {
       lds_load_rows_t<T, BKEY, DP, TS, 64>(Kt, K, a.skl, k0, a.Lk, a.D, lane);
@@ -771,16 +780,16 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_fewq_kernel(AttnArgs a) {
     for (int d = 0; d < ND; ++d) mrg[w][(lane >> 4) * 4 + r][d * 16 + (lane & 15)] = dq[d][r];
   __syncthreads();
   T* dQ = (T*)a.dq + b * a.sdqb + h * a.sdqh;
-  for (int e = tid; e < 16 * DP; e += 256) {
+  for (int e = tid; e < 16 * DP; e += NW * 64) {
     const int row = e / DP, col = e % DP;
     if (row < a.Lq && col < a.D)
       dQ[(int64_t)row * a.sdql + col] =
-          from_f32<T>((mrg[0][row][col] + mrg[1][row][col] + mrg[2][row][col] + mrg[3][row][col]) * a.scale);
+          from_f32<T>(mrg_sum<NW>(&mrg[0][row][col], 16 * (DP + 1)) * a.scale);
   }
 }
 
-template <typename T, int DP>
-__global__ __launch_bounds__(256) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
+template <typename T, int DP, int NW = 4>
+__global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
   if (a.p_drop > 0.f) a.seed = s2h_seed(a.seed, a.seed_off);
   using MF = Mfma<T>;
   constexpr int BQ = sizeof(T) == 2 ? 64 : 32;
@@ -788,9 +797,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
   constexpr int KS = DP + VEC, QS = BQ + VEC;
   constexpr int NKF = DP / MF::KSTEP, NB = BQ / 16, ND = DP / 16, NPF = BQ / MF::KSTEP;
   constexpr int WL = 2 * DP * QS + 2 * 16 * QS;
-  __shared__ __attribute__((aligned(16))) T smem[2 * 16 * KS + 4 * WL];
-  __shared__ float stat[4][2 * BQ];
-  __shared__ float mrg[4][16][2 * DP];
+  __shared__ __attribute__((aligned(16))) T smem[2 * 16 * KS + NW * WL];
+  __shared__ float stat[NW][2 * BQ];
+  __shared__ float mrg[NW][16][2 * DP];
   T* Kn = smem;
   T* Vn = Kn + 16 * KS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -811,15 +820,15 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
   const uint32_t thresh = (uint32_t)(a.p_drop * 4294967296.0);
   const float inv_keep = drop ? 1.f / (1.f - a.p_drop) : 1.f;
 
-  lds_load_rows<T, 16, DP, KS, 256>(Kn, K, a.skl, 0, a.Lk, a.D, tid);
-  lds_load_rows<T, 16, DP, KS, 256>(Vn, V, a.svl, 0, a.Lk, a.D, tid);
+  lds_load_rows<T, 16, DP, KS, NW * 64>(Kn, K, a.skl, 0, a.Lk, a.D, tid);
+  lds_load_rows<T, 16, DP, KS, NW * 64>(Vn, V, a.svl, 0, a.Lk, a.D, tid);
   f32x4 dk[ND], dv[ND];
 #pragma unroll
   for (int d = 0; d < ND; ++d) { dk[d] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[d] = dk[d]; }
 
   const int nqt = (a.Lq + BQ - 1) / BQ;
-  for (int it = 0; it < (nqt + 3) / 4; ++it) {
-    const int qt = it * 4 + w;
+  for (int it = 0; it < (nqt + NW - 1) / NW; ++it) {
+    const int qt = it * NW + w;
     const int q0 = qt * BQ;
     __syncthreads();  // Kn/Vn loaded (first pass); previous tile's reads done
     if (qt < nqt) {
@@ -891,11 +900,11 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_fewk_kernel(AttnArgs a) {
   __syncthreads();
   T* dK = (T*)a.dk + b * a.sdkb + h * a.sdkh;
   T* dV = (T*)a.dv + b * a.sdvb + h * a.sdvh;
-  for (int e = tid; e < 16 * DP; e += 256) {
+  for (int e = tid; e < 16 * DP; e += NW * 64) {
     const int key = e / DP, col = e % DP;
     if (key < a.Lk && col < a.D) {
-      const float sk = mrg[0][key][col] + mrg[1][key][col] + mrg[2][key][col] + mrg[3][key][col];
-      const float sv = mrg[0][key][DP + col] + mrg[1][key][DP + col] + mrg[2][key][DP + col] + mrg[3][key][DP + col];
+      const float sk = mrg_sum<NW>(&mrg[0][key][col], 16 * 2 * DP);
+      const float sv = mrg_sum<NW>(&mrg[0][key][DP + col], 16 * 2 * DP);
       dK[(int64_t)key * a.sdkl + col] = from_f32<T>(sk * a.scale);
       dV[(int64_t)key * a.sdvl + col] = from_f32<T>(sv);
     }
@@ -913,7 +922,9 @@ static int attn_fwd_launch(const AttnArgs& a, hipStream_t st) {
   const int slot = s2h_prof_begin(st, 1, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, sizeof(T));
   if constexpr (DP <= 64) {
     if (attn_fewq(a)) {
-      hipLaunchKernelGGL((attn_fwd_fewq_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
+      // bf16 head dim <= 16 (the decoder's 8 heads x 16): 16 waves, one 64-key tile each at Lk 1024
+      if constexpr (sizeof(T) == 2 && DP == 32) hipLaunchKernelGGL((attn_fwd_fewq_kernel<T, DP, 16>), dim3(a.B * a.H), dim3(1024), 0, st, a);
+      else hipLaunchKernelGGL((attn_fwd_fewq_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
       s2h_prof_end(slot, st);
       return (int)hipGetLastError();
     }
@@ -942,11 +953,13 @@ static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
   bool done_dq = false, done_dkv = false;
   if constexpr (DP <= 64) {
     if (attn_fewq(a)) {
-      hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
+      if constexpr (sizeof(T) == 2 && DP == 32) hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<T, DP, 16>), dim3(a.B * a.H), dim3(1024), 0, st, a);
+      else hipLaunchKernelGGL((attn_bwd_dq_fewq_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
       done_dq = true;
     }
     if (attn_fewk(a)) {
-      hipLaunchKernelGGL((attn_bwd_dkv_fewk_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
+      if constexpr (sizeof(T) == 2 && DP == 32) hipLaunchKernelGGL((attn_bwd_dkv_fewk_kernel<T, DP, 8>), dim3(a.B * a.H), dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((attn_bwd_dkv_fewk_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
       done_dkv = true;
     }
   }

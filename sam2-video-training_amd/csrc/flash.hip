@@ -130,6 +130,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
 
     // ---- S^T = K Q^T: four 16-key blocks, key = 16*kb + 4g + r on the accumulator row
     f32x4 s[4];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -140,6 +141,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         s[kb] = mfma16(kf, qf[t], s[kb]);
       }
     }
+    sched_reads_ahead<4 * C::NT, 4, 1>();  // fragment reads 4 ahead of their MFMAs
+    __builtin_amdgcn_sched_barrier(0);
     // ---- online softmax (lane-local query row; keys spread over the 4 lane groups)
     float mx = -INFINITY;
     if (k0 + C::KT <= a.Lk) {  // full tile (wave-uniform): no key mask
@@ -239,6 +242,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
       for (int j = 0; j < 8; ++j) pb[c][j] = (bf16)s[2 * c + (j >> 2)][j & 3];
 
     // ---- O^T += V^T P^T, V^T fragments by transposing LDS reads (same key permutation)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int r0 = 32 * c + 4 * g + qq;
@@ -251,6 +255,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         o[d] = mfma16(__builtin_bit_cast(bf16x8, cat), pb[c], o[d]);
       }
     }
+    sched_reads_ahead<2 * NDV, 4, 2>();
+    __builtin_amdgcn_sched_barrier(0);
     // every wave done reading this stage before it is refilled (LDS reads retired first)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();

@@ -212,6 +212,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     wg_barrier();
 
     f32x4 s[4], dp[4];
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
       s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -227,6 +228,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
         }
       }
     }
+    sched_reads_ahead<4 * (C::NT + (NTV < C::NT ? NTV : C::NT)), 4, 1>();
+    __builtin_amdgcn_sched_barrier(0);
     const bool full = k0 + C::KT <= Lk;
     uint32_t kwords[2] = {0u, 0u};
     if constexpr (bits) {
@@ -270,10 +273,13 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
 #pragma unroll
       for (int j = 0; j < 8; ++j) dsb[c][j] = (bf16)s[2 * c + (j >> 2)][j & 3];
     // dQ^T += K^T dS^T
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int d = 0; d < C::ND; ++d) acc[d] = mfma16(tr_frag_pad<I::ROWB>(Kb, 32 * c, 16 * d, lane), dsb[c], acc[d]);
+    sched_reads_ahead<2 * C::ND, 4, 2>();
+    __builtin_amdgcn_sched_barrier(0);
 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wg_barrier();
@@ -396,6 +402,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
 #pragma unroll
     for (int hf = 0; hf < QT / 32; ++hf) {
       f32x4 s[2], dp[2];  // S / dP: row q = 32*hf + 16*qb + 4g + r, column key
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         s[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -409,6 +416,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
           dp[qb] = mfma16(ga, vf[t], dp[qb]);
         }
       }
+      sched_reads_ahead<4 * C::NT, 4, 1>();
+      __builtin_amdgcn_sched_barrier(0);
       bf16x8 pdb, dsb;  // B operands over 32 queries: k index 8g + j <-> q 16(j>>2) + 4g + (j&3)
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
@@ -431,11 +440,14 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
           }
         }
       }
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int d = 0; d < C::ND; ++d) {
         dv[d] = mfma16(tr_frag_perm<DP>(Gb, 32 * hf, 16 * d, lane), pdb, dv[d]);
         dk[d] = mfma16(tr_frag_perm<DP>(Qb, 32 * hf, 16 * d, lane), dsb, dk[d]);
       }
+      sched_reads_ahead<2 * C::ND, 4, 2>();
+      __builtin_amdgcn_sched_barrier(0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wg_barrier();
@@ -755,6 +767,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
     const char* rb = st + IQ::TILEB + IG::TILEB;
 
     f32x4 s[2], dp[2];  // row q = 16 qb + 4g + r, column key
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       s[qb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -766,6 +779,8 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
 #pragma unroll
       for (int t = 0; t < DV / 32; ++t) dp[qb] = mfma16(*(const bf16x8*)(grow + 64 * t), vf[t], dp[qb]);
     }
+    sched_reads_ahead<2 * (DP / 32 + DV / 32), 4, 1>();
+    __builtin_amdgcn_sched_barrier(0);
     bf16x8 dsb;  // B operand over 32 queries: k index 8g + j <-> q 16(j >> 2) + 4g + (j & 3)
     // the query-tail test as a separate code path (an in-line `if` became per-element selects)
     auto softmax = [&](auto tail) {
@@ -800,8 +815,11 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
     if (q0 + QT <= a.Lq) softmax(std::false_type{});
     else softmax(std::true_type{});
     // dK^T += Q^T dS (Q^T fragments by transposing reads of the padded Q image)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int d = 0; d < DP / 16; ++d) dk[d] = mfma16(tr_frag_pad<IQ::ROWB>(Qi, 0, 16 * d, lane), dsb, dk[d]);
+    sched_reads_ahead<DP / 16, 4, 2>();
+    __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wg_barrier();
   }

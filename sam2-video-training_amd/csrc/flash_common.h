@@ -177,6 +177,29 @@ __device__ __forceinline__ void wait_kv_pieces(int nk, int nv) {
   }
 }
 
+// Scheduling groups for a phase of N (fragment read, MFMA) pairs: the compiler issued every
+// fragment read right before its MFMA and waited for it (s_waitcnt lgkmcnt(0) per MFMA); this
+// pins the order  R^PF (M R)^(N-PF) M^PF  so PF fragments are always in flight (R = LDS read
+// instructions per fragment: 1 for ds_read_b128, 2 for a transposing b64 pair).  Call right after
+// the phase's code, between __builtin_amdgcn_sched_barrier(0) fences.
+template <int K, typename F>
+__device__ __forceinline__ void sched_rep(F&& f) {
+  if constexpr (K > 0) {
+    f();
+    sched_rep<K - 1>(f);
+  }
+}
+template <int N, int PF, int R>
+__device__ __forceinline__ void sched_reads_ahead() {
+  static_assert(PF <= N, "prefetch depth");
+  sched_rep<PF>([] { __builtin_amdgcn_sched_group_barrier(0x100, R, 0); });
+  sched_rep<N - PF>([] {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
+  });
+  sched_rep<PF>([] { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); });
+}
+
 __device__ __forceinline__ void wg_barrier() {
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");

@@ -34,6 +34,7 @@ SIGNATURES = {
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],
+    "s2h_gemm_split_target": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
     "s2h_gemm_mx8": [I, I, I, P, L, P, L, P, L, P, L, P, I, L, P, P, L, P, L, I, F, c_uint64, c_uint64, F, F, I, P],
     "s2h_mx8_config": [I],

@@ -90,7 +90,7 @@ def test_gemm_lds_dma_path(M, N, K, layout):
     _close(o32, ref + 3.0, 2e-3)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, -1])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, -1])
 @pytest.mark.parametrize("M,N,K", [(1000, 520, 200), (600, 264, 1100), (13312, 256, 256)])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
 def test_gemm_every_tiling(cfg, M, N, K, layout):
