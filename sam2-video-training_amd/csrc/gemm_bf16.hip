@@ -2,6 +2,8 @@
 #include "gemm_bf16.h"
 
 static int g_gemm_cfg = CFG_AUTO;
+// (512 -- one round of two workgroups per CU -- won the hot-cache sweep, profiles/r03_v6_wgrad_sweep.log,
+// but lost inside the step, profiles/r03_v6_trace_diff.log: kept at 768)
 int g_gemm_split_target = 768;
 
 // A/B knob: workgroups a split-K weight-gradient launch aims at (returns the previous value)

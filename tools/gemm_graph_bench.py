@@ -39,6 +39,22 @@ def graph_time(fn, n=20, reps=5):
     return a.elapsed_time(b) / (n * reps) * 1e3  # us per launch
 
 
+_SCRUB = None
+
+
+def graph_time_cold(fn, n=8, reps=3):
+    """per-launch GPU time with the caches cold: every launch follows a pass over a 512 MB buffer
+    (evicts the XCD L2s and the 256 MB Infinity Cache, like the step's operands that were written
+    long before); the scrub's own time, captured alone, is subtracted"""
+    global _SCRUB
+    if _SCRUB is None:
+        _SCRUB = torch.empty(128 * 2**20, device="cuda", dtype=torch.float32)
+    scrub = lambda: _SCRUB.mul_(0.5)  # noqa: E731
+    both = graph_time(lambda: (scrub(), fn()), n=n, reps=reps)
+    alone = graph_time(scrub, n=n, reps=reps)
+    return both - alone
+
+
 def main():
     bf = torch.bfloat16
     for M, N, K in SHAPES:
