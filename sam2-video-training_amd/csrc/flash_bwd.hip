@@ -662,25 +662,29 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
     }
 }
 
-// ------------------------------------------------------------------ dK of the V-fold, two waves per SIMD
-// The V-fold backward has no dV and a 64-wide value (the memory bank M), so a 16-key wave holds
-// K^T fragments (32 VGPRs), M^T fragments (8) and its dK^T accumulators (64): 8 waves x 16 keys run
-// two waves per SIMD (<= 256 VGPRs) and each wave's softmax / dropout VALU issues under its partner's
-// MFMAs.  (flash_bwd_dkv32_kernel<256, DROP, true, 64>, one wave per SIMD on 32x32x16, measured
-// 15 % MFMA-busy at 13.7 VALU per MFMA: its 512-register allocation moved S / dP through the
-// accumulator file every tile and each swizzled fragment read was waited for alone.)
-// Per 32-query tile and wave: S = Q K^T (16 MFMA), dP = du M^T (4), dK^T += Q^T dS (16).  Q and du
-// tiles sit in padded images (one base register + immediate offsets for every fragment, conflict-
-// free b128 and transposing reads); the row constants (lse, Di, dr = du'[:, 64], keep words
-// [word][query]) are DMA'd beside them so a lane reads its 4 consecutive queries with one b128.
-// DMA instructions per stage and wave: w0 Q x3; w1..5 Q x2 + du x1; w6 Q x2 + lse|Di; w7 Q x2 + dr
-// (+ 2 keep-word pieces with the bitmap).
-template <int DROP>
-__global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
-  static_assert(DROP != DROP_HASH, "the V-fold forward always writes the keep bitmap");
-  constexpr int DP = 256, DV = 64, QT = 32, NW = 8;
+// ------------------------------------------------------------------ dK / dV, head dim 256, two waves per SIMD
+// 8 waves x 16 keys per workgroup, 16x16x32 MFMA, two waves per SIMD (<= 256 VGPRs): each wave's
+// softmax / dropout VALU issues under its partner's MFMAs.  (flash_bwd_dkv32_kernel, one wave per
+// SIMD on 32x32x16, measured 15 % MFMA-busy at 13.7 VALU per MFMA on the V-fold: its 512-register
+// allocation moved S / dP through the accumulator file every tile and each swizzled fragment read
+// was waited for alone; the DV = 256 instance also spilled.)
+//   DV = 64 (V-fold, s2h_flash_bwd_frames_vfold): the value is the 64-wide memory bank M, dO is
+//     du' = [du | dr | 0] and there is no dV: K^T (32 VGPRs) + M^T (8) fragments, dK^T (64).
+//   DV = 256 (memory self-attention): K^T + V^T fragments (64), dK^T + dV^T accumulators (128).
+// Per 32-query tile and wave: S = Q K^T (16 MFMA), dP = dO V^T (4 / 16), dK^T += Q^T dS (16),
+// dV^T += dO^T P_drop (16, DV = 256).  Q and dO tiles sit in padded images (one base register +
+// immediate offsets for every fragment, conflict-free b128 and transposing reads); the row
+// constants (lse, Di, dr, keep words [word][query]) are DMA'd beside them so a lane reads its 4
+// consecutive queries with one b128.  DMA pieces per stage and wave: Q pieces w, w + 8 (16: wave 0);
+// DV = 256 dO the same (16: wave 1), DV = 64 du' pieces 0..4 on waves 1..5; lse | Di on wave 6;
+// dr (DV = 64) and the keep words on wave 7.
+template <int DV, int DROP>
+__global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a) {
+  const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
+  constexpr int DP = 256, QT = 32, NW = 8;
+  constexpr bool FOLD = DV != DP;
   using IQ = PadImg<DP, QT, NW>;  // 32 rows x 544 B, 17 pieces
-  using IG = PadImg<DV, QT, 1>;   // 32 rows x 160 B, 5 pieces (waves 1..5 take one each)
+  using IG = PadImg<DV, QT, 1>;   // dO / du': 32 rows x 544 B (17 pieces) or x 160 B (5 pieces)
   constexpr int RB_LSE = 0, RB_DI = 128, RB_DR = 256, RB_KEEP = 384;  // row block: + keep [4 words][32 q]
   constexpr int RB = 384 + 512;
   constexpr int STAGE = IQ::TILEB + IG::TILEB + RB;
@@ -701,28 +705,30 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
   const int nt = (a.Lq + QT - 1) / QT;
   const int Lq1 = a.Lq - 1;
 
+  // one 1-KiB piece of a padded [32][C] image of rows q0.. of src (row stride ld)
+  auto dma_piece = [&](char* img, const bf16* src, int64_t ld, int spr, int ncol, int q0, int piece) {
+    const int slot = piece * 64 + lane;
+    const int row = slot / spr, c = slot % spr;
+    lds_dma16(src + (min(q0 + row, Lq1) * (int)ld + (c < ncol / 8 ? 8 * c : 0)), img + piece * 1024);
+  };
   auto issue = [&](char* st, int q0) {
-    // Q pieces w, w + 8 (and 16 on wave 0)
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      if (i == 2 && w != 0) break;  // wave-uniform
-      const int piece = i == 2 ? 16 : w + 8 * i;
-      const int slot = piece * 64 + lane;
-      const int row = slot / IQ::SPR, c = slot % IQ::SPR;
-      lds_dma16(Q + (min(q0 + row, Lq1) * (int)a.sql + (c < DP / 8 ? 8 * c : 0)), st + piece * 1024);
+    dma_piece(st, Q, a.sql, IQ::SPR, DP, q0, w);
+    dma_piece(st, Q, a.sql, IQ::SPR, DP, q0, w + 8);
+    if (w == 0) dma_piece(st, Q, a.sql, IQ::SPR, DP, q0, 16);
+    char* gimg = st + IQ::TILEB;
+    if constexpr (FOLD) {
+      if (w >= 1 && w <= 5) dma_piece(gimg, G, a.sgl, IG::SPR, DV, q0, w - 1);
+    } else {
+      dma_piece(gimg, G, a.sgl, IG::SPR, DV, q0, w);
+      dma_piece(gimg, G, a.sgl, IG::SPR, DV, q0, w + 8);
+      if (w == 1) dma_piece(gimg, G, a.sgl, IG::SPR, DV, q0, 16);
     }
     char* rb = st + IQ::TILEB + IG::TILEB;
-    if (w >= 1 && w <= 5) {  // du' piece w - 1 (64 value columns; dr comes with the row block)
-      const int piece = w - 1;
-      const int slot = piece * 64 + lane;
-      const int row = slot / IG::SPR, c = slot % IG::SPR;
-      lds_dma16(G + (min(q0 + row, Lq1) * (int)a.sgl + (c < DV / 8 ? 8 * c : 0)), st + IQ::TILEB + piece * 1024);
-    } else if (w == 6) {  // lanes 0..31 lse, 32..63 Di
-      const int qi = min(q0 + (lane & 31), Lq1);
-      lds_dma4((lane < 32 ? LSE : DI) + qi, rb + RB_LSE);
+    if (w == 6) {  // lanes 0..31 lse, 32..63 Di
+      lds_dma4((lane < 32 ? LSE : DI) + min(q0 + (lane & 31), Lq1), rb + RB_LSE);
     } else if (w == 7) {
       // dr = du'[q, DV] (bf16 in the low half of the word); lanes 32..63 repeat 0..31
-      lds_dma4(G + (min(q0 + (lane & 31), Lq1) * (int)a.sgl + DV), rb + RB_DR);
+      if constexpr (FOLD) lds_dma4(G + (min(q0 + (lane & 31), Lq1) * (int)a.sgl + DV), rb + RB_DR);
       if constexpr (bits) {  // keep words (key / 32) of the block's 128 keys: [word][query]
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -732,23 +738,32 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
       }
     }
   };
-  // vmcnt that leaves this wave's DMAs of the next stage in flight
+  // vmcnt that leaves this wave's DMAs of the next stage in flight (wave-uniform counts)
   auto wait_stage = [&]() {
-    if (bits && w == 7) wait_vmcnt<5>();
-    else wait_vmcnt<3>();
+    if constexpr (FOLD) {  // 3 on every wave, 5 on wave 7 with the bitmap
+      if (bits && w == 7) wait_vmcnt<5>();
+      else wait_vmcnt<3>();
+    } else {  // 4, + 1 on waves 0, 1, 6, + 2 on wave 7 with the bitmap
+      if (w == 0 || w == 1 || w == 6) wait_vmcnt<5>();
+      else if (bits && w == 7) wait_vmcnt<6>();
+      else wait_vmcnt<4>();
+    }
   };
 
   issue(smem, 0);
-  bf16x8 kf[DP / 32], vf[DV / 32];  // B operands K^T / M^T: [k = d = 32t + 8g + j][n = key]
+  bf16x8 kf[DP / 32], vf[DV / 32];  // B operands K^T / V^T: [k = d = 32t + 8g + j][n = key]
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
   for (int t = 0; t < DP / 32; ++t) kf[t] = *(const bf16x8*)(fr.k + vkey * a.skl + 32 * t + 8 * g);
 #pragma unroll
   for (int t = 0; t < DV / 32; ++t) vf[t] = *(const bf16x8*)(fr.v + vkey * a.svl + 32 * t + 8 * g);
   __builtin_amdgcn_s_waitcnt(0xF70);  // retire the fragment loads in the compiler's bookkeeping
-  f32x4 dk[DP / 16];  // dK^T: row d = 16 db + 4g + r, column key
+  constexpr int NDV = FOLD ? 1 : DP / 16;
+  f32x4 dk[DP / 16], dv[NDV];  // dK^T / dV^T: row d = 16 db + 4g + r, column key
 #pragma unroll
   for (int d = 0; d < DP / 16; ++d) dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int d = 0; d < NDV; ++d) dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int kword = (w & 1) * 16 + kl;  // this lane's bit in its keep word
   const int kwsel = w >> 1;             // which of the block's 4 words
 
@@ -781,44 +796,52 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
     }
     sched_reads_ahead<2 * (DP / 32 + DV / 32), 4, 1>();
     __builtin_amdgcn_sched_barrier(0);
-    bf16x8 dsb;  // B operand over 32 queries: k index 8g + j <-> q 16(j >> 2) + 4g + (j & 3)
+    // B operands over 32 queries: k index 8g + j <-> q 16(j >> 2) + 4g + (j & 3)
+    bf16x8 dsb, pdb;
     // the query-tail test as a separate code path (an in-line `if` became per-element selects)
     auto softmax = [&](auto tail) {
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
-      const int qo = 16 * qb + 4 * g;
-      const float4 l4 = *(const float4*)(rb + RB_LSE + 4 * qo);
-      const float4 d4 = *(const float4*)(rb + RB_DI + 4 * qo);
-      const uint4 r4 = *(const uint4*)(rb + RB_DR + 4 * qo);
-      uint4 k4 = uint4{0u, 0u, 0u, 0u};
-      if constexpr (bits) k4 = *(const uint4*)(rb + RB_KEEP + kwsel * 128 + 4 * qo);
-      const float lt[4] = {l4.x, l4.y, l4.z, l4.w};
-      const float dt[4] = {d4.x, d4.y, d4.z, d4.w};
-      const uint32_t rt[4] = {r4.x, r4.y, r4.z, r4.w};
-      const uint32_t kt[4] = {k4.x, k4.y, k4.z, k4.w};
+      for (int qb = 0; qb < 2; ++qb) {
+        const int qo = 16 * qb + 4 * g;
+        const float4 l4 = *(const float4*)(rb + RB_LSE + 4 * qo);
+        const float4 d4 = *(const float4*)(rb + RB_DI + 4 * qo);
+        uint4 r4 = uint4{0u, 0u, 0u, 0u}, k4 = uint4{0u, 0u, 0u, 0u};
+        if constexpr (FOLD) r4 = *(const uint4*)(rb + RB_DR + 4 * qo);
+        if constexpr (bits) k4 = *(const uint4*)(rb + RB_KEEP + kwsel * 128 + 4 * qo);
+        const float lt[4] = {l4.x, l4.y, l4.z, l4.w};
+        const float dt[4] = {d4.x, d4.y, d4.z, d4.w};
+        const uint32_t rt[4] = {r4.x, r4.y, r4.z, r4.w};
+        const uint32_t kt[4] = {k4.x, k4.y, k4.z, k4.w};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float p = __builtin_amdgcn_exp2f(fmaf(s[qb][r], a.sl2, -lt[r] * FL_LOG2E));
-        if constexpr (decltype(tail)::value) p = q0 + qo + r < a.Lq ? p : 0.f;
-        const float dpr = dp[qb][r] + __uint_as_float(rt[r] << 16);
-        float dsv;
-        if constexpr (bits) {
-          const float dpd = (kt[r] >> kword) & 1u ? dpr : 0.f;
-          dsv = p * fmaf(dpd, a.inv_keep, -dt[r]);
-        } else {
-          dsv = p * (dpr - dt[r]);
+        for (int r = 0; r < 4; ++r) {
+          float p = __builtin_amdgcn_exp2f(fmaf(s[qb][r], a.sl2, -lt[r] * FL_LOG2E));
+          if constexpr (decltype(tail)::value) p = q0 + qo + r < a.Lq ? p : 0.f;
+          const float dpr = FOLD ? dp[qb][r] + __uint_as_float(rt[r] << 16) : dp[qb][r];
+          float dsv, pk = p;
+          if constexpr (DROP != DROP_NONE) {
+            bool keep;
+            if constexpr (bits) keep = (kt[r] >> kword) & 1u;
+            else keep = s2h_keep(seed, fr.drow0 + (uint64_t)(q0 + qo + r) * (uint64_t)fr.Lk + key, a.thresh);
+            dsv = p * fmaf(keep ? dpr : 0.f, a.inv_keep, -dt[r]);
+            pk = keep ? p : 0.f;  // dV accumulates the kept P unscaled (x 1/keep at the store)
+          } else {
+            dsv = p * (dpr - dt[r]);
+          }
+          dsb[4 * qb + r] = (bf16)dsv;
+          if constexpr (!FOLD) pdb[4 * qb + r] = (bf16)pk;
         }
-        dsb[4 * qb + r] = (bf16)dsv;
       }
-    }
     };
     if (q0 + QT <= a.Lq) softmax(std::false_type{});
     else softmax(std::true_type{});
-    // dK^T += Q^T dS (Q^T fragments by transposing reads of the padded Q image)
+    // dK^T += Q^T dS, dV^T += dO^T P_drop (transposing reads of the padded Q / dO images)
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int d = 0; d < DP / 16; ++d) dk[d] = mfma16(tr_frag_pad<IQ::ROWB>(Qi, 0, 16 * d, lane), dsb, dk[d]);
-    sched_reads_ahead<DP / 16, 4, 2>();
+    for (int d = 0; d < DP / 16; ++d) {
+      dk[d] = mfma16(tr_frag_pad<IQ::ROWB>(Qi, 0, 16 * d, lane), dsb, dk[d]);
+      if constexpr (!FOLD) dv[d] = mfma16(tr_frag_pad<IG::ROWB>(Gi, 0, 16 * d, lane), pdb, dv[d]);
+    }
+    sched_reads_ahead<(FOLD ? 1 : 2) * DP / 16, 4, 2>();
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     wg_barrier();
@@ -832,6 +855,16 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkf_kernel(FlashBwdArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) t4[e] = (bf16)(dk[d][e] * a.scale);
     *(uint2*)(DK + 16 * d + 4 * g) = *(const uint2*)t4;
+  }
+  if constexpr (!FOLD) {
+    bf16* DVp = fr.dv + (int64_t)key * a.sdvl;
+#pragma unroll
+    for (int d = 0; d < DP / 16; ++d) {
+      bf16 t4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t4[e] = (bf16)(dv[d][e] * a.inv_keep);
+      *(uint2*)(DVp + 16 * d + 4 * g) = *(const uint2*)t4;
+    }
   }
 }
 
@@ -908,12 +941,15 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
                        st, a);
   if constexpr (DP == 256) {
     const dim3 gk((a.Lk + 127) / 128, pad_bh8(a.BH), a.kv_splits);
-    if constexpr (DV == 64) {  // V-fold: dK only, two waves per SIMD (variant 1: the 32x32 kernel below)
-      if (drop != DROP_HASH && a.kv_splits == 1 && (s2h_flash_variant() & 1) == 0) {
-        if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkf_kernel<DROP_NONE>), gk, dim3(512), 0, st, a);
-        else hipLaunchKernelGGL((flash_bwd_dkf_kernel<DROP_BITS>), gk, dim3(512), 0, st, a);
-        return (int)hipGetLastError();
-      }
+    // V-fold: two waves per SIMD (flash_bwd_dkv16_kernel) unless variant bit 1 asks for the 32x32
+    // kernel below; it takes a single query range per workgroup (no fp32 partials).  The DV = 256
+    // instance (memory self-attention) spills at 256 VGPRs and measured slower than the 32x32 kernel
+    // (tools/attn_ab.py --variants: self-attention backward 0.565 vs 0.513 ms), so it is not launched.
+    if (DV == 64 && a.kv_splits == 1 && (s2h_flash_variant() & 1) == 0) {
+      if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_NONE>), gk, dim3(512), 0, st, a);
+      else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_BITS>), gk, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_HASH>), gk, dim3(512), 0, st, a);
+      return (int)hipGetLastError();
     }
     if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV>), gk, dim3(256), 0, st, a);
     else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV>), gk, dim3(256), 0, st, a);

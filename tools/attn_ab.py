@@ -31,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--drop", type=float, default=0.1)
+    ap.add_argument("--variants", action="store_true", help="also time the backward with s2h_attn_config(3)")
     ap.add_argument("--targets", default="", help="comma list of flash-forward key-split targets (workgroups) to sweep")
     a = ap.parse_args()
     if a.targets:
@@ -82,6 +83,14 @@ def run(a):
         tf, tb = timeit(fwd, a.iters), timeit(bwd, a.iters)
         fl = 4.0 * B * H * Lq * sum(lks) * D
         out.append(f"{name}: fwd {tf:.3f} ms ({fl / tf / 1e9:.0f} TF/s)  bwd {tb:.3f} ms ({2.5 * fl / tb / 1e9:.0f} TF/s)")
+        if a.variants:  # the same backward with the one-wave-per-SIMD dK / dV kernel (s2h_attn_config 3)
+            from sam2_video.kernels._lib import lib
+            prev = lib().s2h_attn_config(3)
+            try:
+                tb3 = timeit(bwd, a.iters)
+            finally:
+                lib().s2h_attn_config(prev)
+            out.append(f"(bwd with the 32x32 dK/dV kernel {tb3:.3f} ms)")
     print("  ".join(out), flush=True)
 
 
