@@ -274,6 +274,74 @@ class VFoldProj:
         ops.vfold_grad(self._g, gw, gb)
 
 
+class VFoldOutProj:
+    """The folded cross-attention's value projection AND its output projection as ONE GEMM:
+    Y = O Wo^T + bo with O = u' V^T (V = [Wv | bv | 0], VFoldProj) is u' (Wo V)^T + bo, so the
+    [N, 72] weight W' = Wo V (a 256 x 72 x 256 GEMM per step) replaces the [rows, 256] x [256, 256]
+    out-projection GEMM of every layer and frame, and O is never formed (transformer.py:296-311 +
+    memory_attention.py:66-81).  Backward: du' = dY W' is the linear's dgrad; the weight gradients
+    follow from G = dY^T u' ([N, 72], fp32): dWo += G V^T, dV = Wo^T G (scattered into dWv / dbv by
+    ops.vfold_grad), dbo += colsum(dY).  Used by RoPEAttention.attend_mem (S2H_VFOLD_OUT=0: the two
+    GEMMs, for A/B)."""
+
+    def __init__(self, vfold, out_lin):
+        self.vf, self.out = vfold, out_lin
+        self.weight, self.bias = out_lin.weight, out_lin.bias  # autograd anchors (v_proj's ride along)
+        self.out_features, self.in_features = out_lin.out_features, ops.VFOLD_COLS
+        self._w = None
+        self._g = self._gb = self._dv = None
+        self._gen = -1
+
+    def compute_weight(self):
+        if self._gen != _GEN[0]:
+            v = self.vf.compute_weight()   # [Nv, 72] bf16 (Nv = Wo's in_features)
+            wo = self.out.compute_weight()  # [N, Nv] bf16
+            N, Nv = wo.shape
+            if self._w is None:
+                self._w = torch.empty(N, ops.VFOLD_COLS, device=wo.device, dtype=wo.dtype)
+            ops.gemm(wo, v, self._w, M=N, N=ops.VFOLD_COLS, K=Nv, lda_m=Nv, lda_k=1, ldb_k=ops.VFOLD_COLS, ldb_n=1,
+                     ldc=ops.VFOLD_COLS)
+            self._gen = _GEN[0]
+        return self._w
+
+    def compute_bias(self):
+        return self.out.compute_bias()
+
+    def grad_views(self):
+        return None, None
+
+    def wgrad(self, dy, x):
+        gwo, gbo = _grad_of(self.out.weight), _grad_of(self.out.bias)
+        gwv, gbv = _grad_of(self.vf.lin.weight), _grad_of(self.vf.lin.bias)
+        if gbo is not None:
+            ops.colsum(dy, gbo)
+        if gwo is None and gwv is None and gbv is None:
+            return
+        N, C = self.out_features, ops.VFOLD_COLS
+        if self._g is None:
+            self._g = torch.empty(N, C, device=dy.device, dtype=torch.float32)
+            self._gb = torch.empty(N, C, device=dy.device, dtype=dy.dtype)
+        ops.linear_wgrad(dy, x, self._g, accumulate=False)  # G = dY^T u'
+        ops.cast(self._g, self._gb.dtype, out=self._gb)
+        v = self.vf.compute_weight()  # [Nv, 72]
+        wo = self.out.compute_weight()  # [N, Nv]
+        Nv = wo.shape[1]
+        if gwo is not None:  # dWo += G V^T
+            ops.gemm(self._gb, v, gwo.view(N, Nv), M=N, N=Nv, K=C, lda_m=C, lda_k=1, ldb_k=1, ldb_n=C, ldc=Nv,
+                     beta=1.0)
+        if gwv is not None or gbv is not None:  # dV = Wo^T G -> dWv, dbv
+            if self._dv is None:
+                self._dv = torch.empty(Nv, C, device=dy.device, dtype=torch.float32)
+            ops.gemm(wo, self._gb, self._dv, M=Nv, N=C, K=N, lda_m=1, lda_k=Nv, ldb_k=C, ldb_n=1, ldc=C)
+            ops.vfold_grad(self._dv, gwv, gbv)
+
+
+def vfold_out_enabled():
+    """S2H_VFOLD_OUT=0 keeps the V-fold projection and the output projection as two GEMMs (A/B)"""
+    import os
+    return os.environ.get("S2H_VFOLD_OUT", "1") != "0"
+
+
 def vfold_enabled():
     """S2H_VFOLD=0 keeps the unfolded value projection + attention (A/B measurements)"""
     import os

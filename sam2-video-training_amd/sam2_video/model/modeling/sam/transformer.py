@@ -59,12 +59,14 @@ class RoPEAttention(Attention):
         self.rope_k_repeat = rope_k_repeat
         self.head_dim = self.internal_dim // self.num_heads
         self._vfold = None
+        self._vfold_out = None
 
     def bind_arena(self, arena):
         """the memory cross-attention (kv_in_dim 64, one head of 256) folds its value projection
         into the attention (FN.VFoldProj / ops.attn_fwd_vfold)"""
         if self.kv_in_dim == ops.VFOLD_DV and self.num_heads == 1 and self.internal_dim == 256:
             self._vfold = FN.VFoldProj(self.v_proj)
+            self._vfold_out = FN.VFoldOutProj(self._vfold, self.out_proj)
 
     def attend_mem(self, q, k, mem, residual=None, out_drop=0.0):
         """attention of projected q / k over the memory bank `mem` [B, Lk, 64] with its value
@@ -76,6 +78,8 @@ class RoPEAttention(Attention):
         q4 = q.view(B, Lq, 1, I)
         if self._vfold is not None and FN.vfold_enabled() and ops.vfold_ok(q4, mem):
             u = FN.attention_vfold(q4, k.view(B, Lk, 1, I), mem.reshape(B, Lk, 1, mem.shape[-1]), p_drop=self._p())
+            if FN.vfold_out_enabled():  # value and output projection as one GEMM (FN.VFoldOutProj)
+                return FN.linear(u.view(B, Lq, ops.VFOLD_COLS), self._vfold_out, residual=residual, drop_p=out_drop)
             o = FN.linear(u.view(B, Lq, ops.VFOLD_COLS), self._vfold)
             return self.out_proj(o, residual=residual, drop_p=out_drop)
         return self.attend(q, k, self.v_proj(mem), residual=residual, out_drop=out_drop)

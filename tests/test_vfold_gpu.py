@@ -231,3 +231,30 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
     assert torch.equal(out[1][0], out[3][0])
     assert not torch.isnan(out[1][1]).any()
     _close(out[1][1], out[3][1], 1e-2, "dk two-wave vs one-wave")
+
+
+def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
+    """the fused value + output projection (FN.VFoldOutProj: one GEMM with W' = Wo [Wv | bv]) against
+    the two GEMMs (S2H_VFOLD_OUT=0) in a bf16 B+ 256^2 training step, dropout off: logits, loss and
+    the out_proj / v_proj gradients of the memory cross-attention within bf16 rounding"""
+    from step_harness import build_model, golden_batch, grads_by_name, load_golden, mask_iou, run_step
+    g = load_golden("bplus256_point_all")
+    batch = golden_batch(g).to(DEV)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("S2H_VFOLD_OUT", flag)
+        model = build_model("base_plus", 256, ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder",
+                                               "prompt_encoder"], "point", dtype="bf16")
+        stages, merged, losses, _ = run_step(model, batch)
+        res[flag] = ([s["pred_masks"].detach().float().cpu() for s in stages], float(losses["total_loss"]),
+                     grads_by_name(model))
+    (m0, l0, g0), (m1, l1, g1) = res["0"], res["1"]
+    for a, b in zip(m0, m1):
+        assert mask_iou(a, b) >= 0.99
+        _close(a, b, 0.03)
+    assert abs(l0 - l1) <= 0.005 * abs(l0)
+    names = [n for n in g0 if ".cross_attn_image.v_proj." in n or ".cross_attn_image.out_proj." in n]
+    assert len(names) == 16
+    for n in names:
+        cos = torch.nn.functional.cosine_similarity(g0[n].flatten(), g1[n].flatten(), dim=0).item()
+        assert cos >= 0.99, (n, cos)
