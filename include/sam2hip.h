@@ -96,6 +96,10 @@ int s2h_gemm_config(int cfg);
  * t <= 0 leaves it unchanged); returns the previous value. */
 int s2h_gemm_split_target(int t);
 
+/* A/B knob (tests, benchmarks): tiling of the GEMMs with M <= 128 rows (0 = automatic, values as
+ * s2h_gemm_config); returns the previous setting. */
+int s2h_gemm_tiny_config(int cfg);
+
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),
  * db[N] (+)= sum over rows of dy (db may be NULL); `accumulate` 0 overwrites both.

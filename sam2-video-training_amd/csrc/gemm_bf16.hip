@@ -2,6 +2,13 @@
 #include "gemm_bf16.h"
 
 static int g_gemm_cfg = CFG_AUTO;
+static int g_gemm_tiny_cfg = CFG_AUTO;  // A/B knob: tiling of GEMMs with M <= 128 (s2h_gemm_tiny_config)
+
+extern "C" int s2h_gemm_tiny_config(int cfg) {
+  const int prev = g_gemm_tiny_cfg;
+  g_gemm_tiny_cfg = cfg;
+  return prev;
+}
 // (512 -- one round of two workgroups per CU -- won the hot-cache sweep, profiles/r03_v6_wgrad_sweep.log,
 // but lost inside the step, profiles/r03_v6_trace_diff.log: kept at 768)
 int g_gemm_split_target = 768;
@@ -59,7 +66,8 @@ static int pick_cfg(const GemmArgs16& a, int batch) {
 int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   GemmArgs16 a = in;
   a.dbg = g_gemm_dbg;
-  const int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
+  int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
+  if (g_gemm_tiny_cfg && !g_gemm_cfg && a.M <= 128) cfg = g_gemm_tiny_cfg;
   if (cfg < 0 || !gemm_glds_ok(a, batch)) return gemm_cfg_launch_1(CFG_REGS, a, batch, st);  // register-staged
   int rc;
   if ((rc = gemm_cfg_launch_1(cfg, a, batch, st)) >= 0) return rc;

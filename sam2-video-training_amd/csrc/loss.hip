@@ -9,9 +9,19 @@
 
 #define NSTAT 6
 
+// sigmoid(x) and the binary cross-entropy with logits from ONE exponential: e = exp(-|x|),
+// sigma = 1 / (1 + e) or e / (1 + e), ce = max(x, 0) - x t + log(1 + e) (hardware exp / log / rcp;
+// the libm expf / log1pf / division made the loss kernels compute-bound)
+__device__ __forceinline__ float sig_ce(float x, float t, float& ce) {
+  const float e = __expf(-fabsf(x));
+  const float r = __builtin_amdgcn_rcpf(1.f + e);
+  ce = fmaxf(x, 0.f) - x * t + __logf(1.f + e);
+  return x >= 0.f ? r : e * r;
+}
+
 __device__ __forceinline__ float focal_elem(float x, float t, float& p) {
-  p = 1.f / (1.f + expf(-x));
-  const float ce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+  float ce;
+  p = sig_ce(x, t, ce);
   const float pt = p * t + (1.f - p) * (1.f - t);
   const float at = 0.25f * t + 0.75f * (1.f - t);
   const float q = 1.f - pt;
@@ -50,32 +60,43 @@ __global__ __launch_bounds__(256) void mask_stats_kernel(int N, int64_t P, const
   }
 }
 
-// 4 consecutive pixels per thread and iteration (16-B logit loads, 4-B target loads).
+// 4 consecutive pixels per vector, MV vectors per thread: every load of the thread is issued before
+// any arithmetic (the scalar form waited on one dependent load per pixel, ~25 us per 13 x 512^2
+// frame; fewer, larger workgroups were slower still -- the kernel is load-latency bound).
 // Requires P, ldx, ldt multiples of 4 and 16-B / 4-B aligned bases (checked by the host).
-__global__ __launch_bounds__(1024) void mask_stats_vec_kernel(int N, int64_t P, const float* x, int64_t ldx,
-                                                              const uint8_t* tgt, int64_t ldt, float inv_temp,
-                                                              float* stats) {
+template <int MV>
+__global__ __launch_bounds__(256) void mask_stats_vec_kernel(int N, int64_t P, const float* x, int64_t ldx,
+                                                             const uint8_t* tgt, int64_t ldt, float inv_temp,
+                                                             float* stats) {
   const int n = blockIdx.y;
-  const int64_t chunk = ((P + gridDim.x - 1) / gridDim.x + 3) & ~(int64_t)3;
-  const int64_t p0 = blockIdx.x * chunk, p1 = min(P, p0 + chunk);
+  const int64_t p0 = (int64_t)blockIdx.x * (256 * 4 * MV);
+  float4 xv[MV];
+  uint32_t tv[MV];
+#pragma unroll
+  for (int j = 0; j < MV; ++j) {
+    const int64_t p = p0 + 4 * (threadIdx.x + 256 * j);
+    const bool ok = p < P;
+    xv[j] = ok ? *(const float4*)(x + n * ldx + p) : float4{0.f, 0.f, 0.f, 0.f};
+    tv[j] = ok && tgt ? *(const uint32_t*)(tgt + n * ldt + p) : 0u;
+  }
   float acc[NSTAT] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int64_t p = p0 + 4 * threadIdx.x; p < p1; p += 4 * 1024) {
-    const float4 x4 = *(const float4*)(x + n * ldx + p);
-    const uint32_t t4 = tgt ? *(const uint32_t*)(tgt + n * ldt + p) : 0u;
-    const float xs[4] = {x4.x, x4.y, x4.z, x4.w};
+#pragma unroll
+  for (int j = 0; j < MV; ++j) {
+    if (p0 + 4 * (threadIdx.x + 256 * j) >= P) continue;
+    const float xs[4] = {xv[j].x, xv[j].y, xv[j].z, xv[j].w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const float xv = xs[e] * inv_temp;
-      const float t = (t4 >> (8 * e)) & 0xffu ? 1.f : 0.f;
+      const float xe = xs[e] * inv_temp;
+      const float t = (tv[j] >> (8 * e)) & 0xffu ? 1.f : 0.f;
       float sg;
-      const float f = focal_elem(xv, t, sg);
-      const bool pr = xv > 0.f, gt = t > 0.f;
+      const float f = focal_elem(xe, t, sg);
+      const bool pr = xe > 0.f, gt = t > 0.f;
       acc[0] += f; acc[1] += sg; acc[2] += t; acc[3] += sg * t;
       acc[4] += (pr && gt) ? 1.f : 0.f;
       acc[5] += (pr || gt) ? 1.f : 0.f;
     }
   }
-  __shared__ float red[16][NSTAT];
+  __shared__ float red[4][NSTAT];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < NSTAT; ++k) {
@@ -84,9 +105,7 @@ __global__ __launch_bounds__(1024) void mask_stats_vec_kernel(int N, int64_t P, 
   }
   __syncthreads();
   if (threadIdx.x < NSTAT) {
-    float v = 0.f;
-#pragma unroll
-    for (int u = 0; u < 16; ++u) v += red[u][threadIdx.x];
+    float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
     atomicAdd(&stats[n * NSTAT + threadIdx.x], v);
   }
 }
@@ -104,11 +123,11 @@ extern "C" int s2h_mask_stats(int N, int64_t P, const float* x, int64_t ldx, con
   if (chunks > 256) chunks = 256;
   if (chunks < 1) chunks = 1;
   if (mask_vec4_ok(P, x, ldx, tgt, ldt)) {
-    // 1024-thread workgroups, <= 8 per row: the row's statistics are float atomics on 6 addresses, and
-    // 64 workgroups per row serialised on them (24 us per 13 x 512^2 frame with 256-thread groups)
-    int vch = (int)((P + 32767) / 32768);
-    vch = vch < 1 ? 1 : (vch > 8 ? 8 : vch);
-    hipLaunchKernelGGL(mask_stats_vec_kernel, dim3(vch, N), dim3(1024), 0, st, N, P, x, ldx, tgt, ldt, inv_temp, stats);
+    constexpr int MV = 2;  // 2 x 4 pixels per thread, 2048 per workgroup
+    const int64_t vch = (P + 256 * 4 * MV - 1) / (256 * 4 * MV);
+    if (vch > 65535) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(mask_stats_vec_kernel<MV>, dim3((unsigned)vch, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt,
+                       inv_temp, stats);
   } else {
     hipLaunchKernelGGL(mask_stats_kernel, dim3(chunks, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp, stats);
   }
@@ -173,9 +192,9 @@ __global__ void mask_loss_bwd_kernel(int N, int64_t P, const float* x, int64_t l
     if (c[0] != 0.f || c[1] != 0.f || c[2] != 0.f) {
       const float xv = x[n * ldx + p] * inv_temp;
       const float t = tgt[n * ldt + p] ? 1.f : 0.f;
-      const float s = 1.f / (1.f + expf(-xv));
+      float ce;
+      const float s = sig_ce(xv, t, ce);
       const float ds = s * (1.f - s);
-      const float ce = fmaxf(xv, 0.f) - xv * t + log1pf(expf(-fabsf(xv)));
       const float pt = s * t + (1.f - s) * (1.f - t);
       const float at = 0.25f * t + 0.75f * (1.f - t);
       const float q = 1.f - pt;
@@ -205,9 +224,9 @@ __global__ void mask_loss_bwd_vec_kernel(int N, int64_t P, const float* x, int64
       for (int e = 0; e < 4; ++e) {
         const float xv = xs[e] * inv_temp;
         const float t = (t4 >> (8 * e)) & 0xffu ? 1.f : 0.f;
-        const float s = 1.f / (1.f + expf(-xv));
+        float ce;
+        const float s = sig_ce(xv, t, ce);
         const float ds = s * (1.f - s);
-        const float ce = fmaxf(xv, 0.f) - xv * t + log1pf(expf(-fabsf(xv)));
         const float pt = s * t + (1.f - s) * (1.f - t);
         const float at = 0.25f * t + 0.75f * (1.f - t);
         const float q = 1.f - pt;

@@ -35,6 +35,7 @@ SIGNATURES = {
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],
     "s2h_gemm_split_target": [I],
+    "s2h_gemm_tiny_config": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
     "s2h_gemm_mx8": [I, I, I, P, L, P, L, P, L, P, L, P, I, L, P, P, L, P, L, I, F, c_uint64, c_uint64, F, F, I, P],
     "s2h_mx8_config": [I],
@@ -138,6 +139,8 @@ def lib():
             fn.restype = RESTYPES.get(name, c_int)
         if os.environ.get("S2H_GEMM_CFG"):  # measurement override of the GEMM tiling choice
             h.s2h_gemm_config(int(os.environ["S2H_GEMM_CFG"]))
+        if os.environ.get("S2H_GEMM_TINY_CFG"):  # ... of the tiny-M (<= 128 rows) GEMMs only
+            h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
         _LIB = h
     return _LIB
 
