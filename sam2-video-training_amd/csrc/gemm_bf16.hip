@@ -38,6 +38,10 @@ extern "C" int s2h_gemm_config(int cfg) {
 //    occupancy of the smaller tile hides the LDS-DMA latency) and on tiny weight gradients;
 //  * 256^2 (8 waves) only pays on large square problems (4096^3: 146 us vs 170 for 128^2).
 static int pick_cfg(const GemmArgs16& a, int batch) {
+  // M <= 128 (decoder tokens, pooled heads): 64^2 tiles with a 4-deep ring -- the in-step env A/B
+  // (tools/gpu_r3n.sh, S2H_GEMM_TINY_CFG 0 / 19 / 18, two rounds) measured 137.5 / 137.3 clip-frames/s
+  // for the default rules, 136.9 / 137.0 for the 8-deep K32 ring and 137.8 / 138.0 for this one
+  if (a.M <= 128) return CFG_64_NS4;
   const long t256 = (long)((a.M + 255) / 256) * ((a.N + 255) / 256) * batch;
   if (a.M >= 1024 && a.N >= 1024 && a.K >= 1024 && t256 >= 128) return CFG_256;
   const long t128x64 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64) * batch;
