@@ -454,10 +454,14 @@ enum GemmCfg {
   CFG_AUTO = 0, CFG_64 = 1, CFG_128 = 2, CFG_128_NS3 = 3, CFG_256x128 = 4, CFG_256 = 5, CFG_128x256 = 6,
   CFG_128x64 = 7, CFG_64x128 = 8, CFG_64_NS3 = 9, CFG_64_K32_NS4 = 10, CFG_128x64_K32_NS3 = 11,
   CFG_128x64_K32_NS4 = 12, CFG_128x64_NS3 = 13, CFG_256x128_W4_K32_NS3 = 14, CFG_256x128_W4_K64 = 15,
-  CFG_128_K32_NS3 = 16, CFG_256x64_W4_K32_NS3 = 17, CFG_64_NS4 = 18, CFG_64_K32_NS8 = 19, CFG_REGS = 99
+  CFG_128_K32_NS3 = 16, CFG_256x64_W4_K32_NS3 = 17, CFG_64_NS4 = 18, CFG_64_K32_NS8 = 19,
+  // 4 x 1 wave grids: every wave owns whole 64-column rows of the tile (128-B bf16 output rows)
+  CFG_64_W41 = 20, CFG_128x64_W41 = 21, CFG_128x64_W41_K32_NS3 = 22, CFG_64_W41_NS4 = 23, CFG_128x64_W41_NS3 = 24,
+  CFG_REGS = 99
 };
 // per-translation-unit launchers: return -1 when `cfg` is not one of the unit's tilings
 int gemm_cfg_launch_1(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_2(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_3(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_4(int cfg, GemmArgs16& a, int batch, hipStream_t st);
+int gemm_cfg_launch_5(int cfg, GemmArgs16& a, int batch, hipStream_t st);

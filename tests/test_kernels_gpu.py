@@ -90,7 +90,8 @@ def test_gemm_lds_dma_path(M, N, K, layout):
     _close(o32, ref + 3.0, 2e-3)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, -1])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24,
+                                 -1])
 @pytest.mark.parametrize("M,N,K", [(1000, 520, 200), (600, 264, 1100), (13312, 256, 256)])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
 def test_gemm_every_tiling(cfg, M, N, K, layout):
@@ -116,6 +117,40 @@ def test_gemm_every_tiling(cfg, M, N, K, layout):
         _close(o32, ref + 3.0, 2e-3)
     finally:
         _lib.lib().s2h_gemm_config(prev)
+
+
+@pytest.mark.parametrize("pcfg,cfg", [(20, 1), (21, 7), (22, 11), (23, 18), (24, 13)])
+@pytest.mark.parametrize("batch,M,N,K", [(3, 1000, 520, 200), (2, 13312, 256, 256), (1, 64, 64, 64), (5, 70, 24, 40)])
+def test_gemm_wave_grid_4x1_matches_2x2(pcfg, cfg, batch, M, N, K):
+    """the 4 x 1 wave grids (every wave owns whole 64-column tile rows: full-line epilogue stores)
+    are bit-identical to the 2 x 2 grids of the same tile and ring -- same K order per 16x16
+    accumulator, same epilogue incl. the dropout hash of each output index -- on batched, ragged
+    and single-tile problems"""
+    from sam2_video.kernels import _lib
+    ops = _ops()
+    torch.manual_seed(5)
+    bf = torch.bfloat16
+    a = torch.randn(batch, M, K, device=DEV).to(bf)
+    b = torch.randn(batch, N, K, device=DEV).to(bf)
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(batch, M, N, device=DEV).to(bf)
+    ref = torch.relu(a.float() @ b.float().transpose(1, 2) + bias) + res.float()
+    for drop in (0.1, 0.0):
+        kw = dict(M=M, N=N, K=K, lda_m=K, lda_k=1, ldb_k=1, ldb_n=K, ldc=N, batch=batch, sA=M * K, sB=N * K,
+                  sC=M * N, bias=bias, residual=res, ldr=N, sR=M * N, act=1, drop_p=drop, seed=77)
+        outs = []
+        for c in (pcfg, cfg):
+            prev = _lib.lib().s2h_gemm_config(c)
+            try:
+                out = torch.full((batch, M, N), float("nan"), device=DEV, dtype=bf)
+                ops.gemm(a, b, out, **kw)
+                outs.append(out)
+            finally:
+                _lib.lib().s2h_gemm_config(prev)
+        torch.cuda.synchronize()
+        assert not torch.isnan(outs[0].float()).any()
+        assert torch.equal(outs[0], outs[1])
+    _close(outs[0], ref, 1e-2)
 
 
 @pytest.mark.parametrize("rows,N,K", [(20000, 336, 112), (131072, 112, 336), (13312, 256, 256), (4099, 130, 77)])
