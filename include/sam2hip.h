@@ -99,6 +99,10 @@ int s2h_gemm_split_target(int t);
 /* A/B knob (tests, benchmarks): tiling of the GEMMs with M <= 128 rows (0 = automatic, values as
  * s2h_gemm_config); returns the previous setting. */
 int s2h_gemm_tiny_config(int cfg);
+/* A/B knob: the bf16-output GEMMs on 4 x 1 wave grids (whole 64-column rows per wave) instead of
+ * 2 x 2 (1: all, the default; 2: only N >= 768; 0: off); results are bit-identical.  Returns the
+ * previous mode. */
+int s2h_gemm_w41(int mode);
 
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),

@@ -21,6 +21,26 @@ extern "C" int s2h_gemm_split_target(int t) {
 }
 static int g_gemm_dbg = 0;
 
+// 4 x 1 wave grids instead of the 2 x 2 ones for bf16 outputs (1: every such GEMM, the default;
+// 2: only N >= 768; 0: off); bit-identical results.  In-step env A/B (tools/gpu_r3q.sh,
+// S2H_GEMM_W41 0 / 1 / 2, two rounds): 136.77 / 136.71, 136.98 / 137.05, 136.68 / 136.86 clip-frames/s
+static int g_gemm_w41 = 1;
+extern "C" int s2h_gemm_w41(int mode) {
+  const int prev = g_gemm_w41;
+  g_gemm_w41 = mode;
+  return prev;
+}
+static int w41_of(int cfg) {
+  switch (cfg) {
+    case CFG_64: return CFG_64_W41;
+    case CFG_128x64: return CFG_128x64_W41;
+    case CFG_128x64_K32_NS3: return CFG_128x64_W41_K32_NS3;
+    case CFG_64_NS4: return CFG_64_W41_NS4;
+    case CFG_128x64_NS3: return CFG_128x64_W41_NS3;
+    default: return cfg;
+  }
+}
+
 extern "C" int s2h_gemm_config(int cfg) {
   const int prev = g_gemm_cfg | (g_gemm_dbg << 8);
   g_gemm_cfg = cfg < 0 ? cfg : (cfg & 0xff);
@@ -72,6 +92,7 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   a.dbg = g_gemm_dbg;
   int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
   if (g_gemm_tiny_cfg && !g_gemm_cfg && a.M <= 128) cfg = g_gemm_tiny_cfg;
+  if (g_gemm_w41 && !g_gemm_cfg && !a.out_f32 && (g_gemm_w41 == 1 || a.N >= 768)) cfg = w41_of(cfg);
   if (cfg < 0 || !gemm_glds_ok(a, batch)) return gemm_cfg_launch_1(CFG_REGS, a, batch, st);  // register-staged
   int rc;
   if ((rc = gemm_cfg_launch_1(cfg, a, batch, st)) >= 0) return rc;

@@ -36,6 +36,7 @@ SIGNATURES = {
     "s2h_gemm_config": [I],
     "s2h_gemm_split_target": [I],
     "s2h_gemm_tiny_config": [I],
+    "s2h_gemm_w41": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
     "s2h_gemm_mx8": [I, I, I, P, L, P, L, P, L, P, L, P, I, L, P, P, L, P, L, I, F, c_uint64, c_uint64, F, F, I, P],
     "s2h_mx8_config": [I],
@@ -141,6 +142,8 @@ def lib():
             h.s2h_gemm_config(int(os.environ["S2H_GEMM_CFG"]))
         if os.environ.get("S2H_GEMM_TINY_CFG"):  # ... of the tiny-M (<= 128 rows) GEMMs only
             h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
+        if os.environ.get("S2H_GEMM_W41"):  # ... bf16-output GEMMs on 4 x 1 wave grids (A/B)
+            h.s2h_gemm_w41(int(os.environ["S2H_GEMM_W41"]))
         _LIB = h
     return _LIB
 
