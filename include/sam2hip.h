@@ -160,6 +160,10 @@ int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D);
 /* A/B switch (tests, benchmarks): bit 0 of flash_enable = 0 sends every attention to the
  * generic kernels; bits 8+ (if non-zero) set the workgroup count the flash forward key split
  * aims at (default 256).  Returns the previous setting in the same encoding. */
+/* A/B knob: 1 (default) runs bf16 attentions with Lq, Lk <= 64, head dim <= 64 and no dropout (the
+ * Hiera windows) on the whole-instance small-window kernels (attention.hip attn_win_*), 0 on the
+ * tile kernels.  Returns the previous setting. */
+int s2h_attn_win(int on);
 int s2h_attn_config(int flash_enable);
 int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,

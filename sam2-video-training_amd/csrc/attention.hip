@@ -911,6 +911,271 @@ __global__ __launch_bounds__(NW * 64) void attn_bwd_dkv_fewk_kernel(AttnArgs a) 
   }
 }
 
+// ------------------------------------------------- small windows (Lq, Lk <= 64)
+// Hiera's windowed and q-pooled attentions (hieradet.py:56-81: 8x8 / 4x4 windows, 2x2-pooled
+// queries, the 7x7 global stage) are 10^3-10^4 independent (window, head) instances of at most
+// 64 x 64.  The tile kernels above give every instance a 64-query x 64-key workgroup (a 4x4
+// window uses 1/16 of it) and the backward three launches (Di, dQ, dK / dV).  Here a workgroup
+// owns whole instances: Lq <= 16 -> one wave (64 threads) per instance, Lq <= 64 -> four waves
+// of 16 query rows.  The keys are one LDS tile of KR (32 / 64) rows, so the softmax is exact in
+// one pass; the backward computes P, dP, Di = rowsum(P o dP) (= rowsum(dO o O) of the exact
+// forward), dS and dQ in the query waves, then dK / dV per 16-key block from P and dS kept in
+// LDS -- one launch, no atomics, no workspace.  bf16, head dim <= 64 (zero-padded image of 64),
+// no dropout (Hiera has none; dropout sites keep the tile kernels).
+// MFMA fragment maps (16x16x32 bf16): A[m][k] / B[n][k] -> lane (m | n = lane & 15, k = 8 (lane >> 4)
+// .. +7); C -> lane (row 4 (lane >> 4) + r, col lane & 15).  A "k-major" image [k][m] gives the
+// fragment by transposing reads (tr_bfrag), a row-major one [m][k] by ds_read_b128.
+constexpr int WIN_DP = 64, WIN_KS = WIN_DP + 8;
+
+template <int NW, int KR>
+__global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
+  using MF = Mfma<bf16>;
+  constexpr int KS = WIN_KS, PS = KR + 8, QR = 16 * NW, NT = NW * 64, NB = KR / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * KR * KS + QR * PS + QR * KS];
+  bf16* Ks = smem;
+  bf16* Vs = Ks + KR * KS;
+  bf16* Ps = Vs + KR * KS;
+  bf16* Os = Ps + QR * PS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const bf16* Q = (const bf16*)a.q + b * a.sqb + h * a.sqh;
+  const bf16* K = (const bf16*)a.k + b * a.skb + h * a.skh;
+  const bf16* V = (const bf16*)a.v + b * a.svb + h * a.svh;
+  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Ks, K, a.skl, 0, a.Lk, a.D, tid);
+  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Vs, V, a.svl, 0, a.Lk, a.D, tid);
+  const int q0 = 16 * w;
+  MF::frag qf[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) qf[t] = frag_global<bf16>(Q, a.sql, q0 + (lane & 15), a.Lq, t * 32 + (lane >> 4) * 8, a.D);
+  __syncthreads();
+
+  const float sl2 = a.scale * LOG2E;
+  f32x4 s[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) s[j] = MF::mma(qf[t], MF::load(&Ks[(j * 16 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8]), s[j]);
+  }
+  float mx[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) mx[r] = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const bool kvalid = j * 16 + (lane & 15) < a.Lk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[j][r] = kvalid ? s[j][r] * sl2 : -INFINITY;
+      mx[r] = fmaxf(mx[r], s[j][r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    mx[r] = row16_max(mx[r]);
+    l[r] = 0.f;
+  }
+  bf16* Pw = Ps + q0 * PS;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float p = exp2f(s[j][r] - mx[r]);
+      l[r] += p;
+      Pw[(4 * (lane >> 4) + r) * PS + j * 16 + (lane & 15)] = (bf16)p;
+    }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) l[r] = row16_sum(l[r]);
+  // P rows of this wave only: LDS operations of one wave execute in order, no barrier
+  f32x4 o[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < KR / 32; ++t) {
+    const MF::frag pf = MF::load(&Pw[(lane & 15) * PS + t * 32 + (lane >> 4) * 8]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) o[d] = MF::mma(pf, tr_bfrag(Vs, KS, t * 32, d * 16, lane), o[d]);
+  }
+  bf16* Ow = Os + q0 * KS;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float inv = 1.f / l[r];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) Ow[(4 * (lane >> 4) + r) * KS + d * 16 + (lane & 15)] = (bf16)(o[d][r] * inv);
+    const int row = q0 + 4 * (lane >> 4) + r;
+    if ((lane & 15) == 0 && row < a.Lq) a.lse[(int64_t)bh * a.Lq + row] = (mx[r] + log2f(l[r])) * LN2;
+  }
+  bf16* O = (bf16*)a.o + b * a.sob + h * a.soh;
+#pragma unroll
+  for (int c = lane; c < 16 * 8; c += 64) {  // 16 rows x 8 16-B chunks of this wave's output
+    const int row = c >> 3, col = (c & 7) * 8;
+    if (q0 + row < a.Lq && col < a.D) *(uint4*)(O + (int64_t)(q0 + row) * a.sol + col) = *(const uint4*)(Ow + row * KS + col);
+  }
+}
+
+template <int NW, int KR>
+__global__ __launch_bounds__(NW * 64) void attn_win_bwd_kernel(AttnArgs a) {
+  using MF = Mfma<bf16>;
+  constexpr int KS = WIN_KS, PS = KR + 8, QR = 16 * NW, QA = QR < 32 ? 32 : QR, NT = NW * 64, NB = KR / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * KR * KS + 2 * QA * KS + 2 * QA * PS];
+  bf16* Ks = smem;
+  bf16* Vs = Ks + KR * KS;
+  bf16* Qs = Vs + KR * KS;
+  bf16* Gs = Qs + QA * KS;  // dO
+  bf16* Ps = Gs + QA * KS;
+  bf16* Ss = Ps + QA * PS;  // dS
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Ks, (const bf16*)a.k + b * a.skb + h * a.skh, a.skl, 0, a.Lk, a.D, tid);
+  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Vs, (const bf16*)a.v + b * a.svb + h * a.svh, a.svl, 0, a.Lk, a.D, tid);
+  lds_load_rows<bf16, QA, WIN_DP, KS, NT>(Qs, (const bf16*)a.q + b * a.sqb + h * a.sqh, a.sql, 0, a.Lq, a.D, tid);
+  lds_load_rows<bf16, QA, WIN_DP, KS, NT>(Gs, (const bf16*)a.o + b * a.sob + h * a.soh, a.sol, 0, a.Lq, a.D, tid);
+  if constexpr (QA > QR) {  // the k-padding rows of P / dS (reductions over queries run 32 deep)
+    for (int i = tid; i < (QA - QR) * PS; i += NT) {
+      Ps[QR * PS + i] = (bf16)0.f;
+      Ss[QR * PS + i] = (bf16)0.f;
+    }
+  }
+  const int q0 = 16 * w;
+  const float sl2 = a.scale * LOG2E;
+  float lse2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = q0 + 4 * (lane >> 4) + r;
+    lse2[r] = row < a.Lq ? a.lse[(int64_t)bh * a.Lq + row] * LOG2E : 0.f;
+  }
+  __syncthreads();
+
+  // query phase: P, dP, Di, dS of rows q0 .. q0 + 15; dQ = dS K
+  f32x4 s[NB], dp[NB];
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    dp[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ao = (q0 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8;
+      const int bo = (j * 16 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8;
+      s[j] = MF::mma(MF::load(&Qs[ao]), MF::load(&Ks[bo]), s[j]);
+      dp[j] = MF::mma(MF::load(&Gs[ao]), MF::load(&Vs[bo]), dp[j]);
+    }
+  }
+  float di[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int j = 0; j < NB; ++j) {
+    const bool kvalid = j * 16 + (lane & 15) < a.Lk;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const bool qvalid = q0 + 4 * (lane >> 4) + r < a.Lq;
+      s[j][r] = (kvalid && qvalid) ? exp2f(s[j][r] * sl2 - lse2[r]) : 0.f;  // P
+      di[r] += s[j][r] * dp[j][r];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) di[r] = row16_sum(di[r]);
+  bf16* Pw = Ps + q0 * PS;
+  bf16* Sw = Ss + q0 * PS;
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int at = (4 * (lane >> 4) + r) * PS + j * 16 + (lane & 15);
+      Pw[at] = (bf16)s[j][r];
+      Sw[at] = (bf16)(s[j][r] * (dp[j][r] - di[r]));
+    }
+  f32x4 dq[4];
+#pragma unroll
+  for (int d = 0; d < 4; ++d) dq[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < KR / 32; ++t) {
+    const MF::frag sf = MF::load(&Sw[(lane & 15) * PS + t * 32 + (lane >> 4) * 8]);
+#pragma unroll
+    for (int d = 0; d < 4; ++d) dq[d] = MF::mma(sf, tr_bfrag(Ks, KS, t * 32, d * 16, lane), dq[d]);
+  }
+  bf16* dQ = (bf16*)a.dq + b * a.sdqb + h * a.sdqh;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = q0 + 4 * (lane >> 4) + r;
+    if (row < a.Lq)
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        const int col = d * 16 + (lane & 15);
+        if (col < a.D) dQ[(int64_t)row * a.sdql + col] = (bf16)(dq[d][r] * a.scale);
+      }
+  }
+  __syncthreads();
+
+  // key phase: dV = P^T dO, dK = dS^T Q per 16-key block (reductions over all QA query rows)
+  bf16* dK = (bf16*)a.dk + b * a.sdkb + h * a.sdkh;
+  bf16* dV = (bf16*)a.dv + b * a.sdvb + h * a.sdvh;
+  for (int kb = w; kb < NB; kb += NW) {
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+      dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int t = 0; t < QA / 32; ++t) {
+      const MF::frag pt = tr_bfrag(Ps, PS, t * 32, kb * 16, lane);
+      const MF::frag st = tr_bfrag(Ss, PS, t * 32, kb * 16, lane);
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        dv[d] = MF::mma(pt, tr_bfrag(Gs, KS, t * 32, d * 16, lane), dv[d]);
+        dk[d] = MF::mma(st, tr_bfrag(Qs, KS, t * 32, d * 16, lane), dk[d]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = kb * 16 + 4 * (lane >> 4) + r;
+      if (key < a.Lk)
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const int col = d * 16 + (lane & 15);
+          if (col < a.D) {
+            dK[(int64_t)key * a.sdkl + col] = (bf16)(dk[d][r] * a.scale);
+            dV[(int64_t)key * a.sdvl + col] = (bf16)dv[d][r];
+          }
+        }
+    }
+  }
+}
+
+// A/B knob (s2h_attn_win): 0 keeps the small windows on the tile kernels
+static int g_attn_win = 1;
+extern "C" int s2h_attn_win(int on) {
+  const int prev = g_attn_win;
+  g_attn_win = on;
+  return prev;
+}
+static bool attn_win_ok(const AttnArgs& a) {
+  return g_attn_win && a.p_drop <= 0.f && a.D <= WIN_DP && a.Lq <= 64 && a.Lk <= 64;
+}
+template <bool FWD>
+static int attn_win_launch(const AttnArgs& a, hipStream_t st) {
+  const int slot = s2h_prof_begin(st, FWD ? 1 : 2, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, 2);
+  const dim3 grid(a.B * a.H);
+  const bool k32 = a.Lk <= 32;
+  if (a.Lq <= 16) {
+    if (FWD) {
+      if (k32) hipLaunchKernelGGL((attn_win_fwd_kernel<1, 32>), grid, dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((attn_win_fwd_kernel<1, 64>), grid, dim3(64), 0, st, a);
+    } else {
+      if (k32) hipLaunchKernelGGL((attn_win_bwd_kernel<1, 32>), grid, dim3(64), 0, st, a);
+      else hipLaunchKernelGGL((attn_win_bwd_kernel<1, 64>), grid, dim3(64), 0, st, a);
+    }
+  } else {
+    if (FWD) {
+      if (k32) hipLaunchKernelGGL((attn_win_fwd_kernel<4, 32>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_win_fwd_kernel<4, 64>), grid, dim3(256), 0, st, a);
+    } else {
+      if (k32) hipLaunchKernelGGL((attn_win_bwd_kernel<4, 32>), grid, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((attn_win_bwd_kernel<4, 64>), grid, dim3(256), 0, st, a);
+    }
+  }
+  s2h_prof_end(slot, st);
+  return (int)hipGetLastError();
+}
+
 // ------------------------------------------------------------------ launch
 // few-query / few-key paths pay off when the long side spans several 64-row tiles
 static bool attn_fewq(const AttnArgs& a) { return a.Lq <= 16 && a.Lk > 128 && a.D <= 64; }
@@ -1021,6 +1286,7 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.o = o; a.sob = sob; a.soh = soh; a.sol = sol;
   a.lse = lse; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   a.idx0 = idx0;
+  if (dt == S2H_BF16 && attn_win_ok(a) && attn_aligned(dt, D, o, sob, soh, sol)) return attn_win_launch<true>(a, st);
   return dt == S2H_BF16 ? attn_dispatch<bf16, true>(a, st) : attn_dispatch<float, true>(a, st);
 }
 
@@ -1065,5 +1331,6 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.dv = dv; a.sdvb = sdvb; a.sdvh = sdvh; a.sdvl = sdvl;
   a.lse = (float*)lse; a.di = di_ws; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   a.idx0 = idx0;
+  if (dt == S2H_BF16 && attn_win_ok(a)) return attn_win_launch<false>(a, st);
   return dt == S2H_BF16 ? attn_dispatch<bf16, false>(a, st) : attn_dispatch<float, false>(a, st);
 }

@@ -239,6 +239,49 @@ def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
     _close(dv, vr.grad, 3 * tol)
 
 
+@pytest.mark.parametrize("B,H,Lq,Lk,D", [(256, 4, 16, 16, 56), (512, 2, 4, 16, 56), (128, 2, 16, 64, 56),
+                                         (64, 2, 64, 64, 56), (16, 8, 49, 49, 56), (13, 8, 8, 8, 32),
+                                         (3, 2, 7, 5, 40), (2, 3, 33, 17, 64), (5, 1, 1, 2, 8), (4, 2, 17, 64, 24)])
+def test_small_window_attention(B, H, Lq, Lk, D):
+    """Hiera window / pooled-query shapes (Lq, Lk <= 64) on the whole-instance kernels
+    (attention.hip attn_win_*): forward, LSE and the one-launch backward against the fp32
+    reference and against the tile kernels (s2h_attn_win(0)) on the same bf16 inputs"""
+    from sam2_video.kernels import _lib
+    ops = _ops()
+    torch.manual_seed(6)
+    bf = torch.bfloat16
+    q = torch.randn(B, Lq, H, D, device=DEV).to(bf)
+    k = torch.randn(B, Lk, H, D, device=DEV).to(bf)
+    v = torch.randn(B, Lk, H, D, device=DEV).to(bf)
+    do = torch.randn(B, Lq, H, D, device=DEV).to(bf)
+    scale = 1.0 / math.sqrt(D)
+    res = {}
+    for on in (1, 0):
+        prev = _lib.lib().s2h_attn_win(on)
+        try:
+            o = torch.full_like(q, float("nan"))
+            lse = torch.full((B, H, Lq), float("nan"), device=DEV)
+            ops.attn_fwd(q, k, v, o, lse, scale)
+            dq, dk, dv = (torch.full_like(t, float("nan")) for t in (q, k, v))
+            ops.attn_bwd(q, k, v, o, do, lse, dq, dk, dv, scale)
+            res[on] = (o, lse, dq, dk, dv)
+        finally:
+            _lib.lib().s2h_attn_win(prev)
+    qr, kr, vr = (t.float().clone().requires_grad_(True) for t in (q, k, v))
+    ro, rl = _ref_attn(qr, kr, vr, scale)
+    ro.backward(do.float())
+    o, lse, dq, dk, dv = res[1]
+    for t in res[1]:
+        assert not torch.isnan(t.float()).any()
+    _close(o, ro, 2e-2)
+    _close(lse, rl, 2e-2)
+    _close(dq, qr.grad, 6e-2)
+    _close(dk, kr.grad, 6e-2)
+    _close(dv, vr.grad, 6e-2)
+    for a_, b_ in zip(res[1], res[0]):  # same bf16 rounding points as the tile kernels
+        _close(a_, b_, 3e-2)
+
+
 @pytest.mark.parametrize("B,H,Lq,Lk,D", [(13, 1, 1024, 7196, 256), (13, 1, 1024, 1024, 256), (2, 2, 1024, 1028, 128),
                                          (2, 4, 300, 77, 64), (1, 1, 1000, 1031, 256), (3, 1, 128, 40, 256),
                                          # Hiera head dim 56 (and 40) in the padded 64 image
