@@ -319,6 +319,15 @@ int s2h_bilinear_fwd(int N, int hi, int wi, int ho, int wo, const float* x, floa
 int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const float* dy, float* dx, hipStream_t st);
 /* out[c] (=, or += when accum) = sum_r x[r, c] (bias gradients). */
 int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum, hipStream_t st);
+/* Segmented column sums, one launch: out[dsts[s], c] += sum_{r < rows} x[offs[s] + r, c] for s < nseg
+ * (<= 64; cols a multiple of the 16-B vector, <= 256 vectors).  The memory positions' temporal-code
+ * gradient (sam2_base.py:605-611: maskmem_tpos_enc added per memory slot), all slots of all frames. */
+int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const void* x, int64_t ld, const int64_t* offs,
+                   const int* dsts, float* out, hipStream_t st);
+/* Memory positions, one launch: out[j L + l, :] = pos[l, :] + tpos[idx[j], :] for j < n (<= 16)
+ * (sam2_base.py:605-611: the memory encoder position + maskmem_tpos_enc[t] per memory slot). */
+int s2h_memory_pos(int dt, int n, int L, int Dm, const void* pos, const void* tpos, const int* idx, void* out,
+                   hipStream_t st);
 /* out[i] (=/+=) sum_o x[o, i] (gradient of a per-object broadcast of shared
  * features: sam2model.py:307-311, mask_decoder.py:201,209 repeat_interleave). */
 int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* out, int accum, hipStream_t st);

@@ -931,9 +931,9 @@ template <int NW, int KR>
 __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
   using MF = Mfma<bf16>;
   constexpr int KS = WIN_KS, PS = KR + 8, QR = 16 * NW, NT = NW * 64, NB = KR / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * KR * KS + QR * PS + QR * KS];
-  bf16* Ks = smem;
-  bf16* Vs = Ks + KR * KS;
+  // K feeds S = Q K^T only (B operand in its natural layout): fragments straight from global
+  __shared__ __attribute__((aligned(16))) bf16 smem[KR * KS + QR * PS + QR * KS];
+  bf16* Vs = smem;
   bf16* Ps = Vs + KR * KS;
   bf16* Os = Ps + QR * PS;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -941,13 +941,15 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
   const bf16* Q = (const bf16*)a.q + b * a.sqb + h * a.sqh;
   const bf16* K = (const bf16*)a.k + b * a.skb + h * a.skh;
   const bf16* V = (const bf16*)a.v + b * a.svb + h * a.svh;
-  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Ks, K, a.skl, 0, a.Lk, a.D, tid);
-  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Vs, V, a.svl, 0, a.Lk, a.D, tid);
   const int q0 = 16 * w;
-  MF::frag qf[2];
+  MF::frag qf[2], kf[NB][2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) qf[t] = frag_global<bf16>(Q, a.sql, q0 + (lane & 15), a.Lq, t * 32 + (lane >> 4) * 8, a.D);
-  __syncthreads();
+  for (int t = 0; t < 2; ++t) {
+    qf[t] = frag_global<bf16>(Q, a.sql, q0 + (lane & 15), a.Lq, t * 32 + (lane >> 4) * 8, a.D);
+#pragma unroll
+    for (int j = 0; j < NB; ++j) kf[j][t] = frag_global<bf16>(K, a.skl, j * 16 + (lane & 15), a.Lk, t * 32 + (lane >> 4) * 8, a.D);
+  }
+  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Vs, V, a.svl, 0, a.Lk, a.D, tid);
 
   const float sl2 = a.scale * LOG2E;
   f32x4 s[NB];
@@ -955,7 +957,7 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
   for (int j = 0; j < NB; ++j) {
     s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int t = 0; t < 2; ++t) s[j] = MF::mma(qf[t], MF::load(&Ks[(j * 16 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8]), s[j]);
+    for (int t = 0; t < 2; ++t) s[j] = MF::mma(qf[t], kf[j][t], s[j]);
   }
   float mx[4], l[4];
 #pragma unroll
@@ -985,7 +987,7 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
     }
 #pragma unroll
   for (int r = 0; r < 4; ++r) l[r] = row16_sum(l[r]);
-  // P rows of this wave only: LDS operations of one wave execute in order, no barrier
+  __syncthreads();  // the V tile (all waves' loads); P rows are this wave's own
   f32x4 o[4];
 #pragma unroll
   for (int d = 0; d < 4; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1012,29 +1014,39 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
   }
 }
 
+// 16x16x16 operand (k = 4 (lane >> 4) .. +3) from a k-major [k][m] image: one transposing read
+__device__ __forceinline__ attn_v4i16 tr_bfrag16(const bf16* img, int ld, int k0, int n0, int lane) {
+  const int g = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+  typedef __attribute__((address_space(3))) attn_v4i16 lds_v4;
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(img + (k0 + 4 * g + q) * ld + n0 + 4 * p));
+}
+
+// V only feeds dP = dO V^T (B operand in its natural [key][d] layout): its fragments come straight
+// from global, so LDS holds K, Q, dO, P and dS.  One-wave instances (Lq <= 16) reduce dK / dV over
+// their 16 query rows with the 16-deep MFMA (no zero rows padding the reduction to 32): 11.8 /
+// 18.4 KB of LDS per instance at KR = 32 / 64, i.e. 13 / 8 instances resident per CU.
 template <int NW, int KR>
 __global__ __launch_bounds__(NW * 64) void attn_win_bwd_kernel(AttnArgs a) {
   using MF = Mfma<bf16>;
-  constexpr int KS = WIN_KS, PS = KR + 8, QR = 16 * NW, QA = QR < 32 ? 32 : QR, NT = NW * 64, NB = KR / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[2 * KR * KS + 2 * QA * KS + 2 * QA * PS];
+  constexpr int KS = WIN_KS, PS = KR + 8, QA = 16 * NW, NT = NW * 64, NB = KR / 16;
+  constexpr bool X16 = NW == 1;
+  __shared__ __attribute__((aligned(16))) bf16 smem[KR * KS + 2 * QA * KS + 2 * QA * PS];
   bf16* Ks = smem;
-  bf16* Vs = Ks + KR * KS;
-  bf16* Qs = Vs + KR * KS;
+  bf16* Qs = Ks + KR * KS;
   bf16* Gs = Qs + QA * KS;  // dO
   bf16* Ps = Gs + QA * KS;
   bf16* Ss = Ps + QA * PS;  // dS
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int bh = blockIdx.x, b = bh / a.H, h = bh % a.H;
+  const bf16* V = (const bf16*)a.v + b * a.svb + h * a.svh;
+  MF::frag vf[NB][2];
+#pragma unroll
+  for (int j = 0; j < NB; ++j)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) vf[j][t] = frag_global<bf16>(V, a.svl, j * 16 + (lane & 15), a.Lk, t * 32 + (lane >> 4) * 8, a.D);
   lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Ks, (const bf16*)a.k + b * a.skb + h * a.skh, a.skl, 0, a.Lk, a.D, tid);
-  lds_load_rows<bf16, KR, WIN_DP, KS, NT>(Vs, (const bf16*)a.v + b * a.svb + h * a.svh, a.svl, 0, a.Lk, a.D, tid);
   lds_load_rows<bf16, QA, WIN_DP, KS, NT>(Qs, (const bf16*)a.q + b * a.sqb + h * a.sqh, a.sql, 0, a.Lq, a.D, tid);
   lds_load_rows<bf16, QA, WIN_DP, KS, NT>(Gs, (const bf16*)a.o + b * a.sob + h * a.soh, a.sol, 0, a.Lq, a.D, tid);
-  if constexpr (QA > QR) {  // the k-padding rows of P / dS (reductions over queries run 32 deep)
-    for (int i = tid; i < (QA - QR) * PS; i += NT) {
-      Ps[QR * PS + i] = (bf16)0.f;
-      Ss[QR * PS + i] = (bf16)0.f;
-    }
-  }
   const int q0 = 16 * w;
   const float sl2 = a.scale * LOG2E;
   float lse2[4];
@@ -1054,9 +1066,8 @@ __global__ __launch_bounds__(NW * 64) void attn_win_bwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int ao = (q0 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8;
-      const int bo = (j * 16 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8;
-      s[j] = MF::mma(MF::load(&Qs[ao]), MF::load(&Ks[bo]), s[j]);
-      dp[j] = MF::mma(MF::load(&Gs[ao]), MF::load(&Vs[bo]), dp[j]);
+      s[j] = MF::mma(MF::load(&Qs[ao]), MF::load(&Ks[(j * 16 + (lane & 15)) * KS + t * 32 + (lane >> 4) * 8]), s[j]);
+      dp[j] = MF::mma(MF::load(&Gs[ao]), vf[j][t], dp[j]);
     }
   }
   float di[4] = {0.f, 0.f, 0.f, 0.f};
@@ -1114,14 +1125,24 @@ __global__ __launch_bounds__(NW * 64) void attn_win_bwd_kernel(AttnArgs a) {
       dk[d] = f32x4{0.f, 0.f, 0.f, 0.f};
       dv[d] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-#pragma unroll
-    for (int t = 0; t < QA / 32; ++t) {
-      const MF::frag pt = tr_bfrag(Ps, PS, t * 32, kb * 16, lane);
-      const MF::frag st = tr_bfrag(Ss, PS, t * 32, kb * 16, lane);
+    if constexpr (X16) {
+      const attn_v4i16 pt = tr_bfrag16(Ps, PS, 0, kb * 16, lane);
+      const attn_v4i16 st = tr_bfrag16(Ss, PS, 0, kb * 16, lane);
 #pragma unroll
       for (int d = 0; d < 4; ++d) {
-        dv[d] = MF::mma(pt, tr_bfrag(Gs, KS, t * 32, d * 16, lane), dv[d]);
-        dk[d] = MF::mma(st, tr_bfrag(Qs, KS, t * 32, d * 16, lane), dk[d]);
+        dv[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pt, tr_bfrag16(Gs, KS, 0, d * 16, lane), dv[d], 0, 0, 0);
+        dk[d] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(st, tr_bfrag16(Qs, KS, 0, d * 16, lane), dk[d], 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < QA / 32; ++t) {
+        const MF::frag pt = tr_bfrag(Ps, PS, t * 32, kb * 16, lane);
+        const MF::frag st = tr_bfrag(Ss, PS, t * 32, kb * 16, lane);
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          dv[d] = MF::mma(pt, tr_bfrag(Gs, KS, t * 32, d * 16, lane), dv[d]);
+          dk[d] = MF::mma(st, tr_bfrag(Qs, KS, t * 32, d * 16, lane), dk[d]);
+        }
       }
     }
 #pragma unroll

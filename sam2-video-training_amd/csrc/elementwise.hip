@@ -1139,3 +1139,96 @@ extern "C" int s2h_vfold_grad(int N, int K, int ld, const float* g, float* gwv, 
                      ld, g, gwv, gbv);
   return (int)hipGetLastError();
 }
+
+// ------------------------------------------------------- memory positional rows
+// The memory attention's key positions (sam2_base memory pos; functional_sam.memory_pos): slot j of
+// the memory bank gets out[j L + l] = spatial_pos[l] + tpos[idx[j]] -- all slots in one launch
+// (the per-slot broadcast adds were one launch each).  Backward: the tpos rows' gradient is the
+// column sum of each slot's rows, all slots of all frames in one segmented launch.
+struct MposTable { int idx[16]; };
+template <typename T>
+__global__ __launch_bounds__(256) void memory_pos_vec_kernel(int nvec, int L, int dv, const T* pos, const T* tpos,
+                                                             MposTable tb, T* out) {
+  constexpr int V = V16<T>::VEC;
+  for (int v = blockIdx.x * 256 + threadIdx.x; v < nvec; v += gridDim.x * 256) {
+    const int c = (v % dv) * V, row = v / dv, j = row / L, l = row - j * L;
+    float a[V], b[V];
+    V16<T>::load(pos + (int64_t)l * dv * V + c, a);
+    V16<T>::load(tpos + (int64_t)tb.idx[j] * dv * V + c, b);
+#pragma unroll
+    for (int e = 0; e < V; ++e) a[e] += b[e];
+    V16<T>::store(out + (int64_t)row * dv * V + c, a);
+  }
+}
+extern "C" int s2h_memory_pos(int dt, int n, int L, int Dm, const void* pos, const void* tpos, const int* idx, void* out,
+                              hipStream_t st) {
+  if (n <= 0 || L <= 0) return 0;
+  const int V = dt == S2H_BF16 ? 8 : 4;
+  if (n > 16 || Dm % V != 0 || !al16(pos) || !al16(tpos) || !al16(out) || (int64_t)n * L * Dm / V >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  MposTable tb = {};
+  for (int j = 0; j < n; ++j) tb.idx[j] = idx[j];
+  const int nvec = n * L * (Dm / V);
+  if (dt == S2H_BF16)
+    hipLaunchKernelGGL(memory_pos_vec_kernel<bf16>, ew_grid(nvec), dim3(256), 0, st, nvec, L, Dm / V, (const bf16*)pos,
+                       (const bf16*)tpos, tb, (bf16*)out);
+  else
+    hipLaunchKernelGGL(memory_pos_vec_kernel<float>, ew_grid(nvec), dim3(256), 0, st, nvec, L, Dm / V, (const float*)pos,
+                       (const float*)tpos, tb, (float*)out);
+  return (int)hipGetLastError();
+}
+
+// segmented column sums: out[dst[s]][:] += sum over rows r < rows of x[off[s] + r][:]  (s < nseg <= 64,
+// blockIdx.y = segment; colsum_vec_kernel's row-lane plan within each segment)
+struct SegTable { int64_t off[64]; int dst[64]; };
+template <typename T>
+__global__ __launch_bounds__(256) void colsum_seg_kernel(int64_t rows, int cols, const T* x, int64_t ld,
+                                                         int64_t rows_per_block, SegTable tb, float* out) {
+  constexpr int V = 16 / sizeof(T);
+  const int G = cols / V;
+  const int lanes = 256 / G;
+  const int g = threadIdx.x % G, lane = threadIdx.x / G;
+  __shared__ float red[256 * 8];
+  x += tb.off[blockIdx.y] * ld;
+  out += (int64_t)tb.dst[blockIdx.y] * cols;
+  float acc[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) acc[j] = 0.f;
+  const int64_t r0 = blockIdx.x * rows_per_block, r1 = min(rows, r0 + rows_per_block);
+  if (lane < lanes) {
+    for (int64_t r = r0 + lane; r < r1; r += lanes) {
+      const uint4 u = *(const uint4*)(x + r * ld + g * V);
+      const T* t = (const T*)&u;
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += to_f32(t[j]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < V; ++j) red[threadIdx.x * V + j] = (lane < lanes) ? acc[j] : 0.f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const int gg = c / V, j = c % V;
+    float s = 0.f;
+    for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * V + j];
+    atomicAdd(&out[c], s);
+  }
+}
+extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const void* x, int64_t ld, const int64_t* offs,
+                              const int* dsts, float* out, hipStream_t st) {
+  if (nseg <= 0 || rows <= 0 || cols <= 0) return 0;
+  const int V = dt == S2H_BF16 ? 8 : 4;
+  if (nseg > 64 || cols % V != 0 || cols / V > 256 || ld % V != 0 || !al16(x)) return (int)hipErrorInvalidValue;
+  SegTable tb = {};
+  for (int s = 0; s < nseg; ++s) {
+    tb.off[s] = offs[s];
+    tb.dst[s] = dsts[s];
+  }
+  int64_t rpb = (rows + 63) / 64;  // ~64 blocks per segment, each >= 16 rows
+  if (rpb < 16) rpb = 16;
+  const dim3 grid((unsigned)((rows + rpb - 1) / rpb), (unsigned)nseg);
+  if (dt == S2H_BF16)
+    hipLaunchKernelGGL(colsum_seg_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, (const bf16*)x, ld, rpb, tb, out);
+  else
+    hipLaunchKernelGGL(colsum_seg_kernel<float>, grid, dim3(256), 0, st, rows, cols, (const float*)x, ld, rpb, tb, out);
+  return (int)hipGetLastError();
+}

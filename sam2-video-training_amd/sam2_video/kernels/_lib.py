@@ -78,6 +78,8 @@ SIGNATURES = {
     "s2h_bilinear_fwd": [I, I, I, I, I, P, P, P],
     "s2h_bilinear_bwd": [I, I, I, I, I, P, P, P],
     "s2h_colsum": [I, L, I, P, L, P, I, P],
+    "s2h_colsum_seg": [I, I, L, I, P, L, P, P, P, P],
+    "s2h_memory_pos": [I, I, I, I, P, P, P, P, P],
     "s2h_sum_outer": [I, I, L, P, P, I, P],
     "s2h_im2col": [I, I, I, I, I, I, I, I, I, I, I, P, P, P],
     "s2h_mask_down_stage": [I, I, I, I, I, I, P, I, F, F, P, P, P, P, F, P, P],

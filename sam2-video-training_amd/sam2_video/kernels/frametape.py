@@ -1056,8 +1056,12 @@ def memory_pos(tape: FrameTape, tpos_p, obj_pos, spatial_pos, tpos_idx, L, dtype
     if tpos.dtype != dtype:
         tpos = ops.cast(tpos.contiguous(), dtype)
     vid, out = tape._out(0, (M, Dm), dtype, tape.mem_rows)
-    for j, ti in enumerate(tpos_idx):
-        ops.add_bcast(spatial_pos, tpos[ti], out=out[j * L:(j + 1) * L])
+    sp = spatial_pos.reshape(-1, Dm)
+    if 0 < n <= 16 and sp.shape[0] == L and sp.is_contiguous() and tpos.is_contiguous():
+        ops.memory_pos(sp, tpos, tpos_idx, out[:n * L])  # every slot in one launch
+    else:
+        for j, ti in enumerate(tpos_idx):
+            ops.add_bcast(spatial_pos, tpos[ti], out=out[j * L:(j + 1) * L])
     if obj_pos is not None:
         out[n * L:].copy_(obj_pos)
     tape._fattr(op, "tpos_idx", list(tpos_idx))
@@ -1074,6 +1078,11 @@ def _mpos_bw(tape, op, gys):
     L = op.attrs["L"]
     Dm = st.shape0[-1]
     gt2 = gt.view(-1, Dm)
+    segs = [((st.offsets[f] // Dm) + j * L, ti) for f in range(tape.F) for j, ti in enumerate(op.fattrs["tpos_idx"][f])]
+    if 0 < len(segs) <= 64 and g.is_contiguous() and gt2.is_contiguous() and all(o % Dm == 0 for o in st.offsets):
+        # every slot of every frame in one segmented column-sum launch
+        ops.colsum_seg(g.view(-1, Dm), L, [o for o, _ in segs], [t for _, t in segs], gt2)
+        return []
     for f in range(tape.F):
         gf = g[st.offsets[f]:st.offsets[f] + st.numels[f]].view(-1, Dm)
         for j, ti in enumerate(op.fattrs["tpos_idx"][f]):

@@ -609,6 +609,33 @@ def colsum(x, out, accumulate=True):
     return out
 
 
+def colsum_seg(x, rows, offs, dsts, out):
+    """out[dsts[s]] += x[offs[s]:offs[s] + rows].sum(0) for every segment s (x [R, C] row-contiguous,
+    out fp32 [*, C]); one launch for up to 64 segments"""
+    import ctypes
+    C = x.shape[-1]
+    _dev(x, out)
+    assert x.stride(-1) == 1 and out.dtype == torch.float32 and out.is_contiguous() and len(offs) == len(dsts) <= 64
+    o = (ctypes.c_int64 * len(offs))(*[int(v) for v in offs])
+    d = (ctypes.c_int * len(dsts))(*[int(v) for v in dsts])
+    call("s2h_colsum_seg", dt(x), len(offs), int(rows), C, ptr(x), x.stride(-2), ctypes.addressof(o),
+         ctypes.addressof(d), ptr(out), stream())
+    return out
+
+
+def memory_pos(pos, tpos, idx, out):
+    """out[j * L + l] = pos[l] + tpos[idx[j]] for j < len(idx) <= 16 (pos [L, C], tpos [*, C], out [n L, C],
+    all contiguous, one dtype)"""
+    import ctypes
+    L, C = pos.shape
+    _dev(pos, tpos, out)
+    assert pos.is_contiguous() and tpos.is_contiguous() and out.is_contiguous() and len(idx) <= 16
+    assert pos.dtype == tpos.dtype == out.dtype and out.numel() == len(idx) * L * C
+    ix = (ctypes.c_int * len(idx))(*[int(v) for v in idx])
+    call("s2h_memory_pos", dt(out), len(idx), L, C, ptr(pos), ptr(tpos), ctypes.addressof(ix), ptr(out), stream())
+    return out
+
+
 def sum_outer(x, out, accumulate=False):
     """out[j] = sum_o x[o, j]  (same dtype as x)"""
     O = x.shape[0]

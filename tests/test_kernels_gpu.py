@@ -185,6 +185,30 @@ def test_colsum_shapes(dtype, rows, cols):
     _close(out, x.float().sum(0), 1e-4)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_memory_pos_and_segmented_colsum(dtype):
+    """memory positions of every slot in one launch (s2h_memory_pos) == the per-slot broadcast adds;
+    segmented column sums (s2h_colsum_seg) == per-segment colsum, incl. two segments into one row"""
+    ops = _ops()
+    torch.manual_seed(3)
+    L, C = 4096, 64
+    pos = torch.randn(L, C, device=DEV).to(dtype)
+    tpos = torch.randn(7, C, device=DEV).to(dtype)
+    idx = [6, 0, 3, 5, 1]
+    out = torch.empty(len(idx) * L, C, device=DEV, dtype=dtype)
+    ops.memory_pos(pos, tpos, idx, out)
+    ref = torch.cat([ops.add_bcast(pos, tpos[i], out=torch.empty_like(pos)) for i in idx])
+    assert torch.equal(out, ref)
+    x = torch.randn(9 * 1000, C, device=DEV).to(dtype)
+    offs, dsts = [0, 1000, 3000, 7000, 5000], [2, 0, 2, 4, 1]
+    got = torch.full((5, C), 0.5, device=DEV)
+    ops.colsum_seg(x, 1000, offs, dsts, got)
+    want = torch.full((5, C), 0.5, device=DEV)
+    for o, d in zip(offs, dsts):
+        want[d] += x[o:o + 1000].float().sum(0)
+    _close(got, want, 1e-5)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
 def test_bmm_layouts(dtype, tol):
     ops = _ops()

@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--ops", default="", help="comma list of s2h_* entry points: report their call sites instead")
     a = ap.parse_args()
     from sam2_video.data.synthetic import make_clip, sam2_collate_fn
     from sam2_video.kernels import functional as FN
@@ -64,6 +65,25 @@ def main():
                 agg[(name, where)][1] += o.numel() if o is not None else 0
             return out
 
+    if a.ops:
+        from sam2_video.kernels import ops as _ops
+        want = set(a.ops.split(","))
+        real = _ops.call
+        calls = collections.Counter()
+
+        def spy(name, *args):
+            if name in want:
+                fr = [f for f in traceback.extract_stack() if "sam2_video" in f.filename][-4:-1]
+                calls[(name, " <- ".join(f"{f.filename.split('sam2_video/')[-1]}:{f.lineno}" for f in reversed(fr)))] += 1
+            return real(name, *args)
+
+        _ops.call = spy
+        runner(batches[2])
+        torch.cuda.synchronize()
+        _ops.call = real
+        for (name, where), n in calls.most_common(a.top):
+            print(f"n={n:4d}  {name:20s} {where}")
+        return
     with Sites():
         runner(batches[2])
     torch.cuda.synchronize()
