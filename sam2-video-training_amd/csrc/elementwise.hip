@@ -911,10 +911,77 @@ __global__ __launch_bounds__(256) void dwconv_vec_kernel(int B, int H, int W, in
   }
 }
 
+// Row-blocked bf16 form for K = 7 (the memory fuser's CXBlock depthwise 7x7): a thread computes R
+// vertically adjacent outputs of 8 channels; per kernel column kx it loads the R + K - 1 input rows
+// once (16 B each) and applies that column's K taps to all R outputs from registers -- 17.5 input
+// loads per output at R = 4 instead of 49 (the one-output form above is load-issue bound).
+// Out-of-image taps read zeros (the one-output form skips them: same sum, other order).
+template <int K, int R>
+__global__ __launch_bounds__(256) void dwconv_rows_kernel(int B, int H, int W, int C, int pad, const bf16* x,
+                                                          const float* w, const float* bias, bf16* y) {
+  __shared__ __attribute__((aligned(16))) float wl[K * K * 64];
+  const int cg = threadIdx.x & 7, px = threadIdx.x >> 3;  // 8 channel groups x 32 pixels
+  const int c0 = blockIdx.z * 64;
+  const int HB = (H + R - 1) / R;
+  const int y0 = (blockIdx.y % HB) * R, b = blockIdx.y / HB;
+  const int xx = blockIdx.x * 32 + px;
+  for (int i = threadIdx.x; i < K * K * 64; i += 256) {
+    const int t = i / 64, c = i % 64;
+    wl[t * 64 + c] = w[(int64_t)(c0 + c) * K * K + t];
+  }
+  __syncthreads();
+  if (xx >= W) return;
+  const int cc = c0 + cg * 8;
+  float acc[R][8];
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[r][j] = bias ? bias[cc + j] : 0.f;
+  const bf16* xb = x + (int64_t)b * H * W * C + cc;
+#pragma unroll 1
+  for (int kx = 0; kx < K; ++kx) {  // rolled: unrolled, all K*K weight taps get hoisted into VGPRs
+    const int sx = xx - pad + kx;
+    const bool xok = sx >= 0 && sx < W;
+    uint4 in[R + K - 1];
+#pragma unroll
+    for (int i = 0; i < R + K - 1; ++i) {
+      const int sy = y0 - pad + i;
+      in[i] = (xok && sy >= 0 && sy < H) ? *(const uint4*)(xb + ((int64_t)sy * W + sx) * C) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int ky = 0; ky < K; ++ky) {
+      const float4 w0 = *(const float4*)&wl[(ky * K + kx) * 64 + cg * 8];
+      const float4 w1 = *(const float4*)&wl[(ky * K + kx) * 64 + cg * 8 + 4];
+      const float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const bf16* v = (const bf16*)&in[r + ky];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) acc[r][j] += wv[j] * (float)v[j];
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if (y0 + r >= H) break;
+    bf16 o[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (bf16)acc[r][j];
+    *(uint4*)(y + (((int64_t)b * H + y0 + r) * W + xx) * C + cc) = *(const uint4*)o;
+  }
+}
+
 extern "C" int s2h_dwconv(int dt, int B, int H, int W, int C, int K, int pad, const void* x, const float* w,
                           const float* bias, void* y, hipStream_t st) {
   const int64_t n = (int64_t)B * H * W * C;
   if (n <= 0) return 0;
+  if (dt == S2H_BF16 && K == 7 && C % 64 == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
+    constexpr int R = 4;
+    dim3 grid((W + 31) / 32, B * ((H + R - 1) / R), C / 64);
+    hipLaunchKernelGGL((dwconv_rows_kernel<7, R>), grid, dim3(256), 0, st, B, H, W, C, pad, (const bf16*)x, w, bias,
+                       (bf16*)y);
+    return (int)hipGetLastError();
+  }
   if (C % 64 == 0 && K <= 7 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0) {
     dim3 grid((W + 31) / 32, B * H, C / 64);
     if (dt == S2H_BF16)

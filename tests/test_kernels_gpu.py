@@ -526,7 +526,7 @@ def test_im2col_conv_matches_torch():
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("B,H,W,C", [(13, 32, 32, 256), (2, 7, 45, 128)])
+@pytest.mark.parametrize("B,H,W,C", [(13, 32, 32, 256), (2, 7, 45, 128), (13, 64, 64, 256), (1, 5, 3, 64)])
 def test_dwconv_vectorised(dtype, tol, B, H, W, C):
     ops = _ops()
     torch.manual_seed(3)
