@@ -941,7 +941,7 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
   const bf16* Q = (const bf16*)a.q + b * a.sqb + h * a.sqh;
   const bf16* K = (const bf16*)a.k + b * a.skb + h * a.skh;
   const bf16* V = (const bf16*)a.v + b * a.svb + h * a.svh;
-  const int q0 = 16 * w;
+  const int q0 = blockIdx.y * QR + 16 * w;  // query tiles of QR rows (Lq > 64: the decoder's image -> token)
   MF::frag qf[2], kf[NB][2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -976,7 +976,7 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
     mx[r] = row16_max(mx[r]);
     l[r] = 0.f;
   }
-  bf16* Pw = Ps + q0 * PS;
+  bf16* Pw = Ps + 16 * w * PS;
 #pragma unroll
   for (int j = 0; j < NB; ++j)
 #pragma unroll
@@ -997,7 +997,7 @@ __global__ __launch_bounds__(NW * 64) void attn_win_fwd_kernel(AttnArgs a) {
 #pragma unroll
     for (int d = 0; d < 4; ++d) o[d] = MF::mma(pf, tr_bfrag(Vs, KS, t * 32, d * 16, lane), o[d]);
   }
-  bf16* Ow = Os + q0 * KS;
+  bf16* Ow = Os + 16 * w * KS;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const float inv = 1.f / l[r];
@@ -1168,13 +1168,15 @@ extern "C" int s2h_attn_win(int on) {
   g_attn_win = on;
   return prev;
 }
-static bool attn_win_ok(const AttnArgs& a) {
-  return g_attn_win && a.p_drop <= 0.f && a.D <= WIN_DP && a.Lq <= 64 && a.Lk <= 64;
+// the forward also takes Lq > 64 (query tiles on grid.y: the decoder's image -> token attention,
+// 1024 queries x 8 keys); the one-launch backward needs every query of an instance in one workgroup
+static bool attn_win_ok(const AttnArgs& a, bool fwd) {
+  return g_attn_win && a.p_drop <= 0.f && a.D <= WIN_DP && (fwd ? a.Lq <= 65535 * 64 : a.Lq <= 64) && a.Lk <= 64;
 }
 template <bool FWD>
 static int attn_win_launch(const AttnArgs& a, hipStream_t st) {
   const int slot = s2h_prof_begin(st, FWD ? 1 : 2, (int64_t)a.B * a.H, a.Lq, a.Lk, a.D, 2);
-  const dim3 grid(a.B * a.H);
+  const dim3 grid(a.B * a.H, a.Lq <= 16 ? 1 : (a.Lq + 63) / 64);
   const bool k32 = a.Lk <= 32;
   if (a.Lq <= 16) {
     if (FWD) {
@@ -1307,7 +1309,7 @@ extern "C" int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.o = o; a.sob = sob; a.soh = soh; a.sol = sol;
   a.lse = lse; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   a.idx0 = idx0;
-  if (dt == S2H_BF16 && attn_win_ok(a) && attn_aligned(dt, D, o, sob, soh, sol)) return attn_win_launch<true>(a, st);
+  if (dt == S2H_BF16 && attn_win_ok(a, true) && attn_aligned(dt, D, o, sob, soh, sol)) return attn_win_launch<true>(a, st);
   return dt == S2H_BF16 ? attn_dispatch<bf16, true>(a, st) : attn_dispatch<float, true>(a, st);
 }
 
@@ -1352,6 +1354,6 @@ extern "C" int s2h_attn_bwd(int dt, int B, int H, int Lq, int Lk, int D,
   a.dv = dv; a.sdvb = sdvb; a.sdvh = sdvh; a.sdvl = sdvl;
   a.lse = (float*)lse; a.di = di_ws; a.scale = scale; a.p_drop = p_drop; a.seed = seed; a.seed_off = s2h_rng_offset_ptr();
   a.idx0 = idx0;
-  if (dt == S2H_BF16 && attn_win_ok(a)) return attn_win_launch<false>(a, st);
+  if (dt == S2H_BF16 && attn_win_ok(a, false)) return attn_win_launch<false>(a, st);
   return dt == S2H_BF16 ? attn_dispatch<bf16, false>(a, st) : attn_dispatch<float, false>(a, st);
 }

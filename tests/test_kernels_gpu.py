@@ -265,7 +265,9 @@ def test_attention_fwd_bwd(dtype, tol, B, H, Lq, Lk, D):
 
 @pytest.mark.parametrize("B,H,Lq,Lk,D", [(256, 4, 16, 16, 56), (512, 2, 4, 16, 56), (128, 2, 16, 64, 56),
                                          (64, 2, 64, 64, 56), (16, 8, 49, 49, 56), (13, 8, 8, 8, 32),
-                                         (3, 2, 7, 5, 40), (2, 3, 33, 17, 64), (5, 1, 1, 2, 8), (4, 2, 17, 64, 24)])
+                                         (3, 2, 7, 5, 40), (2, 3, 33, 17, 64), (5, 1, 1, 2, 8), (4, 2, 17, 64, 24),
+                                         # long query side, few keys (forward on the window kernel)
+                                         (13, 8, 1024, 8, 16), (2, 2, 130, 40, 64)])
 def test_small_window_attention(B, H, Lq, Lk, D):
     """Hiera window / pooled-query shapes (Lq, Lk <= 64) on the whole-instance kernels
     (attention.hip attn_win_*): forward, LSE and the one-launch backward against the fp32
