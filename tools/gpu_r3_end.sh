@@ -2,4 +2,4 @@
 set -o pipefail
 export TMPDIR=/tmp
 bash tools/gpu_round.sh || exit 1
-bash tools/gpu_prof2.sh r03_v9 || exit 1
+bash tools/gpu_prof2.sh ${TAG:-r03_v12} || exit 1
