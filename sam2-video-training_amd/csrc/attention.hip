@@ -1161,6 +1161,78 @@ __global__ __launch_bounds__(NW * 64) void attn_win_bwd_kernel(AttnArgs a) {
   }
 }
 
+// dK / dV of a few-query attention (Lq <= 16 against a long key side: the decoder's token -> image
+// attention, 8 tokens x 1024 image keys, head dim 16): per 64-key block, 4 waves of 16 keys compute
+// S^T = K Q^T and dP^T = V dO^T (keys on the MFMA rows, K / V fragments straight from global),
+// P^T and dS^T = P^T o (dP^T - Di) with the forward's LSE and the pre-pass Di of each query column,
+// then dV = P^T dO and dK = dS^T Q with the 16-deep MFMA over the query axis (P^T / dS^T through a
+// wave-private LDS slab, Q / dO k-major images read transposed).  The tile kernel ran each 64-key
+// block against a 64-query tile with 8 valid rows.
+template <int DP>
+__global__ __launch_bounds__(256) void attn_fewq_dkv_kernel(AttnArgs a) {
+  using MF = Mfma<bf16>;
+  constexpr int KS = DP + 8, QS = 16 + 8, NKT = DP / 32, ND = DP / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[2 * 16 * KS + 2 * 4 * 16 * QS];
+  bf16* Qs = smem;
+  bf16* Gs = Qs + 16 * KS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bf16* PT = Gs + 16 * KS + w * 2 * 16 * QS;  // this wave's P^T [key][q]
+  bf16* ST = PT + 16 * QS;                     // and dS^T
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int k0 = blockIdx.x * 64 + 16 * w;
+  lds_load_rows<bf16, 16, DP, KS, 256>(Qs, (const bf16*)a.q + b * a.sqb + h * a.sqh, a.sql, 0, a.Lq, a.D, tid);
+  lds_load_rows<bf16, 16, DP, KS, 256>(Gs, (const bf16*)a.o + b * a.sob + h * a.soh, a.sol, 0, a.Lq, a.D, tid);
+  const bf16* K = (const bf16*)a.k + b * a.skb + h * a.skh;
+  const bf16* V = (const bf16*)a.v + b * a.svb + h * a.svh;
+  MF::frag kf[NKT], vf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    kf[t] = frag_global<bf16>(K, a.skl, k0 + (lane & 15), a.Lk, t * 32 + (lane >> 4) * 8, a.D);
+    vf[t] = frag_global<bf16>(V, a.svl, k0 + (lane & 15), a.Lk, t * 32 + (lane >> 4) * 8, a.D);
+  }
+  const int q = lane & 15;
+  const bool qok = q < a.Lq;
+  const float lse2 = qok ? a.lse[(int64_t)bh * a.Lq + q] * LOG2E : 0.f;
+  const float di = qok ? a.di[(int64_t)bh * a.Lq + q] : 0.f;
+  const float sl2 = a.scale * LOG2E;
+  __syncthreads();
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int bo = q * KS + t * 32 + (lane >> 4) * 8;
+    s = MF::mma(kf[t], MF::load(&Qs[bo]), s);
+    dp = MF::mma(vf[t], MF::load(&Gs[bo]), dp);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kl = 4 * (lane >> 4) + r;
+    const float p = (qok && k0 + kl < a.Lk) ? exp2f(s[r] * sl2 - lse2) : 0.f;
+    PT[kl * QS + q] = (bf16)p;
+    ST[kl * QS + q] = (bf16)(p * (dp[r] - di));
+  }
+  // dV = P^T dO, dK = dS^T Q over the 16 query rows (rows >= Lq are zero in Qs / Gs and in P^T)
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  const v4s pa = *(const v4s*)&PT[(lane & 15) * QS + 4 * (lane >> 4)];
+  const v4s sa = *(const v4s*)&ST[(lane & 15) * QS + 4 * (lane >> 4)];
+  bf16* dK = (bf16*)a.dk + b * a.sdkb + h * a.sdkh;
+  bf16* dV = (bf16*)a.dv + b * a.sdvb + h * a.sdvh;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const f32x4 z = f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 dv = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(pa, tr_bfrag16(Gs, KS, 0, d * 16, lane), z, 0, 0, 0);
+    const f32x4 dk = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(sa, tr_bfrag16(Qs, KS, 0, d * 16, lane), z, 0, 0, 0);
+    const int col = d * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = k0 + 4 * (lane >> 4) + r;
+      if (key < a.Lk && col < a.D) {
+        dK[(int64_t)key * a.sdkl + col] = (bf16)(dk[r] * a.scale);
+        dV[(int64_t)key * a.sdvl + col] = (bf16)dv[r];
+      }
+    }
+  }
+}
+
 // A/B knob (s2h_attn_win): 0 keeps the small windows on the tile kernels
 static int g_attn_win = 1;
 extern "C" int s2h_attn_win(int on) {
@@ -1254,6 +1326,12 @@ static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
   if (!done_dq) hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP>), gq, dim3(256), 0, st, a);
   constexpr int NW = AttnCfg<T>::NW_DKV;
   dim3 gk((a.Lk + NW * 16 - 1) / (NW * 16), a.B * a.H);
+  if constexpr (sizeof(T) == 2 && DP <= 64) {
+    if (!done_dkv && g_attn_win && a.Lq <= 16 && a.p_drop <= 0.f) {
+      hipLaunchKernelGGL((attn_fewq_dkv_kernel<DP>), dim3((a.Lk + 63) / 64, a.B * a.H), dim3(256), 0, st, a);
+      done_dkv = true;
+    }
+  }
   if (!done_dkv) hipLaunchKernelGGL((attn_bwd_dkv_kernel<T, DP>), gk, dim3(NW * 64), 0, st, a);
   s2h_prof_end(slot, st);
   return (int)hipGetLastError();
