@@ -1233,6 +1233,73 @@ __global__ __launch_bounds__(256) void attn_fewq_dkv_kernel(AttnArgs a) {
   }
 }
 
+// dQ of a few-key attention (Lk <= 16 against a long query side: the decoder's image -> token
+// attention, 1024 image queries x 8 tokens): per 64-query block, 4 waves of 16 queries compute S, dP
+// against the one 16-key tile (K / V fragments shared from LDS / registers), dS = P o (dP - Di), and
+// dQ = dS K with the 16-deep MFMA over the key axis (dS through a wave-private LDS slab, K read
+// transposed).  The tile kernel paired each 64-query tile with a 64-key tile of 8 valid keys.
+template <int DP>
+__global__ __launch_bounds__(256) void attn_fewk_dq_kernel(AttnArgs a) {
+  using MF = Mfma<bf16>;
+  constexpr int KS = DP + 8, SS = 16 + 8, NKT = DP / 32, ND = DP / 16;
+  __shared__ __attribute__((aligned(16))) bf16 smem[16 * KS + 4 * 16 * SS];
+  bf16* Ks = smem;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  bf16* Sw = Ks + 16 * KS + w * 16 * SS;  // this wave's dS [q][key]
+  const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
+  const int q0 = blockIdx.x * 64 + 16 * w;
+  const bf16* K = (const bf16*)a.k + b * a.skb + h * a.skh;
+  const bf16* V = (const bf16*)a.v + b * a.svb + h * a.svh;
+  const bf16* Q = (const bf16*)a.q + b * a.sqb + h * a.sqh;
+  const bf16* dO = (const bf16*)a.o + b * a.sob + h * a.soh;
+  lds_load_rows<bf16, 16, DP, KS, 256>(Ks, K, a.skl, 0, a.Lk, a.D, tid);
+  MF::frag qf[NKT], gf[NKT], kf[NKT], vf[NKT];
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    const int d = t * 32 + (lane >> 4) * 8;
+    qf[t] = frag_global<bf16>(Q, a.sql, q0 + (lane & 15), a.Lq, d, a.D);
+    gf[t] = frag_global<bf16>(dO, a.sol, q0 + (lane & 15), a.Lq, d, a.D);
+    kf[t] = frag_global<bf16>(K, a.skl, lane & 15, a.Lk, d, a.D);
+    vf[t] = frag_global<bf16>(V, a.svl, lane & 15, a.Lk, d, a.D);
+  }
+  float lse2[4], di[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int row = q0 + 4 * (lane >> 4) + r;
+    lse2[r] = row < a.Lq ? a.lse[(int64_t)bh * a.Lq + row] * LOG2E : 0.f;
+    di[r] = row < a.Lq ? a.di[(int64_t)bh * a.Lq + row] : 0.f;
+  }
+  const float sl2 = a.scale * LOG2E;
+  f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < NKT; ++t) {
+    s = MF::mma(qf[t], kf[t], s);
+    dp = MF::mma(gf[t], vf[t], dp);
+  }
+  const bool kok = (lane & 15) < a.Lk;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const bool qok = q0 + 4 * (lane >> 4) + r < a.Lq;
+    const float p = (kok && qok) ? exp2f(s[r] * sl2 - lse2[r]) : 0.f;
+    Sw[(4 * (lane >> 4) + r) * SS + (lane & 15)] = (bf16)(p * (dp[r] - di[r]));
+  }
+  __syncthreads();  // the K tile (all waves' loads); dS rows are this wave's own
+  typedef short v4s __attribute__((ext_vector_type(4)));
+  const v4s sa = *(const v4s*)&Sw[(lane & 15) * SS + 4 * (lane >> 4)];
+  bf16* dQ = (bf16*)a.dq + b * a.sdqb + h * a.sdqh;
+#pragma unroll
+  for (int d = 0; d < ND; ++d) {
+    const f32x4 dq = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(sa, tr_bfrag16(Ks, KS, 0, d * 16, lane),
+                                                               f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const int col = d * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = q0 + 4 * (lane >> 4) + r;
+      if (row < a.Lq && col < a.D) dQ[(int64_t)row * a.sdql + col] = (bf16)(dq[r] * a.scale);
+    }
+  }
+}
+
 // A/B knob (s2h_attn_win): 0 keeps the small windows on the tile kernels
 static int g_attn_win = 1;
 extern "C" int s2h_attn_win(int on) {
@@ -1321,6 +1388,12 @@ static int attn_bwd_launch(const AttnArgs& a, hipStream_t st) {
       if constexpr (sizeof(T) == 2 && DP == 32) hipLaunchKernelGGL((attn_bwd_dkv_fewk_kernel<T, DP, 8>), dim3(a.B * a.H), dim3(512), 0, st, a);
       else hipLaunchKernelGGL((attn_bwd_dkv_fewk_kernel<T, DP>), dim3(a.B * a.H), dim3(256), 0, st, a);
       done_dkv = true;
+    }
+  }
+  if constexpr (sizeof(T) == 2 && DP <= 64) {
+    if (!done_dq && g_attn_win && a.Lk <= 16 && a.p_drop <= 0.f) {
+      hipLaunchKernelGGL((attn_fewk_dq_kernel<DP>), dim3((a.Lq + 63) / 64, a.B * a.H), dim3(256), 0, st, a);
+      done_dq = true;
     }
   }
   if (!done_dq) hipLaunchKernelGGL((attn_bwd_dq_kernel<T, DP>), gq, dim3(256), 0, st, a);
