@@ -74,7 +74,15 @@ def main():
         def spy(name, *args):
             if name in want:
                 fr = [f for f in traceback.extract_stack() if "sam2_video" in f.filename][-4:-1]
-                calls[(name, " <- ".join(f"{f.filename.split('sam2_video/')[-1]}:{f.lineno}" for f in reversed(fr)))] += 1
+                where = " <- ".join(f"{f.filename.split('sam2_video/')[-1]}:{f.lineno}" for f in reversed(fr))
+                # inside the frame tape's backward: which op's input gradient is being accumulated
+                f0 = sys._getframe(1)
+                while f0 is not None and not (f0.f_code.co_name == "backward" and "frametape" in f0.f_code.co_filename):
+                    f0 = f0.f_back
+                if f0 is not None and "op" in f0.f_locals:
+                    op = f0.f_locals["op"]
+                    where += f"  [tape op {getattr(op, 'kind', '?')} #{getattr(op, 'idx', '?')}, n={args[1] if len(args) > 1 else '?'}]"
+                calls[(name, where)] += 1
             return real(name, *args)
 
         _ops.call = spy
