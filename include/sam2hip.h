@@ -233,6 +233,18 @@ int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* fr_lk, const
                                const void* du, int64_t sgb, int64_t sgl, void* dq, int64_t sdqb, int64_t sdql, void* dk,
                                int64_t sdkl, const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
                                const uint32_t* keep, const int64_t* fr_koff, hipStream_t st);
+/* The same with the keys' inverse RoPE fused into the dK store (position_encoding.py:212-239
+ * apply_rotary_enc with repeat_freqs_k, transposed; replaces the separate rotation pass over dk):
+ * key rows < fr_nrot[f] of every batch block of frame f are rotated back with table row
+ * key % rope_period of cos / sin [period, 128] fp32 (head dim 256, every column rotated); the
+ * remaining rows (object-pointer keys) are stored as computed.  rope_cos == NULL: no rotation. */
+int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
+                                    const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql, const void* k,
+                                    int64_t skl, const void* mem, int64_t sml, const void* u, int64_t sub, int64_t sul,
+                                    const void* du, int64_t sgb, int64_t sgl, void* dq, int64_t sdqb, int64_t sdql,
+                                    void* dk, int64_t sdkl, const float* lse, float* di_ws, float scale, float p_drop,
+                                    uint64_t seed, const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
+                                    const float* rope_sin, int rope_period, const int* fr_nrot, hipStream_t st);
 /* [Wv | bv | 0] as a bf16 [N, ld] matrix (ld >= K + 1) from the bf16 weight [N, K] and the fp32 bias,
  * and its fp32 gradient g [N, ld] scattered back: gwv [N, K] += g[:, :K], gbv [N] += g[:, K]
  * (either nullable).  The value projection's parameters of the folded cross-attention. */

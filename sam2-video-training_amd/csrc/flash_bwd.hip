@@ -58,6 +58,11 @@ struct FlashBwdArgs {
   int64_t fr_krow[S2H_MAX_FRAMES];
   uint64_t fr_idx0[S2H_MAX_FRAMES];
   int64_t fr_koff[S2H_MAX_FRAMES];  // word offset of frame f's keep bitmap
+  // optional inverse RoPE of dK (V-fold key gradient, s2h_flash_bwd_frames_vfold_rope): key rows
+  // < fr_nrot[f] of every batch block are rotated back with table row key % rope_period
+  // (the k projection's RoPE epilogue, transposed); rope_cos == nullptr: none
+  const float* rope_cos; const float* rope_sin; int rope_period;
+  int fr_nrot[S2H_MAX_FRAMES];
 };
 
 // The frame table is read straight from the kernarg segment (scalar loads): indexing the by-value
@@ -849,11 +854,31 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
 
   if (!kv) return;
   bf16* DK = fr.dk + (int64_t)key * a.sdkl;
+  // inverse RoPE of the key gradient: the lane's 4 consecutive columns are 2 rotation pairs
+  const float* rc = nullptr;
+  const float* rsn = nullptr;
+  if (a.rope_cos != nullptr && key < (a.nfr > 0 ? kargs()->fr_nrot[b / a.bpf] : fr.Lk)) {
+    const int t = key % a.rope_period;
+    rc = a.rope_cos + (int64_t)t * (DP / 2);
+    rsn = a.rope_sin + (int64_t)t * (DP / 2);
+  }
 #pragma unroll
   for (int d = 0; d < DP / 16; ++d) {
+    float v4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v4[e] = dk[d][e] * a.scale;
+    if (rc != nullptr) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int i = 8 * d + 2 * g + j;  // pair index of columns 16 d + 4 g + 2 j, + 1
+        const float c = rc[i], sn = rsn[i], x0 = v4[2 * j], x1 = v4[2 * j + 1];
+        v4[2 * j] = x0 * c + x1 * sn;
+        v4[2 * j + 1] = x1 * c - x0 * sn;
+      }
+    }
     bf16 t4[4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) t4[e] = (bf16)(dk[d][e] * a.scale);
+    for (int e = 0; e < 4; ++e) t4[e] = (bf16)v4[e];
     *(uint2*)(DK + 16 * d + 4 * g) = *(const uint2*)t4;
   }
   if constexpr (!FOLD) {
@@ -1093,6 +1118,15 @@ extern "C" int s2h_flash_bwd_ok(int dt, int Lq, int D) { return s2h_flash_bwd_el
 // q / u / du / dq [nfr * bpf, Lq, ...] uniform (batch, row strides), k / m / dk PACKED per frame
 // like s2h_flash_bwd_frames (row strides), u / du rows of >= 72 columns; no dV (the memory is
 // detached).  Di is computed by the dQ kernel into di_ws [nfr * bpf * Lq].
+extern "C" int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
+                                               const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql,
+                                               const void* k, int64_t skl, const void* mem, int64_t sml, const void* u,
+                                               int64_t sub, int64_t sul, const void* du, int64_t sgb, int64_t sgl,
+                                               void* dq, int64_t sdqb, int64_t sdql, void* dk, int64_t sdkl,
+                                               const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                                               const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
+                                               const float* rope_sin, int rope_period, const int* fr_nrot,
+                                               hipStream_t st);
 extern "C" int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
                                           const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql,
                                           const void* k, int64_t skl, const void* mem, int64_t sml, const void* u,
@@ -1100,6 +1134,19 @@ extern "C" int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* f
                                           int64_t sdqb, int64_t sdql, void* dk, int64_t sdkl, const float* lse,
                                           float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
                                           const int64_t* fr_koff, hipStream_t st) {
+  return s2h_flash_bwd_frames_vfold_rope(nfr, bpf, Lq, fr_lk, fr_krow, fr_idx0, q, sqb, sql, k, skl, mem, sml, u, sub,
+                                         sul, du, sgb, sgl, dq, sdqb, sdql, dk, sdkl, lse, di_ws, scale, p_drop, seed,
+                                         keep, fr_koff, nullptr, nullptr, 1, nullptr, st);
+}
+extern "C" int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
+                                               const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql,
+                                               const void* k, int64_t skl, const void* mem, int64_t sml, const void* u,
+                                               int64_t sub, int64_t sul, const void* du, int64_t sgb, int64_t sgl,
+                                               void* dq, int64_t sdqb, int64_t sdql, void* dk, int64_t sdkl,
+                                               const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                                               const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
+                                               const float* rope_sin, int rope_period, const int* fr_nrot,
+                                               hipStream_t st) {
   constexpr int D = 256, DV = 64;
   if (nfr <= 0 || bpf <= 0 || Lq <= 0) return 0;
   if (nfr > S2H_MAX_FRAMES || !s2h_flash_bwd_eligible(S2H_BF16, Lq, D)) return (int)hipErrorInvalidValue;
@@ -1141,6 +1188,12 @@ extern "C" int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* f
   a.seed_off = s2h_rng_offset_ptr();
   a.splits = 1; a.tiles_per_split = (lk_max + 63) / 64;
   a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32;
+  if (rope_cos != nullptr) {  // the dK rotation lives in the two-wave dK kernel's store only
+    if (rope_sin == nullptr || fr_nrot == nullptr || rope_period <= 0 || (s2h_flash_variant() & 1) != 0)
+      return (int)hipErrorInvalidValue;
+    a.rope_cos = rope_cos; a.rope_sin = rope_sin; a.rope_period = rope_period;
+    for (int f = 0; f < nfr; ++f) a.fr_nrot[f] = fr_nrot[f];
+  }
   int64_t lk_sum = 0;
   for (int f = 0; f < nfr; ++f) lk_sum += fr_lk[f];
   // profiler record: m4 = 1000 + DV (bench.py prices 2 (2 D + DV) per pair: dP over DV, dQ, dK)

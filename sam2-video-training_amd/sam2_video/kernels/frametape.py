@@ -27,6 +27,7 @@ from __future__ import annotations
 
 import collections
 import math
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -333,6 +334,7 @@ class FrameTape:
         self.producer = {v: op for op in self.ops for v in op.outs}
         self.nuse = collections.Counter(v for op in self.ops for v in op.ins if v is not None)
         self.premasked = set()
+        self.derotated = set()  # linear-with-RoPE outputs whose consumer returned the un-rotated gradient
         self.seeded = set(out_grads)
 
         def acc(vid, g):
@@ -417,7 +419,7 @@ def _linear_bw(tape, op, gys):
     mod, act, p = op.attrs["mod"], op.attrs["act"], op.attrs["p"]
     N, K = mod.compute_weight().shape
     gy2 = gy.view(-1, N)
-    if op.attrs.get("rope"):  # rotate the output gradient back (in place: the attention's fresh dq / dk)
+    if op.attrs.get("rope") and op.outs[0] not in tape.derotated:  # rotate the output gradient back (in place)
         ropes = op.fattrs["rope"]
         if all(r[2:] == ropes[0][2:] for r in ropes):
             ops.rope_blocks(gy2, ropes[0], inverse=True)
@@ -612,10 +614,34 @@ def _attn_vfold_bw(tape, op, gys):
     for f in range(F - 1):
         krow.append(krow[-1] + B * lks[f])
     ks = tape.stores[("aux", op.idx, "keep")] if a.get("keep") else None
+    rope = _vfold_k_rope(tape, op.ins[1], lks, D)
     ops.flash_bwd_frames_vfold(F, B, lks, krow, op.fattrs["idx0"], q_all, k_st.buf.view(-1, 1, D),
                                m_st.buf.view(-1, 1, ops.VFOLD_DV), u_all, gu, lse, dq, dk.view(-1, 1, D), a["scale"],
-                               a["p"], a["seed"], keep=ks.buf if ks else None, koff=ks.offsets if ks else None)
+                               a["p"], a["seed"], keep=ks.buf if ks else None, koff=ks.offsets if ks else None,
+                               rope=rope)
+    if rope is not None:
+        tape.derotated.add(op.ins[1])
     return [dq.view(-1), dk, None]
+
+
+def _vfold_k_rope(tape, kvid, lks, D):
+    """(cos, sin, period, nrot per frame) when the keys are the output of ONE linear-with-RoPE op
+    (the cross-attention's k projection, RoPE in its epilogue), used by this attention only, one
+    head of D columns rotated in full, one L-row block per object -- the dK store then rotates the
+    gradient back and the linear's backward skips its rope pass; else None"""
+    if os.environ.get("S2H_VFOLD_DK_ROPE", "1") == "0":
+        return None
+    prod = tape.producer.get(kvid)
+    if prod is None or prod.kind != "linear" or tape.nuse[kvid] != 1:
+        return None
+    ropes = prod.fattrs.get("rope")
+    if not ropes or len(ropes) != len(lks) or any(r is None for r in ropes):
+        return None
+    cos, sin, _, _, period, ncol, dh = ropes[0]
+    for f, r in enumerate(ropes):
+        if r[0] is not cos or r[1] is not sin or r[4] != period or r[5] != D or r[6] != D or r[2] != lks[f]:
+            return None
+    return cos, sin, period, [r[3] for r in ropes]
 
 
 def qkv_attention(tape: FrameTape, qkv, scale, p_drop, rope):

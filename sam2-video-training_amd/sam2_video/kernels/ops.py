@@ -323,10 +323,12 @@ def attn_fwd_vfold(q, k, mem, u, lse, scale, p_drop=0.0, seed=0, idx0=0, keep=No
 
 
 def flash_bwd_frames_vfold(nfr, bpf, lk, krow, idx0, q, k, mem, u, du, lse, dq, dk, scale, p_drop, seed, keep=None,
-                           koff=None):
+                           koff=None, rope=None):
     """Frame-batched backward of attn_fwd_vfold (s2h_flash_bwd_frames_vfold): q / u / du / dq
     [nfr*bpf, Lq, 1, C] views, k / mem / dk PACKED [rows, 1, C] (frame f: bpf blocks of lk[f] rows
-    from row krow[f]); keep / koff as flash_bwd_frames"""
+    from row krow[f]); keep / koff as flash_bwd_frames.  rope = (cos, sin, period, nrot per frame):
+    dk comes out rotated back (s2h_flash_bwd_frames_vfold_rope: the k projection's RoPE transposed,
+    fused into the dK store)"""
     import ctypes
     _dev(q, k, mem, u, du, lse, dq, dk)
     B, Lq = q.shape[0], q.shape[1]
@@ -345,11 +347,19 @@ def flash_bwd_frames_vfold(nfr, bpf, lk, krow, idx0, q, k, mem, u, du, lse, dq, 
     def rs(t):  # row stride of a packed [rows, 1, C] view
         assert t.stride(-1) == 1
         return t.stride(0)
-    call("s2h_flash_bwd_frames_vfold", nfr, bpf, Lq, ctypes.cast(alk, ctypes.c_void_p).value,
-         ctypes.cast(akr, ctypes.c_void_p).value, ctypes.cast(aix, ctypes.c_void_p).value,
-         ptr(q), *_brs(q), ptr(k), rs(k), ptr(mem), rs(mem), ptr(u), *_brs(u), ptr(du), *_brs(du),
-         ptr(dq), *_brs(dq), ptr(dk), rs(dk), ptr(lse), ptr(di), float(scale), float(p_drop),
-         int(seed) & (2**64 - 1), kp, ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None, stream())
+    args = [nfr, bpf, Lq, ctypes.cast(alk, ctypes.c_void_p).value, ctypes.cast(akr, ctypes.c_void_p).value,
+            ctypes.cast(aix, ctypes.c_void_p).value, ptr(q), *_brs(q), ptr(k), rs(k), ptr(mem), rs(mem), ptr(u), *_brs(u),
+            ptr(du), *_brs(du), ptr(dq), *_brs(dq), ptr(dk), rs(dk), ptr(lse), ptr(di), float(scale), float(p_drop),
+            int(seed) & (2**64 - 1), kp, ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None]
+    if rope is None:
+        call("s2h_flash_bwd_frames_vfold", *args, stream())
+    else:
+        cos, sin, period, nrot = rope
+        _dev(cos, sin)
+        assert cos.dtype == sin.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+        anr = (ctypes.c_int * nfr)(*[int(x) for x in nrot])
+        call("s2h_flash_bwd_frames_vfold_rope", *args, ptr(cos), ptr(sin), int(period),
+             ctypes.cast(anr, ctypes.c_void_p).value, stream())
     return dq, dk
 
 

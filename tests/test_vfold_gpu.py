@@ -258,3 +258,56 @@ def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
     for n in names:
         cos = torch.nn.functional.cosine_similarity(g0[n].flatten(), g1[n].flatten(), dim=0).item()
         assert cos >= 0.99, (n, cos)
+
+
+@pytest.mark.parametrize("lks,nrots,p_drop", [([1028, 2060], [1024, 2048], 0.1), ([1024, 516], [1024, 512], 0.0)])
+def test_vfold_dk_store_applies_inverse_rope(lks, nrots, p_drop):
+    """the V-fold dK kernel rotating the key gradient back in its store (s2h_flash_bwd_frames_vfold_rope:
+    the k projection's RoPE transposed, rows >= nrot -- object-pointer keys -- untouched) equals the
+    plain dK followed by the separate inverse rotation (ops.rope_blocks) within one bf16 rounding;
+    dQ is unaffected and bit-identical"""
+    from sam2_video.model.modeling.position_encoding import axial_rope_table
+    ops = _ops()
+    B, Lq, seed = 2, 1024, 5
+    fr = [_inputs(B, Lq, lk, 40 + i) for i, lk in enumerate(lks)]
+    scale = 256 ** -0.5
+    cos, sin = axial_rope_table(256, 32, 32, 10000.0, DEV)
+    idx0, koff, acc_e, acc_w, us, lses, keeps = [], [], 0, 0, [], [], []
+    for (q, k, m, _, _), lk in zip(fr, lks):
+        idx0.append(acc_e)
+        koff.append(acc_w)
+        u = torch.empty(B, Lq, 1, 72, device=DEV, dtype=torch.bfloat16)
+        lse = torch.empty(B, 1, Lq, device=DEV)
+        keep = torch.zeros(ops.keep_words(B, 1, Lq, lk), device=DEV, dtype=torch.int32)
+        ops.attn_fwd_vfold(q, k, m, u, lse, scale, p_drop, seed, idx0=acc_e, keep=keep if p_drop > 0 else None)
+        us.append(u)
+        lses.append(lse)
+        keeps.append(keep)
+        acc_e += B * Lq * lk
+        acc_w += keep.numel()
+    du = torch.cat([torch.randn(B, Lq, 1, 72, device=DEV).to(torch.bfloat16) for _ in lks])
+    q_all = torch.cat([f[0] for f in fr])
+    k_all = torch.cat([f[1].reshape(-1, 1, 256) for f in fr])
+    m_all = torch.cat([f[2].reshape(-1, 1, 64) for f in fr])
+    krow = [0, B * lks[0]]
+    kw = dict(keep=torch.cat(keeps) if p_drop > 0 else None, koff=koff if p_drop > 0 else None)
+    out = {}
+    for fused in (False, True):
+        dq = torch.empty_like(q_all)
+        dk = torch.full_like(k_all, float("nan"))
+        ops.flash_bwd_frames_vfold(2, B, lks, krow, idx0, q_all, k_all, m_all, torch.cat(us), du, torch.cat(lses), dq,
+                                   dk, scale, p_drop, seed, rope=(cos, sin, Lq, nrots) if fused else None, **kw)
+        if not fused:  # the separate pass the fusion replaces (frametape._linear_bw)
+            for f, lk in enumerate(lks):
+                blk = dk[krow[f]:krow[f] + B * lk].view(-1, 256)
+                ops.rope_blocks(blk, (cos, sin, lk, nrots[f], Lq, 256, 256), inverse=True)
+        torch.cuda.synchronize()
+        out[fused] = (dq, dk)
+    assert torch.equal(out[False][0], out[True][0])
+    assert not torch.isnan(out[True][1]).any()
+    _close(out[True][1], out[False][1], 1e-2, "dk fused inverse rope vs separate pass")
+    # the unrotated object-pointer rows are bit-identical
+    for f, lk in enumerate(lks):
+        a_ = out[True][1][krow[f]:krow[f] + B * lk].view(B, lk, 256)[:, nrots[f]:]
+        b_ = out[False][1][krow[f]:krow[f] + B * lk].view(B, lk, 256)[:, nrots[f]:]
+        assert torch.equal(a_, b_)

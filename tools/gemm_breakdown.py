@@ -26,13 +26,14 @@ def main():
     ap.add_argument("--hot", action="store_true")
     ap.add_argument("--cfgs", default="0,1,20,18,23,7,21,11,22,13,24")
     ap.add_argument("--ablate", type=int, default=1)
+    ap.add_argument("--shapes", type=int, default=99, help="first N shapes only")
     a = ap.parse_args()
     gt = graph_time if a.hot else graph_time_cold
     bf = torch.bfloat16
     torch.manual_seed(0)
     cfgs = [int(c) for c in a.cfgs.split(",")]
     L = _lib.lib()
-    for M, N, K in SHAPES:
+    for M, N, K in SHAPES[:a.shapes]:
         x = torch.randn(M, K, device="cuda", dtype=bf)
         w = torch.randn(N, K, device="cuda", dtype=bf) * 0.05
         b = torch.zeros(N, device="cuda")
@@ -47,7 +48,8 @@ def main():
                 L.s2h_gemm_config(c)
                 row += f" c{c}:{gt(fn):6.1f}"
             if a.ablate:
-                for d, nm in ((1, "nostore"), (2, "nomfma"), (4, "nodma"), (6, "storeonly")):
+                for d, nm in ((1, "nostore"), (2, "nomfma"), (4, "nodma"), (6, "storeonly"), (7, "skeleton"),
+                              (8, "plainst"), (14, "storeonly_plain")):
                     L.s2h_gemm_config(d << 8)
                     row += f" {nm}:{gt(fn):6.1f}"
             L.s2h_gemm_config(0)
