@@ -357,3 +357,41 @@ def test_arena_tail_ranks_follow_the_staged_backbone_backward():
             if rank(n) == r:
                 assert a.grad_cuts[r] <= a.offsets[n] < a.grad_cuts[r + 1], (n, r)
     assert rank("memory_attention.layers.0.linear1.weight") is None
+
+
+def test_vfold_key_rope_fusion_eligibility():
+    """host decision of the fused key-gradient RoPE (frametape._vfold_k_rope): only when the keys
+    come from ONE linear-with-RoPE op used by this attention alone, with one full-width head, the
+    same tables and period in every frame and one L-row block per object; nrot per frame is passed
+    through (object-pointer keys stay unrotated); S2H_VFOLD_DK_ROPE=0 turns it off"""
+    import collections
+
+    from sam2_video.kernels import frametape as ft
+    cos, sin = torch.zeros(1024, 128), torch.zeros(1024, 128)
+    lks = [1028, 2060]
+    ropes = [(cos, sin, 1028, 1024, 1024, 256, 256), (cos, sin, 2060, 2048, 1024, 256, 256)]
+    prod = SimpleNamespace(kind="linear", fattrs={"rope": ropes})
+    tape = SimpleNamespace(producer={7: prod}, nuse=collections.Counter({7: 1}))
+    got = ft._vfold_k_rope(tape, 7, lks, 256)
+    assert got is not None and got[0] is cos and got[1] is sin and got[2] == 1024 and got[3] == [1024, 2048]
+    tape.nuse[7] = 2  # the keys feed a second consumer: its gradient would not be rotated
+    assert ft._vfold_k_rope(tape, 7, lks, 256) is None
+    tape.nuse[7] = 1
+    assert ft._vfold_k_rope(tape, 7, [1028, 2061], 256) is None  # block length != frame keys
+    bad = [ropes[0], (torch.zeros(1024, 128), sin) + ropes[1][2:]]  # another table object
+    tape.producer[7] = SimpleNamespace(kind="linear", fattrs={"rope": bad})
+    assert ft._vfold_k_rope(tape, 7, lks, 256) is None
+    tape.producer[7] = SimpleNamespace(kind="linear", fattrs={"rope": [r[:5] + (128, 128) for r in ropes]})
+    assert ft._vfold_k_rope(tape, 7, lks, 256) is None  # multi-head / partial rotation
+    tape.producer[7] = SimpleNamespace(kind="add", fattrs={})
+    assert ft._vfold_k_rope(tape, 7, lks, 256) is None
+    tape.producer[7] = prod
+    old = os.environ.get("S2H_VFOLD_DK_ROPE")
+    os.environ["S2H_VFOLD_DK_ROPE"] = "0"
+    try:
+        assert ft._vfold_k_rope(tape, 7, lks, 256) is None
+    finally:
+        if old is None:
+            del os.environ["S2H_VFOLD_DK_ROPE"]
+        else:
+            os.environ["S2H_VFOLD_DK_ROPE"] = old
