@@ -15,6 +15,7 @@ single-mask output.  Other flag values raise.
 from __future__ import annotations
 
 import math
+import warnings
 
 import torch
 from torch import nn
@@ -28,6 +29,10 @@ from .sam.prompt_encoder import PromptEncoder
 from .sam.transformer import TwoWayTransformer
 
 NO_OBJ_SCORE = -1024.0  # sam2_base.py:18
+
+
+class ActivationCheckpointNotice(UserWarning):
+    """`use_activation_checkpoint=True` is accepted but does not recompute (see SAM2Base)"""
 
 
 class SAM2Base(nn.Module):
@@ -50,7 +55,15 @@ class SAM2Base(nn.Module):
         self.num_feature_levels = 3 if use_high_res_features_in_sam else 1
         self.use_obj_ptrs_in_encoder = use_obj_ptrs_in_encoder
         self.max_obj_ptrs_in_encoder = max_obj_ptrs_in_encoder
+        # The reference recomputes the memory attention / memory encoder / image encoder activations
+        # in the backward when set (sam2_base.py:362,706,752): a memory-for-compute trade with
+        # identical results.  Here every saved activation stays resident in HBM (a B+ 512^2 16-frame
+        # step needs a few GB of the 288 GB per GPU), so the flag is accepted and only recorded.
         self.use_activation_checkpoint = bool(use_activation_checkpoint)
+        if self.use_activation_checkpoint:
+            warnings.warn("use_activation_checkpoint=True: accepted, no recompute -- activations stay resident in "
+                          "HBM (results are identical; only peak memory differs from the reference)",
+                          ActivationCheckpointNotice, stacklevel=2)
         if use_obj_ptrs_in_encoder:
             self.mask_downsample = Conv2d(1, 1, 4, 4)
         self.add_tpos_enc_to_obj_ptrs = add_tpos_enc_to_obj_ptrs

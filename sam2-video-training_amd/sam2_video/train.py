@@ -3,6 +3,7 @@ Lightning and W&B are not installed:
 
     python -m sam2_video.train --config-dir /path/to/configs --config-name best \\
         trainer.max_steps=100 data.train_path=... [+key=value ...]
+    python -m sam2_video.train --config-json composed.json [key=value ...]   # an already composed tree
 
 Composes the config (sam2_video.utils.config.compose: defaults list, interpolation,
 overrides), seeds, instantiates `module` and `data_module` with `_recursive_=False` and the
@@ -22,18 +23,26 @@ import sys
 import torch
 
 
-def main(argv=None):
+def main(argv=None, before_fit=None):
+    """`before_fit(module, data_module, trainer)`, when given, runs right before trainer.fit (a test
+    hook: e.g. the parity mode's dropout 0)"""
     ap = argparse.ArgumentParser()
     ap.add_argument("--config-dir", default="configs")
     ap.add_argument("--config-name", default="best")
+    ap.add_argument("--config-json", default=None,
+                    help="a config tree composed beforehand (JSON); overrides still apply")
     ap.add_argument("--run-dir", default=None)
     ap.add_argument("overrides", nargs="*")
     args = ap.parse_args(argv)
     from .model.build import instantiate
-    from .utils.config import compose
+    from .utils.config import apply_overrides, compose
 
     run_dir = args.run_dir or os.path.join("outputs", args.config_name)
-    cfg = compose(args.config_dir, args.config_name, args.overrides, run_dir=run_dir)
+    if args.config_json:
+        with open(args.config_json) as f:
+            cfg = apply_overrides(json.load(f), args.overrides)
+    else:
+        cfg = compose(args.config_dir, args.config_name, args.overrides, run_dir=run_dir)
     seed = int(cfg.get("seed", 42))
     random.seed(seed)
     torch.manual_seed(seed)
@@ -43,6 +52,8 @@ def main(argv=None):
     module = instantiate(cfg["module"], _recursive_=False)
     data_module = instantiate(cfg["data_module"], _recursive_=False)
     trainer = instantiate(cfg["trainer"])
+    if before_fit is not None:
+        before_fit(module, data_module, trainer)
     hist = trainer.fit(module, data_module)
     ck = os.path.join(run_dir, "checkpoints")
     os.makedirs(ck, exist_ok=True)

@@ -84,7 +84,12 @@ def precision_dtype(precision) -> str:
 
 
 class SAM2LightningModule(_ModuleBase):
-    def __init__(self, model: Any, loss: Any, optimizer: Any, scheduler: Any, visualization: Any = None):
+    def __init__(self, model: Any, loss: Any, optimizer: Any, scheduler: Any, visualization: Any = None, *,
+                 gradient_clip_val: Optional[float] = None, accumulate_grad_batches: Optional[int] = None):
+        """The reference's five sections (trainer.py:38-99).  The two keyword-only extras carry the
+        clip and accumulation settings to the arena optimizer under a real Lightning Trainer, which
+        refuses manual optimization when its own `gradient_clip_val` / `accumulate_grad_batches`
+        are set (leave those at None / 1 there); this build's Trainer sets them from its arguments."""
         super().__init__()
         cfg = SimpleNamespace(model=model, loss=_ns(_todict(loss)), optimizer=_ns(_todict(optimizer)),
                               scheduler=_ns(_todict(scheduler)), visualization=_ns(_todict(visualization or {})))
@@ -112,7 +117,10 @@ class SAM2LightningModule(_ModuleBase):
         self.logged: Dict[str, Any] = {}
         self.optimizer = None
         self.lr_at = None
-        self.gradient_clip_val = None  # set by the Trainer (Lightning's trainer.gradient_clip_val)
+        # clip / accumulation of the arena optimizer (this build's Trainer overwrites them with its own
+        # arguments; under Lightning they come from here, see _lightning_runner)
+        self.gradient_clip_val = gradient_clip_val
+        self.accumulate_grad_batches = accumulate_grad_batches
         self.compute_dtype = None  # set by the Trainer from `precision`
         self._runner = None
 
@@ -212,8 +220,11 @@ class SAM2LightningModule(_ModuleBase):
 
     def _lightning_runner(self):
         """Manual-optimization runner for a Lightning trainer, built on the first training_step:
-        accumulation and clip from the trainer's settings, the schedule over its
-        estimated_stepping_batches, and the arena all-reduce whenever the process group has more
+        clip and accumulation from this module (`gradient_clip_val` / `accumulate_grad_batches`
+        keyword arguments) -- Lightning 2.x refuses manual optimization when the trainer's own
+        gradient_clip_val or accumulate_grad_batches is set, and so does this method, with the fix in
+        the message -- the schedule over the trainer's estimated_stepping_batches (optimizer steps:
+        micro-batches / accumulate), and the arena all-reduce whenever the process group has more
         than one rank (Lightning `strategy=ddp` must not wrap the module in
         DistributedDataParallel -- no parameter has a .grad -- use `arena_ddp_strategy()`)."""
         tr = self._attached_trainer()
@@ -221,12 +232,26 @@ class SAM2LightningModule(_ModuleBase):
             return None
         if self._runner is None:
             import torch.distributed as dist
+            clip_tr = getattr(tr, "gradient_clip_val", None)
+            acc_tr = getattr(tr, "accumulate_grad_batches", 1)
+            if clip_tr or (acc_tr or 1) != 1:
+                raise ValueError(
+                    f"Lightning Trainer(gradient_clip_val={clip_tr}, accumulate_grad_batches={acc_tr}) with manual "
+                    "optimization: Lightning rejects these; leave them at None / 1 and pass them to "
+                    "SAM2LightningModule(..., gradient_clip_val=..., accumulate_grad_batches=...) instead")
+            acc = max(1, int(self.accumulate_grad_batches or 1))
+            micro = max(1, int(getattr(tr, "estimated_stepping_batches", 1)))
             distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-            self._runner = StepRunner(self, total_steps=max(1, int(getattr(tr, "estimated_stepping_batches", 1))),
-                                      accumulate_grad_batches=getattr(tr, "accumulate_grad_batches", 1),
-                                      graph=False, gradient_clip_val=getattr(tr, "gradient_clip_val", None),
-                                      distributed=distributed)
+            self._runner = StepRunner(self, total_steps=max(1, math.ceil(micro / acc)), accumulate_grad_batches=acc,
+                                      graph=False, gradient_clip_val=self.gradient_clip_val, distributed=distributed)
         return self._runner
+
+    def on_train_epoch_end(self) -> None:
+        """Lightning hook: close the epoch's partial accumulation window (step the optimizer on what it
+        holds), as this build's Trainer does after each epoch; otherwise its gradient would leak into
+        the next epoch's first window"""
+        if self._runner is not None:
+            self._runner.flush()
 
     @torch.no_grad()
     def validation_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
@@ -465,7 +490,8 @@ class SAM2LightningDataModule(_DataBase):
     (configs/data/*.yaml: train_path, val_path, image_size, video_clip_length, stride,
     num_workers, batch_size, num_categories) is read as the reference reads it; when the COCO
     annotation files are not present the loaders yield deterministic synthetic clips of the same
-    shape (data/synthetic.py), `synthetic_clips` per split."""
+    shape (data/synthetic.py): `synthetic_clips` per split, clip indices from
+    `synthetic_{train,val}_offset` (default 0 / 100000), `synthetic_objects` objects."""
 
     def __init__(self, data: Any, train_shuffle: bool = True):
         if _DataBase is not object:  # pragma: no cover
@@ -488,7 +514,7 @@ class SAM2LightningDataModule(_DataBase):
                                     num_frames=int(_get(d, "video_clip_length", 8)),
                                     image_size=int(_get(d, "image_size", 512)), n_cat=n_cat,
                                     n_obj=int(_get(d, "synthetic_objects", n_cat)),
-                                    offset=0 if split == "train" else 100_000)
+                                    offset=int(_get(d, f"synthetic_{split}_offset", 0 if split == "train" else 100_000)))
 
     def setup(self, stage: str = "fit"):
         if stage == "fit":

@@ -245,8 +245,9 @@ def _lightning_path_worker(rank, world, port, q):
         init_from_env("gloo")
         n = 1000
         mod, arena = _stub_lightning_module(mp_, n, rank)
-        mod._trainer = SimpleNamespace(estimated_stepping_batches=2, accumulate_grad_batches=2,
-                                       gradient_clip_val=1.0)
+        mod.gradient_clip_val, mod.accumulate_grad_batches = 1.0, 2  # on the module, not the trainer
+        mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=1,
+                                       gradient_clip_val=None)
         assert mod.configure_optimizers() is None  # Lightning's own call: the runner owns AdamW
         batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
         for i in range(4):  # 2 accumulation windows of 2 micro-steps
@@ -313,6 +314,88 @@ def test_runner_zeroes_each_window_and_flushes_partial(monkeypatch):
     assert run.flush() and len(mod.optimizer.seen) == 3 and run.micro_step % 3 == 0
     assert torch.allclose(mod.optimizer.seen[2], (base + 30) / 3)
     assert not run.flush()
+
+
+def test_lightning_trainer_clip_or_accumulate_rejected(monkeypatch):
+    """Lightning 2.x refuses manual optimization with the trainer's gradient_clip_val or
+    accumulate_grad_batches set: so does the runner, naming the module arguments that
+    replace them; the module's own settings reach the runner (accumulation, clip, and a schedule
+    over optimizer steps)"""
+    batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
+    for clip, acc in ((1.0, 1), (None, 16), (0.5, 4)):
+        mod, _ = _stub_lightning_module(monkeypatch, 8, 0)
+        mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=acc,
+                                       gradient_clip_val=clip)
+        with pytest.raises(ValueError, match="accumulate_grad_batches=..."):
+            mod.training_step(batch, 0)
+    from sam2_video.training.trainer import SAM2LightningModule
+    mod = SAM2LightningModule(SimpleNamespace(), {"iou_use_l1_loss": True, "weight_dict": {"loss_mask": 1, "loss_dice": 1, "loss_iou": 1}},
+                              {"lr": 1e-4},
+                              {"enabled": False},
+                              gradient_clip_val=1.0, accumulate_grad_batches=16)
+    assert mod.gradient_clip_val == 1.0 and mod.accumulate_grad_batches == 16
+    mod, _ = _stub_lightning_module(monkeypatch, 8, 0)
+    mod.gradient_clip_val, mod.accumulate_grad_batches = 0.1, 3
+    mod._trainer = SimpleNamespace(estimated_stepping_batches=7, accumulate_grad_batches=1, gradient_clip_val=None)
+    mod.training_step(batch, 0)
+    assert mod._runner.accumulate == 3 and mod.optimizer.max_grad_norm == 0.1
+
+
+def test_lightning_epoch_end_flushes_partial_window(monkeypatch):
+    """on_train_epoch_end steps the optimizer on a partial accumulation window and the next
+    epoch's first window starts from a zeroed arena (the window leaked across epochs)"""
+    mod, arena = _stub_lightning_module(monkeypatch, 16, 0)
+    mod.accumulate_grad_batches = 2
+    mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=1, gradient_clip_val=None)
+    batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
+    base = torch.arange(16, dtype=torch.float32)
+    for i in range(3):  # epoch 1: one full window (calls 1, 2) + one partial (call 3)
+        mod.training_step(batch, i)
+    assert len(mod.optimizer.seen) == 1
+    mod.on_train_epoch_end()
+    assert len(mod.optimizer.seen) == 2 and torch.allclose(mod.optimizer.seen[1], (base + 30) / 2)
+    mod.training_step(batch, 0)  # epoch 2: the window restarts from zero
+    mod.training_step(batch, 1)
+    assert len(mod.optimizer.seen) == 3 and torch.allclose(mod.optimizer.seen[2], (2 * base + 40 + 50) / 2)
+    mod.on_train_epoch_end()  # nothing pending
+    assert len(mod.optimizer.seen) == 3
+
+
+def test_activation_checkpoint_flag_is_a_notice():
+    """overfit.yaml:46 sets use_activation_checkpoint: the build accepts it, records it and says
+    once at construction that it does not recompute (activations stay resident in HBM; results
+    are identical, only peak memory differs from the reference's recompute)"""
+    from sam2_video.model.modeling.sam2_base import ActivationCheckpointNotice
+    from sam2_video.model.sam2model import SAM2Model
+    with pytest.warns(ActivationCheckpointNotice, match="no recompute"):
+        m = SAM2Model(None, "tiny@128", use_activation_checkpoint=True)
+    assert m.use_activation_checkpoint
+    import warnings
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", ActivationCheckpointNotice)
+        assert not SAM2Model(None, "tiny@128").use_activation_checkpoint
+
+
+@needs_ref
+def test_overfit_fixture_matches_reference_composition():
+    """tests/golden/overfit_cfg1.json (the GPU box's config-1 input) is exactly the reference's
+    configs/overfit.yaml composed with oracle/gen_config_golden.py's overrides; its data module
+    yields the reference fixture's clip (synthetic clip 7, 4 frames, 256^2, 4 of 13 categories)"""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import gen_config_golden as gcg
+    from sam2_video.data.synthetic import synthetic_batch
+    from sam2_video.model.build import instantiate
+    with open(gcg.OUT) as f:
+        assert json.load(f) == json.loads(json.dumps(gcg.composed()))
+    cfg = gcg.composed()
+    dm = instantiate(cfg["data_module"], _recursive_=False)
+    dm.setup("fit")
+    dm.data.num_workers = 0
+    b = next(iter(dm.train_dataloader()))
+    ref = synthetic_batch(7, 4, 256, 13, 4)
+    assert torch.equal(b.img_batch, ref.img_batch) and torch.equal(b.masks, ref.masks)
 
 
 def test_data_module_shards_clips_across_ranks():

@@ -1,0 +1,7 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 400 python -u tools/replay_diff.py --dtype fp8 --frames 16 --size 512 > gpurun_out/r4_diag_fp8.log 2>&1 || { tail -30 gpurun_out/r4_diag_fp8.log; exit 1; }
+cat gpurun_out/r4_diag_fp8.log
+timeout -k 10 400 python -u tools/replay_diff.py --dtype bf16 --frames 16 --size 512 > gpurun_out/r4_diag_bf16.log 2>&1 || { tail -30 gpurun_out/r4_diag_bf16.log; exit 1; }
+cat gpurun_out/r4_diag_bf16.log
