@@ -153,14 +153,62 @@ def pmc_traffic(kind):
     return float(d["bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
 
 
-def read_prof(_lib):
-    """[(ms, [kind, s0..s4])] of every record of the in-library launch profiler"""
+def read_prof(_lib, with_tags=False):
+    """[(ms, [kind, s0..s4])] of every record of the in-library launch profiler (with_tags: a third
+    element, the kernel tag of s2h_prof_read_tags)"""
     import ctypes
     n = _lib.lib().s2h_prof_count()
     ms = (ctypes.c_float * max(n, 1))()
     meta = (ctypes.c_int64 * (6 * max(n, 1)))()
     n = _lib.lib().s2h_prof_read(n, ctypes.cast(ms, ctypes.c_void_p), ctypes.cast(meta, ctypes.c_void_p))
-    return [(ms[i], [meta[6 * i + j] for j in range(6)]) for i in range(n)]
+    if not with_tags:
+        return [(ms[i], [meta[6 * i + j] for j in range(6)]) for i in range(n)]
+    tags = (ctypes.c_int64 * max(n, 1))()
+    _lib.lib().s2h_prof_read_tags(n, ctypes.cast(tags, ctypes.c_void_p))
+    return [(ms[i], [meta[6 * i + j] for j in range(6)], tags[i]) for i in range(n)]
+
+
+def kernel_name(kind, tag):
+    """the kernel a profiler record launched, as rocprofv3 names it (GEMM tilings from the tag of
+    s2h_prof_read_tags; attention entry points by family -- one record may span a kernel and its
+    key-split combine)"""
+    if kind != 4 or not tag:
+        return {1: "attention forward entry (flash_fwd / attn_fwd kernels)",
+                2: "attention backward entry (flash_bwd kernels)"}.get(kind, "gemm_kernel (fp32)")
+    bm, bn = tag & 0x3FF, (tag >> 10) & 0x3FF
+    wgm, wgn, ns, bk = (tag >> 20) & 0xF, (tag >> 24) & 0xF, (tag >> 28) & 0xF, 32 * ((tag >> 32) & 0xF)
+    akc, bkc, regs, mx8 = [bool((tag >> b) & 1) for b in (36, 37, 38, 39)]
+    tf = lambda x: "true" if x else "false"  # noqa: E731
+    if mx8:
+        return f"gemm_mx8_kernel<{bm}, {bn}>"
+    if regs:
+        return f"gemm16_kernel<{bm}, {bn}, {tf(akc)}, {tf(bkc)}>"
+    return f"gemm16g_kernel<{bm}, {bn}, {wgm}, {wgn}, {ns}, {bk}, {tf(akc)}, {tf(bkc)}>"
+
+
+def dominant_kernel(recs, kind, peak, nsteps=1):
+    """the single kernel with the most time in family `kind` (records tagged with the GEMM tiling
+    they launched): launches and avg duration per launch, algorithmic flop / bytes per launch (the
+    family's pricing), achieved rate and fraction of peak -- traceable to the same kernel's row of
+    a rocprofv3 kernel-stats summary"""
+    agg = {}
+    for ms, m, tag in recs:
+        k = 40 if m[0] == 4 and (m[5] & 8) else m[0]
+        if k != kind:
+            continue
+        a = agg.setdefault(kernel_name(m[0], tag), [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += ms
+        a[2] += record_flops(m[0], m)
+        a[3] += record_bytes(m[0], m)
+    if not agg:
+        return None
+    name, (n, ms, fl, by) = max(agg.items(), key=lambda kv: kv[1][1])
+    ach = fl / (ms * 1e-3) / 1e12
+    return {"name": name, "launches_per_step": n // nsteps, "avg_us": round(1e3 * ms / n, 2),
+            "alg_flop_per_launch": round(fl / n), "alg_bytes_per_launch": round(by / n),
+            "achieved_tflops": round(ach, 1), "frac": round(ach / peak, 4),
+            "share_of_family_ms": None}
 
 
 def kernel_table(recs):
@@ -221,6 +269,20 @@ def cpu_baseline(args):
             "sample": f"1 clip x {frames} frames (the timed workload's clip), {args.size} {args.image_size}^2, "
                       f"{args.objects} objects, fp32 fwd+loss+bwd (oracle, no optimizer step), {dt:.1f} s, "
                       f"{threads} threads"}
+
+
+def roctx():
+    """(resume, pause) of the ROCTx profiler control API, or no-ops: with `rocprofv3
+    --selected-regions` only the timed graph replays are collected (no setup copies, no warm-up,
+    no profiled eager step), so a committed kernel-stats summary covers exactly `steps` steps"""
+    import ctypes
+    for name in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so"):
+        try:
+            h = ctypes.CDLL(name)
+            return (lambda: h.roctxProfilerResume(0)), (lambda: h.roctxProfilerPause(0))
+        except OSError:
+            continue
+    return (lambda: None), (lambda: None)
 
 
 def spawn_ranks(n):
@@ -295,6 +357,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    prof_resume, prof_pause = roctx()
+    prof_resume()
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
         loss = runner(batches[k])
@@ -306,6 +370,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    prof_pause()
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=device)
@@ -329,11 +394,18 @@ def main():
             runner.graph = True
             torch.cuda.synchronize()
             print(f"profiled eager step loss {float(module.logged['train/total_loss']):.5f}", file=sys.stderr)
-        recs = read_prof(_lib)
+        recs3 = read_prof(_lib, with_tags=True)
+        recs = [(ms, m) for ms, m, _ in recs3]
         _lib.call("s2h_prof_enable", 0)
-        roof = family_roofline([(ms, m) for ms, m in recs], 1 if graph else args.steps)
+        nsteps = 1 if graph else args.steps
+        roof = family_roofline(recs, nsteps)
         if roof is not None:
             kind = roof.pop("_kind")
+            dk = dominant_kernel(recs3, kind, roof["peak"], nsteps)
+            if dk is not None:
+                fam_ms = roof["avg_launch_ms"] * roof["launches"]
+                dk["share_of_family_ms"] = round(dk["avg_us"] * 1e-3 * dk["launches_per_step"] * nsteps / fam_ms, 3)
+            roof["dominant_kernel"] = dk
             roof["traffic"], src = pmc_traffic(kind)
             if src:
                 roof["traffic_unit"] = "HBM bytes per launch (2*FETCH_SIZE + WRITE_SIZE), same launch mix"

@@ -52,6 +52,11 @@ int s2h_prof_count(void);
  * attention (1, 2): (batch*heads, Lq, Lk, head_dim, element size);
  * GEMM (4): (batch, M, N, K, 2*A_kcontig + B_kcontig + 4*bf16).  Synchronises the events. */
 int s2h_prof_read(int max, float* ms, int64_t* meta);
+/* tags[i] = the kernel record i launched (0 = not tagged): GEMM tilings as
+ * BM | BN << 10 | WGM << 20 | WGN << 24 | NS << 28 | (BK / 32) << 32 | A_kcontig << 36 |
+ * B_kcontig << 37 | register_staged << 38 | mx_fp8 << 39 -- the template arguments of the kernel
+ * rocprofv3 names (bench.py: the roofline's dominant kernel). */
+int s2h_prof_read_tags(int max, int64_t* tags);
 
 /* ---------------------------------------------------------------- GEMM
  * C[b](m,n) = act(alpha * sum_k A[b](m,k) B[b](k,n) + bias) * cscale[n], dropout(p, seed),

@@ -868,10 +868,14 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
 #pragma unroll
     for (int e = 0; e < 4; ++e) v4[e] = dk[d][e] * a.scale;
     if (rc != nullptr) {
+      // pairs 8 d + 2 g and + 1 (columns 16 d + 4 g .. + 3): one 8-B load per table (8-B aligned:
+      // the pair index is even, table rows DP / 2 floats)
+      const float2 c2 = *(const float2*)(rc + 8 * d + 2 * g);
+      const float2 s2 = *(const float2*)(rsn + 8 * d + 2 * g);
+      const float cs[2] = {c2.x, c2.y}, sns[2] = {s2.x, s2.y};
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int i = 8 * d + 2 * g + j;  // pair index of columns 16 d + 4 g + 2 j, + 1
-        const float c = rc[i], sn = rsn[i], x0 = v4[2 * j], x1 = v4[2 * j + 1];
+        const float c = cs[j], sn = sns[j], x0 = v4[2 * j], x1 = v4[2 * j + 1];
         v4[2 * j] = x0 * c + x1 * sn;
         v4[2 * j + 1] = x1 * c - x0 * sn;
       }

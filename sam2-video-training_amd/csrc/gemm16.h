@@ -32,3 +32,11 @@ struct GemmArgs16 {
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
 void s2h_prof_end(int slot, hipStream_t st);
+void s2h_prof_tag(int64_t tag);  // runtime.hip: the kernel of the current profiler record
+// profiler tag of a GEMM tiling (include/sam2hip.h, s2h_prof_read_tags)
+static inline int64_t gemm_tag(int BM, int BN, int WGM, int WGN, int NS, int BK, bool akc, bool bkc, bool regs,
+                               bool mx8) {
+  return (int64_t)BM | ((int64_t)BN << 10) | ((int64_t)WGM << 20) | ((int64_t)WGN << 24) | ((int64_t)NS << 28) |
+         ((int64_t)(BK / 32) << 32) | ((int64_t)akc << 36) | ((int64_t)bkc << 37) | ((int64_t)regs << 38) |
+         ((int64_t)mx8 << 39);
+}

@@ -429,6 +429,7 @@ static int launch_glds(GemmArgs16& a, int batch, hipStream_t st) {
   plan_splits(a, batch, BM, BN, st);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
   constexpr int NT = GemmShape<BM, BN, WGM, WGN, NS, BK>::NT;
+  s2h_prof_tag(gemm_tag(BM, BN, WGM, WGN, NS, BK, akc, bkc, false, false));
   dim3 g1(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, batch * a.splits);
   if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, true>), g1, dim3(NT), 0, st, a);
   else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, false>), g1, dim3(NT), 0, st, a);
@@ -441,6 +442,7 @@ template <int BM, int BN>
 static int launch16_regs(GemmArgs16& a, int batch, hipStream_t st) {
   plan_splits(a, batch, BM, BN, st);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
+  s2h_prof_tag(gemm_tag(BM, BN, 2, 2, 1, 64, akc, bkc, true, false));
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM, batch * a.splits);
   if (akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, true>), grid, dim3(256), 0, st, a);
   else if (akc && !bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, false>), grid, dim3(256), 0, st, a);

@@ -247,6 +247,7 @@ extern "C" int s2h_mx8_config(int cfg) {
 
 template <int BM, int BN>
 static void launch_mx8(const Mx8Args& a, hipStream_t st) {
+  s2h_prof_tag(gemm_tag(BM, BN, 2, 2, 2, 128, true, true, false, true));
   const dim3 grid(((a.e.N + BN - 1) / BN) * ((a.e.M + BM - 1) / BM));
   hipLaunchKernelGGL((gemm_mx8_kernel<BM, BN>), grid, dim3(256), 0, st, a);
 }

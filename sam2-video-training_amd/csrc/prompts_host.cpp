@@ -240,7 +240,8 @@ int s2h_prompt_objects(int N, int H, int W, const uint8_t* masks, int max_obj, i
   int base = 0;
   for (int c = 0; c < N; ++c) {
     for (int i = 0; i < cnt[c]; ++i) obj_cat[base + i] = c;
-    std::memcpy(stats + (int64_t)base * kStats, cst[c].data(), (size_t)cnt[c] * kStats * sizeof(int64_t));
+    if (cnt[c])  // an empty category's vector may have no storage (memcpy from null is UB even for 0 bytes)
+      std::memcpy(stats + (int64_t)base * kStats, cst[c].data(), (size_t)cnt[c] * kStats * sizeof(int64_t));
     if (lab && base) {
       int32_t* l = lab + c * hw;
       for (int64_t i = 0; i < hw; ++i)
@@ -256,7 +257,7 @@ int s2h_prompt_objects(int N, int H, int W, const uint8_t* masks, int max_obj, i
 int s2h_prompt_object_masks(int N, int H, int W, const int32_t* lab, int n_obj, float* out, int threads) {
   if (N < 0 || H <= 0 || W <= 0 || n_obj < 0 || (n_obj && (!lab || !out))) return 1;
   const int64_t hw = (int64_t)H * W;
-  std::memset(out, 0, (size_t)n_obj * hw * sizeof(float));
+  if (n_obj) std::memset(out, 0, (size_t)n_obj * hw * sizeof(float));
   parallel_for(N, threads, [&](int c) {
     const int32_t* l = lab + c * hw;
     for (int64_t i = 0; i < hw; ++i) {

@@ -22,12 +22,13 @@ extern "C" int s2h_rng_bind(const void* dev_u64) {
 const uint64_t* s2h_rng_offset_ptr() { return g_rng_off; }
 
 namespace {
-struct ProfRec { hipEvent_t a, b; int64_t meta[6]; };
+struct ProfRec { hipEvent_t a, b; int64_t meta[6]; int64_t tag; };
 std::mutex g_mu;
 std::vector<ProfRec> g_pool;
 int g_used = 0;
 bool g_on = false;
 int g_mask = 1;
+thread_local int t_slot = -1;  // the record the calling thread's current launch belongs to
 }  // namespace
 
 extern "C" int s2h_prof_enable(int cap) {
@@ -64,12 +65,26 @@ int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2,
   int i = g_used++;
   int64_t* m = g_pool[i].meta;
   m[0] = kind; m[1] = m0; m[2] = m1; m[3] = m2; m[4] = m3; m[5] = m4;
+  g_pool[i].tag = 0;
+  t_slot = i;
   record(g_pool[i].a, st);
   return i;
 }
+// the kernel the current record launches (called by the launchers once the tiling is chosen)
+void s2h_prof_tag(int64_t tag) {
+  if (t_slot >= 0) g_pool[t_slot].tag = tag;
+}
 void s2h_prof_end(int slot, hipStream_t st) {
   if (slot < 0) return;
+  t_slot = -1;
   record(g_pool[slot].b, st);
+}
+
+extern "C" int s2h_prof_read_tags(int max, int64_t* tags) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int n = g_used < max ? g_used : max;
+  for (int i = 0; i < n; ++i) tags[i] = g_pool[i].tag;
+  return n;
 }
 
 // ms[i] = duration of record i; meta[6*i..] = (kind, shape[5]). Synchronises on the events.

@@ -112,6 +112,7 @@ SIGNATURES = {
     "s2h_prof_reset": [],
     "s2h_prof_count": [],
     "s2h_prof_read": [I, P, P],
+    "s2h_prof_read_tags": [I, P],
     "s2h_prompt_objects": [I, I, I, P, I, P, P, P, P, I],
     "s2h_prompt_object_masks": [I, I, I, P, I, P, I],
     "s2h_mask_moments": [I, I, I, P, P, I],
@@ -153,6 +154,36 @@ def lib():
             h.s2h_gemm_w41(int(os.environ["S2H_GEMM_W41"]))
         _LIB = h
     return _LIB
+
+
+_HOST_LIB = None
+# the prompt stage's host-only entry points (csrc/prompts_host.cpp), resolvable from a separate
+# host build: tools/sanitize_host.sh points S2H_HOST_LIB_PATH at an ASan + UBSan build of them
+HOST_FUNCS = ("s2h_prompt_objects", "s2h_prompt_object_masks", "s2h_mask_moments")
+
+
+def host_lib():
+    """library holding the host-only prompt-stage entry points: libsam2hip.so, or the build named by
+    S2H_HOST_LIB_PATH (sanitizer runs)"""
+    global _HOST_LIB
+    path = os.environ.get("S2H_HOST_LIB_PATH")
+    if not path:
+        return lib()
+    if _HOST_LIB is None:
+        h = ctypes.CDLL(path)
+        for name in HOST_FUNCS:
+            fn = getattr(h, name)
+            fn.argtypes = SIGNATURES[name]
+            fn.restype = c_int
+        _HOST_LIB = h
+    return _HOST_LIB
+
+
+def host_call(name, *args):
+    rc = getattr(host_lib(), name)(*args)
+    if rc != 0:
+        raise HipKernelError(f"{name} failed with error {rc}")
+    return rc
 
 
 def call(name, *args):

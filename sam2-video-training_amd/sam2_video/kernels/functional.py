@@ -289,7 +289,7 @@ class VFoldOutProj:
         self.weight, self.bias = out_lin.weight, out_lin.bias  # autograd anchors (v_proj's ride along)
         self.out_features, self.in_features = out_lin.out_features, ops.VFOLD_COLS
         self._w = None
-        self._g = self._gb = self._dv = None
+        self._g = self._v32 = self._wo32 = self._dv = None
         self._gen = -1
 
     def compute_weight(self):
@@ -318,21 +318,27 @@ class VFoldOutProj:
         if gwo is None and gwv is None and gbv is None:
             return
         N, C = self.out_features, ops.VFOLD_COLS
-        if self._g is None:
-            self._g = torch.empty(N, C, device=dy.device, dtype=torch.float32)
-            self._gb = torch.empty(N, C, device=dy.device, dtype=dy.dtype)
-        ops.linear_wgrad(dy, x, self._g, accumulate=False)  # G = dY^T u'
-        ops.cast(self._g, self._gb.dtype, out=self._gb)
         v = self.vf.compute_weight()  # [Nv, 72]
         wo = self.out.compute_weight()  # [N, Nv]
         Nv = wo.shape[1]
+        if self._g is None:
+            f32 = dict(device=dy.device, dtype=torch.float32)
+            self._g = torch.empty(N, C, **f32)
+            # G stays fp32 for the two small products below (no bf16 rounding of the weight
+            # gradients' common factor; the reference takes dWo, dWv from fp32 accumulations):
+            # fp32 copies of the bf16 operands V and Wo, exact fp32 MFMA products
+            self._v32 = torch.empty(Nv, C, **f32)
+            self._wo32 = torch.empty(N, Nv, **f32)
+        ops.linear_wgrad(dy, x, self._g, accumulate=False)  # G = dY^T u'
+        ops.cast(v, torch.float32, out=self._v32)
+        ops.cast(wo, torch.float32, out=self._wo32)
         if gwo is not None:  # dWo += G V^T
-            ops.gemm(self._gb, v, gwo.view(N, Nv), M=N, N=Nv, K=C, lda_m=C, lda_k=1, ldb_k=1, ldb_n=C, ldc=Nv,
-                     beta=1.0)
+            ops.gemm(self._g, self._v32, gwo.view(N, Nv), M=N, N=Nv, K=C, lda_m=C, lda_k=1, ldb_k=1, ldb_n=C,
+                     ldc=Nv, beta=1.0)
         if gwv is not None or gbv is not None:  # dV = Wo^T G -> dWv, dbv
             if self._dv is None:
                 self._dv = torch.empty(Nv, C, device=dy.device, dtype=torch.float32)
-            ops.gemm(wo, self._gb, self._dv, M=Nv, N=C, K=N, lda_m=1, lda_k=Nv, ldb_k=C, ldb_n=1, ldc=C)
+            ops.gemm(self._wo32, self._g, self._dv, M=Nv, N=C, K=N, lda_m=1, lda_k=Nv, ldb_k=C, ldb_n=1, ldc=C)
             ops.vfold_grad(self._dv, gwv, gbv)
 
 

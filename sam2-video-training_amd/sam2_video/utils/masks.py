@@ -48,8 +48,8 @@ def object_moments(cat_masks, want_labels: bool = False):
         n = ctypes.c_int(0)
         cats = np.empty(cap, np.int32)
         stats = np.empty((cap, N_STATS), np.int64)
-        rc = _lib.lib().s2h_prompt_objects(N, H, W, m.ctypes.data, cap, ctypes.byref(n), cats.ctypes.data,
-                                           stats.ctypes.data, lab.ctypes.data if lab is not None else None, _THREADS)
+        rc = _lib.host_lib().s2h_prompt_objects(N, H, W, m.ctypes.data, cap, ctypes.byref(n), cats.ctypes.data,
+                                                stats.ctypes.data, lab.ctypes.data if lab is not None else None, _THREADS)
         if rc == 2:
             cap = n.value
             continue
@@ -63,7 +63,7 @@ def object_masks(labels: np.ndarray, n_obj: int) -> torch.Tensor:
     from ..kernels import _lib
     N, H, W = labels.shape
     out = torch.empty(n_obj, H, W, dtype=torch.float32)
-    _lib.call("s2h_prompt_object_masks", N, H, W, labels.ctypes.data, n_obj, out.data_ptr(), _THREADS)
+    _lib.host_call("s2h_prompt_object_masks", N, H, W, labels.ctypes.data, n_obj, out.data_ptr(), _THREADS)
     return out
 
 
@@ -73,7 +73,7 @@ def mask_moments(masks) -> np.ndarray:
     m = _u8(masks)
     B, H, W = m.shape
     stats = np.empty((B, N_STATS), np.int64)
-    _lib.call("s2h_mask_moments", B, H, W, m.ctypes.data, stats.ctypes.data, _THREADS)
+    _lib.host_call("s2h_mask_moments", B, H, W, m.ctypes.data, stats.ctypes.data, _THREADS)
     return stats
 
 

@@ -15,8 +15,23 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+# GPU run order: the per-kernel and per-module parity against the oracle / the reference's golden
+# vectors first, then the whole-step and predictor paths, the full-size BASELINE configurations
+# (long, size-independent checks) last -- a failure in a stress configuration under `-x` then no
+# longer hides the hot path's parity results
+_ORDER = ["test_kernels_gpu", "test_determinism_gpu", "test_mx8_gpu", "test_vfold_gpu", "test_frametape_gpu",
+          "test_parity_gpu", "test_eval", "test_training_step_gpu", "test_graph_gpu", "test_predictor_gpu", "test_ddp_gpu",
+          "test_config1_gpu", "test_configs_gpu", "test_fp8_gpu"]
+
+
+def _rank(item):
+    mod = item.module.__name__.rsplit(".", 1)[-1] if item.module is not None else ""
+    return _ORDER.index(mod) if mod in _ORDER else len(_ORDER) // 2
+
+
 def pytest_collection_modifyitems(config, items):
     import torch
+    items.sort(key=_rank)  # stable: file order kept within a module and among unranked modules
     if torch.cuda.is_available():
         return
     skip = pytest.mark.skip(reason="no GPU in this container")

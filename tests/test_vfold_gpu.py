@@ -236,7 +236,8 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
 def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
     """the fused value + output projection (FN.VFoldOutProj: one GEMM with W' = Wo [Wv | bv]) against
     the two GEMMs (S2H_VFOLD_OUT=0) in a bf16 B+ 256^2 training step, dropout off: logits, loss and
-    the out_proj / v_proj gradients of the memory cross-attention within bf16 rounding"""
+    the out_proj / v_proj gradients of the memory cross-attention within bf16 rounding (cosine >= 0.999,
+    max |difference| <= 2 % of the tensor's max |gradient|; G = dY^T u' kept in fp32)"""
     from step_harness import build_model, golden_batch, grads_by_name, load_golden, mask_iou, run_step
     g = load_golden("bplus256_point_all")
     batch = golden_batch(g).to(DEV)
@@ -255,9 +256,15 @@ def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
     assert abs(l0 - l1) <= 0.005 * abs(l0)
     names = [n for n in g0 if ".cross_attn_image.v_proj." in n or ".cross_attn_image.out_proj." in n]
     assert len(names) == 16
+    worst = {}
     for n in names:
         cos = torch.nn.functional.cosine_similarity(g0[n].flatten(), g1[n].flatten(), dim=0).item()
-        assert cos >= 0.99, (n, cos)
+        rel = ((g0[n] - g1[n]).abs().max() / g0[n].abs().max()).item()  # max error relative to the tensor's scale
+        worst[n] = (round(cos, 6), round(rel, 5))
+        assert cos >= 0.999, (n, cos)
+        # a systematic bias of the fused weight gradients (G rounded to bf16) would show here
+        assert rel <= 0.02, (n, rel)
+    print("out_proj / v_proj gradients, fused vs two GEMMs (cosine, max rel err):", worst)
 
 
 @pytest.mark.parametrize("lks,nrots,p_drop", [([1028, 2060], [1024, 2048], 0.1), ([1024, 516], [1024, 512], 0.0)])

@@ -2,8 +2,8 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/determinism_probe.py --reps 20 > gpurun_out/r4_detprobe3.log 2>&1 || { tail -30 gpurun_out/r4_detprobe3.log; exit 1; }
-grep -v "rep " gpurun_out/r4_detprobe3.log
+timeout -k 10 600 python -u -m pytest tests/test_determinism_gpu.py tests/test_vfold_gpu.py -x -q -s --timeout 200 --timeout-method thread > gpurun_out/r4_det_tests.log 2>&1 || { tail -30 gpurun_out/r4_det_tests.log; exit 1; }
+grep -i "passed\\|failed\\|fused vs" gpurun_out/r4_det_tests.log
 timeout -k 10 400 python -u tools/tape_diff.py --dtype bf16 --frames 8 --size 512 --show 6 > gpurun_out/r4_tape3.log 2>&1 || { tail -30 gpurun_out/r4_tape3.log; exit 1; }
 grep -v "      at" gpurun_out/r4_tape3.log | tail -30
 timeout -k 10 400 python -u tools/replay_diff.py --dtype fp8 --frames 16 --size 512 > gpurun_out/r4_replay_fp8.log 2>&1 || { tail -30 gpurun_out/r4_replay_fp8.log; exit 1; }
