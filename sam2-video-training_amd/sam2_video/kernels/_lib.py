@@ -141,7 +141,9 @@ def lib():
                 "or `make -C sam2-video-training_amd/csrc` (there is no CPU fallback)")
         h = ctypes.CDLL(LIB_PATH)
         for name, argtypes in SIGNATURES.items():
-            fn = getattr(h, name)
+            fn = getattr(h, name, None)
+            if fn is None:  # an older build selected by S2H_LIB_PATH (A/B runs): calling it raises
+                continue
             fn.argtypes = argtypes
             fn.restype = RESTYPES.get(name, c_int)
         if os.environ.get("S2H_GEMM_CFG"):  # measurement override of the GEMM tiling choice

@@ -58,7 +58,8 @@ def _losses(module, clips, graph):
                          ids=["config2", "config3", "config4"])
 def test_config_graph_replays_match_eager(cfg):
     """lr = 0 (fixed weights), dropout 0.1 as trained: 12 replays (config 2) / 4 (config 3) / 2
-    (config 4) of the captured step on different clips give the eager step's loss on each clip"""
+    (config 4) of the captured step on different clips give the eager step's loss on each clip to
+    1e-5 relative (the forward is bit-reproducible, tests/test_determinism_gpu.py)"""
     size, S, T, O = cfg
     n = {512: 12, 384: 4, 1024: 2}[S]
     clips = _clips(range(50, 50 + n), T, S, O, O)
@@ -66,8 +67,10 @@ def test_config_graph_replays_match_eager(cfg):
     graphed, run = _losses(_module(size, S), clips, graph=True)
     assert len(run._graphs) == 1
     assert all(math.isfinite(x) for x in eager + graphed), (eager, graphed)
+    # fixed weights: the replay is the eager step bit for bit up to the loss statistics' float
+    # atomics (summation order, ~1e-7); 1e-5 is the fp32-mode bound of test_graph_gpu.py
     for a, b in zip(eager, graphed):
-        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (eager, graphed)
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)
 
 
 def test_config2_bf16_close_to_fp32():
