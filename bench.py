@@ -186,7 +186,33 @@ def kernel_name(kind, tag):
     return f"gemm16g_kernel<{bm}, {bn}, {wgm}, {wgn}, {ns}, {bk}, {tf(akc)}, {tf(bkc)}>"
 
 
-def dominant_kernel(recs, kind, peak, nsteps=1):
+def event_overhead_ms(_lib, n=64):
+    """Per-record overhead of the in-library event brackets: `n` empty kernels (s2h_trace_marker)
+    each bracketed like a profiled launch, minus the per-kernel time of `n` back-to-back empty
+    kernels between one event pair (their execution + dispatch, as a replayed graph sees it).
+    An eager launch bracketed by events also times the dispatch ramp in front of the kernel; this
+    is subtracted from the dominant kernel's average so it is comparable with rocprofv3's
+    start-to-end kernel durations."""
+    st = torch.cuda.current_stream()
+    _lib.call("s2h_prof_reset")
+    _lib.call("s2h_prof_select", 8)
+    for _ in range(n):
+        _lib.call("s2h_trace_marker", 0, st.cuda_stream)
+    torch.cuda.synchronize()
+    bracketed = sorted(ms for ms, m in read_prof(_lib) if m[0] == 8)
+    _lib.call("s2h_prof_select", 0)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(n):
+        _lib.call("s2h_trace_marker", 0, st.cuda_stream)
+    e1.record(st)
+    torch.cuda.synchronize()
+    burst = e0.elapsed_time(e1) / n
+    _lib.call("s2h_prof_reset")
+    return max(0.0, bracketed[len(bracketed) // 2] - burst), bracketed[len(bracketed) // 2], burst
+
+
+def dominant_kernel(recs, kind, peak, nsteps=1, overhead_ms=0.0):
     """the single kernel with the most time in family `kind` (records tagged with the GEMM tiling
     they launched): launches and avg duration per launch, algorithmic flop / bytes per launch (the
     family's pricing), achieved rate and fraction of peak -- traceable to the same kernel's row of
@@ -203,9 +229,12 @@ def dominant_kernel(recs, kind, peak, nsteps=1):
         a[3] += record_bytes(m[0], m)
     if not agg:
         return None
-    name, (n, ms, fl, by) = max(agg.items(), key=lambda kv: kv[1][1])
-    ach = fl / (ms * 1e-3) / 1e12
-    return {"name": name, "launches_per_step": n // nsteps, "avg_us": round(1e3 * ms / n, 2),
+    name, (n, ms, fl, by) = max(agg.items(), key=lambda kv: kv[1][1] - kv[1][0] * overhead_ms)
+    raw = ms / n
+    avg = max(raw - overhead_ms, 1e-6)  # event-bracket overhead removed (event_overhead_ms)
+    ach = fl / n / (avg * 1e-3) / 1e12
+    return {"name": name, "launches_per_step": n // nsteps, "avg_us": round(1e3 * avg, 2),
+            "avg_us_event_bracket": round(1e3 * raw, 2), "event_overhead_us": round(1e3 * overhead_ms, 2),
             "alg_flop_per_launch": round(fl / n), "alg_bytes_per_launch": round(by / n),
             "achieved_tflops": round(ach, 1), "frac": round(ach / peak, 4),
             "share_of_family_ms": None}
@@ -269,20 +298,6 @@ def cpu_baseline(args):
             "sample": f"1 clip x {frames} frames (the timed workload's clip), {args.size} {args.image_size}^2, "
                       f"{args.objects} objects, fp32 fwd+loss+bwd (oracle, no optimizer step), {dt:.1f} s, "
                       f"{threads} threads"}
-
-
-def roctx():
-    """(resume, pause) of the ROCTx profiler control API, or no-ops: with `rocprofv3
-    --selected-regions` only the timed graph replays are collected (no setup copies, no warm-up,
-    no profiled eager step), so a committed kernel-stats summary covers exactly `steps` steps"""
-    import ctypes
-    for name in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so"):
-        try:
-            h = ctypes.CDLL(name)
-            return (lambda: h.roctxProfilerResume(0)), (lambda: h.roctxProfilerPause(0))
-        except OSError:
-            continue
-    return (lambda: None), (lambda: None)
 
 
 def spawn_ranks(n):
@@ -357,8 +372,9 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    prof_resume, prof_pause = roctx()
-    prof_resume()
+    # trace markers: a rocprofv3 kernel trace of this run keeps exactly the timed steps between them
+    # (tools/step_profile.py; no setup copies, warm-up or profiled eager step)
+    _lib.call("s2h_trace_marker", 1, torch.cuda.current_stream().cuda_stream)
     t0 = time.perf_counter()
     for k in range(args.warmup, total):
         loss = runner(batches[k])
@@ -370,7 +386,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
-    prof_pause()
+    _lib.call("s2h_trace_marker", 2, torch.cuda.current_stream().cuda_stream)
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], device=device)
@@ -396,15 +412,19 @@ def main():
             print(f"profiled eager step loss {float(module.logged['train/total_loss']):.5f}", file=sys.stderr)
         recs3 = read_prof(_lib, with_tags=True)
         recs = [(ms, m) for ms, m, _ in recs3]
+        ovh, ev_empty, burst = event_overhead_ms(_lib)  # (profiler still on: bracketed empty launches)
         _lib.call("s2h_prof_enable", 0)
         nsteps = 1 if graph else args.steps
         roof = family_roofline(recs, nsteps)
         if roof is not None:
             kind = roof.pop("_kind")
-            dk = dominant_kernel(recs3, kind, roof["peak"], nsteps)
+            dk = dominant_kernel(recs3, kind, roof["peak"], nsteps, ovh)
             if dk is not None:
                 fam_ms = roof["avg_launch_ms"] * roof["launches"]
-                dk["share_of_family_ms"] = round(dk["avg_us"] * 1e-3 * dk["launches_per_step"] * nsteps / fam_ms, 3)
+                dk["share_of_family_ms"] = round(dk["avg_us_event_bracket"] * 1e-3 * dk["launches_per_step"] * nsteps
+                                                 / fam_ms, 3)
+                dk["event_calibration"] = (f"empty kernel: {1e3 * ev_empty:.2f} us event-bracketed, {1e3 * burst:.2f} us "
+                                           "per kernel back to back; the difference is subtracted")
             roof["dominant_kernel"] = dk
             roof["traffic"], src = pmc_traffic(kind)
             if src:

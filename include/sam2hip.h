@@ -44,7 +44,7 @@ int s2h_rng_bind(const void* dev_u64);
 /* In-library launch profiler: `cap` > 0 pre-creates `cap` HIP event pairs and
  * brackets every launch of a selected kind on the stream it is launched on; 0 disables. */
 int s2h_prof_enable(int cap);
-/* kinds recorded: bit 1 attention forward, 2 attention backward, 4 GEMM (default 1) */
+/* kinds recorded: bit 1 attention forward, 2 attention backward, 4 GEMM, 8 trace markers (default 1) */
 int s2h_prof_select(int mask);
 int s2h_prof_reset(void);
 int s2h_prof_count(void);
@@ -57,6 +57,9 @@ int s2h_prof_read(int max, float* ms, int64_t* meta);
  * B_kcontig << 37 | register_staged << 38 | mx_fp8 << 39 -- the template arguments of the kernel
  * rocprofv3 names (bench.py: the roofline's dominant kernel). */
 int s2h_prof_read_tags(int max, int64_t* tags);
+/* Launches a one-lane no-op kernel (s2h_trace_marker_kernel) on `st`: brackets a region of a
+ * rocprofv3 kernel trace (bench.py's timed steps, tools/step_profile.py). */
+int s2h_trace_marker(int tag, hipStream_t st);
 
 /* ---------------------------------------------------------------- GEMM
  * C[b](m,n) = act(alpha * sum_k A[b](m,k) B[b](k,n) + bias) * cscale[n], dropout(p, seed),

@@ -113,6 +113,7 @@ SIGNATURES = {
     "s2h_prof_count": [],
     "s2h_prof_read": [I, P, P],
     "s2h_prof_read_tags": [I, P],
+    "s2h_trace_marker": [I, P],
     "s2h_prompt_objects": [I, I, I, P, I, P, P, P, P, I],
     "s2h_prompt_object_masks": [I, I, I, P, I, P, I],
     "s2h_mask_moments": [I, I, I, P, P, I],
