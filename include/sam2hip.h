@@ -268,6 +268,16 @@ int s2h_vfold_grad(int N, int K, int ld, const float* g, float* gwv, float* gbv,
 int s2h_linear_rope(int M, int N, int K, const void* A, int64_t lda, const void* W, int64_t ldw, const float* bias,
                     void* Y, int64_t ldy, const float* cosv, const float* sinv, int L, int nrot, int period, int ncol,
                     int dh, hipStream_t stream);
+/* Linear + dropout + residual + LayerNorm in one launch (bf16): C = R + dropout(A W^T + bias)
+ * (the residual stream x'), Y = LN(C) * gamma + beta, mean / rstd per row -- a projection and the
+ * residual add + LayerNorm that reads it (memory_attention.py:60-98: out_proj -> norm2, the
+ * cross-attention output -> norm3, linear2 -> the next layer's norm1; nn.LayerNorm).  N = 128 or 256
+ * (one workgroup per 64 full rows); A [M, K] (lda), W [N, K] (ldw), R / C / Y with row strides;
+ * 16-B aligned rows.  R may be NULL (no residual); dropout index = drop_idx0 + row * N + col. */
+int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda, const void* W, int64_t ldw,
+                      const float* bias, const void* R, int64_t ldr, float drop_p, uint64_t seed,
+                      uint64_t drop_idx0, void* C, int64_t ldc, const float* gamma, const float* beta, float eps,
+                      void* Y, int64_t ldy, float* mean, float* rstd, hipStream_t st);
 
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:

@@ -8,7 +8,7 @@
 // without transposed copies: each operand is either K-contiguous ("KC") or
 // M/N-contiguous, selected at compile time.  Tiles are staged through LDS in a
 // K-contiguous [row][k] image so both MFMA operands read 16-B fragments.
-#include "gemm16.h"
+#include "gemm_bf16.h"
 
 struct GemmArgs {
   int M, N, K;
@@ -265,6 +265,40 @@ extern "C" int s2h_linear_rope(int M, int N, int K, const void* A, int64_t lda, 
   b.rope_cos = cosv; b.rope_sin = sinv;
   b.rope_L = L; b.rope_nrot = nrot; b.rope_period = period; b.rope_ncol = ncol; b.rope_dh = dh;
   const int rc = s2h_gemm_bf16(b, 1, stream);
+  s2h_prof_end(slot, stream);
+  return rc;
+}
+
+// Projection + dropout + residual + LayerNorm in one launch (bf16; round 4):
+//   X' = R + drop(A W^T + bias)   (C, the residual stream)      Y = LN(X') * gamma + beta
+// with mean / rstd per row -- a Linear followed by the residual add + LayerNorm that reads it
+// (memory_attention.py:60-98 out_proj / cross-attention output / linear2 -> norm2 / norm3 / the
+// next layer's norm1).  Full-row tiles (64 rows x N, N = 128 or 256, gemm_cfg6.hip).
+int gemm_cfg_launch_6(int cfg, GemmArgs16& a, int batch, hipStream_t st);
+extern "C" int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda, const void* W, int64_t ldw,
+                                 const float* bias, const void* R, int64_t ldr, float drop_p, uint64_t seed,
+                                 uint64_t drop_idx0, void* C, int64_t ldc, const float* gamma, const float* beta,
+                                 float eps, void* Y, int64_t ldy, float* mean, float* rstd, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if ((N != 256 && N != 128) || K <= 0 || !A || !W || !C || !Y || !gamma || !beta || !mean || !rstd ||
+      !aligned16(A) || !aligned16(W) || !aligned16(C) || !aligned16(Y) || (R && !aligned16(R)) || lda % 8 ||
+      ldw % 8 || ldc % 8 || ldy % 8 || (R && ldr % 8) || K % 8 || (int64_t)M * lda >= (1ll << 31) ||
+      (int64_t)N * ldw >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  const int slot = s2h_prof_begin(stream, 4, 1, M, N, K, 2 + 1 + 4);
+  GemmArgs16 b = {};
+  b.M = M; b.N = N; b.K = K;
+  b.A = (const bf16*)A; b.lda_m = lda; b.lda_k = 1;
+  b.B = (const bf16*)W; b.ldb_k = 1; b.ldb_n = ldw;
+  b.C = C; b.ldc = ldc;
+  b.bias = bias; b.bias_mode = bias ? 1 : 0;
+  b.R = R; b.ldr = ldr;
+  b.drop_p = drop_p; b.seed = seed; b.seed_off = s2h_rng_offset_ptr(); b.drop_idx0 = drop_idx0;
+  b.alpha = 1.f;
+  b.vecA = 1; b.vecB = 1;
+  b.ln_gamma = gamma; b.ln_beta = beta; b.ln_eps = eps; b.ln_y = Y; b.ln_ldy = ldy; b.ln_mean = mean; b.ln_rstd = rstd;
+  const int cfg = N == 128 ? CFG_64x128_W41_NS4 : (K <= 256 ? CFG_64x256_W41_NS4 : CFG_64x256_W41_NS3);
+  const int rc = gemm_cfg_launch_6(cfg, b, 1, stream);
   s2h_prof_end(slot, stream);
   return rc;
 }

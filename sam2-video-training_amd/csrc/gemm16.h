@@ -26,6 +26,12 @@ struct GemmArgs16 {
   // tables' column (c % rope_dh) / 2.  rope_cos == nullptr: no rotation.
   const float* rope_cos; const float* rope_sin;
   int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
+  // optional LayerNorm of the finished output rows (round 4, s2h_linear_add_ln): the tile spans the
+  // whole output width (N <= 256, one wave per 16 full rows); C receives x' = R + drop(A W^T + b)
+  // (bf16, the residual stream), ln_y = LN(x') with gamma / beta / eps, ln_mean / ln_rstd per row --
+  // the residual add + LayerNorm that follows a projection (memory_attention.py:60-98), fused
+  const float* ln_gamma; const float* ln_beta; float ln_eps;
+  void* ln_y; int64_t ln_ldy; float* ln_mean; float* ln_rstd;
   int dbg;        // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
 };
 

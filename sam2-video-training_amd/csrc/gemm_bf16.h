@@ -459,6 +459,9 @@ enum GemmCfg {
   CFG_128_K32_NS3 = 16, CFG_256x64_W4_K32_NS3 = 17, CFG_64_NS4 = 18, CFG_64_K32_NS8 = 19,
   // 4 x 1 wave grids: every wave owns whole 64-column rows of the tile (128-B bf16 output rows)
   CFG_64_W41 = 20, CFG_128x64_W41 = 21, CFG_128x64_W41_K32_NS3 = 22, CFG_64_W41_NS4 = 23, CFG_128x64_W41_NS3 = 24,
+  // full-row tiles (round 4): one workgroup owns 64 rows x the whole N <= 256 output width, the four
+  // waves stacked along M (16 full rows each), the K ring 4 stages deep (K <= 256 in one round trip)
+  CFG_64x256_W41_NS4 = 25, CFG_64x128_W41_NS4 = 26, CFG_64x256_W41_NS3 = 27, CFG_64x256_W41_K32_NS4 = 28,
   CFG_REGS = 99
 };
 // per-translation-unit launchers: return -1 when `cfg` is not one of the unit's tilings
@@ -467,3 +470,4 @@ int gemm_cfg_launch_2(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_3(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_4(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_5(int cfg, GemmArgs16& a, int batch, hipStream_t st);
+int gemm_cfg_launch_6(int cfg, GemmArgs16& a, int batch, hipStream_t st);

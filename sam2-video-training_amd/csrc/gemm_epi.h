@@ -264,6 +264,68 @@ __device__ __forceinline__ void epilogue8(const GemmArgs16& p, int bz, int row, 
   st8_bf16(C, true, v, p.dbg & 8);
 }
 
+// epilogue8 + LayerNorm of the row (GemmArgs16 ln_*): the CPR lanes of one output row each hold 8
+// of its columns (CPR * 8 == N), so the row statistics are a CPR-lane xor reduction.  x' = R +
+// drop(alpha acc + bias) is rounded to bf16 (the residual stream as stored) before the statistics,
+// as the standalone LayerNorm kernel reads it (norm.hip ln_fwd_vec_kernel: two-pass variance).
+// Every lane of the wave calls this (the shuffles need them all); `live` guards the stores.
+template <int CPR>
+__device__ __forceinline__ void epilogue8_ln(const GemmArgs16& p, int bz, int row, int col0, const float* vin,
+                                             const float* bcol, bool live) {
+  float v[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = p.alpha * vin[e] + bcol[e];
+  if (p.drop_p > 0.f) {
+    const uint32_t thresh = (uint32_t)(p.drop_p * 4294967296.0);
+    const float inv_keep = 1.f / (1.f - p.drop_p);
+    const uint64_t idx0 = p.drop_idx0 + (uint64_t)bz * p.M * p.N + (uint64_t)row * p.N + col0;
+    bool k[8];
+    if ((idx0 & 1) == 0) {
+#pragma unroll
+      for (int h = 0; h < 4; ++h) s2h_keep_pair(p.seed, (idx0 >> 1) + h, thresh, k[2 * h], k[2 * h + 1]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) k[e] = s2h_keep(p.seed, idx0 + e, thresh);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
+  }
+  if (p.R && live) {
+    float rs[8];
+    ld8_bf16((const bf16*)p.R + (int64_t)bz * p.sR + (int64_t)row * p.ldr + col0, (p.vec8 & 4) != 0, rs);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += rs[e];
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    v[e] = (float)(bf16)v[e];
+    s += v[e];
+  }
+#pragma unroll
+  for (int o = CPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  const float mu = s / p.N;
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float d = v[e] - mu;
+    q += d * d;
+  }
+#pragma unroll
+  for (int o = CPR / 2; o > 0; o >>= 1) q += __shfl_xor(q, o, 64);
+  const float rs = 1.f / sqrtf(q / p.N + p.ln_eps);
+  if (!live) return;
+  st8_bf16((bf16*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0, true, v, p.dbg & 8);
+  float y[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) y[e] = (v[e] - mu) * rs * p.ln_gamma[col0 + e] + p.ln_beta[col0 + e];
+  st8_bf16((bf16*)p.ln_y + (int64_t)bz * p.M * p.ln_ldy + (int64_t)row * p.ln_ldy + col0, true, y, p.dbg & 8);
+  if (col0 == 0) {
+    p.ln_mean[(int64_t)bz * p.M + row] = mu;
+    p.ln_rstd[(int64_t)bz * p.M + row] = rs;
+  }
+}
+
 // compile-time loop: f(std::integral_constant<int, I>) for I in [B, E)
 template <int B, int E, typename F>
 __device__ __forceinline__ void static_for(F&& f) {
@@ -316,6 +378,18 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
       for (int rr = lane / WN; rr < 16; rr += RPI) {
         const int row = mw + i * 16 + rr;
         if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
+      }
+    } else if (WN % 32 == 0 && p.ln_gamma != nullptr) {
+      // LayerNorm of whole rows (s2h_linear_add_ln checked: N == WN, one wave per 16 full rows)
+      constexpr int CPR = WN / 8, RPP = 64 / CPR;
+      const int c8 = lane % CPR, rg = lane / CPR;
+      for (int ps = 0; ps < 16 / RPP; ++ps) {
+        const int rl = rg + ps * RPP;
+        const float4 lo = *(const float4*)&ep[rl * EPLD + 8 * c8];
+        const float4 hi = *(const float4*)&ep[rl * EPLD + 8 * c8 + 4];
+        const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const int row = mw + i * 16 + rl;
+        epilogue8_ln<CPR>(p, bz, row, nw + 8 * c8, v8, bcol8, row < p.M && !(p.dbg & 1));
       }
     } else if (WN % 32 == 0 && (p.vec8 & 1) && nw + WN <= p.N) {
       // 8 columns per lane, one 16-B store each (the wave's column block is entirely valid)

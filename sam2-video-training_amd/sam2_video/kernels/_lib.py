@@ -31,6 +31,7 @@ SIGNATURES = {
                  F, F, I, P],
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
     "s2h_linear_rope": [I, I, I, P, L, P, L, P, P, L, P, P, I, I, I, I, I, P],
+    "s2h_linear_add_ln": [I, I, I, P, L, P, L, P, P, L, F, c_uint64, c_uint64, P, L, P, P, F, P, L, P, P, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],

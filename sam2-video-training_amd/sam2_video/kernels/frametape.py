@@ -463,6 +463,39 @@ def _linear_bw(tape, op, gys):
     return [dx, dres]
 
 
+def linear_add_ln(tape: FrameTape, inp, mod, x, norm, eps, drop_p):
+    """(LN(x + y), x + y), y = drop(inp W^T + b), recorded as the two ops it replaces -- a linear
+    (its output y a value that is never stored: the fused kernel keeps it in registers; its backward
+    needs only the input and the dropout seed) and an add + LayerNorm (outputs LN(x + y), x + y; its
+    backward reads x + y, mean, rstd) -- and run as ONE launch (ops.linear_add_ln)"""
+    inp = inp if inp.is_contiguous() else inp.contiguous()
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("linear", [inp, None], _linear_bw,
+                            {"mod": mod, "act": None, "p": float(drop_p), "relu_out": False, "rope": False})
+    if first and tape.vid(inp) is None:
+        raise RuntimeError("tape linear: input must be a recorded value or declared input")
+    w = mod.compute_weight()
+    N = w.shape[0]
+    shape = (*inp.shape[:-1], N)
+    vid, y = tape._out(0, shape, inp.dtype, tape._varlen_scale(inp))  # the never-written value y
+    seed = tape._seed() if drop_p > 0 else 0
+    idx0 = tape._idx0(op, y.numel())
+    if first:
+        op.attrs["seed"] = seed
+        op.attrs["K"] = inp.shape[-1]
+    tape._finish(op, [vid], tape._req(op, (mod.weight, mod.bias)))
+    op2, _ = tape._begin("ln", [x, y], _ln_bw, {"mod": norm, "eps": eps, "add": True})
+    rows = x.numel() // x.shape[-1]
+    vt, t = tape._out(0, x.shape, x.dtype)
+    vs, xsum = tape._out(1, x.shape, x.dtype)
+    mean = tape._aux("mean", (rows,), torch.float32)
+    rstd = tape._aux("rstd", (rows,), torch.float32)
+    ops.linear_add_ln(inp, w, mod.compute_bias(), x, norm.weight.detach(), norm.bias.detach(), eps, drop_p=drop_p,
+                      seed=seed, drop_idx0=idx0, xsum=xsum, y=t, mean=mean, rstd=rstd)
+    tape._finish(op2, [vt, vs], tape._req(op2, (norm.weight, norm.bias)))
+    return t, xsum
+
+
 # ---------------------------------------------------------------- layer norms
 def layer_norm(tape: FrameTape, x, mod, eps, add=None):
     """LN(x) or (LN(x + add), x + add)"""

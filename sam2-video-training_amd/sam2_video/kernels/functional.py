@@ -201,6 +201,68 @@ def add_layer_norm(x, add, mod, eps):
     return _LayerNorm.apply(x.contiguous(), mod.weight, mod.bias, mod, eps, add.contiguous(), False)
 
 
+# ------------------------------------------------ Linear + residual add + LayerNorm (one launch)
+def linear_ln_enabled():
+    """S2H_LINEAR_LN=0 keeps the projection and the residual add + LayerNorm as two launches (A/B)"""
+    import os
+    return os.environ.get("S2H_LINEAR_LN", "1") != "0"
+
+
+def _linear_ln_ok(inp, mod, norm):
+    N = mod.out_features
+    return (linear_ln_enabled() and inp.dtype == torch.bfloat16 and N in (128, 256) and norm.weight.shape[0] == N
+            and inp.shape[-1] % 8 == 0 and not (_fp8._eligible(mod) and _fp8._pays(inp.shape[-1], N)))
+
+
+class _LinearAddLN(torch.autograd.Function):
+    """(LN(x + drop(inp W^T + b)), x + drop(inp W^T + b)) from one full-row GEMM launch
+    (ops.linear_add_ln); backward: the LayerNorm backward (with the residual stream's gradient) and
+    the linear backward of its result"""
+
+    @staticmethod
+    def forward(ctx, inp, wp, bp, x, gp, gbp, mod, norm, eps, drop_p):
+        seed = next_seed() if drop_p > 0 else 0
+        t, xsum, mean, rstd = ops.linear_add_ln(inp, mod.compute_weight(), mod.compute_bias(), x, gp.detach(),
+                                                gbp.detach(), eps, drop_p=drop_p, seed=seed)
+        ctx.mod, ctx.norm, ctx.drop_p, ctx.seed = mod, norm, drop_p, seed
+        ctx.save_for_backward(inp, xsum, mean, rstd)
+        return t, xsum
+
+    @staticmethod
+    def backward(ctx, dt, dxsum):
+        inp, xsum, mean, rstd = ctx.saved_tensors
+        mod, norm = ctx.mod, ctx.norm
+        dt = torch.zeros_like(xsum) if dt is None else dt.contiguous()
+        dsum = ops.layernorm_bwd(xsum, dt, norm.weight.detach(), mean, rstd,
+                                 dres=dxsum.contiguous() if dxsum is not None else None,
+                                 dgamma=_grad_of(norm.weight), dbeta=_grad_of(norm.bias))
+        dpre = ops.act_dropout_bwd(None, dsum, None, ctx.drop_p, ctx.seed) if ctx.drop_p > 0 else dsum
+        wgrad = getattr(mod, "wgrad", None)
+        gw, gb = mod.grad_views()
+        if wgrad is not None:
+            wgrad(dpre, inp)
+        elif gw is not None:
+            ops.linear_wgrad(dpre, inp, gw.view(gw.shape[0], -1), db=gb)
+        elif gb is not None:
+            ops.colsum(dpre, gb)
+        dinp = _fp8.linear_dgrad(dpre, mod) if ctx.needs_input_grad[0] else None
+        return dinp, None, None, (dsum if ctx.needs_input_grad[3] else None), None, None, None, None, None, None
+
+
+def linear_add_layer_norm(inp, mod, x, norm, eps, drop_p=0.0):
+    """(LN(x + y), x + y) with y = drop(inp W^T + b): a projection followed by the residual add +
+    LayerNorm that reads it (memory_attention.py:60-98).  bf16 with a 128 / 256-wide output: one
+    full-row GEMM launch with the LayerNorm in its epilogue (s2h_linear_add_ln); else linear +
+    add_layer_norm."""
+    if not _linear_ln_ok(inp, mod, norm):
+        return add_layer_norm(x, linear(inp, mod, drop_p=drop_p), norm, eps)
+    T = _ft.active()
+    if T is not None:
+        return _ft.linear_add_ln(T, inp, mod, x, norm, eps, float(drop_p))
+    return _LinearAddLN.apply(inp.contiguous(), mod.weight, mod.bias, x.contiguous(), norm.weight, norm.bias, mod, norm,
+                              eps, float(drop_p))
+
+
 # ------------------------------------------------------------- attention
 def _keep_buffer(ctx, q, Lk, p_drop, nin):
     """dropout keep bitmap of a training attention on the flash path (the backward reads it

@@ -129,6 +129,27 @@ def linear_rope(x, w, bias, rp, out=None):
     return out
 
 
+def linear_add_ln(x, w, bias, residual, gamma, beta, eps, drop_p=0.0, seed=0, drop_idx0=0, xsum=None, y=None,
+                  mean=None, rstd=None):
+    """xsum = residual + dropout(x @ w^T + bias), y = LN(xsum) (gamma, beta, eps), mean / rstd per row, in
+    one launch (s2h_linear_add_ln; bf16, N = 128 or 256); returns (y, xsum, mean, rstd)"""
+    x2 = x.reshape(-1, x.shape[-1])
+    M, K = x2.shape
+    N = w.shape[0]
+    assert w.shape[1] == K and w.is_contiguous() and x2.stride(1) == 1 and x.dtype == torch.bfloat16
+    shape = (*x.shape[:-1], N)
+    xsum = torch.empty(shape, device=x.device, dtype=x.dtype) if xsum is None else xsum
+    y = torch.empty(shape, device=x.device, dtype=x.dtype) if y is None else y
+    mean = torch.empty(M, device=x.device, dtype=torch.float32) if mean is None else mean
+    rstd = torch.empty(M, device=x.device, dtype=torch.float32) if rstd is None else rstd
+    r2 = residual.reshape(-1, N) if residual is not None else None
+    _dev(x2, w, bias, r2, xsum, y, gamma, beta, mean, rstd)
+    call("s2h_linear_add_ln", M, N, K, ptr(x2), x2.stride(0), ptr(w), w.stride(0), ptr(bias), ptr(r2),
+         r2.stride(0) if r2 is not None else 0, float(drop_p), int(seed) & (2**64 - 1), int(drop_idx0), ptr(xsum), N,
+         ptr(gamma), ptr(beta), float(eps), ptr(y), N, ptr(mean), ptr(rstd), stream())
+    return y, xsum, mean, rstd
+
+
 def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0):
     """dx = alpha * dy @ w   (optionally * act'(pre) elementwise, fusing the previous layer's
     activation grad; for ReLU `pre` may be the previous layer's output, and alpha its 1/keep)."""

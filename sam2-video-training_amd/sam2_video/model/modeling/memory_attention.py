@@ -55,32 +55,35 @@ class MemoryAttentionLayer(nn.Module):
 
     def sublayers(self, x, t, mem_k, mem_v, num_k_exclude_rope, next_norm):
         """The layer on the residual stream x with t = norm1(x) given; returns (x', next_norm(x')).
-        Every residual add is fused with the LayerNorm that reads its result (FN.add_layer_norm:
-        LN(x + y) and x + y from one kernel, and in the backward LN'(.) + the stream's gradient
-        in one pass), so each residual state has a single autograd consumer and no separate
+        Every residual add is fused with the LayerNorm that reads its result, and (bf16) with the
+        projection that produces it: FN.linear_add_layer_norm runs out_proj / the folded
+        cross-attention output / linear2, dropout, the residual add and the next LayerNorm as ONE
+        full-row GEMM launch (LN(x + y) and x + y; in the backward LN'(.) + the stream's gradient in
+        one pass), so each residual state has a single autograd consumer and no separate
         gradient-accumulation adds run (memory_attention.py:58-99 order and dropouts)."""
         L = x.shape[1]
         C = self.d_model
         p = self._drop()
         sa = self.self_attn
         if self._fused_qkv is not None and sa.num_heads == 1:
-            # one q/k/v GEMM with q and k rotated in its epilogue
+            # one q/k/v GEMM with q and k rotated in its epilogue; out_proj + residual + norm2 as one
+            # full-row GEMM with the LayerNorm in its epilogue (FN.linear_add_layer_norm)
             cos, sin = sa.tables(L, t.device)
             qkv = self._fused_qkv(t, rope=(cos, sin, L, L, L, 2 * C, C))
             o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p())
-            y = sa.out_proj(o.reshape(qkv.shape[0], L, C), drop_p=p)
+            t, x = FN.linear_add_layer_norm(o.reshape(qkv.shape[0], L, C), sa.out_proj, x, self.norm2,
+                                            self.norm2.eps, drop_p=p)
         else:
             q = sa.proj_q(t, L)
             k = sa.proj_k(t, L)
             y = sa.attend(q, k, sa.v_proj(t), out_drop=p)
-        t, x = FN.add_layer_norm(x, y, self.norm2, self.norm2.eps)
+            t, x = FN.add_layer_norm(x, y, self.norm2, self.norm2.eps)
         ca = self.cross_attn_image
         q = ca.proj_q(t, L)
         k = ca.proj_k(mem_k, L, num_k_exclude_rope)
-        y = ca.attend_mem(q, k, mem_v, out_drop=p)
-        t, x = FN.add_layer_norm(x, y, self.norm3, self.norm3.eps)
-        y = self.linear2(self.linear1(t, act="relu", drop_p=p), drop_p=p)
-        t, x = FN.add_layer_norm(x, y, next_norm, next_norm.eps)
+        t, x = ca.attend_mem(q, k, mem_v, out_drop=p, add_ln=(x, self.norm3))
+        h = self.linear1(t, act="relu", drop_p=p)
+        t, x = FN.linear_add_layer_norm(h, self.linear2, x, next_norm, next_norm.eps, drop_p=p)
         return x, t
 
     def forward(self, tgt, mem_k, mem_v, num_k_exclude_rope=0):

@@ -68,21 +68,34 @@ class RoPEAttention(Attention):
             self._vfold = FN.VFoldProj(self.v_proj)
             self._vfold_out = FN.VFoldOutProj(self._vfold, self.out_proj)
 
-    def attend_mem(self, q, k, mem, residual=None, out_drop=0.0):
+    def attend_mem(self, q, k, mem, residual=None, out_drop=0.0, add_ln=None):
         """attention of projected q / k over the memory bank `mem` [B, Lk, 64] with its value
         projection: out_proj(attn(q, k, v_proj(mem))) (+ residual).  bf16 on the flash path runs the
         V-fold -- softmax(q k^T) (mem Wv^T + bv) = [P mem | rowsum(P)] [Wv | bv]^T: the 64-wide memory
-        is streamed instead of its 256-wide projection, which is never formed."""
+        is streamed instead of its 256-wide projection, which is never formed.  add_ln = (x, norm):
+        returns (norm(x + y), x + y) for the output y instead -- the residual add + LayerNorm that
+        follows (memory_attention.py:66-94), fused into the output GEMM where it can be."""
         B, Lq, I = q.shape
         Lk = k.shape[1]
         q4 = q.view(B, Lq, 1, I)
         if self._vfold is not None and FN.vfold_enabled() and ops.vfold_ok(q4, mem):
             u = FN.attention_vfold(q4, k.view(B, Lk, 1, I), mem.reshape(B, Lk, 1, mem.shape[-1]), p_drop=self._p())
             if FN.vfold_out_enabled():  # value and output projection as one GEMM (FN.VFoldOutProj)
-                return FN.linear(u.view(B, Lq, ops.VFOLD_COLS), self._vfold_out, residual=residual, drop_p=out_drop)
+                u3 = u.view(B, Lq, ops.VFOLD_COLS)
+                if add_ln is not None:
+                    x, norm = add_ln
+                    return FN.linear_add_layer_norm(u3, self._vfold_out, x, norm, norm.eps, drop_p=out_drop)
+                return FN.linear(u3, self._vfold_out, residual=residual, drop_p=out_drop)
             o = FN.linear(u.view(B, Lq, ops.VFOLD_COLS), self._vfold)
+            if add_ln is not None:
+                x, norm = add_ln
+                return FN.linear_add_layer_norm(o, self.out_proj, x, norm, norm.eps, drop_p=out_drop)
             return self.out_proj(o, residual=residual, drop_p=out_drop)
-        return self.attend(q, k, self.v_proj(mem), residual=residual, out_drop=out_drop)
+        y = self.attend(q, k, self.v_proj(mem), residual=residual, out_drop=out_drop)
+        if add_ln is not None:
+            x, norm = add_ln
+            return FN.add_layer_norm(x, y, norm, norm.eps)
+        return y
 
     def tables(self, Lq, device):
         w = h = math.sqrt(Lq)

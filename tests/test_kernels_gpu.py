@@ -91,7 +91,7 @@ def test_gemm_lds_dma_path(M, N, K, layout):
 
 
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24,
-                                 -1])
+                                 25, 26, 27, 28, -1])
 @pytest.mark.parametrize("M,N,K", [(1000, 520, 200), (600, 264, 1100), (13312, 256, 256)])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
 def test_gemm_every_tiling(cfg, M, N, K, layout):
@@ -977,3 +977,33 @@ def test_linear_rope_matches_linear_then_rope(dtype, Bt, L, nrot, N, ncol, dh):
     back = y.clone().view(-1, N)
     ops.rope_blocks(back, (cos, sin, L, nrot, period, ncol, dh), inverse=True)
     _close(back.view(Bt, L, N), (x.float() @ w.float().t() + b), 3e-2 if dtype == torch.bfloat16 else 1e-5)
+
+
+@pytest.mark.parametrize("M,N,K", [(13312, 256, 256), (13312, 256, 72), (13312, 256, 2048), (1000, 256, 200),
+                                   (13312, 128, 256), (333, 128, 64)])
+@pytest.mark.parametrize("p_drop,res", [(0.0, True), (0.1, True), (0.1, False)])
+def test_linear_add_ln_matches_unfused(M, N, K, p_drop, res):
+    """s2h_linear_add_ln (projection + dropout + residual + LayerNorm in one full-row launch) against
+    the unfused pair ops.linear(..., residual, dropout) + ops.layernorm_fwd: the residual stream x'
+    bit-identical (same tiling order over K, same epilogue), LN(x') / mean / rstd within fp32
+    summation order (one bf16 rounding of y)"""
+    ops = _ops()
+    torch.manual_seed(5)
+    bf = torch.bfloat16
+    ops.rng_offset(DEV).fill_(7)
+    x = torch.randn(M, K, device=DEV).to(bf)
+    w = (torch.randn(N, K, device=DEV) / K ** 0.5).to(bf)
+    b = torch.randn(N, device=DEV) * 0.1
+    r = torch.randn(M, N, device=DEV).to(bf) if res else None
+    g = torch.rand(N, device=DEV) + 0.5
+    be = torch.randn(N, device=DEV) * 0.1
+    y, xs, mean, rstd = ops.linear_add_ln(x, w, b, r, g, be, 1e-5, drop_p=p_drop, seed=99, drop_idx0=12)
+    ref_x = ops.linear(x, w, b, residual=r, drop_p=p_drop, seed=99, drop_idx0=12)
+    assert torch.equal(xs, ref_x)
+    ref_y, ref_m, ref_r = ops.layernorm_fwd(ref_x, g, be, 1e-5)
+    _close(y, ref_y, 8e-3)
+    torch.testing.assert_close(mean, ref_m, atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(rstd, ref_r, atol=1e-5, rtol=1e-4)
+    # and against fp32 torch (LayerNorm of the bf16 residual stream)
+    t = torch.nn.functional.layer_norm(ref_x.float(), (N,), g, be, 1e-5)
+    _close(y, t, 8e-3)
