@@ -139,14 +139,18 @@ class MLP(nn.Module):
         self.act = activation
         self.sigmoid_output = sigmoid_output
 
-    def forward(self, x, residual=None):
+    def forward(self, x, residual=None, norm=None):
+        """norm: the output (+ residual) LayerNorm'ed -- with a residual, the last layer, the add and the
+        LayerNorm as one launch (FN.linear_add_layer_norm; the two-way block's MLP -> norm3)"""
         for i, layer in enumerate(self.layers):
             last = i == self.num_layers - 1
             if last:
+                if norm is not None and residual is not None and not self.sigmoid_output:
+                    return FN.linear_add_layer_norm(x, layer, residual, norm, norm.eps)[0]
                 x = layer(x, act="sigmoid" if self.sigmoid_output else None, residual=residual)
             else:
                 x = layer(x, act=self.act)
-        return x
+        return norm(x) if norm is not None else x
 
 
 class Identity(nn.Module):

@@ -37,17 +37,23 @@ class Attention(nn.Module):
     def _p(self):
         return self.dropout_p if self.training else 0.0
 
-    def attend(self, q, k, v, residual=None, out_drop=0.0):
-        """q [B, Lq, I], k/v [B, Lk, I] projected -> out_proj(attn) (+ residual)"""
+    def attend(self, q, k, v, residual=None, out_drop=0.0, norm=None):
+        """q [B, Lq, I], k/v [B, Lk, I] projected -> out_proj(attn) (+ residual); norm: that sum
+        LayerNorm'ed (the post-norm of the two-way blocks, transformer.py:143-187) -- with a residual
+        as one full-row GEMM launch with the LayerNorm in its epilogue (FN.linear_add_layer_norm)"""
         B, Lq, I = q.shape
         Lk = k.shape[1]
         h = self.num_heads
         o = FN.attention(q.view(B, Lq, h, I // h), k.view(B, Lk, h, I // h), v.view(B, Lk, h, I // h),
                          p_drop=self._p())
-        return self.out_proj(o.reshape(B, Lq, I), residual=residual, drop_p=out_drop)
+        if norm is not None and residual is not None:
+            return FN.linear_add_layer_norm(o.reshape(B, Lq, I), self.out_proj, residual, norm, norm.eps,
+                                            drop_p=out_drop)[0]
+        y = self.out_proj(o.reshape(B, Lq, I), residual=residual, drop_p=out_drop)
+        return norm(y) if norm is not None else y
 
-    def forward(self, q, k, v, residual=None):
-        return self.attend(self.q_proj(q), self.k_proj(k), self.v_proj(v), residual=residual)
+    def forward(self, q, k, v, residual=None, norm=None):
+        return self.attend(self.q_proj(q), self.k_proj(k), self.v_proj(v), residual=residual, norm=norm)
 
 
 class RoPEAttention(Attention):
@@ -152,21 +158,19 @@ class TwoWayAttentionBlock(nn.Module):
         self.skip_first_layer_pe = skip_first_layer_pe
 
     def forward(self, queries, keys, query_pe, key_pe_table):
+        # every residual add and the post-norm after it run in the out-projection's epilogue
+        # (Attention.attend / MLP norm=: FN.linear_add_layer_norm)
         if self.skip_first_layer_pe:
-            queries = self.self_attn(queries, queries, queries)
+            queries = self.self_attn(queries, queries, queries, norm=self.norm1)
         else:
             q = FN.add(queries, query_pe)
-            queries = self.self_attn(q, q, queries, residual=queries)
-        queries = self.norm1(queries)
+            queries = self.self_attn(q, q, queries, residual=queries, norm=self.norm1)
         q = FN.add(queries, query_pe)
         k = FN.add_bcast(keys, key_pe_table)
-        queries = self.cross_attn_token_to_image(q, k, keys, residual=queries)
-        queries = self.norm2(queries)
-        queries = self.mlp(queries, residual=queries)
-        queries = self.norm3(queries)
+        queries = self.cross_attn_token_to_image(q, k, keys, residual=queries, norm=self.norm2)
+        queries = self.mlp(queries, residual=queries, norm=self.norm3)
         q = FN.add(queries, query_pe)
-        keys = self.cross_attn_image_to_token(k, q, queries, residual=keys)
-        keys = self.norm4(keys)
+        keys = self.cross_attn_image_to_token(k, q, queries, residual=keys, norm=self.norm4)
         return queries, keys
 
 
@@ -189,6 +193,5 @@ class TwoWayTransformer(nn.Module):
             queries, keys = layer(queries, keys, point_embedding, image_pe_table)
         q = FN.add(queries, point_embedding)
         k = FN.add_bcast(keys, image_pe_table)
-        queries = self.final_attn_token_to_image(q, k, keys, residual=queries)
-        queries = self.norm_final_attn(queries)
+        queries = self.final_attn_token_to_image(q, k, keys, residual=queries, norm=self.norm_final_attn)
         return queries, keys
