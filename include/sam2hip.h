@@ -278,6 +278,20 @@ int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda, const voi
                       const float* bias, const void* R, int64_t ldr, float drop_p, uint64_t seed,
                       uint64_t drop_idx0, void* C, int64_t ldc, const float* gamma, const float* beta, float eps,
                       void* Y, int64_t ldy, float* mean, float* rstd, hipStream_t st);
+/* Backward twin: input gradient of a Linear whose input is a LayerNorm output read by nothing else,
+ * with that LayerNorm's backward in the GEMM epilogue (bf16): dy = alpha * G W (G [M, K] the Linear's
+ * output gradient, W [K, N] its weight), dx = LN'(dy; X, gamma, mean, rstd) + dres (C [M, N]),
+ * dgamma / dbeta += (both or neither; `part` = s2h_linear_dgrad_ln_bwd_ws_bytes(M, N) bytes of
+ * per-tile partial rows).  Replaces linear dgrad + s2h_layernorm_bwd for memory_attention.py:60-98
+ * norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1 (torch autograd of nn.Linear +
+ * nn.LayerNorm).  N = 128 or 256; 16-B aligned rows; dres may be NULL. */
+int64_t s2h_linear_dgrad_ln_bwd_ws_bytes(int M, int N);
+int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64_t ldg, const void* W, int64_t ldw, float alpha,
+                            const void* X, int64_t ldx, const float* gamma, const float* mean, const float* rstd,
+                            const void* dres, int64_t ldr, void* dx, int64_t lddx, float* part, float* dgamma,
+                            float* dbeta, hipStream_t st);
+/* dgamma += sum_b part[b][0:C], dbeta += sum_b part[b][C:2C] over nb partial rows of 2C floats. */
+int s2h_ln_wgrad_finalize(int nb, int C, const float* part, float* dgamma, float* dbeta, hipStream_t st);
 
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:

@@ -303,6 +303,47 @@ extern "C" int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda
   return rc;
 }
 
+// Input gradient of a Linear whose input is a LayerNorm output it alone reads, with the LayerNorm
+// backward in the GEMM epilogue (bf16; round 4):
+//   dy = alpha * G W        (G [M, K] the Linear's output gradient, W [K, N] its weight)
+//   dx = LN_bwd(dy; X, gamma, mean, rstd) + dres                         (C [M, N], bf16)
+//   dgamma += sum_rows dy * xhat, dbeta += sum_rows dy                   (when dgamma != null)
+// -- memory_attention.py:60-98 norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1 in the
+// backward: the LayerNorm output's gradient stays in registers (never stored as bf16 and re-read).
+// `part` holds ceil(M / 64) * 2N floats (s2h_linear_dgrad_ln_bwd_ws_bytes).  Full-row tiles.
+extern "C" int s2h_ln_wgrad_finalize(int nb, int C, const float* part, float* dgamma, float* dbeta, hipStream_t st);
+extern "C" int64_t s2h_linear_dgrad_ln_bwd_ws_bytes(int M, int N) {
+  return M <= 0 ? 0 : (int64_t)((M + 63) / 64) * 2 * N * sizeof(float);
+}
+extern "C" int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64_t ldg, const void* W, int64_t ldw,
+                                       float alpha, const void* X, int64_t ldx, const float* gamma, const float* mean,
+                                       const float* rstd, const void* dres, int64_t ldr, void* dx, int64_t lddx,
+                                       float* part, float* dgamma, float* dbeta, hipStream_t stream) {
+  if (M <= 0) return 0;
+  if ((N != 256 && N != 128) || K <= 0 || !G || !W || !X || !dx || !gamma || !mean || !rstd ||
+      ((dgamma == nullptr) != (dbeta == nullptr)) || (dgamma && !part) || !aligned16(G) || !aligned16(W) ||
+      !aligned16(X) || !aligned16(dx) || (dres && !aligned16(dres)) || ldg % 8 || ldw % 8 || ldx % 8 || lddx % 8 ||
+      (dres && ldr % 8) || K % 8 || (int64_t)M * ldg >= (1ll << 31) || (int64_t)K * ldw >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  const int slot = s2h_prof_begin(stream, 4, 1, M, N, K, 2 + 0 + 4);
+  GemmArgs16 b = {};
+  b.M = M; b.N = N; b.K = K;
+  b.A = (const bf16*)G; b.lda_m = ldg; b.lda_k = 1;
+  b.B = (const bf16*)W; b.ldb_k = ldw; b.ldb_n = 1;
+  b.C = dx; b.ldc = lddx;
+  b.R = dres; b.ldr = ldr;
+  b.seed_off = s2h_rng_offset_ptr();
+  b.alpha = alpha;
+  b.vecA = 1; b.vecB = 1;
+  b.ln_gamma = gamma; b.ln_mean = const_cast<float*>(mean); b.ln_rstd = const_cast<float*>(rstd);
+  b.lnb_x = X; b.lnb_ldx = ldx; b.lnb_part = dgamma ? part : nullptr;
+  const int cfg = N == 128 ? CFG_64x128_W41_NS4 : (K <= 256 ? CFG_64x256_W41_NS4 : CFG_64x256_W41_NS3);
+  int rc = gemm_cfg_launch_6(cfg, b, 1, stream);
+  s2h_prof_end(slot, stream);
+  if (rc || !dgamma) return rc;
+  return s2h_ln_wgrad_finalize((M + 63) / 64, N, part, dgamma, dbeta, stream);
+}
+
 extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t ld, float* out, int accum,
                           hipStream_t st);
 

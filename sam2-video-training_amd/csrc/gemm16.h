@@ -32,7 +32,13 @@ struct GemmArgs16 {
   // the residual add + LayerNorm that follows a projection (memory_attention.py:60-98), fused
   const float* ln_gamma; const float* ln_beta; float ln_eps;
   void* ln_y; int64_t ln_ldy; float* ln_mean; float* ln_rstd;
-  int dbg;        // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
+  // optional LayerNorm BACKWARD of the finished rows (round 4, s2h_linear_dgrad_ln_bwd): the GEMM is
+  // the dgrad of the LayerNorm output's only consumer, alpha * acc = dL/dy over whole rows; lnb_x is
+  // the LayerNorm input (bf16), ln_gamma / ln_mean / ln_rstd its saved parameters and statistics,
+  // R the residual-stream gradient added to dx (may be null); C receives dx; lnb_part (may be null)
+  // one (sum dy * xhat, sum dy) row of 2N floats per 64-row tile for ln_wgrad_finalize_kernel
+  const void* lnb_x; int64_t lnb_ldx; float* lnb_part;
+  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
 };
 
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);

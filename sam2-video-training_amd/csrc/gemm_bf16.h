@@ -376,6 +376,13 @@ void gemm16g_kernel(GemmArgs16 p) {
   __syncthreads();
 
   if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
+  if constexpr (WGN == 1 && WN >= 128 && WN % 32 == 0) {  // full-row tiles: LayerNorm backward epilogue
+    if (p.lnb_x != nullptr) {
+      static_assert(NW * 16 * (WN + 4) * 4 + NW * 2 * WN * 4 <= NS * STAGE, "LayerNorm-backward epilogue LDS");
+      tile_epilogue_lnbwd<WM, WN, MI, NI, NW>(p, acc, smem, m0 + wm * WM, m0 / BM, lane, w);
+      return;
+    }
+  }
   tile_epilogue<WM, WN, MI, NI>(p, acc, reinterpret_cast<float*>(smem) + w * 16 * (WN + 4), bz, m0 + wm * WM,
                                 n0 + wn * WN, lane);
 }

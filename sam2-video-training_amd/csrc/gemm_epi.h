@@ -371,13 +371,18 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
       for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
     __builtin_amdgcn_wave_barrier();
     if (p.splits > 1) {
-      // split-K: one row per instruction, consecutive lanes on consecutive columns (256 B)
+      // split-K: consecutive lanes on consecutive columns (256 B per instruction): RPI rows of
+      // WN <= 64 columns, or 64-column pieces of one row for the full-row tiles (WN 128 / 256)
       float* C = (float*)p.C + (int64_t)bz * p.sC;
-      constexpr int RPI = 64 / WN;  // rows per instruction
-      const int col = nw + lane % WN;
-      for (int rr = lane / WN; rr < 16; rr += RPI) {
+      constexpr int CPI = WN < 64 ? WN : 64;  // columns per instruction
+      constexpr int RPI = 64 / CPI;           // rows per instruction
+      for (int rr = lane / CPI; rr < 16; rr += RPI) {
         const int row = mw + i * 16 + rr;
-        if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
+#pragma unroll
+        for (int cc = lane % CPI; cc < WN; cc += CPI) {
+          const int col = nw + cc;
+          if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + cc]);
+        }
       }
     } else if (WN % 32 == 0 && p.ln_gamma != nullptr) {
       // LayerNorm of whole rows (s2h_linear_add_ln checked: N == WN, one wave per 16 full rows)
@@ -417,6 +422,113 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
   });
 }
 
+
+// LayerNorm backward over whole output rows in the dgrad GEMM's epilogue (GemmArgs16 lnb_*; full-row
+// tiles, N == WN, the WGM waves stacked along M).  With dy = alpha * acc (fp32, never rounded),
+// g = dy * gamma, xhat = (x - mean) * rstd:
+//   dx = rstd * (g - mean_c(g) - xhat * mean_c(g * xhat)) [+ dres]     (norm.hip ln_bwd_vec_kernel)
+// and the tile's (sum_rows dy * xhat, sum_rows dy) partial row goes to lnb_part[tile] (fixed-order
+// sums: lanes, then the waves through LDS; ln_wgrad_finalize_kernel adds the rows up).  Every wave of
+// the workgroup calls this (one workgroup barrier for the cross-wave sum).
+template <int WM, int WN, int MI, int NI, int NW>
+__device__ __forceinline__ void tile_epilogue_lnbwd(const GemmArgs16& p, f32x4 (&acc)[MI][NI], char* smem, int mw,
+                                                    int tile, int lane, int w) {
+  constexpr int EPLD = WN + 4, CPR = WN / 8, RPP = 64 / CPR;
+  float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;
+  float* red = reinterpret_cast<float*>(smem) + NW * 16 * EPLD;  // [NW][2 WN]
+  const int c8 = lane % CPR, rg = lane / CPR, col0 = 8 * c8;
+  const bf16* X = (const bf16*)p.lnb_x;
+  const bf16* R = (const bf16*)p.R;
+  float gam[8], pg[8], pb[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    gam[e] = p.ln_gamma[col0 + e];
+    pg[e] = 0.f;
+    pb[e] = 0.f;
+  }
+  const float inv_n = 1.f / WN;
+  static_for<0, MI>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) ep[(4 * (lane >> 4) + r) * EPLD + j * 16 + (lane & 15)] = acc[i][j][r];
+    __builtin_amdgcn_wave_barrier();
+    for (int ps = 0; ps < 16 / RPP; ++ps) {
+      const int rl = rg + ps * RPP;
+      const int row = mw + i * 16 + rl;
+      const bool live = row < p.M;
+      const float4 lo = *(const float4*)&ep[rl * EPLD + col0];
+      const float4 hi = *(const float4*)&ep[rl * EPLD + col0 + 4];
+      const float a8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      float xv[8], rv[8], dy[8], xh[8], g[8];
+      float mu = 0.f, rs = 0.f;
+      if (live) {
+        ld8_bf16(X + (int64_t)row * p.lnb_ldx + col0, true, xv);
+        mu = p.ln_mean[row];
+        rs = p.ln_rstd[row];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) xv[e] = 0.f;
+      }
+      if (live && R) {
+        ld8_bf16(R + (int64_t)row * p.ldr + col0, true, rv);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) rv[e] = 0.f;
+      }
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dy[e] = live ? p.alpha * a8[e] : 0.f;  // rows past M hold clamped-operand garbage
+        xh[e] = live ? (xv[e] - mu) * rs : 0.f;
+        pg[e] += dy[e] * xh[e];
+        pb[e] += dy[e];
+        g[e] = dy[e] * gam[e];
+        s1 += g[e];
+        s2 += g[e] * xh[e];
+      }
+#pragma unroll
+      for (int o = CPR / 2; o > 0; o >>= 1) {
+        s1 += __shfl_xor(s1, o, 64);
+        s2 += __shfl_xor(s2, o, 64);
+      }
+      s1 *= inv_n;
+      s2 *= inv_n;
+      if (live && !(p.dbg & 1)) {
+        float o8[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o8[e] = rs * (g[e] - s1 - xh[e] * s2) + rv[e];
+        st8_bf16((bf16*)p.C + (int64_t)row * p.ldc + col0, true, o8, p.dbg & 8);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  });
+  if (p.lnb_part == nullptr) return;  // uniform: no weight gradient of the LayerNorm wanted
+  // the RPP row groups of the wave (lanes with equal c8), then the NW waves through LDS
+#pragma unroll
+  for (int o = 32; o >= CPR; o >>= 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      pg[e] += __shfl_xor(pg[e], o, 64);
+      pb[e] += __shfl_xor(pb[e], o, 64);
+    }
+  }
+  if (lane < CPR) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[w * 2 * WN + col0 + e] = pg[e];
+      red[w * 2 * WN + WN + col0 + e] = pb[e];
+    }
+  }
+  __syncthreads();
+  for (int c = w * 64 + lane; c < 2 * WN; c += NW * 64) {
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) s += red[k * 2 * WN + c];
+    p.lnb_part[(int64_t)tile * 2 * WN + c] = s;
+  }
+}
 
 // output-vector flags of the epilogue (host side)
 static void gemm_plan_vec(GemmArgs16& a, int batch) {

@@ -494,6 +494,18 @@ extern "C" int s2h_layernorm_fwd(int dt, int rows, int C, const void* x, int64_t
                        eps, (float*)y, ldy, mean, rstd, st);
 }
 
+// dgamma += sum_b part[b][0:C], dbeta += sum_b part[b][C:2C] (partial rows written by a fused
+// LayerNorm-backward epilogue, gemm.hip s2h_linear_dgrad_ln_bwd)
+extern "C" int s2h_ln_wgrad_finalize(int nb, int C, const float* part, float* dgamma, float* dbeta, hipStream_t st) {
+  if (nb <= 0) return 0;
+  if (C <= 0 || !part || !dgamma || !dbeta) return (int)hipErrorInvalidValue;
+  int ns = (nb + 31) / 32;
+  if (ns > 32) ns = 32;
+  hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64, ns), dim3(256), 0, st, nb, C, part, dgamma,
+                     dbeta);
+  return (int)hipGetLastError();
+}
+
 extern "C" int64_t s2h_layernorm_bwd_ws_bytes(int dt, int rows, int C) {
   if (rows <= 0 || C <= 0) return 0;
   const LnPlan p = dt == S2H_BF16 ? plan<bf16>(C, {}, {}) : plan<float>(C, {}, {});

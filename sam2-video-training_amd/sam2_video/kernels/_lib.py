@@ -32,6 +32,9 @@ SIGNATURES = {
     "s2h_linear_wgrad": [I, L, I, I, P, L, P, L, P, L, P, I, P],
     "s2h_linear_rope": [I, I, I, P, L, P, L, P, P, L, P, P, I, I, I, I, I, P],
     "s2h_linear_add_ln": [I, I, I, P, L, P, L, P, P, L, F, c_uint64, c_uint64, P, L, P, P, F, P, L, P, P, P],
+    "s2h_linear_dgrad_ln_bwd_ws_bytes": [I, I],
+    "s2h_linear_dgrad_ln_bwd": [I, I, I, P, L, P, L, F, P, L, P, P, P, P, L, P, L, P, P, P, P],
+    "s2h_ln_wgrad_finalize": [I, I, P, P, P, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],
@@ -126,7 +129,7 @@ _LIB = None
 # entry points that do not return a hipError_t
 RESTYPES = {"s2h_attn_fwd_ws_bytes": c_int64, "s2h_attn_bwd_ws_bytes": c_int64, "s2h_attn_keep_words": c_int64,
             "s2h_attn_fwd_vfold_ws_bytes": c_int64,
-            "s2h_layernorm_bwd_ws_bytes": c_int64}
+            "s2h_layernorm_bwd_ws_bytes": c_int64, "s2h_linear_dgrad_ln_bwd_ws_bytes": c_int64}
 
 
 class HipKernelError(RuntimeError):

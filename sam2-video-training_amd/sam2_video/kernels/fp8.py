@@ -131,11 +131,14 @@ def linear_rope(x, mod, w, bias, rope, out=None):
     return ops.linear_rope(x, w, bias, rope, out=out)
 
 
+def dgrad_on_mx8(dy, mod):
+    """linear_dgrad of `mod` runs on MX-fp8 operands"""
+    return dy.dtype != torch.float32 and DGRAD["on"] and _eligible(mod) and _pays(mod.out_features, mod.in_features)
+
+
 def linear_dgrad(dy, mod, **kw):
     """input-gradient GEMM of a Linear: MX-fp8 when `mod` is eligible (and it pays), else the bf16 kernel"""
-    wt8 = None
-    if dy.dtype != torch.float32 and DGRAD["on"] and _eligible(mod) and _pays(mod.out_features, mod.in_features):
-        wt8 = weight_t(mod)
+    wt8 = weight_t(mod) if dgrad_on_mx8(dy, mod) else None
     if wt8 is not None:
         return ops.linear_dgrad_mx8(dy, wt8, **kw)
     return ops.linear_dgrad(dy, mod.compute_weight(), **kw)

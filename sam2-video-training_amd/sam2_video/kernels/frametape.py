@@ -333,6 +333,11 @@ class FrameTape:
         owned = set()
         self.producer = {v: op for op in self.ops for v in op.outs}
         self.nuse = collections.Counter(v for op in self.ops for v in op.ins if v is not None)
+        self.first_use = {}  # value id -> index of the first op reading it
+        for op in self.ops:
+            for v in op.ins:
+                if v is not None and v not in self.first_use:
+                    self.first_use[v] = op.idx
         self.premasked = set()
         self.derotated = set()  # linear-with-RoPE outputs whose consumer returned the un-rotated gradient
         self.seeded = set(out_grads)
@@ -349,6 +354,7 @@ class FrameTape:
                 G[vid] = ops.add(G[vid], g)
                 owned.add(vid)
 
+        self.grads, self.acc = G, acc  # for ops whose backward finishes their producer's (_ln_dgrad_fused)
         for k in range(len(self.ops) - 1, -1, -1):
             op = self.ops[k]
             gys = [G.pop(v, None) for v in op.outs]
@@ -457,10 +463,49 @@ def _linear_bw(tape, op, gys):
             pp = prod.attrs["p"]
             dx = _fp8.linear_dgrad(dpre, mod, pre=x2, act="relu", alpha=1.0 / (1.0 - pp)).view(-1)
             tape.premasked.add(op.ins[0])
-        else:
+        elif not _ln_dgrad_fused(tape, op, prod, dpre, mod):
             dx = _fp8.linear_dgrad(dpre, mod).view(-1)
     dres = gy if op.needs[1] else None
     return [dx, dres]
+
+
+def ln_bwd_fuse_enabled():
+    """S2H_LN_BWD_FUSE=0 keeps the LayerNorm backward as its own launch after the consumer's dgrad"""
+    return os.environ.get("S2H_LN_BWD_FUSE", "1") != "0"
+
+
+def _ln_dgrad_fused(tape, op, prod, dpre, mod):
+    """The input of linear `op` is the output t of LayerNorm op `prod` and nothing else reads t
+    (memory attention: norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1): run the dgrad
+    with the LayerNorm backward in its epilogue (ops.linear_dgrad_ln_bwd) -- dL/dt stays in registers
+    -- and hand the LayerNorm's input gradients to its inputs here; `prod` is then left without
+    output gradients (t has none, its residual-stream output's was consumed), so the backward walk
+    skips it.  Needs the residual stream's gradient complete: every reader of it comes after `op`."""
+    if prod is None or prod.kind != "ln" or not ln_bwd_fuse_enabled():
+        return False
+    t = op.ins[0]
+    if prod.outs[0] != t or tape.nuse[t] != 1 or t in tape.seeded or _fp8.dgrad_on_mx8(dpre, mod):
+        return False
+    add = prod.attrs["add"]
+    if add and tape.first_use.get(prod.outs[1], len(tape.ops)) <= op.idx:
+        return False
+    lnmod = prod.attrs["mod"]
+    C = lnmod.weight.shape[0]
+    w = mod.compute_weight()
+    src = tape.st(prod.outs[1]) if add else tape.st(prod.ins[0])
+    x2 = _flat(src, C)
+    if w.shape[1] != C or not ops.linear_dgrad_ln_bwd_ok(dpre, w, x2):
+        return False
+    gxsum = tape.grads.pop(prod.outs[1], None) if add else None
+    dx = ops.linear_dgrad_ln_bwd(dpre, w, x2, lnmod.weight.detach(), tape.stores[("aux", prod.idx, "mean")].buf,
+                                 tape.stores[("aux", prod.idx, "rstd")].buf,
+                                 dres=gxsum.contiguous().view(-1, C) if gxsum is not None else None,
+                                 dgamma=_grad_of(lnmod.weight), dbeta=_grad_of(lnmod.bias)).view(-1)
+    if prod.needs[0]:
+        tape.acc(prod.ins[0], dx)
+    if add and prod.needs[1]:
+        tape.acc(prod.ins[1], dx)
+    return True
 
 
 def linear_add_ln(tape: FrameTape, inp, mod, x, norm, eps, drop_p):

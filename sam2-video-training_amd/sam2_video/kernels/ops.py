@@ -166,6 +166,40 @@ def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0
     return dx
 
 
+def linear_dgrad_ln_bwd_ok(dy, w, x):
+    """s2h_linear_dgrad_ln_bwd applies: bf16, LayerNorm width 128 / 256, 16-B aligned rows"""
+    K = w.shape[1]
+    return (dy.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and K in (128, 256)
+            and w.is_contiguous() and dy.shape[-1] % 8 == 0 and dy.stride(-1) == 1 and x.is_contiguous()
+            and all(t.data_ptr() % 16 == 0 for t in (dy, w, x)))
+
+
+def linear_dgrad_ln_bwd(dy, w, x, gamma, mean, rstd, dres=None, dgamma=None, dbeta=None, alpha=1.0, dx=None):
+    """dx = LN'(alpha * dy @ w) + dres for a LayerNorm (input x, gamma, saved mean / rstd) whose output
+    feeds only the Linear with weight w; dgamma / dbeta += its weight gradients -- one full-row GEMM
+    launch with the LayerNorm backward in the epilogue (+ the partial-row finalize)"""
+    dy2 = dy.reshape(-1, dy.shape[-1])
+    M, N = dy2.shape
+    C = w.shape[1]
+    x2 = x.reshape(-1, C)
+    assert x2.shape[0] == M and w.shape[0] == N and mean.numel() >= M and rstd.numel() >= M
+    if dx is None:
+        dx = torch.empty(x.shape, device=dy.device, dtype=dy.dtype)
+    d2 = dx.view(-1, C)
+    r2 = dres.reshape(-1, C) if dres is not None else None
+    if r2 is not None:
+        assert r2.stride(1) == 1 and r2.dtype == dx.dtype
+    part = None
+    if dgamma is not None:
+        nbytes = lib().s2h_linear_dgrad_ln_bwd_ws_bytes(M, C)
+        part = torch.empty(max(nbytes // 4, 1), device=dy.device, dtype=torch.float32)
+    _dev(dy2, w, x2, gamma, mean, rstd, r2, d2, dgamma, dbeta)
+    call("s2h_linear_dgrad_ln_bwd", M, C, N, ptr(dy2), dy2.stride(0), ptr(w), w.stride(0), float(alpha), ptr(x2), C,
+         ptr(gamma), ptr(mean), ptr(rstd), ptr(r2), r2.stride(0) if r2 is not None else 0, ptr(d2), C, ptr(part),
+         ptr(dgamma), ptr(dbeta), stream())
+    return dx
+
+
 def linear_wgrad(dy, x, dw, accumulate=True, db=None):
     """dw (fp32 [N, K]) (+)= dy^T @ x;  db (fp32 [N], optional) (+)= dy summed over rows."""
     dy2 = dy.reshape(-1, dy.shape[-1])

@@ -169,3 +169,43 @@ def test_keep_bitmap_backward_equals_rehash():
     torch.cuda.synchronize()
     for a, b in zip(*outs):
         assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
+
+
+def test_ln_bwd_fused_equals_unfused(monkeypatch):
+    """the memory attention's LayerNorm backward fused into the dgrad of its output's only reader
+    (frametape._ln_dgrad_fused: norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1) against
+    the separate dgrad + LayerNorm-backward launches (S2H_LN_BWD_FUSE=0), bf16 B+ 256^2: the same
+    forward bits, gradients within the one bf16 rounding of dL/dt the fused path skips"""
+    from sam2_video.kernels import ops
+    calls = []
+    orig = ops.linear_dgrad_ln_bwd
+
+    def counted(*a, **k):
+        calls.append(1)
+        return orig(*a, **k)
+    monkeypatch.setattr(ops, "linear_dgrad_ln_bwd", counted)
+    g = load_golden("bplus256_point_all")
+    size, prompt, trainable = CASES["bplus256_point_all"]
+    out = []
+    for fuse in ("0", "1"):
+        monkeypatch.setenv("S2H_LN_BWD_FUSE", fuse)
+        m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype="bf16", seed=int(g["meta/seed"]))
+        m.frame_batched = True
+        stages, merged, losses, _ = run_step(m, golden_batch(g).to("cuda"))
+        out.append(([s["pred_masks"].detach().float().cpu() for s in stages], grads_by_name(m)))
+        del m
+        if fuse == "0":
+            assert not calls
+    assert calls, "the fused LayerNorm backward never ran"
+    (la, ga), (lb, gb) = out
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b)
+    num = sum(float((gb[n].double() - ga[n].double()).norm() ** 2) for n in ga)
+    den = sum(float(ga[n].double().norm() ** 2) for n in ga)
+    rel = math.sqrt(num / den)
+    print(f"fused LayerNorm backward: {len(calls)} launches, global relative gradient difference {rel:.3e}")
+    assert rel <= 1e-2, rel
+    for n in ga:
+        if n.startswith("memory_attention.") and ".norm" in n:
+            r = float((gb[n].double() - ga[n].double()).norm() / (ga[n].double().norm() + 1e-12))
+            assert r <= 2e-2, (n, r)

@@ -1007,3 +1007,47 @@ def test_linear_add_ln_matches_unfused(M, N, K, p_drop, res):
     # and against fp32 torch (LayerNorm of the bf16 residual stream)
     t = torch.nn.functional.layer_norm(ref_x.float(), (N,), g, be, 1e-5)
     _close(y, t, 8e-3)
+
+
+@pytest.mark.parametrize("M,C,K", [(13312, 256, 768), (13312, 256, 256), (93184, 256, 2048), (1000, 256, 200),
+                                   (13312, 128, 256), (333, 128, 64)])
+@pytest.mark.parametrize("res,wgrad", [(True, True), (False, True), (True, False)])
+def test_linear_dgrad_ln_bwd_matches_unfused(M, C, K, res, wgrad):
+    """s2h_linear_dgrad_ln_bwd (a Linear's input gradient with the backward of the LayerNorm that
+    produced its input in the GEMM epilogue) against the unfused pair ops.linear_dgrad ->
+    ops.layernorm_bwd and against fp32 torch autograd of layer_norm -> linear: the fused path keeps
+    dL/dt in fp32 (the unfused one rounds it to bf16 once), so dx agrees within bf16 rounding and the
+    LayerNorm weight gradients within fp32 summation order"""
+    ops = _ops()
+    torch.manual_seed(11)
+    bf = torch.bfloat16
+    x = (torch.randn(M, C, device=DEV) * 2 + 0.3).to(bf)
+    g = torch.rand(C, device=DEV) + 0.5
+    be = torch.randn(C, device=DEV) * 0.1
+    w = (torch.randn(K, C, device=DEV) / C ** 0.5).to(bf)  # the consumer Linear: C -> K
+    dy = torch.randn(M, K, device=DEV).to(bf)
+    dres = torch.randn(M, C, device=DEV).to(bf) if res else None
+    _, mean, rstd = ops.layernorm_fwd(x, g, be, 1e-5)
+    dg = torch.zeros(C, device=DEV) if wgrad else None
+    db = torch.zeros(C, device=DEV) if wgrad else None
+    dx = ops.linear_dgrad_ln_bwd(dy, w, x, g, mean, rstd, dres=dres, dgamma=dg, dbeta=db)
+    # unfused twin
+    dt = ops.linear_dgrad(dy, w)
+    dg2 = torch.zeros(C, device=DEV) if wgrad else None
+    db2 = torch.zeros(C, device=DEV) if wgrad else None
+    dx2 = ops.layernorm_bwd(x, dt, g, mean, rstd, dgamma=dg2, dbeta=db2,
+                            dres=dres.contiguous() if dres is not None else None)
+    _close(dx, dx2, 1.5e-2)
+    # fp32 torch reference of the same composition
+    xr = x.float().requires_grad_(True)
+    gr = g.clone().requires_grad_(True)
+    br = be.clone().requires_grad_(True)
+    t = torch.nn.functional.layer_norm(xr, (C,), gr, br, 1e-5)
+    (t @ w.float().t()).backward(dy.float())
+    ref = xr.grad + (dres.float() if dres is not None else 0)
+    _close(dx, ref, 1e-2)
+    if wgrad:
+        _close(dg, gr.grad, 2e-3)
+        _close(db, br.grad, 2e-3)
+        _close(dg, dg2, 1e-2)
+        _close(db, db2, 1e-2)
