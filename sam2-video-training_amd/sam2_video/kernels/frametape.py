@@ -355,6 +355,7 @@ class FrameTape:
                 owned.add(vid)
 
         self.grads, self.acc = G, acc  # for ops whose backward finishes their producer's (_ln_dgrad_fused)
+        self.side = ops.SideWork()  # the Linear weight gradients' stream (joined before returning)
         for k in range(len(self.ops) - 1, -1, -1):
             op = self.ops[k]
             gys = [G.pop(v, None) for v in op.outs]
@@ -364,6 +365,8 @@ class FrameTape:
             for v, need, g in zip(op.ins, op.needs, gins):
                 if need:
                     acc(v, g)
+        self.side.join()
+        self.grads = self.acc = None
         return {name: G.get(vid) for name, vid in self.inputs.items()}
 
     def out_vid(self, t):
@@ -448,12 +451,13 @@ def _linear_bw(tape, op, gys):
     x2 = _flat(tape.st(op.ins[0]), K)
     wgrad = getattr(mod, "wgrad", None)
     gw, gb = mod.grad_views()
-    if wgrad is not None:  # a derived weight (functional.VFoldProj) scatters its own gradient
-        wgrad(dpre, x2)
-    elif gw is not None:
-        ops.linear_wgrad(dpre, x2, gw.view(gw.shape[0], -1), db=gb)
-    elif gb is not None:
-        ops.colsum(dpre, gb)
+    with tape.side.run(dpre, x2):  # on the side stream: nothing below reads these gradients
+        if wgrad is not None:  # a derived weight (functional.VFoldProj) scatters its own gradient
+            wgrad(dpre, x2)
+        elif gw is not None:
+            ops.linear_wgrad(dpre, x2, gw.view(gw.shape[0], -1), db=gb)
+        elif gb is not None:
+            ops.colsum(dpre, gb)
     dx = None
     if op.needs[0]:
         prod = tape.producer.get(op.ins[0])

@@ -6,7 +6,9 @@ mode); norms' gamma/beta, biases, LSE/statistics and weight gradients are fp32.
 """
 from __future__ import annotations
 
+import contextlib
 import math
+import os
 
 import torch
 
@@ -30,6 +32,49 @@ def ptr(t):
 
 def stream():
     return torch.cuda.current_stream().cuda_stream
+
+
+_SIDE = {"on": os.environ.get("S2H_WGRAD_STREAM", "1") != "0", "streams": {}}
+
+
+class SideWork:
+    """Weight-gradient launches of one frame-tape backward on a second HIP stream, beside the
+    input-gradient chain on the current one: a Linear's dW = dY^T X does not feed the next
+    dgrad, so the two streams fill each other's ramp-up and tail (the step's GEMMs are short-K
+    and latency-bound).  run(*reads) forks the side stream off the current one (an event) and
+    keeps the tensors it reads alive; join() makes the current stream wait for everything
+    forked and releases them -- the tape calls it before its gradients leave the backward, so
+    nothing outside ever sees the second stream.  Graph capture records the fork / join as
+    branches of the captured graph.  S2H_WGRAD_STREAM=0: one stream (A/B)."""
+
+    def __init__(self):
+        self.cur = self.ws = None
+        if _SIDE["on"] and torch.cuda.is_available():
+            self.cur = torch.cuda.current_stream()
+            dev = self.cur.device
+            ws = _SIDE["streams"].get(dev)
+            if ws is None:
+                ws = _SIDE["streams"][dev] = torch.cuda.Stream(dev)
+            self.ws = ws
+        self.refs = []
+        self.used = False
+
+    @contextlib.contextmanager
+    def run(self, *reads):
+        if self.ws is None:
+            yield
+            return
+        self.ws.wait_stream(self.cur)
+        with torch.cuda.stream(self.ws):
+            yield
+        self.refs.extend(t for t in reads if t is not None)
+        self.used = True
+
+    def join(self):
+        if self.used:
+            self.cur.wait_stream(self.ws)
+        self.refs.clear()
+        self.used = False
 
 
 def _dev(*ts):

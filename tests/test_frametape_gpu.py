@@ -209,3 +209,28 @@ def test_ln_bwd_fused_equals_unfused(monkeypatch):
         if n.startswith("memory_attention.") and ".norm" in n:
             r = float((gb[n].double() - ga[n].double()).norm() / (ga[n].double().norm() + 1e-12))
             assert r <= 2e-2, (n, r)
+
+
+def test_wgrad_side_stream_equals_one_stream(monkeypatch):
+    """the frame tapes' Linear weight gradients on a second stream (ops.SideWork) against one stream
+    (S2H_WGRAD_STREAM=0): the same kernels on the same operands, so gradients agree up to the
+    split-K atomics' summation order and the forward to the bit -- a missing fork / join or a
+    buffer released to the allocator while the side stream still reads it would show here"""
+    from sam2_video.kernels import ops
+    g = load_golden("bplus256_point_all")
+    size, prompt, trainable = CASES["bplus256_point_all"]
+    out = []
+    for on in (False, True):
+        monkeypatch.setitem(ops._SIDE, "on", on)
+        m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype="bf16", seed=int(g["meta/seed"]))
+        m.frame_batched = True
+        stages, merged, losses, _ = run_step(m, golden_batch(g).to("cuda"))
+        torch.cuda.synchronize()
+        out.append(([s["pred_masks"].detach().float().cpu() for s in stages], grads_by_name(m)))
+        del m
+    (la, ga), (lb, gb) = out
+    for a, b in zip(la, lb):
+        assert torch.equal(a, b)
+    worst = max(float((gb[n].double() - ga[n].double()).norm() / (ga[n].double().norm() + 1e-20)) for n in ga)
+    print("side-stream weight gradients: worst per-parameter relative difference", worst)
+    assert worst <= 1e-4, worst
