@@ -231,6 +231,7 @@ def test_wgrad_side_stream_equals_one_stream(monkeypatch):
     (la, ga), (lb, gb) = out
     for a, b in zip(la, lb):
         assert torch.equal(a, b)
-    worst = max(float((gb[n].double() - ga[n].double()).norm() / (ga[n].double().norm() + 1e-20)) for n in ga)
-    print("side-stream weight gradients: worst per-parameter relative difference", worst)
-    assert worst <= 1e-4, worst
+    gmax = max(float(t.abs().max()) for t in ga.values())
+    bad = [(n, float((gb[n] - ga[n]).abs().max())) for n in ga
+           if float((gb[n].double() - ga[n].double()).abs().max()) > 1e-4 * float(ga[n].abs().max()) + 1e-6 * gmax]
+    assert not bad, bad[:8]
