@@ -171,24 +171,27 @@ def test_keep_bitmap_backward_equals_rehash():
         assert torch.equal(a, b), (a.float() - b.float()).abs().max().item()
 
 
-def test_ln_bwd_fused_equals_unfused(monkeypatch):
-    """the memory attention's LayerNorm backward fused into the dgrad of its output's only reader
-    (frametape._ln_dgrad_fused: norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1) against
-    the separate dgrad + LayerNorm-backward launches (S2H_LN_BWD_FUSE=0), bf16 B+ 256^2: the same
-    forward bits, gradients within the one bf16 rounding of dL/dt the fused path skips"""
+@pytest.mark.parametrize("knob,fn", [("S2H_LN_BWD_FUSE", "linear_dgrad_ln_bwd"), ("S2H_LINEAR_LN", "linear_add_ln")])
+def test_ln_fusions_equal_unfused(monkeypatch, knob, fn):
+    """the opt-in LayerNorm fusions of the memory attention against the separate launches, bf16 B+
+    256^2: S2H_LN_BWD_FUSE=1 -- the LayerNorm backward in the dgrad of its output's only reader
+    (frametape._ln_dgrad_fused: norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1; same
+    forward bits, gradients within the one bf16 rounding of dL/dt it skips); S2H_LINEAR_LN=1 -- the
+    projection + residual add + LayerNorm in one full-row launch (s2h_linear_add_ln; the LayerNorm
+    statistics in another summation order: forward and gradients within bf16 rounding)"""
     from sam2_video.kernels import ops
     calls = []
-    orig = ops.linear_dgrad_ln_bwd
+    orig = getattr(ops, fn)
 
     def counted(*a, **k):
         calls.append(1)
         return orig(*a, **k)
-    monkeypatch.setattr(ops, "linear_dgrad_ln_bwd", counted)
+    monkeypatch.setattr(ops, fn, counted)
     g = load_golden("bplus256_point_all")
     size, prompt, trainable = CASES["bplus256_point_all"]
     out = []
     for fuse in ("0", "1"):
-        monkeypatch.setenv("S2H_LN_BWD_FUSE", fuse)
+        monkeypatch.setenv(knob, fuse)
         m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype="bf16", seed=int(g["meta/seed"]))
         m.frame_batched = True
         stages, merged, losses, _ = run_step(m, golden_batch(g).to("cuda"))
@@ -196,19 +199,22 @@ def test_ln_bwd_fused_equals_unfused(monkeypatch):
         del m
         if fuse == "0":
             assert not calls
-    assert calls, "the fused LayerNorm backward never ran"
+    assert calls, f"{fn} never ran"
     (la, ga), (lb, gb) = out
     for a, b in zip(la, lb):
-        assert torch.equal(a, b)
+        if knob == "S2H_LN_BWD_FUSE":
+            assert torch.equal(a, b)
+        else:
+            assert float((a - b).abs().max()) <= 3e-2 * float(a.abs().max()) + 1e-3
     num = sum(float((gb[n].double() - ga[n].double()).norm() ** 2) for n in ga)
     den = sum(float(ga[n].double().norm() ** 2) for n in ga)
     rel = math.sqrt(num / den)
-    print(f"fused LayerNorm backward: {len(calls)} launches, global relative gradient difference {rel:.3e}")
-    assert rel <= 1e-2, rel
+    print(f"{knob}=1: {len(calls)} {fn} launches, global relative gradient difference {rel:.3e}")
+    assert rel <= 2e-2, rel
     for n in ga:
         if n.startswith("memory_attention.") and ".norm" in n:
             r = float((gb[n].double() - ga[n].double()).norm() / (ga[n].double().norm() + 1e-12))
-            assert r <= 2e-2, (n, r)
+            assert r <= 5e-2, (n, r)
 
 
 def test_wgrad_side_stream_equals_one_stream(monkeypatch):
