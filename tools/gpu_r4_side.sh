@@ -2,7 +2,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_frametape_gpu.py tests/test_determinism_gpu.py tests/test_graph_gpu.py -v -s -x --timeout 150 --timeout-method thread > gpurun_out/r4_side_tests.log 2>&1 || { tail -40 gpurun_out/r4_side_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_frametape_gpu.py tests/test_determinism_gpu.py tests/test_graph_gpu.py -v -s -x -k "not S2H_LINEAR_LN" --timeout 150 --timeout-method thread > gpurun_out/r4_side_tests.log 2>&1 || { tail -40 gpurun_out/r4_side_tests.log; exit 1; }
 tail -2 gpurun_out/r4_side_tests.log
 grep -h "launches, global\|worst" gpurun_out/r4_side_tests.log || true
 for r in 1 2; do
