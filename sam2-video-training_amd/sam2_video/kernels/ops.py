@@ -34,7 +34,7 @@ def stream():
     return torch.cuda.current_stream().cuda_stream
 
 
-_SIDE = {"on": os.environ.get("S2H_WGRAD_STREAM", "1") != "0", "streams": {}}
+_SIDE = {"on": os.environ.get("S2H_WGRAD_STREAM", "0") == "1", "streams": {}}
 
 
 class SideWork:
@@ -45,7 +45,10 @@ class SideWork:
     keeps the tensors it reads alive; join() makes the current stream wait for everything
     forked and releases them -- the tape calls it before its gradients leave the backward, so
     nothing outside ever sees the second stream.  Graph capture records the fork / join as
-    branches of the captured graph.  S2H_WGRAD_STREAM=0: one stream (A/B)."""
+    branches of the captured graph.  Opt-in (S2H_WGRAD_STREAM=1): on MI355X the second stream costs
+    2.5 % of the config-5 step (59.5 vs 58.0 ms, profiles/r04_v4_wgrad_stream_ab.log) -- the weight
+    gradients take CUs from the critical dgrad / attention-backward chain rather than filling idle
+    ones (round 2 measured -4 % for the autograd form)."""
 
     def __init__(self):
         self.cur = self.ws = None

@@ -221,8 +221,8 @@ def test_ln_fusions_equal_unfused(monkeypatch, knob, fn):
 
 
 def test_wgrad_side_stream_equals_one_stream(monkeypatch):
-    """the frame tapes' Linear weight gradients on a second stream (ops.SideWork) against one stream
-    (S2H_WGRAD_STREAM=0): the same kernels on the same operands, so gradients agree up to the
+    """the frame tapes' Linear weight gradients on a second stream (ops.SideWork, opt-in
+    S2H_WGRAD_STREAM=1) against one stream: the same kernels on the same operands, so gradients agree up to the
     split-K atomics' summation order and the forward to the bit -- a missing fork / join or a
     buffer released to the allocator while the side stream still reads it would show here"""
     from sam2_video.kernels import ops
