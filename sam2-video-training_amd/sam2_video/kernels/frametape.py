@@ -476,7 +476,7 @@ def _linear_bw(tape, op, gys):
 def ln_bwd_fuse_enabled():
     """S2H_LN_BWD_FUSE=1 fuses the LayerNorm backward into its consumer's dgrad (full-row tile).  Off
     by default for the same reason as functional.linear_ln_enabled: the full-row dgrad is slower than
-    the 64-row-tile dgrad + the LayerNorm backward launch (config 5: 60.5 vs 59.6 ms per step,
+    the 64-row-tile dgrad + the LayerNorm backward launch (bench step: 60.5 vs 59.6 ms per step,
     profiles/r04_v3_ln_fusion_ab.log)"""
     return os.environ.get("S2H_LN_BWD_FUSE", "0") == "1"
 

@@ -206,7 +206,7 @@ def linear_ln_enabled():
     """S2H_LINEAR_LN=1 runs a projection + the residual add + LayerNorm after it as ONE full-row GEMM
     launch.  Off by default: on MI355X the 64 x 256 full-row tile (160 KB of LDS, one workgroup per
     CU, the whole weight re-read per 64 rows) is slower than the 64 x 64 tile plus a LayerNorm launch
-    (profiles/r04_v3_fullrow_tiles.log; config-5 step 57.8 ms unfused vs 59.6 ms fused,
+    (profiles/r04_v3_fullrow_tiles.log; bench step 57.8 ms unfused vs 59.6 ms fused,
     profiles/r04_v3_ln_fusion_ab.log)"""
     import os
     return os.environ.get("S2H_LINEAR_LN", "0") == "1"

@@ -46,7 +46,7 @@ class SideWork:
     forked and releases them -- the tape calls it before its gradients leave the backward, so
     nothing outside ever sees the second stream.  Graph capture records the fork / join as
     branches of the captured graph.  Opt-in (S2H_WGRAD_STREAM=1): on MI355X the second stream costs
-    2.5 % of the config-5 step (59.5 vs 58.0 ms, profiles/r04_v4_wgrad_stream_ab.log) -- the weight
+    2.5 % of the bench step (59.5 vs 58.0 ms, profiles/r04_v4_wgrad_stream_ab.log) -- the weight
     gradients take CUs from the critical dgrad / attention-backward chain rather than filling idle
     ones (round 2 measured -4 % for the autograd form)."""
 
