@@ -283,11 +283,17 @@ class SAM2Model(SAM2Base):
             raise RuntimeError("call SAM2Model.load(device) before forward")
         if self.fp8:
             fp8.new_step()  # weights moved since the last forward: re-quantise on first use
-        backbone_out = self.forward_image(input.flat_img_batch)
-        # the backbone outputs the tracking loop reads: the split point of a two-phase backward
-        # (StepRunner overlaps the gradient all-reduce of everything after them with the image
-        # encoder's backward)
-        self.last_backbone_outputs = [t for t in backbone_out["backbone_fpn"] if t.requires_grad]
+        if self.training or not self.forward_backbone_per_frame_for_eval:
+            backbone_out = self.forward_image(input.flat_img_batch)
+            # the backbone outputs the tracking loop reads: the split point of a two-phase backward
+            # (StepRunner overlaps the gradient all-reduce of everything after them with the image
+            # encoder's backward)
+            self.last_backbone_outputs = [t for t in backbone_out["backbone_fpn"] if t.requires_grad]
+        else:
+            # evaluation with forward_backbone_per_frame_for_eval (sam2model.py:164-169): each frame's
+            # image features are computed when the tracking loop reaches it (forward_tracking)
+            backbone_out = {"backbone_fpn": None, "vision_pos_enc": None}
+            self.last_backbone_outputs = []
         backbone_out = self.prepare_prompt_inputs(backbone_out, input)
         stages = self.forward_tracking(backbone_out, input)
         out = merge_object_results_to_category(stages, backbone_out["obj_to_cat"], backbone_out["num_categories"])
@@ -377,9 +383,21 @@ class SAM2Model(SAM2Base):
         fpn = backbone_out["backbone_fpn"]
         T = backbone_out["num_frames"]
         h = w = self.sam_image_embedding_size
-        feats = fpn[-1].reshape(T, h * w, -1)
-        pos = backbone_out["vision_pos_enc"][-1]
-        s0, s1 = fpn[0], fpn[1]
+        if fpn is not None:
+            feats = fpn[-1].reshape(T, h * w, -1)
+            pos = backbone_out["vision_pos_enc"][-1]
+            s0, s1 = fpn[0], fpn[1]
+        else:  # per-frame backbone for evaluation (forward): frame t's features computed at frame t
+            feats = s0 = s1 = pos = None
+            imgs = input.flat_img_batch
+
+        def frame_features(t):
+            """(image embedding [h*w, C], its position table, high-res levels 0 / 1 of frame t)"""
+            if fpn is not None:
+                return feats[t], pos, s0[t:t + 1], s1[t:t + 1]
+            out = self.forward_image(imgs[t:t + 1])
+            f = out["backbone_fpn"]
+            return f[-1].reshape(h * w, -1), out["vision_pos_enc"][-1], f[0], f[1]
         O = len(backbone_out["obj_to_cat"])
         output_dict = {"cond_frame_outputs": {}, "non_cond_frame_outputs": {}}
         frames = []
@@ -397,19 +415,18 @@ class SAM2Model(SAM2Base):
             tracker = FrameTracker(self, T, O, feats, s0, s1, mask_cond is not None, pshape)
         for t in range(T):
             is_cond = t == 0
-            feat_t = feats[t]
+            feat_t, pos, s0_t, s1_t = frame_features(t)
             if is_cond and mask_cond is not None:
                 low, high, ious, ptr, score = self._use_mask_as_output(feat_t, mask_cond[0], mask_cond[1],
-                                                                       (s0[t:t + 1], s1[t:t + 1]), O)
+                                                                       (s0_t, s1_t), O)
             elif tracker is not None:
                 prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
                 pix = tracker.memory_conditioned(t, feat_t.detach(), pos, output_dict)
-                low, high, ious, ptr, score = tracker.sam_heads(t, pix, prompt, s0[t:t + 1].detach(),
-                                                                s1[t:t + 1].detach())
+                low, high, ious, ptr, score = tracker.sam_heads(t, pix, prompt, s0_t.detach(), s1_t.detach())
             else:
                 pix = self._prepare_memory_conditioned_features(t, is_cond, feat_t, pos, T, output_dict, O)
                 prompt = backbone_out["prompt_cond"] if is_cond else backbone_out["prompt_pad"]
-                low, high, ious, ptr, score = self._forward_sam_heads(pix, prompt, (s0[t:t + 1], s1[t:t + 1]), O)
+                low, high, ious, ptr, score = self._forward_sam_heads(pix, prompt, (s0_t, s1_t), O)
             mfeat, mpos = self._encode_new_memory(feat_t, high, score, O)
             entry = {"maskmem_features": mfeat, "maskmem_pos_enc": mpos, "obj_ptr": ptr}
             if is_cond:

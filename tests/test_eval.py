@@ -128,3 +128,25 @@ def test_clip_evaluation_matches_oracle_fp32():
             a, b = got["cat_scores"][c][k], ref["cat_scores"][c][k]
             assert (np.isnan(a) and np.isnan(b)) or abs(a - b) <= 1e-4, (c, k, a, b)
     assert abs(got["avg_scores"]["iou"] - ref["avg_scores"]["iou"]) <= 1e-4
+
+
+@pytest.mark.gpu
+def test_per_frame_backbone_for_eval_matches_batched():
+    """forward_backbone_per_frame_for_eval (reference sam2model.py:164-169): in evaluation the image
+    features of frame t are computed when the loop reaches frame t instead of for the whole clip up
+    front -- the same per-frame masks (fp32 parity mode: the GEMM / attention results do not depend
+    on how many frames share a launch)"""
+    from step_harness import ALL, build_model
+    from sam2_video.data.synthetic import make_clip, sam2_collate_fn
+
+    clip = make_clip(7, 3, 128, 4, 3)
+    model = build_model("tiny", 128, ALL, "point", dtype="fp32")
+    model.eval()
+    outs = []
+    for flag in (False, True):
+        model.forward_backbone_per_frame_for_eval = flag
+        with torch.no_grad():
+            merged, _ = model(sam2_collate_fn([clip]).to("cuda"))
+        outs.append([m["pred_masks_high_res"].float().cpu() for m in merged])
+    for a, b in zip(*outs):
+        assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(a.abs().max())), float((a - b).abs().max())
