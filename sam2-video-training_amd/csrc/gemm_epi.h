@@ -384,17 +384,21 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
           if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + cc]);
         }
       }
-    } else if (WN % 32 == 0 && p.ln_gamma != nullptr) {
-      // LayerNorm of whole rows (s2h_linear_add_ln checked: N == WN, one wave per 16 full rows)
-      constexpr int CPR = WN / 8, RPP = 64 / CPR;
-      const int c8 = lane % CPR, rg = lane / CPR;
-      for (int ps = 0; ps < 16 / RPP; ++ps) {
-        const int rl = rg + ps * RPP;
-        const float4 lo = *(const float4*)&ep[rl * EPLD + 8 * c8];
-        const float4 hi = *(const float4*)&ep[rl * EPLD + 8 * c8 + 4];
-        const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-        const int row = mw + i * 16 + rl;
-        epilogue8_ln<CPR>(p, bz, row, nw + 8 * c8, v8, bcol8, row < p.M && !(p.dbg & 1));
+    } else if (WN >= 128 && WN % 32 == 0 && p.ln_gamma != nullptr) {
+      // LayerNorm of whole rows (s2h_linear_add_ln checked: N == WN, one wave per 16 full rows).
+      // Instantiated for the full-row tiles only: compiled into every tiling, the extra epilogue
+      // raised the 64x64 tile's VGPRs 63 -> 81 and cost 1.5 % of the step with the fusion unused
+      if constexpr (WN >= 128 && WN % 32 == 0) {
+        constexpr int CPR = WN / 8, RPP = 64 / CPR;
+        const int c8 = lane % CPR, rg = lane / CPR;
+        for (int ps = 0; ps < 16 / RPP; ++ps) {
+          const int rl = rg + ps * RPP;
+          const float4 lo = *(const float4*)&ep[rl * EPLD + 8 * c8];
+          const float4 hi = *(const float4*)&ep[rl * EPLD + 8 * c8 + 4];
+          const float v8[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          const int row = mw + i * 16 + rl;
+          epilogue8_ln<CPR>(p, bz, row, nw + 8 * c8, v8, bcol8, row < p.M && !(p.dbg & 1));
+        }
       }
     } else if (WN % 32 == 0 && (p.vec8 & 1) && nw + WN <= p.N) {
       // 8 columns per lane, one 16-B store each (the wave's column block is entirely valid)
