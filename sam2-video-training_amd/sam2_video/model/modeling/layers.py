@@ -145,7 +145,8 @@ class MLP(nn.Module):
         for i, layer in enumerate(self.layers):
             last = i == self.num_layers - 1
             if last:
-                if norm is not None and residual is not None and not self.sigmoid_output:
+                if norm is not None and residual is not None and not self.sigmoid_output and \
+                        FN._linear_ln_ok(x, layer, norm):
                     return FN.linear_add_layer_norm(x, layer, residual, norm, norm.eps)[0]
                 x = layer(x, act="sigmoid" if self.sigmoid_output else None, residual=residual)
             else:
