@@ -26,6 +26,10 @@ struct GemmArgs16 {
   // tables' column (c % rope_dh) / 2.  rope_cos == nullptr: no rotation.
   const float* rope_cos; const float* rope_sin;
   int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
+  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
+  // --- read only by the LayerNorm epilogues, so they sit behind every field the plain GEMM reads: each
+  // workgroup loads the argument block's leading cache lines (inserted before `dbg` these fields cost
+  // the 64x64 tilings 3 % in the step)
   // optional LayerNorm of the finished output rows (round 4, s2h_linear_add_ln): the tile spans the
   // whole output width (N <= 256, one wave per 16 full rows); C receives x' = R + drop(A W^T + b)
   // (bf16, the residual stream), ln_y = LN(x') with gamma / beta / eps, ln_mean / ln_rstd per row --
@@ -38,7 +42,6 @@ struct GemmArgs16 {
   // R the residual-stream gradient added to dx (may be null); C receives dx; lnb_part (may be null)
   // one (sum dy * xhat, sum dy) row of 2N floats per 64-row tile for ln_wgrad_finalize_kernel
   const void* lnb_x; int64_t lnb_ldx; float* lnb_part;
-  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
 };
 
 int s2h_gemm_bf16(const GemmArgs16& a, int batch, hipStream_t st);

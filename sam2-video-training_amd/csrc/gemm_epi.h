@@ -374,14 +374,21 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
       // split-K: consecutive lanes on consecutive columns (256 B per instruction): RPI rows of
       // WN <= 64 columns, or 64-column pieces of one row for the full-row tiles (WN 128 / 256)
       float* C = (float*)p.C + (int64_t)bz * p.sC;
-      constexpr int CPI = WN < 64 ? WN : 64;  // columns per instruction
-      constexpr int RPI = 64 / CPI;           // rows per instruction
-      for (int rr = lane / CPI; rr < 16; rr += RPI) {
-        const int row = mw + i * 16 + rr;
+      if constexpr (WN <= 64) {
+        constexpr int RPI = 64 / WN;  // rows per instruction
+        const int col = nw + lane % WN;
+        for (int rr = lane / WN; rr < 16; rr += RPI) {
+          const int row = mw + i * 16 + rr;
+          if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
+        }
+      } else {
+        for (int rr = 0; rr < 16; ++rr) {
+          const int row = mw + i * 16 + rr;
 #pragma unroll
-        for (int cc = lane % CPI; cc < WN; cc += CPI) {
-          const int col = nw + cc;
-          if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + cc]);
+          for (int cc = lane; cc < WN; cc += 64) {
+            const int col = nw + cc;
+            if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + cc]);
+          }
         }
       }
     } else if (WN >= 128 && WN % 32 == 0 && p.ln_gamma != nullptr) {
