@@ -274,7 +274,6 @@ extern "C" int s2h_linear_rope(int M, int N, int K, const void* A, int64_t lda, 
 // with mean / rstd per row -- a Linear followed by the residual add + LayerNorm that reads it
 // (memory_attention.py:60-98 out_proj / cross-attention output / linear2 -> norm2 / norm3 / the
 // next layer's norm1).  Full-row tiles (64 rows x N, N = 128 or 256, gemm_cfg6.hip).
-int gemm_cfg_launch_6(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 extern "C" int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda, const void* W, int64_t ldw,
                                  const float* bias, const void* R, int64_t ldr, float drop_p, uint64_t seed,
                                  uint64_t drop_idx0, void* C, int64_t ldc, const float* gamma, const float* beta,
@@ -286,7 +285,7 @@ extern "C" int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda
       (int64_t)N * ldw >= (1ll << 31))
     return (int)hipErrorInvalidValue;
   const int slot = s2h_prof_begin(stream, 4, 1, M, N, K, 2 + 1 + 4);
-  GemmArgs16 b = {};
+  GemmArgs16Ln b = {};
   b.M = M; b.N = N; b.K = K;
   b.A = (const bf16*)A; b.lda_m = lda; b.lda_k = 1;
   b.B = (const bf16*)W; b.ldb_k = 1; b.ldb_n = ldw;
@@ -298,7 +297,7 @@ extern "C" int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda
   b.vecA = 1; b.vecB = 1;
   b.ln_gamma = gamma; b.ln_beta = beta; b.ln_eps = eps; b.ln_y = Y; b.ln_ldy = ldy; b.ln_mean = mean; b.ln_rstd = rstd;
   const int cfg = N == 128 ? CFG_64x128_W41_NS4 : (K <= 256 ? CFG_64x256_W41_NS4 : CFG_64x256_W41_NS3);
-  const int rc = gemm_cfg_launch_6(cfg, b, 1, stream);
+  const int rc = gemm_cfg_launch_6_ln(cfg, b, 1, stream);
   s2h_prof_end(slot, stream);
   return rc;
 }
@@ -326,7 +325,7 @@ extern "C" int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64
       (dres && ldr % 8) || K % 8 || (int64_t)M * ldg >= (1ll << 31) || (int64_t)K * ldw >= (1ll << 31))
     return (int)hipErrorInvalidValue;
   const int slot = s2h_prof_begin(stream, 4, 1, M, N, K, 2 + 0 + 4);
-  GemmArgs16 b = {};
+  GemmArgs16Ln b = {};
   b.M = M; b.N = N; b.K = K;
   b.A = (const bf16*)G; b.lda_m = ldg; b.lda_k = 1;
   b.B = (const bf16*)W; b.ldb_k = ldw; b.ldb_n = 1;
@@ -338,7 +337,7 @@ extern "C" int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64
   b.ln_gamma = gamma; b.ln_mean = const_cast<float*>(mean); b.ln_rstd = const_cast<float*>(rstd);
   b.lnb_x = X; b.lnb_ldx = ldx; b.lnb_part = dgamma ? part : nullptr;
   const int cfg = N == 128 ? CFG_64x128_W41_NS4 : (K <= 256 ? CFG_64x256_W41_NS4 : CFG_64x256_W41_NS3);
-  int rc = gemm_cfg_launch_6(cfg, b, 1, stream);
+  int rc = gemm_cfg_launch_6_ln(cfg, b, 1, stream);
   s2h_prof_end(slot, stream);
   if (rc || !dgamma) return rc;
   return s2h_ln_wgrad_finalize((M + 63) / 64, N, part, dgamma, dbeta, stream);

@@ -27,20 +27,24 @@ struct GemmArgs16 {
   const float* rope_cos; const float* rope_sin;
   int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
   int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
-  // --- read only by the LayerNorm epilogues, so they sit behind every field the plain GEMM reads: each
-  // workgroup loads the argument block's leading cache lines (inserted before `dbg` these fields cost
-  // the 64x64 tilings 3 % in the step)
-  // optional LayerNorm of the finished output rows (round 4, s2h_linear_add_ln): the tile spans the
-  // whole output width (N <= 256, one wave per 16 full rows); C receives x' = R + drop(A W^T + b)
-  // (bf16, the residual stream), ln_y = LN(x') with gamma / beta / eps, ln_mean / ln_rstd per row --
-  // the residual add + LayerNorm that follows a projection (memory_attention.py:60-98), fused
+};
+
+// The LayerNorm epilogues' extra arguments (round 4), in a derived block that only the full-row tilings
+// (gemm_cfg6.hip) take: the argument block's size is paid by every launch -- 88 more bytes on every
+// GEMM cost 0.35 ms of the bench step (1114 GEMM launches; in-call A/B of the round-4 checkpoint with
+// its block padded by 88 bytes: 56.57 -> 56.95 ms, the same as with the fields inline)
+struct GemmArgs16Ln : GemmArgs16 {
+  // optional LayerNorm of the finished output rows (s2h_linear_add_ln): the tile spans the whole
+  // output width (N <= 256, one wave per 16 full rows); C receives x' = R + drop(A W^T + b) (bf16, the
+  // residual stream), ln_y = LN(x') with gamma / beta / eps, ln_mean / ln_rstd per row -- the
+  // residual add + LayerNorm that follows a projection (memory_attention.py:60-98), fused
   const float* ln_gamma; const float* ln_beta; float ln_eps;
   void* ln_y; int64_t ln_ldy; float* ln_mean; float* ln_rstd;
-  // optional LayerNorm BACKWARD of the finished rows (round 4, s2h_linear_dgrad_ln_bwd): the GEMM is
-  // the dgrad of the LayerNorm output's only consumer, alpha * acc = dL/dy over whole rows; lnb_x is
-  // the LayerNorm input (bf16), ln_gamma / ln_mean / ln_rstd its saved parameters and statistics,
-  // R the residual-stream gradient added to dx (may be null); C receives dx; lnb_part (may be null)
-  // one (sum dy * xhat, sum dy) row of 2N floats per 64-row tile for ln_wgrad_finalize_kernel
+  // optional LayerNorm BACKWARD of the finished rows (s2h_linear_dgrad_ln_bwd): the GEMM is the dgrad of
+  // the LayerNorm output's only consumer, alpha * acc = dL/dy over whole rows; lnb_x is the LayerNorm
+  // input (bf16), ln_gamma / ln_mean / ln_rstd its saved parameters and statistics, R the
+  // residual-stream gradient added to dx (may be null); C receives dx; lnb_part (may be null) one
+  // (sum dy * xhat, sum dy) row of 2N floats per 64-row tile for ln_wgrad_finalize_kernel
   const void* lnb_x; int64_t lnb_ldx; float* lnb_part;
 };
 

@@ -290,9 +290,9 @@ struct GemmShape {
   static constexpr int MINB = NS * STAGE_BYTES <= 80 * 1024 ? 2 : 1;  // workgroups per CU the LDS allows
 };
 
-template <int BM, int BN, int WGM, int WGN, int NS, int BK, bool AKC, bool BKC>
+template <int BM, int BN, int WGM, int WGN, int NS, int BK, bool AKC, bool BKC, typename PA = GemmArgs16>
 __global__ __launch_bounds__((GemmShape<BM, BN, WGM, WGN, NS, BK>::NT), (GemmShape<BM, BN, WGM, WGN, NS, BK>::MINB))
-void gemm16g_kernel(GemmArgs16 p) {
+void gemm16g_kernel(PA p) {
   if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
   using SH = GemmShape<BM, BN, WGM, WGN, NS, BK>;
   constexpr int NW = SH::NW, NT = SH::NT;
@@ -376,14 +376,14 @@ void gemm16g_kernel(GemmArgs16 p) {
   __syncthreads();
 
   if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
-  if constexpr (WGN == 1 && WN >= 128 && WN % 32 == 0) {  // full-row tiles: LayerNorm backward epilogue
-    if (p.lnb_x != nullptr) {
+  if constexpr (WGN == 1 && WN >= 128 && WN % 32 == 0 && std::is_same_v<PA, GemmArgs16Ln>) {
+    if (p.lnb_x != nullptr) {  // full-row tiles: LayerNorm backward epilogue
       static_assert(NW * 16 * (WN + 4) * 4 + NW * 2 * WN * 4 <= NS * STAGE, "LayerNorm-backward epilogue LDS");
       tile_epilogue_lnbwd<WM, WN, MI, NI, NW>(p, acc, smem, m0 + wm * WM, m0 / BM, lane, w);
       return;
     }
   }
-  tile_epilogue<WM, WN, MI, NI>(p, acc, reinterpret_cast<float*>(smem) + w * 16 * (WN + 4), bz, m0 + wm * WM,
+  tile_epilogue<WM, WN, MI, NI, PA>(p, acc, reinterpret_cast<float*>(smem) + w * 16 * (WN + 4), bz, m0 + wm * WM,
                                 n0 + wn * WN, lane);
 }
 
@@ -431,17 +431,24 @@ static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st
   gemm_plan_vec(a, batch);
 }
 
-template <int BM, int BN, int WGM, int WGN, int NS, int BK = 64>
-static int launch_glds(GemmArgs16& a, int batch, hipStream_t st) {
+template <int BM, int BN, int WGM, int WGN, int NS, int BK = 64, typename PA = GemmArgs16>
+static int launch_glds(PA& a, int batch, hipStream_t st) {
   plan_splits(a, batch, BM, BN, st);
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
   constexpr int NT = GemmShape<BM, BN, WGM, WGN, NS, BK>::NT;
   s2h_prof_tag(gemm_tag(BM, BN, WGM, WGN, NS, BK, akc, bkc, false, false));
   dim3 g1(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM), 1, batch * a.splits);
-  if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, true>), g1, dim3(NT), 0, st, a);
-  else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, false>), g1, dim3(NT), 0, st, a);
-  else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, true>), g1, dim3(NT), 0, st, a);
-  else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, false>), g1, dim3(NT), 0, st, a);
+  if constexpr (std::is_same_v<PA, GemmArgs16Ln>) {
+    if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, true, GemmArgs16Ln>), g1, dim3(NT), 0, st, a);
+    else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, false, GemmArgs16Ln>), g1, dim3(NT), 0, st, a);
+    else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, true, GemmArgs16Ln>), g1, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, false, GemmArgs16Ln>), g1, dim3(NT), 0, st, a);
+  } else {
+    if (akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, true>), g1, dim3(NT), 0, st, a);
+    else if (akc && !bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, true, false>), g1, dim3(NT), 0, st, a);
+    else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, true>), g1, dim3(NT), 0, st, a);
+    else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, false>), g1, dim3(NT), 0, st, a);
+  }
   return (int)hipGetLastError();
 }
 
@@ -478,3 +485,4 @@ int gemm_cfg_launch_3(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_4(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_5(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_6(int cfg, GemmArgs16& a, int batch, hipStream_t st);
+int gemm_cfg_launch_6_ln(int cfg, GemmArgs16Ln& a, int batch, hipStream_t st);  // the LayerNorm epilogues

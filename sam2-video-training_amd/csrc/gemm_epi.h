@@ -270,7 +270,7 @@ __device__ __forceinline__ void epilogue8(const GemmArgs16& p, int bz, int row, 
 // as the standalone LayerNorm kernel reads it (norm.hip ln_fwd_vec_kernel: two-pass variance).
 // Every lane of the wave calls this (the shuffles need them all); `live` guards the stores.
 template <int CPR>
-__device__ __forceinline__ void epilogue8_ln(const GemmArgs16& p, int bz, int row, int col0, const float* vin,
+__device__ __forceinline__ void epilogue8_ln(const GemmArgs16Ln& p, int bz, int row, int col0, const float* vin,
                                              const float* bcol, bool live) {
   float v[8];
 #pragma unroll
@@ -355,8 +355,12 @@ __device__ __forceinline__ void vm_wait() {
 // barrier: LDS operations of one wave retire in order.  (A register-direct variant with
 // swapped MFMA operands -- 4 consecutive columns per lane, no staging -- measured 1.5-2.6x
 // slower: its stores scatter 16 rows x 32 B per instruction, and split-K atomics likewise.)
-template <int WM, int WN, int MI, int NI>
-__device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[MI][NI], float* ep, int bz, int mw,
+// a LayerNorm epilogue requested (only the full-row tilings' argument block carries one)
+__device__ __forceinline__ bool ln_epilogue_on(const GemmArgs16&) { return false; }
+__device__ __forceinline__ bool ln_epilogue_on(const GemmArgs16Ln& p) { return p.ln_gamma != nullptr; }
+
+template <int WM, int WN, int MI, int NI, typename PA = GemmArgs16>
+__device__ __forceinline__ void tile_epilogue(const PA& p, f32x4 (&acc)[MI][NI], float* ep, int bz, int mw,
                                               int nw, int lane) {
   constexpr int EPLD = WN + 4;
   float bcol[4], bcol8[8];
@@ -391,11 +395,11 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
           }
         }
       }
-    } else if (WN >= 128 && WN % 32 == 0 && p.ln_gamma != nullptr) {
+    } else if (WN >= 128 && WN % 32 == 0 && ln_epilogue_on(p)) {
       // LayerNorm of whole rows (s2h_linear_add_ln checked: N == WN, one wave per 16 full rows).
       // Instantiated for the full-row tiles only: compiled into every tiling, the extra epilogue
       // raised the 64x64 tile's VGPRs 63 -> 81 and cost 1.5 % of the step with the fusion unused
-      if constexpr (WN >= 128 && WN % 32 == 0) {
+      if constexpr (WN >= 128 && WN % 32 == 0 && std::is_same_v<PA, GemmArgs16Ln>) {
         constexpr int CPR = WN / 8, RPP = 64 / CPR;
         const int c8 = lane % CPR, rg = lane / CPR;
         for (int ps = 0; ps < 16 / RPP; ++ps) {
@@ -442,7 +446,7 @@ __device__ __forceinline__ void tile_epilogue(const GemmArgs16& p, f32x4 (&acc)[
 // sums: lanes, then the waves through LDS; ln_wgrad_finalize_kernel adds the rows up).  Every wave of
 // the workgroup calls this (one workgroup barrier for the cross-wave sum).
 template <int WM, int WN, int MI, int NI, int NW>
-__device__ __forceinline__ void tile_epilogue_lnbwd(const GemmArgs16& p, f32x4 (&acc)[MI][NI], char* smem, int mw,
+__device__ __forceinline__ void tile_epilogue_lnbwd(const GemmArgs16Ln& p, f32x4 (&acc)[MI][NI], char* smem, int mw,
                                                     int tile, int lane, int w) {
   constexpr int EPLD = WN + 4, CPR = WN / 8, RPP = 64 / CPR;
   float* ep = reinterpret_cast<float*>(smem) + w * 16 * EPLD;

@@ -70,7 +70,10 @@ def load(path):
 
 def short(name):
     name = re.sub(r"^void ", "", name)
-    return re.sub(r"\((GemmArgs16|FlashArgs|FlashBwdArgs|Mx8Args|Mx8QArgs)\)$", "", name)
+    name = re.sub(r"\((GemmArgs16|GemmArgs16Ln|FlashArgs|FlashBwdArgs|Mx8Args|Mx8QArgs)\)$", "", name)
+    # gemm16g_kernel's argument-block parameter (GemmArgs16 / GemmArgs16Ln, gemm_bf16.h): bench.py's
+    # kernel_name() spells the tiling without it
+    return re.sub(r", GemmArgs16(Ln)?>$", ">", name)
 
 
 def main():
