@@ -30,9 +30,11 @@ struct GemmArgs16 {
 };
 
 // The LayerNorm epilogues' extra arguments (round 4), in a derived block that only the full-row tilings
-// (gemm_cfg6.hip) take: the argument block's size is paid by every launch -- 88 more bytes on every
-// GEMM cost 0.35 ms of the bench step (1114 GEMM launches; in-call A/B of the round-4 checkpoint with
-// its block padded by 88 bytes: 56.57 -> 56.95 ms, the same as with the fields inline)
+// (gemm_cfg6.hip) take, so the plain GEMM kernels compile exactly as before: with 88 more bytes in
+// every GEMM's block the bench step lost 0.35 ms (in-call A/B of the round-4 checkpoint with its block
+// padded by 88 bytes: 56.57 -> 56.95 ms).  Not the bytes themselves -- a graph of 1000 launches costs
+// 1.53-1.54 us per launch for any block from 64 B to 2 KB (tools/kernarg_probe.hip) -- but the code
+// generated around them
 struct GemmArgs16Ln : GemmArgs16 {
   // optional LayerNorm of the finished output rows (s2h_linear_add_ln): the tile spans the whole
   // output width (N <= 256, one wave per 16 full rows); C receives x' = R + drop(A W^T + b) (bf16, the
