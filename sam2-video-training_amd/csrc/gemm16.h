@@ -26,7 +26,7 @@ struct GemmArgs16 {
   // tables' column (c % rope_dh) / 2.  rope_cos == nullptr: no rotation.
   const float* rope_cos; const float* rope_sin;
   int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
-  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA
+  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA, 8 plain stores, 16 tile-major split-K order
 };
 
 // The LayerNorm epilogues' extra arguments (round 4), in a derived block that only the full-row tilings

@@ -307,12 +307,28 @@ void gemm16g_kernel(PA p) {
   const int wm = w / WGN, wn = w % WGN;
   // XCD-aware tile order (bijective remap): blocks id, id+8, ... share an XCD; give them
   // consecutive tiles of one row block so its A tile stays in that XCD's L2
-  const int nwg = gridDim.x, id = blockIdx.x;
-  const int xcd = id % 8, qd = nwg / 8, rm = nwg % 8;
-  const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + id / 8;
+  const int nwg = gridDim.x;
+  int wg, zi;  // tile, z index (batch * splits + split)
+  if (p.splits > 1 && !(p.dbg & 16)) {
+    // split-K (the weight gradients): the same remap over the (split, tile) pairs in split-major
+    // order, from the dispatch order x + gridDim.x * z -- an XCD runs whole K chunks with all their
+    // tiles side by side, so each chunk of both operands is read from HBM once and shared through
+    // that XCD's L2 (tile-major, every XCD read the whole of the narrow operand: the memory-attention
+    // FFN weight gradients fetched ~2.8x their algorithmic bytes, profiles/r04_v8_gemm_pmc.json)
+    const int total = nwg * gridDim.z, lin = blockIdx.x + nwg * blockIdx.z;
+    const int x8 = lin % 8, q8 = total / 8, r8 = total % 8;
+    const int w2 = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + lin / 8;
+    wg = w2 % nwg;
+    zi = w2 / nwg;
+  } else {
+    const int id = blockIdx.x;
+    const int xcd = id % 8, qd = nwg / 8, rm = nwg % 8;
+    wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + id / 8;
+    zi = blockIdx.z;
+  }
   const int ntn = (p.N + BN - 1) / BN;
   const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
-  const int bz = blockIdx.z / p.splits, split = blockIdx.z % p.splits;
+  const int bz = zi / p.splits, split = zi % p.splits;
   const bf16* A = p.A + (int64_t)bz * p.sA;
   const bf16* B = p.B + (int64_t)bz * p.sB;
   const int kbeg = split * p.kchunk;
