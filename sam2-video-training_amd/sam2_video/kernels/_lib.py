@@ -153,6 +153,8 @@ def lib():
             fn.restype = RESTYPES.get(name, c_int)
         if os.environ.get("S2H_GEMM_CFG"):  # measurement override of the GEMM tiling choice
             h.s2h_gemm_config(int(os.environ["S2H_GEMM_CFG"]))
+        if os.environ.get("S2H_GEMM_SPLIT_TARGET"):  # workgroups a split-K launch aims at (A/B)
+            h.s2h_gemm_split_target(int(os.environ["S2H_GEMM_SPLIT_TARGET"]))
         if os.environ.get("S2H_GEMM_TINY_CFG"):  # ... of the tiny-M (<= 128 rows) GEMMs only
             h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
         if os.environ.get("S2H_ATTN_WIN"):  # small-window attention kernels on / off (A/B)
