@@ -56,8 +56,8 @@ void s2h_prof_end(int slot, hipStream_t st);
 void s2h_prof_tag(int64_t tag);  // runtime.hip: the kernel of the current profiler record
 // profiler tag of a GEMM tiling (include/sam2hip.h, s2h_prof_read_tags)
 static inline int64_t gemm_tag(int BM, int BN, int WGM, int WGN, int NS, int BK, bool akc, bool bkc, bool regs,
-                               bool mx8) {
+                               bool mx8, bool areg = false) {
   return (int64_t)BM | ((int64_t)BN << 10) | ((int64_t)WGM << 20) | ((int64_t)WGN << 24) | ((int64_t)NS << 28) |
          ((int64_t)(BK / 32) << 32) | ((int64_t)akc << 36) | ((int64_t)bkc << 37) | ((int64_t)regs << 38) |
-         ((int64_t)mx8 << 39);
+         ((int64_t)mx8 << 39) | ((int64_t)areg << 40);
 }

@@ -403,6 +403,82 @@ void gemm16g_kernel(PA p) {
                                 n0 + wn * WN, lane);
 }
 
+// Short-K variant (round 4, K <= KMAX = 256 -- the step's projections, FFN linear1 forward and the
+// K = 256 dgrads): the waves are stacked along M (16 rows each), so no wave reads another's A rows;
+// every wave loads ITS A panel (16 rows x K) straight into registers as MFMA fragments (lane l: row
+// l & 15, k 32 ks + 8 (l >> 4); one 16-B load per fragment), and only B -- shared by the 4 waves --
+// goes through LDS, all of its K stages issued at once.  LDS per workgroup is B alone (BN x K x 2 B:
+// 32 KB at BN 64), so 4-5 workgroups fit a CU where the two-operand 64 x 64 tile with all K in flight
+// fits 2 (64 KB).  The A loads are plain (compiler-visible) loads issued before the B DMA: the one
+// wait before the first MFMA (vmcnt(0)) retires both.  Requirements: K-contiguous A, K <= KMAX,
+// no split-K, no fused row sums (gemm_areg_ok).
+template <int BN, int KMAX, bool BKC>
+__global__ __launch_bounds__(256, 4) void gemm16a_kernel(GemmArgs16 p) {
+  if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);
+  constexpr int BM = 64, NW = 4, WM = 16, WN = BN, MI = 1, NI = BN / 16, KS = KMAX / 32, NST = KMAX / 64;
+  using IB = GImg<BN, BKC, NW, 64>;
+  __shared__ __attribute__((aligned(1024))) char smem[NST * IB::BYTES > NW * 16 * (WN + 4) * 4 ? NST * IB::BYTES
+                                                                                              : NW * 16 * (WN + 4) * 4];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int nwg = gridDim.x, id = blockIdx.x;
+  const int xcd = id % 8, qd = nwg / 8, rm = nwg % 8;
+  const int wg = (xcd < rm ? xcd * (qd + 1) : rm * (qd + 1) + (xcd - rm) * qd) + id / 8;
+  const int ntn = (p.N + BN - 1) / BN;
+  const int m0 = (wg / ntn) * BM, n0 = (wg % ntn) * BN;
+  const int bz = blockIdx.z;
+  const bf16* A = p.A + (int64_t)bz * p.sA;
+  const bf16* B = p.B + (int64_t)bz * p.sB;
+  const int K = p.K;
+  const int nk = (K + 63) / 64;
+
+  // A fragments of this wave's 16 rows (rows past M clamped; k >= K zero)
+  bf16x8 af[KS];
+  {
+    const int r = min(m0 + w * WM + (lane & 15), p.M - 1);
+    const bf16* arow = A + (int64_t)r * p.lda_m;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int k = 32 * ks + 8 * (lane >> 4);
+      if (32 * ks < K) af[ks] = k < K ? *(const bf16x8*)(arow + k) : bf16x8{};
+      else af[ks] = bf16x8{};
+    }
+  }
+  // B: every K stage in flight at once
+#pragma unroll
+  for (int st = 0; st < NST; ++st)
+    if (st < nk && !(p.dbg & 4)) IB::dma(smem + st * IB::BYTES, B, p.ldb_n, p.ldb_k, n0, st * 64, p.N, K, w, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (K % 64) {  // zero the K tail of the last stage's image
+    IB::zero_tail(smem + (nk - 1) * IB::BYTES, K - (nk - 1) * 64, tid);
+    __syncthreads();
+  }
+  f32x4 acc[MI][NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) acc[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!(p.dbg & 2)) {
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (32 * ks >= K) break;
+      const char* sb = smem + (ks / 2) * IB::BYTES;
+      bf16x8 b[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) b[j] = IB::frag(sb, j * 16, ks % 2, lane);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[0][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ks], b[j], acc[0][j], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __syncthreads();  // the B images are reused as the epilogue slabs
+  tile_epilogue<WM, WN, MI, NI>(p, acc, reinterpret_cast<float*>(smem) + w * 16 * (WN + 4), bz, m0 + w * WM, n0,
+                                lane);
+}
+
+static bool gemm_areg_ok(const GemmArgs16& a, int kmax) {
+  return a.lda_k == 1 && a.K <= kmax && a.K > 0 && a.rowsum == nullptr && ((uintptr_t)a.A & 15) == 0 &&
+         a.lda_m % 8 == 0 && a.K % 8 == 0 && (a.sA % 8 == 0);
+}
+
 static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
   auto al = [](const void* ptr) { return ((uintptr_t)ptr & 15) == 0; };
   const bool akc = a.lda_k == 1, bkc = a.ldb_k == 1;
@@ -468,6 +544,18 @@ static int launch_glds(PA& a, int batch, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+template <int BN, int KMAX = 256>
+static int launch_areg(GemmArgs16& a, int batch, hipStream_t st) {
+  plan_splits(a, batch, 64, BN, st);
+  if (a.splits != 1) return -1;
+  const bool bkc = a.ldb_k == 1;
+  s2h_prof_tag(gemm_tag(64, BN, 4, 1, 1, 64, true, bkc, false, false, true));
+  dim3 g(((a.N + BN - 1) / BN) * ((a.M + 63) / 64), 1, batch);
+  if (bkc) hipLaunchKernelGGL((gemm16a_kernel<BN, KMAX, true>), g, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((gemm16a_kernel<BN, KMAX, false>), g, dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}
+
 template <int BM, int BN>
 static int launch16_regs(GemmArgs16& a, int batch, hipStream_t st) {
   plan_splits(a, batch, BM, BN, st);
@@ -492,6 +580,8 @@ enum GemmCfg {
   // full-row tiles (round 4): one workgroup owns 64 rows x the whole N <= 256 output width, the four
   // waves stacked along M (16 full rows each), the K ring 4 stages deep (K <= 256 in one round trip)
   CFG_64x256_W41_NS4 = 25, CFG_64x128_W41_NS4 = 26, CFG_64x256_W41_NS3 = 27, CFG_64x256_W41_K32_NS4 = 28,
+  // short K (round 4): A in registers, only B through LDS (gemm16a_kernel), K <= 256
+  CFG_64_AREG = 29, CFG_64x128_AREG = 30,
   CFG_REGS = 99
 };
 // per-translation-unit launchers: return -1 when `cfg` is not one of the unit's tilings
@@ -502,3 +592,4 @@ int gemm_cfg_launch_4(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_5(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_6(int cfg, GemmArgs16& a, int batch, hipStream_t st);
 int gemm_cfg_launch_6_ln(int cfg, GemmArgs16Ln& a, int batch, hipStream_t st);  // the LayerNorm epilogues
+int gemm_cfg_launch_7(int cfg, GemmArgs16& a, int batch, hipStream_t st);

@@ -101,5 +101,6 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   if ((rc = gemm_cfg_launch_4(cfg, a, batch, st)) >= 0) return rc;
   if ((rc = gemm_cfg_launch_5(cfg, a, batch, st)) >= 0) return rc;
   if ((rc = gemm_cfg_launch_6(cfg, a, batch, st)) >= 0) return rc;
+  if ((rc = gemm_cfg_launch_7(cfg, a, batch, st)) >= 0) return rc;
   return gemm_cfg_launch_3(CFG_128, a, batch, st);
 }

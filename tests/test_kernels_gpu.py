@@ -91,8 +91,8 @@ def test_gemm_lds_dma_path(M, N, K, layout):
 
 
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19, 20, 21, 22, 23, 24,
-                                 25, 26, 27, 28, -1])
-@pytest.mark.parametrize("M,N,K", [(1000, 520, 200), (600, 264, 1100), (13312, 256, 256)])
+                                 25, 26, 27, 28, 29, 30, -1])
+@pytest.mark.parametrize("M,N,K", [(1000, 520, 200), (600, 264, 1100), (13312, 256, 256), (333, 136, 72)])
 @pytest.mark.parametrize("layout", ["nt", "nn", "tn", "tt"])
 def test_gemm_every_tiling(cfg, M, N, K, layout):
     """each forced tiling (64^2, 128^2 2/3-deep ring, 256x128, 256^2, 128x256, register-staged)
@@ -1051,3 +1051,32 @@ def test_linear_dgrad_ln_bwd_matches_unfused(M, C, K, res, wgrad):
         _close(db, br.grad, 2e-3)
         _close(dg, dg2, 1e-2)
         _close(db, db2, 1e-2)
+
+
+@pytest.mark.parametrize("cfg", [29, 30])
+@pytest.mark.parametrize("M,N,K,bkc", [(13312, 256, 256, True), (13312, 768, 256, True), (93184, 256, 256, False),
+                                       (1000, 200, 136, True), (70, 24, 40, False), (13312, 2048, 256, False)])
+def test_areg_tiling_bit_identical(cfg, M, N, K, bkc):
+    """the short-K tilings with A in registers (gemm16a_kernel) accumulate every output over the same
+    K order as the LDS-staged 64 x 64 tile, so with the same epilogue (bias, ReLU, dropout, residual)
+    the results are bit-identical"""
+    from sam2_video.kernels import _lib
+    ops = _ops()
+    torch.manual_seed(3)
+    bf = torch.bfloat16
+    ops.rng_offset(DEV).fill_(5)
+    a = torch.randn(M, K, device=DEV).to(bf)
+    b = torch.randn(N, K, device=DEV).to(bf) if bkc else torch.randn(K, N, device=DEV).to(bf)
+    kw = dict(M=M, N=N, K=K, lda_m=K, lda_k=1, ldb_k=1 if bkc else N, ldb_n=K if bkc else 1, ldc=N)
+    bias = torch.randn(N, device=DEV)
+    res = torch.randn(M, N, device=DEV).to(bf)
+    outs = []
+    for c in (1, cfg):
+        prev = _lib.lib().s2h_gemm_config(c)
+        try:
+            out = torch.empty(M, N, device=DEV, dtype=bf)
+            ops.gemm(a, b, out, bias=bias, residual=res, ldr=N, act=1, drop_p=0.1, seed=17, **kw)
+            outs.append(out)
+        finally:
+            _lib.lib().s2h_gemm_config(prev)
+    assert torch.equal(outs[0], outs[1])
