@@ -111,6 +111,10 @@ int s2h_gemm_tiny_config(int cfg);
  * 2 x 2 (1: all, the default; 2: only N >= 768; 0: off); results are bit-identical.  Returns the
  * previous mode. */
 int s2h_gemm_w41(int mode);
+/* A/B knob: GEMMs with a short K that is not a multiple of 64 (K < 256, K-contiguous A, bf16 output)
+ * on the A-in-registers tiling (1: on, the default; 0: off); results are bit-identical.  Returns the
+ * previous mode. */
+int s2h_gemm_areg(int mode);
 
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),

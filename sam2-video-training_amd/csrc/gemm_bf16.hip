@@ -41,6 +41,18 @@ static int w41_of(int cfg) {
   }
 }
 
+// Short K that is not a whole number of 64-deep stages (Hiera's 112 / 224 channels, the V-fold's 72,
+// the memory encoder's 64 + 8 ...) on the A-in-registers tiling: no zero-filled tail stage, no
+// extra barrier, 5 workgroups per CU (tools/areg_bench.py, profiles/r04_v11_areg.log: 32768x224x224
+// 22.1 -> 17.2 us, 8192x448x112 9.3 -> 8.3, 13312x256x72 9.7 -> 8.4; at K = 128 / 256 the LDS-DMA
+// tilings stay ahead).  1 = on (default), 0 = off (A/B, S2H_GEMM_AREG)
+static int g_gemm_areg = 1;
+extern "C" int s2h_gemm_areg(int mode) {
+  const int prev = g_gemm_areg;
+  g_gemm_areg = mode;
+  return prev;
+}
+
 extern "C" int s2h_gemm_config(int cfg) {
   const int prev = g_gemm_cfg | (g_gemm_dbg << 8);
   g_gemm_cfg = cfg < 0 ? cfg : (cfg & 0xff);
@@ -93,6 +105,8 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
   if (g_gemm_tiny_cfg && !g_gemm_cfg && a.M <= 128) cfg = g_gemm_tiny_cfg;
   if (g_gemm_w41 && !g_gemm_cfg && !a.out_f32 && (g_gemm_w41 == 1 || a.N >= 768)) cfg = w41_of(cfg);
+  if (g_gemm_areg && !g_gemm_cfg && a.K < 256 && a.K % 64 != 0 && !a.out_f32 && a.M > 128 && gemm_areg_ok(a, 256))
+    cfg = CFG_64_AREG;
   if (cfg < 0 || !gemm_glds_ok(a, batch)) return gemm_cfg_launch_1(CFG_REGS, a, batch, st);  // register-staged
   int rc;
   if ((rc = gemm_cfg_launch_1(cfg, a, batch, st)) >= 0) return rc;

@@ -41,6 +41,7 @@ SIGNATURES = {
     "s2h_gemm_split_target": [I],
     "s2h_gemm_tiny_config": [I],
     "s2h_gemm_w41": [I],
+    "s2h_gemm_areg": [I],
     "s2h_attn_win": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
     "s2h_gemm_mx8": [I, I, I, P, L, P, L, P, L, P, L, P, I, L, P, P, L, P, L, I, F, c_uint64, c_uint64, F, F, I, P],
@@ -159,6 +160,8 @@ def lib():
             h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
         if os.environ.get("S2H_ATTN_WIN"):  # small-window attention kernels on / off (A/B)
             h.s2h_attn_win(int(os.environ["S2H_ATTN_WIN"]))
+        if os.environ.get("S2H_GEMM_AREG"):  # ... short-K GEMMs with A in registers (A/B)
+            h.s2h_gemm_areg(int(os.environ["S2H_GEMM_AREG"]))
         if os.environ.get("S2H_GEMM_W41"):  # ... bf16-output GEMMs on 4 x 1 wave grids (A/B)
             h.s2h_gemm_w41(int(os.environ["S2H_GEMM_W41"]))
         _LIB = h
