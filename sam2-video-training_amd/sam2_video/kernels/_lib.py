@@ -158,6 +158,8 @@ def lib():
             h.s2h_gemm_split_target(int(os.environ["S2H_GEMM_SPLIT_TARGET"]))
         if os.environ.get("S2H_GEMM_TINY_CFG"):  # ... of the tiny-M (<= 128 rows) GEMMs only
             h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
+        if os.environ.get("S2H_ATTN_CFG"):  # flash switch | forward key-split target << 8 (A/B)
+            h.s2h_attn_config(int(os.environ["S2H_ATTN_CFG"]))
         if os.environ.get("S2H_ATTN_WIN"):  # small-window attention kernels on / off (A/B)
             h.s2h_attn_win(int(os.environ["S2H_ATTN_WIN"]))
         if os.environ.get("S2H_GEMM_AREG"):  # ... short-K GEMMs with A in registers (A/B)
