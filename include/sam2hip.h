@@ -297,6 +297,17 @@ int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64_t ldg, con
 /* dgamma += sum_b part[b][0:C], dbeta += sum_b part[b][C:2C] over nb partial rows of 2C floats. */
 int s2h_ln_wgrad_finalize(int nb, int C, const float* part, float* dgamma, float* dbeta, hipStream_t st);
 
+/* Per-object MLP heads under no_grad in ONE launch (bf16): for each of nheads (<= 4) heads, rows
+ * x[h] [M, dims[4h]] (row stride ldx[h]) through nl[h] (<= 3) Linear layers w[3h + l]
+ * [dims[4h+l+1], dims[4h+l]] (+ fp32 bias b[3h + l] or NULL), ReLU between layers, act_last[h]
+ * (S2HAct) after the last, into y[h] [M, dims[4h + nl]] (row stride ldy[h]); widths <= 256 (hidden
+ * ones multiples of 8), 16-B aligned rows.  Bit-identical to the per-layer GEMMs.  Replaces the
+ * object-score head (mask_decoder.py:234-238) and the object-pointer projection (sam2_base.py:296-305
+ * obj_ptr_proj): 6 launches of 13 rows per frame -> 1.  Argument arrays are host memory. */
+int s2h_mlp_heads(int nheads, int M, const void* const* x, const int64_t* ldx, const void* const* w,
+                  const float* const* b, const int* dims, const int* nl, const int* act_last, void* const* y,
+                  const int64_t* ldy, hipStream_t st);
+
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:
  * xsum = x + badd (badd broadcast over rows when b_bcast), y = LN(xsum) * gamma + beta;

@@ -1,0 +1,135 @@
+// Per-object MLP heads in one launch (round 4): the SAM2 heads that run under no_grad on the
+// objects' tokens -- the object-score head (mask_decoder.py:234-238, MLP 256 -> 256 -> 256 -> 1) and
+// the object-pointer projection (sam2_base.py:296-305 obj_ptr_proj, MLP 256 -> 256 -> 256 -> 256) --
+// were 3 + 3 GEMM launches of 13 rows each per frame.  Here one workgroup carries 16 rows of one head
+// through all of its layers: the activation rows stay in LDS between layers, each wave computes
+// 16-column output tiles with 16x16x32 MFMAs whose weight fragments are loaded straight from global
+// memory (lane l: output column l & 15, k 32 ks + 8 (l >> 4)), and the bias / activation / bf16
+// rounding follow every layer exactly as the GEMM epilogue does -- so the outputs are bit-identical
+// to the per-layer GEMMs (same K order per output element, same epilogue arithmetic).
+#include "common.h"
+
+namespace {
+
+constexpr int HD_MAXH = 4;    // heads per launch
+constexpr int HD_MAXL = 3;    // layers per head
+constexpr int HD_MAXK = 256;  // widest layer input / output
+constexpr int HD_LD = HD_MAXK + 8;  // LDS activation row (bf16), padded: conflict-free b128 reads
+
+struct HeadDesc {
+  const bf16* x;  // [M, dims[0]] rows, row stride ldx
+  int64_t ldx;
+  const bf16* w[HD_MAXL];     // [dims[l + 1], dims[l]] row-major (the Linear weight)
+  const float* b[HD_MAXL];    // [dims[l + 1]] or null
+  int dims[HD_MAXL + 1];
+  int nl;        // layers
+  int act_last;  // S2HAct of the last layer (the hidden layers are ReLU)
+  bf16* y;       // [M, dims[nl]], row stride ldy
+  int64_t ldy;
+};
+
+struct HeadsArgs {
+  HeadDesc h[HD_MAXH];
+  int nheads, M;
+};
+
+typedef __attribute__((ext_vector_type(8))) __bf16 hd_bf16x8;
+typedef __attribute__((ext_vector_type(4))) float hd_f32x4;
+
+__global__ __launch_bounds__(256) void mlp_heads_kernel(HeadsArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 act[2][16 * HD_LD];
+  const HeadDesc& d = a.h[blockIdx.y];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = blockIdx.x * 16;
+  // layer-0 input rows (rows past M and columns past K zero), 8 columns per thread
+  {
+    const int K0 = d.dims[0];
+    for (int i = tid; i < 16 * (HD_MAXK / 8); i += 256) {
+      const int r = i / (HD_MAXK / 8), c = (i % (HD_MAXK / 8)) * 8;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (r0 + r < a.M && c < K0) v = *(const uint4*)(d.x + (int64_t)(r0 + r) * d.ldx + c);
+      *(uint4*)(act[0] + r * HD_LD + c) = v;
+    }
+  }
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < d.nl; ++l) {
+    const int K = d.dims[l], N = d.dims[l + 1];
+    const bool last = l == d.nl - 1;
+    const int act_fn = last ? d.act_last : S2H_ACT_RELU;
+    const bf16* W = d.w[l];
+    const float* bias = d.b[l];
+    const bf16* in = act[cur];
+    bf16* out = act[cur ^ 1];
+    const int ntiles = (N + 15) / 16;
+    for (int t = w; t < ntiles; t += 4) {
+      const int n = 16 * t + (lane & 15);
+      hd_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      for (int ks = 0; ks < (K + 31) / 32; ++ks) {
+        const int k = 32 * ks + 8 * (lane >> 4);
+        const hd_bf16x8 af = *(const hd_bf16x8*)(in + (lane & 15) * HD_LD + k);
+        hd_bf16x8 bf = {};
+        if (n < N && k < K) bf = *(const hd_bf16x8*)(W + (int64_t)n * K + k);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
+      }
+      // lane holds rows 4 (lane >> 4) + e of column n
+      const float bn = (bias != nullptr && n < N) ? bias[n] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int r = 4 * (lane >> 4) + e;
+        const bf16 v = (bf16)apply_act(acc[e] + bn, act_fn);
+        if (n < N) {
+          out[r * HD_LD + n] = v;
+          if (last && r0 + r < a.M) d.y[(int64_t)(r0 + r) * d.ldy + n] = v;
+        }
+      }
+    }
+    // columns [N, round up to 32) of the next input must read as zero
+    if (!last) {
+      for (int i = tid; i < 16 * 32; i += 256) {
+        const int r = i / 32, c = N + i % 32;
+        if (c < HD_MAXK + 8 && c < ((N + 31) / 32) * 32) out[r * HD_LD + c] = (bf16)0.f;
+      }
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+}
+
+}  // namespace
+
+// heads[h]: x [M, dims[h*4]] (row stride ldx[h]), weights w[h*3 + l] [dims[h*4+l+1], dims[h*4+l]],
+// biases b[h*3 + l] (fp32 or null), nl[h] layers (<= 3; hidden layers ReLU, the last act_last[h]),
+// y [M, dims[h*4 + nl]] (row stride ldy[h]); bf16; every width <= 256 and a multiple of 8 (the last
+// may be any width <= 256); 16-B aligned rows.
+extern "C" int s2h_mlp_heads(int nheads, int M, const void* const* x, const int64_t* ldx, const void* const* w,
+                             const float* const* b, const int* dims, const int* nl, const int* act_last,
+                             void* const* y, const int64_t* ldy, hipStream_t st) {
+  if (M <= 0 || nheads <= 0) return 0;
+  if (nheads > HD_MAXH) return (int)hipErrorInvalidValue;
+  HeadsArgs a = {};
+  a.nheads = nheads;
+  a.M = M;
+  for (int h = 0; h < nheads; ++h) {
+    HeadDesc& d = a.h[h];
+    d.nl = nl[h];
+    if (d.nl < 1 || d.nl > HD_MAXL || !x[h] || !y[h] || ((uintptr_t)x[h] & 15) || ldx[h] % 8)
+      return (int)hipErrorInvalidValue;
+    d.x = (const bf16*)x[h];
+    d.ldx = ldx[h];
+    d.y = (bf16*)y[h];
+    d.ldy = ldy[h];
+    d.act_last = act_last[h];
+    for (int l = 0; l <= d.nl; ++l) {
+      d.dims[l] = dims[h * (HD_MAXL + 1) + l];
+      if (d.dims[l] <= 0 || d.dims[l] > HD_MAXK || (l < d.nl && d.dims[l] % 8)) return (int)hipErrorInvalidValue;
+    }
+    for (int l = 0; l < d.nl; ++l) {
+      d.w[l] = (const bf16*)w[h * HD_MAXL + l];
+      d.b[l] = b[h * HD_MAXL + l];
+      if (!d.w[l] || ((uintptr_t)d.w[l] & 15)) return (int)hipErrorInvalidValue;
+    }
+  }
+  hipLaunchKernelGGL(mlp_heads_kernel, dim3((M + 15) / 16, nheads), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}

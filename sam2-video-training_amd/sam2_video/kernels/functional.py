@@ -201,6 +201,39 @@ def add_layer_norm(x, add, mod, eps):
     return _LayerNorm.apply(x.contiguous(), mod.weight, mod.bias, mod, eps, add.contiguous(), False)
 
 
+# ------------------------------------------------ no-grad per-object MLP heads (one launch)
+def _head_ok(m, x):
+    layers = getattr(m, "layers", None)
+    if layers is None or getattr(m, "act", None) != "relu" or not (1 <= len(layers) <= 3):
+        return False
+    if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1 or x.stride(0) % 8 or x.data_ptr() % 16:
+        return False
+    k = x.shape[1]
+    for i, lin in enumerate(layers):
+        w = lin.compute_weight()
+        last = i == len(layers) - 1
+        if w.dtype != torch.bfloat16 or not w.is_contiguous() or w.shape[1] != k or k > 256 or k % 8 or \
+                w.shape[0] > 256 or (not last and w.shape[0] % 8) or w.data_ptr() % 16:
+            return False
+        k = w.shape[0]
+    return True
+
+
+def mlp_heads_nograd(pairs):
+    """[(MLP module, x [M, K] rows)] -> [module(x)] for heads whose outputs need no gradient (the object
+    score head, mask_decoder.py:234-238, and the object-pointer projection, sam2_base.py:296-305): one
+    launch for all of them (s2h_mlp_heads: per head the layers chained in LDS, bit-identical to the
+    per-layer GEMMs) when every head is a bf16 ReLU MLP of <= 3 layers no wider than 256; else each
+    head's own forward.  S2H_MLP_HEADS=0 keeps the per-layer GEMMs (A/B)."""
+    import os
+    ok = (0 < len(pairs) <= 4 and os.environ.get("S2H_MLP_HEADS", "1") != "0"
+          and len({x.shape[0] for _, x in pairs}) == 1 and all(_head_ok(m, x) for m, x in pairs))
+    if not ok:
+        return [m(x) for m, x in pairs]
+    return ops.mlp_heads([(x, [lin.compute_weight() for lin in m.layers], [lin.compute_bias() for lin in m.layers],
+                           "sigmoid" if m.sigmoid_output else None) for m, x in pairs])
+
+
 # ------------------------------------------------ Linear + residual add + LayerNorm (one launch)
 def linear_ln_enabled():
     """S2H_LINEAR_LN=1 runs a projection + the residual add + LayerNorm after it as ONE full-row GEMM

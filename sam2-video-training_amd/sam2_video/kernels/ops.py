@@ -248,6 +248,36 @@ def linear_dgrad_ln_bwd(dy, w, x, gamma, mean, rstd, dres=None, dgamma=None, dbe
     return dx
 
 
+def mlp_heads(heads):
+    """no-grad MLP heads in one launch (s2h_mlp_heads): heads = [(x [M, K0] bf16 rows, [W_l] bf16
+    [N_l, K_l], [b_l fp32 or None], act_last)] with the same M; ReLU between layers.  Returns [y]"""
+    import ctypes
+    n = len(heads)
+    M = heads[0][0].shape[0]
+    xs, lds, ws, bs, dims, nls, acts, ys, ldys = [], [], [], [], [], [], [], [], []
+    for x, wl, bl, act_last in heads:
+        assert x.dtype == torch.bfloat16 and x.shape[0] == M and x.stride(1) == 1 and len(wl) <= 3
+        y = torch.empty(M, wl[-1].shape[0], device=x.device, dtype=x.dtype)
+        _dev(x, y, *wl, *[b for b in bl if b is not None])
+        xs.append(ptr(x))
+        lds.append(x.stride(0))
+        d = [x.shape[1]] + [w.shape[0] for w in wl]
+        for w, k in zip(wl, d[:-1]):
+            assert w.is_contiguous() and w.dtype == torch.bfloat16 and w.shape[1] == k
+        dims += d + [0] * (4 - len(d))
+        ws += [ptr(w) for w in wl] + [None] * (3 - len(wl))
+        bs += [ptr(b) for b in bl] + [None] * (3 - len(bl))
+        nls.append(len(wl))
+        acts.append(ACT[act_last])
+        ys.append(y)
+        ldys.append(y.stride(0))
+    P = ctypes.c_void_p
+    call("s2h_mlp_heads", n, M, (P * n)(*xs), (ctypes.c_int64 * n)(*lds), (P * (3 * n))(*ws),
+         (P * (3 * n))(*bs), (ctypes.c_int * (4 * n))(*dims), (ctypes.c_int * n)(*nls), (ctypes.c_int * n)(*acts),
+         (P * n)(*[ptr(y) for y in ys]), (ctypes.c_int64 * n)(*ldys), stream())
+    return ys
+
+
 def linear_wgrad(dy, x, dw, accumulate=True, db=None):
     """dw (fp32 [N, K]) (+)= dy^T @ x;  db (fp32 [N], optional) (+)= dy summed over rows."""
     dy2 = dy.reshape(-1, dy.shape[-1])

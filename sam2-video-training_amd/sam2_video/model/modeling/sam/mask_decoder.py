@@ -81,7 +81,8 @@ class MaskDecoder(nn.Module):
         self.pred_obj_score_head = (MLP(transformer_dim, transformer_dim, 1, 3) if pred_obj_scores_mlp
                                     else Linear(transformer_dim, 1))
 
-    def forward(self, image_embeddings, h, w, image_pe_table, sparse, no_mask_embed, high_res_features, dense=None):
+    def forward(self, image_embeddings, h, w, image_pe_table, sparse, no_mask_embed, high_res_features, dense=None,
+                defer_score=False):
         """image_embeddings [O, h*w, C]; sparse [O, Ns, C]; high_res_features (s0 [1|O, 4h, 4w, C/8],
         s1 [1|O, 2h, 2w, C/4]) -> (low-res mask logits [O, 4h*4w] compute dtype, iou [O, 1],
         mask token 0 [O, C], object score logits [O, 1] f32)"""
@@ -109,6 +110,8 @@ class MaskDecoder(nn.Module):
         masks = hyper_mask(hyper0, u.view(O, -1, C // 8))
         iou_pred = self.iou_prediction_head(iou_token_out)
         iou0 = FN.cast(FN.select_token(iou_pred.unsqueeze(-1), 0), torch.float32)
+        if defer_score:  # the caller runs the object-score head with its other no-grad heads (one launch)
+            return masks, iou0, mask_token0, hs[:, 0].detach()
         with torch.no_grad():
             score = self.pred_obj_score_head(hs[:, 0].detach().contiguous())
             score = ops.cast(score, torch.float32) if score.dtype != torch.float32 else score

@@ -281,16 +281,25 @@ class SAM2Base(nn.Module):
         pe_dev, lab_dev = prompt
         sparse = self.sam_prompt_encoder.sparse(pe_dev, lab_dev, dt)
         dense_pe = self.sam_prompt_encoder.dense_pe_table(pix.device, dt)
+        defer = pix.dtype == torch.bfloat16 and hasattr(self.obj_ptr_proj, "layers")
         masks, ious, token0, score = self.sam_mask_decoder(pix, h, w, dense_pe, sparse,
                                                            self.sam_prompt_encoder.no_mask_embed, high_res,
-                                                           **({"dense": dense} if dense is not None else {}))
+                                                           **({"dense": dense} if dense is not None else {}),
+                                                           defer_score=defer)
+        ptr = None
+        if defer:  # object-score head and object-pointer projection: no gradient, one launch for both
+            with torch.no_grad():
+                score, ptr = FN.mlp_heads_nograd([(self.sam_mask_decoder.pred_obj_score_head, score),
+                                                  (self.obj_ptr_proj, token0.detach())])
+                score = ops.cast(score, torch.float32)
         score_flat = score.view(-1).contiguous()
         low = FN.cast(masks, torch.float32)
         low = FN.row_gate(low, score_flat, NO_OBJ_SCORE)
         low = low.view(O, 4 * h, 4 * w)
         high = FN.bilinear(low, self.image_size, self.image_size)
         with torch.no_grad():
-            ptr = self.obj_ptr_proj(token0.detach())
+            if ptr is None:
+                ptr = self.obj_ptr_proj(token0.detach())
             ptr = ops.gate_mix(ptr, score_flat, self.no_obj_ptr._s2h_compute.view(-1), scale_x=self.fixed_no_obj_ptr)
         return low, high, ious, ptr, score
 

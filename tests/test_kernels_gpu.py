@@ -1080,3 +1080,29 @@ def test_areg_tiling_bit_identical(cfg, M, N, K, bkc):
         finally:
             _lib.lib().s2h_gemm_config(prev)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("M", [13, 3, 40])
+def test_mlp_heads_bit_identical(M):
+    """s2h_mlp_heads (no-grad per-object MLP heads in one launch: the object-score head and the
+    object-pointer projection) against the per-layer GEMMs: same K order and epilogue arithmetic per
+    layer, so bit-identical -- a strided input view (the decoder's token rows), 1- / 32- / 256-wide
+    outputs, a sigmoid last layer, rows spanning several workgroups"""
+    ops = _ops()
+    torch.manual_seed(9)
+    bf = torch.bfloat16
+    hs = torch.randn(M, 9, 256, device=DEV).to(bf)
+    specs = [(hs[:, 0], [256, 256, 256, 1], None), (hs[:, 2].contiguous(), [256, 256, 256, 256], None),
+             (hs[:, 3].contiguous(), [256, 256, 256, 32], "sigmoid"), (hs[:, 1].contiguous(), [256, 128, 4], None)]
+    heads, refs = [], []
+    for x, dims, last_act in specs:
+        ws = [(torch.randn(dims[i + 1], dims[i], device=DEV) / dims[i] ** 0.5).to(bf) for i in range(len(dims) - 1)]
+        bs = [torch.randn(dims[i + 1], device=DEV) * 0.1 for i in range(len(dims) - 1)]
+        heads.append((x, ws, bs, last_act))
+        y = x.contiguous()
+        for i, (w, b) in enumerate(zip(ws, bs)):
+            y = ops.linear(y, w, b, act=("relu" if i < len(ws) - 1 else last_act))
+        refs.append(y)
+    outs = ops.mlp_heads(heads)
+    for o, r in zip(outs, refs):
+        assert torch.equal(o, r), float((o.float() - r.float()).abs().max())
