@@ -36,63 +36,75 @@ struct HeadsArgs {
 typedef __attribute__((ext_vector_type(8))) __bf16 hd_bf16x8;
 typedef __attribute__((ext_vector_type(4))) float hd_f32x4;
 
-__global__ __launch_bounds__(256) void mlp_heads_kernel(HeadsArgs a) {
+// 16 waves: wave w owns output columns 16w .. 16w + 15 of every layer (widths <= 256), and loads ALL
+// of its weight fragments for all layers at kernel start -- they do not depend on the activations --
+// so the head costs one global round trip plus three LDS exchanges (the first form, 4 waves looping
+// over tiles with a load before every MFMA, was slower than the 6 GEMM launches it replaced)
+__global__ __launch_bounds__(1024) void mlp_heads_kernel(HeadsArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 act[2][16 * HD_LD];
   const HeadDesc& d = a.h[blockIdx.y];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r0 = blockIdx.x * 16;
+  const int nl = d.nl;
+  const int n = 16 * w + (lane & 15);
+  hd_bf16x8 bfr[HD_MAXL][HD_MAXK / 32];
+#pragma unroll
+  for (int l = 0; l < HD_MAXL; ++l) {
+    const int K = l < nl ? d.dims[l] : 0, N = l < nl ? d.dims[l + 1] : 0;
+    const bf16* W = d.w[l];
+#pragma unroll
+    for (int ks = 0; ks < HD_MAXK / 32; ++ks) {
+      const int k = 32 * ks + 8 * (lane >> 4);
+      bfr[l][ks] = (n < N && k < K) ? *(const hd_bf16x8*)(W + (int64_t)n * K + k) : hd_bf16x8{};
+    }
+  }
   // layer-0 input rows (rows past M and columns past K zero), 8 columns per thread
   {
     const int K0 = d.dims[0];
-    for (int i = tid; i < 16 * (HD_MAXK / 8); i += 256) {
-      const int r = i / (HD_MAXK / 8), c = (i % (HD_MAXK / 8)) * 8;
+    if (tid < 16 * (HD_MAXK / 8)) {
+      const int r = tid / (HD_MAXK / 8), c = (tid % (HD_MAXK / 8)) * 8;
       uint4 v = make_uint4(0, 0, 0, 0);
       if (r0 + r < a.M && c < K0) v = *(const uint4*)(d.x + (int64_t)(r0 + r) * d.ldx + c);
       *(uint4*)(act[0] + r * HD_LD + c) = v;
     }
   }
   __syncthreads();
-  int cur = 0;
-  for (int l = 0; l < d.nl; ++l) {
-    const int K = d.dims[l], N = d.dims[l + 1];
-    const bool last = l == d.nl - 1;
-    const int act_fn = last ? d.act_last : S2H_ACT_RELU;
-    const bf16* W = d.w[l];
-    const float* bias = d.b[l];
-    const bf16* in = act[cur];
-    bf16* out = act[cur ^ 1];
-    const int ntiles = (N + 15) / 16;
-    for (int t = w; t < ntiles; t += 4) {
-      const int n = 16 * t + (lane & 15);
-      hd_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-      for (int ks = 0; ks < (K + 31) / 32; ++ks) {
-        const int k = 32 * ks + 8 * (lane >> 4);
-        const hd_bf16x8 af = *(const hd_bf16x8*)(in + (lane & 15) * HD_LD + k);
-        hd_bf16x8 bf = {};
-        if (n < N && k < K) bf = *(const hd_bf16x8*)(W + (int64_t)n * K + k);
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc, 0, 0, 0);
-      }
-      // lane holds rows 4 (lane >> 4) + e of column n
-      const float bn = (bias != nullptr && n < N) ? bias[n] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int r = 4 * (lane >> 4) + e;
-        const bf16 v = (bf16)apply_act(acc[e] + bn, act_fn);
-        if (n < N) {
-          out[r * HD_LD + n] = v;
-          if (last && r0 + r < a.M) d.y[(int64_t)(r0 + r) * d.ldy + n] = v;
+  for (int l = 0; l < HD_MAXL; ++l) {
+    if (l < nl) {
+      const int K = d.dims[l], N = d.dims[l + 1];
+      const bool last = l == nl - 1;
+      const int act_fn = last ? d.act_last : S2H_ACT_RELU;
+      const bf16* in = act[l & 1];
+      bf16* out = act[(l & 1) ^ 1];
+      if (16 * w < N) {
+        hd_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < HD_MAXK / 32; ++ks) {
+          if (32 * ks < K) {
+            const hd_bf16x8 af = *(const hd_bf16x8*)(in + (lane & 15) * HD_LD + 32 * ks + 8 * (lane >> 4));
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bfr[l][ks], acc, 0, 0, 0);
+          }
+        }
+        // lane holds rows 4 (lane >> 4) + e of column n
+        const float bn = (d.b[l] != nullptr && n < N) ? d.b[l][n] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = 4 * (lane >> 4) + e;
+          const bf16 v = (bf16)apply_act(acc[e] + bn, act_fn);
+          if (n < N) {
+            out[r * HD_LD + n] = v;
+            if (last && r0 + r < a.M) d.y[(int64_t)(r0 + r) * d.ldy + n] = v;
+          }
         }
       }
-    }
-    // columns [N, round up to 32) of the next input must read as zero
-    if (!last) {
-      for (int i = tid; i < 16 * 32; i += 256) {
-        const int r = i / 32, c = N + i % 32;
-        if (c < HD_MAXK + 8 && c < ((N + 31) / 32) * 32) out[r * HD_LD + c] = (bf16)0.f;
+      // columns [N, N rounded up to 32) of the next layer's input read as zero
+      if (!last && tid < 16 * 32) {
+        const int r = tid / 32, c = N + tid % 32;
+        if (c < ((N + 31) / 32) * 32) out[r * HD_LD + c] = (bf16)0.f;
       }
+      __syncthreads();
     }
-    __syncthreads();
-    cur ^= 1;
   }
 }
 
@@ -130,6 +142,6 @@ extern "C" int s2h_mlp_heads(int nheads, int M, const void* const* x, const int6
       if (!d.w[l] || ((uintptr_t)d.w[l] & 15)) return (int)hipErrorInvalidValue;
     }
   }
-  hipLaunchKernelGGL(mlp_heads_kernel, dim3((M + 15) / 16, nheads), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(mlp_heads_kernel, dim3((M + 15) / 16, nheads), dim3(1024), 0, st, a);
   return (int)hipGetLastError();
 }
