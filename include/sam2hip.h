@@ -306,7 +306,10 @@ int s2h_ln_wgrad_finalize(int nb, int C, const float* part, float* dgamma, float
  * obj_ptr_proj): 6 launches of 13 rows per frame -> 1.  Argument arrays are host memory. */
 int s2h_mlp_heads(int nheads, int M, const void* const* x, const int64_t* ldx, const void* const* w,
                   const float* const* b, const int* dims, const int* nl, const int* act_last, void* const* y,
-                  const int64_t* ldy, hipStream_t st);
+                  const int64_t* ldy, void* const* hid, void* const* pre, hipStream_t st);
+/* (hid[2h + l], optional: layer l's ReLU output [M, dims[4h+l+1]] for l < nl - 1; pre[h], optional:
+ * the last layer's pre-activation -- saved for the backward of trained heads: the mask decoder's
+ * hypernetwork MLP and IoU head, mask_decoder.py:227-233, in the frame-batched tape) */
 
 /* ---------------------------------------------------------------- normalisation
  * Row LayerNorm over C (<= 1280) with an optional fused pre-add:

@@ -26,6 +26,8 @@ struct HeadDesc {
   int act_last;  // S2HAct of the last layer (the hidden layers are ReLU)
   bf16* y;       // [M, dims[nl]], row stride ldy
   int64_t ldy;
+  bf16* hid[HD_MAXL - 1];  // optional [M, dims[l + 1]] hidden outputs (after ReLU), contiguous rows
+  bf16* pre;               // optional [M, dims[nl]] last layer's pre-activation, contiguous rows
 };
 
 struct HeadsArgs {
@@ -88,13 +90,22 @@ __global__ __launch_bounds__(1024) void mlp_heads_kernel(HeadsArgs a) {
         }
         // lane holds rows 4 (lane >> 4) + e of column n
         const float bn = (d.b[l] != nullptr && n < N) ? d.b[l][n] : 0.f;
+        bf16* hid = last ? nullptr : d.hid[l];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int r = 4 * (lane >> 4) + e;
-          const bf16 v = (bf16)apply_act(acc[e] + bn, act_fn);
+          const float pv = acc[e] + bn;
+          const bf16 v = (bf16)apply_act(pv, act_fn);
           if (n < N) {
             out[r * HD_LD + n] = v;
-            if (last && r0 + r < a.M) d.y[(int64_t)(r0 + r) * d.ldy + n] = v;
+            if (r0 + r < a.M) {
+              if (last) {
+                d.y[(int64_t)(r0 + r) * d.ldy + n] = v;
+                if (d.pre) d.pre[(int64_t)(r0 + r) * N + n] = (bf16)pv;
+              } else if (hid) {
+                hid[(int64_t)(r0 + r) * N + n] = v;
+              }
+            }
           }
         }
       }
@@ -114,9 +125,13 @@ __global__ __launch_bounds__(1024) void mlp_heads_kernel(HeadsArgs a) {
 // biases b[h*3 + l] (fp32 or null), nl[h] layers (<= 3; hidden layers ReLU, the last act_last[h]),
 // y [M, dims[h*4 + nl]] (row stride ldy[h]); bf16; every width <= 256 and a multiple of 8 (the last
 // may be any width <= 256); 16-B aligned rows.
+// hid (optional, may be NULL): hid[2h + l] receives layer l's output (after ReLU, [M, dims[4h+l+1]]
+// contiguous) for l < nl - 1; pre (optional): pre[h] the last layer's pre-activation [M, dims[4h+nl]] --
+// what the backward of a trained head reads (tape op frametape.mlp_heads)
 extern "C" int s2h_mlp_heads(int nheads, int M, const void* const* x, const int64_t* ldx, const void* const* w,
                              const float* const* b, const int* dims, const int* nl, const int* act_last,
-                             void* const* y, const int64_t* ldy, hipStream_t st) {
+                             void* const* y, const int64_t* ldy, void* const* hid, void* const* pre,
+                             hipStream_t st) {
   if (M <= 0 || nheads <= 0) return 0;
   if (nheads > HD_MAXH) return (int)hipErrorInvalidValue;
   HeadsArgs a = {};
@@ -136,6 +151,8 @@ extern "C" int s2h_mlp_heads(int nheads, int M, const void* const* x, const int6
       d.dims[l] = dims[h * (HD_MAXL + 1) + l];
       if (d.dims[l] <= 0 || d.dims[l] > HD_MAXK || (l < d.nl && d.dims[l] % 8)) return (int)hipErrorInvalidValue;
     }
+    for (int l = 0; l < HD_MAXL - 1; ++l) d.hid[l] = hid ? (bf16*)hid[h * (HD_MAXL - 1) + l] : nullptr;
+    d.pre = pre ? (bf16*)pre[h] : nullptr;
     for (int l = 0; l < d.nl; ++l) {
       d.w[l] = (const bf16*)w[h * HD_MAXL + l];
       d.b[l] = b[h * HD_MAXL + l];

@@ -35,7 +35,7 @@ SIGNATURES = {
     "s2h_linear_dgrad_ln_bwd_ws_bytes": [I, I],
     "s2h_linear_dgrad_ln_bwd": [I, I, I, P, L, P, L, F, P, L, P, P, P, P, L, P, L, P, P, P, P],
     "s2h_ln_wgrad_finalize": [I, I, P, P, P, P],
-    "s2h_mlp_heads": [I, I, P, P, P, P, P, P, P, P, P, P],
+    "s2h_mlp_heads": [I, I, P, P, P, P, P, P, P, P, P, P, P, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_gemm_config": [I],

@@ -548,6 +548,62 @@ def linear_add_ln(tape: FrameTape, inp, mod, x, norm, eps, drop_p):
     return t, xsum
 
 
+def mlp_heads(tape: FrameTape, pairs):
+    """per-object MLP heads [(MLP, x)] as ONE op and one launch (ops.mlp_heads): outputs y per head;
+    saved per head every hidden layer's ReLU output and, for a sigmoid head, the last pre-activation.
+    The backward is the per-layer chain the separate linear ops would run (sigmoid' from the saved
+    pre-activation, weight gradient, dgrad with the previous layer's ReLU' in its epilogue)"""
+    xs = [x if x.is_contiguous() else x.contiguous() for _, x in pairs]
+    mods = [m for m, _ in pairs]
+    op, first = tape._begin("mlp_heads", xs, _mlp_heads_bw, {"mods": mods})
+    if first and any(tape.vid(x) is None for x in xs):
+        raise RuntimeError("tape mlp_heads: inputs must be recorded values or declared inputs")
+    rows = xs[0].shape[0]
+    vids, ys, hidden, pres, heads = [], [], [], [], []
+    for hi, (m, x) in enumerate(zip(mods, xs)):
+        layers = list(m.layers)
+        vid, y = tape._out(hi, (rows, layers[-1].out_features), x.dtype)
+        vids.append(vid)
+        ys.append(y)
+        hidden.append([tape._aux(f"h{hi}_{l}", (rows, layers[l].out_features), x.dtype) for l in range(len(layers) - 1)])
+        pres.append(tape._aux(f"pre{hi}", (rows, layers[-1].out_features), x.dtype) if m.sigmoid_output else None)
+        heads.append((x, [lin.compute_weight() for lin in layers], [lin.compute_bias() for lin in layers],
+                      "sigmoid" if m.sigmoid_output else None))
+    ops.mlp_heads(heads, outs=ys, hidden=hidden, pre=pres)
+    params = [p for m in mods for lin in m.layers for p in (lin.weight, lin.bias)]
+    tape._finish(op, vids, tape._req(op, params))
+    return ys
+
+
+def _mlp_heads_bw(tape, op, gys):
+    dxs = []
+    for hi, (m, gy) in enumerate(zip(op.attrs["mods"], gys)):
+        if gy is None:
+            dxs.append(None)
+            continue
+        layers = list(m.layers)
+        L = len(layers)
+        g = gy.view(-1, layers[-1].out_features)
+        if m.sigmoid_output:
+            g = ops.act_bwd(_flat(tape.stores[("aux", op.idx, f"pre{hi}")], layers[-1].out_features), g, "sigmoid")
+        hs = [_flat(tape.stores[("aux", op.idx, f"h{hi}_{l}")], layers[l].out_features) for l in range(L - 1)]
+        dx = None
+        for l in range(L - 1, -1, -1):
+            mod = layers[l]
+            inp = _flat(tape.st(op.ins[hi]), layers[0].in_features) if l == 0 else hs[l - 1]
+            gw, gb = mod.grad_views()
+            if gw is not None:
+                ops.linear_wgrad(g, inp, gw.view(gw.shape[0], -1), db=gb)
+            elif gb is not None:
+                ops.colsum(g, gb)
+            if l > 0:  # the previous layer's ReLU' (from its output) in this dgrad's epilogue
+                g = _fp8.linear_dgrad(g, mod, pre=hs[l - 1], act="relu", alpha=1.0)
+            elif op.needs[hi]:
+                dx = _fp8.linear_dgrad(g, mod).view(-1)
+        dxs.append(dx)
+    return dxs
+
+
 # ---------------------------------------------------------------- layer norms
 def layer_norm(tape: FrameTape, x, mod, eps, add=None):
     """LN(x) or (LN(x + add), x + add)"""

@@ -219,16 +219,32 @@ def _head_ok(m, x):
     return True
 
 
+def _heads_fusable(pairs):
+    import os
+    return (0 < len(pairs) <= 4 and os.environ.get("S2H_MLP_HEADS", "1") != "0"
+            and len({x.shape[0] for _, x in pairs}) == 1 and all(_head_ok(m, x) for m, x in pairs))
+
+
+def mlp_heads(pairs):
+    """[(MLP module, x [M, K] rows)] -> [module(x)] for the decoder's trained per-object heads (the
+    hypernetwork MLP of mask token 0 and the IoU head, mask_decoder.py:227-233): in the frame tape one
+    launch for all of them with the hidden activations saved for the frame-batched backward
+    (frametape.mlp_heads); without autograd the no-grad launch; else each head's own forward"""
+    if not torch.is_grad_enabled():
+        return mlp_heads_nograd(pairs)
+    T = _ft.active()
+    if T is not None and _heads_fusable(pairs):
+        return _ft.mlp_heads(T, pairs)
+    return [m(x) for m, x in pairs]
+
+
 def mlp_heads_nograd(pairs):
     """[(MLP module, x [M, K] rows)] -> [module(x)] for heads whose outputs need no gradient (the object
     score head, mask_decoder.py:234-238, and the object-pointer projection, sam2_base.py:296-305): one
     launch for all of them (s2h_mlp_heads: per head the layers chained in LDS, bit-identical to the
     per-layer GEMMs) when every head is a bf16 ReLU MLP of <= 3 layers no wider than 256; else each
     head's own forward.  S2H_MLP_HEADS=0 keeps the per-layer GEMMs (A/B)."""
-    import os
-    ok = (0 < len(pairs) <= 4 and os.environ.get("S2H_MLP_HEADS", "1") != "0"
-          and len({x.shape[0] for _, x in pairs}) == 1 and all(_head_ok(m, x) for m, x in pairs))
-    if not ok:
+    if not _heads_fusable(pairs):
         return [m(x) for m, x in pairs]
     return ops.mlp_heads([(x, [lin.compute_weight() for lin in m.layers], [lin.compute_bias() for lin in m.layers],
                            "sigmoid" if m.sigmoid_output else None) for m, x in pairs])

@@ -248,16 +248,27 @@ def linear_dgrad_ln_bwd(dy, w, x, gamma, mean, rstd, dres=None, dgamma=None, dbe
     return dx
 
 
-def mlp_heads(heads):
-    """no-grad MLP heads in one launch (s2h_mlp_heads): heads = [(x [M, K0] bf16 rows, [W_l] bf16
-    [N_l, K_l], [b_l fp32 or None], act_last)] with the same M; ReLU between layers.  Returns [y]"""
+def mlp_heads(heads, outs=None, hidden=None, pre=None):
+    """MLP heads in one launch (s2h_mlp_heads): heads = [(x [M, K0] bf16 rows, [W_l] bf16 [N_l, K_l],
+    [b_l fp32 or None], act_last)] with the same M; ReLU between layers.  outs: optional [y] to write;
+    hidden: optional [[h_l]] per head (each hidden layer's ReLU output, contiguous); pre: optional
+    [pre-activation of the last layer or None] per head.  Returns [y]"""
     import ctypes
     n = len(heads)
     M = heads[0][0].shape[0]
     xs, lds, ws, bs, dims, nls, acts, ys, ldys = [], [], [], [], [], [], [], [], []
-    for x, wl, bl, act_last in heads:
+    hids, pres = [], []
+    for hi, (x, wl, bl, act_last) in enumerate(heads):
         assert x.dtype == torch.bfloat16 and x.shape[0] == M and x.stride(1) == 1 and len(wl) <= 3
-        y = torch.empty(M, wl[-1].shape[0], device=x.device, dtype=x.dtype)
+        y = outs[hi] if outs is not None else torch.empty(M, wl[-1].shape[0], device=x.device, dtype=x.dtype)
+        assert y.shape == (M, wl[-1].shape[0]) and y.stride(1) == 1
+        hl = hidden[hi] if hidden is not None else []
+        for h, w in zip(hl, wl[:-1]):
+            assert h.is_contiguous() and h.shape == (M, w.shape[0])
+        hids += [ptr(h) for h in hl] + [None] * (2 - len(hl))
+        pl = pre[hi] if pre is not None else None
+        assert pl is None or (pl.is_contiguous() and pl.shape == y.shape)
+        pres.append(ptr(pl))
         _dev(x, y, *wl, *[b for b in bl if b is not None])
         xs.append(ptr(x))
         lds.append(x.stride(0))
@@ -274,7 +285,8 @@ def mlp_heads(heads):
     P = ctypes.c_void_p
     call("s2h_mlp_heads", n, M, (P * n)(*xs), (ctypes.c_int64 * n)(*lds), (P * (3 * n))(*ws),
          (P * (3 * n))(*bs), (ctypes.c_int * (4 * n))(*dims), (ctypes.c_int * n)(*nls), (ctypes.c_int * n)(*acts),
-         (P * n)(*[ptr(y) for y in ys]), (ctypes.c_int64 * n)(*ldys), stream())
+         (P * n)(*[ptr(y) for y in ys]), (ctypes.c_int64 * n)(*ldys),
+         (P * (2 * n))(*hids) if hidden is not None else None, (P * n)(*pres) if pre is not None else None, stream())
     return ys
 
 

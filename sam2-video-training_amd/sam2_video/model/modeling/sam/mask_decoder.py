@@ -106,9 +106,10 @@ class MaskDecoder(nn.Module):
         u = FN.act(ln1(u), "gelu")
         u = conv_transpose2x2(u, dc2, add=feat_s0)
         u = FN.act(u, "gelu")
-        hyper0 = self.output_hypernetworks_mlps[0](mask_token0)
+        # the hypernetwork MLP of mask token 0 and the IoU head: one launch (FN.mlp_heads)
+        hyper0, iou_pred = FN.mlp_heads([(self.output_hypernetworks_mlps[0], mask_token0),
+                                         (self.iou_prediction_head, iou_token_out)])
         masks = hyper_mask(hyper0, u.view(O, -1, C // 8))
-        iou_pred = self.iou_prediction_head(iou_token_out)
         iou0 = FN.cast(FN.select_token(iou_pred.unsqueeze(-1), 0), torch.float32)
         if defer_score:  # the caller runs the object-score head with its other no-grad heads (one launch)
             return masks, iou0, mask_token0, hs[:, 0].detach()

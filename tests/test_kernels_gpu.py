@@ -1094,15 +1094,32 @@ def test_mlp_heads_bit_identical(M):
     hs = torch.randn(M, 9, 256, device=DEV).to(bf)
     specs = [(hs[:, 0], [256, 256, 256, 1], None), (hs[:, 2].contiguous(), [256, 256, 256, 256], None),
              (hs[:, 3].contiguous(), [256, 256, 256, 32], "sigmoid"), (hs[:, 1].contiguous(), [256, 128, 4], None)]
-    heads, refs = [], []
+    heads, refs, rhid, rpre, hid, pre = [], [], [], [], [], []
     for x, dims, last_act in specs:
         ws = [(torch.randn(dims[i + 1], dims[i], device=DEV) / dims[i] ** 0.5).to(bf) for i in range(len(dims) - 1)]
         bs = [torch.randn(dims[i + 1], device=DEV) * 0.1 for i in range(len(dims) - 1)]
         heads.append((x, ws, bs, last_act))
         y = x.contiguous()
+        hl = []
         for i, (w, b) in enumerate(zip(ws, bs)):
-            y = ops.linear(y, w, b, act=("relu" if i < len(ws) - 1 else last_act))
+            last = i == len(ws) - 1
+            p = torch.empty(M, w.shape[0], device=DEV, dtype=bf) if last and last_act else None
+            y = ops.linear(y, w, b, act=("relu" if not last else last_act), pre=p)
+            if not last:
+                hl.append(y)
         refs.append(y)
+        rhid.append(hl)
+        rpre.append(p)
+        hid.append([torch.empty_like(h) for h in hl])
+        pre.append(torch.empty_like(p) if p is not None else None)
     outs = ops.mlp_heads(heads)
     for o, r in zip(outs, refs):
         assert torch.equal(o, r), float((o.float() - r.float()).abs().max())
+    # with the saved hidden activations / last pre-activation (the trained heads' tape op)
+    outs = ops.mlp_heads(heads, hidden=hid, pre=pre)
+    for o, r, h, rh, p, rp in zip(outs, refs, hid, rhid, pre, rpre):
+        assert torch.equal(o, r)
+        for a, b in zip(h, rh):
+            assert torch.equal(a, b)
+        if rp is not None:
+            assert torch.equal(p, rp)
