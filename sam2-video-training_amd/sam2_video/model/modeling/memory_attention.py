@@ -12,11 +12,18 @@ LN3 -> linear1 (ReLU + dropout in the epilogue) -> linear2 (+dropout, +res).
 from __future__ import annotations
 
 import copy
+import os
 
 from torch import nn
 
 from ...kernels import functional as FN
 from .layers import FusedLinear, LayerNorm, Linear
+
+
+def shared_qkv_enabled():
+    """layer 0's norm1 + q/k/v GEMM once per frame instead of once per object (default on;
+    S2H_MA_SHARED_QKV=0 restores the per-object form for A/B)"""
+    return os.environ.get("S2H_MA_SHARED_QKV", "1") != "0"
 
 
 class MemoryAttentionLayer(nn.Module):
@@ -55,6 +62,9 @@ class MemoryAttentionLayer(nn.Module):
 
     def sublayers(self, x, t, mem_k, mem_v, num_k_exclude_rope, next_norm):
         """The layer on the residual stream x with t = norm1(x) given; returns (x', next_norm(x')).
+        t may hold ONE object's rows ([1, L, C]) when every object's stream is the same (layer 0: the
+        current frame's features broadcast to the objects) -- then the q/k/v projection runs once and
+        its output is broadcast (its gradient summed over the objects) instead of running per object.
         Every residual add is fused with the LayerNorm that reads its result, and (bf16) with the
         projection that produces it: FN.linear_add_layer_norm runs out_proj / the folded
         cross-attention output / linear2, dropout, the residual add and the next LayerNorm as ONE
@@ -70,10 +80,14 @@ class MemoryAttentionLayer(nn.Module):
             # full-row GEMM with the LayerNorm in its epilogue (FN.linear_add_layer_norm)
             cos, sin = sa.tables(L, t.device)
             qkv = self._fused_qkv(t, rope=(cos, sin, L, L, L, 2 * C, C))
+            if qkv.shape[0] != x.shape[0]:
+                qkv = FN.expand_batch(qkv, x.shape[0])
             o = FN.qkv_attention(qkv.view(qkv.shape[0], L, 3, 1, C), p_drop=sa._p())
             t, x = FN.linear_add_layer_norm(o.reshape(qkv.shape[0], L, C), sa.out_proj, x, self.norm2,
                                             self.norm2.eps, drop_p=p)
         else:
+            if t.shape[0] != x.shape[0]:
+                t = FN.expand_batch(t, x.shape[0])
             q = sa.proj_q(t, L)
             k = sa.proj_k(t, L)
             y = sa.attend(q, k, sa.v_proj(t), out_drop=p)
@@ -133,9 +147,11 @@ class MemoryAttention(nn.Module):
         memory [O, M, 64] (detached bank), memory_pos_table [M, 64] (shared by objects)
         -> [O, L, C]"""
         x = FN.add(curr, curr_pos, beta=0.1) if self.pos_enc_at_input else curr
-        x = FN.expand_batch(x.unsqueeze(0), num_objects)
+        x1 = x.unsqueeze(0)
+        x = FN.expand_batch(x1, num_objects)
         mem_k = FN.add_bcast(memory, memory_pos_table)
-        t = self.layers[0].norm1(x)
+        # layer 0's LN1 (and q/k/v projection, MemoryAttentionLayer.sublayers) on the one shared frame
+        t = self.layers[0].norm1(x1 if shared_qkv_enabled() else x)
         for i, layer in enumerate(self.layers):
             nxt = self.layers[i + 1].norm1 if i + 1 < len(self.layers) else self.norm
             x, t = layer.sublayers(x, t, mem_k, memory, num_obj_ptr_tokens, nxt)

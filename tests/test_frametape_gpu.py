@@ -249,3 +249,42 @@ def test_wgrad_side_stream_equals_one_stream(monkeypatch):
     bad = [(n, float((gb[n] - ga[n]).abs().max())) for n in ga
            if float((gb[n].double() - ga[n].double()).abs().max()) > 1e-4 * float(ga[n].abs().max()) + 1e-6 * gmax]
     assert not bad, bad[:8]
+
+
+def test_ma_shared_qkv_equals_per_object(monkeypatch):
+    """memory attention layer 0 with its norm1 + q/k/v GEMM once per frame and the result broadcast to
+    the objects (S2H_MA_SHARED_QKV, default on: MemoryAttention.forward / MemoryAttentionLayer.sublayers;
+    the q/k/v gradient summed over the objects before ONE dgrad / wgrad) against the per-object form,
+    bf16 B+ 256^2 frame-batched step: the same forward values (LayerNorm and GEMM rows are
+    row-independent), gradients within the one bf16 rounding of the object-summed dL/dqkv"""
+    from sam2_video.kernels import frametape
+    calls = []
+    orig = frametape.expand_batch
+
+    def counted(*a, **k):
+        calls.append(a[1].shape)
+        return orig(*a, **k)
+    monkeypatch.setattr(frametape, "expand_batch", counted)
+    g = load_golden("bplus256_point_all")
+    size, prompt, trainable = CASES["bplus256_point_all"]
+    out, ncalls = [], []
+    for on in ("0", "1"):
+        monkeypatch.setenv("S2H_MA_SHARED_QKV", on)
+        calls.clear()
+        m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype="bf16", seed=int(g["meta/seed"]))
+        m.frame_batched = True
+        stages, merged, losses, _ = run_step(m, golden_batch(g).to("cuda"))
+        out.append(([s["pred_masks"].detach().float().cpu() for s in stages], grads_by_name(m)))
+        ncalls.append(len(calls))
+        del m
+    # one more broadcast (of the packed q/k/v) per memory-conditioned frame
+    assert ncalls[1] > ncalls[0], ncalls
+    (la, ga), (lb, gb) = out
+    for a, b in zip(la, lb):
+        assert float((a - b).abs().max()) <= 1e-2 * float(a.abs().max()) + 1e-3
+    num = sum(float((gb[n].double() - ga[n].double()).norm() ** 2) for n in ga)
+    den = sum(float(ga[n].double().norm() ** 2) for n in ga)
+    rel = math.sqrt(num / den)
+    print(f"S2H_MA_SHARED_QKV=1: {ncalls} broadcasts, masks equal: {all(torch.equal(a, b) for a, b in zip(la, lb))}, "
+          f"global relative gradient difference {rel:.3e}")
+    assert rel <= 2e-2, rel
