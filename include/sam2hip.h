@@ -115,6 +115,9 @@ int s2h_gemm_w41(int mode);
  * on the A-in-registers tiling (1: on, the default; 0: off); results are bit-identical.  Returns the
  * previous mode. */
 int s2h_gemm_areg(int mode);
+/* flash forward: 16-query sets per wave (1 or 2; bits 0-3 V-fold launches, 4-7 plain launches with
+   head dim <= 128); returns the previous mode, < 0 only queries.  Same results either way. */
+int s2h_flash_fwd_sets(int mode);
 
 /* Weight and bias gradient of a Linear layer (autograd of nn.Linear, e.g. hieradet.py:56-81,
  * memory_attention.py:58-99): dw[N, K] (+)= dy[rows, N]^T x[rows, K] (dw row stride lddw),

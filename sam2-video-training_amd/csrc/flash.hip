@@ -59,9 +59,12 @@ enum { FDROP_NONE = 0, FDROP_HASH = 1, FDROP_BITS = 2 };
 // partial-row scalars in the key-split workspace: (m, l) or, V-fold, (m, l, rowsum(D), -)
 #define FL_MLW(FOLD) ((FOLD) ? 4 : 2)
 
-template <int DP, int DROP, int DV = DP>
+// QS: 16-query sets per wave (QS = 2: every K / V fragment read from LDS feeds two MFMAs -- the
+// kernel's LDS read traffic per query halves; the workgroup covers 128 QS query rows)
+template <int DP, int DROP, int DV = DP, int QS = 1>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
   constexpr bool FOLD = DV != DP;
+  constexpr int QB = FL_QB * QS;
   const uint32_t hkey = DROP != FDROP_NONE ? s2h_hash_key(s2h_seed(a.seed, a.seed_off)) : 0u;
   const uint32_t t16 = a.thresh >> 16;
   using C = FlashCfg<DP>;
@@ -76,7 +79,9 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   if (wi.y >= a.BH) return;  // grid padding
   const int bh = wi.y, b = bh / a.H, h = bh % a.H;
   const int split = wi.z;
-  const int q = wi.x * FL_QB + w * 16 + ql;  // this lane's query row
+  int q[QS];  // this lane's query row in each set
+#pragma unroll
+  for (int u = 0; u < QS; ++u) q[u] = wi.x * QB + (w * QS + u) * 16 + ql;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
   const bf16* K = a.k + b * a.skb + h * a.skh;
   const bf16* V = a.v + b * a.svb + h * a.svh;
@@ -90,25 +95,40 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     dma_tile_pad<DV, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, a.Lk, w, lane, FOLD ? DV : a.D);
   }
   const int npw = I::pieces(w), npv = IV::pieces(w);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  PadDma<DP> kdma;
+  PadDma<DV> vdma;
+  kdma.init(a.skl, w, lane, a.D);
+  vdma.init(a.svl, w, lane, FOLD ? DV : a.D);
 
   // Q^T fragments (B operand of K Q^T): lane -> query q, d = 32t + 8g + j
-  bf16x8 qf[C::NT];
+  bf16x8 qf[QS][C::NT];
 #pragma unroll
-  for (int t = 0; t < C::NT; ++t) {
-    if (q < a.Lq && 32 * t + 8 * g < a.D) qf[t] = *(const bf16x8*)(Q + (int64_t)q * a.sql + 32 * t + 8 * g);
-    else qf[t] = bf16x8{};
-  }
+  for (int u = 0; u < QS; ++u)
+#pragma unroll
+    for (int t = 0; t < C::NT; ++t) {
+      if (q[u] < a.Lq && 32 * t + 8 * g < a.D)
+        qf[u][t] = *(const bf16x8*)(Q + (int64_t)q[u] * a.sql + 32 * t + 8 * g);
+      else
+        qf[u][t] = bf16x8{};
+    }
   // compiler-visible vmcnt(0): retires the Q loads in the compiler's own bookkeeping too;
   // otherwise it keeps them "maybe pending" around the key loop and waits vmcnt(0) before
   // the first MFMA of every tile -- which also drains the (asm, invisible) K/V prefetch
   __builtin_amdgcn_s_waitcnt(0xF70);  // vmcnt(0) expcnt(7) lgkmcnt(15)
 
-  f32x4 o[NDV];  // O^T: row d = 16*db + 4g + r, column q
+  f32x4 o[QS][NDV];  // O^T: row d = 16*db + 4g + r, column q
 #pragma unroll
-  for (int d = 0; d < NDV; ++d) o[d] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m = -INFINITY, l = 0.f;
-  float rd = 0.f;  // V-fold with dropout: running rowsum of the dropped probabilities (scaled like l)
-  const uint64_t drow = a.idx0 + ((uint64_t)bh * a.Lq + q) * (uint64_t)a.Lk;
+  for (int u = 0; u < QS; ++u)
+#pragma unroll
+    for (int d = 0; d < NDV; ++d) o[u][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[QS], l[QS], rd[QS];  // rd: V-fold with dropout, running rowsum of the dropped probabilities
+  uint64_t drow[QS];
+#pragma unroll
+  for (int u = 0; u < QS; ++u) {
+    m[u] = -INFINITY, l[u] = 0.f, rd[u] = 0.f;
+    drow[u] = a.idx0 + ((uint64_t)bh * a.Lq + q[u]) * (uint64_t)a.Lk;
+  }
   const int qq = (lane >> 2) & 3, pp = lane & 3;  // transposing-read lane roles
 
   for (int it = 0; it < nt; ++it) {
@@ -118,8 +138,13 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     char* Vb = Kb + I::TILEB;
     if (it + 1 < nt) {
       char* Kn = smem + ((it + 1) & 1) * STG;
-      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane, a.D);
-      dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane, FOLD ? DV : a.D);
+      if (k0 + 2 * C::KT <= a.Lk) {  // whole next tile: precomputed offsets on an SGPR row base
+        kdma.issue(Kn, K, a.skl, k0 + C::KT, wu);
+        vdma.issue(Kn + I::TILEB, V, a.svl, k0 + C::KT, wu);
+      } else {
+        dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane, a.D);
+        dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane, FOLD ? DV : a.D);
+      }
       // this wave's pieces of tile `it` have landed once all but the npw + npv just issued retired
       wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
     } else {
@@ -129,117 +154,127 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     asm volatile("" ::: "memory");
 
     // ---- S^T = K Q^T: four 16-key blocks, key = 16*kb + 4g + r on the accumulator row
-    f32x4 s[4];
+    f32x4 s[QS][4];
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-      s[kb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < QS; ++u) s[u][kb] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int row = kb * 16 + ql;
 #pragma unroll
       for (int t = 0; t < C::NT; ++t) {
         const bf16x8 kf = *(const bf16x8*)(Kb + row * I::ROWB + 16 * (4 * t + g));
-        s[kb] = mfma16(kf, qf[t], s[kb]);
+#pragma unroll
+        for (int u = 0; u < QS; ++u) s[u][kb] = mfma16(kf, qf[u][t], s[u][kb]);
       }
     }
-    sched_reads_ahead<4 * C::NT, 4, 1>();  // fragment reads 4 ahead of their MFMAs
+    sched_reads_ahead<4 * C::NT, 4, 1, QS>();  // fragment reads 4 ahead of their MFMAs
     __builtin_amdgcn_sched_barrier(0);
-    // ---- online softmax (lane-local query row; keys spread over the 4 lane groups)
-    float mx = -INFINITY;
-    if (k0 + C::KT <= a.Lk) {  // full tile (wave-uniform): no key mask
+    // ---- online softmax per query set (lane-local query row; keys spread over the 4 lane groups)
+    bf16x8 pb[QS][2];
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+    for (int u = 0; u < QS; ++u) {
+      float mx = -INFINITY;
+      if (k0 + C::KT <= a.Lk) {  // full tile (wave-uniform): no key mask
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          s[kb][r] *= a.sl2;
-          mx = fmaxf(mx, s[kb][r]);
-        }
-    } else {
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = k0 + kb * 16 + 4 * g + r;
-          const float x = key < a.Lk ? s[kb][r] * a.sl2 : -INFINITY;
-          s[kb][r] = x;
-          mx = fmaxf(mx, x);
-        }
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    // deferred rescale: keep the running reference max until a row's max grows by more
-    // than 2^8 (p <= 256 stays exact enough in bf16 / fp32)
-    const float mn = (mx > m + 8.f) ? mx : m;
-    const float alpha = (m == -INFINITY) ? (mn == -INFINITY ? 1.f : 0.f) : __builtin_amdgcn_exp2f(m - mn);
-    const float mref = (mn == -INFINITY) ? 0.f : mn;
-    m = mn;
-    float rs = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        s[kb][r] = __builtin_amdgcn_exp2f(s[kb][r] - mref);
-        rs += s[kb][r];
-      }
-    float rdt = 0.f;  // V-fold: this tile's dropped-probability sum (lane part)
-    if constexpr (DROP != FDROP_NONE) {
-      uint32_t kbits[2] = {0u, 0u};  // this lane's keep flags: bit 16kb + 4g + e of the tile's 64 keys
-      // the 4 keys of a (kb) block are consecutive: two hashes per block when pairs align
-#pragma unroll
-      for (int kb = 0; kb < 4; ++kb) {
-        const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
-        bool kp[4];
-        if ((e0 & 1) == 0) {
-          const uint64_t pr = e0 >> 1;
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            const uint32_t hsh = s2h_hash_mixed(hkey, (uint32_t)(pr + j) + (uint32_t)((pr + j) >> 32) * 0x9E3779B9u);
-            kp[2 * j] = (hsh & 0xFFFFu) >= t16;
-            kp[2 * j + 1] = (hsh >> 16) >= t16;
+          for (int r = 0; r < 4; ++r) {
+            s[u][kb][r] *= a.sl2;
+            mx = fmaxf(mx, s[u][kb][r]);
           }
-        } else {
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int key = k0 + kb * 16 + 4 * g + r;
+            const float x = key < a.Lk ? s[u][kb][r] * a.sl2 : -INFINITY;
+            s[u][kb][r] = x;
+            mx = fmaxf(mx, x);
+          }
+      }
+      mx = quad_max(mx);
+      // deferred rescale: keep the running reference max until a row's max grows by more
+      // than 2^8 (p <= 256 stays exact enough in bf16 / fp32)
+      const float mn = (mx > m[u] + 8.f) ? mx : m[u];
+      const float alpha = (m[u] == -INFINITY) ? (mn == -INFINITY ? 1.f : 0.f) : __builtin_amdgcn_exp2f(m[u] - mn);
+      const float mref = (mn == -INFINITY) ? 0.f : mn;
+      m[u] = mn;
+      float rs = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          s[u][kb][r] = __builtin_amdgcn_exp2f(s[u][kb][r] - mref);
+          rs += s[u][kb][r];
+        }
+      float rdt = 0.f;  // V-fold: this tile's dropped-probability sum (lane part)
+      if constexpr (DROP != FDROP_NONE) {
+        uint32_t kbits[2] = {0u, 0u};  // this lane's keep flags: bit 16kb + 4g + e of the tile's 64 keys
+        // the 4 keys of a (kb) block are consecutive: with even element indices (a.pair_ok) key pair
+        // (16 kb + 4g + 2j, + 1) is hash pair pt + 8 kb + j, pt = (drow + k0) / 2 + 2g, and while no lane's
+        // low word carries within the tile (wave-uniform test) the hash input lo + hi * C is xt + 8 kb + j
+        // -- 32-bit adds instead of 64-bit index arithmetic and a multiply-add per hash (same hashes)
+        const uint64_t pt = (drow[u] + (uint64_t)k0) / 2 + 2 * g;
+        const uint32_t ptl = (uint32_t)pt;
+        const bool fast = a.pair_ok && !__builtin_amdgcn_ballot_w64(ptl > 0xFFFFFFFFu - 32u);
+        const uint32_t xt = ptl + (uint32_t)(pt >> 32) * 0x9E3779B9u;
+        // keep masks as integers: (int)(t16 - 1 - u16) >> 31 is all ones iff u16 >= t16 (kept) -- the
+        // product is masked and the bitmap bit or-ed in without materialised booleans
+        const int t16m1 = (int)t16 - 1;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb) {
+          const uint64_t e0 = drow[u] + k0 + kb * 16 + 4 * g;
+          uint32_t km[4];
+          if (fast) {
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const uint32_t hsh = s2h_hash_mixed(hkey, xt + (uint32_t)(8 * kb + j));
+              km[2 * j] = (uint32_t)((t16m1 - (int)(hsh & 0xFFFFu)) >> 31);
+              km[2 * j + 1] = (uint32_t)((t16m1 - (int)(hsh >> 16)) >> 31);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint64_t pr = (e0 + e) >> 1;
+              const uint32_t hsh = s2h_hash_mixed(hkey, (uint32_t)pr + (uint32_t)(pr >> 32) * 0x9E3779B9u);
+              km[e] = (uint32_t)((t16m1 - (int)(((e0 + e) & 1) ? (hsh >> 16) : (hsh & 0xFFFFu))) >> 31);
+            }
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const uint64_t pr = (e0 + e) >> 1;
-            const uint32_t hsh = s2h_hash_mixed(hkey, (uint32_t)pr + (uint32_t)(pr >> 32) * 0x9E3779B9u);
-            kp[e] = (((e0 + e) & 1) ? (hsh >> 16) : (hsh & 0xFFFFu)) >= t16;
+            s[u][kb][e] = __uint_as_float(__float_as_uint(s[u][kb][e] * a.inv_keep) & km[e]);
+            kbits[kb >> 1] |= km[e] & (1u << (16 * (kb & 1) + 4 * g + e));
+          }
+          if constexpr (FOLD) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) rdt += s[u][kb][e];
           }
         }
+        if constexpr (DROP == FDROP_BITS) {  // OR the 4 key groups of the query row, one 8-B store per row and tile
 #pragma unroll
-        for (int e = 0; e < 4; ++e) s[kb][e] = kp[e] ? s[kb][e] * a.inv_keep : 0.f;
-        if constexpr (FOLD) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) rdt += s[kb][e];
+          for (int h2 = 0; h2 < 2; ++h2) kbits[h2] = quad_or(kbits[h2]);
+          if (g == 0 && q[u] < a.Lq)
+            *(uint2*)(a.keep + ((int64_t)bh * a.Lq + q[u]) * a.kw + (k0 >> 5)) = uint2{kbits[0], kbits[1]};
         }
-        kbits[kb >> 1] |= ((uint32_t)kp[0] | ((uint32_t)kp[1] << 1) | ((uint32_t)kp[2] << 2) | ((uint32_t)kp[3] << 3))
-                          << (16 * (kb & 1) + 4 * g);
       }
-      if constexpr (DROP == FDROP_BITS) {  // OR the 4 key groups of the query row, one 8-B store per row and tile
-#pragma unroll
-        for (int h2 = 0; h2 < 2; ++h2) {
-          kbits[h2] |= (uint32_t)__shfl_xor((int)kbits[h2], 16);
-          kbits[h2] |= (uint32_t)__shfl_xor((int)kbits[h2], 32);
-        }
-        if (g == 0 && q < a.Lq) *(uint2*)(a.keep + ((int64_t)bh * a.Lq + q) * a.kw + (k0 >> 5)) = uint2{kbits[0], kbits[1]};
+      rs = quad_sum(rs);
+      l[u] = l[u] * alpha + rs;
+      if constexpr (FOLD && DROP != FDROP_NONE) {
+        rdt = quad_sum(rdt);
+        rd[u] = rd[u] * alpha + rdt;
       }
-    }
-    rs += __shfl_xor(rs, 16);
-    rs += __shfl_xor(rs, 32);
-    l = l * alpha + rs;
-    if constexpr (FOLD && DROP != FDROP_NONE) {
-      rdt += __shfl_xor(rdt, 16);
-      rdt += __shfl_xor(rdt, 32);
-      rd = rd * alpha + rdt;
-    }
-    if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
+      if (__builtin_amdgcn_ballot_w64(alpha != 1.f)) {
 #pragma unroll
-      for (int d = 0; d < NDV; ++d) o[d] *= alpha;
+        for (int d = 0; d < NDV; ++d) o[u][d] *= alpha;
+      }
+      // P^T as the B operand: 32-key step c, k index 8g + j <-> key 32c + 16(j>>2) + 4g + (j&3)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pb[u][c][j] = (bf16)s[u][2 * c + (j >> 2)][j & 3];
     }
-    // P^T as the B operand: 32-key step c, k index 8g + j <-> key 32c + 16(j>>2) + 4g + (j&3)
-    bf16x8 pb[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) pb[c][j] = (bf16)s[2 * c + (j >> 2)][j & 3];
 
     // ---- O^T += V^T P^T, V^T fragments by transposing LDS reads (same key permutation)
     __builtin_amdgcn_sched_barrier(0);
@@ -252,10 +287,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
         v4i16 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + r0 * IV::ROWB + 2 * dcol));
         v4i16 hv = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(Vb + (r0 + 16) * IV::ROWB + 2 * dcol));
         v8i16 cat = __builtin_shufflevector(lo, hv, 0, 1, 2, 3, 4, 5, 6, 7);
-        o[d] = mfma16(__builtin_bit_cast(bf16x8, cat), pb[c], o[d]);
+#pragma unroll
+        for (int u = 0; u < QS; ++u) o[u][d] = mfma16(__builtin_bit_cast(bf16x8, cat), pb[u][c], o[u][d]);
       }
     }
-    sched_reads_ahead<2 * NDV, 4, 2>();
+    sched_reads_ahead<2 * NDV, 4, 2, QS>();
     __builtin_amdgcn_sched_barrier(0);
     // every wave done reading this stage before it is refilled (LDS reads retired first)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -263,34 +299,38 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     asm volatile("" ::: "memory");
   }
 
-  if (q >= a.Lq) return;
-  if (a.splits == 1) {
-    bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
-    const float inv = l > 0.f ? 1.f / l : 0.f;
 #pragma unroll
-    for (int d = 0; d < NDV; ++d) {
-      bf16 t4[4];
+  for (int u = 0; u < QS; ++u) {
+    if (q[u] >= a.Lq) continue;
+    if (a.splits == 1) {
+      bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q[u] * a.sol;
+      const float inv = l[u] > 0.f ? 1.f / l[u] : 0.f;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) t4[e] = (bf16)(o[d][e] * inv);
-      if (FOLD || 16 * d + 4 * g < a.D) *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
-    }
-    if constexpr (FOLD) {  // rowsum(D): exactly 1 without dropout (l is the sum of the same p)
-      if (g == 0) {
-        bf16 t8[8] = {};
-        t8[0] = (bf16)(DROP == FDROP_NONE ? (l > 0.f ? 1.f : 0.f) : rd * inv);
-        *(uint4*)(O + DV) = *(const uint4*)t8;
+      for (int d = 0; d < NDV; ++d) {
+        bf16 t4[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) t4[e] = (bf16)(o[u][d][e] * inv);
+        if (FOLD || 16 * d + 4 * g < a.D) *(uint2*)(O + 16 * d + 4 * g) = *(const uint2*)t4;
       }
-    }
-    if (g == 0) a.lse[(int64_t)bh * a.Lq + q] = (m + log2f(l)) * FL_LN2;
-  } else {
-    const int64_t row = (int64_t)split * a.BH * a.Lq + (int64_t)bh * a.Lq + q;
-    float* W = a.ws_o + row * DV;
+      if constexpr (FOLD) {  // rowsum(D): exactly 1 without dropout (l is the sum of the same p)
+        if (g == 0) {
+          bf16 t8[8] = {};
+          t8[0] = (bf16)(DROP == FDROP_NONE ? (l[u] > 0.f ? 1.f : 0.f) : rd[u] * inv);
+          *(uint4*)(O + DV) = *(const uint4*)t8;
+        }
+      }
+      if (g == 0) a.lse[(int64_t)bh * a.Lq + q[u]] = (m[u] + log2f(l[u])) * FL_LN2;
+    } else {
+      const int64_t row = (int64_t)split * a.BH * a.Lq + (int64_t)bh * a.Lq + q[u];
+      float* W = a.ws_o + row * DV;
 #pragma unroll
-    for (int d = 0; d < NDV; ++d) *(float4*)(W + 16 * d + 4 * g) = float4{o[d][0], o[d][1], o[d][2], o[d][3]};
-    if (g == 0) {
-      a.ws_ml[FL_MLW(FOLD) * row] = m;
-      a.ws_ml[FL_MLW(FOLD) * row + 1] = l;
-      if constexpr (FOLD) a.ws_ml[FL_MLW(FOLD) * row + 2] = DROP == FDROP_NONE ? l : rd;
+      for (int d = 0; d < NDV; ++d)
+        *(float4*)(W + 16 * d + 4 * g) = float4{o[u][d][0], o[u][d][1], o[u][d][2], o[u][d][3]};
+      if (g == 0) {
+        a.ws_ml[FL_MLW(FOLD) * row] = m[u];
+        a.ws_ml[FL_MLW(FOLD) * row + 1] = l[u];
+        if constexpr (FOLD) a.ws_ml[FL_MLW(FOLD) * row + 2] = DROP == FDROP_NONE ? l[u] : rd[u];
+      }
     }
   }
 }
@@ -342,8 +382,22 @@ __global__ __launch_bounds__(256) void flash_combine_kernel(FlashArgs a) {
 // extra split adds an fp32 [rows][D] partial written and re-read by the combine.
 static int g_flash_fwd_target = 256;  // workgroups the key split aims at (s2h_attn_config bits 8+)
 
-static void flash_plan(int BH, int Lq, int Lk, int& splits, int& tps) {
-  const int qblocks = (Lq + FL_QB - 1) / FL_QB;
+// 16-query sets per wave of the forward (flash_fwd_kernel QS): V-fold launches (bits 0-3) and plain
+// launches with head dims <= 128 (bits 4-7); the 256-wide plain form keeps 1 (its O^T alone would take
+// 128 VGPRs per set).  A/B knob s2h_flash_fwd_sets (S2H_FLASH_QS).
+static int g_flash_qs = 1 | (1 << 4);
+extern "C" int s2h_flash_fwd_sets(int mode) {
+  const int prev = g_flash_qs;
+  if (mode >= 0) g_flash_qs = mode;
+  return prev;
+}
+static int flash_qs(bool vfold, int D) {
+  const int v = vfold ? (g_flash_qs & 15) : D <= 128 ? ((g_flash_qs >> 4) & 15) : 1;
+  return v == 2 ? 2 : 1;
+}
+
+static void flash_plan(int BH, int Lq, int Lk, int& splits, int& tps, int qs = 1) {
+  const int qblocks = (Lq + FL_QB * qs - 1) / (FL_QB * qs);
   const int base = qblocks * BH;
   const int ntiles = (Lk + 63) / 64;
   int s = g_flash_fwd_target / base;
@@ -374,18 +428,21 @@ int s2h_flash_eligible(int dt, int Lq, int D) {
 
 int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
   int splits, tps;
-  flash_plan(B * H, Lq, Lk, splits, tps);
+  flash_plan(B * H, Lq, Lk, splits, tps, flash_qs(false, D));
   if (splits <= 1) return 0;
   const int DPd = flash_dp(D);  // padded image width
   return (int64_t)splits * B * H * Lq * (DPd + 2) * 4;
 }
 
-template <int DP, int DV = DP>
+template <int DP, int DV = DP, int QS = 1>
 static int flash_launch(FlashArgs& a, hipStream_t st) {
-  dim3 grid((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
-  if (a.p_drop <= 0.f) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV>), grid, dim3(FL_WAVES * 64), 0, st, a);
-  else if (a.keep) hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV>), grid, dim3(FL_WAVES * 64), 0, st, a);
-  else hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  dim3 grid((a.Lq + FL_QB * QS - 1) / (FL_QB * QS), pad_bh8(a.BH), a.splits);
+  if (a.p_drop <= 0.f)
+    hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  else if (a.keep)
+    hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  else
+    hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_combine_kernel<DP, DV>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0,
                        st, a);
@@ -418,7 +475,8 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
   a.seed = seed;
   a.seed_off = s2h_rng_offset_ptr();
   const int DPd = flash_dp(D);  // padded image width of the partials
-  flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
+  const int qs = flash_qs(false, D);
+  flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split, qs);
   const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (DPd + 2) * 4 : 0;
   if (need > ws_bytes || (need > 0 && ws == nullptr)) {  // no workspace: one split
     a.splits = 1;
@@ -428,8 +486,8 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
     a.ws_ml = a.ws_o + (int64_t)a.splits * a.BH * Lq * DPd;
   }
   if (D == 256) return flash_launch<256>(a, st);
-  if (D > 64) return flash_launch<128>(a, st);  // 72..128 (s2h_flash_eligible)
-  return flash_launch<64>(a, st);               // 32..64
+  if (D > 64) return qs == 2 ? flash_launch<128, 128, 2>(a, st) : flash_launch<128>(a, st);  // 72..128
+  return qs == 2 ? flash_launch<64, 64, 2>(a, st) : flash_launch<64>(a, st);                 // 32..64
 }
 
 // ---------------------------------------------------------------------------- V-fold
@@ -442,7 +500,7 @@ int s2h_flash_fwd(int B, int H, int Lq, int Lk, int D,
 
 extern "C" int64_t s2h_attn_fwd_vfold_ws_bytes(int B, int Lq, int Lk) {
   int splits, tps;
-  flash_plan(B, Lq, Lk, splits, tps);
+  flash_plan(B, Lq, Lk, splits, tps, flash_qs(true, VF_D));
   if (splits <= 1) return 0;
   return (int64_t)splits * B * Lq * (VF_DV + FL_MLW(true)) * 4;
 }
@@ -478,7 +536,8 @@ extern "C" int s2h_attn_fwd_vfold(int B, int Lq, int Lk, const void* q, int64_t 
   a.inv_keep = p_drop > 0.f ? 1.f / (1.f - p_drop) : 1.f;
   a.seed = seed;
   a.seed_off = s2h_rng_offset_ptr();
-  flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split);
+  const int qs = flash_qs(true, VF_D);
+  flash_plan(a.BH, Lq, Lk, a.splits, a.tiles_per_split, qs);
   const int64_t need = a.splits > 1 ? (int64_t)a.splits * a.BH * Lq * (VF_DV + FL_MLW(true)) * 4 : 0;
   if (need > ws_bytes || (need > 0 && ws == nullptr)) {
     a.splits = 1;
@@ -489,7 +548,7 @@ extern "C" int s2h_attn_fwd_vfold(int B, int Lq, int Lk, const void* q, int64_t 
   }
   // profiler record: m4 = 1000 + DV marks the folded value width (bench.py prices 2 (D + DV) per pair)
   const int slot = s2h_prof_begin(st, 1, (int64_t)B, Lq, Lk, VF_D, 1000 + VF_DV);
-  const int rc = flash_launch<VF_D, VF_DV>(a, st);
+  const int rc = qs == 2 ? flash_launch<VF_D, VF_DV, 2>(a, st) : flash_launch<VF_D, VF_DV>(a, st);
   s2h_prof_end(slot, st);
   return rc;
 }

@@ -18,6 +18,42 @@ __device__ __forceinline__ f32x4 mfma16(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// Reductions over the 4 lane groups (lanes l, l ^ 16, l ^ 32, l ^ 48) on v_permlane16/32_swap (VALU
+// exchanges) instead of ds_bpermute (an LDS-pipe op and an lgkmcnt wait inside the softmax).  With
+// both operands the same register the swap leaves, in every lane, the two values of its pair in the
+// two results, so op(r[0], r[1]) is op(own, partner) up to commutativity: the same bits as the
+// __shfl_xor form.
+template <int W>
+__device__ __forceinline__ void lane_pair(uint32_t x, uint32_t& a, uint32_t& b) {
+  if constexpr (W == 16) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    a = r[0], b = r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    a = r[0], b = r[1];
+  }
+}
+__device__ __forceinline__ float quad_max(float x) {
+  uint32_t a, b;
+  lane_pair<16>(__float_as_uint(x), a, b);
+  x = fmaxf(__uint_as_float(a), __uint_as_float(b));
+  lane_pair<32>(__float_as_uint(x), a, b);
+  return fmaxf(__uint_as_float(a), __uint_as_float(b));
+}
+__device__ __forceinline__ float quad_sum(float x) {
+  uint32_t a, b;
+  lane_pair<16>(__float_as_uint(x), a, b);
+  x = __uint_as_float(a) + __uint_as_float(b);
+  lane_pair<32>(__float_as_uint(x), a, b);
+  return __uint_as_float(a) + __uint_as_float(b);
+}
+__device__ __forceinline__ uint32_t quad_or(uint32_t x) {
+  uint32_t a, b;
+  lane_pair<16>(x, a, b);
+  lane_pair<32>(a | b, a, b);
+  return a | b;
+}
+
 template <int DP, int ROWS = 64, int NWV = FL_WAVES>
 struct FlashCfg {
   static constexpr int KT = ROWS;            // rows per streamed tile
@@ -132,6 +168,40 @@ __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, in
   }
 }
 
+// dma_tile_pad with the lane-constant part of the addresses computed once (init) and the tile's row
+// base a wave-uniform SGPR pair: per piece one s_mov m0 + global_load_lds_dwordx4 on a 32-bit VGPR
+// byte offset (the saddr form) -- dma_tile_pad's per-tile VALU address arithmetic (a division by the
+// padded row pitch, a clamp, a 64-bit multiply-add per piece) is gone.  Whole tiles only: a ragged
+// last tile takes dma_tile_pad's clamped rows.  Same bytes, same LDS image.
+template <int DP, int ROWS = 64, int NWV = FL_WAVES>
+struct PadDma {
+  using I = PadImg<DP, ROWS, NWV>;
+  static constexpr int NP = I::PPW_LO + (I::NHI ? 1 : 0);
+  uint32_t off[NP];
+  __device__ __forceinline__ void init(int64_t ld, int w, int lane, int dvalid) {
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int slot = (w + i * NWV) * 64 + lane;
+      const int row = slot / I::SPR, c = slot % I::SPR;
+      off[i] = (uint32_t)((int64_t)row * ld + (c < DP / 8 && c * 8 < dvalid ? c * 8 : 0)) * 2u;
+    }
+  }
+  // wu: the wave index as a provably wave-uniform value (readfirstlane)
+  __device__ __forceinline__ void issue(char* lds_tile, const bf16* src, int64_t ld, int r0, int wu) const {
+    const uint64_t b = (uint64_t)(uintptr_t)(src + (int64_t)r0 * ld);
+    // (readfirstlane returns int: through uint32_t, or the low word's sign bit smears into the high one)
+    const uint64_t bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (i == I::PPW_LO && wu >= I::NHI) break;  // wave-uniform
+      const uint32_t m0 = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)(lds_tile + (wu + i * NWV) * 1024));
+      asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(off[i]), "s"(bs), "s"(m0) : "memory", "m0");
+    }
+  }
+};
+
 // XCD-aware work order: workgroup `id` (x fastest) runs on XCD id % 8, so round-robin placed the
 // workgroups that re-read one (batch, head)'s operands -- the query blocks of a forward / dQ
 // launch, the key blocks of a dK/dV launch -- on 8 different L2s.  Here XCD j runs every x (and z)
@@ -189,15 +259,16 @@ __device__ __forceinline__ void sched_rep(F&& f) {
     sched_rep<K - 1>(f);
   }
 }
-template <int N, int PF, int R>
+// (MM: MFMAs per fragment -- 2 when one fragment feeds two 16-query sets, flash_fwd_kernel QS = 2)
+template <int N, int PF, int R, int MM = 1>
 __device__ __forceinline__ void sched_reads_ahead() {
   static_assert(PF <= N, "prefetch depth");
   sched_rep<PF>([] { __builtin_amdgcn_sched_group_barrier(0x100, R, 0); });
   sched_rep<N - PF>([] {
-    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, MM, 0);
     __builtin_amdgcn_sched_group_barrier(0x100, R, 0);
   });
-  sched_rep<PF>([] { __builtin_amdgcn_sched_group_barrier(0x008, 1, 0); });
+  sched_rep<PF>([] { __builtin_amdgcn_sched_group_barrier(0x008, MM, 0); });
 }
 
 __device__ __forceinline__ void wg_barrier() {

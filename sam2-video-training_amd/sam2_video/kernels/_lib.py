@@ -43,6 +43,7 @@ SIGNATURES = {
     "s2h_gemm_tiny_config": [I],
     "s2h_gemm_w41": [I],
     "s2h_gemm_areg": [I],
+    "s2h_flash_fwd_sets": [I],
     "s2h_attn_win": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
     "s2h_gemm_mx8": [I, I, I, P, L, P, L, P, L, P, L, P, I, L, P, P, L, P, L, I, F, c_uint64, c_uint64, F, F, I, P],
@@ -165,6 +166,8 @@ def lib():
             h.s2h_attn_win(int(os.environ["S2H_ATTN_WIN"]))
         if os.environ.get("S2H_GEMM_AREG"):  # ... short-K GEMMs with A in registers (A/B)
             h.s2h_gemm_areg(int(os.environ["S2H_GEMM_AREG"]))
+        if os.environ.get("S2H_FLASH_QS"):  # ... forward 16-query sets per wave, V-fold | plain << 4 (A/B)
+            h.s2h_flash_fwd_sets(int(os.environ["S2H_FLASH_QS"]))
         if os.environ.get("S2H_GEMM_W41"):  # ... bf16-output GEMMs on 4 x 1 wave grids (A/B)
             h.s2h_gemm_w41(int(os.environ["S2H_GEMM_W41"]))
         _LIB = h

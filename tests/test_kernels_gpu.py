@@ -361,6 +361,55 @@ def test_flash_forward_split_counts(target):
     _close(lse, rl, 1e-3)
 
 
+@pytest.mark.parametrize("kind,B,H,Lq,Lk,D,p,target", [
+    ("vfold", 13, 1, 1024, 3084, 256, 0.1, 256), ("vfold", 3, 1, 300, 1028, 256, 0.1, 256),
+    ("vfold", 2, 1, 1000, 700, 256, 0.0, 64), ("vfold", 13, 1, 1024, 7196, 256, 0.1, 4096),
+    ("plain", 1, 8, 1024, 1024, 56, 0.0, 256), ("plain", 2, 2, 196, 196, 56, 0.0, 64),
+    ("plain", 2, 4, 300, 77, 64, 0.1, 256), ("plain", 1, 4, 4096, 4096, 72, 0.0, 256),
+    ("plain", 2, 1, 130, 200, 120, 0.1, 64)])
+def test_flash_forward_query_sets_bit_identical(kind, B, H, Lq, Lk, D, p, target):
+    """the forward with two 16-query sets per wave (s2h_flash_fwd_sets, default for the V-fold
+    cross-attention and head dims <= 128: every K / V fragment read from LDS feeds two MFMAs) gives
+    the one-set kernel's bits -- output, log-sum-exp and dropout keep bitmap -- on one key split,
+    across ragged query / key tails and padded head dims; with key splits (whose count follows the
+    workgroup count, so differs between the two forms) the outputs agree to the combine's rounding"""
+    from sam2_video.kernels._lib import lib
+    ops = _ops()
+    torch.manual_seed(11)
+    bf = torch.bfloat16
+    q = (torch.randn(B, Lq, H, D, device=DEV) * 0.5).to(bf)
+    k = (torch.randn(B, Lk, H, D, device=DEV) * 0.5).to(bf)
+    v = torch.randn(B, Lk, H, 64 if kind == "vfold" else D, device=DEV).to(bf)
+
+    def run(qs, tgt):
+        prev_t = lib().s2h_attn_config(1 | (tgt << 8))
+        prev = lib().s2h_flash_fwd_sets(qs)
+        try:
+            o = torch.full((B, Lq, H, 72 if kind == "vfold" else D), 7.0, device=DEV, dtype=bf)
+            lse = torch.full((B, H, Lq), 7.0, device=DEV)
+            # (a keep bitmap only for the 256-wide heads whose backward reads it)
+            keep = (torch.zeros(ops.keep_words(B, H, Lq, Lk), device=DEV, dtype=torch.int32)
+                    if p > 0 and kind == "vfold" else None)
+            if kind == "vfold":
+                ops.attn_fwd_vfold(q, k, v, o, lse, 0.0625, p, 5, idx0=6, keep=keep)
+            else:
+                ops.attn_fwd(q, k, v, o, lse, D ** -0.5, p, 5, idx0=6, keep=keep)
+            torch.cuda.synchronize()
+            return o, lse, keep
+        finally:
+            lib().s2h_flash_fwd_sets(prev)
+            lib().s2h_attn_config(prev_t)
+    (o1, l1, k1), (o2, l2, k2) = run(0x11, 1), run(0x22, 1)
+    assert torch.equal(o1, o2), (o1.float() - o2.float()).abs().max().item()
+    assert torch.equal(l1, l2)
+    (o3, l3, k3), (o4, l4, k4) = run(0x11, target), run(0x22, target)
+    _close(o4, o3.float(), 2e-2)
+    _close(l4, l3, 1e-4)
+    _close(o4, o1.float(), 2e-2)
+    if k1 is not None:
+        assert torch.equal(k1, k2) and torch.equal(k1, k3) and torch.equal(k1, k4)
+
+
 def test_flash_dropout_matches_generic_kernel():
     """Same counter-hash dropout mask in the flash and the generic forward (the backward
     regenerates it), so both produce the same output up to bf16 rounding."""
