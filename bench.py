@@ -42,7 +42,9 @@ def parse():
     ap.add_argument("--image-size", type=int, default=512)
     ap.add_argument("--frames", type=int, default=8)
     ap.add_argument("--objects", type=int, default=13)
-    ap.add_argument("--dtype", default="bf16", help="bf16 | fp32 | fp8 (MX-fp8 projections / FFN, kernels/fp8.py)")
+    ap.add_argument("--dtype", default=None,
+                    help="bf16 | fp32 | fp8 (MX-fp8 projections / FFN, kernels/fp8.py); default: bf16, "
+                         "fp8 under --config 5 (--config 5 --dtype bf16 is its bf16 twin)")
     ap.add_argument("--config", type=int, default=2, choices=[2, 5],
                     help="BASELINE config preset: 2 = B+ 512^2 8 frames bf16 (the headline), "
                          "5 = B+ 512^2 16 frames MX-fp8 (long-memory stress)")
@@ -59,7 +61,11 @@ def parse():
                     help="after timing, profile one extra step and print per-shape GEMM/attention TF/s to stderr")
     args = ap.parse_args()
     if args.config == 5:
-        args.frames, args.dtype = 16, "fp8"
+        args.frames = 16
+        if args.dtype is None:
+            args.dtype = "fp8"
+    if args.dtype is None:
+        args.dtype = "bf16"
     return args
 
 
