@@ -370,6 +370,13 @@ int s2h_rope(int dt, int64_t nb, int nrot, int D, const void* x, int64_t sxb, in
 int s2h_maxpool2_fwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, void* y, hipStream_t st);
 int s2h_maxpool2_bwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, const void* dy,
                      void* dx, int64_t lddx, hipStream_t st);
+/* Up to 16 strided 2-D copies in one launch (replaces torch.cat / copy_ of the memory bank
+ * assembly, reference sam2_base.py:649-676, and the tracking loop's per-frame gradient packing):
+ * segment s copies rows[s] rows of row_bytes[s] bytes from src[s] (pitch src_ld[s] bytes) to dst[s]
+ * (pitch dst_ld[s]).  Host arrays of n entries; bases, pitches and row lengths 16-B aligned, else
+ * hipErrorInvalidValue. */
+int s2h_copy2d_batch(int n, const void* const* src, void* const* dst, const int64_t* rows, const int64_t* row_bytes,
+                     const int64_t* src_ld, const int64_t* dst_ld, hipStream_t st);
 /* window_partition (dir 0) / window_unpartition (dir 1) with zero padding
  * (backbones/utils.py:16-60); accum adds into dst. */
 int s2h_window(int dt, int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum,

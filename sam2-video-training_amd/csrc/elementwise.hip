@@ -1299,3 +1299,55 @@ extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const vo
     hipLaunchKernelGGL(colsum_seg_kernel<float>, grid, dim3(256), 0, st, rows, cols, (const float*)x, ld, rpb, tb, out);
   return (int)hipGetLastError();
 }
+
+// ---------------------------------------------------------------- batched 2-D copies
+// Up to 16 strided 2-D copies in ONE launch: the per-frame memory bank assembly (the reference's
+// torch.cat of the spatial memories and object pointers, sam2_base.py:649-676) and the tracking
+// loop's per-frame gradient packing, which otherwise cost one copy launch per bank entry / frame.
+// Segment s: rows[s] rows of row_bytes[s] bytes, source / destination pitches in bytes; every base,
+// pitch and row length a multiple of 16 B.  One lane per 16-B piece, grid-stride over the pieces
+// of all segments (segment found by a scan of the <= 16 prefix offsets, uniform in most waves).
+constexpr int kCopySegs = 16;
+struct CopySegs {
+  const uint4* src[kCopySegs];
+  uint4* dst[kCopySegs];
+  int64_t start[kCopySegs + 1];  // first piece of each segment
+  int64_t src_ld[kCopySegs], dst_ld[kCopySegs];  // pitches in 16-B pieces
+  uint32_t row_pieces[kCopySegs];
+  int n;
+};
+__global__ __launch_bounds__(256) void copy_segs_kernel(CopySegs a) {
+  const int64_t total = a.start[a.n];
+  GRID_STRIDE(i, total) {
+    int s = 0;
+    while (s + 1 < a.n && i >= a.start[s + 1]) ++s;
+    const uint32_t c = (uint32_t)(i - a.start[s]);
+    const uint32_t r = c / a.row_pieces[s], col = c - r * a.row_pieces[s];
+    a.dst[s][(int64_t)r * a.dst_ld[s] + col] = a.src[s][(int64_t)r * a.src_ld[s] + col];
+  }
+}
+extern "C" int s2h_copy2d_batch(int n, const void* const* src, void* const* dst, const int64_t* rows,
+                                const int64_t* row_bytes, const int64_t* src_ld, const int64_t* dst_ld,
+                                hipStream_t st) {
+  if (n <= 0) return 0;
+  if (n > kCopySegs) return (int)hipErrorInvalidValue;
+  CopySegs a = {};
+  a.n = n;
+  a.start[0] = 0;
+  for (int s = 0; s < n; ++s) {
+    if (!al16(src[s]) || !al16(dst[s]) || rows[s] < 0 || row_bytes[s] <= 0 || row_bytes[s] % 16 ||
+        src_ld[s] % 16 || dst_ld[s] % 16 || (rows[s] > 1 && (src_ld[s] < row_bytes[s] || dst_ld[s] < row_bytes[s])))
+      return (int)hipErrorInvalidValue;
+    const int64_t pieces = rows[s] * (row_bytes[s] / 16);
+    if (pieces >= (1ll << 32)) return (int)hipErrorInvalidValue;
+    a.src[s] = (const uint4*)src[s];
+    a.dst[s] = (uint4*)dst[s];
+    a.row_pieces[s] = (uint32_t)(row_bytes[s] / 16);
+    a.src_ld[s] = src_ld[s] / 16;
+    a.dst_ld[s] = dst_ld[s] / 16;
+    a.start[s + 1] = a.start[s] + pieces;
+  }
+  if (a.start[n] == 0) return 0;
+  hipLaunchKernelGGL(copy_segs_kernel, ew_grid(a.start[n]), dim3(256), 0, st, a);
+  return (int)hipGetLastError();
+}

@@ -725,6 +725,58 @@ def window_unpartition(win, ws, B, H, W, out=None, accumulate=False):
     return out
 
 
+# S2H_COPY_BATCH=0: one Tensor.copy_ per pair (A/B of s2h_copy2d_batch)
+_COPY_BATCH = os.environ.get("S2H_COPY_BATCH", "1") != "0"
+
+
+def _pair_rows(src, dst):
+    """(rows, row_bytes, src_pitch, dst_pitch) of the copy dst <- src (same shape and dtype) as a
+    2-D byte copy, or None when the layouts do not reduce to one (contiguous rows, uniform pitch)"""
+    if src.shape != dst.shape or src.dtype != dst.dtype:
+        return None
+    dims = [d for d in range(src.dim()) if src.shape[d] != 1]
+    es = src.element_size()
+    inner, k = 1, len(dims)
+    while k > 0 and src.stride(dims[k - 1]) == inner and dst.stride(dims[k - 1]) == inner:
+        inner *= src.shape[dims[k - 1]]
+        k -= 1
+    lead = dims[:k]
+    if not lead:
+        return 1, inner * es, inner * es, inner * es
+    rows = 1
+    for a, b in zip(lead[:-1], lead[1:]):  # the leading dims must collapse into one pitch
+        if src.stride(a) != src.stride(b) * src.shape[b] or dst.stride(a) != dst.stride(b) * dst.shape[b]:
+            return None
+    for d in lead:
+        rows *= src.shape[d]
+    return rows, inner * es, src.stride(lead[-1]) * es, dst.stride(lead[-1]) * es
+
+
+def copy_segments(pairs):
+    """dst.copy_(src) for every (src, dst) pair, up to 16 pairs per launch (s2h_copy2d_batch): the
+    memory bank assembly of a tracked frame (sam2_base.py:649-676) and the tracking loop's gradient
+    packing.  A pair whose layout is not a 16-B aligned 2-D copy goes through Tensor.copy_."""
+    import ctypes
+    if not _COPY_BATCH:
+        for src, dst in pairs:
+            dst.copy_(src)
+        return
+    segs = []
+    for src, dst in pairs:
+        r = _pair_rows(src, dst) if src.is_cuda and dst.is_cuda else None
+        if r is None or src.numel() == 0 or any(v % 16 for v in r[1:]) or src.data_ptr() % 16 or dst.data_ptr() % 16 \
+                or (r[0] > 1 and min(r[2], r[3]) < r[1]):  # broadcast / overlapping rows
+            dst.copy_(src)
+            continue
+        segs.append((src.data_ptr(), dst.data_ptr()) + r)
+    for i in range(0, len(segs), 16):
+        chunk = segs[i:i + 16]
+        n = len(chunk)
+        P, L = ctypes.c_void_p * n, ctypes.c_int64 * n
+        arrs = [P(*[c[0] for c in chunk]), P(*[c[1] for c in chunk])] + [L(*[c[j] for c in chunk]) for j in range(2, 6)]
+        call("s2h_copy2d_batch", n, *arrs, stream())
+
+
 def up2_add(lat, prev, out=None):
     B, H, W, C = lat.shape
     if out is None:

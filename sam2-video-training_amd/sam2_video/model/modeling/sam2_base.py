@@ -259,10 +259,11 @@ class SAM2Base(nn.Module):
                 obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device)
             M = sum(f.shape[1] for f in feats) + n_ptr_tok
             memory = tape.varlen_slot("memory", (num_objects, M, self.mem_dim), feat.dtype)
-            r = 0
+            r, pairs = 0, []
             for f in feats + [ptr_tokens]:
-                memory[:, r:r + f.shape[1]].copy_(f)
+                pairs.append((f, memory[:, r:r + f.shape[1]]))
                 r += f.shape[1]
+            ops.copy_segments(pairs)  # one launch for the whole bank
         else:
             obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device)
             memory = torch.cat(feats + [ptr_tokens], dim=1)

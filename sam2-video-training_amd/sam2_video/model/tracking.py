@@ -116,13 +116,15 @@ class FrameTracker:
             hs, is_ = tp.st(vh), tp.st(vi)
             gh = torch.empty(hs.buf.numel(), device=dev, dtype=hs.dtype)
             gio = torch.empty(is_.buf.numel(), device=dev, dtype=is_.dtype)
+            pairs = []
             for j, t in enumerate(frames):
                 for g, st, dst in ((grads[2 * gpos[t]], hs, gh), (grads[2 * gpos[t] + 1], is_, gio)):
                     d = dst[st.offsets[j]:st.offsets[j] + st.numels[j]]
                     if g is None:
                         d.zero_()
                     else:
-                        d.copy_(g.reshape(-1))
+                        pairs.append((g.reshape(-1), d))
+            ops.copy_segments(pairs)
             din = tp.backward({vh: gh, vi: gio})
             for j, t in enumerate(frames):
                 if din.get("pix") is not None:
@@ -165,8 +167,7 @@ class FrameTracker:
                 continue
             full = torch.zeros(src.shape, device=dev, dtype=src.dtype)
             per = full[0].numel()
-            for t, g in dhr[key].items():
-                full.view(T, per)[t].copy_(g)
+            ops.copy_segments([(g.reshape(-1), full.view(T, per)[t]) for t, g in dhr[key].items()])
             if key == "s0":
                 ds0 = full
             else:
