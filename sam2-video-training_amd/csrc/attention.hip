@@ -1242,10 +1242,11 @@ template <int DP>
 __global__ __launch_bounds__(256) void attn_fewk_dq_kernel(AttnArgs a) {
   using MF = Mfma<bf16>;
   constexpr int KS = DP + 8, SS = 16 + 8, NKT = DP / 32, ND = DP / 16;
-  __shared__ __attribute__((aligned(16))) bf16 smem[16 * KS + 4 * 16 * SS];
+  __shared__ __attribute__((aligned(16))) bf16 smem[16 * KS + 8 * 16 * SS];
   bf16* Ks = smem;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  bf16* Sw = Ks + 16 * KS + w * 16 * SS;  // this wave's dS [q][key]
+  bf16* Sw = Ks + 16 * KS + w * 2 * 16 * SS;  // this wave's dS [q][key]: bf16 high part, then the residual
+  bf16* Sl = Sw + 16 * SS;
   const int bh = blockIdx.y, b = bh / a.H, h = bh % a.H;
   const int q0 = blockIdx.x * 64 + 16 * w;
   const bf16* K = (const bf16*)a.k + b * a.skb + h * a.skh;
@@ -1281,16 +1282,23 @@ __global__ __launch_bounds__(256) void attn_fewk_dq_kernel(AttnArgs a) {
   for (int r = 0; r < 4; ++r) {
     const bool qok = q0 + 4 * (lane >> 4) + r < a.Lq;
     const float p = (kok && qok) ? exp2f(s[r] * sl2 - lse2[r]) : 0.f;
-    Sw[(4 * (lane >> 4) + r) * SS + (lane & 15)] = (bf16)(p * (dp[r] - di[r]));
+    const float ds = p * (dp[r] - di[r]);
+    const bf16 hi = (bf16)ds;
+    Sw[(4 * (lane >> 4) + r) * SS + (lane & 15)] = hi;
+    Sl[(4 * (lane >> 4) + r) * SS + (lane & 15)] = (bf16)(ds - (float)hi);
   }
   __syncthreads();  // the K tile (all waves' loads); dS rows are this wave's own
+  // dQ = dS K with dS as a bf16 pair (high part + rounding residual, two MFMAs at Lk <= 16): dQ
+  // carries dS to fp32-accumulation precision before its one bf16 rounding
   typedef short v4s __attribute__((ext_vector_type(4)));
   const v4s sa = *(const v4s*)&Sw[(lane & 15) * SS + 4 * (lane >> 4)];
+  const v4s sl = *(const v4s*)&Sl[(lane & 15) * SS + 4 * (lane >> 4)];
   bf16* dQ = (bf16*)a.dq + b * a.sdqb + h * a.sdqh;
 #pragma unroll
   for (int d = 0; d < ND; ++d) {
-    const f32x4 dq = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(sa, tr_bfrag16(Ks, KS, 0, d * 16, lane),
-                                                               f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    const auto kb = tr_bfrag16(Ks, KS, 0, d * 16, lane);
+    f32x4 dq = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(sl, kb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    dq = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(sa, kb, dq, 0, 0, 0);
     const int col = d * 16 + (lane & 15);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

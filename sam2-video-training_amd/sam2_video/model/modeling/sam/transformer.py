@@ -46,10 +46,10 @@ class Attention(nn.Module):
         h = self.num_heads
         o = FN.attention(q.view(B, Lq, h, I // h), k.view(B, Lk, h, I // h), v.view(B, Lk, h, I // h),
                          p_drop=self._p())
-        if norm is not None and residual is not None and FN._linear_ln_ok(o, self.out_proj, norm):
-            return FN.linear_add_layer_norm(o.reshape(B, Lq, I), self.out_proj, residual, norm, norm.eps,
-                                            drop_p=out_drop)[0]
-        y = self.out_proj(o.reshape(B, Lq, I), residual=residual, drop_p=out_drop)
+        o3 = o.reshape(B, Lq, I)
+        if norm is not None and residual is not None and FN._linear_ln_ok(o3, self.out_proj, norm):
+            return FN.linear_add_layer_norm(o3, self.out_proj, residual, norm, norm.eps, drop_p=out_drop)[0]
+        y = self.out_proj(o3, residual=residual, drop_p=out_drop)
         return norm(y) if norm is not None else y
 
     def forward(self, q, k, v, residual=None, norm=None):

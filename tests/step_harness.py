@@ -74,6 +74,92 @@ def grads_by_name(model):
     return out
 
 
+def structural_zero_grads(gf):
+    """key biases of attentions without RoPE: their gradient is exactly zero in exact arithmetic
+    (softmax is shift invariant along the keys), the reference holds fp32 cancellation noise
+    there (|dk_bias| ~ 1e-8 x |dk_weight|)"""
+    out = set()
+    for k in [k for k in gf if k.startswith("gnorm/") and k.endswith("k_proj.bias")]:
+        n = k[6:]
+        if float(gf[k]) <= 1e-6 * float(gf["gnorm/" + n[:-4] + "weight"]):
+            out.add(n)
+    return out
+
+
+def grad_group(name):
+    """module group of a parameter for the bf16 gradient statistics (the decoder split by block)"""
+    parts = name.split(".")
+    return ".".join(parts[:2]) if parts[0] == "sam_mask_decoder" else parts[0]
+
+
+def bf16_grad_report(grads, gf, gb, floor=0.01, eps_cos=0.002):
+    """the bench path's (bf16) gradients against the reference's fp32 step (gf), with the
+    reference's own CPU-bf16-autocast step (gb) of the same clip as the scale.
+
+    Relative error of an entry: | |g| - |g32| | / |g32| for `gnorm/` entries, |g - g32| / |g32|
+    (Frobenius) for `grad/` tensors; e_ours for this build, e_ref for the reference's bf16 step.
+    Where the whole tensor is stored (`grad/`), the gnorm entry's e_ref is the reference's VECTOR
+    drift |g16 - g32| / |g32| (it bounds what the norm can be off by; the norm of a noise-dominated
+    vector can land near |g32| by chance -- the decoder's image -> token q bias: norm 6 % off in the
+    reference's bf16 run, the vector 32 %).  Bounds, per module group (`grad_group`) and kind:
+      * groups of >= 8 entries: RMS of e_ours <= 1.25 RMS of e_ref + floor;
+      * every entry: e_ours <= 2 max(e_ref, q90) + floor, q90 = the 90th percentile of e_ref in
+        its group (a bf16 gradient's drift is noisy per tensor -- the reference's own bf16 run puts
+        one q projection 0.5 % and the next 5 % off -- so a tensor is held to twice what the
+        reference's bf16 step shows on that tensor or on the group's worse tensors);
+      * every non-zero `grad/` tensor: 1 - cos(g, g32) <= 2 (1 - cos(g16, g32)) + eps_cos.
+    Structural zeros (`structural_zero_grads`): |g| <= 2 |g16| + 1e-3 |sibling weight grad|.
+    Returns (rows, bad); rows = (name, kind, e_ours, e_ref[, cos_ours, cos_ref])."""
+    import collections
+    import math
+    structural = structural_zero_grads(gf)
+    rows, bad = [], []
+    for k in gf:
+        if not (k.startswith("gnorm/") or k.startswith("grad/")):
+            continue
+        kind, n = k.split("/", 1)
+        g = grads[n].double()
+        if n in structural:
+            if kind == "gnorm":
+                sib = float(gf["gnorm/" + n[:-4] + "weight"])
+                if float(g.norm()) > 2.0 * float(gb[k]) + 1e-3 * sib:
+                    bad.append((n, "structural", float(g.norm()), float(gb[k]), sib))
+            continue
+        if kind == "gnorm":
+            r32, r16, got = float(gf[k]), float(gb[k]), float(g.norm())
+            e_ref = abs(r16 - r32)
+            if "grad/" + n in gf:
+                e_ref = max(e_ref, float((gb["grad/" + n].double() - gf["grad/" + n].double()).norm()))
+            rows.append((n, "gnorm", abs(got - r32) / max(r32, 1e-30), e_ref / max(r32, 1e-30)))
+        else:
+            r32, r16 = gf[k].double(), gb[k].double()
+            n32, n16, no = float(r32.norm()), float(r16.norm()), float(g.norm())
+            e_ours, e_ref = float((g - r32).norm()), float((r16 - r32).norm())
+            if n32 == 0.0:  # an unused embedding row set: both must stay zero
+                if no != 0.0:
+                    bad.append((n, "zero", no, n16))
+                continue
+            c_ours = float((g.flatten() @ r32.flatten()) / max(no * n32, 1e-300))
+            c_ref = float((r16.flatten() @ r32.flatten()) / max(n16 * n32, 1e-300))
+            rows.append((n, "grad", e_ours / n32, e_ref / n32, c_ours, c_ref))
+            if 1.0 - c_ours > 2.0 * (1.0 - c_ref) + eps_cos:
+                bad.append(rows[-1] + ("cos",))
+    groups = collections.defaultdict(list)
+    for r in rows:
+        groups[(grad_group(r[0]), r[1])].append(r)
+    for key, rs in groups.items():
+        ref = sorted(r[3] for r in rs)
+        q90 = ref[min(len(ref) - 1, int(0.9 * len(ref)))]
+        rms_o = math.sqrt(sum(r[2] ** 2 for r in rs) / len(rs))
+        rms_r = math.sqrt(sum(r[3] ** 2 for r in rs) / len(rs))
+        if len(rs) >= 8 and rms_o > 1.25 * rms_r + floor:
+            bad.append((key, "rms", rms_o, rms_r))
+        for r in rs:
+            if r[2] > 2.0 * max(r[3], q90) + floor:
+                bad.append(r + ("q90", q90))
+    return rows, bad
+
+
 def mask_iou(a, b):
     a, b = a > 0, b > 0
     inter = (a & b).sum().item()
