@@ -54,8 +54,9 @@ int s2h_prof_count(void);
 int s2h_prof_read(int max, float* ms, int64_t* meta);
 /* tags[i] = the kernel record i launched (0 = not tagged): GEMM tilings as
  * BM | BN << 10 | WGM << 20 | WGN << 24 | NS << 28 | (BK / 32) << 32 | A_kcontig << 36 |
- * B_kcontig << 37 | register_staged << 38 | mx_fp8 << 39 -- the template arguments of the kernel
- * rocprofv3 names (bench.py: the roofline's dominant kernel). */
+ * B_kcontig << 37 | register_staged << 38 | mx_fp8 << 39 | a_in_registers << 40 |
+ * deterministic_wgrad << 41 -- the template arguments of the kernel rocprofv3 names (bench.py: the
+ * roofline's dominant kernel). */
 int s2h_prof_read_tags(int max, int64_t* tags);
 /* Launches a one-lane no-op kernel (s2h_trace_marker_kernel) on `st`: brackets a region of a
  * rocprofv3 kernel trace (bench.py's timed steps, tools/step_profile.py). */
@@ -125,6 +126,16 @@ int s2h_flash_fwd_sets(int mode);
  * bf16 dy/x: one launch, the bias gradient summed from the GEMM's staged dy tiles. */
 int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t lddy, const void* x,
                      int64_t ldx, float* dw, int64_t lddw, float* db, int accumulate, hipStream_t stream);
+
+/* Workspace of the deterministic weight-gradient GEMM (round 5, csrc/gemm_wgrad.hip): bf16 GEMMs with
+ * an fp32 output, both operands row-contiguous over a reduction of >= kmin rows (the Linear weight
+ * gradients of s2h_linear_wgrad / s2h_gemm, e.g. memory_attention.py:97's FFN over 93184 rows) run on
+ * 256 x 256-class tiles, write per-split fp32 partial tiles here and add them in fixed split order:
+ * the gradient arena is bit-identical from run to run (the split-K path added with fp32 atomics).
+ * ws: device memory of `bytes` owned by the caller (NULL: none, the atomic path runs); launches
+ * using it must be stream-ordered.  kmin 0 turns the kernel off, -1 keeps the current value (4096).
+ * Returns 0. */
+int s2h_wgrad_workspace(void* ws, int64_t bytes, int kmin);
 
 /* ---------------------------------------------------------------- MX-fp8 (BASELINE config 5)
  * No reference counterpart: the reference trains in fp32 / bf16 autocast only
@@ -404,9 +415,10 @@ int s2h_memory_pos(int dt, int n, int L, int Dm, const void* pos, const void* tp
  * features: sam2model.py:307-311, mask_decoder.py:201,209 repeat_interleave). */
 int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* out, int accum, hipStream_t st);
 /* NHWC im2col in PyTorch weight order (c, ky, kx) for the strided convolutions
- * (PatchEmbed utils.py:85; MaskDownSampler memory_encoder.py:43). */
+ * (PatchEmbed utils.py:85; MaskDownSampler memory_encoder.py:43): rows of ldcol >= C*kh*kw elements,
+ * the columns past C*kh*kw written as zeros. */
 int s2h_im2col(int dt, int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
-               const void* x, void* col, hipStream_t st);
+               int64_t ldcol, const void* x, void* col, hipStream_t st);
 /* Mask down-sampler stage, fused 3x3/2 pad-1 conv + LayerNorm2d(cout) + GELU, NHWC
  * (memory_encoder.py:17-55 MaskDownSampler.encoder[3i..3i+2] with the SAM2.1 config
  * kernel_size 3, stride 2, padding 1).  Supported (cin, cout): (1, 4), (4, 16), (16, 64).

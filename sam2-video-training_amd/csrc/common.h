@@ -160,6 +160,12 @@ __device__ __forceinline__ float act_grad(float x, int act) {
 // rows x cols floats with row stride ld (ld == cols: one contiguous range).
 void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t st);
 
+// Deterministic reductions (round 5): the workspace registered by s2h_wgrad_workspace (gemm_wgrad.hip)
+// for kernels that write per-block partials and add them in fixed order in a second pass instead of
+// float atomics; nullptr when none is registered, it is switched off or smaller than `bytes` (the caller
+// then keeps its atomic path).  Users are stream-ordered (one stream).
+float* s2h_det_ws(int64_t bytes);
+
 // LDS-DMA (global_load_lds_dwordx4 / _dword: 16 / 4 B per lane into lds_piece + lane * size)
 // issued through inline asm.  Issued through the builtin, the compiler's waitcnt pass sees an
 // LDS write it cannot tell apart from later ds_reads and puts s_waitcnt vmcnt(0) before the

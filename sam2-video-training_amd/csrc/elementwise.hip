@@ -5,6 +5,7 @@
 // coalesced along the contiguous (channel) dimension.
 #include "common.h"
 
+#include <algorithm>
 #include <initializer_list>
 
 #define GRID_STRIDE(i, n) for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (n); i += (int64_t)gridDim.x * blockDim.x)
@@ -714,22 +715,39 @@ extern "C" int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const flo
 
 // ------------------------------------------------------------ column sums
 // out[c] (+)= sum_r x[r*ld + c]  -> f32 (bias gradients, reductions over objects)
+// part != nullptr: the block's sums go to part[block row][c] for colsum_finalize_kernel (fixed order,
+// deterministic); otherwise float atomics into out
 template <typename T>
-__global__ void colsum_kernel(int64_t rows, int cols, const void* x, int64_t ld, float* out) {
+__global__ void colsum_kernel(int64_t rows, int cols, const void* x, int64_t ld, float* out, float* part) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   const int64_t chunk = (rows + gridDim.y - 1) / gridDim.y;
   const int64_t r0 = blockIdx.y * chunk, r1 = min(rows, r0 + chunk);
   float acc = 0.f;
   for (int64_t r = r0; r < r1; ++r) acc += to_f32(((const T*)x)[r * ld + c]);
-  atomicAdd(&out[c], acc);
+  if (part) part[(int64_t)blockIdx.y * cols + c] = acc;
+  else atomicAdd(&out[c], acc);
+}
+// out[c] += sum_{b < nb} part[b][c] in a fixed order: 4 interleaved partial sums per thread
+// (independent loads in flight), combined as (s0 + s1) + (s2 + s3)
+__global__ __launch_bounds__(256) void colsum_finalize_kernel(int nb, int cols, const float* part, float* out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int b = 0;
+  for (; b + 4 <= nb; b += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] += part[(int64_t)(b + j) * cols + c];
+  }
+  for (int j = 0; b < nb; ++b, ++j) s[j] += part[(int64_t)b * cols + c];
+  out[c] += (s[0] + s[1]) + (s[2] + s[3]);
 }
 // Vectorised column sum (bias gradients): a thread owns 8 consecutive columns (one 16-B
 // load per row), G = cols/8 threads cover a row, 256/G rows per pass; a block walks a
 // contiguous row range, reduces its row-lanes through LDS and issues one atomic per column.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t rows, int cols, const T* x, int64_t ld,
-                                                         int64_t rows_per_block, float* out) {
+                                                         int64_t rows_per_block, float* out, float* part) {
   constexpr int V = 16 / sizeof(T);
   const int G = cols / V;
   const int lanes = 256 / G;  // row lanes per pass
@@ -754,7 +772,8 @@ __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t rows, int cols,
     const int gg = c / V, j = c % V;
     float s = 0.f;
     for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * V + j];
-    atomicAdd(&out[c], s);
+    if (part) part[(int64_t)blockIdx.x * cols + c] = s;
+    else atomicAdd(&out[c], s);
   }
 }
 
@@ -769,12 +788,15 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
     int64_t rpb = (rows + 1023) / 1024;
     if (rpb < 16) rpb = 16;
     const int64_t nb = (rows + rpb - 1) / rpb;
+    float* part = s2h_det_ws(nb * cols * (int64_t)sizeof(float));
     if (dt == S2H_BF16)
       hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
-                         (const bf16*)x, ld, rpb, out);
+                         (const bf16*)x, ld, rpb, out, part);
     else
       hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
-                         (const float*)x, ld, rpb, out);
+                         (const float*)x, ld, rpb, out, part);
+    if (part)
+      hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, (int)nb, cols, part, out);
     return (int)hipGetLastError();
   }
   const int cb = (cols + 255) / 256;
@@ -783,8 +805,10 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
   if (want < 1) want = 1;
   if (ry > want) ry = want;
   dim3 grid(cb, (unsigned)ry);
-  if (dt == S2H_BF16) hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, x, ld, out);
-  else hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, x, ld, out);
+  float* part = s2h_det_ws(ry * cols * (int64_t)sizeof(float));
+  if (dt == S2H_BF16) hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, x, ld, out, part);
+  else hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, x, ld, out, part);
+  if (part) hipLaunchKernelGGL(colsum_finalize_kernel, dim3(cb), dim3(256), 0, st, (int)ry, cols, part, out);
   return (int)hipGetLastError();
 }
 // out[j] = sum_{o<O} x[o*inner + j]   written in T (broadcast-input gradients)
@@ -804,30 +828,35 @@ extern "C" int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* 
 }
 
 // ------------------------------------------------------------ NHWC im2col
-// col[(b*Ho+oy)*Wo+ox][c*kh*kw + ky*kw + kx] = x[b][oy*s-p+ky][ox*s-p+kx][c]  (PyTorch weight order)
+// col[(b*Ho+oy)*Wo+ox][c*kh*kw + ky*kw + kx] = x[b][oy*s-p+ky][ox*s-p+kx][c]  (PyTorch weight order);
+// rows of ldc >= C*kh*kw elements, the columns past C*kh*kw zero (a row pitch that is a multiple of 8
+// keeps the patch embedding's 147-column weight gradient on the LDS-DMA GEMM)
 template <typename T>
 __global__ void im2col_kernel(int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
-                              const void* x, void* col) {
+                              int ldc, const void* x, void* col) {
   const int Kc = C * kh * kw;
-  const int64_t n = (int64_t)B * Ho * Wo * Kc;
+  const int64_t n = (int64_t)B * Ho * Wo * ldc;
   GRID_STRIDE(i, n) {
-    const int k = i % Kc;
-    const int64_t p = i / Kc;
-    const int ox = p % Wo;
-    const int oy = (p / Wo) % Ho;
-    const int b = p / ((int64_t)Wo * Ho);
-    const int c = k / (kh * kw), r = k % (kh * kw), ky = r / kw, kx = r % kw;
-    const int yy = oy * stride - pad + ky, xx = ox * stride - pad + kx;
+    const int k = i % ldc;
+    const int64_t p = i / ldc;
     float v = 0.f;
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = to_f32(((const T*)x)[(((int64_t)b * H + yy) * W + xx) * C + c]);
+    if (k < Kc) {
+      const int ox = p % Wo;
+      const int oy = (p / Wo) % Ho;
+      const int b = p / ((int64_t)Wo * Ho);
+      const int c = k / (kh * kw), r = k % (kh * kw), ky = r / kw, kx = r % kw;
+      const int yy = oy * stride - pad + ky, xx = ox * stride - pad + kx;
+      if (yy >= 0 && yy < H && xx >= 0 && xx < W) v = to_f32(((const T*)x)[(((int64_t)b * H + yy) * W + xx) * C + c]);
+    }
     ((T*)col)[i] = from_f32<T>(v);
   }
 }
 extern "C" int s2h_im2col(int dt, int B, int H, int W, int C, int kh, int kw, int stride, int pad, int Ho, int Wo,
-                          const void* x, void* col, hipStream_t st) {
-  const int64_t n = (int64_t)B * Ho * Wo * C * kh * kw;
+                          int64_t ldcol, const void* x, void* col, hipStream_t st) {
+  if (ldcol < (int64_t)C * kh * kw) return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * Ho * Wo * ldcol;
   if (n <= 0) return 0;
-  DISPATCH_T(dt, im2col_kernel, ew_grid(n), B, H, W, C, kh, kw, stride, pad, Ho, Wo, x, col);
+  DISPATCH_T(dt, im2col_kernel, ew_grid(n), B, H, W, C, kh, kw, stride, pad, Ho, Wo, (int)ldcol, x, col);
   return (int)hipGetLastError();
 }
 
@@ -1100,11 +1129,29 @@ extern "C" int s2h_pos_embed(int dt, int C, int h, int w, int ws, const float* Y
   DISPATCH_T(dt, pos_embed_fwd_kernel, ew_grid(n), C, h, w, ws, Y, win, out);
   return (int)hipGetLastError();
 }
+// dwin[c, a, b] += sum over (i % ws == a, j % ws == b) dout[i, j, c]: one thread per window element,
+// the positions in row-major order (deterministic; the scatter form added with float atomics)
+template <typename T>
+__global__ void pos_win_bwd_kernel(int C, int h, int w, int ws, const void* dout, float* dwin) {
+  const int n = C * ws * ws;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= n) return;
+  const int c = e % C, ab = e / C, a = ab / ws, b = ab % ws;
+  float s = 0.f;
+  for (int y = a; y < h; y += ws)
+    for (int x = b; x < w; x += ws) s += to_f32(((const T*)dout)[((int64_t)y * w + x) * C + c]);
+  dwin[(c * ws + a) * ws + b] += s;
+}
 extern "C" int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void* dout, float* dY, float* dwin,
                                  hipStream_t st) {
   const int64_t n = (int64_t)h * w * C;
   if (n <= 0) return 0;
-  DISPATCH_T(dt, pos_embed_bwd_kernel, ew_grid(n), C, h, w, ws, dout, dY, dwin);
+  if (dY) DISPATCH_T(dt, pos_embed_bwd_kernel, ew_grid(n), C, h, w, ws, dout, dY, (float*)nullptr);
+  if (dwin) {
+    const dim3 g((C * ws * ws + 255) / 256);
+    if (dt == S2H_BF16) hipLaunchKernelGGL(pos_win_bwd_kernel<bf16>, g, dim3(256), 0, st, C, h, w, ws, dout, dwin);
+    else hipLaunchKernelGGL(pos_win_bwd_kernel<float>, g, dim3(256), 0, st, C, h, w, ws, dout, dwin);
+  }
   return (int)hipGetLastError();
 }
 
@@ -1250,7 +1297,7 @@ extern "C" int s2h_memory_pos(int dt, int n, int L, int Dm, const void* pos, con
 struct SegTable { int64_t off[64]; int dst[64]; };
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_seg_kernel(int64_t rows, int cols, const T* x, int64_t ld,
-                                                         int64_t rows_per_block, SegTable tb, float* out) {
+                                                         int64_t rows_per_block, SegTable tb, float* out, float* part) {
   constexpr int V = 16 / sizeof(T);
   const int G = cols / V;
   const int lanes = 256 / G;
@@ -1258,6 +1305,7 @@ __global__ __launch_bounds__(256) void colsum_seg_kernel(int64_t rows, int cols,
   __shared__ float red[256 * 8];
   x += tb.off[blockIdx.y] * ld;
   out += (int64_t)tb.dst[blockIdx.y] * cols;
+  if (part) part += ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * cols;
   float acc[V];
 #pragma unroll
   for (int j = 0; j < V; ++j) acc[j] = 0.f;
@@ -1277,8 +1325,33 @@ __global__ __launch_bounds__(256) void colsum_seg_kernel(int64_t rows, int cols,
     const int gg = c / V, j = c % V;
     float s = 0.f;
     for (int l = 0; l < lanes; ++l) s += red[(l * G + gg) * V + j];
-    atomicAdd(&out[c], s);
+    if (part) part[c] = s;
+    else atomicAdd(&out[c], s);
   }
+}
+// out[d][c] += the partials of every segment s with dst[s] == d (segments in order, then blocks in
+// order): one thread per (destination row, column), deterministic
+__global__ __launch_bounds__(256) void colsum_seg_finalize_kernel(int nseg, int nbx, int ndst, int cols, SegTable tb,
+                                                                  const float* part, float* out) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= ndst * cols) return;
+  const int d = e / cols, c = e % cols;
+  float acc = 0.f;
+  bool any = false;
+  for (int sg = 0; sg < nseg; ++sg) {
+    if (tb.dst[sg] != d) continue;
+    any = true;
+    const float* p = part + (int64_t)sg * nbx * cols + c;
+    float s0 = 0.f, s1 = 0.f;
+    int b = 0;
+    for (; b + 2 <= nbx; b += 2) {
+      s0 += p[(int64_t)b * cols];
+      s1 += p[(int64_t)(b + 1) * cols];
+    }
+    if (b < nbx) s0 += p[(int64_t)b * cols];
+    acc += s0 + s1;
+  }
+  if (any) out[(int64_t)d * cols + c] += acc;
 }
 extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const void* x, int64_t ld, const int64_t* offs,
                               const int* dsts, float* out, hipStream_t st) {
@@ -1293,10 +1366,19 @@ extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const vo
   int64_t rpb = (rows + 63) / 64;  // ~64 blocks per segment, each >= 16 rows
   if (rpb < 16) rpb = 16;
   const dim3 grid((unsigned)((rows + rpb - 1) / rpb), (unsigned)nseg);
+  float* part = s2h_det_ws((int64_t)grid.x * nseg * cols * (int64_t)sizeof(float));
   if (dt == S2H_BF16)
-    hipLaunchKernelGGL(colsum_seg_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, (const bf16*)x, ld, rpb, tb, out);
+    hipLaunchKernelGGL(colsum_seg_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, (const bf16*)x, ld, rpb, tb, out,
+                       part);
   else
-    hipLaunchKernelGGL(colsum_seg_kernel<float>, grid, dim3(256), 0, st, rows, cols, (const float*)x, ld, rpb, tb, out);
+    hipLaunchKernelGGL(colsum_seg_kernel<float>, grid, dim3(256), 0, st, rows, cols, (const float*)x, ld, rpb, tb, out,
+                       part);
+  if (part) {
+    int ndst = 0;
+    for (int sg = 0; sg < nseg; ++sg) ndst = std::max(ndst, dsts[sg] + 1);
+    hipLaunchKernelGGL(colsum_seg_finalize_kernel, dim3((ndst * cols + 255) / 256), dim3(256), 0, st, nseg,
+                       (int)grid.x, ndst, cols, tb, part, out);
+  }
   return (int)hipGetLastError();
 }
 

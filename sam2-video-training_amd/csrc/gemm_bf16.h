@@ -492,6 +492,9 @@ static bool gemm_glds_ok(const GemmArgs16& a, int batch) {
          bspan < (1ll << 31);
 }
 
+// weight gradients over a long reduction, deterministic split-K (gemm_wgrad.hip); -1: not its case
+int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st);
+
 // workgroups a split-K launch aims at (s2h_gemm_split_target; gemm_bf16.hip)
 extern int g_gemm_split_target;
 

@@ -102,6 +102,10 @@ static int pick_cfg(const GemmArgs16& a, int batch) {
 int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   GemmArgs16 a = in;
   a.dbg = g_gemm_dbg;
+  if (!g_gemm_cfg && a.out_f32 && a.K >= 1024) {  // long-reduction weight gradients (gemm_wgrad.hip)
+    const int rc = s2h_gemm_wgrad_det(a, batch, st);
+    if (rc >= 0) return rc;
+  }
   int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
   if (g_gemm_tiny_cfg && !g_gemm_cfg && a.M <= 128) cfg = g_gemm_tiny_cfg;
   if (g_gemm_w41 && !g_gemm_cfg && !a.out_f32 && (g_gemm_w41 == 1 || a.N >= 768)) cfg = w41_of(cfg);

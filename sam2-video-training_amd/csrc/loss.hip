@@ -31,7 +31,7 @@ __device__ __forceinline__ float focal_elem(float x, float t, float& p) {
 // grid (chunks, N): block-reduce partial sums, atomically added into stats (zeroed by caller)
 __global__ __launch_bounds__(256) void mask_stats_kernel(int N, int64_t P, const float* x, int64_t ldx,
                                                          const uint8_t* tgt, int64_t ldt, float inv_temp,
-                                                         float* stats) {
+                                                         float* stats, float* part) {
   const int n = blockIdx.y;
   const int64_t chunk = (P + gridDim.x - 1) / gridDim.x;
   const int64_t p0 = blockIdx.x * chunk, p1 = min(P, p0 + chunk);
@@ -56,7 +56,8 @@ __global__ __launch_bounds__(256) void mask_stats_kernel(int N, int64_t P, const
   __syncthreads();
   if (threadIdx.x < NSTAT) {
     float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(&stats[n * NSTAT + threadIdx.x], v);
+    if (part) part[((int64_t)n * gridDim.x + blockIdx.x) * NSTAT + threadIdx.x] = v;
+    else atomicAdd(&stats[n * NSTAT + threadIdx.x], v);
   }
 }
 
@@ -67,7 +68,7 @@ __global__ __launch_bounds__(256) void mask_stats_kernel(int N, int64_t P, const
 template <int MV>
 __global__ __launch_bounds__(256) void mask_stats_vec_kernel(int N, int64_t P, const float* x, int64_t ldx,
                                                              const uint8_t* tgt, int64_t ldt, float inv_temp,
-                                                             float* stats) {
+                                                             float* stats, float* part) {
   const int n = blockIdx.y;
   const int64_t p0 = (int64_t)blockIdx.x * (256 * 4 * MV);
   float4 xv[MV];
@@ -106,8 +107,27 @@ __global__ __launch_bounds__(256) void mask_stats_vec_kernel(int N, int64_t P, c
   __syncthreads();
   if (threadIdx.x < NSTAT) {
     float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(&stats[n * NSTAT + threadIdx.x], v);
+    if (part) part[((int64_t)n * gridDim.x + blockIdx.x) * NSTAT + threadIdx.x] = v;
+    else atomicAdd(&stats[n * NSTAT + threadIdx.x], v);
   }
+}
+
+// stats[n][k] = sum over the chunks c of part[n][c][k], in chunk order (4 interleaved sums combined
+// as (s0 + s1) + (s2 + s3)): the deterministic second pass of the statistics kernels (their first pass
+// wrote one partial row per workgroup instead of adding it with float atomics)
+__global__ __launch_bounds__(256) void stats_finalize_kernel(int N, int nch, int K, const float* part, float* stats) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= N * K) return;
+  const int n = e / K, k = e % K;
+  const float* p = part + (int64_t)n * nch * K + k;
+  float s[4] = {0.f, 0.f, 0.f, 0.f};
+  int c = 0;
+  for (; c + 4 <= nch; c += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s[j] += p[(int64_t)(c + j) * K];
+  }
+  for (int j = 0; c < nch; ++c, ++j) s[j] += p[(int64_t)c * K];
+  stats[e] = (s[0] + s[1]) + (s[2] + s[3]);
 }
 
 static bool mask_vec4_ok(int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt) {
@@ -118,19 +138,25 @@ static bool mask_vec4_ok(int64_t P, const float* x, int64_t ldx, const uint8_t* 
 extern "C" int s2h_mask_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
                               float inv_temp, float* stats, hipStream_t st) {
   if (N <= 0) return 0;
-  s2h_zero_f32(stats, 1, (int64_t)N * NSTAT, (int64_t)N * NSTAT, st);
-  int chunks = (int)((P + 4095) / 4096);
-  if (chunks > 256) chunks = 256;
-  if (chunks < 1) chunks = 1;
-  if (mask_vec4_ok(P, x, ldx, tgt, ldt)) {
-    constexpr int MV = 2;  // 2 x 4 pixels per thread, 2048 per workgroup
-    const int64_t vch = (P + 256 * 4 * MV - 1) / (256 * 4 * MV);
-    if (vch > 65535) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(mask_stats_vec_kernel<MV>, dim3((unsigned)vch, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt,
-                       inv_temp, stats);
-  } else {
-    hipLaunchKernelGGL(mask_stats_kernel, dim3(chunks, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp, stats);
-  }
+  constexpr int MV = 2;  // vector kernel: 2 x 4 pixels per thread, 2048 per workgroup
+  const bool vec = mask_vec4_ok(P, x, ldx, tgt, ldt);
+  int64_t nch = vec ? (P + 256 * 4 * MV - 1) / (256 * 4 * MV) : (P + 4095) / 4096;
+  if (!vec && nch > 256) nch = 256;
+  if (nch < 1) nch = 1;
+  if (nch > 65535) return (int)hipErrorInvalidValue;
+  // one partial row per workgroup + a fixed-order finalize (deterministic) when the workspace is
+  // there; otherwise float atomics into the zeroed statistics
+  float* part = s2h_det_ws((int64_t)N * nch * NSTAT * (int64_t)sizeof(float));
+  if (!part) s2h_zero_f32(stats, 1, (int64_t)N * NSTAT, (int64_t)N * NSTAT, st);
+  if (vec)
+    hipLaunchKernelGGL(mask_stats_vec_kernel<MV>, dim3((unsigned)nch, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt,
+                       inv_temp, stats, part);
+  else
+    hipLaunchKernelGGL(mask_stats_kernel, dim3((unsigned)nch, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
+                       stats, part);
+  if (part)
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3((N * NSTAT + 255) / 256), dim3(256), 0, st, N, (int)nch, NSTAT,
+                       part, stats);
   return (int)hipGetLastError();
 }
 
@@ -266,7 +292,7 @@ extern "C" int s2h_mask_loss_bwd(int N, int64_t P, const float* x, int64_t ldx, 
 // stats[n] = {sum bce, sum t}
 __global__ __launch_bounds__(256) void bce_stats_kernel(int N, int64_t P, const float* x, int64_t ldx,
                                                         const uint8_t* tgt, int64_t ldt, float inv_temp,
-                                                        const float* pos_weight, float* stats) {
+                                                        const float* pos_weight, float* stats, float* part) {
   const int n = blockIdx.y;
   const int64_t chunk = (P + gridDim.x - 1) / gridDim.x;
   const int64_t p0 = blockIdx.x * chunk, p1 = min(P, p0 + chunk);
@@ -287,18 +313,22 @@ __global__ __launch_bounds__(256) void bce_stats_kernel(int N, int64_t P, const 
   __syncthreads();
   if (threadIdx.x < 2) {
     const float v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-    atomicAdd(&stats[n * 2 + threadIdx.x], v);
+    if (part) part[((int64_t)n * gridDim.x + blockIdx.x) * 2 + threadIdx.x] = v;
+    else atomicAdd(&stats[n * 2 + threadIdx.x], v);
   }
 }
 extern "C" int s2h_bce_stats(int N, int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt,
                              float inv_temp, const float* pos_weight, float* stats, hipStream_t st) {
   if (N <= 0) return 0;
-  s2h_zero_f32(stats, 1, (int64_t)N * 2, (int64_t)N * 2, st);
   int chunks = (int)((P + 4095) / 4096);
   if (chunks > 256) chunks = 256;
   if (chunks < 1) chunks = 1;
+  float* part = s2h_det_ws((int64_t)N * chunks * 2 * (int64_t)sizeof(float));
+  if (!part) s2h_zero_f32(stats, 1, (int64_t)N * 2, (int64_t)N * 2, st);
   hipLaunchKernelGGL(bce_stats_kernel, dim3(chunks, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
-                     pos_weight, stats);
+                     pos_weight, stats, part);
+  if (part)
+    hipLaunchKernelGGL(stats_finalize_kernel, dim3((N * 2 + 255) / 256), dim3(256), 0, st, N, chunks, 2, part, stats);
   return (int)hipGetLastError();
 }
 // losses[0] += frame_scale * frame loss; coef[n] = d(frame_scale * loss) / d(bce sum of row n).

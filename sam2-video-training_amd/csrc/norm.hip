@@ -256,27 +256,31 @@ __global__ __launch_bounds__(256) void ln_bwd_vec_kernel(int rows, int C, const 
     part[(int64_t)blockIdx.x * 2 * C + c] = sh[c] + sh[2 * C + c] + sh[4 * C + c] + sh[6 * C + c];
 }
 
-// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][C + c].  Grid (column blocks of 64,
-// NS slices of the block partials); 256 threads = 64 columns x 4 interleaved partial rows, so
-// every thread sums only ~nb / (4 NS) values (independent loads in flight), then one atomic
-// per column and slice (NS <= 32 same-address atomics, no contention).
-__global__ __launch_bounds__(256) void ln_wgrad_finalize_kernel(int nb, int C, const float* part, float* dgamma,
-                                                                float* dbeta) {
-  __shared__ float sh[4][64];
+// dgamma[c] += sum_b part[b][c], dbeta[c] += sum_b part[b][C + c], deterministic: one workgroup per 64
+// columns, 1024 threads = 64 columns x 16 slices; slice s sums the rows b = s, s + 16, ... in order
+// (independent loads in flight), the 16 slice sums are added in a fixed tree through LDS, and one thread
+// per column updates it (no atomics: the round-4 form added up to 32 slices with float atomics, in an
+// order that changed from run to run)
+__global__ __launch_bounds__(1024) void ln_wgrad_finalize_kernel(int nb, int C, const float* part, float* dgamma,
+                                                                 float* dbeta) {
+  __shared__ float sh[16][64];
   const int col = blockIdx.x * 64 + (threadIdx.x & 63);
   const int sl = threadIdx.x >> 6;
-  const int per = (nb + gridDim.y - 1) / gridDim.y;
-  const int b0 = blockIdx.y * per, b1 = min(nb, b0 + per);
   float s = 0.f;
   if (col < 2 * C) {
 #pragma unroll 8
-    for (int b = b0 + sl; b < b1; b += 4) s += part[(int64_t)b * 2 * C + col];
+    for (int b = sl; b < nb; b += 16) s += part[(int64_t)b * 2 * C + col];
   }
   sh[sl][threadIdx.x & 63] = s;
   __syncthreads();
-  if (sl == 0 && col < 2 * C && b0 < b1) {
-    const float t = sh[0][threadIdx.x] + sh[1][threadIdx.x] + sh[2][threadIdx.x] + sh[3][threadIdx.x];
-    atomicAdd(col < C ? &dgamma[col] : &dbeta[col - C], t);
+#pragma unroll
+  for (int h = 8; h >= 1; h >>= 1) {
+    if (sl < h) sh[sl][threadIdx.x & 63] += sh[sl + h][threadIdx.x & 63];
+    __syncthreads();
+  }
+  if (sl == 0 && col < 2 * C) {
+    float* d = col < C ? &dgamma[col] : &dbeta[col - C];
+    *d += sh[0][threadIdx.x];
   }
 }
 
@@ -332,10 +336,11 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int C, const T* x
                                                      int64_t lddy, const float* gamma, const float* mean,
                                                      const float* rstd, T* dx, int64_t lddx, int dx_accum,
                                                      const T* dres, int64_t ldres, float* part) {
-  extern __shared__ float sh[];  // 2*C floats
-  for (int c = threadIdx.x; c < 2 * C; c += 256) sh[c] = 0.f;
+  extern __shared__ float sh[];  // [4 waves][2C] floats: each wave's own partial row (no LDS atomics)
+  for (int c = threadIdx.x; c < 8 * C; c += 256) sh[c] = 0.f;
   __syncthreads();
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float* shw = sh + w * 2 * C;
   for (int64_t row = (int64_t)blockIdx.x * 4 + w; row < rows; row += (int64_t)gridDim.x * 4) {
     const T* xr = x + row * ldx;
     const T* gr = dy + row * lddy;
@@ -347,7 +352,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int C, const T* x
       const float g = gamma ? d * gamma[c] : d;
       s1 += g;
       s2 += g * xh;
-      if (part) { atomicAdd(&sh[c], d * xh); atomicAdd(&sh[C + c], d); }
+      if (part) { shw[c] += d * xh; shw[C + c] += d; }  // lane-exclusive columns of the wave's row
     }
     s1 = wave_sum(s1) / C;
     s2 = wave_sum(s2) / C;
@@ -364,7 +369,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(int rows, int C, const T* x
   }
   if (!part) return;
   __syncthreads();
-  for (int c = threadIdx.x; c < 2 * C; c += 256) part[(int64_t)blockIdx.x * 2 * C + c] = sh[c];
+  for (int c = threadIdx.x; c < 2 * C; c += 256)
+    part[(int64_t)blockIdx.x * 2 * C + c] = (sh[c] + sh[2 * C + c]) + (sh[4 * C + c] + sh[6 * C + c]);
 }
 
 // ------------------------------------------------------------ launch plumbing
@@ -469,15 +475,11 @@ int ln_bwd(int rows, int C, const T* x, int64_t ldx, const T* dy, int64_t lddy, 
     S2H_LN_DISPATCH(bwd_launch, p, nb, st, rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dx, lddx, dx_accum, dres,
                     ldres, part);
   } else {
-    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 2 * C * sizeof(float), st, rows, C, x, ldx, dy, lddy,
+    hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 8 * C * sizeof(float), st, rows, C, x, ldx, dy, lddy,
                        gamma, mean, rstd, dx, lddx, dx_accum, dres, ldres, part);
   }
-  if (part) {
-    int ns = (nb + 31) / 32;
-    if (ns > 32) ns = 32;
-    hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64, ns), dim3(256), 0, st, nb, C, part, dgamma,
-                       dbeta);
-  }
+  if (part)
+    hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, nb, C, part, dgamma, dbeta);
   return (int)hipGetLastError();
 }
 }  // namespace
@@ -499,10 +501,7 @@ extern "C" int s2h_layernorm_fwd(int dt, int rows, int C, const void* x, int64_t
 extern "C" int s2h_ln_wgrad_finalize(int nb, int C, const float* part, float* dgamma, float* dbeta, hipStream_t st) {
   if (nb <= 0) return 0;
   if (C <= 0 || !part || !dgamma || !dbeta) return (int)hipErrorInvalidValue;
-  int ns = (nb + 31) / 32;
-  if (ns > 32) ns = 32;
-  hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64, ns), dim3(256), 0, st, nb, C, part, dgamma,
-                     dbeta);
+  hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, nb, C, part, dgamma, dbeta);
   return (int)hipGetLastError();
 }
 

@@ -43,6 +43,7 @@ SIGNATURES = {
     "s2h_gemm_tiny_config": [I],
     "s2h_gemm_w41": [I],
     "s2h_gemm_areg": [I],
+    "s2h_wgrad_workspace": [P, L, I],
     "s2h_flash_fwd_sets": [I],
     "s2h_attn_win": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
@@ -91,7 +92,7 @@ SIGNATURES = {
     "s2h_colsum_seg": [I, I, L, I, P, L, P, P, P, P],
     "s2h_memory_pos": [I, I, I, I, P, P, P, P, P],
     "s2h_sum_outer": [I, I, L, P, P, I, P],
-    "s2h_im2col": [I, I, I, I, I, I, I, I, I, I, I, P, P, P],
+    "s2h_im2col": [I, I, I, I, I, I, I, I, I, I, I, L, P, P, P],
     "s2h_mask_down_stage": [I, I, I, I, I, I, P, I, F, F, P, P, P, P, F, P, P],
     "s2h_dwconv": [I, I, I, I, I, I, I, P, P, P, P, P],
     "s2h_convt2": [I, I, I, I, I, P, P, P, P, I, P],
@@ -149,12 +150,19 @@ def lib():
                 f"libsam2hip.so not found at {LIB_PATH}; build it with `python __graft_entry__.py` "
                 "or `make -C sam2-video-training_amd/csrc` (there is no CPU fallback)")
         h = ctypes.CDLL(LIB_PATH)
+        missing = []
         for name, argtypes in SIGNATURES.items():
             fn = getattr(h, name, None)
-            if fn is None:  # an older build selected by S2H_LIB_PATH (A/B runs): calling it raises
+            if fn is None:
+                missing.append(name)
                 continue
             fn.argtypes = argtypes
             fn.restype = RESTYPES.get(name, c_int)
+        # an older build selected by S2H_LIB_PATH (A/B runs) may lack newer entry points (calling one
+        # raises); the shipped library must have them all
+        if missing and not os.environ.get("S2H_LIB_PATH"):
+            raise RuntimeError(f"{LIB_PATH} lacks entry points {missing} (a stale build): rebuild it with "
+                               "`make -C sam2-video-training_amd/csrc`")
         if os.environ.get("S2H_GEMM_CFG"):  # measurement override of the GEMM tiling choice
             h.s2h_gemm_config(int(os.environ["S2H_GEMM_CFG"]))
         if os.environ.get("S2H_GEMM_SPLIT_TARGET"):  # workgroups a split-K launch aims at (A/B)

@@ -107,7 +107,11 @@ def linear(x, mod, act=None, residual=None, drop_p=0.0, rope=None):
     T = _ft.active()
     if T is not None:
         return _ft.linear(T, x, mod, act, residual, float(drop_p), rope=rope)
-    return _Linear.apply(x.contiguous(), mod.weight, mod.bias, mod, act, residual, float(drop_p), rope)
+    # a 2-D input with contiguous rows keeps its row pitch (the patch embedding's im2col matrix: 147
+    # columns in 152-element rows, so its weight gradient stays on the LDS-DMA kernel)
+    if not (x.dim() == 2 and x.stride(1) == 1 and x.stride(0) >= x.shape[1]):
+        x = x.contiguous()
+    return _Linear.apply(x, mod.weight, mod.bias, mod, act, residual, float(drop_p), rope)
 
 
 class _MLP2(torch.autograd.Function):

@@ -104,6 +104,24 @@ def rng_offset(device):
     return t
 
 
+# Workspace of the deterministic long-reduction weight-gradient GEMM (csrc/gemm_wgrad.hip): fp32
+# partial tiles of <= ~256 (split, tile) workgroups x 256 KB plus the bias-gradient partials.  One per
+# process, registered once, never freed (the library keeps its address); the GEMMs that use it are
+# ordered on one stream -- with the opt-in weight-gradient side stream (S2H_WGRAD_STREAM) the library
+# keeps the atomic split-K path instead (kmin 0).
+WGRAD_WS_BYTES = 96 << 20
+_WG_WS = {}
+
+
+def wgrad_workspace(device=None):
+    t = _WG_WS.get("t")
+    if t is None:
+        t = torch.empty(WGRAD_WS_BYTES // 4, dtype=torch.float32, device=device if device is not None else "cuda")
+        call("s2h_wgrad_workspace", t.data_ptr(), WGRAD_WS_BYTES, 0 if _SIDE["on"] else -1)
+        _WG_WS["t"] = t
+    return t
+
+
 # ----------------------------------------------------------------- GEMM
 def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB=0, sC=0,
          bias=None, bias_mode=1, residual=None, ldr=0, sR=0, aux=None, ldx=0, sX=0, aux_mode=0,
@@ -111,6 +129,8 @@ def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB
     _dev(a, b, c, bias, residual, aux)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
+    if c.dtype == torch.float32 and K >= 1024 and "t" not in _WG_WS:
+        wgrad_workspace(c.device)
     call("s2h_gemm", dt(a), dt(c), batch, M, N, K,
          ptr(a), lda_m, lda_k, sA, ptr(b), ldb_k, ldb_n, sB, ptr(c), ldc, sC,
          ptr(bias), bias_mode, ptr(residual), ldr, sR, ptr(aux), ldx, sX, aux_mode,
@@ -301,6 +321,8 @@ def linear_wgrad(dy, x, dw, accumulate=True, db=None):
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() == N and db.is_contiguous()
     _dev(dy2, x2, dw, db)
+    if M >= 1024 and "t" not in _WG_WS:
+        wgrad_workspace(dw.device)
     call("s2h_linear_wgrad", dt(dy2), M, N, K, ptr(dy2), dy2.stride(0), ptr(x2), x2.stride(0), ptr(dw), dw.stride(0),
          ptr(db), int(accumulate), stream())
     return dw
@@ -850,13 +872,17 @@ def sum_outer(x, out, accumulate=False):
     return out
 
 
-def im2col(x, kh, kw, stride, pad):
+def im2col(x, kh, kw, stride, pad, pad8=False):
+    """[B*Ho*Wo, C*kh*kw] patches; pad8: a view of rows padded to a multiple of 8 elements (zeros), so
+    the GEMMs reading it (the patch embedding's 147 columns) get 16-B aligned rows"""
     B, H, W, C = x.shape
     Ho = (H + 2 * pad - kh) // stride + 1
     Wo = (W + 2 * pad - kw) // stride + 1
-    col = torch.empty(B * Ho * Wo, C * kh * kw, device=x.device, dtype=x.dtype)
-    call("s2h_im2col", dt(x), B, H, W, C, kh, kw, stride, pad, Ho, Wo, ptr(x), ptr(col), stream())
-    return col, Ho, Wo
+    Kc = C * kh * kw
+    ld = (Kc + 7) // 8 * 8 if pad8 else Kc
+    buf = torch.empty(B * Ho * Wo, ld, device=x.device, dtype=x.dtype)
+    call("s2h_im2col", dt(x), B, H, W, C, kh, kw, stride, pad, Ho, Wo, ld, ptr(x), ptr(buf), stream())
+    return (buf[:, :Kc] if ld != Kc else buf), Ho, Wo
 
 
 def dwconv(x, w, bias, pad):

@@ -98,7 +98,7 @@ class PatchEmbed(nn.Module):
 
     def forward(self, x_nhwc):
         T = x_nhwc.shape[0]
-        col, Ho, Wo = ops.im2col(x_nhwc, self.k, self.k, self.s, self.p)
+        col, Ho, Wo = ops.im2col(x_nhwc, self.k, self.k, self.s, self.p, pad8=True)
         return self.proj(col).view(T, Ho, Wo, -1)
 
 

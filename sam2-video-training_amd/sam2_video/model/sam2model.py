@@ -181,6 +181,7 @@ class SAM2Model(SAM2Base):
         device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
         if device.type != "cuda":
             raise RuntimeError("SAM2Model runs on MI355X only (libsam2hip has no CPU path)")
+        ops.wgrad_workspace(device)  # before any graph capture: the weight-gradient GEMM's partials
         for name, buf in self.named_buffers():
             mod = self.get_submodule(name.rsplit(".", 1)[0]) if "." in name else self
             setattr(mod, name.rsplit(".", 1)[-1], buf.to(device))

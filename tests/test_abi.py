@@ -88,3 +88,31 @@ def test_header_declares_the_hot_path_entry_points():
                  "s2h_mask_stats", "s2h_mask_loss_finalize", "s2h_mask_loss_bwd", "s2h_group_max_fwd",
                  "s2h_grad_norm", "s2h_adamw", "s2h_rope"):
         assert name in protos
+
+
+def test_device_code_has_no_packed_fp32(tmp_path):
+    """every gfx950 code object in libsam2hip.so is free of packed-fp32 VALU (v_pk_mul / fma / add_f32):
+    round 4 traced intermittently wrong results to such pairs (csrc/Makefile builds with the
+    packed-fp32-ops target feature off; tools/pk_f32_scan.py explains the pattern)"""
+    lib_path = os.path.join(ROOT, "sam2-video-training_amd", "sam2_video", "_lib", "libsam2hip.so")
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not (os.path.exists(lib_path) and os.path.exists(os.path.join(llvm, "llvm-objdump"))):
+        pytest.skip("library or ROCm LLVM tools absent")
+    fb = tmp_path / "fatbin.bin"
+    subprocess.run(["objcopy", "-O", "binary", "--only-section=.hip_fatbin", lib_path, str(fb)], check=True)
+    data = fb.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    assert starts, "no offload bundles in .hip_fatbin"
+    packed, mfma = 0, 0
+    for i, (a, b) in enumerate(zip(starts, starts[1:] + [len(data)])):
+        bundle, co = tmp_path / f"b{i}.bin", tmp_path / f"b{i}.co"
+        bundle.write_bytes(data[a:b])
+        subprocess.run([os.path.join(llvm, "clang-offload-bundler"), "--unbundle", "--type=o", f"--input={bundle}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True)
+        dis = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-d", str(co)], check=True, capture_output=True,
+                             text=True).stdout
+        packed += len(re.findall(r"\bv_pk_(?:mul|fma|add)_f32\b", dis))
+        mfma += len(re.findall(r"\bv_mfma_", dis))
+    assert mfma > 1000  # the disassembly really covers the kernels
+    assert packed == 0, f"{packed} packed-fp32 instructions in the device code"

@@ -98,3 +98,39 @@ def test_training_forward_repeats_bitwise(dtype):
     for r in (1, 2):
         for t, (a, b) in enumerate(zip(runs[0], runs[r])):
             assert torch.equal(a, b), (r, t, (a - b).abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_training_step_gradients_repeat_bitwise(dtype):
+    """two eager forward + loss + backward steps of the same clip, weights and dropout draws (B+ 256^2,
+    4 frames, dropout 0.1), the allocator's free memory overwritten in between: the whole gradient
+    arena is bit-identical (round 5: the weight gradients' split-K reduction, the bias / LayerNorm /
+    positional-table column sums and the loss statistics add per-workgroup partials in a fixed order
+    instead of float atomics)"""
+    from step_harness import ALL, build_model, run_step
+    from test_configs_gpu import _clips
+    from sam2_video.kernels import functional as FN
+    from sam2_video.kernels.ops import rng_offset
+    m = build_model("base_plus", 256, ALL, dtype=dtype, dropout=0.1)
+    clip = _clips([70], 4, 256, 13, 13)[0]
+    rng = rng_offset(m.arena.device)
+    names = [(n, p) for n, p in m.named_parameters() if getattr(p, "_s2h_grad", None) is not None]
+    grads, losses = [], []
+    for r in range(3):
+        if r:
+            _garble()
+        FN.set_seed(777)
+        rng.fill_(1)
+        _, _, lo, _ = run_step(m, clip)
+        losses.append(float(lo["total_loss"].detach()))
+        grads.append(m.arena.grad_region().clone())
+    assert losses[0] == losses[1] == losses[2], losses
+    for r in (1, 2):
+        if not torch.equal(grads[0], grads[r]):
+            diff = []
+            for n, p in names:
+                off = p._s2h_grad.data_ptr() - m.arena.grad.data_ptr()
+                o, k = off // 4, p.numel()
+                if not torch.equal(grads[0][o:o + k], grads[r][o:o + k]):
+                    diff.append(n)
+            raise AssertionError(f"run {r}: {len(diff)} parameters' gradients differ, e.g. {diff[:8]}")

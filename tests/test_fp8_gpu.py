@@ -77,12 +77,9 @@ def test_config5_graph_replays_match_eager():
     print("config 5 losses eager", eager, "graph", graphed)
     assert len(run._graphs) == 1
     assert all(math.isfinite(x) for x in eager + graphed), (eager, graphed)
-    # clip 1 (identical weights): the forward is bit-reproducible (tests/test_determinism_gpu.py), so
-    # the fp32 bound; later clips follow AdamW steps on gradients that differ in summation order
-    # (split-K / column-sum float atomics, ~1e-7 relative).  Adam's first steps move every weight by
-    # about +-lr whatever the gradient's size, so a near-zero gradient whose sign the summation order
-    # flips moves its weight by 2 lr, and the fp8 re-quantisation of the weights amplifies that:
-    # measured 6e-4 relative on clip 2 (r04_v1), bounded at 2e-3
-    assert abs(eager[0] - graphed[0]) <= 1e-5 * max(1.0, abs(eager[0])), (eager, graphed)
-    for a, b in zip(eager[1:], graphed[1:]):
-        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (eager, graphed)
+    # the forward and (round 5) the whole gradient arena are bit-reproducible
+    # (tests/test_determinism_gpu.py: the split-K weight gradients, column sums and loss statistics add
+    # per-workgroup partials in a fixed order), so every clip -- also after AdamW has moved the weights
+    # and the fp8 copies were re-quantised -- is held to the fp32 bound (round 4 needed 2e-3 after clip 1)
+    for a, b in zip(eager, graphed):
+        assert abs(a - b) <= 1e-5 * max(1.0, abs(a)), (eager, graphed)

@@ -172,6 +172,37 @@ def test_wgrad_split_k(rows, N, K):
     _close(out[0], ref, 2e-3)
 
 
+@pytest.mark.parametrize("rows,N,K", [(20480, 256, 2048), (16384, 2048, 256), (8192, 448, 1792), (14112, 1344, 448),
+                                      (40000, 256, 64), (9000, 128, 256), (20000, 112, 448), (3528, 2688, 896),
+                                      (3528, 896, 896), (131072, 32, 256), (4100, 72, 136)])
+def test_wgrad_deterministic(rows, N, K):
+    """long-reduction weight gradients on the deterministic kernel (csrc/gemm_wgrad.hip: per-split fp32
+    partial tiles added in fixed order, bias gradient by MFMA against ones): every tile shape it picks
+    (256^2, 256x128, 128x256, 128^2, 256x64, 64x256), K tails, partial M / N tiles; against the fp32
+    product, accumulate semantics, and bit-identical across repeats with garbage in the workspace"""
+    ops = _ops()
+    torch.manual_seed(3)
+    dy = torch.randn(rows, N, device=DEV).to(torch.bfloat16)
+    x = torch.randn(rows, K, device=DEV).to(torch.bfloat16)
+    ref = dy.float().t() @ x.float()
+    ws = ops.wgrad_workspace(DEV)
+    outs = []
+    for r in range(4):
+        ws.fill_(float("nan") if r % 2 else 1e30)
+        dw = torch.full((N, K), 0.5, device=DEV)
+        db = torch.full((N,), 0.25, device=DEV)
+        ops.linear_wgrad(dy, x, dw, db=db)
+        torch.cuda.synchronize()
+        outs.append((dw, db))
+    _close(outs[0][0], ref + 0.5, 2e-3)
+    _close(outs[0][1], dy.float().sum(0) + 0.25, 1e-4)
+    for dw, db in outs[1:]:
+        assert torch.equal(dw, outs[0][0]) and torch.equal(db, outs[0][1])
+    ops.linear_wgrad(dy, x, outs[0][0], accumulate=False, db=outs[0][1])
+    _close(outs[0][0], ref, 2e-3)
+    _close(outs[0][1], dy.float().sum(0), 1e-4)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,cols", [(131072, 112), (13312, 2048), (5, 24), (1000, 37), (70000, 256), (3, 4096)])
 def test_colsum_shapes(dtype, rows, cols):
