@@ -136,6 +136,10 @@ int s2h_linear_wgrad(int dt, int64_t rows, int N, int K, const void* dy, int64_t
  * using it must be stream-ordered.  kmin 0 turns the kernel off, -1 keeps the current value (4096).
  * Returns 0. */
 int s2h_wgrad_workspace(void* ws, int64_t bytes, int kmin);
+/* Measurement knob (tools/wgrad_bench.py): force that kernel's tile (0 = 256x256, 1 = 256x128,
+ * 2 = 128x256, 3 = 128x128, 4 = 256x64, 5 = 64x256; -1 = its cost model) and split count (0 = the cost
+ * model's).  Results stay bit-identical for a given choice.  Returns 0. */
+int s2h_wgrad_force(int tile, int splits);
 
 /* ---------------------------------------------------------------- MX-fp8 (BASELINE config 5)
  * No reference counterpart: the reference trains in fp32 / bf16 autocast only

@@ -4,6 +4,7 @@
 // NHWC im2col / depthwise conv / transposed-conv scatter.  All grid-stride,
 // coalesced along the contiguous (channel) dimension.
 #include "common.h"
+#include "reduce_det.h"
 
 #include <algorithm>
 #include <initializer_list>
@@ -728,23 +729,6 @@ __global__ void colsum_kernel(int64_t rows, int cols, const void* x, int64_t ld,
   if (part) part[(int64_t)blockIdx.y * cols + c] = acc;
   else atomicAdd(&out[c], acc);
 }
-// out[c] += sum_{b < nb} part[b][c] in a fixed order: 4 interleaved partial sums per thread
-// (independent loads in flight), combined as (s0 + s1) + (s2 + s3)
-__global__ __launch_bounds__(256) void colsum_finalize_kernel(int nb, int cols, const float* part, float* out) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  int b = 0;
-  for (; b + 4 <= nb; b += 4) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] += part[(int64_t)(b + j) * cols + c];
-  }
-  for (int j = 0; b < nb; ++b, ++j) s[j] += part[(int64_t)b * cols + c];
-  out[c] += (s[0] + s[1]) + (s[2] + s[3]);
-}
-// Vectorised column sum (bias gradients): a thread owns 8 consecutive columns (one 16-B
-// load per row), G = cols/8 threads cover a row, 256/G rows per pass; a block walks a
-// contiguous row range, reduces its row-lanes through LDS and issues one atomic per column.
 template <typename T>
 __global__ __launch_bounds__(256) void colsum_vec_kernel(int64_t rows, int cols, const T* x, int64_t ld,
                                                          int64_t rows_per_block, float* out, float* part) {
@@ -787,16 +771,19 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
     // ~1024 blocks, each >= 16 rows
     int64_t rpb = (rows + 1023) / 1024;
     if (rpb < 16) rpb = 16;
-    const int64_t nb = (rows + rpb - 1) / rpb;
+    int64_t nb = (rows + rpb - 1) / rpb;
     float* part = s2h_det_ws(nb * cols * (int64_t)sizeof(float));
+    if (part && nb > 256) {  // deterministic: <= 256 partial rows for the second pass
+      rpb = (rows + 255) / 256;
+      nb = (rows + rpb - 1) / rpb;
+    }
     if (dt == S2H_BF16)
       hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
                          (const bf16*)x, ld, rpb, out, part);
     else
       hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
                          (const float*)x, ld, rpb, out, part);
-    if (part)
-      hipLaunchKernelGGL(colsum_finalize_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, (int)nb, cols, part, out);
+    if (part) det_colsum(1, (int)nb, cols, part, out, 1, st);
     return (int)hipGetLastError();
   }
   const int cb = (cols + 255) / 256;
@@ -808,7 +795,7 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
   float* part = s2h_det_ws(ry * cols * (int64_t)sizeof(float));
   if (dt == S2H_BF16) hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, x, ld, out, part);
   else hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, x, ld, out, part);
-  if (part) hipLaunchKernelGGL(colsum_finalize_kernel, dim3(cb), dim3(256), 0, st, (int)ry, cols, part, out);
+  if (part) det_colsum(1, (int)ry, cols, part, out, 1, st);
   return (int)hipGetLastError();
 }
 // out[j] = sum_{o<O} x[o*inner + j]   written in T (broadcast-input gradients)

@@ -145,66 +145,72 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_wg_kernel(WgArgs p) {
   }
 }
 
-// Fixed-order sum of n f32x4 values p[0], p[stride], ..., p[(n-1) stride]: eight independent chains
-// (value j in chain j mod 8, so eight loads are in flight per thread), combined as a fixed tree.
-__device__ __forceinline__ f32x4 sum8(const f32x4* p, int n, int64_t stride) {
-  f32x4 c[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) c[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int s = 0;
-  for (; s + 8 <= n; s += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) c[j] += p[(int64_t)(s + j) * stride];
-  }
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-    if (s + j < n) c[j] += p[(int64_t)(s + j) * stride];
-  return ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
-}
-__device__ __forceinline__ float sum8f(const float* p, int n, int64_t stride) {
-  float c[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int s = 0;
-  for (; s + 8 <= n; s += 8) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) c[j] += p[(int64_t)(s + j) * stride];
-  }
-#pragma unroll
-  for (int j = 0; j < 7; ++j)
-    if (s + j < n) c[j] += p[(int64_t)(s + j) * stride];
-  return ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
-}
-
-// The split reduction, deterministic: the S partials of every fragment slot are cut into G groups of
-// consecutive splits; level 1 (lvl2 != nullptr) sums each group (thread per (slot, group)) into lvl2,
-// level 2 sums the G group sums of a slot and writes C = beta C + alpha sum (with G == 1 level 1 writes
-// C directly).  The first ntm * BM threads of the final level also finish rowsum[m] += sum_s part_rs[s][m].
-template <int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(256) void gemm_wg_reduce_kernel(WgArgs p, int G, f32x4* lvl2, int final_level, float* C,
-                                                             int64_t ldc, float alpha, float beta, float* rowsum) {
+// The split reduction, deterministic, one launch: a 256-thread workgroup covers 256 / SL fragment slots
+// x SL slices of the splits; slice q sums splits q, q + SL, ... with eight independent f32x4 chains
+// (eight 16-B loads in flight per thread), the SL slice sums are added in a fixed tree through LDS and
+// slice 0 writes C = beta C + alpha sum.  Workgroups past the slots do the same for the bias gradient,
+// rowsum[m] += sum_s part_rs[s][m].  Every assignment is fixed by the launch shape: the result does not
+// depend on timing.
+template <int BM, int BN, int WGM, int WGN, int SL>
+__global__ __launch_bounds__(256) void gemm_wg_reduce_kernel(WgArgs p, float* C, int64_t ldc, float alpha, float beta,
+                                                             float* rowsum) {
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NI = WN / 16;
-  constexpr int SLOTS = BM * BN / 4;
+  constexpr int SLOTS = BM * BN / 4, CPB = 256 / SL;
+  __shared__ f32x4 red[SL][CPB];
   const int tiles = p.ntm * p.ntn;
   const int64_t nslots = (int64_t)tiles * SLOTS;
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (final_level && rowsum != nullptr && g < (int64_t)p.ntm * BM) {
-    const int mt = (int)(g / BM), ml = (int)(g % BM);
-    if (mt * BM + ml < p.Mo) rowsum[mt * BM + ml] += sum8f(p.part_rs + (int64_t)mt * BM + ml, p.splits, (int64_t)p.ntm * BM);
-  }
-  const f32x4* P = reinterpret_cast<const f32x4*>(p.part);
-  int64_t slot;
-  f32x4 v;
-  if (!final_level) {  // level 1 of two: group gi of slot
-    if (g >= nslots * G) return;
-    slot = g % nslots;
-    const int gi = (int)(g / nslots);
-    const int per = (p.splits + G - 1) / G, s0 = gi * per, s1 = min(p.splits, s0 + per);
-    lvl2[(int64_t)gi * nslots + slot] = s1 > s0 ? sum8(P + (int64_t)s0 * nslots + slot, s1 - s0, nslots)
-                                                : f32x4{0.f, 0.f, 0.f, 0.f};
+  const int64_t nsb = (nslots + CPB - 1) / CPB;  // workgroups of fragment slots
+  const int c = threadIdx.x % CPB, q = threadIdx.x / CPB;
+  const int S = p.splits;
+  if ((int64_t)blockIdx.x >= nsb) {  // bias gradient
+    const int64_t m = ((int64_t)blockIdx.x - nsb) * CPB + c;
+    const int64_t nm = (int64_t)p.ntm * BM;
+    float ch[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    if (m < nm) {
+      int s = q;
+      for (; s + 7 * SL < S; s += 8 * SL) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) ch[j] += p.part_rs[(int64_t)(s + j * SL) * nm + m];
+      }
+#pragma unroll
+      for (int j = 0; j < 7; ++j)
+        if (s + j * SL < S) ch[j] += p.part_rs[(int64_t)(s + j * SL) * nm + m];
+    }
+    float* rf = reinterpret_cast<float*>(&red[0][0]);
+    rf[q * CPB + c] = ((ch[0] + ch[1]) + (ch[2] + ch[3])) + ((ch[4] + ch[5]) + (ch[6] + ch[7]));
+    __syncthreads();
+#pragma unroll
+    for (int h = SL / 2; h >= 1; h >>= 1) {
+      if (q < h) rf[q * CPB + c] += rf[(q + h) * CPB + c];
+      __syncthreads();
+    }
+    if (q == 0 && m < nm && m < p.Mo) rowsum[m] += rf[c];
     return;
   }
-  if (g >= nslots) return;
-  slot = g;
-  v = lvl2 ? sum8(lvl2 + slot, G, nslots) : sum8(P + slot, p.splits, nslots);
+  const int64_t slot = (int64_t)blockIdx.x * CPB + c;
+  const f32x4* P = reinterpret_cast<const f32x4*>(p.part);
+  f32x4 ch[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) ch[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (slot < nslots) {
+    int s = q;
+    for (; s + 7 * SL < S; s += 8 * SL) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ch[j] += P[(int64_t)(s + j * SL) * nslots + slot];
+    }
+#pragma unroll
+    for (int j = 0; j < 7; ++j)
+      if (s + j * SL < S) ch[j] += P[(int64_t)(s + j * SL) * nslots + slot];
+  }
+  red[q][c] = ((ch[0] + ch[1]) + (ch[2] + ch[3])) + ((ch[4] + ch[5]) + (ch[6] + ch[7]));
+  __syncthreads();
+#pragma unroll
+  for (int h = SL / 2; h >= 1; h >>= 1) {
+    if (q < h) red[q][c] += red[q + h][c];
+    __syncthreads();
+  }
+  if (q != 0 || slot >= nslots) return;
+  const f32x4 v = red[0][c];
   const int tile = (int)(slot / SLOTS);
   int rem = (int)(slot % SLOTS);
   const int lane = rem % 64;
@@ -222,15 +228,34 @@ __global__ __launch_bounds__(256) void gemm_wg_reduce_kernel(WgArgs p, int G, f3
   for (int r = 0; r < 4; ++r) {
     const int row = row0 + r;
     if (row < p.Mo) {
-      float* c = C + (int64_t)row * ldc + col;
-      *c = beta != 0.f ? beta * *c + alpha * v[r] : alpha * v[r];
+      float* cp = C + (int64_t)row * ldc + col;
+      *cp = beta != 0.f ? beta * *cp + alpha * v[r] : alpha * v[r];
     }
   }
+}
+
+template <int BM, int BN, int WGM, int WGN, int SL>
+static void wg_reduce_launch(const WgArgs& p, const GemmArgs16& a, hipStream_t st) {
+  constexpr int CPB = 256 / SL;
+  const int64_t nslots = (int64_t)p.ntm * p.ntn * (BM * BN / 4);
+  const int64_t nsb = (nslots + CPB - 1) / CPB;
+  const int64_t nrb = a.rowsum ? ((int64_t)p.ntm * BM + CPB - 1) / CPB : 0;
+  hipLaunchKernelGGL((gemm_wg_reduce_kernel<BM, BN, WGM, WGN, SL>), dim3((unsigned)(nsb + nrb)), dim3(256), 0, st, p,
+                     (float*)a.C, a.ldc, a.alpha, a.beta, a.rowsum);
 }
 
 static float* g_wg_ws = nullptr;
 static int64_t g_wg_ws_bytes = 0;
 static int g_wg_kmin = 4096;  // reductions at least this long take the deterministic kernel (0: off)
+static int g_wg_force_tile = -1, g_wg_force_splits = 0;  // measurement override (s2h_wgrad_force)
+
+// Measurement knob (tools/wgrad_bench.py): force the tile (0 256x256, 1 256x128, 2 128x256, 3 128x128,
+// 4 256x64, 5 64x256; -1 = the cost model) and the split count (0 = the cost model's).  Returns 0.
+extern "C" int s2h_wgrad_force(int tile, int splits) {
+  g_wg_force_tile = tile;
+  g_wg_force_splits = splits;
+  return 0;
+}
 
 // Register the weight-gradient workspace (device memory of `bytes`, owned by the caller; nullptr
 // unregisters it); kmin: the shortest reduction routed here (0 turns the kernel off, -1 keeps the
@@ -266,24 +291,20 @@ static int wg_launch(const GemmArgs16& a, int Md, int Nd, int s, hipStream_t st)
   p.splits = (a.K + p.kchunk - 1) / p.kchunk;
   p.part = g_wg_ws;
   p.part_rs = a.rowsum ? g_wg_ws + (int64_t)p.splits * tiles * BM * BN : nullptr;
-  const int64_t used_floats = (int64_t)p.splits * tiles * BM * BN + (a.rowsum ? (int64_t)p.splits * p.ntm * BM : 0);
   s2h_prof_tag(gemm_tag(BM, BN, WGM, WGN, NS, 64, false, false, false, false) | ((int64_t)1 << 41));
   hipLaunchKernelGGL((gemm_wg_kernel<BM, BN, WGM, WGN, NS>), dim3(tiles * p.splits), dim3(WGM * WGN * 64), 0, st, p);
-  // reduction: about 2^17 threads with 8 loads in flight each; groups of >= 8 splits per thread
+  // reduction: SL slices per slot so that about 2^17 threads (eight 16-B loads in flight each) read
+  // the partials
   const int64_t slots = (int64_t)tiles * (BM * BN / 4);
-  int G = (int)std::min<int64_t>((131072 + slots - 1) / slots, (p.splits + 7) / 8);
-  if (G < 1) G = 1;
-  f32x4* lvl2 = nullptr;
-  if (G > 1) {
-    lvl2 = reinterpret_cast<f32x4*>(g_wg_ws + used_floats);
-    if ((used_floats + (int64_t)G * slots * 4) * 4 > g_wg_ws_bytes) { G = 1; lvl2 = nullptr; }
+  int sl = 1;
+  while (sl < 16 && slots * sl < 131072 && sl * 2 <= p.splits) sl *= 2;
+  switch (sl) {
+    case 16: wg_reduce_launch<BM, BN, WGM, WGN, 16>(p, a, st); break;
+    case 8: wg_reduce_launch<BM, BN, WGM, WGN, 8>(p, a, st); break;
+    case 4: wg_reduce_launch<BM, BN, WGM, WGN, 4>(p, a, st); break;
+    case 2: wg_reduce_launch<BM, BN, WGM, WGN, 2>(p, a, st); break;
+    default: wg_reduce_launch<BM, BN, WGM, WGN, 1>(p, a, st); break;
   }
-  if (G > 1)
-    hipLaunchKernelGGL((gemm_wg_reduce_kernel<BM, BN, WGM, WGN>), dim3((unsigned)((slots * G + 255) / 256)), dim3(256),
-                       0, st, p, G, lvl2, 0, (float*)a.C, a.ldc, a.alpha, a.beta, a.rowsum);
-  const int64_t thr = a.rowsum && (int64_t)p.ntm * BM > slots ? (int64_t)p.ntm * BM : slots;
-  hipLaunchKernelGGL((gemm_wg_reduce_kernel<BM, BN, WGM, WGN>), dim3((unsigned)((thr + 255) / 256)), dim3(256), 0, st,
-                     p, G, lvl2, 1, (float*)a.C, a.ldc, a.alpha, a.beta, a.rowsum);
   return (int)hipGetLastError();
 }
 
@@ -305,7 +326,8 @@ int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st) {
   if ((int64_t)a.K * a.lda_k >= (1ll << 31) - 8 || (int64_t)a.K * a.ldb_k >= (1ll << 31)) return -1;
   // tile and split count from a cost model (one workgroup per CU): rounds of workgroups x (the
   // K chunk's MFMA work at the tile's measured rate + a fixed prologue / epilogue) + the partial tiles
-  // written and read back once each.  Per-CU rates (TF/s) fitted to tools/wgrad_bench.py.
+  // written and read back once each.  Per-CU rates (TF/s) fitted to tools/wgrad_sweep.py
+  // (profiles/r05_v2_wgrad_sweep.log: the model's pick within ~10 % of the best forced tile x split).
   struct Cand { int bm, bn; double rate; };
   const Cand cands[] = {{256, 256, 4.2}, {256, 128, 3.4}, {128, 256, 3.4}, {128, 128, 2.4}, {256, 64, 2.0},
                         {64, 256, 2.0}};
@@ -315,7 +337,7 @@ int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st) {
     const int bm = cands[c].bm, bn = cands[c].bn;
     const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
     const int smax = std::max(1, std::min(256, a.K / 512));
-    for (int sp = 1; sp <= smax; sp = sp < 8 ? sp + 1 : sp + sp / 4) {
+    for (int sp = 1; sp <= smax; ++sp) {
       const long kchunk = ((a.K + sp - 1) / sp + 63) / 64 * 64;
       const long wgs = tiles * sp;
       const long rounds = (wgs + 255) / 256;
@@ -324,6 +346,8 @@ int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st) {
       if (t < best_t) { best_t = t; best = c; best_s = sp; }
     }
   }
+  if (g_wg_force_tile >= 0 && g_wg_force_tile < 6) best = g_wg_force_tile;
+  if (g_wg_force_splits > 0) best_s = g_wg_force_splits;
   switch (best) {
     case 0: return wg_launch<256, 256, 2, 4, 2>(a, Md, Nd, best_s, st);
     case 1: return wg_launch<256, 128, 4, 2, 2>(a, Md, Nd, best_s, st);

@@ -6,6 +6,7 @@
 //
 // stats[n] = {sum focal, sum sigma, sum t, sum sigma*t, |pred & gt|, |pred | gt|}
 #include "common.h"
+#include "reduce_det.h"
 
 #define NSTAT 6
 
@@ -112,24 +113,6 @@ __global__ __launch_bounds__(256) void mask_stats_vec_kernel(int N, int64_t P, c
   }
 }
 
-// stats[n][k] = sum over the chunks c of part[n][c][k], in chunk order (4 interleaved sums combined
-// as (s0 + s1) + (s2 + s3)): the deterministic second pass of the statistics kernels (their first pass
-// wrote one partial row per workgroup instead of adding it with float atomics)
-__global__ __launch_bounds__(256) void stats_finalize_kernel(int N, int nch, int K, const float* part, float* stats) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= N * K) return;
-  const int n = e / K, k = e % K;
-  const float* p = part + (int64_t)n * nch * K + k;
-  float s[4] = {0.f, 0.f, 0.f, 0.f};
-  int c = 0;
-  for (; c + 4 <= nch; c += 4) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) s[j] += p[(int64_t)(c + j) * K];
-  }
-  for (int j = 0; c < nch; ++c, ++j) s[j] += p[(int64_t)c * K];
-  stats[e] = (s[0] + s[1]) + (s[2] + s[3]);
-}
-
 static bool mask_vec4_ok(int64_t P, const float* x, int64_t ldx, const uint8_t* tgt, int64_t ldt) {
   return P % 4 == 0 && ldx % 4 == 0 && ((uintptr_t)x & 15) == 0 &&
          (tgt == nullptr || (ldt % 4 == 0 && ((uintptr_t)tgt & 3) == 0));
@@ -154,9 +137,7 @@ extern "C" int s2h_mask_stats(int N, int64_t P, const float* x, int64_t ldx, con
   else
     hipLaunchKernelGGL(mask_stats_kernel, dim3((unsigned)nch, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
                        stats, part);
-  if (part)
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3((N * NSTAT + 255) / 256), dim3(256), 0, st, N, (int)nch, NSTAT,
-                       part, stats);
+  if (part) det_colsum(N, (int)nch, NSTAT, part, stats, 0, st);
   return (int)hipGetLastError();
 }
 
@@ -327,8 +308,7 @@ extern "C" int s2h_bce_stats(int N, int64_t P, const float* x, int64_t ldx, cons
   if (!part) s2h_zero_f32(stats, 1, (int64_t)N * 2, (int64_t)N * 2, st);
   hipLaunchKernelGGL(bce_stats_kernel, dim3(chunks, N), dim3(256), 0, st, N, P, x, ldx, tgt, ldt, inv_temp,
                      pos_weight, stats, part);
-  if (part)
-    hipLaunchKernelGGL(stats_finalize_kernel, dim3((N * 2 + 255) / 256), dim3(256), 0, st, N, chunks, 2, part, stats);
+  if (part) det_colsum(N, chunks, 2, part, stats, 0, st);
   return (int)hipGetLastError();
 }
 // losses[0] += frame_scale * frame loss; coef[n] = d(frame_scale * loss) / d(bce sum of row n).

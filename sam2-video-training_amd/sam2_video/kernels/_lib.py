@@ -44,6 +44,7 @@ SIGNATURES = {
     "s2h_gemm_w41": [I],
     "s2h_gemm_areg": [I],
     "s2h_wgrad_workspace": [P, L, I],
+    "s2h_wgrad_force": [I, I],
     "s2h_flash_fwd_sets": [I],
     "s2h_attn_win": [I],
     "s2h_mx8_quant": [I, I, I, P, L, L, P, L, P, L, P],
