@@ -73,3 +73,74 @@ def cosine_with_warmup(base_lr, num_warmup_steps, num_training_steps, num_cycles
         return base_lr * max(0.0, 0.5 * (1.0 + math.cos(math.pi * float(num_cycles) * 2.0 * progress)))
 
     return lr_at
+
+
+class ArenaOptimizer(torch.optim.Optimizer):
+    """The arena AdamW as a `torch.optim.Optimizer`, for Lightning's automatic optimization (the
+    reference trains that way: trainer.py:117-177 returns torch AdamW, and best.yaml:105-106 puts
+    gradient_clip_val: 1.0 and accumulate_grad_batches: 16 on the Trainer).
+
+    * param_groups hold the trainable parameters; each `p.grad` is bound to the parameter's slice of
+      the gradient arena (the HIP backward writes there, autograd never sets a .grad), so torch /
+      Lightning code that walks `p.grad` -- GradScaler.unscale_ of precision=16, gradient-norm
+      logging -- sees the real gradients;
+    * zero_grad zeroes the arena and keeps the bindings (set_to_none is ignored: a None .grad would
+      cut the view);
+    * step(closure) runs the closure (Lightning's training_step + backward), the arena all-reduce
+      when a process group of > 1 rank is up (arena_ddp_strategy: no DistributedDataParallel wrapper),
+      then the fused clip + AdamW kernels over the whole arena with `max_grad_norm`, which
+      SAM2LightningModule.configure_gradient_clipping sets from the Trainer's gradient_clip_val;
+    * the learning rate is param_groups[0]["lr"] (a torch LambdaLR drives it);
+    * state_dict carries the arena moments (Lightning checkpoints)."""
+
+    def __init__(self, arena, params, lr=1e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=0.01, max_grad_norm=0.0):
+        params = list(params)
+        super().__init__(params, dict(lr=float(lr), betas=tuple(betas), eps=float(eps),
+                                      weight_decay=float(weight_decay)))
+        self.impl = ArenaAdamW(arena, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                               max_grad_norm=max_grad_norm)
+        self.arena = arena
+        self.max_grad_norm = float(max_grad_norm or 0.0)
+        self.reducer = None
+        self._bind()
+
+    def _bind(self):
+        for g in self.param_groups:
+            for p in g["params"]:
+                view = getattr(p, "_s2h_grad", None)
+                if view is None:
+                    raise ValueError("ArenaOptimizer: parameter without an arena gradient slice")
+                if p.grad is None or p.grad.data_ptr() != view.data_ptr():
+                    p.grad = view
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.arena.zero_grad()
+        self._bind()
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        scale = 1.0
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            if self.reducer is None:
+                from .ddp import ArenaGradReducer
+                self.reducer = ArenaGradReducer(self.arena.grad_region())
+            self.reducer.reduce()
+            scale = self.reducer.grad_scale
+        self.impl.max_grad_norm = self.max_grad_norm
+        self.impl.step(lr=self.param_groups[0]["lr"], grad_scale=scale)
+        return loss
+
+    def state_dict(self):
+        sd = self.impl.state_dict()
+        sd["param_groups_lr"] = [g["lr"] for g in self.param_groups]
+        return sd
+
+    def load_state_dict(self, sd):
+        self.impl.load_state_dict(sd)
+        for g, lr in zip(self.param_groups, sd.get("param_groups_lr", [])):
+            g["lr"] = lr

@@ -41,7 +41,7 @@ from ..eval.eval import evaluate_clip
 from ..model.build import instantiate
 from ..model.losses import CORE_LOSS_KEY, BCECategoryLoss, MultiStepMultiMasksAndIous
 from .ddp import ArenaGradReducer
-from .optim import ArenaAdamW, cosine_with_warmup
+from .optim import ArenaAdamW, ArenaOptimizer, cosine_with_warmup
 
 try:  # the reference's base classes when Lightning is installed (it is not in this image)
     import lightning.pytorch as _pl
@@ -86,16 +86,18 @@ def precision_dtype(precision) -> str:
 class SAM2LightningModule(_ModuleBase):
     def __init__(self, model: Any, loss: Any, optimizer: Any, scheduler: Any, visualization: Any = None, *,
                  gradient_clip_val: Optional[float] = None, accumulate_grad_batches: Optional[int] = None):
-        """The reference's five sections (trainer.py:38-99).  The two keyword-only extras carry the
-        clip and accumulation settings to the arena optimizer under a real Lightning Trainer, which
-        refuses manual optimization when its own `gradient_clip_val` / `accumulate_grad_batches`
-        are set (leave those at None / 1 there); this build's Trainer sets them from its arguments."""
+        """The reference's five sections (trainer.py:38-99).  Under a Lightning Trainer the module uses
+        Lightning's automatic optimization exactly as the reference does: the Trainer's
+        gradient_clip_val and accumulate_grad_batches (best.yaml:105-106) apply as configured
+        (configure_optimizers returns a torch.optim.Optimizer over the gradient arena,
+        configure_gradient_clipping routes the clip into its fused kernel).  The two keyword-only
+        extras are the same settings for this build's StepRunner when it is driven without a
+        Trainer; this build's Trainer sets them from its own arguments."""
         super().__init__()
         cfg = SimpleNamespace(model=model, loss=_ns(_todict(loss)), optimizer=_ns(_todict(optimizer)),
                               scheduler=_ns(_todict(scheduler)), visualization=_ns(_todict(visualization or {})))
         if HAVE_LIGHTNING:  # pragma: no cover
             self.save_hyperparameters(ignore=["model"] if isinstance(model, nn.Module) else None)
-            self.automatic_optimization = False  # the arena optimizer steps itself (training_step)
         else:
             self.hparams = cfg
         self.cfg = cfg
@@ -117,18 +119,20 @@ class SAM2LightningModule(_ModuleBase):
         self.logged: Dict[str, Any] = {}
         self.optimizer = None
         self.lr_at = None
-        # clip / accumulation of the arena optimizer (this build's Trainer overwrites them with its own
-        # arguments; under Lightning they come from here, see _lightning_runner)
+        # clip / accumulation of the StepRunner (this build's Trainer overwrites them with its own
+        # arguments; under Lightning the Trainer's own settings apply)
         self.gradient_clip_val = gradient_clip_val
         self.accumulate_grad_batches = accumulate_grad_batches
-        self.compute_dtype = None  # set by the Trainer from `precision`
-        self._runner = None
+        self.compute_dtype = None  # set by the Trainer from `precision` (Lightning: setup reads it)
 
     # ------------------------------------------------------------ setup
     def setup(self, stage: str = "fit", device=None):
         """trainer.py:101-115: instantiate the model section, load it on the device (the current
         CUDA device -- the rank's own under DDP -- when none is given), train mode"""
         if stage == "fit":
+            tr = self._attached_trainer()
+            if self.compute_dtype is None and tr is not None and getattr(tr, "precision", None) is not None:
+                self.compute_dtype = precision_dtype(tr.precision)  # Lightning's "16-mixed" etc.
             if self.model is None:
                 m = self.cfg.model
                 if isinstance(m, nn.Module):
@@ -145,15 +149,18 @@ class SAM2LightningModule(_ModuleBase):
         """trainer.py:117-177: AdamW(lr, weight_decay, betas) -- eps 1e-8 / amsgrad False whatever the
         YAML says -- with get_cosine_schedule_with_warmup(total * warmup_factor, total), stepped per
         optimizer step.  The clip is the Trainer's gradient_clip_val (Lightning's clip_grad_norm_).
-        Called by Lightning itself (no argument, a trainer attached) it returns None: the arena
-        optimizer is not a torch.optim.Optimizer over `param.grad`; the manual-optimization runner
-        builds it on the first training_step."""
-        if total_steps is None and self._attached_trainer() is not None:
-            return None
-        total_steps = 1 if total_steps is None else total_steps
+        Called by Lightning (no argument, a trainer attached): ArenaOptimizer, a torch.optim.Optimizer
+        over the gradient arena, with a LambdaLR of that schedule over the trainer's
+        estimated_stepping_batches (optimizer steps: Lightning counts them with its own
+        accumulate_grad_batches and max_steps).  Called by StepRunner (total_steps given): the arena
+        AdamW and the schedule as a step -> lr function."""
         o = self.cfg.optimizer
         if str(_get(o, "type", "adamw")).lower() != "adamw":
             raise NotImplementedError("only AdamW (the reference configs' optimizer) is built")
+        tr = self._attached_trainer()
+        if total_steps is None and tr is not None:
+            return self._lightning_optimizers(tr)
+        total_steps = 1 if total_steps is None else total_steps
         opt = ArenaAdamW(self.model.arena, lr=_get(o, "lr", 1e-4), weight_decay=_get(o, "weight_decay", 0.01),
                          betas=tuple(_get(o, "betas", (0.9, 0.999))), eps=1e-8,
                          max_grad_norm=self.gradient_clip_val)
@@ -167,6 +174,33 @@ class SAM2LightningModule(_ModuleBase):
             self.lr_at = cosine_with_warmup(opt.lr, warm, total, float(_get(self.cfg.scheduler, "num_cycles", 0.5)))
             sched = {"scheduler": self.lr_at, "interval": "step", "frequency": 1}
         return {"optimizer": opt, "lr_scheduler": sched} if sched else {"optimizer": opt}
+
+    def _lightning_optimizers(self, tr) -> Dict[str, Any]:
+        o = self.cfg.optimizer
+        params = [p for p in self.model.parameters() if getattr(p, "_s2h_grad", None) is not None]
+        lr = float(_get(o, "lr", 1e-4))
+        opt = ArenaOptimizer(self.model.arena, params, lr=lr, weight_decay=_get(o, "weight_decay", 0.01),
+                             betas=tuple(_get(o, "betas", (0.9, 0.999))), eps=1e-8,
+                             max_grad_norm=getattr(tr, "gradient_clip_val", None) or 0.0)
+        self.optimizer = opt
+        if not _get(self.cfg.scheduler, "enabled", True):
+            return {"optimizer": opt}
+        total = max(1, int(getattr(tr, "estimated_stepping_batches", 1)))
+        warm = total * float(_get(o, "warmup_factor", 0.0))
+        if warm >= total:
+            warm = max(0, total - 1)
+        self.lr_at = cosine_with_warmup(lr, warm, total, float(_get(self.cfg.scheduler, "num_cycles", 0.5)))
+        sched = torch.optim.lr_scheduler.LambdaLR(opt, lambda step: self.lr_at(step) / lr)
+        return {"optimizer": opt, "lr_scheduler": {"scheduler": sched, "interval": "step", "frequency": 1}}
+
+    def configure_gradient_clipping(self, optimizer, gradient_clip_val=None, gradient_clip_algorithm=None):
+        """Lightning hook (automatic optimization, before each optimizer step): the Trainer's
+        gradient_clip_val becomes the fused AdamW kernel's clip (clip_grad_norm_, norm type 2, on the
+        device, no host sync) instead of torch's clip over every `p.grad`"""
+        if gradient_clip_algorithm not in (None, "norm"):
+            raise NotImplementedError("gradient_clip_algorithm='value' is not built (the reference clips by norm)")
+        opt = getattr(optimizer, "_optimizer", optimizer)  # LightningOptimizer wraps the optimizer
+        opt.max_grad_norm = float(gradient_clip_val or 0.0)
 
     # --------------------------------------------------------- forward
     def forward(self, batch):
@@ -186,13 +220,8 @@ class SAM2LightningModule(_ModuleBase):
             super().log(name, value, batch_size=1, **kw)
 
     def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
-        """trainer.py:256-289.  Under a Lightning trainer (manual optimization, see
-        `_lightning_runner`) it also runs the backward into the gradient arena and, at accumulation
-        boundaries, the all-reduce + clip + AdamW -- the work Lightning's automatic optimization
-        and DDP wrapper would do on `param.grad`, which this build never fills."""
-        runner = self._lightning_runner()
-        if runner is not None:
-            runner.begin_micro_step()
+        """trainer.py:256-289: forward, the loss on the gt_stride frames, the logged terms; returns
+        the loss (Lightning / StepRunner run the backward into the gradient arena)"""
         outs_per_frame, obj_to_cat = self.forward(batch)
         self.last_outputs = outs_per_frame
         outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
@@ -205,53 +234,12 @@ class SAM2LightningModule(_ModuleBase):
             self.log(f"train/{k}", v)
         if self.optimizer is not None:
             self.log("train/learning_rate", self.optimizer.param_groups[0]["lr"])
-        if runner is not None:
-            if hasattr(self, "manual_backward"):  # pragma: no cover - LightningModule only
-                self.manual_backward(total)
-            else:
-                total.backward()
-            runner.after_backward()
         return total
 
     def _attached_trainer(self):
         """the Lightning trainer driving this module (LightningModule._trainer), if any; this
         build's own Trainer drives StepRunner directly and does not attach itself"""
         return getattr(self, "_trainer", None)
-
-    def _lightning_runner(self):
-        """Manual-optimization runner for a Lightning trainer, built on the first training_step:
-        clip and accumulation from this module (`gradient_clip_val` / `accumulate_grad_batches`
-        keyword arguments) -- Lightning 2.x refuses manual optimization when the trainer's own
-        gradient_clip_val or accumulate_grad_batches is set, and so does this method, with the fix in
-        the message -- the schedule over the trainer's estimated_stepping_batches (optimizer steps:
-        micro-batches / accumulate), and the arena all-reduce whenever the process group has more
-        than one rank (Lightning `strategy=ddp` must not wrap the module in
-        DistributedDataParallel -- no parameter has a .grad -- use `arena_ddp_strategy()`)."""
-        tr = self._attached_trainer()
-        if tr is None:
-            return None
-        if self._runner is None:
-            import torch.distributed as dist
-            clip_tr = getattr(tr, "gradient_clip_val", None)
-            acc_tr = getattr(tr, "accumulate_grad_batches", 1)
-            if clip_tr or (acc_tr or 1) != 1:
-                raise ValueError(
-                    f"Lightning Trainer(gradient_clip_val={clip_tr}, accumulate_grad_batches={acc_tr}) with manual "
-                    "optimization: Lightning rejects these; leave them at None / 1 and pass them to "
-                    "SAM2LightningModule(..., gradient_clip_val=..., accumulate_grad_batches=...) instead")
-            acc = max(1, int(self.accumulate_grad_batches or 1))
-            micro = max(1, int(getattr(tr, "estimated_stepping_batches", 1)))
-            distributed = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
-            self._runner = StepRunner(self, total_steps=max(1, math.ceil(micro / acc)), accumulate_grad_batches=acc,
-                                      graph=False, gradient_clip_val=self.gradient_clip_val, distributed=distributed)
-        return self._runner
-
-    def on_train_epoch_end(self) -> None:
-        """Lightning hook: close the epoch's partial accumulation window (step the optimizer on what it
-        holds), as this build's Trainer does after each epoch; otherwise its gradient would leak into
-        the next epoch's first window"""
-        if self._runner is not None:
-            self._runner.flush()
 
     @torch.no_grad()
     def validation_step(self, batch, batch_idx: int = 0) -> torch.Tensor:

@@ -167,6 +167,7 @@ class _Arena:
     def __init__(self, n):
         self.device = torch.device("cpu")
         self.grad = torch.zeros(n)
+        self.data = torch.linspace(-1, 1, n)
         self.n_grad = self.grad_split = n
 
     def grad_region(self):
@@ -176,17 +177,26 @@ class _Arena:
         self.grad.zero_()
 
 
-class _StubOptimizer:
-    """records the gradient the arena AdamW would consume at each step (grad * grad_scale)"""
+class _StubAdamW:
+    """stands in for the fused clip + AdamW kernels of ArenaAdamW (CPU): records the gradient the
+    kernels would consume (arena grad x grad_scale), the clip and the learning rate of each step"""
 
     def __init__(self, arena, lr=1e-4, **kw):
         self.arena = arena
         self.param_groups = [{"lr": lr}]
-        self.seen = []
+        self.seen, self.clips, self.lrs = [], [], []
         self.max_grad_norm = kw.get("max_grad_norm")
 
     def step(self, lr=None, grad_scale=1.0):
         self.seen.append(self.arena.grad_region() * grad_scale)
+        self.clips.append(self.max_grad_norm)
+        self.lrs.append(lr)
+
+    def state_dict(self):
+        return {"step": len(self.seen)}
+
+    def load_state_dict(self, sd):
+        pass
 
 
 class _GradToArena(torch.autograd.Function):
@@ -203,13 +213,26 @@ class _GradToArena(torch.autograd.Function):
         return g, None, None
 
 
-def _stub_lightning_module(monkeypatch, n, rank):
-    """SAM2LightningModule with the device parts stubbed (model forward, criterion, optimizer,
-    RNG): what remains is the Lightning manual-optimization control flow under test"""
-    from sam2_video.kernels import ops
+class _StubModel(torch.nn.Module):
+    """two parameters that are views of the arena's data, their `_s2h_grad` views of its gradient"""
+
+    def __init__(self, arena):
+        super().__init__()
+        n = arena.n_grad
+        self.arena = arena
+        self.w = torch.nn.Parameter(arena.data[: n // 2].view(-1))
+        self.b = torch.nn.Parameter(arena.data[n // 2:].view(-1))
+        self.w._s2h_grad = arena.grad[: n // 2]
+        self.b._s2h_grad = arena.grad[n // 2:]
+
+
+def _stub_lightning_module(monkeypatch, n, rank, trainer):
+    """SAM2LightningModule with the device parts stubbed (model forward, criterion, the fused AdamW
+    kernels) and a (stub) Lightning trainer attached: what remains is the automatic-optimization
+    surface -- configure_optimizers / ArenaOptimizer / configure_gradient_clipping -- under test"""
+    from sam2_video.training import optim
     from sam2_video.training import trainer as T
-    monkeypatch.setattr(T, "ArenaAdamW", _StubOptimizer)
-    monkeypatch.setattr(ops, "rng_offset", lambda device: torch.zeros(1, dtype=torch.int64))
+    monkeypatch.setattr(optim, "ArenaAdamW", _StubAdamW)
     arena = _Arena(n)
     calls = {"n": 0}
 
@@ -219,19 +242,95 @@ def _stub_lightning_module(monkeypatch, n, rank):
         contrib = torch.arange(n, dtype=torch.float32) * (rank + 1) + 10 * calls["n"]
         return [{"y": _GradToArena.apply(x, arena, contrib)}], [0]
 
-    model = SimpleNamespace(arena=arena, frame_batched=False, __call__=forward)
-    mod = T.SAM2LightningModule(SimpleNamespace(), {"gt_stride": 1, "iou_use_l1_loss": True, "weight_dict": {"loss_mask": 1, "loss_dice": 1,
-                                                                                    "loss_iou": 1}},
-                                {"lr": 1e-4}, {"enabled": False})
-    mod.model = model
+    mod = T.SAM2LightningModule(SimpleNamespace(), {"gt_stride": 1, "iou_use_l1_loss": True,
+                                                    "weight_dict": {"loss_mask": 1, "loss_dice": 1, "loss_iou": 1}},
+                                {"lr": 1e-4, "warmup_factor": 0.25}, {"enabled": True})
+    mod.model = _StubModel(arena)
     mod.forward = forward
     mod.criterion = _StubCriterion()
+    mod._trainer = trainer
     return mod, arena
 
 
 class _StubCriterion(torch.nn.Module):
     def forward(self, outs, targets):
         return {"total_loss": outs[0]["y"]}
+
+
+def _lightning_fit(mod, n_batches, acc, clip, scaler=None):
+    """Lightning 2.x automatic optimization over n_batches (training_epoch_loop + optimizer loop +
+    precision plugin): each micro-batch's loss / accumulate_grad_batches is backpropagated; at a
+    window boundary (and on the epoch's last batch) the optimizer steps -- with precision=16 through
+    GradScaler (closure, unscale_, clip, scaler.step, update), else optimizer.step(closure) with the
+    clip after the closure's backward -- then zero_grad and the per-step scheduler"""
+    conf = mod.configure_optimizers()
+    opt, sched = conf["optimizer"], conf["lr_scheduler"]["scheduler"]
+    assert isinstance(opt, torch.optim.Optimizer) and conf["lr_scheduler"]["interval"] == "step"
+    batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
+    for i in range(n_batches):
+        def closure(i=i):
+            loss = mod.training_step(batch, i) / acc
+            (scaler.scale(loss) if scaler is not None else loss).backward()
+            return loss
+        if (i + 1) % acc and i + 1 < n_batches:
+            closure()
+            continue
+        if scaler is not None:
+            closure()
+            scaler.unscale_(opt)
+            mod.configure_gradient_clipping(opt, clip, "norm")
+            scaler.step(opt)
+            scaler.update()
+        else:
+            def wrapped():
+                out = closure()
+                mod.configure_gradient_clipping(opt, clip, "norm")
+                return out
+            opt.step(closure=wrapped)
+        opt.zero_grad()
+        sched.step()
+    return opt
+
+
+@pytest.mark.parametrize("fp16", [False, True])
+def test_lightning_automatic_optimization_clip_and_accumulate_on_the_trainer(monkeypatch, fp16):
+    """the reference's Trainer section as written (best.yaml:103-106: precision 16,
+    gradient_clip_val 1.0, accumulate_grad_batches 16 -- here 3): Lightning's automatic optimization
+    drives the module with no user edit.  The optimizer is a torch.optim.Optimizer whose params'
+    .grad are the arena slices (GradScaler unscales them in place), the window's micro-gradients
+    are summed / accumulate_grad_batches, the clip reaches the fused kernel, the cosine schedule
+    runs over estimated_stepping_batches (optimizer steps), and zero_grad keeps the bindings"""
+    n, acc, nb = 16, 3, 7  # two full windows + a partial one (Lightning steps on the epoch's last batch)
+    tr = SimpleNamespace(estimated_stepping_batches=3, accumulate_grad_batches=acc, gradient_clip_val=1.0,
+                         precision="16-mixed" if fp16 else "32-true")
+    mod, arena = _stub_lightning_module(monkeypatch, n, 0, tr)
+    scaler = torch.amp.GradScaler("cpu", init_scale=256.0) if fp16 else None
+    opt = _lightning_fit(mod, nb, acc, 1.0, scaler)
+    impl = opt.impl
+    base = torch.arange(n, dtype=torch.float32)
+    exp = [(3 * base + 10 * (1 + 2 + 3)) / acc, (3 * base + 10 * (4 + 5 + 6)) / acc, (base + 70) / acc]
+    assert len(impl.seen) == 3
+    for got, want in zip(impl.seen, exp):
+        torch.testing.assert_close(got, want)
+    assert impl.clips == [1.0, 1.0, 1.0]
+    assert impl.lrs[0] == 0.0 and 0.0 < impl.lrs[1] <= 1e-4  # warmup 0.25 x 3 steps, then cosine
+    for p in mod.model.parameters():  # the bindings survive zero_grad
+        assert p.grad is not None and p.grad.data_ptr() == p._s2h_grad.data_ptr()
+    assert float(arena.grad.abs().max()) == 0.0
+
+
+def test_configure_gradient_clipping_routes_to_the_kernel(monkeypatch):
+    tr = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=1, gradient_clip_val=None)
+    mod, _ = _stub_lightning_module(monkeypatch, 8, 0, tr)
+    opt = mod.configure_optimizers()["optimizer"]
+    assert opt.max_grad_norm == 0.0  # no clip on the trainer: none in the kernel
+    mod.configure_gradient_clipping(SimpleNamespace(_optimizer=opt), 0.5, "norm")  # a LightningOptimizer
+    assert opt.max_grad_norm == 0.5
+    with pytest.raises(NotImplementedError):
+        mod.configure_gradient_clipping(opt, 0.5, "value")
+    sd = opt.state_dict()
+    assert "param_groups_lr" in sd
+    opt.load_state_dict(sd)
 
 
 def _lightning_path_worker(rank, world, port, q):
@@ -243,27 +342,21 @@ def _lightning_path_worker(rank, world, port, q):
         mp_ = pytest.MonkeyPatch()
         from sam2_video.training.ddp import init_from_env
         init_from_env("gloo")
-        n = 1000
-        mod, arena = _stub_lightning_module(mp_, n, rank)
-        mod.gradient_clip_val, mod.accumulate_grad_batches = 1.0, 2  # on the module, not the trainer
-        mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=1,
-                                       gradient_clip_val=None)
-        assert mod.configure_optimizers() is None  # Lightning's own call: the runner owns AdamW
-        batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
-        for i in range(4):  # 2 accumulation windows of 2 micro-steps
-            mod.training_step(batch, i)
-        run = mod._runner
-        ok = run.reducer is not None and run.global_step == 2
+        n, acc = 1000, 2
+        tr = SimpleNamespace(estimated_stepping_batches=2, accumulate_grad_batches=acc, gradient_clip_val=1.0)
+        mod, arena = _stub_lightning_module(mp_, n, rank, tr)
+        opt = _lightning_fit(mod, 4, acc, 1.0)
         base = torch.arange(n, dtype=torch.float32)
         sumr = sum(base * (r + 1) for r in range(world))
-        # window 1 = micro-steps 1, 2; window 2 = micro-steps 3, 4 (arena re-zeroed in between)
-        exp1 = (2 * sumr + world * (10 + 20)) / (2 * world)
-        exp2 = (2 * sumr + world * (30 + 40)) / (2 * world)
-        seen = mod.optimizer.seen
-        ok = ok and len(seen) == 2 and torch.allclose(seen[0], exp1) and torch.allclose(seen[1], exp2)
+        # window 1 = micro-steps 1, 2; window 2 = micro-steps 3, 4 (arena zeroed in between), averaged
+        # over the ranks by the optimizer's arena all-reduce (grad_scale 1/world)
+        exp1 = (2 * sumr + world * (10 + 20)) / (acc * world)
+        exp2 = (2 * sumr + world * (30 + 40)) / (acc * world)
+        seen = opt.impl.seen
+        ok = opt.reducer is not None and len(seen) == 2 and torch.allclose(seen[0], exp1) and torch.allclose(seen[1], exp2)
         mp_.undo()
         q.put((rank, bool(ok), ""))
-    except Exception as e:  # pragma: no cover - reported to the parent
+    except Exception:  # pragma: no cover - reported to the parent
         import traceback
         q.put((rank, False, traceback.format_exc()))
     finally:
@@ -272,11 +365,9 @@ def _lightning_path_worker(rank, world, port, q):
             dist.destroy_process_group()
 
 
-def test_lightning_manual_step_two_ranks_gloo():
-    """training_step under an attached (stub) Lightning trainer on 2 gloo ranks: the runner is built
-    with the arena all-reduce, the arena is zeroed at each accumulation window, and AdamW sees
-    the window's gradient summed over micro-steps, averaged over ranks and scaled by
-    1/accumulate -- what Lightning DDP + accumulate_grad_batches compute"""
+def test_lightning_automatic_optimization_two_ranks_gloo():
+    """the same under Lightning DDP without the DistributedDataParallel wrapper (arena_ddp_strategy)
+    on 2 gloo ranks: ArenaOptimizer.step all-reduces the arena once per window"""
     import socket
     import torch.multiprocessing as mp
     s = socket.socket()
@@ -293,72 +384,6 @@ def test_lightning_manual_step_two_ranks_gloo():
     for p in procs:
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
-
-
-def test_runner_zeroes_each_window_and_flushes_partial(monkeypatch):
-    """one process: two single-step windows leave exactly one step's gradient each (ADVICE r2:
-    the arena was never re-zeroed on the Lightning path), and flush() closes a partial window"""
-    mod, arena = _stub_lightning_module(monkeypatch, 16, 0)
-    mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=1, gradient_clip_val=None)
-    batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
-    mod.training_step(batch, 0)
-    mod.training_step(batch, 1)
-    base = torch.arange(16, dtype=torch.float32)
-    assert torch.allclose(mod.optimizer.seen[1], base + 20)
-    assert mod._runner.reducer is None
-    run = mod._runner
-    run.accumulate = 3
-    run.micro_step = 3
-    mod.training_step(batch, 2)  # window of 3, only 1 micro-step taken
-    assert len(mod.optimizer.seen) == 2
-    assert run.flush() and len(mod.optimizer.seen) == 3 and run.micro_step % 3 == 0
-    assert torch.allclose(mod.optimizer.seen[2], (base + 30) / 3)
-    assert not run.flush()
-
-
-def test_lightning_trainer_clip_or_accumulate_rejected(monkeypatch):
-    """Lightning 2.x refuses manual optimization with the trainer's gradient_clip_val or
-    accumulate_grad_batches set: so does the runner, naming the module arguments that
-    replace them; the module's own settings reach the runner (accumulation, clip, and a schedule
-    over optimizer steps)"""
-    batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
-    for clip, acc in ((1.0, 1), (None, 16), (0.5, 4)):
-        mod, _ = _stub_lightning_module(monkeypatch, 8, 0)
-        mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=acc,
-                                       gradient_clip_val=clip)
-        with pytest.raises(ValueError, match="accumulate_grad_batches=..."):
-            mod.training_step(batch, 0)
-    from sam2_video.training.trainer import SAM2LightningModule
-    mod = SAM2LightningModule(SimpleNamespace(), {"iou_use_l1_loss": True, "weight_dict": {"loss_mask": 1, "loss_dice": 1, "loss_iou": 1}},
-                              {"lr": 1e-4},
-                              {"enabled": False},
-                              gradient_clip_val=1.0, accumulate_grad_batches=16)
-    assert mod.gradient_clip_val == 1.0 and mod.accumulate_grad_batches == 16
-    mod, _ = _stub_lightning_module(monkeypatch, 8, 0)
-    mod.gradient_clip_val, mod.accumulate_grad_batches = 0.1, 3
-    mod._trainer = SimpleNamespace(estimated_stepping_batches=7, accumulate_grad_batches=1, gradient_clip_val=None)
-    mod.training_step(batch, 0)
-    assert mod._runner.accumulate == 3 and mod.optimizer.max_grad_norm == 0.1
-
-
-def test_lightning_epoch_end_flushes_partial_window(monkeypatch):
-    """on_train_epoch_end steps the optimizer on a partial accumulation window and the next
-    epoch's first window starts from a zeroed arena (the window leaked across epochs)"""
-    mod, arena = _stub_lightning_module(monkeypatch, 16, 0)
-    mod.accumulate_grad_batches = 2
-    mod._trainer = SimpleNamespace(estimated_stepping_batches=4, accumulate_grad_batches=1, gradient_clip_val=None)
-    batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
-    base = torch.arange(16, dtype=torch.float32)
-    for i in range(3):  # epoch 1: one full window (calls 1, 2) + one partial (call 3)
-        mod.training_step(batch, i)
-    assert len(mod.optimizer.seen) == 1
-    mod.on_train_epoch_end()
-    assert len(mod.optimizer.seen) == 2 and torch.allclose(mod.optimizer.seen[1], (base + 30) / 2)
-    mod.training_step(batch, 0)  # epoch 2: the window restarts from zero
-    mod.training_step(batch, 1)
-    assert len(mod.optimizer.seen) == 3 and torch.allclose(mod.optimizer.seen[2], (2 * base + 40 + 50) / 2)
-    mod.on_train_epoch_end()  # nothing pending
-    assert len(mod.optimizer.seen) == 3
 
 
 def test_activation_checkpoint_flag_is_a_notice():
