@@ -183,8 +183,10 @@ def kernel_name(kind, tag):
                 2: "attention backward entry (flash_bwd kernels)"}.get(kind, "gemm_kernel (fp32)")
     bm, bn = tag & 0x3FF, (tag >> 10) & 0x3FF
     wgm, wgn, ns, bk = (tag >> 20) & 0xF, (tag >> 24) & 0xF, (tag >> 28) & 0xF, 32 * ((tag >> 32) & 0xF)
-    akc, bkc, regs, mx8, areg, wgdet = [bool((tag >> b) & 1) for b in (36, 37, 38, 39, 40, 41)]
+    akc, bkc, regs, mx8, areg, wgdet, ffn = [bool((tag >> b) & 1) for b in (36, 37, 38, 39, 40, 41, 42)]
     tf = lambda x: "true" if x else "false"  # noqa: E731
+    if ffn:  # memory-attention FFN backward input gradients in one launch (csrc/ffn.hip)
+        return "ffn_bwd_dgrad_kernel"
     if wgdet:  # deterministic long-reduction weight gradient (csrc/gemm_wgrad.hip)
         return f"gemm_wg_kernel<{bm}, {bn}, {wgm}, {wgn}, {ns}>"
     if areg:  # short-K tiling with A in registers (gemm_bf16.h gemm16a_kernel, K <= 256)

@@ -307,6 +307,14 @@ int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda, const voi
  * per-tile partial rows).  Replaces linear dgrad + s2h_layernorm_bwd for memory_attention.py:60-98
  * norm1 -> q/k/v, norm2 -> cross-attention q, norm3 -> linear1 (torch autograd of nn.Linear +
  * nn.LayerNorm).  N = 128 or 256; 16-B aligned rows; dres may be NULL. */
+/* Memory-attention FFN backward, input-gradient side, one launch (bf16; memory_attention.py:97,
+ * replacing torch autograd's linear2 input gradient -> ReLU/dropout backward -> linear1 input gradient):
+ *   dh [R, H] = alpha * (dy [R, 256] w2 [256, H]) * [hid > 0]     (alpha = 1 / keep)
+ *   dx [R, 256] = dh w1 [H, 256]
+ * hid = linear2's saved input (ReLU -> dropout output).  R a multiple of 64, H of 128; 16-B aligned
+ * bases, row strides multiples of 8 elements. */
+int s2h_ffn_bwd_dgrad(int R, int H, const void* dy, int64_t lddy, const void* w2, const void* w1, const void* hid,
+                      int64_t ldh, float alpha, void* dh, int64_t lddh, void* dx, int64_t lddx, hipStream_t st);
 int64_t s2h_linear_dgrad_ln_bwd_ws_bytes(int M, int N);
 int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64_t ldg, const void* W, int64_t ldw, float alpha,
                             const void* X, int64_t ldx, const float* gamma, const float* mean, const float* rstd,

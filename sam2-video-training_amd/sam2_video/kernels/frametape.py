@@ -339,6 +339,7 @@ class FrameTape:
                 if v is not None and v not in self.first_use:
                     self.first_use[v] = op.idx
         self.premasked = set()
+        self.prefused_dx = {}  # linear op index -> its input gradient, computed by its consumer (FFN fusion)
         self.derotated = set()  # linear-with-RoPE outputs whose consumer returned the un-rotated gradient
         self.seeded = set(out_grads)
 
@@ -459,18 +460,46 @@ def _linear_bw(tape, op, gys):
         elif gb is not None:
             ops.colsum(dpre, gb)
     dx = None
-    if op.needs[0]:
+    if op.needs[0] and op.idx in tape.prefused_dx:  # computed by the consumer's fused FFN backward
+        dx = tape.prefused_dx.pop(op.idx)
+    elif op.needs[0]:
         prod = tape.producer.get(op.ins[0])
         if prod is not None and prod.kind == "linear" and prod.attrs["relu_out"] and tape.nuse[op.ins[0]] == 1 \
                 and op.ins[0] not in tape.seeded:
             # sole consumer of a ReLU (-> dropout) linear: its mask and 1/keep fused into this dgrad
-            pp = prod.attrs["p"]
-            dx = _fp8.linear_dgrad(dpre, mod, pre=x2, act="relu", alpha=1.0 / (1.0 - pp)).view(-1)
+            alpha = 1.0 / (1.0 - prod.attrs["p"])
+            dx = _ffn_dgrad_fused(tape, op, prod, dpre, mod, x2, alpha)
+            if dx is None:
+                dx = _fp8.linear_dgrad(dpre, mod, pre=x2, act="relu", alpha=alpha).view(-1)
             tape.premasked.add(op.ins[0])
         elif not _ln_dgrad_fused(tape, op, prod, dpre, mod):
             dx = _fp8.linear_dgrad(dpre, mod).view(-1)
     dres = gy if op.needs[1] else None
     return [dx, dres]
+
+
+def ffn_fuse_enabled():
+    """S2H_FFN_FUSE=0 runs the memory-attention FFN's input gradients as two GEMMs (dH with the ReLU /
+    dropout mask in its epilogue, then dX = dH W1) instead of the one-launch ops.ffn_bwd_dgrad"""
+    return os.environ.get("S2H_FFN_FUSE", "1") == "1"
+
+
+def _ffn_dgrad_fused(tape, op, prod, dpre, mod, hid, alpha):
+    """`op` = linear2 of a ReLU FFN whose linear1 is `prod` (memory_attention.py:97): compute both input
+    gradients in one launch -- linear1's pre-activation gradient dH (returned, flat, as the gradient of
+    hid; premasked) and linear1's input gradient dH W1 (handed to prod's backward through
+    tape.prefused_dx).  None when the kernel does not apply (then the two-GEMM path runs)."""
+    if not ffn_fuse_enabled() or not prod.needs[0]:
+        return None
+    mod1 = prod.attrs["mod"]
+    if _fp8.dgrad_on_mx8(dpre, mod) or _fp8.dgrad_on_mx8(dpre, mod1):
+        return None
+    w2, w1 = mod.compute_weight(), mod1.compute_weight()
+    if not ops.ffn_bwd_dgrad_ok(dpre, w2, w1, hid):
+        return None
+    dh, dx1 = ops.ffn_bwd_dgrad(dpre, w2, w1, hid, alpha)
+    tape.prefused_dx[prod.idx] = dx1.view(-1)
+    return dh.view(-1)
 
 
 def ln_bwd_fuse_enabled():

@@ -234,6 +234,36 @@ def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0
     return dx
 
 
+def ffn_bwd_dgrad_ok(dy, w2, w1, hid):
+    """s2h_ffn_bwd_dgrad applies: bf16, d_model 256, hidden a multiple of 128, rows a multiple of 64,
+    contiguous weights, unit-stride 16-B aligned rows"""
+    if dy.dim() != 2 or hid.dim() != 2:
+        return False
+    R, H = hid.shape
+    return (all(t.dtype == torch.bfloat16 for t in (dy, w2, w1, hid)) and dy.shape == (R, 256)
+            and tuple(w2.shape) == (256, H) and tuple(w1.shape) == (H, 256) and H % 128 == 0 and R % 64 == 0
+            and w2.is_contiguous() and w1.is_contiguous() and hid.is_contiguous() and dy.stride(1) == 1
+            and dy.stride(0) % 8 == 0 and R * max(H, dy.stride(0)) < 2**31
+            and all(t.data_ptr() % 16 == 0 for t in (dy, w2, w1, hid)))
+
+
+def ffn_bwd_dgrad(dy, w2, w1, hid, alpha=1.0, dh=None, dx=None):
+    """Memory-attention FFN backward, input-gradient side, in one launch (csrc/ffn.hip):
+    dh = alpha * (dy @ w2) * [hid > 0] (linear1's pre-activation gradient) and dx = dh @ w1.
+    dy [R, 256], w2 [256, H] (linear2.weight), w1 [H, 256] (linear1.weight), hid [R, H] (linear2's
+    saved input).  Returns (dh, dx)."""
+    assert ffn_bwd_dgrad_ok(dy, w2, w1, hid)
+    R, H = hid.shape
+    if dh is None:
+        dh = torch.empty(R, H, device=dy.device, dtype=dy.dtype)
+    if dx is None:
+        dx = torch.empty(R, 256, device=dy.device, dtype=dy.dtype)
+    _dev(dy, w2, w1, hid, dh, dx)
+    call("s2h_ffn_bwd_dgrad", R, H, ptr(dy), dy.stride(0), ptr(w2), ptr(w1), ptr(hid), H, float(alpha), ptr(dh),
+         dh.stride(0), ptr(dx), dx.stride(0), stream())
+    return dh, dx
+
+
 def linear_dgrad_ln_bwd_ok(dy, w, x):
     """s2h_linear_dgrad_ln_bwd applies: bf16, LayerNorm width 128 / 256, 16-B aligned rows"""
     K = w.shape[1]

@@ -203,6 +203,43 @@ def test_wgrad_deterministic(rows, N, K):
     _close(outs[0][1], dy.float().sum(0), 1e-4)
 
 
+@pytest.mark.parametrize("rows,H,p", [(93184, 2048, 0.1), (1024, 2048, 0.0), (64, 128, 0.25), (13312, 384, 0.1)])
+def test_ffn_bwd_dgrad(rows, H, p):
+    """memory-attention FFN backward, input-gradient side, in one launch (csrc/ffn.hip): dH = (dY W2) *
+    [hid > 0] / keep and dX = dH W1 against the fp32 products (dX from the kernel's own bf16 dH, as the
+    two-GEMM path computes it), the two-GEMM path itself, and bit-identical repeats.  The bench shape
+    (93 184 rows, H 2048), one chunk (H 128), a single tile."""
+    ops = _ops()
+    torch.manual_seed(5)
+    bf = torch.bfloat16
+    dy = torch.randn(rows, 256, device=DEV).to(bf)
+    w2 = (torch.randn(256, H, device=DEV) / math.sqrt(H)).to(bf)
+    w1 = (torch.randn(H, 256, device=DEV) / 16).to(bf)
+    hid = torch.relu(torch.randn(rows, H, device=DEV)).to(bf)
+    if p > 0:  # dropped elements are zeros of hid too
+        hid = hid * (torch.rand(rows, H, device=DEV) >= p).to(bf)
+    alpha = 1.0 / (1.0 - p)
+    dh, dx = ops.ffn_bwd_dgrad(dy, w2, w1, hid, alpha)
+    torch.cuda.synchronize()
+    ref_h = alpha * (dy.float() @ w2.float()) * (hid > 0).float()
+    _close(dh.float(), ref_h, 8e-3)
+    assert not dh[hid == 0].any()
+    _close(dx.float(), dh.float() @ w1.float(), 8e-3)
+    # the two-GEMM path
+    dh2 = ops.linear_dgrad(dy, w2, pre=hid, act="relu", alpha=alpha)
+    dx2 = ops.linear_dgrad(dh2, w1)
+    _close(dh.float(), dh2.float(), 8e-3)
+    _close(dx.float(), dx2.float(), 8e-3)
+    for _ in range(2):
+        dh3, dx3 = ops.ffn_bwd_dgrad(dy, w2, w1, hid, alpha)
+        assert torch.equal(dh3, dh) and torch.equal(dx3, dx)
+    # strided dY rows (a view of a wider buffer)
+    wide = torch.zeros(rows, 264, device=DEV, dtype=bf)
+    wide[:, :256] = dy
+    dh4, dx4 = ops.ffn_bwd_dgrad(wide[:, :256], w2, w1, hid, alpha)
+    assert torch.equal(dh4, dh) and torch.equal(dx4, dx)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,cols", [(131072, 112), (13312, 2048), (5, 24), (1000, 37), (70000, 256), (3, 4096)])
 def test_colsum_shapes(dtype, rows, cols):
