@@ -9,6 +9,14 @@ in HBM before the timed region.  Prints ONE JSON line on rank 0.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+The roofline (N = 1): before it touches the GPU, bench.py runs a copy of itself under
+`rocprofv3 --kernel-trace` (--trace-child: same workload, --trace-steps timed replays between the
+trace markers); per-family and dominant-kernel durations come from that trace of the timed replays,
+algorithmic flops per launch from the in-library profiler's records of one eager step after the
+timed region.  The event-bracketed durations of that eager step ride along under
+roofline.event_based.  --trace-out writes the trace's per-kernel CSV (tools/step_profile.py reads it
+with the same bench line).  --no-trace skips the traced run.
 """
 from __future__ import annotations
 
@@ -59,6 +67,11 @@ def parse():
                     help="launch every kernel from Python each step instead of replaying the captured HIP graph")
     ap.add_argument("--kernel-table", action="store_true",
                     help="after timing, profile one extra step and print per-shape GEMM/attention TF/s to stderr")
+    ap.add_argument("--no-trace", action="store_true",
+                    help="skip the rocprofv3 kernel-trace run that the roofline's durations come from (N=1)")
+    ap.add_argument("--trace-steps", type=int, default=5, help="timed steps of the traced run")
+    ap.add_argument("--trace-out", default=None, help="write the traced run's per-kernel CSV here")
+    ap.add_argument("--trace-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.config == 5:
         args.frames = 16
@@ -198,6 +211,110 @@ def kernel_name(kind, tag):
     return f"gemm16g_kernel<{bm}, {bn}, {wgm}, {wgn}, {ns}, {bk}, {tf(akc)}, {tf(bkc)}>"
 
 
+# kernel-name families of the rocprofv3 trace, matching the in-library profiler's record kinds
+TRACE_FAMILY_RX = {4: r"gemm16[ag]?_kernel|gemm16_kernel|gemm_kernel<|gemm_wg|ffn_bwd",
+                   40: r"gemm_mx8|mx8_quant",
+                   1: r"flash_fwd|flash_combine|attn_fwd|attn_win_fwd",
+                   2: r"flash_bwd|attn_bwd|attn_win_bwd|attn_fewq_dkv|attn_fewk_dq"}
+
+
+def traced_run(args):
+    """A child `rocprofv3 --kernel-trace -- python bench.py --trace-child ...` of the same workload
+    (started before this process touches the GPU): per-kernel (name, calls, total ms) of the dispatches
+    between its trace markers, i.e. its timed graph replays; (rows, steps, note)"""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, 0, "rocprofv3 not found"
+    tdir = tempfile.mkdtemp(prefix="s2h_trace_")
+    cmd = [prof, "--kernel-trace", "-f", "csv", "-d", tdir, "-o", "kt", "--", sys.executable,
+           os.path.abspath(__file__), "--trace-child", "--no-trace", "--no-prof", "--cpu-baseline", "0",
+           "--steps", str(args.trace_steps), "--warmup", "2", "--size", args.size, "--image-size",
+           str(args.image_size), "--frames", str(args.frames), "--objects", str(args.objects), "--dtype",
+           args.dtype, "--config", str(args.config), "--trainable", args.trainable]
+    if args.dropout is not None:
+        cmd += ["--dropout", str(args.dropout)]
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, timeout=420)
+        if r.returncode != 0:
+            return None, 0, f"traced run exited {r.returncode}: {r.stderr.decode(errors='replace')[-300:]}"
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import step_profile
+        rows = step_profile.load_region(tdir, verbose=False)
+        if not rows:
+            return None, 0, "no kernel trace written"
+        if args.trace_out:
+            step_profile.write_stats(rows, args.trace_steps, args.trace_out)
+        return rows, args.trace_steps, "ok"
+    except Exception as e:  # the trace refines the roofline; it is never required
+        return None, 0, f"trace failed: {e!r}"
+    finally:
+        shutil.rmtree(tdir, ignore_errors=True)
+
+
+def trace_roofline(rows, tsteps, recs3, kind_hint=None):
+    """The roofline from the kernel trace of the timed replays: per family, the algorithmic flops of
+    one step (the in-library profiler's records of the profiled eager step: shapes only, its event
+    times unused) over the family's kernel time per step in the trace; the dominant family is the one
+    with the most traced time, its dominant kernel the traced kernel with the most time, priced with
+    the flops per launch of the records that launched that kernel (bench.kernel_name of their tags)."""
+    import re
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import step_profile
+    fam_ms, fam_calls = {}, {}
+    per_name = {}
+    for name, calls, ms in rows:
+        sn = step_profile.short(name)
+        per_name[sn] = (calls, ms)
+        for k, rx in TRACE_FAMILY_RX.items():
+            if re.search(rx, name):
+                fam_ms[k] = fam_ms.get(k, 0.0) + ms / tsteps
+                fam_calls[k] = fam_calls.get(k, 0) + calls / tsteps
+                break
+    fl, by, names = {}, {}, {}
+    for ms, m, tag in recs3:
+        k = 40 if m[0] == 4 and (m[5] & 8) else m[0]
+        fl[k] = fl.get(k, 0.0) + record_flops(m[0], m)
+        by[k] = by.get(k, 0.0) + record_bytes(m[0], m)
+        a = names.setdefault(kernel_name(m[0], tag), [0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += record_flops(m[0], m)
+        a[2] += record_bytes(m[0], m)
+    if not fam_ms or not fl:
+        return None
+    peak = lambda kk: PEAK_FP8_TFLOPS if kk == 40 else PEAK_BF16_TFLOPS  # noqa: E731
+    table = {}
+    for k in fam_ms:
+        if k not in fl:
+            continue
+        ach = fl[k] / (fam_ms[k] * 1e-3) / 1e12
+        table[FAMILY[k].split(" (")[0]] = {"ms_per_step": round(fam_ms[k], 3), "tflop_per_step": round(fl[k] / 1e12, 4),
+                                          "achieved": round(ach, 1), "frac": round(ach / peak(k), 4),
+                                          "kernels_per_step": round(fam_calls[k], 1)}
+    k = kind_hint if kind_hint in fam_ms and kind_hint in fl else max((kk for kk in fam_ms if kk in fl),
+                                                                      key=lambda kk: fam_ms[kk])
+    ach = fl[k] / (fam_ms[k] * 1e-3) / 1e12
+    out = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak(k), "unit": "TFLOP/s", "frac": round(ach / peak(k), 4),
+           "kernel": FAMILY[k], "kernels_per_step": round(fam_calls[k], 1), "ms_per_step": round(fam_ms[k], 3),
+           "alg_flop_per_step": fl[k], "alg_bytes_per_step": by[k], "families": table, "_kind": k}
+    # dominant kernel: the family's traced kernel with the most time that the profiler records name
+    cands = [(n, c, ms) for n, (c, ms) in per_name.items() if n in names
+             and re.search(TRACE_FAMILY_RX[k], n)]
+    if cands:
+        n, c, ms = max(cands, key=lambda r: r[2])
+        rn, rfl, rby = names[n]
+        avg_us = 1e3 * ms / c
+        a = rfl / rn / (avg_us * 1e-6) / 1e12
+        out["dominant_kernel"] = {"name": n, "launches_per_step": round(c / tsteps, 1), "avg_us": round(avg_us, 2),
+                                  "alg_flop_per_launch": round(rfl / rn), "alg_bytes_per_launch": round(rby / rn),
+                                  "achieved_tflops": round(a, 1), "frac": round(a / peak(k), 4),
+                                  "share_of_family_ms": round(ms / tsteps / fam_ms[k], 3),
+                                  "profiled_launches_per_step": rn}
+    return out
+
+
 def event_overhead_ms(_lib, n=64):
     """Per-record overhead of the in-library event brackets: `n` empty kernels (s2h_trace_marker)
     each bracketed like a profiled launch, minus the per-kernel time of `n` back-to-back empty
@@ -335,6 +452,11 @@ def main():
     args = parse()
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
+    trace = (None, 0, "off")
+    under_profiler = any(k.startswith("ROCPROF") for k in os.environ)  # never nest a traced run in one
+    if (not args.no_trace and not args.trace_child and not args.no_prof and args.gpus == 1 and not under_profiler
+            and os.environ.get("WORLD_SIZE", "1") == "1"):
+        trace = traced_run(args)  # before this process initialises the GPU
     from sam2_video.data.synthetic import make_clip, sam2_collate_fn
     from sam2_video.kernels import _lib
     from sam2_video.kernels import functional as FN
@@ -444,12 +566,32 @@ def main():
                 roof["traffic_source"] = src
             roof["timing"] = ("HIP events per launch, one eager step after the timed graph replays" if graph
                               else "HIP events per launch over the timed region")
+            rows, tsteps, note = trace
+            troof = trace_roofline(rows, tsteps, recs3) if rows else None
+            if troof is not None:
+                # the trace drives bound / achieved / frac / dominant_kernel; the event-bracketed figures
+                # stay beside them for comparison
+                troof.pop("_kind")
+                ev = {k: roof[k] for k in ("kernel", "achieved", "frac", "launches", "avg_launch_ms", "families",
+                                          "dominant_kernel", "timing") if k in roof}
+                for k in ("traffic", "traffic_unit", "traffic_source", "alg_bytes_per_launch"):
+                    if k in roof:
+                        troof[k] = roof[k]
+                troof["timing"] = (f"rocprofv3 kernel trace of the {tsteps} timed graph replays of a traced run of "
+                                   "this workload (bench.py --trace-child, started before the timed run); flops "
+                                   "per launch from the in-library profiler's records of one eager step")
+                troof["event_based"] = ev
+                roof = troof
+            else:
+                roof["trace"] = note
         if args.kernel_table and rank == 0:
             print(kernel_table(recs), file=sys.stderr, flush=True)
         _lib.call("s2h_prof_select", 1)
 
     frames = args.frames * args.steps * world
     value = frames / elapsed
+    if args.trace_child:  # the traced run only supplies the kernel trace of its timed replays
+        return
 
     # validation IoU (eval/eval.py formulas, in-loop) on a held-out synthetic clip per rank
     val_clip = make_clip(100_000 + rank, args.frames, args.image_size, args.objects, args.objects)

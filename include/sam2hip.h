@@ -404,6 +404,15 @@ int s2h_copy2d_batch(int n, const void* const* src, void* const* dst, const int6
  * (backbones/utils.py:16-60); accum adds into dst. */
 int s2h_window(int dt, int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum,
                hipStream_t st);
+/* window_partition of a per-token projection's output with the padded positions set to padrow
+ * (fp32 [C], rounded to dt): with padrow = the projection's bias this equals the projection of the
+ * zero-padded partition (hieradet.py:146 pads before attn.qkv), so the projection runs over the real
+ * tokens only.  C a multiple of 16 B, 16-B aligned tensors. */
+int s2h_window_pad(int dt, int B, int H, int W, int C, int ws, const void* src, const float* padrow, void* dst,
+                   hipStream_t st);
+/* Its bias gradient: out[c] += sum of win[row][c] over the padded rows of the windowed tensor
+ * (fixed-order partial sums). */
+int s2h_window_pad_colsum(int dt, int B, int H, int W, int C, int ws, const void* win, float* out, hipStream_t st);
 /* FPN top-down: out = lat + nearest_up2(prev) (image_encoder.py:102-134). */
 int s2h_up2_add(int dt, int B, int H, int W, int C, const void* lat, const void* prev, void* out, hipStream_t st);
 /* Backward of the nearest 2x upsample: dprev (+)= 2x2 sum of dout. */

@@ -583,6 +583,127 @@ __global__ void window_vec_kernel(int B, int H, int W, int C, int ws, const void
   }
 }
 
+// Window partition of a per-token projection's OUTPUT (round 5): the padded positions get `padrow`
+// (fp32, rounded to T) instead of zeros -- the projection of a zero-padded input row is its bias, so
+// partition(linear(x)) with padrow = bias equals linear(partition(x)) bit for bit, and the
+// projection runs over the real tokens only (hieradet.py:146 pads before the qkv projection).
+template <typename T>
+__global__ void window_pad_vec_kernel(int B, int H, int W, int C, int ws, const T* src, const float* padrow, T* dst) {
+  constexpr int VEC = V16<T>::VEC;
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws, cc = C / VEC;
+  const int64_t n = (int64_t)B * nh * nw * ws * ws * cc;
+  GRID_STRIDE(i, n) {
+    const int ii = (int)i;
+    int p = ii / cc;
+    const int c = (ii - p * cc) * VEC;
+    const int ix = p % ws; p /= ws;
+    const int iy = p % ws; p /= ws;
+    const int wx = p % nw; p /= nw;
+    const int wy = p % nh;
+    const int b = p / nh;
+    const int yy = wy * ws + iy, xx = wx * ws + ix;
+    float v[VEC];
+    if (yy < H && xx < W) {
+      V16<T>::load(src + (((int64_t)b * H + yy) * W + xx) * C + c, v);
+    } else {
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) v[j] = padrow[c + j];
+    }
+    V16<T>::store(dst + (int64_t)ii * VEC, v);
+  }
+}
+
+extern "C" int s2h_window_pad(int dt, int B, int H, int W, int C, int ws, const void* src, const float* padrow, void* dst,
+                              hipStream_t st) {
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws;
+  const int64_t n = (int64_t)B * nh * nw * ws * ws * C;
+  if (n <= 0) return 0;
+  const int vec = dt == S2H_BF16 ? 8 : 4;
+  if (C % vec || !al16(src) || !al16(dst) || n / vec >= (1ll << 31) || !padrow) return (int)hipErrorInvalidValue;
+  if (dt == S2H_BF16)
+    hipLaunchKernelGGL(window_pad_vec_kernel<bf16>, ew_grid(n / vec), dim3(256), 0, st, B, H, W, C, ws,
+                       (const bf16*)src, padrow, (bf16*)dst);
+  else
+    hipLaunchKernelGGL(window_pad_vec_kernel<float>, ew_grid(n / vec), dim3(256), 0, st, B, H, W, C, ws,
+                       (const float*)src, padrow, (float*)dst);
+  return (int)hipGetLastError();
+}
+
+// Its bias gradient: out[c] += sum over the PADDED rows of the windowed gradient (the rows whose
+// input was the zero padding; their projection output was the bias).  Padded positions of one image,
+// in the padded (Hp, Wp) frame: rows y >= H (all x), then rows y < H with x >= W.  Block = 32 column
+// groups of 16 B x 8 row lanes over one chunk of padded rows; the 8 lanes' sums are added in fixed
+// order through LDS, the chunk's partial row goes to the workspace and det_colsum finishes (or float
+// atomics without the deterministic workspace).
+template <typename T>
+__global__ __launch_bounds__(256) void window_pad_colsum_kernel(int B, int H, int W, int C, int ws, const T* win,
+                                                                int rows_per_chunk, float* out, float* part) {
+  constexpr int VEC = V16<T>::VEC;
+  const int cg = threadIdx.x & 31, lane = threadIdx.x >> 5;
+  const int c = (blockIdx.x * 32 + cg) * VEC;
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws, Hp = nh * ws, Wp = nw * ws;
+  const int P = Hp * Wp - H * W, rows = B * P, top = (Hp - H) * Wp;
+  const int r0 = blockIdx.y * rows_per_chunk, r1 = min(rows, r0 + rows_per_chunk);
+  float acc[VEC];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) acc[j] = 0.f;
+  if (c < C) {
+    for (int r = r0 + lane; r < r1; r += 8) {
+      const int b = r / P;
+      int q = r - b * P, y, x;
+      if (q < top) { y = H + q / Wp; x = q - (q / Wp) * Wp; }
+      else { q -= top; y = q / (Wp - W); x = W + q - y * (Wp - W); }
+      const int64_t wrow = (((int64_t)(b * nh + y / ws) * nw + x / ws) * ws + y % ws) * ws + x % ws;
+      float v[VEC];
+      V16<T>::load(win + wrow * C + c, v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) acc[j] += v[j];
+    }
+  }
+  __shared__ float red[8][32 * 8 + 4];
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) red[lane][cg * VEC + j] = acc[j];
+  __syncthreads();
+  // 256 threads finish the block's 32 * VEC columns: thread t -> column t (VEC 8: 256 columns)
+  const int cl = threadIdx.x;
+  if (cl < 32 * VEC) {
+    const int cc = blockIdx.x * 32 * VEC + cl;
+    if (cc < C) {
+      float s2 = 0.f;
+#pragma unroll
+      for (int l = 0; l < 8; ++l) s2 += red[l][cl];
+      if (part) part[(int64_t)blockIdx.y * C + cc] = s2;
+      else atomicAdd(&out[cc], s2);
+    }
+  }
+}
+
+extern "C" int s2h_window_pad_colsum(int dt, int B, int H, int W, int C, int ws, const void* win, float* out,
+                                     hipStream_t st) {
+  const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws;
+  const int64_t rows = (int64_t)B * ((int64_t)nh * ws * nw * ws - (int64_t)H * W);
+  const int vec = dt == S2H_BF16 ? 8 : 4;
+  if (C % vec || !al16(win) || rows >= (1ll << 31)) return (int)hipErrorInvalidValue;
+  if (rows <= 0 || C <= 0) return 0;
+  // chunks of >= 32 rows, <= 256 of them (the fixed-order finalize's partial rows)
+  int rpc = 32;
+  int nchunk = (int)((rows + rpc - 1) / rpc);
+  if (nchunk > 256) {
+    rpc = (int)((rows + 255) / 256);
+    nchunk = (int)((rows + rpc - 1) / rpc);
+  }
+  float* part = s2h_det_ws(nchunk * C * (int64_t)sizeof(float));
+  const dim3 grid((unsigned)((C / vec + 31) / 32), (unsigned)nchunk);
+  if (dt == S2H_BF16)
+    hipLaunchKernelGGL(window_pad_colsum_kernel<bf16>, grid, dim3(256), 0, st, B, H, W, C, ws, (const bf16*)win, rpc,
+                       out, part);
+  else
+    hipLaunchKernelGGL(window_pad_colsum_kernel<float>, grid, dim3(256), 0, st, B, H, W, C, ws, (const float*)win, rpc,
+                       out, part);
+  if (part) det_colsum(1, nchunk, C, part, out, 1, st);
+  return (int)hipGetLastError();
+}
+
 extern "C" int s2h_window(int dt, int B, int H, int W, int C, int ws, const void* src, void* dst, int dir, int accum,
                           hipStream_t st) {
   const int nh = (H + ws - 1) / ws, nw = (W + ws - 1) / ws;

@@ -85,6 +85,8 @@ SIGNATURES = {
     "s2h_maxpool2_fwd": [I, I, I, I, I, P, L, P, P],
     "s2h_maxpool2_bwd": [I, I, I, I, I, P, L, P, P, L, P],
     "s2h_window": [I, I, I, I, I, I, P, P, I, I, P],
+    "s2h_window_pad": [I, I, I, I, I, I, P, P, P, P],
+    "s2h_window_pad_colsum": [I, I, I, I, I, I, P, P, P],
     "s2h_copy2d_batch": [I, P, P, P, P, P, P, P],
     "s2h_up2_add": [I, I, I, I, I, P, P, P, P],
     "s2h_pool2_sum": [I, I, I, I, I, P, P, I, P],

@@ -805,6 +805,34 @@ class _WindowUnpartition(torch.autograd.Function):
         return ops.window_partition(g.contiguous(), ctx.ws), None, None, None, None
 
 
+class _WindowPad(torch.autograd.Function):
+    """partition(linear(x)) with the padded positions = linear's bias (= linear(partition(x)) of the
+    zero-padded partition, hieradet.py:146): the linear ran over the real tokens only.  Backward: the
+    real rows' gradient by unpartition; the padded rows' column sums go to the linear's bias
+    gradient (the arena; accumulating, like every weight-gradient write of the step)."""
+
+    @staticmethod
+    def forward(ctx, y, ws, mod):
+        ctx.ws, ctx.shape, ctx.mod = ws, y.shape, mod
+        return ops.window_pad(y.contiguous(), ws, mod.compute_bias())
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        B, H, W, C = ctx.shape
+        gb = ctx.mod.grad_views()[1]
+        if gb is not None:
+            ops.window_pad_colsum(g, ctx.ws, B, H, W, gb.view(-1))
+        return ops.window_unpartition(g, ctx.ws, B, H, W), None, None
+
+
+def window_pad(y, ws, mod):
+    """partition of linear `mod`'s output y [B, H, W, C] into ws x ws windows, padded positions = the
+    bias (what `mod` gives for a zero-padded input row)"""
+    assert mod.compute_bias() is not None
+    return _WindowPad.apply(y, int(ws), mod)
+
+
 def window_partition(x, ws):
     return _WindowPartition.apply(x, int(ws))
 

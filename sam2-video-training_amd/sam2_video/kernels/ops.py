@@ -769,6 +769,28 @@ def window_partition(x, ws, out=None, accumulate=False):
     return out
 
 
+def window_pad(x, ws, padrow, out=None):
+    """window_partition of a projection's output x [B, H, W, C] with the padded positions = padrow
+    (fp32 [C], the projection's bias): [B * nh * nw, ws, ws, C]"""
+    B, H, W, C = x.shape
+    nh, nw = -(-H // ws), -(-W // ws)
+    assert padrow.dtype == torch.float32 and padrow.numel() == C and padrow.is_contiguous() and x.is_contiguous()
+    if out is None:
+        out = torch.empty(B * nh * nw, ws, ws, C, device=x.device, dtype=x.dtype)
+    _dev(x, padrow, out)
+    call("s2h_window_pad", dt(x), B, H, W, C, ws, ptr(x), ptr(padrow), ptr(out), stream())
+    return out
+
+
+def window_pad_colsum(win, ws, B, H, W, out):
+    """out (fp32 [C]) += the column sums of win's padded rows (window_pad's bias gradient)"""
+    C = win.shape[-1]
+    assert out.dtype == torch.float32 and out.numel() == C and out.is_contiguous() and win.is_contiguous()
+    _dev(win, out)
+    call("s2h_window_pad_colsum", dt(win), B, H, W, C, ws, ptr(win), ptr(out), stream())
+    return out
+
+
 def window_unpartition(win, ws, B, H, W, out=None, accumulate=False):
     C = win.shape[-1]
     if out is None:

@@ -3,13 +3,15 @@ sam2.modeling.backbones.hieradet), NHWC on the device.
 
 Same constructor signature / parameter names as the reference (hieradet.py:169-262)
 so SAM2.1 checkpoints load.  Per block: LayerNorm kernel -> (proj + 2x2 max-pool
-shortcut) -> window partition (zero pad) -> fused qkv GEMM -> (q max-pool read
+shortcut) -> window partition (zero pad; windows that need padding partition the qkv
+projection of the real tokens with bias rows instead) -> fused qkv GEMM -> (q max-pool read
 in place from the qkv tensor) -> flash attention over [windows, L, heads, d] ->
 proj GEMM -> unpartition -> residual-add fused into norm2 -> MLP GEMMs (GELU in
 the epilogue, residual in the second epilogue).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Tuple
 
 import torch
@@ -19,6 +21,12 @@ from ....kernels import functional as FN
 from ....kernels import ops
 from ....kernels.functional_sam import hiera_pos_embed
 from ..layers import MLP, Conv2d, LayerNorm, Linear
+
+
+def _pad_after_qkv():
+    """S2H_HIERA_PAD_QKV=0: padded windows partition the normed input (zero rows) before the qkv
+    projection, as the reference does, instead of the projection's output (bias rows)"""
+    return os.environ.get("S2H_HIERA_PAD_QKV", "1") == "1"
 
 
 class MultiScaleAttention(nn.Module):
@@ -73,13 +81,24 @@ class MultiScaleBlock(nn.Module):
                 shortcut = FN.maxpool2(shortcut)
         ws = self.window_size
         H, W = xn.shape[1:3]
-        xw = FN.window_partition(xn, ws) if ws > 0 else xn
-        y = self.attn(xw)
-        if self.q_stride:
-            ws = ws // self.q_stride[0]
-            H, W = shortcut.shape[1:3]
-        if self.window_size > 0:
-            y = FN.window_unpartition(y, ws, B, H, W)
+        if ws > 0 and not self.q_stride and (H % ws or W % ws) and _pad_after_qkv():
+            # windows that need padding (stage 3: 32 -> 42, stage 4: 16 -> 21 at 512^2): the qkv
+            # projection of a zero-padded row is its bias, so project the real tokens only, partition
+            # the projection with bias rows, and project back after unpartition -- the qkv and proj
+            # GEMMs (and their backward) run on H*W instead of the padded rows (0.58x at 512^2)
+            a = self.attn
+            qkvw = FN.window_pad(a.qkv(xn), ws, a.qkv)
+            nwin, d, nh = qkvw.shape[0], a.dim_out, a.num_heads
+            o = FN.qkv_attention(qkvw.view(nwin, ws * ws, 3, nh, d // nh))
+            y = a.proj(FN.window_unpartition(o.reshape(nwin, ws, ws, d), ws, B, H, W))
+        else:
+            xw = FN.window_partition(xn, ws) if ws > 0 else xn
+            y = self.attn(xw)
+            if self.q_stride:
+                ws = ws // self.q_stride[0]
+                H, W = shortcut.shape[1:3]
+            if self.window_size > 0:
+                y = FN.window_unpartition(y, ws, B, H, W)
         h, x = FN.add_layer_norm(shortcut, y, self.norm2, self.norm2.eps)
         fc1, fc2 = self.mlp.layers[0], self.mlp.layers[1]
         if next_norm is None:

@@ -241,6 +241,72 @@ def test_ffn_bwd_dgrad(rows, H, p):
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,H,W,C,ws", [(8, 32, 32, 1344, 14), (8, 16, 16, 2688, 7), (2, 9, 13, 48, 4), (1, 8, 8, 16, 8)])
+def test_window_pad(dtype, B, H, W, C, ws):
+    """partition of a projection's output with bias rows at the padded positions (Hiera's padded windows,
+    csrc/elementwise.hip window_pad_vec_kernel) against zero-pad + partition + bias fill in torch, and
+    its bias gradient (the padded rows' column sums, window_pad_colsum_kernel) against torch"""
+    ops = _ops()
+    ops.wgrad_workspace(DEV)  # the deterministic-reduction workspace (SAM2Model.load registers it)
+    torch.manual_seed(7)
+    x = torch.randn(B, H, W, C, device=DEV).to(dtype)
+    bias = torch.randn(C, device=DEV)
+    nh, nw = -(-H // ws), -(-W // ws)
+    pad = torch.zeros(B, nh * ws, nw * ws, C, device=DEV, dtype=dtype)
+    pad[:] = bias.to(dtype)
+    pad[:, :H, :W] = x
+    ref = pad.view(B, nh, ws, nw, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B * nh * nw, ws, ws, C)
+    out = ops.window_pad(x, ws, bias)
+    assert torch.equal(out, ref)
+    g = torch.randn(B * nh * nw, ws, ws, C, device=DEV).to(dtype)
+    gp = g.view(B, nh, nw, ws, ws, C).permute(0, 1, 3, 2, 4, 5).reshape(B, nh * ws, nw * ws, C).float()
+    mask = torch.ones(nh * ws, nw * ws, dtype=torch.bool, device=DEV)
+    mask[:H, :W] = False
+    want = gp[:, mask].sum((0, 1)) + 0.5
+    got = torch.full((C,), 0.5, device=DEV)
+    ops.window_pad_colsum(g, ws, B, H, W, got)
+    _close(got, want, 1e-5)
+    again = torch.full((C,), 0.5, device=DEV)
+    ops.window_pad_colsum(g, ws, B, H, W, again)
+    assert torch.equal(again, got)
+
+
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+@pytest.mark.parametrize("dim,heads,ws,HW", [(448, 8, 14, 32), (896, 8, 7, 16)])
+def test_hiera_padded_window_block(compute, dim, heads, ws, HW, monkeypatch):
+    """a Hiera block whose windows need padding (B+ at 512^2: stage 3, 32 -> 42; stage 4, 16 -> 21) with the
+    qkv projection over the real tokens + bias-row partition (hieradet.py, S2H_HIERA_PAD_QKV=1) against the
+    reference order (zero-pad the normed input, project every padded row; =0): the block output
+    bit-identical, every parameter gradient within summation order"""
+    from sam2_video.kernels.arena import ParamArena
+    from sam2_video.model.modeling.backbones.hieradet import MultiScaleBlock
+    _ops().wgrad_workspace(DEV)
+    torch.manual_seed(11)
+    blk = MultiScaleBlock(dim, dim, heads, window_size=ws)
+    for p in blk.parameters():
+        p.data = torch.randn_like(p) * 0.05
+    cd = torch.float32 if compute == "fp32" else torch.bfloat16
+    arena = ParamArena(list(blk.named_parameters()), [n for n, _ in blk.named_parameters()], cd, DEV)
+    x0 = torch.randn(4, HW, HW, dim, device=DEV).to(cd)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("S2H_HIERA_PAD_QKV", flag)
+        arena.grad.zero_()
+        x = x0.clone().requires_grad_(True)
+        y = blk(x)
+        g = torch.randn(y.shape, device=DEV, generator=torch.Generator(DEV).manual_seed(3)).to(cd)
+        y.backward(g)
+        torch.cuda.synchronize()
+        res[flag] = (y.detach().clone(), x.grad.clone(), arena.grad.clone())
+    assert torch.equal(res["0"][0], res["1"][0])
+    tol = 1e-5 if compute == "fp32" else 1e-2
+    _close(res["1"][1], res["0"][1], tol)
+    for n in arena.grad_names:
+        o, k = arena.offsets[n], blk.get_parameter(n).numel()
+        _close(res["1"][2][o:o + k], res["0"][2][o:o + k], tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,cols", [(131072, 112), (13312, 2048), (5, 24), (1000, 37), (70000, 256), (3, 4096)])
 def test_colsum_shapes(dtype, rows, cols):
     ops = _ops()

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 TAG=${1:-prof}
 STEPS=${2:-10}
 RX='gemm|flash|attn_'
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${TAG}_kt -o kt -- python3 bench.py --steps $STEPS --warmup 3 --cpu-baseline 0 > gpurun_out/${TAG}_kt_bench.log 2>&1 || { echo KT_FAILED; tail -20 gpurun_out/${TAG}_kt_bench.log; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/${TAG}_kt -o kt -- python3 bench.py --no-trace --steps $STEPS --warmup 3 --cpu-baseline 0 > gpurun_out/${TAG}_kt_bench.log 2>&1 || { echo KT_FAILED; tail -20 gpurun_out/${TAG}_kt_bench.log; exit 1; }
 tail -1 gpurun_out/${TAG}_kt_bench.log | cut -c1-200
 python3 tools/step_profile.py gpurun_out/${TAG}_kt gpurun_out/${TAG}_kernel_stats.csv --steps $STEPS --bench gpurun_out/${TAG}_kt_bench.log || exit 1
 if [ -n "$NO_PMC" ]; then echo PROF_DONE; exit 0; fi

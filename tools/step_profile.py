@@ -1,6 +1,8 @@
 """Per-step kernel table of the timed graph replays from a rocprofv3 `--kernel-trace --stats -f csv`
 run of bench.py: only the dispatches between the two trace markers bench.py launches around its
 timed steps (s2h_trace_marker_kernel) count -- no setup copies, no warm-up, no profiled eager step.
+`dir` may also be the per-kernel CSV bench.py itself writes from its traced run (--trace-out), so the
+table and the bench line come from one trace.
 
 Writes a CSV (name, calls, calls_per_step, total_ms, ms_per_step, avg_us, pct) and prints the
 per-family split; with --bench <bench JSON line> it also recomputes the roofline's dominant-kernel
@@ -25,7 +27,7 @@ FAMILIES = [("GEMM (bf16)", r"gemm16[ag]?_kernel|gemm_kernel<|gemm_wg|ffn_bwd"),
             ("stock torch", r"at::|elementwise_kernel|vectorized|__amd_rocclr|Memset|fill")]
 
 
-def load_region(path):
+def load_region(path, verbose=True):
     """per-kernel (name, calls, total ms) of the dispatches between bench.py's two trace markers
     (s2h_trace_marker_kernel) in a rocprofv3 kernel-trace CSV; None if there is no such trace"""
     traces = glob.glob(os.path.join(path, "**", "*kernel_trace.csv"), recursive=True)
@@ -38,18 +40,27 @@ def load_region(path):
     rows.sort()
     marks = [i for i, r in enumerate(rows) if "s2h_trace_marker_kernel" in r[2]]
     if len(marks) < 2:
-        sys.exit(f"{traces[0]}: {len(marks)} trace markers (bench.py launches one before and one after the timed steps)")
+        raise ValueError(f"{traces[0]}: {len(marks)} trace markers (bench.py launches one before and one after the "
+                         "timed steps)")
     agg = {}
     for st, en, name in rows[marks[0] + 1:marks[1]]:
         a = agg.setdefault(name, [0, 0.0])
         a[0] += 1
         a[1] += (en - st) / 1e6
     span = (rows[marks[1]][0] - rows[marks[0]][1]) / 1e6
-    print(f"timed region: {marks[1] - marks[0] - 1} dispatches, {span:.2f} ms wall between the markers")
+    if verbose:
+        print(f"timed region: {marks[1] - marks[0] - 1} dispatches, {span:.2f} ms wall between the markers")
     return [(n, c, t) for n, (c, t) in agg.items()]
 
 
 def load(path):
+    if os.path.isfile(path):  # a per-kernel CSV written by write_stats (bench.py --trace-out): totals
+        out = []
+        with open(path) as f:
+            next(f)
+            for r in csv.DictReader(f):
+                out.append((r["name"], int(r["calls"]), float(r["total_ms"])))
+        return out
     reg = load_region(path)
     if reg is not None:
         return reg
@@ -76,6 +87,24 @@ def short(name):
     return re.sub(r", GemmArgs16(Ln)?>$", ">", name)
 
 
+def family_of(name):
+    return next((fn for fn, pat in FAMILIES if re.search(pat, name)), "element-wise / other")
+
+
+def write_stats(rows, steps, out):
+    """the per-kernel CSV of `rows` [(name, calls, total ms)] over `steps` timed steps"""
+    rows = sorted(rows, key=lambda r: -r[2])
+    tot = sum(r[2] for r in rows)
+    with open(out, "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow([f"# rocprofv3 kernel trace of {steps} timed graph-replayed steps (the dispatches between "
+                    f"bench.py's trace markers); {tot / steps:.3f} ms of kernel time per step"])
+        w.writerow(["name", "calls", "calls_per_step", "total_ms", "ms_per_step", "avg_us", "pct"])
+        for n, c, t in rows:
+            w.writerow([short(n), c, round(c / steps, 2), round(t, 4), round(t / steps, 4),
+                        round(1e3 * t / c, 3), round(100 * t / tot, 2)])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
@@ -86,17 +115,10 @@ def main():
     a = ap.parse_args()
     rows = sorted(load(a.dir), key=lambda r: -r[2])
     tot = sum(r[2] for r in rows)
-    with open(a.out, "w", newline="") as f:
-        w = csv.writer(f)
-        w.writerow([f"# rocprofv3 kernel trace of {a.steps} timed graph-replayed steps (the dispatches between "
-                    f"bench.py's trace markers); {tot / a.steps:.3f} ms of kernel time per step"])
-        w.writerow(["name", "calls", "calls_per_step", "total_ms", "ms_per_step", "avg_us", "pct"])
-        for n, c, t in rows:
-            w.writerow([short(n), c, round(c / a.steps, 2), round(t, 4), round(t / a.steps, 4),
-                        round(1e3 * t / c, 3), round(100 * t / tot, 2)])
+    write_stats(rows, a.steps, a.out)
     fam = {}
     for n, c, t in rows:
-        k = next((fn for fn, pat in FAMILIES if re.search(pat, n)), "element-wise / other")
+        k = family_of(n)
         fam[k] = fam.get(k, 0.0) + t
     print(f"{tot / a.steps:.3f} ms kernel time per step over {a.steps} steps, {sum(r[1] for r in rows) / a.steps:.0f} "
           "kernels per step")
