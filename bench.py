@@ -196,10 +196,12 @@ def kernel_name(kind, tag):
                 2: "attention backward entry (flash_bwd kernels)"}.get(kind, "gemm_kernel (fp32)")
     bm, bn = tag & 0x3FF, (tag >> 10) & 0x3FF
     wgm, wgn, ns, bk = (tag >> 20) & 0xF, (tag >> 24) & 0xF, (tag >> 28) & 0xF, 32 * ((tag >> 32) & 0xF)
-    akc, bkc, regs, mx8, areg, wgdet, ffn = [bool((tag >> b) & 1) for b in (36, 37, 38, 39, 40, 41, 42)]
+    akc, bkc, regs, mx8, areg, wgdet, ffn, ffnf = [bool((tag >> b) & 1) for b in (36, 37, 38, 39, 40, 41, 42, 43)]
     tf = lambda x: "true" if x else "false"  # noqa: E731
     if ffn:  # memory-attention FFN backward input gradients in one launch (csrc/ffn.hip)
-        return "ffn_bwd_dgrad_kernel"
+        return f"(anonymous namespace)::ffn_bwd_dgrad_kernel<{bm}>((anonymous namespace)::FfnArgs)"
+    if ffnf:  # memory-attention FFN forward in one launch (csrc/ffn.hip, opt-in)
+        return "(anonymous namespace)::ffn_fwd_kernel"
     if wgdet:  # deterministic long-reduction weight gradient (csrc/gemm_wgrad.hip)
         return f"gemm_wg_kernel<{bm}, {bn}, {wgm}, {wgn}, {ns}>"
     if areg:  # short-K tiling with A in registers (gemm_bf16.h gemm16a_kernel, K <= 256)
@@ -212,7 +214,7 @@ def kernel_name(kind, tag):
 
 
 # kernel-name families of the rocprofv3 trace, matching the in-library profiler's record kinds
-TRACE_FAMILY_RX = {4: r"gemm16[ag]?_kernel|gemm16_kernel|gemm_kernel<|gemm_wg|ffn_bwd",
+TRACE_FAMILY_RX = {4: r"gemm16[ag]?_kernel|gemm16_kernel|gemm_kernel<|gemm_wg|ffn_",
                    40: r"gemm_mx8|mx8_quant",
                    1: r"flash_fwd|flash_combine|attn_fwd|attn_win_fwd",
                    2: r"flash_bwd|attn_bwd|attn_win_bwd|attn_fewq_dkv|attn_fewk_dq"}

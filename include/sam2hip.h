@@ -55,7 +55,7 @@ int s2h_prof_read(int max, float* ms, int64_t* meta);
 /* tags[i] = the kernel record i launched (0 = not tagged): GEMM tilings as
  * BM | BN << 10 | WGM << 20 | WGN << 24 | NS << 28 | (BK / 32) << 32 | A_kcontig << 36 |
  * B_kcontig << 37 | register_staged << 38 | mx_fp8 << 39 | a_in_registers << 40 |
- * deterministic_wgrad << 41 -- the template arguments of the kernel rocprofv3 names (bench.py: the
+ * deterministic_wgrad << 41 | ffn_bwd_dgrad << 42 | ffn_fwd << 43 -- the template arguments of the kernel rocprofv3 names (bench.py: the
  * roofline's dominant kernel). */
 int s2h_prof_read_tags(int max, int64_t* tags);
 /* Launches a one-lane no-op kernel (s2h_trace_marker_kernel) on `st`: brackets a region of a
@@ -315,6 +315,16 @@ int s2h_linear_add_ln(int M, int N, int K, const void* A, int64_t lda, const voi
  * bases, row strides multiples of 8 elements. */
 int s2h_ffn_bwd_dgrad(int R, int H, const void* dy, int64_t lddy, const void* w2, const void* w1, const void* hid,
                       int64_t ldh, float alpha, void* dh, int64_t lddh, void* dx, int64_t lddx, hipStream_t st);
+/* Memory-attention FFN forward, one launch (bf16; memory_attention.py:97, replacing linear1 + ReLU +
+ * dropout and linear2 + dropout as two GEMM launches):
+ *   hid [R, H] = drop1(relu(x [R, 256] w1 [H, 256]^T + b1))      (saved for the backward)
+ *   y [R, 256] = drop2(hid w2 [256, H]^T + b2)
+ * b1 / b2 fp32; dropout p with the GEMM epilogue's counter hash (seed1, element idx1 + row * H + h;
+ * seed2, idx2 + row * 256 + n), each seed folded with the bound RNG offset.  R a multiple of 64, H 1024
+ * or 2048; 16-B aligned bases, row strides multiples of 8 elements. */
+int s2h_ffn_fwd(int R, int H, const void* x, int64_t ldx, const void* w1, const float* b1, const void* w2,
+                const float* b2, float p, uint64_t seed1, uint64_t idx1, uint64_t seed2, uint64_t idx2, void* hid,
+                int64_t ldh, void* y, int64_t ldy, hipStream_t st);
 int64_t s2h_linear_dgrad_ln_bwd_ws_bytes(int M, int N);
 int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64_t ldg, const void* W, int64_t ldw, float alpha,
                             const void* X, int64_t ldx, const float* gamma, const float* mean, const float* rstd,

@@ -280,7 +280,303 @@ __global__ __launch_bounds__(256, 1) void ffn_bwd_dgrad_kernel(FfnArgs p) {
   }
 }
 
+// ================================================================================ forward
+// The same walk for the forward (memory_attention.py:97, per tracked frame: 13 312 rows):
+//   phase A  H_c^T = W1[c, :] x^T           (K = 256; x's tile resident in LDS)
+//   epilogue + b1, ReLU, dropout (the GEMM epilogue's counter hash, seed1 / element index
+//            idx1 + row * H + h), bf16 -> the hid image (phase C's operand) and, 16 B per lane, the
+//            saved hid (the backward's mask and dW2 operand)
+//   phase C  y^T += W2[:, c] H_c^T          (K = 128, registers)
+//   epilogue + b2, dropout (seed2, idx2 + row * 256 + n), bf16 -> y
+// = linear2(dropout(relu(linear1(x)))) -> dropout as two GEMM launches compute it, without writing and
+// re-reading hid between them.  Both weights are K-contiguous here (W1 [H][256] rows = hidden units,
+// W2 [256][H] rows = outputs): the ring steps are plain K-contiguous images (b128 fragment reads).
+#ifndef FFN_FWD_NS64
+#define FFN_FWD_NS64 6
+#endif
+constexpr int FFN_FWD_HMAX = 2048;
+using IF1 = GImg<FFN_HC, true, 4, 64>;  // W1 step: [128 h][64 k (d)], A operand of phase A
+using IF2 = GImg<FFN_D, true, 4, 32>;   // W2 step: [256 n][32 k (h)], A operand of phase C
+static_assert(IF1::BYTES == FFN_RING && IF2::BYTES == FFN_RING && IF1::PPW == 4 && IF2::PPW == 4, "ring steps");
+
+template <int BM, int NS>
+struct FfnFwdShape {
+  using IX = GImg<BM, true, 4, 64>;   // x tile: 4 x [BM r][64 k (d)], B operand of phase A
+  using IH = GImg<BM, true, 4, 64>;   // hid chunk: 2 x [BM r][64 k (h)], B operand of phase C
+  static constexpr int NI = BM / 32;
+  static constexpr int OFF_X = 0;
+  static constexpr int OFF_RING = OFF_X + 4 * IX::BYTES;
+  static constexpr int OFF_H = OFF_RING + NS * FFN_RING;
+  static constexpr int OFF_B1 = OFF_H + 2 * IH::BYTES;  // b1 (fp32, H <= FFN_FWD_HMAX), DMA'd at the start
+  static constexpr int LDS = OFF_B1 + FFN_FWD_HMAX * 4;
+  static constexpr int STW = BM / 16;            // hid 16-B stores per lane per chunk
+  static constexpr int XLD = FFN_D * 2 + 16;     // y staging row pitch (bytes)
+  static_assert(LDS <= 160 * 1024 && BM * XLD <= LDS, "LDS");
+};
+
+struct FfnFwdArgs {
+  int R, H;
+  const bf16* x; int64_t ldx;
+  const bf16* w1; const float* b1;   // [H][256], [H]   (linear1)
+  const bf16* w2; const float* b2;   // [256][H], [256] (linear2)
+  bf16* hid; int64_t ldh;
+  bf16* y; int64_t ldy;
+  float p;
+  uint64_t seed1, seed2, idx1, idx2;
+  const uint64_t* seed_off;
+};
+
+struct FfnFwdDma {
+  uint32_t w1[4], w2[4];
+  __device__ __forceinline__ void init(const FfnFwdArgs& p, int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int piece = w * 4 + i;
+      int r = piece * (1024 / IF1::RB) + lane / IF1::LPR;
+      w1[i] = (uint32_t)(r * FFN_D + 8 * IF1::swz(r, lane % IF1::LPR)) * 2u;
+      r = piece * (1024 / IF2::RB) + lane / IF2::LPR;
+      w2[i] = (uint32_t)(r * p.H + 8 * IF2::swz(r, lane % IF2::LPR)) * 2u;
+    }
+  }
+};
+
+// ring step q: chunk q / 8; steps 0-3 W1 (64-deep over d), 4-7 W2 (32-deep over the chunk's h)
+template <int BM, int NS>
+__device__ __forceinline__ void ffn_fwd_issue(char* smem, const FfnFwdArgs& p, const FfnFwdDma& d, int q, int w) {
+  using S = FfnFwdShape<BM, NS>;
+  char* slot = smem + S::OFF_RING + (q % NS) * FFN_RING;
+  const int c = q >> 3, sub = q & 7;
+  if (sub < 4) {
+    const uint64_t b = sgpr_base(p.w1 + (int64_t)c * FFN_HC * FFN_D + sub * 64);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds_dma16_so(b, d.w1[i], slot + (w * 4 + i) * 1024);
+  } else {
+    const uint64_t b = sgpr_base(p.w2 + c * FFN_HC + (sub - 4) * 32);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) lds_dma16_so(b, d.w2[i], slot + (w * 4 + i) * 1024);
+  }
+}
+
+// as ffn_wait: 4 DMAs per wave per step, the hid stores at the end of step 3
+template <int BM, int NS, int SUB>
+__device__ __forceinline__ void ffn_fwd_wait(bool first_chunk, bool last_chunk) {
+  using S = FfnFwdShape<BM, NS>;
+  constexpr int later = 4 * (NS - 2);
+  constexpr int own = (SUB >= 4 && SUB <= NS + 2) ? S::STW : 0;
+  constexpr bool prev = SUB + 8 <= NS + 2;
+  if (SUB + NS - 2 >= 8 && last_chunk) vm_wait<0>();
+  else if (prev && !first_chunk) vm_wait<later + own + S::STW>();
+  else vm_wait<later + own>();
+}
+
+// dropout keep flags of 4 consecutive elements starting at idx (the GEMM epilogue's form)
+__device__ __forceinline__ void keep4(uint64_t seed, uint64_t idx, uint32_t thresh, bool* k) {
+  if ((idx & 1) == 0) {
+    s2h_keep_pair(seed, idx >> 1, thresh, k[0], k[1]);
+    s2h_keep_pair(seed, (idx >> 1) + 1, thresh, k[2], k[3]);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) k[e] = s2h_keep(seed, idx + e, thresh);
+  }
+}
+
+template <int BM, int NS>
+__global__ __launch_bounds__(256, 1) void ffn_fwd_kernel(FfnFwdArgs p) {
+  using S = FfnFwdShape<BM, NS>;
+  using IX = typename S::IX;
+  using IH = typename S::IH;
+  constexpr int NI = S::NI;
+  __shared__ __attribute__((aligned(1024))) char smem[S::LDS];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r0 = blockIdx.x * BM;
+  const int nchunk = p.H / FFN_HC;
+  const int nq = nchunk * 8;
+  const int wc = w & 1, wr = w >> 1;
+  constexpr int WR = BM / 2;
+  const bool drop = p.p > 0.f;
+  const uint32_t thresh = drop ? (uint32_t)(p.p * 4294967296.0) : 0u;
+  const float inv_keep = drop ? 1.f / (1.f - p.p) : 1.f;
+  const uint64_t seed1 = drop ? s2h_seed(p.seed1, p.seed_off) : 0, seed2 = drop ? s2h_seed(p.seed2, p.seed_off) : 0;
+
+  // b1 into LDS first (H / 256 pieces of 1 KB, H % 1024 == 0: the same count per wave): the epilogue
+  // reads it from there -- a plain global load inside the loop would make the compiler wait for
+  // vmcnt(0), draining the ring's DMAs every chunk
+  for (int i = w; i < p.H / 256; i += 4) lds_dma16(p.b1 + i * 256 + lane * 4, smem + S::OFF_B1 + i * 1024);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) IX::dma(smem + S::OFF_X + s * IX::BYTES, p.x, p.ldx, 1, r0, s * 64, p.R, FFN_D, w, lane);
+  FfnFwdDma dma;
+  dma.init(p, w, lane);
+#pragma unroll
+  for (int q = 0; q < NS - 1; ++q) ffn_fwd_issue<BM, NS>(smem, p, dma, q, w);
+
+  f32x4 acc1[4][NI], acc2[8][NI];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc2[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll 1
+  for (int c = 0; c < nchunk; ++c) {
+    const bool last = c + 1 == nchunk;
+    static_for<0, 8>([&](auto subc) {
+      constexpr int SUB = decltype(subc)::value;
+      const int q = c * 8 + SUB;
+      ffn_fwd_wait<BM, NS, SUB>(c == 0, last);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (q + NS - 1 < nq) ffn_fwd_issue<BM, NS>(smem, p, dma, q + NS - 1, w);
+      const char* slot = smem + S::OFF_RING + (q % NS) * FFN_RING;
+      if constexpr (SUB < 4) {
+        if constexpr (SUB == 0) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc1[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        const char* xi = smem + S::OFF_X + SUB * IX::BYTES;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          bf16x8 a[4], b[NI];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[i] = IF1::frag(slot, wc * 64 + i * 16, ks, lane);
+#pragma unroll
+          for (int j = 0; j < NI; ++j) b[j] = IX::frag(xi, wr * WR + j * 16, ks, lane);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j) acc1[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc1[i][j], 0, 0, 0);
+        }
+        if constexpr (SUB == 3) {
+          // + b1, ReLU, dropout, bf16 -> the hid image
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int hl = wc * 64 + i * 16 + 4 * (lane >> 4);
+            const int hg = c * FFN_HC + hl;
+            const float4 bb = *(const float4*)(smem + S::OFF_B1 + hg * 4);
+            const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+            for (int j = 0; j < NI; ++j) {
+              const int r = wr * WR + j * 16 + (lane & 15);
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc1[i][j][e] + bv[e], 0.f);
+              if (drop) {
+                bool k[4];
+                keep4(seed1, p.idx1 + (uint64_t)(r0 + r) * p.H + hg, thresh, k);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
+              }
+              bf16 t[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) t[e] = (bf16)v[e];
+              *(uint2*)(smem + S::OFF_H + (hl >> 6) * IH::BYTES + IH::at(r, hl & 63)) = *(const uint2*)t;
+            }
+          }
+          raw_barrier_lds();
+#pragma unroll
+          for (int e = 0; e < S::STW; ++e) {
+            const int id = tid + 256 * e;
+            const int r = id >> 4, kc = id & 15;
+            const uint4 v = *(const uint4*)(smem + S::OFF_H + (kc >> 3) * IH::BYTES + IH::at(r, (kc & 7) * 8));
+            st16_nt(p.hid + (int64_t)(r0 + r) * p.ldh + c * FFN_HC + 8 * kc, v, false);
+          }
+        }
+      } else {
+        constexpr int KS = SUB - 4;
+        const char* hi = smem + S::OFF_H + (KS >> 1) * IH::BYTES;
+        bf16x8 b[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) b[j] = IH::frag(hi, wr * WR + j * 16, KS & 1, lane);
+#pragma unroll
+        for (int ih = 0; ih < 2; ++ih) {
+          bf16x8 a[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[i] = IF2::frag(slot, wc * 128 + (ih * 4 + i) * 16, 0, lane);
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+              acc2[ih * 4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc2[ih * 4 + i][j], 0, 0, 0);
+        }
+      }
+    });
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  // y = drop(acc + b2), 4 consecutive n of one row per lane -> bf16 staging -> 16-B row stores
+  char* ys = smem;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int n = wc * 128 + i * 16 + 4 * (lane >> 4);
+    const float4 bb = *(const float4*)(p.b2 + n);
+    const float bv[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int r = wr * WR + j * 16 + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = acc2[i][j][e] + bv[e];
+      if (drop) {
+        bool k[4];
+        keep4(seed2, p.idx2 + (uint64_t)(r0 + r) * FFN_D + n, thresh, k);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = k[e] ? v[e] * inv_keep : 0.f;
+      }
+      bf16 t[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) t[e] = (bf16)v[e];
+      *(uint2*)(ys + r * S::XLD + n * 2) = *(const uint2*)t;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int e = 0; e < BM / 8; ++e) {
+    const int id = tid + 256 * e;
+    const int r = id >> 5, nc = id & 31;
+    const uint4 v = *(const uint4*)(ys + r * S::XLD + nc * 16);
+    *(uint4*)(p.y + (int64_t)(r0 + r) * p.ldy + 8 * nc) = v;
+  }
+}
+
 }  // namespace
+
+// Memory-attention FFN forward in one launch (memory_attention.py:97, bf16):
+//   hid[R, H] = drop1(relu(x w1^T + b1))       (saved for the backward)
+//   y[R, 256] = drop2(hid w2^T + b2)
+// x [R, 256], w1 [H, 256] (linear1.weight), b1 [H] fp32, w2 [256, H] (linear2.weight), b2 [256] fp32;
+// dropout p with the GEMM epilogue's counter hash: seed1 / element index idx1 + row * H + h for hid,
+// seed2 / idx2 + row * 256 + n for y (so the backward's regenerated masks are the two GEMMs' own).
+// R a multiple of 64, H a multiple of 1024 up to 2048; 16-B aligned bases, row strides multiples of 8.
+extern "C" int s2h_ffn_fwd(int R, int H, const void* x, int64_t ldx, const void* w1, const float* b1, const void* w2,
+                           const float* b2, float p, uint64_t seed1, uint64_t idx1, uint64_t seed2, uint64_t idx2,
+                           void* hid, int64_t ldh, void* y, int64_t ldy, hipStream_t st) {
+  if (R <= 0) return 0;
+  auto al = [](const void* q) { return ((uintptr_t)q & 15) == 0; };
+  if (R % 64 || H <= 0 || H % 1024 || H > FFN_FWD_HMAX || !al(x) || !al(w1) || !al(w2) || !al(b1) || !al(b2) || !al(hid) || !al(y) ||
+      ldx % 8 || ldh % 8 || ldy % 8 || (int64_t)R * ldx >= (1ll << 31) || (int64_t)H * H >= (1ll << 31))
+    return (int)hipErrorInvalidValue;
+  FfnFwdArgs a;
+  a.R = R; a.H = H;
+  a.x = (const bf16*)x; a.ldx = ldx;
+  a.w1 = (const bf16*)w1; a.b1 = b1;
+  a.w2 = (const bf16*)w2; a.b2 = b2;
+  a.hid = (bf16*)hid; a.ldh = ldh;
+  a.y = (bf16*)y; a.ldy = ldy;
+  a.p = p; a.seed1 = seed1; a.seed2 = seed2; a.idx1 = idx1; a.idx2 = idx2;
+  a.seed_off = s2h_rng_offset_ptr();
+  const bool big = R % 128 == 0 && R / 128 >= 512;
+  const int slot = s2h_prof_begin(st, 4, 1, R, 2 * H, FFN_D, 4 | 16);
+  s2h_prof_tag(((int64_t)1 << 43) | (big ? 128 : 64));
+  // 64-row tiles (a tracked frame's 13 312 rows: 208 workgroups, one per CU) take a 6-deep ring to
+  // hide the weight steps' DMA latency
+  if (big)
+    hipLaunchKernelGGL((ffn_fwd_kernel<128, 3>), dim3(R / 128), dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((ffn_fwd_kernel<64, FFN_FWD_NS64>), dim3(R / 64), dim3(256), 0, st, a);
+  s2h_prof_end(slot, st);
+  return (int)hipGetLastError();
+}
 
 // Memory-attention FFN backward, input-gradient side (memory_attention.py:97): from dy (the gradient
 // at linear2's output, [R, 256]), hid (linear2's saved input, [R, H]) and the bf16 weights w2
@@ -310,7 +606,7 @@ extern "C" int s2h_ffn_bwd_dgrad(int R, int H, const void* dy, int64_t lddy, con
   p.alpha = alpha;
   // 128-row tiles when they still give >= 2 waves of workgroups over the 256 CUs
   const bool big = R % 128 == 0 && R / 128 >= 512;
-  const int slot = s2h_prof_begin(st, 4, 1, R, H + FFN_D, FFN_D, 4 | 16);
+  const int slot = s2h_prof_begin(st, 4, 1, R, 2 * H, FFN_D, 4 | 16);  // 4 R H 256 flop
   s2h_prof_tag(((int64_t)1 << 42) | (big ? 128 : 64));
   if (big)
     hipLaunchKernelGGL(ffn_bwd_dgrad_kernel<128>, dim3(R / 128), dim3(256), 0, st, p);

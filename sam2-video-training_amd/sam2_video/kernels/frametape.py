@@ -424,6 +424,49 @@ def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0, rope=No
     return out
 
 
+def ffn_fwd_ok(x, mod1, mod2):
+    """ops.ffn_fwd applies to linear2(drop(relu(linear1(x)))) on the tape (bf16, not MX-fp8)"""
+    if _fp8._eligible(mod1) or _fp8._eligible(mod2):
+        return False
+    x2 = x.reshape(-1, x.shape[-1]) if x.is_contiguous() else None
+    return x2 is not None and ops.ffn_fwd_ok(x2, mod1.compute_weight(), mod1.compute_bias(), mod2.compute_weight(),
+                                            mod2.compute_bias())
+
+
+def ffn(tape: FrameTape, x, mod1, mod2, drop_p=0.0):
+    """linear(x, mod1, relu, drop_p) -> linear(., mod2, drop_p) (memory_attention.py:97), recorded as
+    exactly those two tape ops -- same op records, seeds and dropout element offsets as two `linear`
+    calls, so the backward is theirs (the ReLU linear's consumer runs ops.ffn_bwd_dgrad) -- but
+    computed by ONE ops.ffn_fwd launch: hid is written once for the backward and never re-read here."""
+    w1, b1, w2, b2 = mod1.compute_weight(), mod1.compute_bias(), mod2.compute_weight(), mod2.compute_bias()
+    H, C = w1.shape
+    N = w2.shape[0]
+    scale = tape._varlen_scale(x)
+    op1, first1 = tape._begin("linear", [x, None], _linear_bw,
+                              {"mod": mod1, "act": "relu", "p": float(drop_p), "relu_out": True, "rope": False})
+    if first1 and tape.vid(x) is None:
+        raise RuntimeError("tape ffn: input must be a recorded value or declared input")
+    vid1, hid = tape._out(0, (*x.shape[:-1], H), x.dtype, scale)
+    seed1 = tape._seed() if drop_p > 0 else 0
+    idx1 = tape._idx0(op1, hid.numel())
+    if first1:
+        op1.attrs["seed"] = seed1
+        op1.attrs["K"] = C
+    tape._finish(op1, [vid1], tape._req(op1, (mod1.weight, mod1.bias)))
+    op2, first2 = tape._begin("linear", [hid, None], _linear_bw,
+                              {"mod": mod2, "act": None, "p": float(drop_p), "relu_out": False, "rope": False})
+    vid2, y = tape._out(0, (*x.shape[:-1], N), x.dtype, scale)
+    seed2 = tape._seed() if drop_p > 0 else 0
+    idx2 = tape._idx0(op2, y.numel())
+    if first2:
+        op2.attrs["seed"] = seed2
+        op2.attrs["K"] = H
+    tape._finish(op2, [vid2], tape._req(op2, (mod2.weight, mod2.bias)))
+    ops.ffn_fwd(x.reshape(-1, C), w1, b1, w2, b2, drop_p, seed1, idx1, seed2, idx2, hid=hid.view(-1, H),
+                y=y.view(-1, N))
+    return y
+
+
 def _linear_bw(tape, op, gys):
     (gy,) = gys
     mod, act, p = op.attrs["mod"], op.attrs["act"], op.attrs["p"]

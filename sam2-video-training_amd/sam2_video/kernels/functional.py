@@ -255,6 +255,25 @@ def mlp_heads_nograd(pairs):
 
 
 # ------------------------------------------------ Linear + residual add + LayerNorm (one launch)
+def ffn_fwd_enabled():
+    """S2H_FFN_FWD=1 runs the memory-attention FFN forward as one ops.ffn_fwd launch instead of its two
+    Linear launches.  Off by default: at a tracked frame's 13 312 rows the fused kernel has 208 one-per-CU
+    workgroups and its ReLU / dropout-hash epilogue runs with the MFMA pipes idle -- 73.7 us per launch
+    against 70.5 us for the two GEMMs (graph-replayed, tools/ffn_bench.py, profiles/r05_ffn_bench.log),
+    bench step 153.0 / 152.8 vs 154.4 / 154.3 clip-frames/s (profiles/r05_v8_ffn_fwd_ab.log)"""
+    import os
+    return os.environ.get("S2H_FFN_FWD", "0") == "1"
+
+
+def ffn(x, mod1, mod2, drop_p=0.0):
+    """drop(linear2(drop(relu(linear1(x))))) (memory_attention.py:97): on the frame tape one launch
+    (_ft.ffn: the two Linear ops recorded as such, ops.ffn_fwd computing both), else the two Linears"""
+    T = _ft.active()
+    if T is not None and ffn_fwd_enabled() and _ft.ffn_fwd_ok(x, mod1, mod2):
+        return _ft.ffn(T, x if x.is_contiguous() else x.contiguous(), mod1, mod2, float(drop_p))
+    return linear(linear(x, mod1, act="relu", drop_p=drop_p), mod2, drop_p=drop_p)
+
+
 def linear_ln_enabled():
     """S2H_LINEAR_LN=1 runs a projection + the residual add + LayerNorm after it as ONE full-row GEMM
     launch.  Off by default: on MI355X the 64 x 256 full-row tile (160 KB of LDS, one workgroup per

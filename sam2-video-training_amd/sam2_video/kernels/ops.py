@@ -264,6 +264,39 @@ def ffn_bwd_dgrad(dy, w2, w1, hid, alpha=1.0, dh=None, dx=None):
     return dh, dx
 
 
+def ffn_fwd_ok(x, w1, b1, w2, b2):
+    """s2h_ffn_fwd applies: bf16, d_model 256, hidden 1024 or 2048, rows a multiple of 64,
+    contiguous 16-B aligned operands, fp32 biases"""
+    if x.dim() != 2:
+        return False
+    R, C = x.shape
+    H = w1.shape[0]
+    return (x.dtype == torch.bfloat16 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16
+            and b1 is not None and b2 is not None and b1.dtype == torch.float32 and b2.dtype == torch.float32
+            and C == 256 and tuple(w1.shape) == (H, 256) and tuple(w2.shape) == (256, H) and H in (1024, 2048)
+            and R % 64 == 0 and R * max(H, x.stride(0)) < 2**31 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and all(t.is_contiguous() for t in (w1, w2, b1, b2))
+            and all(t.data_ptr() % 16 == 0 for t in (x, w1, w2, b1, b2)))
+
+
+def ffn_fwd(x, w1, b1, w2, b2, p=0.0, seed1=0, idx1=0, seed2=0, idx2=0, hid=None, y=None):
+    """Memory-attention FFN forward in one launch (csrc/ffn.hip): hid = drop(relu(x w1^T + b1)),
+    y = drop(hid w2^T + b2) with the GEMM epilogue's dropout hash (seed1 / idx1, seed2 / idx2).
+    Returns (hid, y)."""
+    assert ffn_fwd_ok(x, w1, b1, w2, b2)
+    R = x.shape[0]
+    H = w1.shape[0]
+    if hid is None:
+        hid = torch.empty(R, H, device=x.device, dtype=x.dtype)
+    if y is None:
+        y = torch.empty(R, 256, device=x.device, dtype=x.dtype)
+    assert hid.is_contiguous() and y.is_contiguous()
+    _dev(x, w1, b1, w2, b2, hid, y)
+    call("s2h_ffn_fwd", R, H, ptr(x), x.stride(0), ptr(w1), ptr(b1), ptr(w2), ptr(b2), float(p),
+         int(seed1) & (2**64 - 1), int(idx1), int(seed2) & (2**64 - 1), int(idx2), ptr(hid), H, ptr(y), 256, stream())
+    return hid, y
+
+
 def linear_dgrad_ln_bwd_ok(dy, w, x):
     """s2h_linear_dgrad_ln_bwd applies: bf16, LayerNorm width 128 / 256, 16-B aligned rows"""
     K = w.shape[1]

@@ -96,8 +96,11 @@ class MemoryAttentionLayer(nn.Module):
         q = ca.proj_q(t, L)
         k = ca.proj_k(mem_k, L, num_k_exclude_rope)
         t, x = ca.attend_mem(q, k, mem_v, out_drop=p, add_ln=(x, self.norm3))
-        h = self.linear1(t, act="relu", drop_p=p)
-        t, x = FN.linear_add_layer_norm(h, self.linear2, x, next_norm, next_norm.eps, drop_p=p)
+        if FN._linear_ln_ok(t, self.linear2, next_norm):  # opt-in full-row linear2 + add + LayerNorm
+            h = self.linear1(t, act="relu", drop_p=p)
+            t, x = FN.linear_add_layer_norm(h, self.linear2, x, next_norm, next_norm.eps, drop_p=p)
+        else:  # both FFN GEMMs as one launch on the frame tape (FN.ffn), then add + LayerNorm
+            t, x = FN.add_layer_norm(x, FN.ffn(t, self.linear1, self.linear2, p), next_norm, next_norm.eps)
         return x, t
 
     def forward(self, tgt, mem_k, mem_v, num_k_exclude_rope=0):

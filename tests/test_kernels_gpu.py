@@ -240,8 +240,39 @@ def test_ffn_bwd_dgrad(rows, H, p):
     assert torch.equal(dh4, dh) and torch.equal(dx4, dx)
 
 
+@pytest.mark.parametrize("rows,H,p,idx", [(13312, 2048, 0.1, 13312 * 2048 * 3), (1024, 2048, 0.0, 0),
+                                          (64, 1024, 0.25, 7), (93184, 2048, 0.1, 0)])
+def test_ffn_fwd(rows, H, p, idx):
+    """memory-attention FFN forward in one launch (csrc/ffn.hip ffn_fwd_kernel) against the two GEMM
+    launches it replaces with the same dropout seeds and element offsets (an odd offset takes the
+    per-element hash path): the saved hid and the output within bf16 rounding, the dropout / ReLU
+    zeros identical, bit-identical repeats"""
+    ops = _ops()
+    torch.manual_seed(9)
+    bf = torch.bfloat16
+    x = torch.randn(rows, 256, device=DEV).to(bf)
+    w1 = (torch.randn(H, 256, device=DEV) / 16).to(bf)
+    b1 = torch.randn(H, device=DEV) * 0.1
+    w2 = (torch.randn(256, H, device=DEV) / math.sqrt(H)).to(bf)
+    b2 = torch.randn(256, device=DEV) * 0.1
+    s1, s2 = 0x1234567, 0x89ABCDEF
+    hid, y = ops.ffn_fwd(x, w1, b1, w2, b2, p, s1, idx, s2, idx + 1)
+    hid_r = ops.linear(x, w1, b1, act="relu", drop_p=p, seed=s1, drop_idx0=idx)
+    y_r = ops.linear(hid_r, w2, b2, drop_p=p, seed=s2, drop_idx0=idx + 1)
+    torch.cuda.synchronize()
+    assert torch.equal(hid == 0, hid_r == 0)
+    _close(hid.float(), hid_r.float(), 8e-3)
+    _close(y.float(), y_r.float(), 8e-3)
+    if p > 0:
+        assert torch.equal(y == 0, y_r == 0)
+    pos = (x.float() @ w1.float().t() + b1) > 1e-2  # clearly positive pre-activations: dropped at rate p
+    assert abs((hid[pos] == 0).float().mean().item() - p) < 0.03
+    hid2, y2 = ops.ffn_fwd(x, w1, b1, w2, b2, p, s1, idx, s2, idx + 1)
+    assert torch.equal(hid2, hid) and torch.equal(y2, y)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("B,H,W,C,ws", [(8, 32, 32, 1344, 14), (8, 16, 16, 2688, 7), (2, 9, 13, 48, 4), (1, 8, 8, 16, 8)])
+@pytest.mark.parametrize("B,H,W,C,ws",[(8, 32, 32, 1344, 14), (8, 16, 16, 2688, 7), (2, 9, 13, 48, 4), (1, 8, 8, 16, 8)])
 def test_window_pad(dtype, B, H, W, C, ws):
     """partition of a projection's output with bias rows at the padded positions (Hiera's padded windows,
     csrc/elementwise.hip window_pad_vec_kernel) against zero-pad + partition + bias fill in torch, and

@@ -1,5 +1,5 @@
-"""Memory-attention FFN backward, input-gradient side: the one-launch kernel (csrc/ffn.hip) against the
-two GEMMs it replaces (dH with the ReLU/dropout mask in the epilogue, then dX = dH W1), graph-replayed
+"""Memory-attention FFN backward (input-gradient side) and forward: the one-launch kernels (csrc/ffn.hip)
+against the two GEMMs each replaces (dH with the ReLU/dropout mask in the epilogue, then dX = dH W1), graph-replayed
 at the frame-batched bench shape.   GPU only.   python tools/ffn_bench.py"""
 import os
 import sys
@@ -32,6 +32,17 @@ def main():
         byts = 2 * (R * 256 + R * H + R * H + R * 256)
         print(f"ffn bwd R={R} H={H}: fused {t_f:7.1f} us ({flops / t_f / 1e6:5.0f} TF/s, {byts / t_f / 1e3:5.0f} GB/s)"
               f" | two GEMMs {t_a:7.1f} + {t_b:7.1f} = {t_a + t_b:7.1f} us", flush=True)
+        x = torch.randn(R, 256, device="cuda", dtype=bf)
+        b1 = torch.randn(H, device="cuda") * 0.1
+        b2 = torch.randn(256, device="cuda") * 0.1
+        w1f = (torch.randn(H, 256, device="cuda") / 16).to(bf)
+        w2f = (torch.randn(256, H, device="cuda") / 45).to(bf)
+        y = torch.empty(R, 256, device="cuda", dtype=bf)
+        f_f = graph_time(lambda: ops.ffn_fwd(x, w1f, b1, w2f, b2, 0.1, 11, 0, 12, 0, hid=dh, y=y))
+        f_a = graph_time(lambda: ops.linear(x, w1f, b1, act="relu", drop_p=0.1, seed=11, out=dh))
+        f_b = graph_time(lambda: ops.linear(dh, w2f, b2, drop_p=0.1, seed=12, out=y))
+        print(f"ffn fwd R={R} H={H}: fused {f_f:7.1f} us ({flops / f_f / 1e6:5.0f} TF/s) | two GEMMs {f_a:7.1f} + "
+              f"{f_b:7.1f} = {f_a + f_b:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":
