@@ -325,6 +325,34 @@ int s2h_ffn_bwd_dgrad(int R, int H, const void* dy, int64_t lddy, const void* w2
 int s2h_ffn_fwd(int R, int H, const void* x, int64_t ldx, const void* w1, const float* b1, const void* w2,
                 const float* b2, float p, uint64_t seed1, uint64_t idx1, uint64_t seed2, uint64_t idx2, void* hid,
                 int64_t ldh, void* y, int64_t ldy, hipStream_t st);
+/* Two-way transformer token side, forward (bf16; sam/transformer.py:112-197, replacing per block ~17
+ * of ~17 launches (13 objects x 8 tokens) to five).  R = objects x T rows (T <= 16
+ * tokens per object, an object never split), width 256, self-attention 8 heads of 32, cross-attention
+ * width 128, MLP 256 -> 2048 -> 256 ReLU; weights [N, K] bf16 row-major, biases / LayerNorm fp32.  Every
+ * intermediate is written where the frame tape stores the corresponding op's output (lse [objects, 8,
+ * T] natural log; mean / rstd per row).
+ * s2h_dec_self (transformer.py:163-170): qa = x + pe (skip == 0, else unused), q / k from (skip ? x : qa),
+ *   v from x, os = self-attention, y1 = os Wo^T + bo (+ x unless skip), x1 = norm1(y1), qt = x1 + pe,
+ *   qq = qt Wqc^T + bqc (the token -> image query). */
+int s2h_dec_self(int R, int T, int skip, float scale, const void* x, const void* pe, const void* wq, const float* bq,
+                 const void* wk, const float* bk, const void* wv, const float* bv, const void* wo, const float* bo,
+                 const float* g1, const float* b1, float eps1, const void* wqc, const float* bqc, void* qa, void* qs,
+                 void* ks, void* vs, void* os, float* lse, void* y1, void* x1, float* mean1, float* rstd1, void* qt,
+                 void* qq, hipStream_t st);
+/* The second half's token side around the MLP (whose two GEMMs stay s2h_gemm launches; transformer.py:170-173):
+ * s2h_dec_post_a: y2 = ot Wo^T + bo + x1, x2 = norm2(y2);
+ * s2h_dec_post_b: x3 = norm3(y3) (y3 = MLP output + x2), q2 = x3 + pe, kio = q2 Wki^T + bki,
+ *   vio = x3 Wvi^T + bvi (the image -> token keys / values); final_q: qfa = x3 + pe, qqf = qfa Wqf^T + bqf
+ *   (TwoWayTransformer's final token -> image query, :194-196). */
+int s2h_dec_post_a(int R, int T, const void* ot, const void* x1, const void* wo, const float* bo, const float* g2,
+                   const float* b2n, float eps2, void* y2, void* x2, float* mean2, float* rstd2, hipStream_t st);
+int s2h_dec_post_b(int R, int T, int final_q, const void* y3, const void* pe, const float* g3, const float* b3n,
+                   float eps3, const void* wki, const float* bki, const void* wvi, const float* bvi, const void* wqf,
+                   const float* bqf, void* x3, float* mean3, float* rstd3, void* q2, void* kio, void* vio, void* qfa,
+                   void* qqf, hipStream_t st);
+/* s2h_dec_final (transformer.py:196-197): y = of Wo^T + bo + x3, hs = norm(y). */
+int s2h_dec_final(int R, int T, const void* of, const void* x3, const void* wo, const float* bo, const float* g,
+                  const float* bn, float eps, void* y, void* hs, float* mean, float* rstd, hipStream_t st);
 int64_t s2h_linear_dgrad_ln_bwd_ws_bytes(int M, int N);
 int s2h_linear_dgrad_ln_bwd(int M, int N, int K, const void* G, int64_t ldg, const void* W, int64_t ldw, float alpha,
                             const void* X, int64_t ldx, const float* gamma, const float* mean, const float* rstd,

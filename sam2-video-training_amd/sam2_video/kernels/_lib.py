@@ -35,6 +35,10 @@ SIGNATURES = {
     "s2h_linear_dgrad_ln_bwd_ws_bytes": [I, I],
     "s2h_linear_dgrad_ln_bwd": [I, I, I, P, L, P, L, F, P, L, P, P, P, P, L, P, L, P, P, P, P],
     "s2h_ffn_bwd_dgrad": [I, I, P, L, P, P, P, L, F, P, L, P, L, P],
+    "s2h_dec_self": [I, I, I, F, P, P, P, P, P, P, P, P, P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "s2h_dec_post_a": [I, I, P, P, P, P, P, P, F, P, P, P, P, P],
+    "s2h_dec_post_b": [I, I, I, P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
+    "s2h_dec_final": [I, I, P, P, P, P, P, P, F, P, P, P, P, P],
     "s2h_ffn_fwd": [I, I, P, L, P, P, P, P, F, c_uint64, c_uint64, c_uint64, c_uint64, P, L, P, L, P],
     "s2h_ln_wgrad_finalize": [I, I, P, P, P, P],
     "s2h_mlp_heads": [I, I, P, P, P, P, P, P, P, P, P, P, P, P],

@@ -391,7 +391,9 @@ def _empty_like_store(tape, st: Store, dtype=None):
 
 
 # ---------------------------------------------------------------- linear
-def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0, rope=None):
+def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0, rope=None, _compute=True):
+    """_compute=False records the op and returns its output slot without launching (a fused kernel
+    writes it: dec_self / dec_post / dec_final)"""
     x = x if x.is_contiguous() else x.contiguous()
     # ReLU without residual: the backward masks with the output (> 0 exactly where the
     # pre-activation was positive and the element kept), so no pre-activation is stored
@@ -410,7 +412,9 @@ def linear(tape: FrameTape, x, mod, act=None, residual=None, drop_p=0.0, rope=No
     pre = tape._aux("pre", shape, x.dtype, scale) if act and not relu_out else None
     seed = tape._seed() if drop_p > 0 else 0
     idx0 = tape._idx0(op, out.numel())
-    if rope is not None:  # RoPE of the output in the GEMM epilogue; per-frame (L, nrot) for the backward
+    if not _compute:
+        assert rope is None and pre is None and drop_p == 0
+    elif rope is not None:  # RoPE of the output in the GEMM epilogue; per-frame (L, nrot) for the backward
         assert act is None and residual is None and drop_p == 0
         _fp8.linear_rope(x, mod, w, b, rope, out=out)
         tape._fattr(op, "rope", rope)
@@ -677,8 +681,8 @@ def _mlp_heads_bw(tape, op, gys):
 
 
 # ---------------------------------------------------------------- layer norms
-def layer_norm(tape: FrameTape, x, mod, eps, add=None):
-    """LN(x) or (LN(x + add), x + add)"""
+def layer_norm(tape: FrameTape, x, mod, eps, add=None, _compute=True):
+    """LN(x) or (LN(x + add), x + add); _compute=False (no add): record only, returns (y, mean, rstd)"""
     x = x if x.is_contiguous() else x.contiguous()
     op, first = tape._begin("ln", [x, add], _ln_bw, {"mod": mod, "eps": eps, "add": add is not None})
     rows = x.numel() // x.shape[-1]
@@ -690,8 +694,12 @@ def layer_norm(tape: FrameTape, x, mod, eps, add=None):
         outs.append(vid2)
     mean = tape._aux("mean", (rows,), torch.float32)
     rstd = tape._aux("rstd", (rows,), torch.float32)
-    call_ln_fwd(x, mod, eps, y, mean, rstd, add, xsum)
+    if _compute:
+        call_ln_fwd(x, mod, eps, y, mean, rstd, add, xsum)
     tape._finish(op, outs, tape._req(op, (mod.weight, mod.bias)))
+    if not _compute:
+        assert add is None
+        return y, mean, rstd
     return (y, xsum) if add is not None else y
 
 
@@ -724,8 +732,9 @@ def _ln_bw(tape, op, gys):
 
 
 # ---------------------------------------------------------------- attention
-def attention(tape: FrameTape, q, k, v, scale, p_drop):
-    """q [B, Lq, H, D], k / v [B, Lk, H, D] views of recorded values (contiguous per value)"""
+def attention(tape: FrameTape, q, k, v, scale, p_drop, _compute=True):
+    """q [B, Lq, H, D], k / v [B, Lk, H, D] views of recorded values (contiguous per value);
+    _compute=False: record only, returns (o, lse)"""
     op, first = tape._begin("attn", [q, k, v], _attn_bw, {"scale": scale, "p": p_drop})
     B, Lq, H, D = q.shape
     Lk = k.shape[1]
@@ -734,12 +743,15 @@ def attention(tape: FrameTape, q, k, v, scale, p_drop):
     seed = tape._seed() if p_drop > 0 else 0
     idx0 = tape._idx0(op, B * H * Lq * Lk)
     keep = tape._keep_bits(q, Lk, op.ins[1], p_drop)
-    ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0, keep=keep)
+    if _compute:
+        ops.attn_fwd(q, k, v, o, lse, scale, p_drop, seed, idx0=idx0, keep=keep)
+    else:
+        assert p_drop == 0 and keep is None
     tape._fattr(op, "Lk", Lk)
     if first:
         op.attrs.update(seed=seed, B=B, Lq=Lq, H=H, D=D, qshape=tuple(q.shape), keep=keep is not None)
     tape._finish(op, [vid], any(op.needs))
-    return o
+    return o if _compute else (o, lse)
 
 
 def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_buf, dv_buf):
@@ -962,13 +974,14 @@ def _rope_bw(tape, op, gys):
 
 
 # ---------------------------------------------------------------- elementwise
-def add(tape: FrameTape, a, b, alpha, beta):
+def add(tape: FrameTape, a, b, alpha, beta, _compute=True):
     a = a if a.is_contiguous() else a.contiguous()
     b = b if b.is_contiguous() else b.contiguous()
     op, first = tape._begin("add", [a, b], _add_bw, {"alpha": alpha, "beta": beta})
     scale = tape._varlen_scale(a, b)
     vid, out = tape._out(0, a.shape, a.dtype, scale)
-    ops.add(a, b, out=out, alpha=alpha, beta=beta)
+    if _compute:
+        ops.add(a, b, out=out, alpha=alpha, beta=beta)
     tape._finish(op, [vid], any(op.needs))
     return out
 
@@ -1250,6 +1263,92 @@ def _point_embed_bw(tape, op, gys):
         if gp is not None:
             ops.add(gp.view(-1), dtable[i], out=gp.view(-1))
     return []
+
+
+# ---------------------------------------------------------------- two-way decoder, token side
+def dec_tok_ok(x, blk, mlp_dim=2048):
+    """the fused token-side launches (csrc/decoder_tok.hip) apply: bf16 tokens [B, T <= 16, 256], 8-head
+    self-attention, 128-wide cross-attentions, a 256 -> 2048 -> 256 ReLU MLP, no dropout"""
+    sa, t2i, i2t = blk.self_attn, blk.cross_attn_token_to_image, blk.cross_attn_image_to_token
+    fc1, fc2 = blk.mlp.layers[0], blk.mlp.layers[-1]
+    return (x.dtype == torch.bfloat16 and x.dim() == 3 and x.shape[1] <= 16 and x.shape[2] == 256
+            and sa.num_heads == 8 and sa.internal_dim == 256 and t2i.internal_dim == 128
+            and i2t.internal_dim == 128 and len(blk.mlp.layers) == 2 and blk.mlp.act == "relu"
+            and not blk.mlp.sigmoid_output and fc1.out_features == mlp_dim and fc2.in_features == mlp_dim
+            and sa.dropout_p == 0 and t2i.dropout_p == 0 and i2t.dropout_p == 0)
+
+
+def _p(t):
+    return t.data_ptr() if t is not None else None
+
+
+def dec_self(tape: FrameTape, x, pe, sa, norm1, qc, skip):
+    """The first half of a TwoWayAttentionBlock's token side (transformer.py:163-170): [q = x + pe] ->
+    self-attention -> out-projection (+ x) -> norm1 -> x1; qt = x1 + pe -> token -> image q projection.
+    Recorded as exactly those tape ops (so their backward is the usual one), computed by ONE
+    s2h_dec_self launch.  Returns (x1, qq)."""
+    from ._lib import call
+    qa = None if skip else add(tape, x, pe, 1.0, 1.0, _compute=False)
+    qin = x if skip else qa
+    qs = linear(tape, qin, sa.q_proj, _compute=False)
+    ks = linear(tape, qin, sa.k_proj, _compute=False)
+    vs = linear(tape, x, sa.v_proj, _compute=False)
+    B, L, C = qs.shape
+    h = sa.num_heads
+    scale = 1.0 / math.sqrt(C // h)
+    os_, lse = attention(tape, qs.view(B, L, h, C // h), ks.view(B, L, h, C // h), vs.view(B, L, h, C // h), scale,
+                         0.0, _compute=False)
+    y1 = linear(tape, os_.reshape(B, L, C), sa.out_proj, residual=None if skip else x, _compute=False)
+    x1, m1, r1 = layer_norm(tape, y1, norm1, norm1.eps, _compute=False)
+    qt = add(tape, x1, pe, 1.0, 1.0, _compute=False)
+    qq = linear(tape, qt, qc, _compute=False)
+    w = lambda m: (_p(m.compute_weight()), _p(m.compute_bias()))  # noqa: E731
+    call("s2h_dec_self", B * L, L, int(skip), float(scale), _p(x), _p(pe), *w(sa.q_proj), *w(sa.k_proj),
+         *w(sa.v_proj), *w(sa.out_proj), _p(norm1.weight.detach()), _p(norm1.bias.detach()), float(norm1.eps),
+         *w(qc), _p(qa), _p(qs), _p(ks), _p(vs), _p(os_), _p(lse), _p(y1), _p(x1), _p(m1), _p(r1), _p(qt), _p(qq),
+         ops.stream())
+    return x1, qq
+
+
+def dec_post(tape: FrameTape, ot, x1, pe, out_proj, norm2, mlp, norm3, ki_mod, vi_mod, qf_mod=None):
+    """The second half's token side (transformer.py:170-173): out-projection of the token -> image
+    attention (+ x1) -> norm2 (one s2h_dec_post_a launch), the MLP's two GEMMs as usual, norm3 -> x3,
+    q2 = x3 + pe -> the image -> token k / v projections, with qf_mod (the last block) also
+    TwoWayTransformer's final q = x3 + pe and its projection (:194-196) (one s2h_dec_post_b launch).
+    Recorded as those tape ops.  Returns (x3, ki, vi, qqf)."""
+    from ._lib import call
+    fc1, fc2 = mlp.layers[0], mlp.layers[-1]
+    y2 = linear(tape, ot, out_proj, residual=x1, _compute=False)
+    x2, m2, r2 = layer_norm(tape, y2, norm2, norm2.eps, _compute=False)
+    B, L, C = x2.shape
+    w = lambda m: (_p(m.compute_weight()), _p(m.compute_bias())) if m is not None else (None, None)  # noqa: E731
+    call("s2h_dec_post_a", B * L, L, _p(ot), _p(x1), *w(out_proj), _p(norm2.weight.detach()),
+         _p(norm2.bias.detach()), float(norm2.eps), _p(y2), _p(x2), _p(m2), _p(r2), ops.stream())
+    y3 = linear(tape, linear(tape, x2, fc1, act="relu"), fc2, residual=x2)
+    x3, m3, r3 = layer_norm(tape, y3, norm3, norm3.eps, _compute=False)
+    q2 = add(tape, x3, pe, 1.0, 1.0, _compute=False)
+    ki = linear(tape, q2, ki_mod, _compute=False)
+    vi = linear(tape, x3, vi_mod, _compute=False)
+    qfa = qqf = None
+    if qf_mod is not None:
+        qfa = add(tape, x3, pe, 1.0, 1.0, _compute=False)
+        qqf = linear(tape, qfa, qf_mod, _compute=False)
+    call("s2h_dec_post_b", B * L, L, int(qf_mod is not None), _p(y3), _p(pe), _p(norm3.weight.detach()),
+         _p(norm3.bias.detach()), float(norm3.eps), *w(ki_mod), *w(vi_mod), *w(qf_mod), _p(x3), _p(m3), _p(r3),
+         _p(q2), _p(ki), _p(vi), _p(qfa), _p(qqf), ops.stream())
+    return x3, ki, vi, qqf
+
+
+def dec_final(tape: FrameTape, of, x3, out_proj, norm):
+    """TwoWayTransformer's final token side (transformer.py:196-197): out-projection (+ x3) -> norm,
+    recorded as those two tape ops, one s2h_dec_final launch"""
+    from ._lib import call
+    y = linear(tape, of, out_proj, residual=x3, _compute=False)
+    hs, m, r = layer_norm(tape, y, norm, norm.eps, _compute=False)
+    B, L, C = x3.shape
+    call("s2h_dec_final", B * L, L, _p(of), _p(x3), _p(out_proj.compute_weight()), _p(out_proj.compute_bias()),
+         _p(norm.weight.detach()), _p(norm.bias.detach()), float(norm.eps), _p(y), _p(hs), _p(m), _p(r), ops.stream())
+    return hs
 
 
 def decoder_tokens(tape: FrameTape, sparse, dtype, params):

@@ -12,6 +12,7 @@ import math
 import torch
 from torch import nn
 
+from ....kernels import frametape as _ft
 from ....kernels import functional as FN
 from ....kernels import ops
 from ..layers import MLP, LayerNorm, Linear
@@ -188,6 +189,9 @@ class TwoWayTransformer(nn.Module):
 
     def forward(self, image_embedding, image_pe_table, point_embedding):
         """image_embedding [B, HW, C]; image_pe_table [HW, C] constant; point_embedding [B, T, C]"""
+        tape = _ft.active()
+        if tape is not None and dec_tok_enabled() and all(_ft.dec_tok_ok(point_embedding, b) for b in self.layers):
+            return self._forward_tape_fused(tape, image_embedding, image_pe_table, point_embedding)
         queries, keys = point_embedding, image_embedding
         for layer in self.layers:
             queries, keys = layer(queries, keys, point_embedding, image_pe_table)
@@ -195,3 +199,42 @@ class TwoWayTransformer(nn.Module):
         k = FN.add_bcast(keys, image_pe_table)
         queries = self.final_attn_token_to_image(q, k, keys, residual=queries, norm=self.norm_final_attn)
         return queries, keys
+
+    def _forward_tape_fused(self, tape, keys, pe_table, pe):
+        """forward() on the frame tape with each block's token side as two launches (csrc/decoder_tok.hip:
+        _ft.dec_self before the token -> image attention, _ft.dec_post after it) and the final token side
+        as one (_ft.dec_final); the image-side projections, both cross-attentions and norm4 as before.
+        The tape records the same ops (the token ones in the order the fused launches compute them)."""
+        queries = pe
+        n = len(self.layers)
+        fa = self.final_attn_token_to_image
+        qqf = None
+        for i, blk in enumerate(self.layers):
+            t2i, i2t = blk.cross_attn_token_to_image, blk.cross_attn_image_to_token
+            x1, qq = _ft.dec_self(tape, queries, pe, blk.self_attn, blk.norm1, t2i.q_proj, blk.skip_first_layer_pe)
+            k = FN.add_bcast(keys, pe_table)
+            B, Lq, I = qq.shape
+            Lk, h = k.shape[1], t2i.num_heads
+            o = FN.attention(qq.view(B, Lq, h, I // h), t2i.k_proj(k).view(B, Lk, h, I // h),
+                             t2i.v_proj(keys).view(B, Lk, h, I // h), p_drop=t2i._p())
+            queries, ki, vi, qf = _ft.dec_post(tape, o.reshape(B, Lq, I), x1, pe, t2i.out_proj, blk.norm2, blk.mlp,
+                                               blk.norm3, i2t.k_proj, i2t.v_proj, fa.q_proj if i == n - 1 else None)
+            if qf is not None:
+                qqf = qf
+            oi = FN.attention(i2t.q_proj(k).view(B, Lk, h, I // h), ki.view(B, Lq, h, I // h),
+                              vi.view(B, Lq, h, I // h), p_drop=i2t._p())
+            keys = blk.norm4(i2t.out_proj(oi.reshape(B, Lk, I), residual=keys))
+        k = FN.add_bcast(keys, pe_table)
+        B, Lq, I = qqf.shape
+        Lk, h = k.shape[1], fa.num_heads
+        o = FN.attention(qqf.view(B, Lq, h, I // h), fa.k_proj(k).view(B, Lk, h, I // h),
+                         fa.v_proj(keys).view(B, Lk, h, I // h), p_drop=fa._p())
+        queries = _ft.dec_final(tape, o.reshape(B, Lq, I), queries, fa.out_proj, self.norm_final_attn)
+        return queries, keys
+
+
+def dec_tok_enabled():
+    """S2H_DEC_TOK=0: the two-way transformer's token side as its separate launches (A/B of
+    csrc/decoder_tok.hip)"""
+    import os
+    return os.environ.get("S2H_DEC_TOK", "1") == "1"
