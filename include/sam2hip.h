@@ -141,6 +141,21 @@ int s2h_wgrad_workspace(void* ws, int64_t bytes, int kmin);
  * model's).  Results stay bit-identical for a given choice.  Returns 0. */
 int s2h_wgrad_force(int tile, int splits);
 
+/* Deferred gradient sums (round 5, csrc/grad_defer.hip).  No reference counterpart: the reference's
+ * parameter gradients come from torch autograd's per-op accumulation (the LayerNorm / Linear bias
+ * backward inside nn.LayerNorm / nn.Linear, hieradet.py:98-166, memory_attention.py:58-99,
+ * transformer.py:137-311).  Here those column reductions run as per-block partial rows + a fixed-order
+ * sum; between s2h_grad_defer(ws, ...) and s2h_grad_defer(NULL, ...) the fixed-order sums whose
+ * destinations lie inside [sink, sink + sink_bytes) (the gradient arena) are recorded instead of
+ * launched, their partials kept in ws (device memory owned by the caller, 256-B aligned), and
+ * s2h_grad_defer_flush adds them all in a few launches on `stream` (64 records per launch, in record
+ * order for overlapping destinations).  Nothing may read those destinations before the flush.
+ * s2h_grad_defer(NULL, ...) with records pending returns hipErrorNotReady. */
+int s2h_grad_defer(void* ws, int64_t ws_bytes, void* sink, int64_t sink_bytes);
+int s2h_grad_defer_flush(hipStream_t stream);
+/* records waiting for s2h_grad_defer_flush (not a hipError_t) */
+int s2h_grad_defer_pending(void);
+
 /* ---------------------------------------------------------------- MX-fp8 (BASELINE config 5)
  * No reference counterpart: the reference trains in fp32 / bf16 autocast only
  * (trainer.py:256-289 under Lightning `precision`); this is the fp8 variant of the projection

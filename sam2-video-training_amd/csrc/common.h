@@ -165,6 +165,11 @@ void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t 
 // float atomics; nullptr when none is registered, it is switched off or smaller than `bytes` (the caller
 // then keeps its atomic path).  Users are stream-ordered (one stream).
 float* s2h_det_ws(int64_t bytes);
+// Deferred second pass (grad_defer.hip): inside a s2h_grad_defer scope, partial storage for nb rows of
+// n0 + n1 columns whose fixed-order column sums go to out0[0:n0] (+=) and out1[0:n1] (+=), recorded for
+// s2h_grad_defer_flush; nullptr when no scope is open or a destination is outside the registered sink
+// (the caller then runs its own second pass).
+float* s2h_defer_sink(int nb, int n0, float* out0, int n1, float* out1, hipStream_t st);
 
 // LDS-DMA (global_load_lds_dwordx4 / _dword: 16 / 4 B per lane into lds_piece + lane * size)
 // issued through inline asm.  Issued through the builtin, the compiler's waitcnt pass sees an

@@ -692,7 +692,8 @@ extern "C" int s2h_window_pad_colsum(int dt, int B, int H, int W, int C, int ws,
     rpc = (int)((rows + 255) / 256);
     nchunk = (int)((rows + rpc - 1) / rpc);
   }
-  float* part = s2h_det_ws(nchunk * C * (int64_t)sizeof(float));
+  float* deferred = s2h_defer_sink(nchunk, C, out, 0, nullptr, st);
+  float* part = deferred ? deferred : s2h_det_ws(nchunk * C * (int64_t)sizeof(float));
   const dim3 grid((unsigned)((C / vec + 31) / 32), (unsigned)nchunk);
   if (dt == S2H_BF16)
     hipLaunchKernelGGL(window_pad_colsum_kernel<bf16>, grid, dim3(256), 0, st, B, H, W, C, ws, (const bf16*)win, rpc,
@@ -700,7 +701,7 @@ extern "C" int s2h_window_pad_colsum(int dt, int B, int H, int W, int C, int ws,
   else
     hipLaunchKernelGGL(window_pad_colsum_kernel<float>, grid, dim3(256), 0, st, B, H, W, C, ws, (const float*)win, rpc,
                        out, part);
-  if (part) det_colsum(1, nchunk, C, part, out, 1, st);
+  if (part && !deferred) det_colsum(1, nchunk, C, part, out, 1, st);
   return (int)hipGetLastError();
 }
 
@@ -893,10 +894,15 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
     int64_t rpb = (rows + 1023) / 1024;
     if (rpb < 16) rpb = 16;
     int64_t nb = (rows + rpb - 1) / rpb;
-    float* part = s2h_det_ws(nb * cols * (int64_t)sizeof(float));
-    if (part && nb > 256) {  // deterministic: <= 256 partial rows for the second pass
-      rpb = (rows + 255) / 256;
-      nb = (rows + rpb - 1) / rpb;
+    // deterministic: <= 256 partial rows for the second pass (deferred into the arena inside a
+    // s2h_grad_defer scope, grad_defer.hip)
+    const int64_t rpb_d = nb > 256 ? (rows + 255) / 256 : rpb;
+    const int64_t nb_d = (rows + rpb_d - 1) / rpb_d;
+    float* deferred = s2h_defer_sink((int)nb_d, cols, out, 0, nullptr, st);
+    float* part = deferred ? deferred : s2h_det_ws(nb * cols * (int64_t)sizeof(float));
+    if (part) {
+      rpb = rpb_d;
+      nb = nb_d;
     }
     if (dt == S2H_BF16)
       hipLaunchKernelGGL(colsum_vec_kernel<bf16>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
@@ -904,7 +910,7 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
     else
       hipLaunchKernelGGL(colsum_vec_kernel<float>, dim3((unsigned)nb), dim3(256), 0, st, rows, cols,
                          (const float*)x, ld, rpb, out, part);
-    if (part) det_colsum(1, (int)nb, cols, part, out, 1, st);
+    if (part && !deferred) det_colsum(1, (int)nb, cols, part, out, 1, st);
     return (int)hipGetLastError();
   }
   const int cb = (cols + 255) / 256;
@@ -913,10 +919,11 @@ extern "C" int s2h_colsum(int dt, int64_t rows, int cols, const void* x, int64_t
   if (want < 1) want = 1;
   if (ry > want) ry = want;
   dim3 grid(cb, (unsigned)ry);
-  float* part = s2h_det_ws(ry * cols * (int64_t)sizeof(float));
+  float* deferred = s2h_defer_sink((int)ry, cols, out, 0, nullptr, st);
+  float* part = deferred ? deferred : s2h_det_ws(ry * cols * (int64_t)sizeof(float));
   if (dt == S2H_BF16) hipLaunchKernelGGL(colsum_kernel<bf16>, grid, dim3(256), 0, st, rows, cols, x, ld, out, part);
   else hipLaunchKernelGGL(colsum_kernel<float>, grid, dim3(256), 0, st, rows, cols, x, ld, out, part);
-  if (part) det_colsum(1, (int)ry, cols, part, out, 1, st);
+  if (part && !deferred) det_colsum(1, (int)ry, cols, part, out, 1, st);
   return (int)hipGetLastError();
 }
 // out[j] = sum_{o<O} x[o*inner + j]   written in T (broadcast-input gradients)

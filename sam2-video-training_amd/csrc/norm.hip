@@ -469,8 +469,11 @@ int ln_bwd(int rows, int C, const T* x, int64_t ldx, const T* dy, int64_t lddy, 
            float* dbeta, float* ws, hipStream_t st) {
   const LnPlan p = plan<T>(C, {ldx, lddy, lddx, dres ? ldres : 0}, {x, dy, dx, dres});
   const int nb = bwd_blocks(rows, p);
-  float* part = dgamma ? ws : nullptr;
-  if (dgamma && !ws) return (int)hipErrorInvalidValue;
+  // gamma / beta gradients into the arena inside a deferral scope: the fixed-order sum of the block
+  // partials runs later, batched with the step's other deferred sums (grad_defer.hip)
+  float* deferred = dgamma ? s2h_defer_sink(nb, C, dgamma, C, dbeta, st) : nullptr;
+  float* part = deferred ? deferred : dgamma ? ws : nullptr;
+  if (dgamma && !part) return (int)hipErrorInvalidValue;
   if (p.vec) {
     S2H_LN_DISPATCH(bwd_launch, p, nb, st, rows, C, x, ldx, dy, lddy, gamma, mean, rstd, dx, lddx, dx_accum, dres,
                     ldres, part);
@@ -478,7 +481,7 @@ int ln_bwd(int rows, int C, const T* x, int64_t ldx, const T* dy, int64_t lddy, 
     hipLaunchKernelGGL(ln_bwd_kernel<T>, dim3(nb), dim3(256), 8 * C * sizeof(float), st, rows, C, x, ldx, dy, lddy,
                        gamma, mean, rstd, dx, lddx, dx_accum, dres, ldres, part);
   }
-  if (part)
+  if (part && !deferred)
     hipLaunchKernelGGL(ln_wgrad_finalize_kernel, dim3((2 * C + 63) / 64), dim3(1024), 0, st, nb, C, part, dgamma, dbeta);
   return (int)hipGetLastError();
 }

@@ -50,6 +50,9 @@ SIGNATURES = {
     "s2h_gemm_w41": [I],
     "s2h_gemm_areg": [I],
     "s2h_wgrad_workspace": [P, L, I],
+    "s2h_grad_defer": [P, L, P, L],
+    "s2h_grad_defer_flush": [P],
+    "s2h_grad_defer_pending": [],
     "s2h_wgrad_force": [I, I],
     "s2h_flash_fwd_sets": [I],
     "s2h_attn_win": [I],
@@ -143,7 +146,8 @@ _LIB = None
 # entry points that do not return a hipError_t
 RESTYPES = {"s2h_attn_fwd_ws_bytes": c_int64, "s2h_attn_bwd_ws_bytes": c_int64, "s2h_attn_keep_words": c_int64,
             "s2h_attn_fwd_vfold_ws_bytes": c_int64,
-            "s2h_layernorm_bwd_ws_bytes": c_int64, "s2h_linear_dgrad_ln_bwd_ws_bytes": c_int64}
+            "s2h_layernorm_bwd_ws_bytes": c_int64, "s2h_linear_dgrad_ln_bwd_ws_bytes": c_int64,
+            "s2h_grad_defer_pending": c_int}
 
 
 class HipKernelError(RuntimeError):

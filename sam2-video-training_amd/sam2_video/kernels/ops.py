@@ -122,6 +122,42 @@ def wgrad_workspace(device=None):
     return t
 
 
+# Deferred gradient sums (csrc/grad_defer.hip): inside the scope, the fixed-order second pass of the
+# column reductions whose destination lies in `sink` (the gradient arena: LayerNorm gamma / beta, bias
+# gradients) is recorded and run for all of them in a few launches when the scope closes.  The scope
+# must enclose whole backward passes whose arena gradients nothing reads before it closes (the
+# StepRunner's backward phases; the DDP all-reduce of a range is issued after its phase's scope).
+# S2H_GRAD_DEFER=0 keeps the immediate second pass (A/B).
+GRAD_DEFER_BYTES = 256 << 20
+_DEFER = {"t": None, "depth": 0}
+
+
+def grad_defer_enabled():
+    return os.environ.get("S2H_GRAD_DEFER", "1") == "1"
+
+
+@contextlib.contextmanager
+def deferred_grad_sums(sink):
+    if sink is None or not sink.is_cuda or _DEFER["depth"] > 0 or not grad_defer_enabled():
+        _DEFER["depth"] += 1
+        try:
+            yield
+        finally:
+            _DEFER["depth"] -= 1
+        return
+    t = _DEFER["t"]
+    if t is None or t.device != sink.device:
+        t = _DEFER["t"] = torch.empty(GRAD_DEFER_BYTES // 4, dtype=torch.float32, device=sink.device)
+    call("s2h_grad_defer", t.data_ptr(), GRAD_DEFER_BYTES, sink.data_ptr(), sink.numel() * sink.element_size())
+    _DEFER["depth"] += 1
+    try:
+        yield
+    finally:
+        _DEFER["depth"] -= 1
+        call("s2h_grad_defer_flush", stream())
+        call("s2h_grad_defer", None, 0, None, 0)
+
+
 # ----------------------------------------------------------------- GEMM
 def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB=0, sC=0,
          bias=None, bias_mode=1, residual=None, ldr=0, sR=0, aux=None, ldx=0, sX=0, aux_mode=0,
@@ -693,7 +729,7 @@ def layernorm_bwd(x, dy, gamma, mean, rstd, dx=None, accumulate=False, dgamma=No
     if dres is not None:
         assert dres.is_contiguous() and dres.dtype == x.dtype and dres.numel() == x.numel() and not accumulate
     ws = None
-    if dgamma is not None:
+    if dgamma is not None:  # (unused when the library defers the gamma / beta sums)
         nbytes = lib().s2h_layernorm_bwd_ws_bytes(dt(x), rows, C)
         ws = torch.empty(max(nbytes // 4, 1), device=x.device, dtype=torch.float32)
     call("s2h_layernorm_bwd", dt(x), rows, C, ptr(x), C, ptr(dy), C, ptr(gamma), ptr(mean), ptr(rstd),

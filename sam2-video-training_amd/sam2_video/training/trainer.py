@@ -202,6 +202,13 @@ class SAM2LightningModule(_ModuleBase):
         opt = getattr(optimizer, "_optimizer", optimizer)  # LightningOptimizer wraps the optimizer
         opt.max_grad_norm = float(gradient_clip_val or 0.0)
 
+    def backward(self, loss, *args, **kwargs):
+        """Lightning hook (automatic optimization): loss.backward() with the gradient arena's
+        deferred fixed-order sums flushed at its end (kernels.ops.deferred_grad_sums)"""
+        from ..kernels.ops import deferred_grad_sums
+        with deferred_grad_sums(self.model.arena.grad_region()):
+            loss.backward(*args, **kwargs)
+
     # --------------------------------------------------------- forward
     def forward(self, batch):
         """trainer.py:182-188"""
@@ -309,8 +316,9 @@ class StepRunner:
         self._graphs: Dict[Any, Dict[str, Any]] = {}
         self.before_capture = None  # optional callable, run right before a graph is captured
         from ..kernels import functional as FN
-        from ..kernels.ops import rng_offset
+        from ..kernels.ops import deferred_grad_sums, rng_offset
         self._fn = FN
+        self._sums = lambda: deferred_grad_sums(module.model.arena.grad_region())
         self.rng = rng_offset(module.model.arena.device)
         # every step (eager, warm-up, capture) draws the same per-launch host seeds; the step-to-step
         # variation of the dropout masks comes from the device RNG offset alone, so an eager step
@@ -325,12 +333,13 @@ class StepRunner:
         self._fn.set_seed(self.seed_base)
         loss = self.module.training_step(batch, self.micro_step)
         bb = getattr(self.module.model, "last_backbone_outputs", None) if self.overlap else None
-        if bb:
-            grads = torch.autograd.grad(loss, bb, allow_unused=True)
-            self._pending = [(t, g) for t, g in zip(bb, grads) if g is not None]
-        else:
-            self._pending = None
-            loss.backward()
+        with self._sums():  # each backward phase flushes its deferred gradient sums at its end
+            if bb:
+                grads = torch.autograd.grad(loss, bb, allow_unused=True)
+                self._pending = [(t, g) for t, g in zip(bb, grads) if g is not None]
+            else:
+                self._pending = None
+                loss.backward()
         return loss
 
     def _segments(self):
@@ -341,8 +350,16 @@ class StepRunner:
             return []
         segs = getattr(self.module.model, "backbone_backward_segments", None)
         if segs is None:
-            return [(lambda: torch.autograd.backward([t for t, _ in pend], [g for _, g in pend]), 0)]
-        return segs(pend)
+            segs = [(lambda: torch.autograd.backward([t for t, _ in pend], [g for _, g in pend]), 0)]
+        else:
+            segs = segs(pend)
+
+        def phase(run):
+            def f():
+                with self._sums():
+                    run()
+            return f
+        return [(phase(run), rank) for run, rank in segs]
 
     def _phase2(self):
         for run, _ in self._segments():
