@@ -1152,12 +1152,15 @@ def conv_transpose2x2(tape: FrameTape, x, mod, add=None):
     op, first = tape._begin("convt", [x, add], _convt_bw, {"mod": mod})
     B, H, W, Ci = x.shape
     Co = mod.out_ch
-    w = mod.compute_weight()
-    Y = tape._aux("Y", (B * H * W, 4 * Co), x.dtype)
-    ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
-             ldc=4 * Co)
     vid, out = tape._out(0, (B, 2 * H, 2 * W, Co), x.dtype)
-    ops.convt2_scatter(Y, B, H, W, Co, bias=mod.bias.detach(), add=None, out=out)
+    if ops.convt2_direct():  # the GEMM stores into the NHWC output (no [rows, 4 Co] aux + scatter)
+        ops.convt2_gemm(x, *mod.store_weight(), out)
+    else:
+        w = mod.compute_weight()
+        Y = tape._aux("Y", (B * H * W, 4 * Co), x.dtype)
+        ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
+                 ldc=4 * Co)
+        ops.convt2_scatter(Y, B, H, W, Co, bias=mod.bias.detach(), add=None, out=out)
     if add is not None:
         add = add.contiguous()
         if add.shape[0] == B:

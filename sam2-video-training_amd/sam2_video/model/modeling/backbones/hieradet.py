@@ -23,6 +23,12 @@ from ....kernels.functional_sam import hiera_pos_embed
 from ..layers import MLP, Conv2d, LayerNorm, Linear
 
 
+def _stage_windows():
+    """S2H_HIERA_WIN_STAGE=0: every windowed block partitions its normed input and unpartitions its
+    attention output, as the reference does (hieradet.py:146,161), instead of the stage-level window order"""
+    return os.environ.get("S2H_HIERA_WIN_STAGE", "1") == "1"
+
+
 def _pad_after_qkv():
     """S2H_HIERA_PAD_QKV=0: padded windows partition the normed input (zero rows) before the qkv
     projection, as the reference does, instead of the projection's output (bias rows)"""
@@ -67,10 +73,14 @@ class MultiScaleBlock(nn.Module):
         if dim != dim_out:
             self.proj = Linear(dim, dim_out)
 
-    def forward(self, x, xn=None, next_norm=None):
+    def forward(self, x, xn=None, next_norm=None, windowed=False):
         """x: residual stream [B, H, W, C]; xn = norm1(x) when the previous block already produced
         it (fused with its residual add).  With next_norm, returns (x', next_norm(x')) from one
-        fused add + LayerNorm so the stream has a single autograd consumer; else x'."""
+        fused add + LayerNorm so the stream has a single autograd consumer; else x'.
+        windowed: x is already in window order, [B * windows, ws, ws, C] (Hiera.forward keeps a
+        stage whose blocks all use whole windows of one grid in that order): every op of the block
+        but the attention is per token and the 2x2 q-pool stays inside a window, so the block runs
+        on the windows as they are, with no partition / unpartition of its own"""
         B = x.shape[0]
         if xn is None:
             xn = self.norm1(x)
@@ -81,7 +91,9 @@ class MultiScaleBlock(nn.Module):
                 shortcut = FN.maxpool2(shortcut)
         ws = self.window_size
         H, W = xn.shape[1:3]
-        if ws > 0 and not self.q_stride and (H % ws or W % ws) and _pad_after_qkv():
+        if windowed:
+            y = self.attn(xn)
+        elif ws > 0 and not self.q_stride and (H % ws or W % ws) and _pad_after_qkv():
             # windows that need padding (stage 3: 32 -> 42, stage 4: 16 -> 21 at 512^2): the qkv
             # projection of a zero-padded row is its bias, so project the real tokens only, partition
             # the projection with bias rows, and project back after unpartition -- the qkv and proj
@@ -159,6 +171,35 @@ class Hiera(nn.Module):
         self.channel_list = ([self.blocks[i].dim_out for i in self.stage_ends[::-1]] if return_interm_layers
                              else [self.blocks[-1].dim_out])
 
+    def window_stages(self, H, W):
+        """{first block: (last block, window size at the stage's input)} of the stages whose blocks
+        all attend within whole (unpadded) windows of one grid -- the q-pool block that opens a stage
+        halves the window with the image, so its output windows are the next blocks' (at 512^2:
+        stage 1, 8x8 windows of 128^2, and stage 2, 8x8 -> 4x4 windows of 128^2 -> 64^2).  Such a
+        stage runs in window order between one partition at its start and one unpartition at its end
+        instead of both around every block's attention (hieradet.py:146,161)."""
+        runs = {}
+        if not _stage_windows():
+            return runs
+        b0 = 0
+        for b1 in self.stage_ends:
+            h, w, ok, ws_cur = H, W, True, None
+            for i in range(b0, b1 + 1):
+                blk = self.blocks[i]
+                ws = blk.window_size
+                if ws <= 0 or h % ws or w % ws or (ws_cur is not None and ws != ws_cur):
+                    ok = False
+                if blk.q_stride:
+                    ok = ok and ws % blk.q_stride[0] == 0 and tuple(blk.q_stride) == (2, 2)
+                    h, w, ws_cur = h // 2, w // 2, ws // 2
+                else:
+                    ws_cur = ws
+            if ok:
+                runs[b0] = (b1, self.blocks[b0].window_size)
+            H, W = h, w
+            b0 = b1 + 1
+        return runs
+
     def forward(self, x_nhwc) -> List[torch.Tensor]:
         """x: [T, H, W, 3] compute dtype -> stage outputs NHWC (high -> low resolution)"""
         x = self.patch_embed(x_nhwc)
@@ -166,12 +207,25 @@ class Hiera(nn.Module):
         x = FN.add_bcast(x, pe)
         outputs = []
         t = None
+        runs = self.window_stages(x.shape[1], x.shape[2])
+        run_end, img = -1, None  # last block of the window-ordered stage, its output's (B, H, W, ws)
         for i, blk in enumerate(self.blocks):
             is_out = (i == self.stage_ends[-1]) or (i in self.stage_ends and self.return_interm_layers)
-            if is_out or i + 1 == len(self.blocks):
-                x, t = blk(x, t), None
+            if i in runs:
+                run_end, ws = runs[i]
+                B, H, W = x.shape[:3]
+                for j in range(i, run_end + 1):
+                    if self.blocks[j].q_stride:
+                        H, W, ws = H // 2, W // 2, ws // 2
+                img = (B, H, W, ws)
+                x = FN.window_partition(x, runs[i][1])  # (t is None: see below)
+            windowed = i <= run_end
+            if is_out or i + 1 == len(self.blocks) or i == run_end or i + 1 in runs:
+                x, t = blk(x, t, windowed=windowed), None
             else:
-                x, t = blk(x, t, next_norm=self.blocks[i + 1].norm1)
+                x, t = blk(x, t, next_norm=self.blocks[i + 1].norm1, windowed=windowed)
+            if i == run_end:
+                x = FN.window_unpartition(x, img[3], *img[:3])
             if is_out:
                 outputs.append(x)
         # the stage outputs: the cut points of the staged backbone backward

@@ -337,6 +337,41 @@ def test_hiera_padded_window_block(compute, dim, heads, ws, HW, monkeypatch):
         _close(res["1"][2][o:o + k], res["0"][2][o:o + k], tol)
 
 
+@pytest.mark.parametrize("compute", ["fp32", "bf16"])
+def test_hiera_stage_window_order(compute, monkeypatch):
+    """the Hiera trunk with its whole-window stages kept in window order between one partition and one
+    unpartition (S2H_HIERA_WIN_STAGE=1; B+ at 256^2: stages 1 and 2) against a partition / unpartition
+    around every block's attention (=0, hieradet.py:146,161): every stage output bit-identical (the same
+    per-token ops and per-window attention), input and parameter gradients within summation order"""
+    from sam2_video.kernels.arena import ParamArena
+    from sam2_video.model.modeling.backbones.hieradet import Hiera
+    _ops().wgrad_workspace(DEV)
+    torch.manual_seed(12)
+    trunk = Hiera(embed_dim=112, num_heads=2, stages=(2, 3, 16, 3), global_att_blocks=(12, 16, 20))
+    assert trunk.window_stages(64, 64) == {0: (1, 8), 2: (4, 8)}
+    for p in trunk.parameters():
+        p.data = torch.randn_like(p) * 0.05
+    cd = torch.float32 if compute == "fp32" else torch.bfloat16
+    arena = ParamArena(list(trunk.named_parameters()), [n for n, _ in trunk.named_parameters()], cd, DEV)
+    x0 = torch.randn(2, 256, 256, 3, device=DEV).to(cd)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("S2H_HIERA_WIN_STAGE", flag)
+        arena.grad.zero_()
+        outs = trunk(x0)
+        gen = torch.Generator(DEV).manual_seed(5)
+        gs = [torch.randn(o.shape, device=DEV, generator=gen).to(cd) for o in outs]
+        torch.autograd.backward(outs, gs)
+        torch.cuda.synchronize()
+        res[flag] = ([o.detach().clone() for o in outs], arena.grad.clone())
+    for a, b in zip(res["0"][0], res["1"][0]):
+        assert torch.equal(a, b)
+    tol = 1e-5 if compute == "fp32" else 2e-2
+    for n in arena.grad_names:
+        o, k = arena.offsets[n], trunk.get_parameter(n).numel()
+        _close(res["1"][1][o:o + k], res["0"][1][o:o + k], tol)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("rows,cols", [(131072, 112), (13312, 2048), (5, 24), (1000, 37), (70000, 256), (3, 4096)])
 def test_colsum_shapes(dtype, rows, cols):

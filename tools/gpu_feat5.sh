@@ -14,10 +14,13 @@ timeout -k 10 900 python3 bench.py --trace-steps 10 --trace-out gpurun_out/${TAG
 cut -c1-200 gpurun_out/${TAG}_bench.log
 python3 tools/step_profile.py gpurun_out/${TAG}_kernel_stats.csv gpurun_out/${TAG}_kernel_stats_sorted.csv --steps 10 --bench gpurun_out/${TAG}_bench.log > gpurun_out/${TAG}_step_profile.txt || exit 1
 head -14 gpurun_out/${TAG}_step_profile.txt
-if [ -n "$VAR" ]; then
-  for v in "$A" "$B" "$A" "$B"; do
-    env "$VAR=$v" timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-prof --no-trace --steps 20 --warmup 3 > gpurun_out/${TAG}_ab_$v.log 2> gpurun_out/${TAG}_ab_$v.err || { echo "AB_FAILED $VAR=$v"; tail -20 gpurun_out/${TAG}_ab_$v.err; exit 1; }
-    python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_ab_$v.log'));print('$VAR=$v', d['value'], d['ms_per_step'])" | tee -a gpurun_out/${TAG}_ab.txt
+ab() {  # VAR A B: alternating A/B of one switch
+  local var=$1 a=$2 b=$3
+  for v in "$a" "$b" "$a" "$b"; do
+    env "$var=$v" timeout -k 10 300 python -u bench.py --cpu-baseline 0 --no-prof --no-trace --steps 20 --warmup 3 > gpurun_out/${TAG}_ab_$var$v.log 2> gpurun_out/${TAG}_ab_$var$v.err || { echo "AB_FAILED $var=$v"; tail -20 gpurun_out/${TAG}_ab_$var$v.err; return 1; }
+    python3 -c "import json;d=json.load(open('gpurun_out/${TAG}_ab_$var$v.log'));print('$var=$v', d['value'], d['ms_per_step'])" | tee -a gpurun_out/${TAG}_ab.txt
   done
-fi
+}
+if [ -n "$VAR" ]; then ab "$VAR" "$A" "$B" || exit 1; fi
+if [ -n "$VAR2" ]; then ab "$VAR2" "$A" "$B" || exit 1; fi
 echo CHECK_DONE
