@@ -18,30 +18,38 @@
 // O*H*W*cin, writes O*H/2*W/2*cout elements.
 #include "common.h"
 
-template <typename T, int CIN, int COUT, bool LOGIT>
+// SPLIT lanes per output pixel (adjacent lanes), each accumulating COUT / SPLIT channels: the 16 -> 64
+// stage at one thread per pixel ran ~1 wave per SIMD with 9216 dependent-free FMAs each and no latency
+// hiding (65 us per frame, profiles/r05_v16_kernel_stats.csv); the LayerNorm statistics gather the
+// pixel's channels from its SPLIT lanes and sum them in channel order.
+template <typename T, int CIN, int COUT, bool LOGIT, int SPLIT = 1>
 __global__ __launch_bounds__(256) void mask_down_kernel(int O, int H, int W, int Ho, int Wo, const void* xin,
                                                         float scale, float shift, const float* __restrict__ w,
                                                         const float* __restrict__ bias,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps, T* y) {
+  constexpr int CPT = COUT / SPLIT;
+  static_assert(CPT % 4 == 0 && (SPLIT & (SPLIT - 1)) == 0, "channel split");
   // weights transposed into LDS as [tap][ci][co]: the inner loop reads 4 output channels per
-  // ds_read_b128, the same address on every lane (broadcast)
+  // ds_read_b128, the same address on every lane of a channel group (broadcast)
   __shared__ __attribute__((aligned(16))) float wl[9 * CIN * COUT];
   for (int e = threadIdx.x; e < 9 * CIN * COUT; e += 256) {
     const int co = e % COUT, ci = (e / COUT) % CIN, tap = e / (COUT * CIN);
     wl[e] = w[(co * CIN + ci) * 9 + tap];
   }
   __syncthreads();
-  const int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) / SPLIT;
+  const int c0 = (int)(threadIdx.x % SPLIT) * CPT;
   const int64_t total = (int64_t)O * Ho * Wo;
+  // (a pixel's SPLIT lanes are adjacent and 256 % SPLIT == 0: whole pixel groups leave together)
   if (p >= total) return;
   const int ox = (int)(p % Wo);
   const int64_t t = p / Wo;
   const int oy = (int)(t % Ho);
   const int o = (int)(t / Ho);
-  float acc[COUT];
+  float acc[CPT];
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) acc[co] = bias[co];
+  for (int c = 0; c < CPT; ++c) acc[c] = bias[c0 + c];
   for (int tap = 0; tap < 9; ++tap) {
     const int iy = 2 * oy - 1 + tap / 3, ix = 2 * ox - 1 + tap % 3;
     if (iy < 0 || iy >= H || ix < 0 || ix >= W) continue;
@@ -55,42 +63,51 @@ __global__ __launch_bounds__(256) void mask_down_kernel(int O, int H, int W, int
 #pragma unroll
       for (int ci = 0; ci < CIN; ++ci) in[ci] = to_f32(xp[ci]);
     }
-    const float* wt = wl + tap * CIN * COUT;
+    const float* wt = wl + tap * CIN * COUT + c0;
 #pragma unroll
     for (int ci = 0; ci < CIN; ++ci)
 #pragma unroll
-      for (int co = 0; co < COUT; co += 4) {
-        const float4 w4 = *(const float4*)&wt[ci * COUT + co];
-        acc[co] += in[ci] * w4.x;
-        acc[co + 1] += in[ci] * w4.y;
-        acc[co + 2] += in[ci] * w4.z;
-        acc[co + 3] += in[ci] * w4.w;
+      for (int c = 0; c < CPT; c += 4) {
+        const float4 w4 = *(const float4*)&wt[ci * COUT + c];
+        acc[c] += in[ci] * w4.x;
+        acc[c + 1] += in[ci] * w4.y;
+        acc[c + 2] += in[ci] * w4.z;
+        acc[c + 3] += in[ci] * w4.w;
       }
   }
+  // the LayerNorm statistics over all COUT channels in channel order, as one thread per pixel sums
+  // them (bit-identical to SPLIT = 1): every lane of the pixel gathers the other lanes' channels
+  float all[COUT];
+  const int lane0 = (threadIdx.x & 63) & ~(SPLIT - 1);
+#pragma unroll
+  for (int j = 0; j < SPLIT; ++j)
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) all[j * CPT + c] = SPLIT == 1 ? acc[c] : __shfl(acc[c], lane0 + j, 64);
   float s = 0.f;
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) s += acc[co];
+  for (int co = 0; co < COUT; ++co) s += all[co];
   const float mu = s / COUT;
   float q = 0.f;
 #pragma unroll
-  for (int co = 0; co < COUT; ++co) q += (acc[co] - mu) * (acc[co] - mu);
+  for (int co = 0; co < COUT; ++co) q += (all[co] - mu) * (all[co] - mu);
   const float rs = 1.f / sqrtf(q / COUT + eps);
-  T* yp = y + p * COUT;
+  T* yp = y + p * COUT + c0;
 #pragma unroll
-  for (int co = 0; co < COUT; co += 4) {
+  for (int c = 0; c < CPT; c += 4) {
     T r[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) r[j] = from_f32<T>(gelu_erf((acc[co + j] - mu) * rs * gamma[co + j] + beta[co + j]));
+    for (int j = 0; j < 4; ++j)
+      r[j] = from_f32<T>(gelu_erf((acc[c + j] - mu) * rs * gamma[c0 + c + j] + beta[c0 + c + j]));
     if constexpr (sizeof(T) == 2) {
       bf16x4 v;
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = r[j];
-      *(bf16x4*)(yp + co) = v;
+      *(bf16x4*)(yp + c) = v;
     } else {
       f32x4 v;
 #pragma unroll
       for (int j = 0; j < 4; ++j) v[j] = r[j];
-      *(f32x4*)(yp + co) = v;
+      *(f32x4*)(yp + c) = v;
     }
   }
 }
@@ -102,6 +119,7 @@ static int mask_down(int O, int H, int W, int cin, int cout, const void* x, int 
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;  // (H + 2 - 3) / 2 + 1
   const int64_t total = (int64_t)O * Ho * Wo;
   const dim3 grid((unsigned)((total + 255) / 256)), blk(256);
+  const dim3 grid4((unsigned)((4 * total + 255) / 256));  // 4 lanes per pixel
   if (cin == 1 && cout == 4 && x_logit)
     hipLaunchKernelGGL((mask_down_kernel<T, 1, 4, true>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b, g,
                        be, eps, (T*)y);
@@ -112,8 +130,8 @@ static int mask_down(int O, int H, int W, int cin, int cout, const void* x, int 
     hipLaunchKernelGGL((mask_down_kernel<T, 4, 16, false>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b,
                        g, be, eps, (T*)y);
   else if (cin == 16 && cout == 64 && !x_logit)
-    hipLaunchKernelGGL((mask_down_kernel<T, 16, 64, false>), grid, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w, b,
-                       g, be, eps, (T*)y);
+    hipLaunchKernelGGL((mask_down_kernel<T, 16, 64, false, 4>), grid4, blk, 0, st, O, H, W, Ho, Wo, x, scale, shift, w,
+                       b, g, be, eps, (T*)y);
   else
     return (int)hipErrorInvalidValue;
   return (int)hipGetLastError();
