@@ -509,6 +509,12 @@ int s2h_dwconv(int dt, int B, int H, int W, int C, int K, int pad, const void* x
  * dir 1 gathers the output gradient into GEMM layout (mask_decoder.py:66-75). */
 int s2h_convt2(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
                void* out, int dir, hipStream_t st);
+/* The forward scatter vectorised with the bias and the residual add fused (round 5; mask_decoder.py:105-107
+ * dc1(x) + feat_s1, dc2(x) + feat_s0): out[b, 2y+dy, 2x+dx, co] = Y[(b,y,x)][co*4 + dy*2 + dx] + bias[co]
+ * (+ add[b or 0 when add_bcast, 2y+dy, 2x+dx, co]), rounded after the bias and after the add as the
+ * two launches it replaces.  Co % (16 B / element) == 0, 16-B aligned buffers. */
+int s2h_convt2_store(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                     int add_bcast, void* out, hipStream_t st);
 /* y[r, :] = gate[r] > 0 ? x[r, :] : fill; dir 1 = backward (object-score gating to
  * NO_OBJ_SCORE, sam2_base.py:380-389). */
 int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, float fill,

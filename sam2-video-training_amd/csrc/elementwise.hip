@@ -1172,6 +1172,69 @@ extern "C" int s2h_convt2(int dt, int B, int H, int W, int Co, const void* Y, co
   return (int)hipGetLastError();
 }
 
+// Vectorised scatter with the bias and the residual add fused (round 5, the mask decoder's upscaling
+// dc1(x) + feat_s1 / dc2(x) + feat_s0, mask_decoder.py:105-107): one thread per (pixel, 16-B channel
+// group) reads the group's 4 x V contiguous GEMM outputs (4 16-B loads: co*4 + s for its V channels)
+// and writes the 2 x 2 output pixels (4 16-B stores), + bias[co] + add (add_bcast: one batch broadcast
+// over B), bit-identical to the scalar scatter (2-B accesses at stride 4) followed by the separate
+// (broadcast) add it replaces.
+template <typename T>
+__global__ __launch_bounds__(256) void convt2_store_kernel(int B, int H, int W, int Co, const T* Y,
+                                                           const float* bias, const T* add, int add_bcast, T* out) {
+  constexpr int V = 16 / sizeof(T);
+  const int CG = Co / V;
+  const int64_t n = (int64_t)B * H * W * CG;
+  GRID_STRIDE(i, n) {
+    const int cg = (int)(i % CG);
+    const int64_t p = i / CG;  // (b * H + y) * W + x
+    const int x = (int)(p % W);
+    const int64_t t = p / W;
+    const int y = (int)(t % H);
+    const int b = (int)(t / H);
+    T e[4 * V];
+    const uint4* yr = (const uint4*)(Y + p * 4 * Co + (int64_t)cg * V * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *(uint4*)(e + u * V) = yr[u];
+    float bv[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) bv[j] = bias ? bias[cg * V + j] : 0.f;
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      const int dy = sidx >> 1, dx = sidx & 1;
+      const int64_t pix = ((int64_t)(2 * y + dy) * 2 * W + 2 * x + dx);  // within batch b
+      const int64_t o = ((int64_t)b * 4 * H * W + pix) * Co + cg * V;
+      float v[V];
+      // rounded to T after the bias and again after the add: the values of the scatter + add launches
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = to_f32(from_f32<T>(to_f32(e[4 * j + sidx]) + bv[j]));
+      if (add) {
+        T ad[V];
+        *(uint4*)ad = *(const uint4*)(add + (add_bcast ? pix * Co + cg * V : o));
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] += to_f32(ad[j]);
+      }
+      T r[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) r[j] = from_f32<T>(v[j]);
+      *(uint4*)(out + o) = *(const uint4*)r;
+    }
+  }
+}
+extern "C" int s2h_convt2_store(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                                int add_bcast, void* out, hipStream_t st) {
+  const int V = dt == S2H_BF16 ? 8 : 4;
+  if (Co % V || !al16(Y) || !al16(out) || (add && !al16(add))) return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * H * W * (Co / V);
+  if (n <= 0) return 0;
+  if (dt == S2H_BF16)
+    hipLaunchKernelGGL(convt2_store_kernel<bf16>, ew_grid(n), dim3(256), 0, st, B, H, W, Co, (const bf16*)Y, bias,
+                       (const bf16*)add, add_bcast, (bf16*)out);
+  else
+    hipLaunchKernelGGL(convt2_store_kernel<float>, ew_grid(n), dim3(256), 0, st, B, H, W, Co, (const float*)Y, bias,
+                       (const float*)add, add_bcast, (float*)out);
+  return (int)hipGetLastError();
+}
+
 // -------------------------------------------------- per-row gate / select
 // y[r, j] = gate[r] > 0 ? x[r, j] : fill ;  backward (dir 1): dx = gate > 0 ? dy : 0
 template <typename T>

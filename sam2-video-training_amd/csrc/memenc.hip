@@ -33,9 +33,19 @@ __global__ __launch_bounds__(256) void mask_down_kernel(int O, int H, int W, int
   // weights transposed into LDS as [tap][ci][co]: the inner loop reads 4 output channels per
   // ds_read_b128, the same address on every lane of a channel group (broadcast)
   __shared__ __attribute__((aligned(16))) float wl[9 * CIN * COUT];
-  for (int e = threadIdx.x; e < 9 * CIN * COUT; e += 256) {
-    const int co = e % COUT, ci = (e / COUT) % CIN, tap = e / (COUT * CIN);
-    wl[e] = w[(co * CIN + ci) * 9 + tap];
+  {  // every load issued before the first LDS store (a rolled load -> store loop paid one L2 round trip
+     // per element: 36 of them per thread in the 16 -> 64 stage)
+    constexpr int NWT = 9 * CIN * COUT, PER = (NWT + 255) / 256;
+    float tw[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = threadIdx.x + 256 * j;
+      const int co = e % COUT, ci = (e / COUT) % CIN, tap = e / (COUT * CIN);
+      tw[j] = e < NWT ? w[(co * CIN + ci) * 9 + tap] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (threadIdx.x + 256 * j < NWT) wl[threadIdx.x + 256 * j] = tw[j];
   }
   __syncthreads();
   const int64_t p = ((int64_t)blockIdx.x * 256 + threadIdx.x) / SPLIT;

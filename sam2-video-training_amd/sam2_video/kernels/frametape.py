@@ -1152,21 +1152,23 @@ def conv_transpose2x2(tape: FrameTape, x, mod, add=None):
     op, first = tape._begin("convt", [x, add], _convt_bw, {"mod": mod})
     B, H, W, Ci = x.shape
     Co = mod.out_ch
+    w = mod.compute_weight()
+    # the GEMM output is scratch: the backward needs only x and the output gradient
+    Y = torch.empty(B * H * W, 4 * Co, device=x.device, dtype=x.dtype)
+    ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
+             ldc=4 * Co)
     vid, out = tape._out(0, (B, 2 * H, 2 * W, Co), x.dtype)
-    if ops.convt2_direct():  # the GEMM stores into the NHWC output (no [rows, 4 Co] aux + scatter)
-        ops.convt2_gemm(x, *mod.store_weight(), out)
+    if ops.convt2_direct() and Co % (16 // x.element_size()) == 0:  # scatter + bias + add, one launch
+        ops.convt2_store(Y, B, H, W, Co, bias=mod.bias.detach(), add=None if add is None else add.contiguous(),
+                         out=out)
     else:
-        w = mod.compute_weight()
-        Y = tape._aux("Y", (B * H * W, 4 * Co), x.dtype)
-        ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
-                 ldc=4 * Co)
         ops.convt2_scatter(Y, B, H, W, Co, bias=mod.bias.detach(), add=None, out=out)
-    if add is not None:
-        add = add.contiguous()
-        if add.shape[0] == B:
-            ops.add(out, add, out=out)
-        else:
-            ops.add_bcast(out, add, out=out)
+        if add is not None:
+            add = add.contiguous()
+            if add.shape[0] == B:
+                ops.add(out, add, out=out)
+            else:
+                ops.add_bcast(out, add, out=out)
     if first:
         op.attrs.update(B=B, H=H, W=W, Ci=Ci, Co=Co, bcast=add is not None and add.shape[0] != B)
     tape._finish(op, [vid], tape._req(op, (mod.weight, mod.bias)))

@@ -150,20 +150,19 @@ class _ConvT2(torch.autograd.Function):
     def forward(ctx, x, wp, bp, mod, add):
         B, H, W, Ci = x.shape
         Co = mod.out_ch
-        if ops.convt2_direct():
-            out = torch.empty(B, 2 * H, 2 * W, Co, device=x.device, dtype=x.dtype)
-            ops.convt2_gemm(x.contiguous(), *mod.store_weight(), out)
+        w = mod.compute_weight()
+        Y = torch.empty(B * H * W, 4 * Co, device=x.device, dtype=x.dtype)
+        ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co,
+                 ldb_n=1, ldc=4 * Co)
+        if ops.convt2_direct() and Co % (16 // x.element_size()) == 0:  # scatter + bias + add, one launch
+            out = ops.convt2_store(Y, B, H, W, Co, bias=bp.detach(), add=None if add is None else add.contiguous())
         else:
-            w = mod.compute_weight()
-            Y = torch.empty(B * H * W, 4 * Co, device=x.device, dtype=x.dtype)
-            ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co,
-                     ldb_n=1, ldc=4 * Co)
             out = ops.convt2_scatter(Y, B, H, W, Co, bias=bp.detach(), add=None)
-        if add is not None:
-            if add.shape[0] == B:
-                out = ops.add(out, add.contiguous())
-            else:
-                out = ops.add_bcast(out, add.contiguous())
+            if add is not None:
+                if add.shape[0] == B:
+                    out = ops.add(out, add.contiguous())
+                else:
+                    out = ops.add_bcast(out, add.contiguous())
         ctx.mod = mod
         ctx.add_bcast = add is not None and add.shape[0] != B
         ctx.has_add = add is not None

@@ -1021,28 +1021,26 @@ def convt2_scatter(Y, B, H, W, Co, bias=None, add=None, out=None):
     return out
 
 
-# S2H_CONVT_DIRECT=0: the GEMM into an aux [rows, 4 Co] buffer + the scatter kernel (A/B)
+# S2H_CONVT_DIRECT=0: the scalar scatter + a separate (broadcast) add (A/B)
 _CONVT_DIRECT = os.environ.get("S2H_CONVT_DIRECT", "1") == "1"
-
-
-def convt2_gemm(x, wp, b2, out):
-    """ConvTranspose2d(2, 2) + bias, stored straight into the NHWC output: for each dy the GEMM over
-    the (b, y) image rows, M = W pixels, N = 2 Co columns (dx, co) with W' = the (dy, dx, co)-ordered
-    weight (ConvTranspose2x2.store_weight), lands in out[b, 2y + dy, 2x + dx, co] -- row x at
-    2 Co * x, image row (b, y) at 4 W Co * (b H + y), column block dy at 2 W Co * dy: plain strides,
-    so two batched GEMM launches replace the GEMM + the scatter pass (mask_decoder.py:105-107)"""
-    B, H, W, Ci = x.shape
-    Co = out.shape[-1]
-    assert out.shape == (B, 2 * H, 2 * W, Co) and out.is_contiguous() and x.is_contiguous()
-    flat = out.view(-1)
-    for dy in (0, 1):
-        gemm(x, wp[:, dy * 2 * Co:], flat[dy * 2 * W * Co:], M=W, N=2 * Co, K=Ci, lda_m=Ci, lda_k=1,
-             ldb_k=4 * Co, ldb_n=1, ldc=2 * Co, batch=B * H, sA=W * Ci, sB=0, sC=4 * W * Co, bias=b2)
-    return out
 
 
 def convt2_direct():
     return _CONVT_DIRECT
+
+
+def convt2_store(Y, B, H, W, Co, bias=None, add=None, out=None):
+    """out = scatter(Y) + bias (+ add: [B or 1, 2H, 2W, Co], broadcast over B when it has one batch),
+    vectorised, one rounding (s2h_convt2_store)"""
+    if out is None:
+        out = torch.empty(B, 2 * H, 2 * W, Co, device=Y.device, dtype=Y.dtype)
+    bc = 0
+    if add is not None:
+        assert add.is_contiguous() and add.dtype == Y.dtype and add.shape[1:] == out.shape[1:]
+        assert add.shape[0] in (1, B)
+        bc = int(add.shape[0] == 1 and B > 1)
+    call("s2h_convt2_store", dt(Y), B, H, W, Co, ptr(Y), ptr(bias), ptr(add), bc, ptr(out), stream())
+    return out
 
 
 def convt2_gather(dout, B, H, W, Co, dY=None):

@@ -8,7 +8,6 @@ import torch
 from torch import nn
 
 from ...kernels import functional as FN
-from ...kernels import ops
 
 
 def _compute(p):
@@ -98,23 +97,6 @@ class ConvTranspose2x2(nn.Module):
 
     def compute_weight(self):
         return _compute(self.weight).view(self.in_ch, self.out_ch * 4)
-
-    def store_weight(self):
-        """(W', b2) for the forward's direct store (ops.convt2_gemm): the weight's columns reordered
-        (co, dy, dx) -> (dy, dx, co), so each 2x2 output position is a contiguous block of Co columns,
-        and the bias repeated for the two dx positions; rebuilt once per weight generation"""
-        if getattr(self, "_st_gen", None) != FN._GEN[0]:
-            w = self.compute_weight()
-            Ci, Co = self.in_ch, self.out_ch
-            if getattr(self, "_st_w", None) is None:
-                self._st_w = torch.empty(Ci, 4 * Co, device=w.device, dtype=w.dtype)
-                self._st_b = torch.empty(2 * Co, device=w.device, dtype=torch.float32)
-            # [ci][co*4 + dy*2 + dx] -> [ci][(dy*2 + dx)*Co + co]: the 2x2 scatter with H = W = 1
-            ops.convt2_scatter(w, Ci, 1, 1, Co, out=self._st_w.view(Ci, 2, 2, Co))
-            b = self.bias.detach()
-            ops.copy_segments([(b, self._st_b[:Co]), (b, self._st_b[Co:])])
-            self._st_gen = FN._GEN[0]
-        return self._st_w, self._st_b
 
 
 class LayerNorm(nn.Module):

@@ -184,9 +184,10 @@ def test_vfold_step_matches_unfolded_step_bf16(monkeypatch):
     assert torch.nn.functional.cosine_similarity(flat0, flat1, dim=0).item() >= 0.99
 
 
-@pytest.mark.parametrize("Lq,lks,p_drop", [(200, [300, 700], 0.1), (256, [1028, 129], 0.0)])
+@pytest.mark.parametrize("Lq,lks,p_drop", [(200, [300, 700], 0.1), (256, [1028, 129], 0.0), (160, [70, 33], 0.1),
+                                          (128, [200, 64], 0.0)])
 def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
-    """the two-waves-per-SIMD V-fold dK kernel (flash_bwd_dkf_kernel, default) against the
+    """the two-waves-per-SIMD V-fold dK kernel (flash_bwd_dkv16_kernel, default) against the
     one-wave-per-SIMD 32x32 kernel it replaced (s2h_attn_config(3)) on the same frame table: dK
     equal to fp32-summation-order rounding (query tails, key tails, keep bitmap on and off); dQ is
     the same kernel in both and must be bit-identical"""
@@ -237,7 +238,9 @@ def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
     """the fused value + output projection (FN.VFoldOutProj: one GEMM with W' = Wo [Wv | bv]) against
     the two GEMMs (S2H_VFOLD_OUT=0) in a bf16 B+ 256^2 training step, dropout off: logits, loss and
     the out_proj / v_proj gradients of the memory cross-attention within bf16 rounding (cosine >= 0.999,
-    max |difference| <= 3 % of the tensor's max |gradient| (measured 1.5-1.7 %); G = dY^T u' kept in fp32)"""
+    max |difference| <= 3 % of the tensor's max |gradient| (measured 1.5-1.8 %); G = dY^T u' kept in fp32;
+    a round-5 variant of the mask decoder's ConvTranspose that rounded its output once instead of twice
+    moved this to 2.7-3.9 %, bf16 noise that the step's data amplifies)"""
     from step_harness import build_model, golden_batch, grads_by_name, load_golden, mask_iou, run_step
     g = load_golden("bplus256_point_all")
     batch = golden_batch(g).to(DEV)
@@ -261,10 +264,11 @@ def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
         cos = torch.nn.functional.cosine_similarity(g0[n].flatten(), g1[n].flatten(), dim=0).item()
         rel = ((g0[n] - g1[n]).abs().max() / g0[n].abs().max()).item()  # max error relative to the tensor's scale
         worst[n] = (round(cos, 6), round(rel, 5))
+    print("out_proj / v_proj gradients, fused vs two GEMMs (cosine, max rel err):", worst)
+    for n, (cos, rel) in worst.items():
         assert cos >= 0.999, (n, cos)
         # a systematic bias of the fused weight gradients (G rounded to bf16) would show here
         assert rel <= 0.03, (n, rel)
-    print("out_proj / v_proj gradients, fused vs two GEMMs (cosine, max rel err):", worst)
 
 
 @pytest.mark.parametrize("lks,nrots,p_drop", [([1028, 2060], [1024, 2048], 0.1), ([1024, 516], [1024, 512], 0.0)])

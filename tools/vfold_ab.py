@@ -2,7 +2,7 @@
 13 objects x 1024 queries against the 7 frames' packed memories (1028 n keys, n = 1..7), dropout
 0.1 with the forward's keep bitmap, one frame-table launch (s2h_flash_bwd_frames_vfold).  Variants
 by s2h_attn_config: 1 = current kernels (two-waves-per-SIMD dK), 3 = the one-wave-per-SIMD 32x32 dK
-kernel.  Rounds interleave the variants.   GPU only:  python tools/vfold_ab.py [--iters 10]"""
+kernel.  Rounds interleave the variants.   GPU only:  python tools/vfold_ab.py [--iters 10] [--variants 1,3]"""
 import argparse
 import os
 import sys
@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--drop", type=float, default=0.1)
+    ap.add_argument("--variants", default="1,3")
     a = ap.parse_args()
     torch.manual_seed(0)
     B, Lq = 13, 1024
@@ -68,10 +69,11 @@ def main():
                                    koff=koff)
     pairs = B * Lq * sum(lks)
     prev = lib().s2h_attn_config(1)
-    res = {1: [], 3: []}
+    vs = [int(v) for v in a.variants.split(",")]
+    res = {v: [] for v in vs}
     try:
         for _ in range(a.rounds):
-            for v in (1, 3):
+            for v in vs:
                 lib().s2h_attn_config(v)
                 res[v].append(timeit(bwd, a.iters))
     finally:
