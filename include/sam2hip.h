@@ -515,6 +515,11 @@ int s2h_convt2(int dt, int B, int H, int W, int Co, const void* Y, const float* 
  * two launches it replaces.  Co % (16 B / element) == 0, 16-B aligned buffers. */
 int s2h_convt2_store(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
                      int add_bcast, void* out, hipStream_t st);
+/* The mask decoder's last upscaling step and mask head in one pass (mask_decoder.py:105-113, bf16,
+ * Co = 32): pre = the s2h_convt2_store values, post = gelu(pre) (as s2h_act_fwd rounds it), masks[b][p] =
+ * sum_c hyper[b][c] post[b][p][c] (fp32 sum, bf16 store); pre / post [B, 2H, 2W, 32], masks [B, 2H * 2W]. */
+int s2h_convt2_tail(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                    int add_bcast, const void* hyper, void* pre, void* post, void* masks, hipStream_t st);
 /* y[r, :] = gate[r] > 0 ? x[r, :] : fill; dir 1 = backward (object-score gating to
  * NO_OBJ_SCORE, sam2_base.py:380-389). */
 int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, float fill,

@@ -1235,6 +1235,80 @@ extern "C" int s2h_convt2_store(int dt, int B, int H, int W, int Co, const void*
   return (int)hipGetLastError();
 }
 
+// The mask decoder's last upscaling step and mask head in one pass (round 5; mask_decoder.py:105-113:
+// u = gelu(dc2(x) + feat_s0), masks = hyper0 . u per pixel): the convt2_store values (pre, the GEMM
+// output scattered + bias + add, rounded as the separate launches round it), post = gelu(pre) rounded
+// as act_fwd rounds it, and masks[b][pixel] = sum_c hyper[b][c] post[c] (fp32, the CG lanes of a pixel
+// reduced by xor shuffles).  pre and post are stored for the backward (the GELU' and the hyper
+// product's gradients).  Replaces the scatter, the activation and a batched M = 1 GEMM (30 us per
+// frame, 13 row-vector products).
+template <typename T, int CG>
+__global__ __launch_bounds__(256) void convt2_tail_kernel(int B, int H, int W, const T* Y, const float* bias,
+                                                          const T* add, int add_bcast, const T* hyper, T* pre, T* post,
+                                                          T* masks) {
+  constexpr int V = 16 / sizeof(T);
+  constexpr int Co = CG * V;
+  const int64_t n = (int64_t)B * H * W * CG;
+  GRID_STRIDE(i, n) {  // (n is a multiple of CG: a pixel's CG lanes stay together)
+    const int cg = (int)(i % CG);
+    const int64_t p = i / CG;  // (b * H + y) * W + x
+    const int x = (int)(p % W);
+    const int64_t t = p / W;
+    const int y = (int)(t % H);
+    const int b = (int)(t / H);
+    T e[4 * V];
+    const uint4* yr = (const uint4*)(Y + p * 4 * Co + (int64_t)cg * V * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *(uint4*)(e + u * V) = yr[u];
+    float bv[V], hv[V];
+    T hb[V];
+    *(uint4*)hb = *(const uint4*)(hyper + (int64_t)b * Co + cg * V);
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      bv[j] = bias ? bias[cg * V + j] : 0.f;
+      hv[j] = to_f32(hb[j]);
+    }
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      const int dy = sidx >> 1, dx = sidx & 1;
+      const int64_t pix = ((int64_t)(2 * y + dy) * 2 * W + 2 * x + dx);  // within batch b
+      const int64_t o = ((int64_t)b * 4 * H * W + pix) * Co + cg * V;
+      float v[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = to_f32(from_f32<T>(to_f32(e[4 * j + sidx]) + bv[j]));
+      if (add) {
+        T ad[V];
+        *(uint4*)ad = *(const uint4*)(add + (add_bcast ? pix * Co + cg * V : o));
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] += to_f32(ad[j]);
+      }
+      T r[V], g[V];
+      float dot = 0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        r[j] = from_f32<T>(v[j]);
+        g[j] = from_f32<T>(gelu_erf(to_f32(r[j])) + 0.f);  // (+ 0: act_fwd's `* 1 + 0`, -0 -> +0)
+        dot += hv[j] * to_f32(g[j]);
+      }
+      *(uint4*)(pre + o) = *(const uint4*)r;
+      *(uint4*)(post + o) = *(const uint4*)g;
+#pragma unroll
+      for (int m = 1; m < CG; m <<= 1) dot += __shfl_xor(dot, m, 64);
+      if (cg == 0) masks[(int64_t)b * 4 * H * W + pix] = from_f32<T>(dot);
+    }
+  }
+}
+extern "C" int s2h_convt2_tail(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                               int add_bcast, const void* hyper, void* pre, void* post, void* masks, hipStream_t st) {
+  if (dt != S2H_BF16 || Co != 32 || !al16(Y) || !al16(pre) || !al16(post) || !al16(hyper) || (add && !al16(add)))
+    return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * H * W * 4;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL((convt2_tail_kernel<bf16, 4>), ew_grid(n), dim3(256), 0, st, B, H, W, (const bf16*)Y, bias,
+                     (const bf16*)add, add_bcast, (const bf16*)hyper, (bf16*)pre, (bf16*)post, (bf16*)masks);
+  return (int)hipGetLastError();
+}
+
 // -------------------------------------------------- per-row gate / select
 // y[r, j] = gate[r] > 0 ? x[r, j] : fill ;  backward (dir 1): dx = gate > 0 ? dy : 0
 template <typename T>

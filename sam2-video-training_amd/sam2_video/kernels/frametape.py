@@ -1042,11 +1042,12 @@ def _add_bcast_bw(tape, op, gys):
     return [da, db]
 
 
-def act(tape: FrameTape, x, a):
+def act(tape: FrameTape, x, a, _compute=True):
     x = x if x.is_contiguous() else x.contiguous()
     op, first = tape._begin("act", [x], _act_bw, {"act": a})
     vid, out = tape._out(0, x.shape, x.dtype)
-    ops.act_fwd(x, a, out=out)
+    if _compute:
+        ops.act_fwd(x, a, out=out)
     tape._finish(op, [vid], any(op.needs))
     return out
 
@@ -1146,12 +1147,19 @@ def _select_bw(tape, op, gys):
 
 
 # ---------------------------------------------------------------- SAM pieces
-def conv_transpose2x2(tape: FrameTape, x, mod, add=None):
-    """ConvTranspose2d(2, 2) + bias (+ add broadcast over the batch when it has batch 1)"""
+def conv_transpose2x2(tape: FrameTape, x, mod, add=None, _compute=True):
+    """ConvTranspose2d(2, 2) + bias (+ add broadcast over the batch when it has batch 1);
+    _compute=False: record only, returns the output slot"""
     x = x if x.is_contiguous() else x.contiguous()
     op, first = tape._begin("convt", [x, add], _convt_bw, {"mod": mod})
     B, H, W, Ci = x.shape
     Co = mod.out_ch
+    if not _compute:
+        vid, out = tape._out(0, (B, 2 * H, 2 * W, Co), x.dtype)
+        if first:
+            op.attrs.update(B=B, H=H, W=W, Ci=Ci, Co=Co, bcast=add is not None and add.shape[0] != B)
+        tape._finish(op, [vid], tape._req(op, (mod.weight, mod.bias)))
+        return out
     w = mod.compute_weight()
     # the GEMM output is scratch: the backward needs only x and the output gradient
     Y = torch.empty(B * H * W, 4 * Co, device=x.device, dtype=x.dtype)
@@ -1208,13 +1216,14 @@ def _convt_bw(tape, op, gys):
     return [dx, dadd]
 
 
-def hyper_mask(tape: FrameTape, hyper, up):
+def hyper_mask(tape: FrameTape, hyper, up, _compute=True):
     """masks[o, p] = sum_c hyper[o, c] up[o, p, c]"""
     hyper = hyper if hyper.is_contiguous() else hyper.contiguous()
     op, first = tape._begin("hyper", [hyper, up], _hyper_bw, {})
     O, P, C = up.shape
     vid, out = tape._out(0, (O, P), up.dtype)
-    ops.bmm(hyper.view(O, 1, C), up, out.view(O, 1, P), trans_b=True)
+    if _compute:
+        ops.bmm(hyper.view(O, 1, C), up, out.view(O, 1, P), trans_b=True)
     if first:
         op.attrs.update(O=O, P=P, C=C)
     tape._finish(op, [vid], any(op.needs))
@@ -1238,6 +1247,30 @@ def _hyper_bw(tape, op, gys):
                  sC=P * C)
         dup = dup.view(-1)
     return [dh, dup]
+
+
+def convt_tail_ok(x, mod, add, hyper):
+    return (ops.convt2_tail_enabled() and x.dtype == torch.bfloat16 and mod.out_ch == 32 and hyper.dim() == 2
+            and hyper.shape == (x.shape[0], 32) and (add is None or add.shape[1:] == (2 * x.shape[1], 2 * x.shape[2], 32)))
+
+
+def convt_tail(tape: FrameTape, x, mod, add, hyper):
+    """masks = hyper_mask(hyper, gelu(conv_transpose2x2(x, mod, add))) (mask_decoder.py:105-113) as
+    one GEMM + one launch (s2h_convt2_tail), recorded as the same three tape ops (convt, act, hyper)
+    with their saved values, so the frame-batched backward is unchanged"""
+    x = x if x.is_contiguous() else x.contiguous()
+    hyper = hyper if hyper.is_contiguous() else hyper.contiguous()
+    add = None if add is None else add.contiguous()
+    B, H, W, Ci = x.shape
+    Co = mod.out_ch
+    pre = conv_transpose2x2(tape, x, mod, add=add, _compute=False)
+    post = act(tape, pre, "gelu", _compute=False)
+    masks = hyper_mask(tape, hyper, post.view(B, -1, Co), _compute=False)
+    Y = torch.empty(B * H * W, 4 * Co, device=x.device, dtype=x.dtype)  # scratch
+    ops.gemm(x.reshape(-1, Ci), mod.compute_weight(), Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1,
+             ldb_k=4 * Co, ldb_n=1, ldc=4 * Co)
+    ops.convt2_tail(Y, B, H, W, Co, mod.bias.detach(), add, hyper, pre, post, masks)
+    return masks
 
 
 def point_embed(tape: FrameTape, pe, labels, dtype, tables):

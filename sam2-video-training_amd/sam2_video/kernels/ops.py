@@ -1043,6 +1043,22 @@ def convt2_store(Y, B, H, W, Co, bias=None, add=None, out=None):
     return out
 
 
+def convt2_tail(Y, B, H, W, Co, bias, add, hyper, pre, post, masks):
+    """pre = convt2_store(Y) + bias + add, post = gelu(pre), masks[b] = post[b] . hyper[b] (s2h_convt2_tail)"""
+    bc = 0
+    if add is not None:
+        assert add.is_contiguous() and add.dtype == Y.dtype and add.shape[0] in (1, B)
+        bc = int(add.shape[0] == 1 and B > 1)
+    assert hyper.is_contiguous() and hyper.numel() == B * Co and pre.is_contiguous() and post.is_contiguous()
+    call("s2h_convt2_tail", dt(Y), B, H, W, Co, ptr(Y), ptr(bias), ptr(add), bc, ptr(hyper), ptr(pre), ptr(post),
+         ptr(masks), stream())
+    return masks
+
+
+def convt2_tail_enabled():
+    return os.environ.get("S2H_CONVT_TAIL", "1") == "1"
+
+
 def convt2_gather(dout, B, H, W, Co, dY=None):
     if dY is None:
         dY = torch.empty(B * H * W, 4 * Co, device=dout.device, dtype=dout.dtype)

@@ -104,12 +104,16 @@ class MaskDecoder(nn.Module):
         dc1, ln1, _, dc2, _ = self.output_upscaling
         u = conv_transpose2x2(src.view(O, h, w, C), dc1, add=feat_s1)
         u = FN.act(ln1(u), "gelu")
-        u = conv_transpose2x2(u, dc2, add=feat_s0)
-        u = FN.act(u, "gelu")
         # the hypernetwork MLP of mask token 0 and the IoU head: one launch (FN.mlp_heads)
         hyper0, iou_pred = FN.mlp_heads([(self.output_hypernetworks_mlps[0], mask_token0),
                                          (self.iou_prediction_head, iou_token_out)])
-        masks = hyper_mask(hyper0, u.view(O, -1, C // 8))
+        if T is not None and _ft.convt_tail_ok(u, dc2, feat_s0, hyper0):
+            # dc2 + feat_s0, GELU and the mask head in one launch after the GEMM (frametape.convt_tail)
+            masks = _ft.convt_tail(T, u, dc2, feat_s0, hyper0)
+        else:
+            u = conv_transpose2x2(u, dc2, add=feat_s0)
+            u = FN.act(u, "gelu")
+            masks = hyper_mask(hyper0, u.view(O, -1, C // 8))
         iou0 = FN.cast(FN.select_token(iou_pred.unsqueeze(-1), 0), torch.float32)
         if defer_score:  # the caller runs the object-score head with its other no-grad heads (one launch)
             return masks, iou0, mask_token0, hs[:, 0].detach()

@@ -37,3 +37,68 @@ def test_convt2_store(dtype, shape, add_batch):
     assert torch.equal(out, ref)
     tol = 1e-2 if dtype == torch.bfloat16 else 1e-4
     assert (out.float() - t).abs().max().item() <= tol * t.abs().max().item()
+
+
+def test_convt2_tail_matches_three_launches():
+    """dc2 + feat_s0, GELU and the hypernetwork mask product in one launch (s2h_convt2_tail,
+    mask_decoder.py:105-113) against convt2_store + act_fwd + the batched GEMM: the saved pre / post
+    activations bit-identical, the mask logits equal to the bf16 rounding of a differently ordered
+    32-term fp32 sum"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(3)
+    B, H, W, Ci, Co = 13, 64, 64, 64, 32
+    bf = torch.bfloat16
+    w = (torch.randn(Ci, 4 * Co, device=DEV) / 8).to(bf)
+    bias = torch.randn(Co, device=DEV) * 0.1
+    x = torch.randn(B, H, W, Ci, device=DEV).to(bf)
+    add = torch.randn(1, 2 * H, 2 * W, Co, device=DEV).to(bf)
+    hyper = torch.randn(B, Co, device=DEV).to(bf)
+    Y = torch.empty(B * H * W, 4 * Co, device=DEV, dtype=bf)
+    ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
+             ldc=4 * Co)
+    pre = torch.empty(B, 2 * H, 2 * W, Co, device=DEV, dtype=bf)
+    post = torch.empty_like(pre)
+    masks = torch.empty(B, 4 * H * W, device=DEV, dtype=bf)
+    ops.convt2_tail(Y, B, H, W, Co, bias, add, hyper, pre, post, masks)
+    ref_pre = ops.convt2_store(Y, B, H, W, Co, bias=bias, add=add)
+    ref_post = ops.act_fwd(ref_pre, "gelu")
+    ref_masks = torch.empty(B, 1, 4 * H * W, device=DEV, dtype=bf)
+    ops.bmm(hyper.view(B, 1, Co), ref_post.view(B, -1, Co), ref_masks, trans_b=True)
+    torch.cuda.synchronize()
+    assert torch.equal(pre, ref_pre)
+    assert torch.equal(post, ref_post)
+    exact = (post.float().view(B, -1, Co) * hyper.float().view(B, 1, Co)).sum(-1)
+    scale = exact.abs().max().item()
+    assert (masks.float() - exact).abs().max().item() <= 8e-3 * scale
+    assert (masks.float() - ref_masks.view(B, -1).float()).abs().max().item() <= 8e-3 * scale
+    # at most a few bf16 ulps apart on a small fraction of the logits
+    assert (masks != ref_masks.view(B, -1)).float().mean().item() < 0.05
+
+
+def test_mask_decoder_tail_fused_matches_unfused_bf16(monkeypatch):
+    """a bf16 B+ 256^2 training step with the mask decoder's dc2 / GELU / mask head fused (default) and
+    as three launches (S2H_CONVT_TAIL=0): per-stage mask logits, loss and every gradient within bf16
+    rounding of the mask logits' fp32 sum order"""
+    from step_harness import build_model, golden_batch, grads_by_name, load_golden, mask_iou, run_step
+    g = load_golden("bplus256_point_all")
+    batch = golden_batch(g).to(DEV)
+    res = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("S2H_CONVT_TAIL", flag)
+        model = build_model("base_plus", 256, ["image_encoder", "memory_attention", "memory_encoder", "mask_decoder",
+                                               "prompt_encoder"], "point", dtype="bf16")
+        stages, merged, losses, _ = run_step(model, batch)
+        res[flag] = ([s["pred_masks"].detach().float().cpu() for s in stages], float(losses["total_loss"]),
+                     grads_by_name(model))
+    (m0, l0, g0), (m1, l1, g1) = res["0"], res["1"]
+    for a, b in zip(m0, m1):
+        assert mask_iou(a, b) >= 0.99
+        assert (a - b).abs().max().item() <= 0.03 * b.abs().max().item()
+    assert abs(l0 - l1) <= 3e-3 * abs(l0), (l0, l1)
+    flat0 = torch.cat([v.flatten() for v in g0.values()]).double()
+    flat1 = torch.cat([v.flatten() for v in g1.values()]).double()
+    assert torch.nn.functional.cosine_similarity(flat0, flat1, dim=0).item() >= 0.999
+    for n in ("sam_mask_decoder.output_upscaling.3.weight", "sam_mask_decoder.output_upscaling.3.bias",
+              "sam_mask_decoder.output_hypernetworks_mlps.0.layers.2.weight"):
+        cos = torch.nn.functional.cosine_similarity(g0[n].flatten().double(), g1[n].flatten().double(), dim=0).item()
+        assert cos >= 0.99, (n, cos)
