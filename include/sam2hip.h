@@ -520,6 +520,12 @@ int s2h_convt2_store(int dt, int B, int H, int W, int Co, const void* Y, const f
  * sum_c hyper[b][c] post[b][p][c] (fp32 sum, bf16 store); pre / post [B, 2H, 2W, 32], masks [B, 2H * 2W]. */
 int s2h_convt2_tail(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
                     int add_bcast, const void* hyper, void* pre, void* post, void* masks, hipStream_t st);
+/* The first upscaling step in one pass (mask_decoder.py:105-106, bf16, Co = 64): pre = the s2h_convt2_store
+ * values, y / mean / rstd = LayerNorm2d(pre) over the channels (gamma, beta, eps; the values of
+ * s2h_layernorm_fwd), post = gelu(y) (as s2h_act_fwd rounds it); mean / rstd [B * 2H * 2W] fp32. */
+int s2h_convt2_ln_gelu(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
+                       int add_bcast, const float* gamma, const float* beta, float eps, void* pre, void* y,
+                       float* mean, float* rstd, void* post, hipStream_t st);
 /* y[r, :] = gate[r] > 0 ? x[r, :] : fill; dir 1 = backward (object-score gating to
  * NO_OBJ_SCORE, sam2_base.py:380-389). */
 int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, float fill,

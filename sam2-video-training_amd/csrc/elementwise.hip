@@ -1164,10 +1164,54 @@ __global__ void convt2_kernel(int B, int H, int W, int Co, const void* Y, const 
     }
   }
 }
+// gather (dir 1), vectorised: one thread per (pixel, 16-B channel group) reads the 2 x 2 output
+// pixels' V channels (4 16-B loads) and writes the group's 4 x V contiguous dY entries (co*4 + s:
+// 4 16-B stores); the scalar form wrote 2-B elements at stride 4 (98 us per frame-batched launch)
+template <typename T>
+__global__ __launch_bounds__(256) void convt2_gather_vec_kernel(int B, int H, int W, int Co, const T* dout, T* dY) {
+  constexpr int V = 16 / sizeof(T);
+  const int CG = Co / V;
+  const int64_t n = (int64_t)B * H * W * CG;
+  GRID_STRIDE(i, n) {
+    const int cg = (int)(i % CG);
+    const int64_t p = i / CG;
+    const int x = (int)(p % W);
+    const int64_t t = p / W;
+    const int y = (int)(t % H);
+    const int b = (int)(t / H);
+    T g[4][V];
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      const int dy = sidx >> 1, dx = sidx & 1;
+      const int64_t o = (((int64_t)b * 2 * H + 2 * y + dy) * 2 * W + 2 * x + dx) * Co + cg * V;
+      *(uint4*)g[sidx] = *(const uint4*)(dout + o);
+    }
+    T e[4 * V];
+#pragma unroll
+    for (int j = 0; j < V; ++j)
+#pragma unroll
+      for (int sidx = 0; sidx < 4; ++sidx) e[4 * j + sidx] = g[sidx][j];
+    uint4* yr = (uint4*)(dY + p * 4 * Co + (int64_t)cg * V * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) yr[u] = *(const uint4*)(e + u * V);
+  }
+}
+
 extern "C" int s2h_convt2(int dt, int B, int H, int W, int Co, const void* Y, const float* bias, const void* add,
                           void* out, int dir, hipStream_t st) {
   const int64_t n = (int64_t)B * 4 * H * W * Co;
   if (n <= 0) return 0;
+  const int V = dt == S2H_BF16 ? 8 : 4;
+  if (dir == 1 && Co % V == 0 && al16(Y) && al16(out)) {
+    const int64_t nv = n / 4 / V;
+    if (dt == S2H_BF16)
+      hipLaunchKernelGGL(convt2_gather_vec_kernel<bf16>, ew_grid(nv), dim3(256), 0, st, B, H, W, Co, (const bf16*)Y,
+                         (bf16*)out);
+    else
+      hipLaunchKernelGGL(convt2_gather_vec_kernel<float>, ew_grid(nv), dim3(256), 0, st, B, H, W, Co,
+                         (const float*)Y, (float*)out);
+    return (int)hipGetLastError();
+  }
   DISPATCH_T(dt, convt2_kernel, ew_grid(n), B, H, W, Co, Y, bias, add, out, dir);
   return (int)hipGetLastError();
 }
@@ -1306,6 +1350,102 @@ extern "C" int s2h_convt2_tail(int dt, int B, int H, int W, int Co, const void* 
   if (n <= 0) return 0;
   hipLaunchKernelGGL((convt2_tail_kernel<bf16, 4>), ew_grid(n), dim3(256), 0, st, B, H, W, (const bf16*)Y, bias,
                      (const bf16*)add, add_bcast, (const bf16*)hyper, (bf16*)pre, (bf16*)post, (bf16*)masks);
+  return (int)hipGetLastError();
+}
+
+// The mask decoder's first upscaling step in one pass (round 5; mask_decoder.py:105-106:
+// u = gelu(LayerNorm2d(dc1(x) + feat_s1))): pre = the convt2_store values, y = LayerNorm over the Co
+// channels of each output pixel with the arithmetic of norm.hip ln_fwd_vec_kernel<bf16, CG, 1> (the CG
+// lanes of a pixel each sum their 8 channels in order, then xor 4, 2, 1; two-pass variance) -- so y,
+// mean and rstd are bit-identical to that kernel's -- and post = gelu(y) as act_fwd rounds it.  pre,
+// mean / rstd and y / post are what the LayerNorm's, the GELU's and dc2's backward read.
+template <typename T, int CG>
+__global__ __launch_bounds__(256) void convt2_ln_gelu_kernel(int B, int H, int W, const T* Y, const float* bias,
+                                                             const T* add, int add_bcast, const float* gamma,
+                                                             const float* beta, float eps, T* pre, T* y, float* mean,
+                                                             float* rstd, T* post) {
+  constexpr int V = 16 / sizeof(T);
+  constexpr int Co = CG * V;
+  const int64_t n = (int64_t)B * H * W * CG;
+  GRID_STRIDE(i, n) {  // (n is a multiple of CG: a pixel's CG lanes stay together)
+    const int cg = (int)(i % CG);
+    const int64_t p = i / CG;  // (b * H + y) * W + x
+    const int x = (int)(p % W);
+    const int64_t t = p / W;
+    const int yy = (int)(t % H);
+    const int b = (int)(t / H);
+    T e[4 * V];
+    const uint4* yr = (const uint4*)(Y + p * 4 * Co + (int64_t)cg * V * 4);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) *(uint4*)(e + u * V) = yr[u];
+    float bv[V], gv[V], be[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      bv[j] = bias ? bias[cg * V + j] : 0.f;
+      gv[j] = gamma[cg * V + j];
+      be[j] = beta[cg * V + j];
+    }
+#pragma unroll
+    for (int sidx = 0; sidx < 4; ++sidx) {
+      const int dy = sidx >> 1, dx = sidx & 1;
+      const int64_t pix = ((int64_t)(2 * yy + dy) * 2 * W + 2 * x + dx);  // within batch b
+      const int64_t row = (int64_t)b * 4 * H * W + pix;
+      const int64_t o = row * Co + cg * V;
+      float v[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) v[j] = to_f32(from_f32<T>(to_f32(e[4 * j + sidx]) + bv[j]));
+      if (add) {
+        T ad[V];
+        *(uint4*)ad = *(const uint4*)(add + (add_bcast ? pix * Co + cg * V : o));
+#pragma unroll
+        for (int j = 0; j < V; ++j) v[j] += to_f32(ad[j]);
+      }
+      T r[V];
+      float s = 0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        r[j] = from_f32<T>(v[j]);
+        v[j] = to_f32(r[j]);
+        s += v[j];
+      }
+      *(uint4*)(pre + o) = *(const uint4*)r;
+#pragma unroll
+      for (int m = CG / 2; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+      const float mu = s / Co;
+      float q = 0.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const float d = v[j] - mu;
+        q += d * d;
+      }
+#pragma unroll
+      for (int m = CG / 2; m > 0; m >>= 1) q += __shfl_xor(q, m, 64);
+      const float rs = 1.f / sqrtf(q / Co + eps);
+      T yo[V], g[V];
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        yo[j] = from_f32<T>((v[j] - mu) * rs * gv[j] + be[j]);
+        g[j] = from_f32<T>(gelu_erf(to_f32(yo[j])) + 0.f);  // (+ 0: act_fwd's `* 1 + 0`)
+      }
+      *(uint4*)(y + o) = *(const uint4*)yo;
+      *(uint4*)(post + o) = *(const uint4*)g;
+      if (cg == 0) {
+        mean[row] = mu;
+        rstd[row] = rs;
+      }
+    }
+  }
+}
+extern "C" int s2h_convt2_ln_gelu(int dt, int B, int H, int W, int Co, const void* Y, const float* bias,
+                                  const void* add, int add_bcast, const float* gamma, const float* beta, float eps,
+                                  void* pre, void* y, float* mean, float* rstd, void* post, hipStream_t st) {
+  if (dt != S2H_BF16 || Co != 64 || !al16(Y) || !al16(pre) || !al16(y) || !al16(post) || (add && !al16(add)) ||
+      !gamma || !beta)
+    return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * H * W * 8;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL((convt2_ln_gelu_kernel<bf16, 8>), ew_grid(n), dim3(256), 0, st, B, H, W, (const bf16*)Y, bias,
+                     (const bf16*)add, add_bcast, gamma, beta, eps, (bf16*)pre, (bf16*)y, mean, rstd, (bf16*)post);
   return (int)hipGetLastError();
 }
 

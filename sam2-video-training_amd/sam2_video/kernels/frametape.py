@@ -1273,6 +1273,32 @@ def convt_tail(tape: FrameTape, x, mod, add, hyper):
     return masks
 
 
+def convt_ln_gelu_ok(x, mod, add, ln):
+    return (ops.convt2_tail_enabled() and x.dtype == torch.bfloat16 and mod.out_ch == 64
+            and ln.weight.shape[0] == 64 and (add is None or add.shape[1:] == (2 * x.shape[1], 2 * x.shape[2], 64)))
+
+
+def convt_ln_gelu(tape: FrameTape, x, mod, add, ln):
+    """gelu(ln(conv_transpose2x2(x, mod, add))) (mask_decoder.py:105-106) as one GEMM + one launch
+    (s2h_convt2_ln_gelu), recorded as the same three tape ops (convt, ln, act) with their saved values"""
+    x = x if x.is_contiguous() else x.contiguous()
+    add = None if add is None else add.contiguous()
+    B, H, W, Ci = x.shape
+    Co = mod.out_ch
+    pre = conv_transpose2x2(tape, x, mod, add=add, _compute=False)
+    y, mean, rstd = layer_norm(tape, pre, ln, ln.eps, _compute=False)
+    post = act(tape, y, "gelu", _compute=False)
+    Y = torch.empty(B * H * W, 4 * Co, device=x.device, dtype=x.dtype)  # scratch
+    ops.gemm(x.reshape(-1, Ci), mod.compute_weight(), Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1,
+             ldb_k=4 * Co, ldb_n=1, ldc=4 * Co)
+    bc = int(add is not None and add.shape[0] == 1 and B > 1)
+    from ._lib import call
+    call("s2h_convt2_ln_gelu", ops.dt(x), B, H, W, Co, ops.ptr(Y), ops.ptr(mod.bias.detach()), ops.ptr(add), bc,
+         ops.ptr(ln.weight.detach()), ops.ptr(ln.bias.detach()), float(ln.eps), ops.ptr(pre), ops.ptr(y),
+         ops.ptr(mean), ops.ptr(rstd), ops.ptr(post), ops.stream())
+    return post
+
+
 def point_embed(tape: FrameTape, pe, labels, dtype, tables):
     """PromptEncoder point embeddings (per-frame constant clicks + learned label embeddings)"""
     op, first = tape._begin("point_embed", [], _point_embed_bw, {"tables": tables})

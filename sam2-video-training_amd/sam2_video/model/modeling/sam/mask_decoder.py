@@ -102,8 +102,13 @@ class MaskDecoder(nn.Module):
         mask_token0 = FN.select_token(hs, 2)
         feat_s0, feat_s1 = high_res_features
         dc1, ln1, _, dc2, _ = self.output_upscaling
-        u = conv_transpose2x2(src.view(O, h, w, C), dc1, add=feat_s1)
-        u = FN.act(ln1(u), "gelu")
+        u = src.view(O, h, w, C)
+        if T is not None and _ft.convt_ln_gelu_ok(u, dc1, feat_s1, ln1):
+            # dc1 + feat_s1, LayerNorm2d and GELU in one launch after the GEMM (frametape.convt_ln_gelu)
+            u = _ft.convt_ln_gelu(T, u, dc1, feat_s1, ln1)
+        else:
+            u = conv_transpose2x2(u, dc1, add=feat_s1)
+            u = FN.act(ln1(u), "gelu")
         # the hypernetwork MLP of mask token 0 and the IoU head: one launch (FN.mlp_heads)
         hyper0, iou_pred = FN.mlp_heads([(self.output_hypernetworks_mlps[0], mask_token0),
                                          (self.iou_prediction_head, iou_token_out)])

@@ -102,3 +102,54 @@ def test_mask_decoder_tail_fused_matches_unfused_bf16(monkeypatch):
               "sam_mask_decoder.output_hypernetworks_mlps.0.layers.2.weight"):
         cos = torch.nn.functional.cosine_similarity(g0[n].flatten().double(), g1[n].flatten().double(), dim=0).item()
         assert cos >= 0.99, (n, cos)
+
+
+def test_convt2_ln_gelu_matches_three_launches():
+    """dc1 + feat_s1, LayerNorm2d and GELU in one launch (s2h_convt2_ln_gelu, mask_decoder.py:105-106)
+    against convt2_store + layernorm_fwd + act_fwd: every stored value bit-identical"""
+    from sam2_video.kernels import ops
+    from sam2_video.model.modeling.layers import LayerNorm2d
+    torch.manual_seed(4)
+    B, H, W, Ci, Co = 13, 32, 32, 256, 64
+    bf = torch.bfloat16
+    w = (torch.randn(Ci, 4 * Co, device=DEV) / 16).to(bf)
+    bias = torch.randn(Co, device=DEV) * 0.1
+    x = torch.randn(B, H, W, Ci, device=DEV).to(bf)
+    add = torch.randn(1, 2 * H, 2 * W, Co, device=DEV).to(bf)
+    ln = LayerNorm2d(Co).to(DEV)
+    ln.weight.data = torch.randn(Co, device=DEV)
+    ln.bias.data = torch.randn(Co, device=DEV)
+    Y = torch.empty(B * H * W, 4 * Co, device=DEV, dtype=bf)
+    ops.gemm(x.reshape(-1, Ci), w, Y, M=B * H * W, N=4 * Co, K=Ci, lda_m=Ci, lda_k=1, ldb_k=4 * Co, ldb_n=1,
+             ldc=4 * Co)
+    rows = B * 4 * H * W
+    pre = torch.empty(B, 2 * H, 2 * W, Co, device=DEV, dtype=bf)
+    y, post = torch.empty_like(pre), torch.empty_like(pre)
+    mean, rstd = torch.empty(rows, device=DEV), torch.empty(rows, device=DEV)
+    from sam2_video.kernels._lib import call
+    call("s2h_convt2_ln_gelu", 1, B, H, W, Co, Y.data_ptr(), bias.data_ptr(), add.data_ptr(), 1,
+         ln.weight.data_ptr(), ln.bias.data_ptr(), float(ln.eps), pre.data_ptr(), y.data_ptr(), mean.data_ptr(),
+         rstd.data_ptr(), post.data_ptr(), ops.stream())
+    ref_pre = ops.convt2_store(Y, B, H, W, Co, bias=bias, add=add)
+    ref_y, ref_mean, ref_rstd = ops.layernorm_fwd(ref_pre, ln.weight.data, ln.bias.data, ln.eps)
+    ref_post = ops.act_fwd(ref_y, "gelu")
+    torch.cuda.synchronize()
+    assert torch.equal(pre, ref_pre)
+    assert torch.equal(mean, ref_mean.view(-1)) and torch.equal(rstd, ref_rstd.view(-1))
+    assert torch.equal(y, ref_y)
+    assert torch.equal(post, ref_post)
+
+
+@pytest.mark.parametrize("dtype,Co", [(torch.bfloat16, 32), (torch.bfloat16, 64), (torch.float32, 16)])
+def test_convt2_gather_vectorised(dtype, Co):
+    """the backward's gather (vectorised, s2h_convt2 dir 1) is the exact inverse of the scatter and
+    matches an index-built reference"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(5)
+    B, H, W = 13, 16, 24
+    dout = torch.randn(B, 2 * H, 2 * W, Co, device=DEV).to(dtype)
+    dY = ops.convt2_gather(dout, B, H, W, Co)
+    ref = dout.view(B, H, 2, W, 2, Co).permute(0, 1, 3, 5, 2, 4).reshape(B * H * W, 4 * Co)
+    torch.cuda.synchronize()
+    assert torch.equal(dY, ref)
+    assert torch.equal(ops.convt2_scatter(dY, B, H, W, Co), dout)
