@@ -805,14 +805,23 @@ __global__ void bilinear_bwd_kernel(int N, int hi, int wi, int ho, int wo, const
     const int64_t r = i / wi;
     const int iy = r % hi;
     const int p = r / hi;
-    const int cy = (int)((iy + 0.5f) / sh), cx = (int)((ix + 0.5f) / sw);
+    // the outputs whose taps can reach (iy, ix): source coordinate s = scale (o + 0.5) - 0.5 within
+    // (i - 1, i + 1), widened by one output on each side (the weight tests below are exact, so the
+    // contributing outputs and their order are those of the wider cy +- (ry + 1) search: 10 x 10
+    // candidates instead of 15 x 15 at a 4x upsampling)
+    const int oy0 = max(0, (int)floorf((iy - 0.5f) / sh - 0.5f) - 1);
+    const int oy1 = min(ho - 1, (int)ceilf((iy + 1.5f) / sh - 0.5f) + 1);
+    const int ox0 = max(0, (int)floorf((ix - 0.5f) / sw - 0.5f) - 1);
+    const int ox1 = min(wo - 1, (int)ceilf((ix + 1.5f) / sw - 0.5f) + 1);
+    (void)ry;
+    (void)rx;
     float acc = 0.f;
-    for (int oy = max(0, cy - ry - 1); oy <= min(ho - 1, cy + ry + 1); ++oy) {
+    for (int oy = oy0; oy <= oy1; ++oy) {
       int y0, y1; float ly;
       bil_src(oy, sh, hi, y0, y1, ly);
       float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
       if (wy == 0.f) continue;
-      for (int ox = max(0, cx - rx - 1); ox <= min(wo - 1, cx + rx + 1); ++ox) {
+      for (int ox = ox0; ox <= ox1; ++ox) {
         int x0, x1; float lx;
         bil_src(ox, sw, wi, x0, x1, lx);
         float wx = (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f);
@@ -1523,16 +1532,36 @@ extern "C" int s2h_pos_embed(int dt, int C, int h, int w, int ws, const float* Y
 }
 // dwin[c, a, b] += sum over (i % ws == a, j % ws == b) dout[i, j, c]: one thread per window element,
 // the positions in row-major order (deterministic; the scatter form added with float atomics)
+// (16 slices per window element: slice sl takes the copies k = sl, sl + 16, ... in row-major order,
+// the slice sums added in a fixed LDS tree -- one serial chain of (h / ws) * (w / ws) loads per element
+// and only C * ws^2 threads took 68 us for Hiera-B+ at 512^2)
 template <typename T>
-__global__ void pos_win_bwd_kernel(int C, int h, int w, int ws, const void* dout, float* dwin) {
+__global__ __launch_bounds__(256) void pos_win_bwd_kernel(int C, int h, int w, int ws, const void* dout, float* dwin) {
+  constexpr int SL = 16;
   const int n = C * ws * ws;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= n) return;
-  const int c = e % C, ab = e / C, a = ab / ws, b = ab % ws;
+  const int e = blockIdx.x * 16 + (threadIdx.x & 15);
+  const int sl = threadIdx.x >> 4;
+  __shared__ float red[SL][16];
   float s = 0.f;
-  for (int y = a; y < h; y += ws)
-    for (int x = b; x < w; x += ws) s += to_f32(((const T*)dout)[((int64_t)y * w + x) * C + c]);
-  dwin[(c * ws + a) * ws + b] += s;
+  if (e < n) {
+    const int c = e % C, ab = e / C, a = ab / ws, b = ab % ws;
+    const int ny = (h - a + ws - 1) / ws, nx = (w - b + ws - 1) / ws;
+    for (int k = sl; k < ny * nx; k += SL) {
+      const int y = a + (k / nx) * ws, x = b + (k % nx) * ws;
+      s += to_f32(((const T*)dout)[((int64_t)y * w + x) * C + c]);
+    }
+  }
+  red[sl][threadIdx.x & 15] = s;
+  __syncthreads();
+#pragma unroll
+  for (int hh = SL / 2; hh >= 1; hh >>= 1) {
+    if (sl < hh) red[sl][threadIdx.x & 15] += red[sl + hh][threadIdx.x & 15];
+    __syncthreads();
+  }
+  if (sl == 0 && e < n) {
+    const int c = e % C, ab = e / C, a = ab / ws, b = ab % ws;
+    dwin[(c * ws + a) * ws + b] += red[0][threadIdx.x & 15];
+  }
 }
 extern "C" int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void* dout, float* dY, float* dwin,
                                  hipStream_t st) {
@@ -1540,7 +1569,7 @@ extern "C" int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void
   if (n <= 0) return 0;
   if (dY) DISPATCH_T(dt, pos_embed_bwd_kernel, ew_grid(n), C, h, w, ws, dout, dY, (float*)nullptr);
   if (dwin) {
-    const dim3 g((C * ws * ws + 255) / 256);
+    const dim3 g((C * ws * ws + 15) / 16);
     if (dt == S2H_BF16) hipLaunchKernelGGL(pos_win_bwd_kernel<bf16>, g, dim3(256), 0, st, C, h, w, ws, dout, dwin);
     else hipLaunchKernelGGL(pos_win_bwd_kernel<float>, g, dim3(256), 0, st, C, h, w, ws, dout, dwin);
   }
@@ -1560,11 +1589,26 @@ __global__ void point_embed_kernel(int R, int D, const float* pe, const int* lab
     ((T*)out)[i] = from_f32<T>(v);
   }
 }
+// one thread per column; the 5 label rows' sums in registers in row order (the same additions, in the
+// same order, as adding into dtable row by row -- which made every row wait for the previous row's
+// store: 53 us for the step's ~200 click rows)
 template <typename T>
 __global__ void point_embed_bwd_kernel(int R, int D, const int* labels, const void* dout, float* dtable) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= D) return;
-  for (int r = 0; r < R; ++r) dtable[(labels[r] + 1) * D + d] += to_f32(((const T*)dout)[(int64_t)r * D + d]);
+  float acc[5];
+#pragma unroll
+  for (int k = 0; k < 5; ++k) acc[k] = dtable[k * D + d];
+#pragma unroll 8
+  for (int r = 0; r < R; ++r) {
+    const int l = labels[r] + 1;
+    const float v = to_f32(((const T*)dout)[(int64_t)r * D + d]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+      if (l == k) acc[k] += v;
+  }
+#pragma unroll
+  for (int k = 0; k < 5; ++k) dtable[k * D + d] = acc[k];
 }
 extern "C" int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
                                hipStream_t st) {
@@ -1723,27 +1767,37 @@ __global__ __launch_bounds__(256) void colsum_seg_kernel(int64_t rows, int cols,
 }
 // out[d][c] += the partials of every segment s with dst[s] == d (segments in order, then blocks in
 // order): one thread per (destination row, column), deterministic
-__global__ __launch_bounds__(256) void colsum_seg_finalize_kernel(int nseg, int nbx, int ndst, int cols, SegTable tb,
-                                                                  const float* part, float* out) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= ndst * cols) return;
-  const int d = e / cols, c = e % cols;
-  float acc = 0.f;
+// one workgroup per (destination row, 64 columns), 1024 threads = 64 columns x 16 slices: the
+// destination's partial rows (its segments in order, nbx blocks each) are dealt to the slices
+// round-robin, the slice sums added in a fixed LDS tree (one thread per column walking every
+// segment's blocks took 56 us)
+__global__ __launch_bounds__(1024) void colsum_seg_finalize_kernel(int nseg, int nbx, int ndst, int cols, SegTable tb,
+                                                                   const float* part, float* out) {
+  const int d = blockIdx.y;
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int sl = threadIdx.x >> 6;
+  __shared__ float red[16][64];
+  float s = 0.f;
   bool any = false;
+  int q = 0;  // index of this destination's partial rows
   for (int sg = 0; sg < nseg; ++sg) {
     if (tb.dst[sg] != d) continue;
     any = true;
-    const float* p = part + (int64_t)sg * nbx * cols + c;
-    float s0 = 0.f, s1 = 0.f;
-    int b = 0;
-    for (; b + 2 <= nbx; b += 2) {
-      s0 += p[(int64_t)b * cols];
-      s1 += p[(int64_t)(b + 1) * cols];
+    if (c < cols) {
+      const float* p = part + (int64_t)sg * nbx * cols + c;
+      // rows b of this segment with (q + b) % 16 == sl
+      for (int b = (sl - q % 16 + 16) % 16; b < nbx; b += 16) s += p[(int64_t)b * cols];
     }
-    if (b < nbx) s0 += p[(int64_t)b * cols];
-    acc += s0 + s1;
+    q += nbx;
   }
-  if (any) out[(int64_t)d * cols + c] += acc;
+  red[sl][threadIdx.x & 63] = s;
+  __syncthreads();
+#pragma unroll
+  for (int hh = 8; hh >= 1; hh >>= 1) {
+    if (sl < hh) red[sl][threadIdx.x & 63] += red[sl + hh][threadIdx.x & 63];
+    __syncthreads();
+  }
+  if (sl == 0 && any && c < cols) out[(int64_t)d * cols + c] += red[0][threadIdx.x & 63];
 }
 extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const void* x, int64_t ld, const int64_t* offs,
                               const int* dsts, float* out, hipStream_t st) {
@@ -1768,7 +1822,7 @@ extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const vo
   if (part) {
     int ndst = 0;
     for (int sg = 0; sg < nseg; ++sg) ndst = std::max(ndst, dsts[sg] + 1);
-    hipLaunchKernelGGL(colsum_seg_finalize_kernel, dim3((ndst * cols + 255) / 256), dim3(256), 0, st, nseg,
+    hipLaunchKernelGGL(colsum_seg_finalize_kernel, dim3((cols + 63) / 64, ndst), dim3(1024), 0, st, nseg,
                        (int)grid.x, ndst, cols, tb, part, out);
   }
   return (int)hipGetLastError();
