@@ -488,6 +488,11 @@ int s2h_memory_pos(int dt, int n, int L, int Dm, const void* pos, const void* tp
 /* out[i] (=/+=) sum_o x[o, i] (gradient of a per-object broadcast of shared
  * features: sam2model.py:307-311, mask_decoder.py:201,209 repeat_interleave). */
 int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* out, int accum, hipStream_t st);
+/* out[f][:] (+)= sum over o < O of x[f][o][:] for F frames in one launch (x [F, O, inner], out [F, inner];
+ * the frame-batched backward of a broadcast over objects, tracking.py / mask_decoder.py); each element
+ * summed in o order (the values of F s2h_sum_outer launches). */
+int s2h_sum_outer_batched(int dt, int F, int O, int64_t inner, const void* x, void* out, int accum,
+                          hipStream_t st);
 /* NHWC im2col in PyTorch weight order (c, ky, kx) for the strided convolutions
  * (PatchEmbed utils.py:85; MaskDownSampler memory_encoder.py:43): rows of ldcol >= C*kh*kw elements,
  * the columns past C*kh*kw written as zeros. */

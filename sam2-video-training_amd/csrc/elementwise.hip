@@ -950,6 +950,58 @@ extern "C" int s2h_sum_outer(int dt, int O, int64_t inner, const void* x, void* 
   DISPATCH_T(dt, sum_outer_kernel, ew_grid(inner), O, inner, x, out, accum);
   return (int)hipGetLastError();
 }
+// out[f][j] = sum_{o<O} x[f][o][j] for F frames in one launch (the frame-batched backward of a broadcast
+// over objects), 16 B per thread; each element's sum in o order, as sum_outer_kernel adds it
+template <typename T>
+__global__ __launch_bounds__(256) void sum_outer_vec_kernel(int F, int O, int64_t inner, const T* x, T* out, int accum) {
+  constexpr int V = 16 / sizeof(T);
+  const int64_t nv = inner / V;
+  GRID_STRIDE(i, (int64_t)F * nv) {
+    const int64_t f = i / nv, jv = i - f * nv;
+    const T* xp = x + f * O * inner + jv * V;
+    float acc[V];
+#pragma unroll
+    for (int j = 0; j < V; ++j) acc[j] = 0.f;
+    for (int o = 0; o < O; ++o) {
+      T t[V];
+      *(uint4*)t = *(const uint4*)(xp + (int64_t)o * inner);
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += to_f32(t[j]);
+    }
+    T* op = out + f * inner + jv * V;
+    T r[V];
+    if (accum) {
+      T prev[V];
+      *(uint4*)prev = *(const uint4*)op;
+#pragma unroll
+      for (int j = 0; j < V; ++j) acc[j] += to_f32(prev[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) r[j] = from_f32<T>(acc[j]);
+    *(uint4*)op = *(const uint4*)r;
+  }
+}
+extern "C" int s2h_sum_outer_batched(int dt, int F, int O, int64_t inner, const void* x, void* out, int accum,
+                                     hipStream_t st) {
+  if (inner <= 0 || F <= 0) return 0;
+  const int V = dt == S2H_BF16 ? 8 : 4;
+  if (inner % V == 0 && al16(x) && al16(out)) {
+    const int64_t n = (int64_t)F * (inner / V);
+    if (dt == S2H_BF16)
+      hipLaunchKernelGGL(sum_outer_vec_kernel<bf16>, ew_grid(n), dim3(256), 0, st, F, O, inner, (const bf16*)x,
+                         (bf16*)out, accum);
+    else
+      hipLaunchKernelGGL(sum_outer_vec_kernel<float>, ew_grid(n), dim3(256), 0, st, F, O, inner, (const float*)x,
+                         (float*)out, accum);
+    return (int)hipGetLastError();
+  }
+  for (int f = 0; f < F; ++f) {
+    const int64_t esz = dt == S2H_BF16 ? 2 : 4;
+    DISPATCH_T(dt, sum_outer_kernel, ew_grid(inner), O, inner, (const char*)x + f * O * inner * esz,
+               (char*)out + f * inner * esz, accum);
+  }
+  return (int)hipGetLastError();
+}
 
 // ------------------------------------------------------------ NHWC im2col
 // col[(b*Ho+oy)*Wo+ox][c*kh*kw + ky*kw + kx] = x[b][oy*s-p+ky][ox*s-p+kx][c]  (PyTorch weight order);

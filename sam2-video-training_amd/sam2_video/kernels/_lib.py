@@ -104,6 +104,7 @@ SIGNATURES = {
     "s2h_colsum_seg": [I, I, L, I, P, L, P, P, P, P],
     "s2h_memory_pos": [I, I, I, I, P, P, P, P, P],
     "s2h_sum_outer": [I, I, L, P, P, I, P],
+    "s2h_sum_outer_batched": [I, I, I, L, P, P, I, P],
     "s2h_im2col": [I, I, I, I, I, I, I, I, I, I, I, L, P, P, P],
     "s2h_mask_down_stage": [I, I, I, I, I, I, P, I, F, F, P, P, P, P, F, P, P],
     "s2h_dwconv": [I, I, I, I, I, I, I, P, P, P, P, P],

@@ -1086,9 +1086,7 @@ def _expand_bw(tape, op, gys):
     O = op.attrs["O"]
     inner = tape.st(op.ins[0]).numels[0]
     d = torch.empty(tape.F * inner, device=g.device, dtype=g.dtype)
-    g3 = g.view(tape.F, O, inner)
-    for f in range(tape.F):
-        ops.sum_outer(g3[f], d[f * inner:(f + 1) * inner])
+    ops.sum_outer_batched(g.contiguous().view(tape.F, O, inner), d)  # every frame in one launch
     return [d]
 
 
@@ -1208,9 +1206,7 @@ def _convt_bw(tape, op, gys):
         if a["bcast"]:
             inner = 4 * H * W * Co
             dadd = torch.empty(F * inner, device=g.device, dtype=g.dtype)
-            g3 = g.view(F, B, inner)
-            for f in range(F):
-                ops.sum_outer(g3[f], dadd[f * inner:(f + 1) * inner])
+            ops.sum_outer_batched(g.view(F, B, inner), dadd)  # every frame in one launch
         else:
             dadd = g.view(-1)
     return [dx, dadd]

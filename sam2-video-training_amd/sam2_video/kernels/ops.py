@@ -993,6 +993,14 @@ def sum_outer(x, out, accumulate=False):
     return out
 
 
+def sum_outer_batched(x3, out, accumulate=False):
+    """out[f] (+)= x3[f].sum(0) for x3 [F, O, inner] (one launch; the values of F sum_outer calls)"""
+    F, O, inner = x3.shape
+    assert x3.is_contiguous() and out.is_contiguous() and out.numel() == F * inner and out.dtype == x3.dtype
+    call("s2h_sum_outer_batched", dt(x3), F, O, inner, ptr(x3), ptr(out), int(accumulate), stream())
+    return out
+
+
 def im2col(x, kh, kw, stride, pad, pad8=False):
     """[B*Ho*Wo, C*kh*kw] patches; pad8: a view of rows padded to a multiple of 8 elements (zeros), so
     the GEMMs reading it (the patch embedding's 147 columns) get 16-B aligned rows"""

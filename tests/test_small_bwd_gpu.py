@@ -54,3 +54,21 @@ def test_point_embed_grad(dtype):
         ref[int(labels[r]) + 1] += dout[r].float()
     torch.cuda.synchronize()
     assert torch.equal(dtable, ref)
+
+
+@pytest.mark.parametrize("dtype,F,O,inner", [(torch.bfloat16, 7, 13, 262144), (torch.float32, 3, 5, 1000),
+                                             (torch.bfloat16, 2, 3, 50)])
+def test_sum_outer_batched_equals_per_frame(dtype, F, O, inner):
+    """the frame-batched broadcast-gradient sum (one launch) gives the bits of one sum_outer per frame"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(3)
+    x = torch.randn(F, O, inner, device=DEV).to(dtype)
+    out = torch.empty(F * inner, device=DEV, dtype=dtype)
+    ops.sum_outer_batched(x, out)
+    ref = torch.empty_like(out)
+    for f in range(F):
+        ops.sum_outer(x[f], ref[f * inner:(f + 1) * inner])
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    t = x.double().sum(1).flatten()
+    assert (out.double() - t).abs().max().item() <= (1e-2 if dtype == torch.bfloat16 else 1e-5) * t.abs().max().item()
