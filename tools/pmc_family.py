@@ -22,7 +22,11 @@ FAMILIES = {"gemm": ("GEMM", r"gemm"), "attn_bwd": ("attention backward", r"flas
 def main(tag, steps, bench_log, prefix):
     steps = int(steps)
     line = [ln for ln in open(bench_log) if ln.startswith("{")][-1]
-    fams = json.loads(line)["roofline"]["families"]
+    rl = json.loads(line)["roofline"]
+    fams = rl["families"]
+    # host-level launches (one ABI call = one launch: the unit of the bench line's alg_bytes_per_launch);
+    # the trace-based families count kernels, the event-based ones count launches
+    ev = rl.get("event_based", {}).get("families", {})
     per = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(f"gpurun_out/{tag}_pmc*/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
@@ -47,7 +51,7 @@ def main(tag, steps, bench_log, prefix):
             continue
         rows.sort(key=lambda r: -r.get("hbm_bytes_per_dispatch", 0) * r["dispatches_per_step"])
         step_bytes = (2 * fetch + write) * 1024 / steps
-        launches = fams.get(name, {}).get("launches_per_step", 0)
+        launches = ev.get(name, {}).get("launches_per_step") or fams.get(name, {}).get("launches_per_step", 0)
         doc = {"family": name, "tag": tag, "steps": steps, "launches_per_step": launches,
                "hbm_bytes_per_step": step_bytes, "bytes_per_launch": step_bytes / max(launches, 1),
                "correction": "hbm_bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (gfx950 FETCH_SIZE = half the bytes of "
