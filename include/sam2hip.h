@@ -254,6 +254,20 @@ int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_l
                          int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh, int64_t sdvl, const float* lse,
                          float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
                          const int64_t* fr_koff, hipStream_t st);
+/* s2h_flash_bwd_frames with the q projection's RoPE epilogue transposed into the dQ store
+ * (position_encoding.py:212-239 apply_rotary_enc, transposed; head dim 256; replaces the separate
+ * rotation pass over dq of the memory self-attention, transformer.py:296-307): query rows
+ * < fr_nrotq[f] of every batch block of frame f are rotated back with table row (row % rope_period)
+ * of cos / sin [period, 128] fp32 (fr_nrotq NULL: unrotated); dk is stored unrotated. */
+int s2h_flash_bwd_frames_rope(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk, const int64_t* fr_krow,
+                              const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
+                              const void* k, int64_t skh, int64_t skl, const void* v, int64_t svh, int64_t svl,
+                              const void* o, int64_t sob, int64_t soh, int64_t sol, const void* dout, int64_t sgb,
+                              int64_t sgh, int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk,
+                              int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh, int64_t sdvl, const float* lse,
+                              float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
+                              const int64_t* fr_koff, const float* rope_cos, const float* rope_sin, int rope_period,
+                              const int* fr_nrotq, hipStream_t st);
 
 /* V-fold of the memory-attention cross-attention (RoPEAttention, transformer.py:275-311, with
  * kv_in_dim 64: memory_attention.py:66-81, sam2.1_hiera_t.yaml:49-58).  Its values are a projection
@@ -290,6 +304,16 @@ int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const int* fr_lk, 
                                     void* dk, int64_t sdkl, const float* lse, float* di_ws, float scale, float p_drop,
                                     uint64_t seed, const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
                                     const float* rope_sin, int rope_period, const int* fr_nrot, hipStream_t st);
+/* + the query projection's inverse RoPE in the dQ store (query rows < fr_nrotq[f], same tables;
+ * transformer.py:296 q rotation transposed).  fr_nrot / fr_nrotq each NULL: that gradient unrotated. */
+int s2h_flash_bwd_frames_vfold_rope_qk(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
+                                       const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql, const void* k,
+                                       int64_t skl, const void* mem, int64_t sml, const void* u, int64_t sub,
+                                       int64_t sul, const void* du, int64_t sgb, int64_t sgl, void* dq, int64_t sdqb,
+                                       int64_t sdql, void* dk, int64_t sdkl, const float* lse, float* di_ws,
+                                       float scale, float p_drop, uint64_t seed, const uint32_t* keep,
+                                       const int64_t* fr_koff, const float* rope_cos, const float* rope_sin,
+                                       int rope_period, const int* fr_nrot, const int* fr_nrotq, hipStream_t st);
 /* [Wv | bv | 0] as a bf16 [N, ld] matrix (ld >= K + 1) from the bf16 weight [N, K] and the fp32 bias,
  * and its fp32 gradient g [N, ld] scattered back: gwv [N, K] += g[:, :K], gbv [N] += g[:, K]
  * (either nullable).  The value projection's parameters of the folded cross-attention. */

@@ -58,11 +58,14 @@ struct FlashBwdArgs {
   int64_t fr_krow[S2H_MAX_FRAMES];
   uint64_t fr_idx0[S2H_MAX_FRAMES];
   int64_t fr_koff[S2H_MAX_FRAMES];  // word offset of frame f's keep bitmap
-  // optional inverse RoPE of dK (V-fold key gradient, s2h_flash_bwd_frames_vfold_rope): key rows
-  // < fr_nrot[f] of every batch block are rotated back with table row key % rope_period
-  // (the k projection's RoPE epilogue, transposed); rope_cos == nullptr: none
+  // optional inverse RoPE of dQ / dK (s2h_flash_bwd_frames_rope: dQ; s2h_flash_bwd_frames_vfold_rope_qk;
+  // head dim 256, frame-table launches): with rope_k, key rows < fr_nrot[f] of every batch block are
+  // rotated back with table row key % rope_period (the k projection's RoPE epilogue, transposed);
+  // with rope_q, query rows < fr_nrotq[f] the same way (the q projection's).  Tables [period][D / 2].
   const float* rope_cos; const float* rope_sin; int rope_period;
+  int rope_k, rope_q;
   int fr_nrot[S2H_MAX_FRAMES];
+  int fr_nrotq[S2H_MAX_FRAMES];
 };
 
 // The frame table is read straight from the kernarg segment (scalar loads): indexing the by-value
@@ -105,6 +108,33 @@ __device__ __forceinline__ KvFrame kv_frame(const FlashBwdArgs& a, int bh) {
     r.keep = a.keep ? a.keep + (int64_t)bh * a.Lq * a.kw : nullptr;
   }
   return r;
+}
+
+// the RoPE table row of gradient row `row` when it is rotated (row < nrot), else nullptr
+__device__ __forceinline__ const float* rope_row(const FlashBwdArgs& a, int row, int nrot, const float* tab) {
+  if (row >= nrot) return nullptr;
+  return tab + (int64_t)(row % a.rope_period) * (a.D / 2);
+}
+
+// the table entries of the 4 consecutive gradient columns c0..c0+3 (2 rotation pairs, c0 % 4 == 0):
+// one 8-B load per table.  Store loops load every entry they need BEFORE their first store (a load
+// after a global store waits for it: vmcnt counts both).  What remains is one exposed table-load
+// latency per workgroup (these kernels run one workgroup per CU): +13..15 us per launch of the
+// 1664-workgroup dQ kernels, about what the separate rotation launch cost (profiles/r05_v29-v30;
+// an L2 warm-up at kernel start did not change it, holding the entries from kernel start spilled)
+struct RopeCS { float2 c, s; };
+__device__ __forceinline__ RopeCS rope_load(const float* rc, const float* rsn, int c0) {
+  return RopeCS{*(const float2*)(rc + c0 / 2), *(const float2*)(rsn + c0 / 2)};
+}
+// the inverse rotation (the projection epilogue's, transposed) of those 4 columns
+__device__ __forceinline__ void rope_apply(float (&v)[4], const RopeCS& t) {
+  const float cs[2] = {t.c.x, t.c.y}, sns[2] = {t.s.x, t.s.y};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float c = cs[j], sn = sns[j], x0 = v[2 * j], x1 = v[2 * j + 1];
+    v[2 * j] = x0 * c + x1 * sn;
+    v[2 * j + 1] = x1 * c - x0 * sn;
+  }
 }
 
 // dropout handling of the backward kernels (a template parameter: a runtime test per element
@@ -293,12 +323,25 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   if (!qv) return;
   if (a.splits == 1) {
     bf16* DQ = a.dq + b * a.sdqb + h * a.sdqh + (int64_t)q * a.sdql;
+    // inverse RoPE of the query gradient (frame-table launches, rope_q)
+    const int nrq = a.rope_q ? (a.nfr > 0 ? kargs()->fr_nrotq[b / a.bpf] : a.Lq) : 0;
+    const float* rc = rope_row(a, q, nrq, a.rope_cos);
+    const float* rsn = rope_row(a, q, nrq, a.rope_sin);
+    RopeCS tab[C::ND];
+    if (rc != nullptr) {
+#pragma unroll
+      for (int d = 0; d < C::ND; ++d) tab[d] = rope_load(rc, rsn, min(16 * d + 4 * g, a.D - 4));
+    }
 #pragma unroll
     for (int d = 0; d < C::ND; ++d) {
       if (16 * d + 4 * g >= a.D) continue;
+      float v4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v4[e] = acc[d][e] * a.scale;
+      if (rc != nullptr) rope_apply(v4, tab[d]);
       bf16 t4[4];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) t4[e] = (bf16)(acc[d][e] * a.scale);
+      for (int e = 0; e < 4; ++e) t4[e] = (bf16)v4[e];
       *(uint2*)(DQ + 16 * d + 4 * g) = *(const uint2*)t4;
     }
   } else {
@@ -650,15 +693,35 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   }
   bf16* DK = fr.dk + (int64_t)key * a.sdkl;
   bf16* DVp = FOLD ? nullptr : fr.dv + (int64_t)key * a.sdvl;
+  // inverse RoPE of the key gradient (V-fold instance only: rope_k; in the DV = 256 instance the table
+  // entries held over the dV stores spilled, and loads issued between stores serialise on them)
+  const int nrk = FOLD && a.rope_k ? (a.nfr > 0 ? kargs()->fr_nrot[b / a.bpf] : fr.Lk) : 0;
+  const float* rc = rope_row(a, key, nrk, a.rope_cos);
+  const float* rsn = rope_row(a, key, nrk, a.rope_sin);
+  RopeCS tab[FOLD ? ND : 1][4];
+  if constexpr (FOLD) {
+    if (rc != nullptr) {
+#pragma unroll
+      for (int d = 0; d < ND; ++d)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) tab[d][j] = rope_load(rc, rsn, 32 * d + 8 * j + 4 * hi);
+    }
+  }
 #pragma unroll
   for (int d = 0; d < ND; ++d)
 #pragma unroll
     for (int G4 = 0; G4 < 4; ++G4) {
       bf16 tk[4], tv[4];
       const int dvd = FOLD ? 0 : d;
+      float k4[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) k4[e] = dk[d][4 * G4 + e] * a.scale;
+      if constexpr (FOLD) {
+        if (rc != nullptr) rope_apply(k4, tab[d][G4]);
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        tk[e] = (bf16)(dk[d][4 * G4 + e] * a.scale);
+        tk[e] = (bf16)k4[e];
         tv[e] = (bf16)(dv[dvd][4 * G4 + e] * a.inv_keep);
       }
       const int d0 = 32 * d + 8 * G4 + 4 * hi;
@@ -855,31 +918,20 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
   if (!kv) return;
   bf16* DK = fr.dk + (int64_t)key * a.sdkl;
   // inverse RoPE of the key gradient: the lane's 4 consecutive columns are 2 rotation pairs
-  const float* rc = nullptr;
-  const float* rsn = nullptr;
-  if (a.rope_cos != nullptr && key < (a.nfr > 0 ? kargs()->fr_nrot[b / a.bpf] : fr.Lk)) {
-    const int t = key % a.rope_period;
-    rc = a.rope_cos + (int64_t)t * (DP / 2);
-    rsn = a.rope_sin + (int64_t)t * (DP / 2);
+  const int nrk = a.rope_k ? (a.nfr > 0 ? kargs()->fr_nrot[b / a.bpf] : fr.Lk) : 0;
+  const float* rc = rope_row(a, key, nrk, a.rope_cos);
+  const float* rsn = rope_row(a, key, nrk, a.rope_sin);
+  RopeCS tab[DP / 16];
+  if (rc != nullptr) {
+#pragma unroll
+    for (int d = 0; d < DP / 16; ++d) tab[d] = rope_load(rc, rsn, 16 * d + 4 * g);
   }
 #pragma unroll
   for (int d = 0; d < DP / 16; ++d) {
     float v4[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) v4[e] = dk[d][e] * a.scale;
-    if (rc != nullptr) {
-      // pairs 8 d + 2 g and + 1 (columns 16 d + 4 g .. + 3): one 8-B load per table (8-B aligned:
-      // the pair index is even, table rows DP / 2 floats)
-      const float2 c2 = *(const float2*)(rc + 8 * d + 2 * g);
-      const float2 s2 = *(const float2*)(rsn + 8 * d + 2 * g);
-      const float cs[2] = {c2.x, c2.y}, sns[2] = {s2.x, s2.y};
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const float c = cs[j], sn = sns[j], x0 = v4[2 * j], x1 = v4[2 * j + 1];
-        v4[2 * j] = x0 * c + x1 * sn;
-        v4[2 * j + 1] = x1 * c - x0 * sn;
-      }
-    }
+    if (rc != nullptr) rope_apply(v4, tab[d]);
     bf16 t4[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) t4[e] = (bf16)v4[e];
@@ -1062,6 +1114,33 @@ int s2h_flash_bwd_eligible(int dt, int Lq, int D) { return s2h_flash_eligible(dt
 // f's forward keep bitmap from word fr_koff[f] (flash.hip layout: bpf * H * Lq rows of
 // 2 * ceil(fr_lk[f] / 64) words).  nfr * bpf * (Lq / 128)
 // query blocks fill the chip without key or query splits, so no fp32 partials or combines.
+// the frame-table launches' optional inverse RoPE of dQ (fr_nrotq) and / or dK (fr_nrotk), head dim 256
+static int flash_bwd_rope_args(FlashBwdArgs& a, int nfr, int D, const float* cos, const float* sin, int period,
+                               const int* fr_nrotq, const int* fr_nrotk) {
+  if (fr_nrotq == nullptr && fr_nrotk == nullptr) return 0;
+  if (D != 256 || cos == nullptr || sin == nullptr || period <= 0 || ((uintptr_t)cos & 7) || ((uintptr_t)sin & 7))
+    return (int)hipErrorInvalidValue;
+  a.rope_cos = cos; a.rope_sin = sin; a.rope_period = period;
+  a.rope_q = fr_nrotq != nullptr;
+  a.rope_k = fr_nrotk != nullptr;
+  for (int f = 0; f < nfr; ++f) {
+    a.fr_nrotq[f] = fr_nrotq ? fr_nrotq[f] : 0;
+    a.fr_nrot[f] = fr_nrotk ? fr_nrotk[f] : 0;
+  }
+  return 0;
+}
+
+extern "C" int s2h_flash_bwd_frames_rope(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk,
+                                         const int64_t* fr_krow, const uint64_t* fr_idx0, const void* q, int64_t sqb,
+                                         int64_t sqh, int64_t sql, const void* k, int64_t skh, int64_t skl,
+                                         const void* v, int64_t svh, int64_t svl, const void* o, int64_t sob,
+                                         int64_t soh, int64_t sol, const void* dout, int64_t sgb, int64_t sgh,
+                                         int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk,
+                                         int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh, int64_t sdvl,
+                                         const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                                         const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
+                                         const float* rope_sin, int rope_period, const int* fr_nrotq,
+                                         hipStream_t st);
 extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk, const int64_t* fr_krow,
                                     const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                                     const void* k, int64_t skh, int64_t skl, const void* v, int64_t svh, int64_t svl,
@@ -1070,11 +1149,34 @@ extern "C" int s2h_flash_bwd_frames(int nfr, int bpf, int H, int Lq, int D, cons
                                     int64_t sdql, void* dk, int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh,
                                     int64_t sdvl, const float* lse, float* di_ws, float scale, float p_drop,
                                     uint64_t seed, const uint32_t* keep, const int64_t* fr_koff, hipStream_t st) {
+  return s2h_flash_bwd_frames_rope(nfr, bpf, H, Lq, D, fr_lk, fr_krow, fr_idx0, q, sqb, sqh, sql, k, skh, skl, v, svh,
+                                   svl, o, sob, soh, sol, dout, sgb, sgh, sgl, dq, sdqb, sdqh, sdql, dk, sdkh, sdkl, dv,
+                                   sdvh, sdvl, lse, di_ws, scale, p_drop, seed, keep, fr_koff, nullptr, nullptr, 1,
+                                   nullptr, st);
+}
+// s2h_flash_bwd_frames with the q projection's RoPE epilogue transposed into the dQ store (head dim
+// 256): query rows < fr_nrotq[f] of every batch block of frame f come out rotated back with table row
+// (row % rope_period) of rope_cos / rope_sin [period][D / 2] (fr_nrotq == nullptr: unrotated).  The
+// key gradient stays unrotated: the DV = 256 dK kernel's store did not take the rotation without
+// spilling (see flash_bwd_dkv32_kernel)
+extern "C" int s2h_flash_bwd_frames_rope(int nfr, int bpf, int H, int Lq, int D, const int* fr_lk,
+                                         const int64_t* fr_krow, const uint64_t* fr_idx0, const void* q, int64_t sqb,
+                                         int64_t sqh, int64_t sql, const void* k, int64_t skh, int64_t skl,
+                                         const void* v, int64_t svh, int64_t svl, const void* o, int64_t sob,
+                                         int64_t soh, int64_t sol, const void* dout, int64_t sgb, int64_t sgh,
+                                         int64_t sgl, void* dq, int64_t sdqb, int64_t sdqh, int64_t sdql, void* dk,
+                                         int64_t sdkh, int64_t sdkl, void* dv, int64_t sdvh, int64_t sdvl,
+                                         const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed,
+                                         const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
+                                         const float* rope_sin, int rope_period, const int* fr_nrotq,
+                                         hipStream_t st) {
   if (nfr <= 0 || bpf <= 0 || H <= 0 || Lq <= 0) return 0;
   if (nfr > S2H_MAX_FRAMES || !s2h_flash_bwd_eligible(S2H_BF16, Lq, D)) return (int)hipErrorInvalidValue;
   if (keep && (D != 256 || fr_koff == nullptr)) return (int)hipErrorInvalidValue;
   if (!flash_bwd_o_aligned(o, sob, soh, sol)) return (int)hipErrorInvalidValue;
   FlashBwdArgs a = {};
+  if (flash_bwd_rope_args(a, nfr, D, rope_cos, rope_sin, rope_period, fr_nrotq, nullptr) != 0)
+    return (int)hipErrorInvalidValue;
   a.D = D;
   a.nfr = nfr; a.bpf = bpf;
   a.keep = keep;
@@ -1142,6 +1244,13 @@ extern "C" int s2h_flash_bwd_frames_vfold(int nfr, int bpf, int Lq, const int* f
                                          sul, du, sgb, sgl, dq, sdqb, sdql, dk, sdkl, lse, di_ws, scale, p_drop, seed,
                                          keep, fr_koff, nullptr, nullptr, 1, nullptr, st);
 }
+extern "C" int s2h_flash_bwd_frames_vfold_rope_qk(
+    int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow, const uint64_t* fr_idx0, const void* q,
+    int64_t sqb, int64_t sql, const void* k, int64_t skl, const void* mem, int64_t sml, const void* u, int64_t sub,
+    int64_t sul, const void* du, int64_t sgb, int64_t sgl, void* dq, int64_t sdqb, int64_t sdql, void* dk,
+    int64_t sdkl, const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
+    const int64_t* fr_koff, const float* rope_cos, const float* rope_sin, int rope_period, const int* fr_nrot,
+    const int* fr_nrotq, hipStream_t st);
 extern "C" int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow,
                                                const uint64_t* fr_idx0, const void* q, int64_t sqb, int64_t sql,
                                                const void* k, int64_t skl, const void* mem, int64_t sml, const void* u,
@@ -1151,6 +1260,19 @@ extern "C" int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const i
                                                const uint32_t* keep, const int64_t* fr_koff, const float* rope_cos,
                                                const float* rope_sin, int rope_period, const int* fr_nrot,
                                                hipStream_t st) {
+  return s2h_flash_bwd_frames_vfold_rope_qk(nfr, bpf, Lq, fr_lk, fr_krow, fr_idx0, q, sqb, sql, k, skl, mem, sml, u,
+                                            sub, sul, du, sgb, sgl, dq, sdqb, sdql, dk, sdkl, lse, di_ws, scale,
+                                            p_drop, seed, keep, fr_koff, rope_cos, rope_sin, rope_period,
+                                            rope_cos ? fr_nrot : nullptr, nullptr, st);
+}
+// + the q projection's RoPE transposed into the dQ store (query rows < fr_nrotq[f]; nullable)
+extern "C" int s2h_flash_bwd_frames_vfold_rope_qk(
+    int nfr, int bpf, int Lq, const int* fr_lk, const int64_t* fr_krow, const uint64_t* fr_idx0, const void* q,
+    int64_t sqb, int64_t sql, const void* k, int64_t skl, const void* mem, int64_t sml, const void* u, int64_t sub,
+    int64_t sul, const void* du, int64_t sgb, int64_t sgl, void* dq, int64_t sdqb, int64_t sdql, void* dk,
+    int64_t sdkl, const float* lse, float* di_ws, float scale, float p_drop, uint64_t seed, const uint32_t* keep,
+    const int64_t* fr_koff, const float* rope_cos, const float* rope_sin, int rope_period, const int* fr_nrot,
+    const int* fr_nrotq, hipStream_t st) {
   constexpr int D = 256, DV = 64;
   if (nfr <= 0 || bpf <= 0 || Lq <= 0) return 0;
   if (nfr > S2H_MAX_FRAMES || !s2h_flash_bwd_eligible(S2H_BF16, Lq, D)) return (int)hipErrorInvalidValue;
@@ -1192,12 +1314,8 @@ extern "C" int s2h_flash_bwd_frames_vfold_rope(int nfr, int bpf, int Lq, const i
   a.seed_off = s2h_rng_offset_ptr();
   a.splits = 1; a.tiles_per_split = (lk_max + 63) / 64;
   a.kv_splits = 1; a.kv_tiles_per_split = (Lq + 31) / 32;
-  if (rope_cos != nullptr) {  // the dK rotation lives in the two-wave dK kernel's store only
-    if (rope_sin == nullptr || fr_nrot == nullptr || rope_period <= 0 || (s2h_flash_variant() & 1) != 0)
-      return (int)hipErrorInvalidValue;
-    a.rope_cos = rope_cos; a.rope_sin = rope_sin; a.rope_period = rope_period;
-    for (int f = 0; f < nfr; ++f) a.fr_nrot[f] = fr_nrot[f];
-  }
+  if (flash_bwd_rope_args(a, nfr, D, rope_cos, rope_sin, rope_period, fr_nrotq, fr_nrot) != 0)
+    return (int)hipErrorInvalidValue;
   int64_t lk_sum = 0;
   for (int f = 0; f < nfr; ++f) lk_sum += fr_lk[f];
   // profiler record: m4 = 1000 + DV (bench.py prices 2 (2 D + DV) per pair: dP over DV, dQ, dK)

@@ -70,12 +70,16 @@ SIGNATURES = {
     "s2h_flash_bwd_ok": [I, I, I],
     "s2h_flash_bwd_frames": [I, I, I, I, I, P, P, P, P, L, L, L, P, L, L, P, L, L, P, L, L, L, P, L, L, L, P, L, L, L,
                              P, L, L, P, L, L, P, P, F, F, c_uint64, P, P, P],
+    "s2h_flash_bwd_frames_rope": [I, I, I, I, I, P, P, P, P, L, L, L, P, L, L, P, L, L, P, L, L, L, P, L, L, L, P, L,
+                                  L, L, P, L, L, P, L, L, P, P, F, F, c_uint64, P, P, P, P, I, P, P],
     "s2h_attn_fwd_vfold_ws_bytes": [I, I, I],
     "s2h_attn_fwd_vfold": [I, I, I, P, L, L, P, L, L, P, L, L, P, L, L, P, F, F, c_uint64, c_uint64, P, P, L, P],
     "s2h_flash_bwd_frames_vfold": [I, I, I, P, P, P, P, L, L, P, L, P, L, P, L, L, P, L, L, P, L, L, P, L, P, P, F, F,
                                    c_uint64, P, P, P],
     "s2h_flash_bwd_frames_vfold_rope": [I, I, I, P, P, P, P, L, L, P, L, P, L, P, L, L, P, L, L, P, L, L, P, L, P, P, F, F,
                                    c_uint64, P, P, P, P, I, P, P],
+    "s2h_flash_bwd_frames_vfold_rope_qk": [I, I, I, P, P, P, P, L, L, P, L, P, L, P, L, L, P, L, L, P, L, L, P, L, P,
+                                           P, F, F, c_uint64, P, P, P, P, I, P, P, P],
     "s2h_vfold_weight": [I, I, I, P, P, P, P],
     "s2h_vfold_grad": [I, I, I, P, P, P, P],
     "s2h_layernorm_fwd": [I, I, I, P, L, P, L, I, P, P, P, F, P, L, P, P, P],

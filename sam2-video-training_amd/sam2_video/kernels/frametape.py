@@ -341,6 +341,7 @@ class FrameTape:
         self.premasked = set()
         self.prefused_dx = {}  # linear op index -> its input gradient, computed by its consumer (FFN fusion)
         self.derotated = set()  # linear-with-RoPE outputs whose consumer returned the un-rotated gradient
+        self.derotated_cols = {}  # ... whose consumer un-rotated the gradient's columns < the value
         self.seeded = set(out_grads)
 
         def acc(vid, g):
@@ -478,12 +479,15 @@ def _linear_bw(tape, op, gys):
     gy2 = gy.view(-1, N)
     if op.attrs.get("rope") and op.outs[0] not in tape.derotated:  # rotate the output gradient back (in place)
         ropes = op.fattrs["rope"]
+        c0 = tape.derotated_cols.get(op.outs[0], 0)  # columns the consumer already rotated back
+        if c0:
+            ropes = [r[:5] + (r[5] - c0, r[6]) for r in ropes]
         if all(r[2:] == ropes[0][2:] for r in ropes):
-            ops.rope_blocks(gy2, ropes[0], inverse=True)
+            ops.rope_blocks(gy2[:, c0:], ropes[0], inverse=True)
         else:
             st = tape.st(op.outs[0])
             for f, r in enumerate(ropes):
-                ops.rope_blocks(gy[st.offsets[f]:st.offsets[f] + st.numels[f]].view(-1, N), r, inverse=True)
+                ops.rope_blocks(gy[st.offsets[f]:st.offsets[f] + st.numels[f]].view(-1, N)[:, c0:], r, inverse=True)
     if op.outs[0] in tape.premasked:  # the consumer's dgrad already applied ReLU' and 1/keep
         dpre = gy2
     elif op.attrs["relu_out"]:
@@ -754,8 +758,9 @@ def attention(tape: FrameTape, q, k, v, scale, p_drop, _compute=True):
     return o if _compute else (o, lse)
 
 
-def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_buf, dv_buf):
-    """one frame-table flash launch, or a per-frame loop of the generic kernels"""
+def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_buf, dv_buf, rope=None):
+    """one frame-table flash launch, or a per-frame loop of the generic kernels; rope (flash launch
+    only, see ops.flash_bwd_frames): True when the launch rotated dq / dk back"""
     a = op.attrs
     F, B, Lq, H, D = tape.F, a["B"], a["Lq"], a["H"], a["D"]
     lks = op.fattrs["Lk"]
@@ -767,8 +772,8 @@ def _attn_frames_bwd(tape, op, q_all, k_st, v_st, kview, o_all, go, lse, dq, dk_
     if ops.flash_bwd_eligible(q_all):
         ops.flash_bwd_frames(F, B, lks, krow, op.fattrs["idx0"], q_all, k_rows, v_rows, o_all, go, lse, dq,
                              dk_rows, dv_rows, a["scale"], a["p"], a["seed"], keep=ks.buf if ks else None,
-                             koff=ks.offsets if ks else None)
-        return
+                             koff=ks.offsets if ks else None, rope=rope)
+        return rope is not None
     assert ks is None, "keep bitmap written but the flash backward is not eligible"
     if len(set(lks)) == 1:
         # uniform key count: the frames ARE one [F*B] batch (frame f's dropout indices start at
@@ -840,12 +845,20 @@ def _attn_vfold_bw(tape, op, gys):
         krow.append(krow[-1] + B * lks[f])
     ks = tape.stores[("aux", op.idx, "keep")] if a.get("keep") else None
     rope = _vfold_k_rope(tape, op.ins[1], lks, D)
+    # the q projection's RoPE (transformer.py:296) into the dQ store when it uses the same tables
+    rq = _proj_rope(tape, op.ins[0], [Lq] * F, D, D) if bwd_rope_fuse_enabled() else None
+    if rq is not None and rope is not None and (rq[0] is not rope[0] or rq[1] is not rope[1] or rq[2] != rope[2]):
+        rq = None
+    if rope is None and rq is not None:
+        rope = (rq[0], rq[1], rq[2], None)
     ops.flash_bwd_frames_vfold(F, B, lks, krow, op.fattrs["idx0"], q_all, k_st.buf.view(-1, 1, D),
                                m_st.buf.view(-1, 1, ops.VFOLD_DV), u_all, gu, lse, dq, dk.view(-1, 1, D), a["scale"],
                                a["p"], a["seed"], keep=ks.buf if ks else None, koff=ks.offsets if ks else None,
-                               rope=rope)
-    if rope is not None:
+                               rope=rope, rope_q=rq[3] if rq else None)
+    if rope is not None and rope[3] is not None:
         tape.derotated.add(op.ins[1])
+    if rq is not None:
+        tape.derotated.add(op.ins[0])
     return [dq.view(-1), dk, None]
 
 
@@ -856,15 +869,28 @@ def _vfold_k_rope(tape, kvid, lks, D):
     gradient back and the linear's backward skips its rope pass; else None"""
     if os.environ.get("S2H_VFOLD_DK_ROPE", "1") == "0":
         return None
-    prod = tape.producer.get(kvid)
-    if prod is None or prod.kind != "linear" or tape.nuse[kvid] != 1:
+    return _proj_rope(tape, kvid, lks, D, D)
+
+
+def bwd_rope_fuse_enabled():
+    """S2H_BWD_ROPE_FUSE=0 keeps the q (and self-attention k) projections' inverse RoPE as separate
+    passes in the linear backward instead of the attention backward's dQ / dK stores"""
+    return os.environ.get("S2H_BWD_ROPE_FUSE", "1") != "0"
+
+
+def _proj_rope(tape, vid, rows, D, ncol):
+    """(cos, sin, period, rotated rows per frame) when value vid is the output of ONE linear-with-RoPE
+    op used by one attention only, whose epilogue rotates D-wide heads over its first ncol columns in
+    blocks of rows[f] rows with the same tables in every frame; else None"""
+    prod = tape.producer.get(vid)
+    if prod is None or prod.kind != "linear" or tape.nuse[vid] != 1:
         return None
     ropes = prod.fattrs.get("rope")
-    if not ropes or len(ropes) != len(lks) or any(r is None for r in ropes):
+    if not ropes or len(ropes) != len(rows) or any(r is None for r in ropes):
         return None
-    cos, sin, _, _, period, ncol, dh = ropes[0]
+    cos, sin, _, _, period, _, _ = ropes[0]
     for f, r in enumerate(ropes):
-        if r[0] is not cos or r[1] is not sin or r[4] != period or r[5] != D or r[6] != D or r[2] != lks[f]:
+        if r[0] is not cos or r[1] is not sin or r[4] != period or r[5] != ncol or r[6] != D or r[2] != rows[f]:
             return None
     return cos, sin, period, [r[3] for r in ropes]
 
@@ -923,8 +949,16 @@ def _qkv_bw(tape, op, gys):
     def rows(t):  # [F*B, L, H, D] slice of a packed projection -> [F*B*L, H, D] rows (uniform row stride)
         assert t.stride(0) == L * t.stride(1)
         return torch.as_strided(t, (F * B * L, H, D), (t.stride(1), t.stride(2), 1), t.storage_offset())
-    _attn_frames_bwd(tape, op, q_all, None, None, (rows(k_all), rows(v_all), rows(dk), rows(dv)), o_all, go, lse,
-                     dq, None, None)
+    # the qkv projection's RoPE epilogue on q (its first D columns) transposed into the dQ store when
+    # this attention is its only consumer; the linear's backward then rotates only the k columns
+    fuse = None
+    if rope is None and H == 1 and D == 256 and bwd_rope_fuse_enabled():
+        pr = _proj_rope(tape, op.ins[0], [L] * F, D, 2 * D)
+        if pr is not None:
+            fuse = (pr[0], pr[1], pr[2], pr[3])
+    if _attn_frames_bwd(tape, op, q_all, None, None, (rows(k_all), rows(v_all), rows(dk), rows(dv)), o_all, go, lse,
+                        dq, None, None, rope=fuse):
+        tape.derotated_cols[op.ins[0]] = D
     if rope is not None:
         cos, sin, period = rope
         for g in (dq, dk):

@@ -588,13 +588,30 @@ def attn_fwd_vfold(q, k, mem, u, lse, scale, p_drop=0.0, seed=0, idx0=0, keep=No
     return u, lse
 
 
+def _rope_table_args(nfr, rope):
+    """(cos, sin, period) checks and the per-frame row-count arrays of a fused inverse RoPE"""
+    import ctypes
+    cos, sin, period = rope[:3]
+    _dev(cos, sin)
+    assert cos.dtype == sin.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
+
+    def arr(n):  # (address, the ctypes array that must outlive the call)
+        if n is None:
+            return None
+        assert len(n) == nfr
+        a = (ctypes.c_int * nfr)(*[int(x) for x in n])
+        return ctypes.addressof(a), a
+    return ptr(cos), ptr(sin), int(period), arr
+
+
 def flash_bwd_frames_vfold(nfr, bpf, lk, krow, idx0, q, k, mem, u, du, lse, dq, dk, scale, p_drop, seed, keep=None,
-                           koff=None, rope=None):
+                           koff=None, rope=None, rope_q=None):
     """Frame-batched backward of attn_fwd_vfold (s2h_flash_bwd_frames_vfold): q / u / du / dq
     [nfr*bpf, Lq, 1, C] views, k / mem / dk PACKED [rows, 1, C] (frame f: bpf blocks of lk[f] rows
-    from row krow[f]); keep / koff as flash_bwd_frames.  rope = (cos, sin, period, nrot per frame):
-    dk comes out rotated back (s2h_flash_bwd_frames_vfold_rope: the k projection's RoPE transposed,
-    fused into the dK store)"""
+    from row krow[f]); keep / koff as flash_bwd_frames.  rope = (cos, sin, period, nrot per frame or
+    None): dk comes out rotated back (the k projection's RoPE transposed, fused into the dK store);
+    rope_q = query rows rotated per frame (same tables): dq rotated back in the dQ store
+    (s2h_flash_bwd_frames_vfold_rope_qk)"""
     import ctypes
     _dev(q, k, mem, u, du, lse, dq, dk)
     B, Lq = q.shape[0], q.shape[1]
@@ -618,14 +635,13 @@ def flash_bwd_frames_vfold(nfr, bpf, lk, krow, idx0, q, k, mem, u, du, lse, dq, 
             ptr(du), *_brs(du), ptr(dq), *_brs(dq), ptr(dk), rs(dk), ptr(lse), ptr(di), float(scale), float(p_drop),
             int(seed) & (2**64 - 1), kp, ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None]
     if rope is None:
+        assert rope_q is None
         call("s2h_flash_bwd_frames_vfold", *args, stream())
     else:
-        cos, sin, period, nrot = rope
-        _dev(cos, sin)
-        assert cos.dtype == sin.dtype == torch.float32 and cos.is_contiguous() and sin.is_contiguous()
-        anr = (ctypes.c_int * nfr)(*[int(x) for x in nrot])
-        call("s2h_flash_bwd_frames_vfold_rope", *args, ptr(cos), ptr(sin), int(period),
-             ctypes.cast(anr, ctypes.c_void_p).value, stream())
+        pc, ps, period, arr = _rope_table_args(nfr, rope)
+        ank, anq = arr(rope[3]), arr(rope_q)  # (pointer, keep-alive list)
+        call("s2h_flash_bwd_frames_vfold_rope_qk", *args, pc, ps, period, ank[0] if ank else None,
+             anq[0] if anq else None, stream())
     return dq, dk
 
 
@@ -675,11 +691,13 @@ def flash_bwd_eligible(q):
 
 
 def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, scale, p_drop, seed, keep=None,
-                     koff=None):
+                     koff=None, rope=None):
     """Frame-batched flash backward (s2h_flash_bwd_frames): q/o/do/dq [nfr*bpf, Lq, H, D] views,
     k/v/dk/dv PACKED [rows, H, D] views (frame f: bpf blocks of lk[f] rows from row krow[f]),
     lse [nfr*bpf, H, Lq]; frame f's dropout indices start at idx0[f]; keep (optional int32) holds
-    frame f's forward keep bitmap from word koff[f]."""
+    frame f's forward keep bitmap from word koff[f].  rope = (cos, sin, period, query rows per frame):
+    dq comes out rotated back (s2h_flash_bwd_frames_rope, the q projection's RoPE transposed in the
+    dQ store; head dim 256)"""
     import ctypes
     _dev(q, k, v, o, do, lse, dq, dk, dv)
     B, Lq, H, D = q.shape
@@ -698,11 +716,17 @@ def flash_bwd_frames(nfr, bpf, lk, krow, idx0, q, k, v, o, do, lse, dq, dk, dv, 
     def hl(t):  # (head, row) strides of a packed [rows, H, D] view
         assert t.stride(-1) == 1
         return t.stride(1), t.stride(0)
-    call("s2h_flash_bwd_frames", nfr, bpf, H, Lq, D, ctypes.cast(alk, ctypes.c_void_p).value,
-         ctypes.cast(akr, ctypes.c_void_p).value, ctypes.cast(aix, ctypes.c_void_p).value,
-         ptr(q), *_bhl(q), ptr(k), *hl(k), ptr(v), *hl(v), ptr(o), *_bhl(o), ptr(do), *_bhl(do),
-         ptr(dq), *_bhl(dq), ptr(dk), *hl(dk), ptr(dv), *hl(dv), ptr(lse), ptr(di), float(scale), float(p_drop),
-         int(seed) & (2**64 - 1), kp, ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None, stream())
+    args = [nfr, bpf, H, Lq, D, ctypes.cast(alk, ctypes.c_void_p).value, ctypes.cast(akr, ctypes.c_void_p).value,
+            ctypes.cast(aix, ctypes.c_void_p).value, ptr(q), *_bhl(q), ptr(k), *hl(k), ptr(v), *hl(v), ptr(o),
+            *_bhl(o), ptr(do), *_bhl(do), ptr(dq), *_bhl(dq), ptr(dk), *hl(dk), ptr(dv), *hl(dv), ptr(lse), ptr(di),
+            float(scale), float(p_drop), int(seed) & (2**64 - 1), kp,
+            ctypes.cast(ako, ctypes.c_void_p).value if kp is not None else None]
+    if rope is None:
+        call("s2h_flash_bwd_frames", *args, stream())
+    else:
+        pc, ps, period, arr = _rope_table_args(nfr, rope)
+        anq = arr(rope[3])
+        call("s2h_flash_bwd_frames_rope", *args, pc, ps, period, anq[0], stream())
     return dq, dk, dv
 
 
