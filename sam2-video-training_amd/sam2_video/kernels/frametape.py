@@ -357,6 +357,7 @@ class FrameTape:
                 owned.add(vid)
 
         self.grads, self.acc = G, acc  # for ops whose backward finishes their producer's (_ln_dgrad_fused)
+        self.owned = owned  # gradients this backward allocated (safe to add into in place)
         self.side = ops.SideWork()  # the Linear weight gradients' stream (joined before returning)
         for k in range(len(self.ops) - 1, -1, -1):
             op = self.ops[k]
@@ -368,7 +369,7 @@ class FrameTape:
                 if need:
                     acc(v, g)
         self.side.join()
-        self.grads = self.acc = None
+        self.grads = self.acc = self.owned = None
         return {name: G.get(vid) for name, vid in self.inputs.items()}
 
     def out_vid(self, t):
@@ -524,9 +525,33 @@ def _linear_bw(tape, op, gys):
                 dx = _fp8.linear_dgrad(dpre, mod, pre=x2, act="relu", alpha=alpha).view(-1)
             tape.premasked.add(op.ins[0])
         elif not _ln_dgrad_fused(tape, op, prod, dpre, mod):
-            dx = _fp8.linear_dgrad(dpre, mod).view(-1)
+            dx = _dgrad_into(tape, op.ins[0], dpre, mod)
     dres = gy if op.needs[1] else None
     return [dx, dres]
+
+
+def dgrad_acc_enabled():
+    """S2H_DGRAD_ACC=0: a Linear's input gradient is always a new tensor, summed with the value's
+    other gradients by a separate add (A/B of _dgrad_into)"""
+    return os.environ.get("S2H_DGRAD_ACC", "1") != "0"
+
+
+def _dgrad_into(tape, vid, dy, mod):
+    """dx = dy @ W of a Linear whose input vid already holds a gradient from a later consumer: the
+    dgrad GEMM's epilogue adds it (into it in place when this backward owns it, else as the residual
+    of a new buffer) and the separate add launch goes; returns None then (nothing left to sum)"""
+    prev = tape.grads.get(vid) if dgrad_acc_enabled() else None
+    K = mod.compute_weight().shape[1]
+    if (prev is None or prev.dtype != dy.dtype or dy.dtype != torch.bfloat16 or not prev.is_contiguous()
+            or prev.numel() != dy.numel() // dy.shape[-1] * K or _fp8.dgrad_on_mx8(dy, mod)):
+        return _fp8.linear_dgrad(dy, mod).view(-1)
+    w = mod.compute_weight()
+    if vid in tape.owned:
+        ops.linear_dgrad(dy, w, dx=prev.view(-1, K), accumulate=True)
+    else:
+        tape.grads[vid] = ops.linear_dgrad(dy, w, residual=prev.view(-1, K)).view(-1)
+        tape.owned.add(vid)
+    return None
 
 
 def ffn_fuse_enabled():

@@ -380,8 +380,49 @@ class _MergeScores(torch.autograd.Function):
         return ds, dhr, None, None, None, None
 
 
+class _MergeMasksScores(torch.autograd.Function):
+    """_MergeMasks of the high-res logits and _MergeScores weighted by the same logits as one node: the
+    backward writes the max-merge gradient and adds the weights' sigmoid term into the same buffer
+    (the sum autograd formed from two nodes, without its zero fill and add launches)"""
+
+    @staticmethod
+    def forward(ctx, hr, s, cat_off, cat_obj, obj_cat, ncat):
+        O, P = hr.shape[0], hr[0].numel()
+        out = torch.empty((ncat, *hr.shape[1:]), device=hr.device, dtype=torch.float32)
+        arg = torch.empty(ncat, P, device=hr.device, dtype=torch.int32)
+        ops.group_max(hr.reshape(O, P), cat_off, cat_obj, ncat, out.view(ncat, P), arg)
+        stats = ops.mask_stats(hr.detach().reshape(O, -1), None)
+        sout = torch.empty(ncat, s.shape[1], device=s.device, dtype=torch.float32)
+        ops.group_wavg(s.contiguous(), stats, cat_off, cat_obj, ncat, sout)
+        ctx.save_for_backward(arg, s, hr, stats, sout, obj_cat, cat_off)
+        ctx.shape = hr.shape
+        return out, sout
+
+    @staticmethod
+    def backward(ctx, g, gs):
+        arg, s, hr, stats, sout, obj_cat, cat_off = ctx.saved_tensors
+        O = ctx.shape[0]
+        dx = torch.empty(ctx.shape, device=hr.device, dtype=torch.float32)
+        if g is None:
+            dx.zero_()
+        else:
+            ops.group_max_bwd(g.contiguous().view(g.shape[0], -1), obj_cat, arg, dx.view(O, -1))
+        ds = None
+        if gs is not None:
+            ds = torch.empty_like(s)
+            dw = torch.empty(O, device=s.device)
+            ops.group_wavg_bwd(s.contiguous(), sout, gs.contiguous(), stats, obj_cat, cat_off, ds, dw)
+            ops.sigmoid_grad_axpy(hr.detach().reshape(O, -1), dw, dx.view(O, -1))
+        return dx, ds, None, None, None, None
+
+
 def merge_masks(x, groups):
     return _MergeMasks.apply(x, groups.cat_off, groups.cat_obj, groups.obj_cat, groups.ncat)
+
+
+def merge_masks_scores(hr, s, groups):
+    """(merge_masks(hr), merge_scores(s, hr)) as one autograd node"""
+    return _MergeMasksScores.apply(hr, s, groups.cat_off, groups.cat_obj, groups.obj_cat, groups.ncat)
 
 
 def merge_scores(s, hr, groups):

@@ -254,9 +254,11 @@ def linear_add_ln(x, w, bias, residual, gamma, beta, eps, drop_p=0.0, seed=0, dr
     return y, xsum, mean, rstd
 
 
-def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0):
+def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0, residual=None):
     """dx = alpha * dy @ w   (optionally * act'(pre) elementwise, fusing the previous layer's
-    activation grad; for ReLU `pre` may be the previous layer's output, and alpha its 1/keep)."""
+    activation grad; for ReLU `pre` may be the previous layer's output, and alpha its 1/keep);
+    accumulate: dx += ...; residual [rows, K] (same dtype, contiguous): dx = ... + residual (one
+    rounding of the fp32 sum)"""
     dy2 = dy.reshape(-1, dy.shape[-1])
     M, N = dy2.shape
     K = w.shape[1]
@@ -264,9 +266,10 @@ def linear_dgrad(dy, w, dx=None, accumulate=False, pre=None, act=None, alpha=1.0
         dx = torch.empty(*dy.shape[:-1], K, device=dy.device, dtype=dy.dtype)
     d2 = dx.view(-1, K)
     p2 = pre.reshape(-1, K) if pre is not None else None
+    r2 = residual.view(-1, K) if residual is not None else None
     gemm(dy2, w, d2, M=M, N=K, K=N, lda_m=dy2.stride(0), lda_k=1, ldb_k=K, ldb_n=1, ldc=K,
          aux=p2, ldx=K, aux_mode=2 if pre is not None else 0, act=ACT[act] if pre is not None else 0,
-         alpha=alpha, beta=1.0 if accumulate else 0.0)
+         alpha=alpha, beta=1.0 if accumulate else 0.0, residual=r2, ldr=K if r2 is not None else 0)
     return dx
 
 

@@ -117,7 +117,7 @@ class CategoryGroups:
 def merge_object_results_to_category(previous_stages_out: List[Dict[str, Any]], obj_to_cat: List[int],
                                      num_categories: int) -> List[Dict[str, Any]]:
     """masks.py:53-213 for the per-frame outputs of forward_tracking."""
-    from ..kernels.functional_sam import merge_masks, merge_scores
+    from ..kernels.functional_sam import merge_masks, merge_masks_scores, merge_scores
 
     if not previous_stages_out:
         return []
@@ -130,14 +130,15 @@ def merge_object_results_to_category(previous_stages_out: List[Dict[str, Any]], 
     for fo in previous_stages_out:
         hr = fo["pred_masks_high_res"]
         m = {}
-        m["pred_masks_high_res"] = merge_masks(hr, groups)
+        # the high-res masks and the IoU scores weighted by them as one autograd node
+        m["pred_masks_high_res"], merged_ious = merge_masks_scores(hr, fo["multistep_pred_ious"][0], groups)
         with torch.no_grad():
             m["pred_masks"] = merge_masks(fo["pred_masks"].detach(), groups)
         m["multistep_pred_masks"] = m["pred_masks"]
         m["multistep_pred_masks_high_res"] = m["pred_masks_high_res"]
         m["multistep_pred_multimasks"] = [m["pred_masks"]]
         m["multistep_pred_multimasks_high_res"] = [m["pred_masks_high_res"]]
-        m["multistep_pred_ious"] = [merge_scores(fo["multistep_pred_ious"][0], hr, groups)]
+        m["multistep_pred_ious"] = [merged_ious]
         with torch.no_grad():
             m["multistep_object_score_logits"] = [merge_scores(fo["multistep_object_score_logits"][0], hr.detach(),
                                                                groups)]

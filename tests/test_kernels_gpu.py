@@ -1051,6 +1051,15 @@ def test_category_merge_multi_object_matches_reference_formulas():
     ((hr_ref * gh).sum() + (mi_ref * gi).sum()).backward()
     _close(x.grad, xr.grad, 1e-4)
     _close(s.grad, sr.grad, 1e-5)
+    # the one-node merge (merge_masks_scores) gives the bits of the two separate nodes
+    from sam2_video.kernels.functional_sam import merge_scores
+    from sam2_video.utils.masks import CategoryGroups as _CG
+    x2 = logits.clone().requires_grad_(True)
+    s2 = ious.clone().requires_grad_(True)
+    grp = _CG(obj_to_cat, 3, x2.device)
+    from sam2_video.kernels.functional_sam import merge_masks as _mm
+    ((_mm(x2, grp) * gh).sum() + (merge_scores(s2, x2, grp) * gi).sum()).backward()
+    assert torch.equal(x.grad, x2.grad) and torch.equal(s.grad, s2.grad)
     # a NaN logit propagates through the max like torch.max (the kernel once dropped it)
     from sam2_video.kernels.functional_sam import merge_masks
     from sam2_video.utils.masks import CategoryGroups
