@@ -423,6 +423,12 @@ int s2h_mlp_heads(int nheads, int M, const void* const* x, const int64_t* ldx, c
 int s2h_layernorm_fwd(int dt, int rows, int C, const void* x, int64_t ldx, const void* badd, int64_t ldb,
                       int b_bcast, void* xsum, const float* gamma, const float* beta, float eps, void* y,
                       int64_t ldy, float* mean, float* rstd, hipStream_t st);
+/* bf16 LayerNorm of contiguous rows that also stores ype = y + pe[row % pe_rows] (the two-way
+ * transformer's keys + key_pe after norm4, transformer.py:182-185 feeding the next block's
+ * k = keys + key_pe, transformer.py:170 / :102): y bit-identical to s2h_layernorm_fwd, ype to the
+ * broadcast add it replaces.  16-B aligned rows, C / 8 <= 64. */
+int s2h_layernorm_fwd_pe(int dt, int rows, int C, const void* x, const float* gamma, const float* beta, float eps,
+                         void* y, float* mean, float* rstd, const void* pe, int pe_rows, void* ype, hipStream_t st);
 /* dx = LN'(dy) (+= when dx_accum, or + dres: the residual-stream gradient of the fused
  * pre-add, so the caller needs no copy), dgamma += , dbeta += (fp32, both or neither).
  * The weight gradients go through per-block partials in `ws`

@@ -79,11 +79,15 @@ __device__ __forceinline__ void load_param(const float* p, float* out) {
 }
 
 // ------------------------------------------------------------ forward (vector)
-template <typename T, int G, int K>
+// PE: also ype = y + pe[row % pe_rows] (the stored y, rounded to T, plus a positional table; the
+// add_bcast it replaces rounds the same fp32 sum) -- the two-way transformer's keys + key_pe after
+// norm4 (transformer.py:182-185 feeding :170 / :102)
+template <typename T, int G, int K, bool PE = false>
 __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int C, const T* a, int64_t lda, const T* badd,
                                                          int64_t ldb, int b_bcast, T* xsum, const float* gamma,
                                                          const float* beta, float eps, T* y, int64_t ldy,
-                                                         float* mean, float* rstd) {
+                                                         float* mean, float* rstd, const T* pe, int pe_rows,
+                                                         T* ype) {
   constexpr int VEC = Chunk<T>::VEC;
   constexpr int RPW = 64 / G;  // rows per wave
   const int lane = threadIdx.x & 63;
@@ -147,6 +151,13 @@ __global__ __launch_bounds__(256) void ln_fwd_vec_kernel(int rows, int C, const 
 #pragma unroll
       for (int j = 0; j < VEC; ++j) o[j] = (v[k][j] - mu) * rs * gv[k][j] + bv[k][j];
       Chunk<T>::store(y + row * ldy + ch * VEC, o);
+      if constexpr (PE) {
+        float t[VEC];
+        Chunk<T>::load(pe + (row % pe_rows) * (int64_t)C + ch * VEC, t);
+#pragma unroll
+        for (int j = 0; j < VEC; ++j) t[j] += (float)(T)o[j];
+        Chunk<T>::store(ype + row * (int64_t)C + ch * VEC, t);
+      }
     }
   }
   if (gl == 0) { mean[row] = mu; rstd[row] = rs; }
@@ -416,7 +427,7 @@ void fwd_launch(int rows, dim3 blk, hipStream_t st, int C, const T* x, int64_t l
                 float* mean, float* rstd) {
   const int rpb = 4 * (64 / G);
   hipLaunchKernelGGL((ln_fwd_vec_kernel<T, G, K>), dim3((rows + rpb - 1) / rpb), blk, 0, st, rows, C, x, ldx, badd,
-                     ldb, b_bcast, xsum, gamma, beta, eps, y, ldy, mean, rstd);
+                     ldb, b_bcast, xsum, gamma, beta, eps, y, ldy, mean, rstd, nullptr, 1, nullptr);
 }
 
 template <typename T, int G, int K>
@@ -497,6 +508,34 @@ extern "C" int s2h_layernorm_fwd(int dt, int rows, int C, const void* x, int64_t
                         (bf16*)y, ldy, mean, rstd, st);
   return ln_fwd<float>(rows, C, (const float*)x, ldx, (const float*)badd, ldb, b_bcast, (float*)xsum, gamma, beta,
                        eps, (float*)y, ldy, mean, rstd, st);
+}
+
+// LayerNorm of contiguous bf16 rows (C / 8 lanes per row, the vector plan) that also stores
+// ype = y + pe[row % pe_rows]: y bit-identical to s2h_layernorm_fwd, ype to its add_bcast
+extern "C" int s2h_layernorm_fwd_pe(int dt, int rows, int C, const void* x, const float* gamma, const float* beta,
+                                    float eps, void* y, float* mean, float* rstd, const void* pe, int pe_rows,
+                                    void* ype, hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (dt != S2H_BF16 || C <= 0 || C > 1280 || pe == nullptr || ype == nullptr || pe_rows <= 0)
+    return (int)hipErrorInvalidValue;
+  const LnPlan p = plan<bf16>(C, {C, 0, C}, {x, nullptr, nullptr, y});
+  if (!p.vec || p.K != 1 || ((uintptr_t)pe & 15) || ((uintptr_t)ype & 15)) return (int)hipErrorInvalidValue;
+  const int rpb = 4 * (64 / p.G);
+  const dim3 grid((rows + rpb - 1) / rpb);
+  const bf16* xb = (const bf16*)x;
+#define S2H_LN_PE(GG)                                                                                           \
+  hipLaunchKernelGGL((ln_fwd_vec_kernel<bf16, GG, 1, true>), grid, dim3(256), 0, st, rows, C, xb, (int64_t)C,   \
+                     (const bf16*)nullptr, (int64_t)0, 0, (bf16*)nullptr, gamma, beta, eps, (bf16*)y, (int64_t)C, \
+                     mean, rstd, (const bf16*)pe, pe_rows, (bf16*)ype)
+  switch (p.G) {
+    case 8: S2H_LN_PE(8); break;
+    case 16: S2H_LN_PE(16); break;
+    case 32: S2H_LN_PE(32); break;
+    case 64: S2H_LN_PE(64); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef S2H_LN_PE
+  return (int)hipGetLastError();
 }
 
 // dgamma += sum_b part[b][0:C], dbeta += sum_b part[b][C:2C] (partial rows written by a fused

@@ -83,6 +83,7 @@ SIGNATURES = {
     "s2h_vfold_weight": [I, I, I, P, P, P, P],
     "s2h_vfold_grad": [I, I, I, P, P, P, P],
     "s2h_layernorm_fwd": [I, I, I, P, L, P, L, I, P, P, P, F, P, L, P, P, P],
+    "s2h_layernorm_fwd_pe": [I, I, I, P, P, P, F, P, P, P, P, I, P, P],
     "s2h_layernorm_bwd_ws_bytes": [I, I, I],
     "s2h_layernorm_bwd": [I, I, I, P, L, P, L, P, P, P, P, L, I, P, L, P, P, P, P],
     "s2h_add": [I, L, P, P, F, F, P, P],

@@ -732,6 +732,28 @@ def layer_norm(tape: FrameTape, x, mod, eps, add=None, _compute=True):
     return (y, xsum) if add is not None else y
 
 
+def layer_norm_pe_ok(x, mod, pe):
+    """layer_norm_pe applies: bf16 rows of 256 (LayerNorm width), a contiguous bf16 [L, C] table
+    whose L divides the rows, S2H_LN_PE not 0"""
+    C = x.shape[-1]
+    return (os.environ.get("S2H_LN_PE", "1") != "0" and x.dtype == torch.bfloat16 and pe.dtype == torch.bfloat16
+            and C == 256 and x.is_contiguous() and mod.weight.shape[0] == C and pe.is_contiguous() and pe.dim() == 2 and pe.shape[1] == C
+            and (x.numel() // C) % pe.shape[0] == 0)
+
+
+def layer_norm_pe(tape: FrameTape, x, mod, eps, pe):
+    """(LN(x), LN(x) + pe) in one launch (s2h_layernorm_fwd_pe): records the LayerNorm and the
+    broadcast add of the constant table pe [L, C] (FN.add_bcast) as the two ops they replace"""
+    y, mean, rstd = layer_norm(tape, x, mod, eps, _compute=False)
+    k = add_bcast(tape, y, pe, 1.0, 1.0, None, None, _compute=False)
+    C = x.shape[-1]
+    from ._lib import call
+    call("s2h_layernorm_fwd_pe", ops.dt(x), x.numel() // C, C, ops.ptr(x),
+         ops.ptr(mod.weight.detach()), ops.ptr(mod.bias.detach()), float(eps), ops.ptr(y), ops.ptr(mean),
+         ops.ptr(rstd), ops.ptr(pe), pe.shape[0], ops.ptr(k), ops.stream())
+    return y, k
+
+
 def call_ln_fwd(x, mod, eps, y, mean, rstd, add, xsum):
     from ._lib import call
     C = x.shape[-1]
@@ -1055,16 +1077,17 @@ def _add_bw(tape, op, gys):
             _scaled(g, op.attrs["beta"]) if op.needs[1] else None]
 
 
-def add_bcast(tape: FrameTape, a, b, alpha, beta, shape, bparam):
+def add_bcast(tape: FrameTape, a, b, alpha, beta, shape, bparam, _compute=True):
     """out[o, ...] = alpha a[o, ...] + beta b[...]; b is a constant table, a parameter's compute
-    copy (bparam) or a recorded value (the memory positional table)"""
+    copy (bparam) or a recorded value (the memory positional table); _compute=False: record only"""
     a = a if (a is None or a.is_contiguous()) else a.contiguous()
     b = b.contiguous()
     op, first = tape._begin("add_bcast", [a, b], _add_bcast_bw, {"alpha": alpha, "beta": beta, "bparam": bparam})
     scale = tape._varlen_scale(a, b)
     oshape = a.shape if a is not None else shape
     vid, out = tape._out(0, oshape, b.dtype, scale)
-    ops.add_bcast(a, b, out=out, alpha=alpha, beta=beta)
+    if _compute:
+        ops.add_bcast(a, b, out=out, alpha=alpha, beta=beta)
     tape._fattr(op, "inner", b.numel())
     tape._fattr(op, "outer", out.numel() // b.numel())
     tape._finish(op, [vid], tape._req(op, (bparam,)))

@@ -24,6 +24,12 @@ def _lin(x, mod, act=None, residual=None, cscale=None):
     return ops.linear(x, mod.compute_weight(), mod.bias.detach(), act=act, residual=residual, cscale=cscale)
 
 
+def fused_add_enabled():
+    """S2H_MEMENC_ADD=0: the pixel-feature add as its own broadcast-add launch (A/B)"""
+    import os
+    return os.environ.get("S2H_MEMENC_ADD", "1") != "0"
+
+
 class MaskDownSampler(nn.Module):
     def __init__(self, embed_dim=256, kernel_size=4, stride=4, padding=0, total_stride=16, activation=None):
         super().__init__()
@@ -45,10 +51,11 @@ class MaskDownSampler(nn.Module):
     def _fused(self, conv):
         return (self.k, self.s, self.p) == (3, 2, 1) and (conv.in_ch, conv.out_ch) in self.FUSED
 
-    def forward(self, x=None, logits=None, scale=1.0, shift=0.0, dtype=None):
+    def forward(self, x=None, logits=None, scale=1.0, shift=0.0, dtype=None, add=None):
         """x [O, H, W, 1] compute dtype, or `logits` [O, H, W] fp32 with the memory-encoder
         input transform sigmoid(logits) * scale + shift fused into the first stage
-        -> [O, H/16, W/16, embed_dim]"""
+        -> [O, H/16, W/16, embed_dim]; add [H/16 * W/16, embed_dim] (shared by the objects): added to
+        every object's output in the final projection's epilogue"""
         for i in range(self.num_layers):
             conv, ln = self.encoder[3 * i], self.encoder[3 * i + 1]
             if self._fused(conv):
@@ -66,7 +73,21 @@ class MaskDownSampler(nn.Module):
             y = _lin(col, conv).view(O, Ho, Wo, -1)
             y, _, _ = ops.layernorm_fwd(y, ln.weight.detach(), ln.bias.detach(), ln.eps)
             x = ops.act_fwd(y, "gelu")
-        return _lin(x, self.encoder[3 * self.num_layers])
+        proj = self.encoder[3 * self.num_layers]
+        if add is None or not fused_add_enabled():
+            y = _lin(x, proj)
+            return y if add is None else ops.add_bcast(y, add)
+        # one batched GEMM (batch = objects) whose residual has batch stride 0: the shared pixel
+        # features added in the epilogue (memory_encoder.py:174-175: pix_feat_proj(pix_feat) + masks)
+        O, Ho, Wo, K = x.shape
+        w = proj.compute_weight()
+        N = w.shape[0]
+        assert tuple(add.shape) == (Ho * Wo, N) and add.is_contiguous() and x.is_contiguous()
+        out = torch.empty(O, Ho, Wo, N, device=x.device, dtype=x.dtype)
+        ops.gemm(x.view(O * Ho * Wo, K), w, out.view(-1, N), M=Ho * Wo, N=N, K=K, lda_m=K, lda_k=1, ldb_k=1,
+                 ldb_n=K, ldc=N, batch=O, sA=Ho * Wo * K, sB=0, sC=Ho * Wo * N, bias=proj.bias.detach(),
+                 residual=add, ldr=N, sR=0)
+        return out
 
 
 class CXBlock(nn.Module):
@@ -115,9 +136,8 @@ class MemoryEncoder(nn.Module):
         logits, transformed as sigmoid(masks) * scale + shift inside the first down-sampler stage
         -> (features [O, h, w, out_dim], pos table [h*w, out_dim])"""
         O = masks.shape[0]
-        m = self.mask_downsampler(logits=masks, scale=scale, shift=shift, dtype=pix_feat.dtype)  # [O, h, w, C]
         p = _lin(pix_feat.detach(), self.pix_feat_proj)  # [h*w, C]
-        x = ops.add_bcast(m, p)
+        x = self.mask_downsampler(logits=masks, scale=scale, shift=shift, dtype=pix_feat.dtype, add=p)  # [O, h, w, C]
         x = self.fuser(x)
         x = _lin(x, self.out_proj)
         pos = self.position_encoding.table(h, w, x.device, x.dtype)

@@ -209,10 +209,11 @@ class TwoWayTransformer(nn.Module):
         n = len(self.layers)
         fa = self.final_attn_token_to_image
         qqf = None
+        k_next = None  # keys + key_pe written by the previous block's norm4 launch (_ft.layer_norm_pe)
         for i, blk in enumerate(self.layers):
             t2i, i2t = blk.cross_attn_token_to_image, blk.cross_attn_image_to_token
             x1, qq = _ft.dec_self(tape, queries, pe, blk.self_attn, blk.norm1, t2i.q_proj, blk.skip_first_layer_pe)
-            k = FN.add_bcast(keys, pe_table)
+            k = k_next if k_next is not None else FN.add_bcast(keys, pe_table)
             B, Lq, I = qq.shape
             Lk, h = k.shape[1], t2i.num_heads
             o = FN.attention(qq.view(B, Lq, h, I // h), t2i.k_proj(k).view(B, Lk, h, I // h),
@@ -223,8 +224,12 @@ class TwoWayTransformer(nn.Module):
                 qqf = qf
             oi = FN.attention(i2t.q_proj(k).view(B, Lk, h, I // h), ki.view(B, Lq, h, I // h),
                               vi.view(B, Lq, h, I // h), p_drop=i2t._p())
-            keys = blk.norm4(i2t.out_proj(oi.reshape(B, Lk, I), residual=keys))
-        k = FN.add_bcast(keys, pe_table)
+            xk = i2t.out_proj(oi.reshape(B, Lk, I), residual=keys)
+            if _ft.layer_norm_pe_ok(xk, blk.norm4, pe_table):  # norm4 and the next k = keys + key_pe: one launch
+                keys, k_next = _ft.layer_norm_pe(tape, xk, blk.norm4, blk.norm4.eps, pe_table)
+            else:
+                keys, k_next = blk.norm4(xk), None
+        k = k_next if k_next is not None else FN.add_bcast(keys, pe_table)
         B, Lq, I = qqf.shape
         Lk, h = k.shape[1], fa.num_heads
         o = FN.attention(qqf.view(B, Lq, h, I // h), fa.k_proj(k).view(B, Lk, h, I // h),

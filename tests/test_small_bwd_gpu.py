@@ -72,3 +72,55 @@ def test_sum_outer_batched_equals_per_frame(dtype, F, O, inner):
     assert torch.equal(out, ref)
     t = x.double().sum(1).flatten()
     assert (out.double() - t).abs().max().item() <= (1e-2 if dtype == torch.bfloat16 else 1e-5) * t.abs().max().item()
+
+
+def test_memory_encoder_pixel_add_in_projection_epilogue(monkeypatch):
+    """the memory encoder's pix_feat_proj(pix_feat) + masks (memory_encoder.py:174-175) added in the
+    mask down-sampler's final projection (one batched GEMM, residual with object stride 0) against the
+    projection + broadcast add (S2H_MEMENC_ADD=0): equal to one bf16 rounding of the same fp32 sum"""
+    import sys
+    import os
+    sys.path.insert(0, os.path.dirname(__file__))
+    from step_harness import build_model
+    model = build_model("base_plus", 256, ["memory_encoder"], dtype="bf16")
+    enc = model.memory_encoder
+    torch.manual_seed(6)
+    h = w = 16
+    pix = torch.randn(h * w, 256, device=DEV).to(torch.bfloat16)
+    masks = torch.randn(13, 16 * h, 16 * w, device=DEV) * 4
+    out = {}
+    for flag in ("0", "1"):
+        monkeypatch.setenv("S2H_MEMENC_ADD", flag)
+        feat, pos = enc(pix, masks, h, w, scale=20.0, shift=-10.0)
+        torch.cuda.synchronize()
+        out[flag] = feat.float()
+    a, b = out["1"], out["0"]
+    assert torch.isfinite(a).all()
+    # one bf16 rounding of x, carried through the fuser's CX blocks and the output projection
+    assert (a - b).abs().max().item() <= 2e-2 * b.abs().max().item()
+    assert torch.nn.functional.cosine_similarity(a.flatten().double(), b.flatten().double(), dim=0).item() >= 0.9999
+
+
+@pytest.mark.parametrize("rows,L", [(13 * 1024, 1024), (3 * 64, 64), (40, 8)])
+def test_layernorm_fwd_pe_equals_ln_then_add_bcast(rows, L):
+    """s2h_layernorm_fwd_pe (norm4 + the next block's keys + key_pe, transformer.py:182-185, :170) gives
+    the bits of the LayerNorm launch followed by the broadcast add"""
+    from sam2_video.kernels import ops
+    from sam2_video.kernels._lib import call
+    torch.manual_seed(7)
+    C = 256
+    x = torch.randn(rows, C, device=DEV).to(torch.bfloat16)
+    pe = torch.randn(L, C, device=DEV).to(torch.bfloat16)
+    g = torch.randn(C, device=DEV)
+    b = torch.randn(C, device=DEV)
+    y = torch.empty_like(x)
+    k = torch.empty_like(x)
+    mean = torch.empty(rows, device=DEV)
+    rstd = torch.empty(rows, device=DEV)
+    call("s2h_layernorm_fwd_pe", 1, rows, C, x.data_ptr(), g.data_ptr(), b.data_ptr(), 1e-5, y.data_ptr(),
+         mean.data_ptr(), rstd.data_ptr(), pe.data_ptr(), L, k.data_ptr(), ops.stream())
+    ry, rm, rr = ops.layernorm_fwd(x, g, b, 1e-5)
+    rk = ops.add_bcast(ry.view(rows // L, L, C), pe)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ry) and torch.equal(mean, rm.view(-1)) and torch.equal(rstd, rr.view(-1))
+    assert torch.equal(k, rk.view(rows, C))
