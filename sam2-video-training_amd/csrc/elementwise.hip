@@ -1885,7 +1885,8 @@ extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const vo
 // torch.cat of the spatial memories and object pointers, sam2_base.py:649-676) and the tracking
 // loop's per-frame gradient packing, which otherwise cost one copy launch per bank entry / frame.
 // Segment s: rows[s] rows of row_bytes[s] bytes, source / destination pitches in bytes; every base,
-// pitch and row length a multiple of 16 B.  One lane per 16-B piece, grid-stride over the pieces
+// pitch and row length a multiple of 16 B; destination rows may not overlap, source rows may (a
+// source pitch of 0 broadcasts one row block: the decoder's learned tokens into every object).  One lane per 16-B piece, grid-stride over the pieces
 // of all segments (segment found by a scan of the <= 16 prefix offsets, uniform in most waves).
 constexpr int kCopySegs = 16;
 struct CopySegs {
@@ -1916,7 +1917,7 @@ extern "C" int s2h_copy2d_batch(int n, const void* const* src, void* const* dst,
   a.start[0] = 0;
   for (int s = 0; s < n; ++s) {
     if (!al16(src[s]) || !al16(dst[s]) || rows[s] < 0 || row_bytes[s] <= 0 || row_bytes[s] % 16 ||
-        src_ld[s] % 16 || dst_ld[s] % 16 || (rows[s] > 1 && (src_ld[s] < row_bytes[s] || dst_ld[s] < row_bytes[s])))
+        src_ld[s] % 16 || dst_ld[s] % 16 || src_ld[s] < 0 || (rows[s] > 1 && dst_ld[s] < row_bytes[s]))
       return (int)hipErrorInvalidValue;
     const int64_t pieces = rows[s] * (row_bytes[s] / 16);
     if (pieces >= (1ll << 32)) return (int)hipErrorInvalidValue;

@@ -1218,6 +1218,36 @@ def select_token(tape: FrameTape, x, i):
     return out
 
 
+def select_tokens_ok(x):
+    """select_tokens applies: 16-B aligned token rows (ops.copy_segments' batched 2-D copies)"""
+    return (os.environ.get("S2H_SELECT_N", "1") != "0" and x.dim() == 3 and x.is_contiguous()
+            and (x.shape[-1] * x.element_size()) % 16 == 0 and x.data_ptr() % 16 == 0)
+
+
+def select_tokens(tape: FrameTape, x, idxs):
+    """x [B, N, C] -> [x[:, i] for i in idxs] (contiguous copies) as one op: one batched copy launch
+    forward (ops.copy_segments), one zero fill + one batched copy backward"""
+    op, first = tape._begin("select_n", [x], _select_n_bw, {"idxs": tuple(idxs), "shape": tuple(x.shape)})
+    B, N, C = x.shape
+    vids, outs = [], []
+    for j in range(len(idxs)):
+        vid, out = tape._out(j, (B, C), x.dtype)
+        vids.append(vid)
+        outs.append(out)
+    ops.copy_segments([(x[:, i], out) for i, out in zip(idxs, outs)])
+    tape._finish(op, vids, any(op.needs))
+    return outs
+
+
+def _select_n_bw(tape, op, gys):
+    B, N, C = op.attrs["shape"]
+    ref = next(g for g in gys if g is not None)
+    d = torch.zeros(tape.F * B, N, C, device=ref.device, dtype=ref.dtype)
+    ops.copy_segments([(g.contiguous().view(tape.F * B, C), d[:, i]) for i, g in zip(op.attrs["idxs"], gys)
+                       if g is not None])
+    return [d.view(-1)]
+
+
 def _select_bw(tape, op, gys):
     (g,) = gys
     B, N, C = op.attrs["shape"]
@@ -1500,8 +1530,8 @@ def decoder_tokens(tape: FrameTape, sparse, dtype, params):
     head = torch.cat([p._s2h_compute.reshape(-1, C) for p in params], 0) if first else op.attrs["head"]
     nh = head.shape[0]
     vid, out = tape._out(0, (O, nh + Ns, C), dtype)
-    out[:, :nh].copy_(head.unsqueeze(0).expand(O, -1, -1))
-    out[:, nh:].copy_(sparse)
+    # the learned tokens (broadcast over the objects: source pitch 0) and the prompt rows, one launch
+    ops.copy_segments([(head.unsqueeze(0).expand(O, -1, -1), out[:, :nh]), (sparse, out[:, nh:])])
     if first:
         op.attrs.update(head=head, nh=nh, Ns=Ns, C=C, O=O)
     tape._finish(op, [vid], any(op.needs) or any(_grad_of(p) is not None for p in params))

@@ -982,3 +982,11 @@ def select_token(x, i):
     if T is not None:
         return _ft.select_token(T, x, int(i))
     return _SelectToken.apply(x, int(i))
+
+
+def select_tokens(x, idxs):
+    """[select_token(x, i) for i in idxs]; on the frame tape one op and one copy launch"""
+    T = _ft.active()
+    if T is not None and _ft.select_tokens_ok(x):
+        return _ft.select_tokens(T, x, [int(i) for i in idxs])
+    return [select_token(x, i) for i in idxs]

@@ -935,7 +935,7 @@ def copy_segments(pairs):
     for src, dst in pairs:
         r = _pair_rows(src, dst) if src.is_cuda and dst.is_cuda else None
         if r is None or src.numel() == 0 or any(v % 16 for v in r[1:]) or src.data_ptr() % 16 or dst.data_ptr() % 16 \
-                or (r[0] > 1 and min(r[2], r[3]) < r[1]):  # broadcast / overlapping rows
+                or (r[0] > 1 and r[3] < r[1]):  # overlapping destination rows (a source pitch of 0 broadcasts)
             dst.copy_(src)
             continue
         segs.append((src.data_ptr(), dst.data_ptr()) + r)

@@ -98,8 +98,7 @@ class MaskDecoder(nn.Module):
         else:  # mask-prompt dense embedding [O, h*w, C]
             src = FN.add(image_embeddings, dense)
         hs, src = self.transformer(src, image_pe_table, tokens)
-        iou_token_out = FN.select_token(hs, 1)
-        mask_token0 = FN.select_token(hs, 2)
+        iou_token_out, mask_token0 = FN.select_tokens(hs, (1, 2))
         feat_s0, feat_s1 = high_res_features
         dc1, ln1, _, dc2, _ = self.output_upscaling
         u = src.view(O, h, w, C)

@@ -64,3 +64,30 @@ def test_copy_segments_ragged_and_many():
     ops.copy_segments(pairs)
     torch.cuda.synchronize()
     assert torch.equal(dst, ref)
+
+
+def test_pair_rows_broadcast_source():
+    """the decoder's learned tokens broadcast over the objects: a 2-D copy with source pitch 0"""
+    ops = _ops()
+    head = torch.empty(6, 256, dtype=torch.bfloat16)
+    out = torch.empty(13, 8, 256, dtype=torch.bfloat16)
+    assert ops._pair_rows(head.unsqueeze(0).expand(13, -1, -1), out[:, :6]) == (13, 6 * 512, 0, 8 * 512)
+
+
+@pytest.mark.gpu
+def test_copy_segments_broadcast_and_token_rows():
+    """decoder_tokens' two copies (learned tokens to every object, source pitch 0; the prompt rows)
+    and select_tokens' strided token reads in one launch each, bit-identical to Tensor.copy_"""
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(5)
+    O, nh, Ns, C = 13, 6, 2, 256
+    head = torch.randn(nh, C, device="cuda", generator=g).bfloat16()
+    sparse = torch.randn(O, Ns, C, device="cuda", generator=g).bfloat16()
+    out = torch.full((O, nh + Ns, C), float("nan"), device="cuda", dtype=torch.bfloat16)
+    ops.copy_segments([(head.unsqueeze(0).expand(O, -1, -1), out[:, :nh]), (sparse, out[:, nh:])])
+    ref = torch.cat([head.unsqueeze(0).expand(O, -1, -1), sparse], 1)
+    toks = [torch.empty(O, C, device="cuda", dtype=torch.bfloat16) for _ in range(2)]
+    ops.copy_segments([(out[:, 1], toks[0]), (out[:, 2], toks[1])])
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref)
+    assert torch.equal(toks[0], ref[:, 1]) and torch.equal(toks[1], ref[:, 2])
