@@ -1555,13 +1555,14 @@ def _tokens_bw(tape, op, gys):
     return [dsp]
 
 
-def memory_pos(tape: FrameTape, tpos_p, obj_pos, spatial_pos, tpos_idx, L, dtype):
+def memory_pos(tape: FrameTape, tpos_p, obj_pos, spatial_pos, tpos_idx, L, dtype, obj_rep=1):
     """memory positional table of this frame (sam2_base.py:597-674): spatial pos +
-    maskmem_tpos_enc[tpos_idx[j]] per memory slot, then the object-pointer rows (constant)"""
+    maskmem_tpos_enc[tpos_idx[j]] per memory slot, then the object-pointer rows (constant; obj_rep > 1:
+    one row per pointer, written into its obj_rep rows -- the repeat_interleave -- by one batched copy)"""
     op, first = tape._begin("memory_pos", [], _mpos_bw, {"tpos_p": tpos_p, "L": L})
     n = len(tpos_idx)
     Dm = spatial_pos.shape[-1]
-    M = n * L + (obj_pos.shape[0] if obj_pos is not None else 0)
+    M = n * L + (obj_pos.shape[0] * obj_rep if obj_pos is not None else 0)
     tpos = tpos_p._s2h_compute.reshape(-1, Dm)
     if tpos.dtype != dtype:
         tpos = ops.cast(tpos.contiguous(), dtype)
@@ -1572,7 +1573,10 @@ def memory_pos(tape: FrameTape, tpos_p, obj_pos, spatial_pos, tpos_idx, L, dtype
     else:
         for j, ti in enumerate(tpos_idx):
             ops.add_bcast(spatial_pos, tpos[ti], out=out[j * L:(j + 1) * L])
-    if obj_pos is not None:
+    if obj_pos is not None and obj_rep > 1:
+        dst = out[n * L:].view(obj_pos.shape[0], obj_rep, Dm)
+        ops.copy_segments([(obj_pos, dst[:, j]) for j in range(obj_rep)])
+    elif obj_pos is not None:
         out[n * L:].copy_(obj_pos)
     tape._fattr(op, "tpos_idx", list(tpos_idx))
     tape._finish(op, [vid], _grad_of(tpos_p) is not None)

@@ -322,10 +322,13 @@ class _MemoryPos(torch.autograd.Function):
         return None, dobj, None, None, None, None
 
 
-def memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype):
+def memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype, obj_rep=1):
+    """obj_rep > 1: obj_pos holds one row per object pointer, each repeated obj_rep times"""
     T = _ft.active()
     if T is not None:
-        return _ft.memory_pos(T, tpos_param, obj_pos, spatial_pos, list(tpos_idx), int(L), dtype)
+        return _ft.memory_pos(T, tpos_param, obj_pos, spatial_pos, list(tpos_idx), int(L), dtype, obj_rep)
+    if obj_pos is not None and obj_rep > 1:
+        obj_pos = obj_pos.repeat_interleave(obj_rep, dim=0)
     return _MemoryPos.apply(tpos_param, obj_pos, spatial_pos, list(tpos_idx), int(L), dtype)
 
 

@@ -169,9 +169,10 @@ class SAM2Base(nn.Module):
         return out
 
     # ------------------------------------------------------- memory bank
-    def _obj_pos_table(self, pos_list, max_ptr, dtype, device):
+    def _obj_pos_table(self, pos_list, max_ptr, dtype, device, repeat=True):
         """temporal encoding of object pointers (sam2_base.py:655-672): sine of the signed frame
-        distance / (max_ptr - 1), projected to mem_dim, repeated for the C/mem_dim pointer tokens"""
+        distance / (max_ptr - 1), projected to mem_dim, repeated for the C/mem_dim pointer tokens
+        (repeat=False: one row per pointer, the consumer repeats)"""
         key = (tuple(pos_list), max_ptr, dtype, str(device))
         pe = self._tpos_cache.get(key) if hasattr(self, "_tpos_cache") else None
         if pe is None:
@@ -182,7 +183,7 @@ class SAM2Base(nn.Module):
                 self._tpos_cache = {}
             self._tpos_cache[key] = pe
         op = self.obj_ptr_tpos_proj(pe)  # [n_ptr, mem_dim]
-        return op.repeat_interleave(self.hidden_dim // self.mem_dim, dim=0)
+        return op.repeat_interleave(self.hidden_dim // self.mem_dim, dim=0) if repeat else op
 
     def _memory_selection(self, frame_idx, num_frames, cond_keys, non_cond_keys, track_in_reverse=False):
         """which bank entries frame `frame_idx` attends to (sam2_base.py:549-647, training order):
@@ -251,23 +252,29 @@ class SAM2Base(nn.Module):
         n_ptr_tok = len(ptrs) * (C // self.mem_dim)
         if not ptrs:  # eval, tracking away from every conditioning frame (sam2_base.py:677)
             raise NotImplementedError("memory attention without object-pointer tokens")
-        ptr_tokens = torch.stack(ptrs, dim=1).reshape(num_objects, n_ptr_tok, self.mem_dim)
         if tape is not None:
             if self.obj_ptr_tpos_proj.weight.requires_grad:
                 raise NotImplementedError("frame-batched backward with a trainable obj_ptr_tpos_proj")
-            with torch.no_grad():
-                obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device)
+            with torch.no_grad():  # one row per pointer: the tape's memory_pos writes each into its k rows
+                obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device, repeat=False)
+            obj_rep = C // self.mem_dim
             M = sum(f.shape[1] for f in feats) + n_ptr_tok
             memory = tape.varlen_slot("memory", (num_objects, M, self.mem_dim), feat.dtype)
             r, pairs = 0, []
-            for f in feats + [ptr_tokens]:
+            for f in feats:
                 pairs.append((f, memory[:, r:r + f.shape[1]]))
                 r += f.shape[1]
+            k = C // self.mem_dim  # each pointer [O, C] fills k memory rows of mem_dim (the stack + reshape)
+            for i, ptr in enumerate(ptrs):
+                pairs.append((ptr, memory[:, r + k * i:r + k * (i + 1)].view(num_objects, C)))
             ops.copy_segments(pairs)  # one launch for the whole bank
         else:
             obj_pos = self._obj_pos_table(pos_list, max_ptr, feat.dtype, feat.device)
+            obj_rep = 1
+            ptr_tokens = torch.stack(ptrs, dim=1).reshape(num_objects, n_ptr_tok, self.mem_dim)
             memory = torch.cat(feats + [ptr_tokens], dim=1)
-        mpos = FN_memory_pos(self.maskmem_tpos_enc, obj_pos, spatial_pos, tpos_idx, spatial_pos.shape[0], feat.dtype)
+        mpos = FN_memory_pos(self.maskmem_tpos_enc, obj_pos, spatial_pos, tpos_idx, spatial_pos.shape[0], feat.dtype,
+                             obj_rep)
         return self.memory_attention(feat, pos, memory, mpos, num_obj_ptr_tokens=n_ptr_tok, num_objects=num_objects)
 
     # ------------------------------------------------------------ heads
@@ -349,9 +356,9 @@ class SAM2Base(nn.Module):
         return mfeat, mpos
 
 
-def FN_memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype):
+def FN_memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype, obj_rep=1):
     from ...kernels.functional_sam import memory_pos
-    return memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype)
+    return memory_pos(tpos_param, obj_pos, spatial_pos, tpos_idx, L, dtype, obj_rep)
 
 
 _ = math
