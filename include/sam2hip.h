@@ -480,7 +480,8 @@ int s2h_maxpool2_bwd(int dt, int B, int H, int W, int C, const void* x, int64_t 
  * assembly, reference sam2_base.py:649-676, and the tracking loop's per-frame gradient packing):
  * segment s copies rows[s] rows of row_bytes[s] bytes from src[s] (pitch src_ld[s] bytes) to dst[s]
  * (pitch dst_ld[s]; destination rows must not overlap, a source pitch of 0 broadcasts).  Host arrays
- * of n entries; bases, pitches and row lengths 16-B aligned, else hipErrorInvalidValue. */
+ * of n entries; bases, pitches and row lengths 4-B aligned (16-B aligned segments move in 16-B
+ * pieces), else hipErrorInvalidValue. */
 int s2h_copy2d_batch(int n, const void* const* src, void* const* dst, const int64_t* rows, const int64_t* row_bytes,
                      const int64_t* src_ld, const int64_t* dst_ld, hipStream_t st);
 /* window_partition (dir 0) / window_unpartition (dir 1) with zero padding

@@ -1885,16 +1885,19 @@ extern "C" int s2h_colsum_seg(int dt, int nseg, int64_t rows, int cols, const vo
 // torch.cat of the spatial memories and object pointers, sam2_base.py:649-676) and the tracking
 // loop's per-frame gradient packing, which otherwise cost one copy launch per bank entry / frame.
 // Segment s: rows[s] rows of row_bytes[s] bytes, source / destination pitches in bytes; every base,
-// pitch and row length a multiple of 16 B; destination rows may not overlap, source rows may (a
-// source pitch of 0 broadcasts one row block: the decoder's learned tokens into every object).  One lane per 16-B piece, grid-stride over the pieces
-// of all segments (segment found by a scan of the <= 16 prefix offsets, uniform in most waves).
+// pitch and row length a multiple of 16 B (16-B pieces) or of 4 B (4-B pieces: the per-frame IoU
+// gradients of the tracking loop, 13 floats); destination rows may not overlap, source rows may (a
+// source pitch of 0 broadcasts one row block: the decoder's learned tokens into every object).
+// One lane per piece, grid-stride over the pieces of all segments (segment found by a scan of the
+// <= 16 prefix offsets, uniform in most waves).
 constexpr int kCopySegs = 16;
 struct CopySegs {
-  const uint4* src[kCopySegs];
-  uint4* dst[kCopySegs];
+  const char* src[kCopySegs];
+  char* dst[kCopySegs];
   int64_t start[kCopySegs + 1];  // first piece of each segment
-  int64_t src_ld[kCopySegs], dst_ld[kCopySegs];  // pitches in 16-B pieces
+  int64_t src_ld[kCopySegs], dst_ld[kCopySegs];  // pitches in bytes
   uint32_t row_pieces[kCopySegs];
+  int shift[kCopySegs];  // log2 of the segment's piece size: 4 (16 B) or 2 (4 B)
   int n;
 };
 __global__ __launch_bounds__(256) void copy_segs_kernel(CopySegs a) {
@@ -1904,7 +1907,11 @@ __global__ __launch_bounds__(256) void copy_segs_kernel(CopySegs a) {
     while (s + 1 < a.n && i >= a.start[s + 1]) ++s;
     const uint32_t c = (uint32_t)(i - a.start[s]);
     const uint32_t r = c / a.row_pieces[s], col = c - r * a.row_pieces[s];
-    a.dst[s][(int64_t)r * a.dst_ld[s] + col] = a.src[s][(int64_t)r * a.src_ld[s] + col];
+    const int sh = a.shift[s];
+    const char* sp = a.src[s] + (int64_t)r * a.src_ld[s] + ((int64_t)col << sh);
+    char* dp = a.dst[s] + (int64_t)r * a.dst_ld[s] + ((int64_t)col << sh);
+    if (sh == 4) *(uint4*)dp = *(const uint4*)sp;
+    else *(uint32_t*)dp = *(const uint32_t*)sp;
   }
 }
 extern "C" int s2h_copy2d_batch(int n, const void* const* src, void* const* dst, const int64_t* rows,
@@ -1915,17 +1922,22 @@ extern "C" int s2h_copy2d_batch(int n, const void* const* src, void* const* dst,
   CopySegs a = {};
   a.n = n;
   a.start[0] = 0;
+  auto al = [](int64_t v, int64_t m) { return v % m == 0; };
   for (int s = 0; s < n; ++s) {
-    if (!al16(src[s]) || !al16(dst[s]) || rows[s] < 0 || row_bytes[s] <= 0 || row_bytes[s] % 16 ||
-        src_ld[s] % 16 || dst_ld[s] % 16 || src_ld[s] < 0 || (rows[s] > 1 && dst_ld[s] < row_bytes[s]))
+    const bool v16 = al16(src[s]) && al16(dst[s]) && al(row_bytes[s], 16) && al(src_ld[s], 16) && al(dst_ld[s], 16);
+    const bool v4 = ((uintptr_t)src[s] & 3) == 0 && ((uintptr_t)dst[s] & 3) == 0 && al(row_bytes[s], 4) &&
+                    al(src_ld[s], 4) && al(dst_ld[s], 4);
+    if ((!v16 && !v4) || rows[s] < 0 || row_bytes[s] <= 0 || src_ld[s] < 0 ||
+        (rows[s] > 1 && dst_ld[s] < row_bytes[s]))
       return (int)hipErrorInvalidValue;
-    const int64_t pieces = rows[s] * (row_bytes[s] / 16);
+    a.shift[s] = v16 ? 4 : 2;
+    const int64_t pieces = rows[s] * (row_bytes[s] >> a.shift[s]);
     if (pieces >= (1ll << 32)) return (int)hipErrorInvalidValue;
-    a.src[s] = (const uint4*)src[s];
-    a.dst[s] = (uint4*)dst[s];
-    a.row_pieces[s] = (uint32_t)(row_bytes[s] / 16);
-    a.src_ld[s] = src_ld[s] / 16;
-    a.dst_ld[s] = dst_ld[s] / 16;
+    a.src[s] = (const char*)src[s];
+    a.dst[s] = (char*)dst[s];
+    a.row_pieces[s] = (uint32_t)(row_bytes[s] >> a.shift[s]);
+    a.src_ld[s] = src_ld[s];
+    a.dst_ld[s] = dst_ld[s];
     a.start[s + 1] = a.start[s] + pieces;
   }
   if (a.start[n] == 0) return 0;

@@ -1428,10 +1428,16 @@ def _point_embed_bw(tape, op, gys):
     (g,) = gys
     D = op.attrs["D"]
     labels = tape.stores[("aux", op.idx, "labels")].buf
-    dtable = torch.zeros(len(op.attrs["tables"]), D, device=g.device)
+    gps = [_grad_of(p) for p in op.attrs["tables"]]
+    n = len(gps)
+    if all(gp is not None and gp.dtype == torch.float32 and gp.is_contiguous() and gp.numel() == D for gp in gps) \
+            and all(gps[i].data_ptr() == gps[0].data_ptr() + 4 * D * i for i in range(n)):
+        # the label embeddings' gradients are consecutive rows of the arena: accumulate straight into them
+        ops.point_embed_bwd(labels, g.contiguous().view(-1, D), torch.as_strided(gps[0], (n, D), (D, 1)))
+        return []
+    dtable = torch.zeros(n, D, device=g.device)
     ops.point_embed_bwd(labels, g.contiguous().view(-1, D), dtable)
-    for i, p in enumerate(op.attrs["tables"]):
-        gp = _grad_of(p)
+    for i, gp in enumerate(gps):
         if gp is not None:
             ops.add(gp.view(-1), dtable[i], out=gp.view(-1))
     return []

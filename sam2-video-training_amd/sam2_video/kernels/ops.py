@@ -925,7 +925,8 @@ def _pair_rows(src, dst):
 def copy_segments(pairs):
     """dst.copy_(src) for every (src, dst) pair, up to 16 pairs per launch (s2h_copy2d_batch): the
     memory bank assembly of a tracked frame (sam2_base.py:649-676) and the tracking loop's gradient
-    packing.  A pair whose layout is not a 16-B aligned 2-D copy goes through Tensor.copy_."""
+    packing.  A pair whose layout is not a 4-B aligned 2-D copy goes through Tensor.copy_ (16-B
+    aligned pairs move in 16-B pieces, the rest in 4-B pieces)."""
     import ctypes
     if not _COPY_BATCH:
         for src, dst in pairs:
@@ -934,7 +935,7 @@ def copy_segments(pairs):
     segs = []
     for src, dst in pairs:
         r = _pair_rows(src, dst) if src.is_cuda and dst.is_cuda else None
-        if r is None or src.numel() == 0 or any(v % 16 for v in r[1:]) or src.data_ptr() % 16 or dst.data_ptr() % 16 \
+        if r is None or src.numel() == 0 or any(v % 4 for v in r[1:]) or src.data_ptr() % 4 or dst.data_ptr() % 4 \
                 or (r[0] > 1 and r[3] < r[1]):  # overlapping destination rows (a source pitch of 0 broadcasts)
             dst.copy_(src)
             continue

@@ -1,7 +1,7 @@
 """ops.copy_segments (s2h_copy2d_batch): the memory bank assembly and gradient packing copies in one
 launch.  Host: the 2-D reduction of (src, dst) layouts.  GPU: bit-identical to Tensor.copy_ for the
-step's layouts (bank rows into a packed [O, M, C] buffer, flat gradient slices), ragged / misaligned
-pairs through the Tensor.copy_ path, more than 16 pairs split over launches."""
+step's layouts (bank rows into a packed [O, M, C] buffer, flat gradient slices), ragged pairs in 4-B
+pieces, 2-B ragged pairs through the Tensor.copy_ path, more than 16 pairs split over launches."""
 import pytest
 import torch
 
@@ -55,7 +55,7 @@ def test_copy_segments_ragged_and_many():
     dst = torch.zeros(40000, device="cuda", dtype=torch.float32)
     ref = dst.clone()
     pairs, off = [], 0
-    for i in range(21):  # > 16 pairs: two launches; sizes not multiples of 4 floats -> copy_ path
+    for i in range(21):  # > 16 pairs: two launches; sizes not multiples of 4 floats -> 4-B pieces
         n = 96 * (i + 1) + (3 if i % 5 == 4 else 0)
         src = torch.randn(n, device="cuda", generator=g)
         pairs.append((src, dst[off:off + n]))
@@ -91,3 +91,17 @@ def test_copy_segments_broadcast_and_token_rows():
     torch.cuda.synchronize()
     assert torch.equal(out, ref)
     assert torch.equal(toks[0], ref[:, 1]) and torch.equal(toks[1], ref[:, 2])
+
+
+@pytest.mark.gpu
+def test_copy_segments_odd_bf16_falls_back():
+    """a bf16 pair of odd length (not a 4-B multiple) goes through Tensor.copy_, beside batched pairs"""
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(9)
+    a = torch.randn(13, device="cuda", generator=g).bfloat16()
+    b = torch.randn(13, 1, device="cuda", generator=g)  # 52 B: 4-B pieces
+    da = torch.zeros(13, device="cuda", dtype=torch.bfloat16)
+    db = torch.zeros(13, 1, device="cuda")
+    ops.copy_segments([(a, da), (b, db)])
+    torch.cuda.synchronize()
+    assert torch.equal(da, a) and torch.equal(db, b)
