@@ -467,6 +467,52 @@ def frame_loss(logits, ious, tgt, valid, weights=(20.0, 1.0, 1.0), temperature=1
     return _FrameLoss.apply(logits, ious, tgt, valid, tuple(float(w) for w in weights), 1.0 / float(temperature))
 
 
+class _ClipLoss(torch.autograd.Function):
+    """_FrameLoss of every frame of a clip summed (losses.py:111-121) as one node: the frames'
+    finalize launches accumulate into one [4] buffer (the same fp32 additions in the same order as
+    the per-frame buffers and their adds, without the per-frame zero fills and adds); the backward
+    runs the per-frame gradient launches with the shared upstream gradient"""
+
+    @staticmethod
+    def forward(ctx, weights, inv_temp, n, *args):
+        losses = None
+        saved, shapes = [], []
+        for f in range(n):
+            logits, ious, tgt = args[3 * f:3 * f + 3]
+            N = logits.shape[0]
+            x = logits.reshape(N, -1)
+            t = tgt.reshape(N, -1).view(torch.uint8)
+            if losses is None:
+                losses = torch.zeros(4, device=x.device)
+            stats = ops.mask_stats(x, t, inv_temp)
+            coef = torch.empty(N, 4, device=x.device)
+            ops.mask_loss_finalize(stats, ious.reshape(N).contiguous(), None, x.shape[1], weights, 1.0, losses, coef)
+            saved += [x, t, coef]
+            shapes.append(logits.shape)
+        ctx.save_for_backward(*saved)
+        ctx.inv_temp, ctx.shapes, ctx.n = inv_temp, shapes, n
+        return losses
+
+    @staticmethod
+    def backward(ctx, g):
+        sv = ctx.saved_tensors
+        gc = g.contiguous()
+        grads = [None, None, None]
+        for f in range(ctx.n):
+            x, t, coef = sv[3 * f:3 * f + 3]
+            dx = torch.empty_like(x)
+            dious = torch.empty(x.shape[0], 1, device=x.device)
+            ops.mask_loss_bwd(x, t, coef, ctx.inv_temp, dx, gtot=gc, dious=dious)
+            grads += [dx.view(ctx.shapes[f]), dious, None]
+        return tuple(grads)
+
+
+def clip_loss(frames, weights=(20.0, 1.0, 1.0), temperature=1.0):
+    """sum over frames of frame_loss(logits, ious, tgt, None) for frames = [(logits, ious, tgt), ...]"""
+    flat = [t for fr in frames for t in fr]
+    return _ClipLoss.apply(tuple(float(w) for w in weights), 1.0 / float(temperature), len(frames), *flat)
+
+
 class _BCEFrame(torch.autograd.Function):
     """one frame of BCECategoryLoss (losses.py:306-366): BCE-with-logits over the categories with
     ground truth, reduced and scaled by 1/num_frames; accumulates into `acc` [1] f32"""

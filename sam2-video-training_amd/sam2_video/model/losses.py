@@ -15,7 +15,7 @@ import torch
 from torch import nn
 
 from ..kernels import functional as FN
-from ..kernels.functional_sam import bce_frame_loss, frame_loss
+from ..kernels.functional_sam import bce_frame_loss, clip_loss
 
 CORE_LOSS_KEY = "total_loss"
 
@@ -43,12 +43,10 @@ class MultiStepMultiMasksAndIous(nn.Module):
         assert len(outs_batch) == len(targets_batch)
         w = (float(self.weight_dict["loss_mask"]), float(self.weight_dict["loss_dice"]),
              float(self.weight_dict["loss_iou"]))
-        acc = None
-        for outs, targets in zip(outs_batch, targets_batch):
-            src = outs["multistep_pred_multimasks_high_res"][0]
-            ious = outs["multistep_pred_ious"][0]
-            lt = frame_loss(src, ious, targets.contiguous(), None, w, self.logit_temperature)
-            acc = lt if acc is None else FN.add(acc, lt)
+        # every frame's losses accumulated into one buffer by one autograd node (FN clip_loss)
+        acc = clip_loss([(outs["multistep_pred_multimasks_high_res"][0], outs["multistep_pred_ious"][0],
+                          targets.contiguous()) for outs, targets in zip(outs_batch, targets_batch)],
+                        w, self.logit_temperature)
         losses = {"loss_mask": acc[0], "loss_dice": acc[1], "loss_iou": acc[2],
                   "loss_class": torch.zeros((), device=acc.device), CORE_LOSS_KEY: acc[3]}
         return losses
