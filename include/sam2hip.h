@@ -566,6 +566,10 @@ int s2h_convt2_ln_gelu(int dt, int B, int H, int W, int Co, const void* Y, const
  * NO_OBJ_SCORE, sam2_base.py:380-389). */
 int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, float fill,
                  void* y, int dir, hipStream_t st);
+/* s2h_row_gate with input type dt_in and output type dt_out (the low-res mask logits' cast to fp32
+ * fused with the gate; its backward back to bf16); gate_out (nullable): gate[0:rows] copied. */
+int s2h_row_gate_cast(int dt_in, int dt_out, int64_t rows, int64_t inner, const void* x, const float* gate,
+                      float fill, void* y, int dir, float* gate_out, hipStream_t st);
 /* y = (scale_x ? g*x : x) + (1-g)*vec for g = (gate > 0) (obj_ptr / no_obj_ptr mix,
  * sam2_base.py:413-424; no_obj_embed_spatial sam2_base.py:761-767). */
 int s2h_gate_mix(int dt, int64_t rows, int64_t inner, const void* x, const float* gate, const void* vec,

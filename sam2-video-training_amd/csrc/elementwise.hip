@@ -1528,6 +1528,39 @@ extern "C" int s2h_row_gate(int dt, int64_t rows, int64_t inner, const void* x, 
   DISPATCH_T(dt, row_gate_kernel, ew_grid(rows * inner), rows, inner, x, gate, fill, y, dir);
   return (int)hipGetLastError();
 }
+// row_gate with its own input and output types: the low-res mask logits' cast to fp32 and the
+// object-score gate of sam2_base.py:380-389 in one pass (forward bf16 -> fp32; backward fp32 ->
+// bf16, dx = gate > 0 ? dy : 0); gate_out (nullable): the gate copied for the backward
+template <typename TI, typename TO>
+__global__ void row_gate_cast_kernel(int64_t rows, int64_t inner, const TI* x, const float* gate, float fill, TO* y,
+                                     int dir, float* gate_out) {
+  const int64_t n = rows * inner;
+  GRID_STRIDE(i, n) {
+    const bool on = gate[i / inner] > 0.f;
+    y[i] = from_f32<TO>(on ? to_f32(x[i]) : (dir == 0 ? fill : 0.f));
+    if (gate_out != nullptr && i < rows) gate_out[i] = gate[i];
+  }
+}
+extern "C" int s2h_row_gate_cast(int dt_in, int dt_out, int64_t rows, int64_t inner, const void* x, const float* gate,
+                                 float fill, void* y, int dir, float* gate_out, hipStream_t st) {
+  if (rows * inner <= 0) return 0;
+  const dim3 g = ew_grid(rows * inner);
+  if (dt_in == S2H_BF16 && dt_out == S2H_F32)
+    hipLaunchKernelGGL((row_gate_cast_kernel<bf16, float>), g, dim3(256), 0, st, rows, inner, (const bf16*)x, gate,
+                       fill, (float*)y, dir, gate_out);
+  else if (dt_in == S2H_F32 && dt_out == S2H_BF16)
+    hipLaunchKernelGGL((row_gate_cast_kernel<float, bf16>), g, dim3(256), 0, st, rows, inner, (const float*)x, gate,
+                       fill, (bf16*)y, dir, gate_out);
+  else if (dt_in == S2H_F32 && dt_out == S2H_F32)
+    hipLaunchKernelGGL((row_gate_cast_kernel<float, float>), g, dim3(256), 0, st, rows, inner, (const float*)x, gate,
+                       fill, (float*)y, dir, gate_out);
+  else if (dt_in == S2H_BF16 && dt_out == S2H_BF16)
+    hipLaunchKernelGGL((row_gate_cast_kernel<bf16, bf16>), g, dim3(256), 0, st, rows, inner, (const bf16*)x, gate,
+                       fill, (bf16*)y, dir, gate_out);
+  else
+    return (int)hipErrorInvalidValue;
+  return (int)hipGetLastError();
+}
 // y[r, j] = x[r, j] + (1 - (gate[r] > 0)) * vec[j]   (no-object embedding / pointer mixing)
 // if scale_x: y = (gate>0)*x + (1-(gate>0))*vec  (fixed_no_obj_ptr form)
 template <typename T>

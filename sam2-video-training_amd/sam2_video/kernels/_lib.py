@@ -118,6 +118,7 @@ SIGNATURES = {
     "s2h_convt2_tail": [I, I, I, I, I, P, P, P, I, P, P, P, P, P],
     "s2h_convt2_ln_gelu": [I, I, I, I, I, P, P, P, I, P, P, F, P, P, P, P, P, P],
     "s2h_row_gate": [I, L, L, P, P, F, P, I, P],
+    "s2h_row_gate_cast": [I, I, L, L, P, P, F, P, I, P, P],
     "s2h_gate_mix": [I, L, L, P, P, P, I, I, P, P],
     "s2h_mask_stats": [I, L, P, L, P, L, F, P, P],
     "s2h_mask_loss_finalize": [I, L, P, P, P, F, F, F, F, P, P, P],

@@ -1184,6 +1184,25 @@ def row_gate(tape: FrameTape, x, gate, fill):
     return out
 
 
+def cast_gate(tape: FrameTape, x, dtype, gate, fill):
+    """row_gate(cast(x, dtype), gate, fill) as one op and one launch (s2h_row_gate_cast, which also
+    saves the gate); backward: gate > 0 ? g : 0 cast back to x's dtype in one launch"""
+    x = x if x.is_contiguous() else x.contiguous()
+    op, first = tape._begin("cast_gate", [x], _cast_gate_bw, {"src": x.dtype})
+    vid, out = tape._out(0, x.shape, dtype)
+    gsave = tape._aux("gate", gate.shape, gate.dtype)
+    ops.row_gate_cast(x, gate, fill, dtype, out=out, gate_out=gsave)
+    tape._finish(op, [vid], any(op.needs))
+    return out
+
+
+def _cast_gate_bw(tape, op, gys):
+    (g,) = gys
+    gate = tape.stores[("aux", op.idx, "gate")].buf
+    R = gate.numel()
+    return [ops.row_gate_cast(g.contiguous().view(R, -1), gate, 0.0, op.attrs["src"], backward=True).view(-1)]
+
+
 def _row_gate_bw(tape, op, gys):
     (g,) = gys
     gate = tape.stores[("aux", op.idx, "gate")].buf

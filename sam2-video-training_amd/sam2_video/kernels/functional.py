@@ -13,6 +13,7 @@ torch provides allocation, views and the autograd tape.
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 
@@ -916,6 +917,15 @@ def row_gate(x, gate, fill):
     if T is not None:
         return _ft.row_gate(T, x, gate, float(fill))
     return _RowGate.apply(x, gate, float(fill))
+
+
+def cast_gate(x, dtype, gate, fill):
+    """row_gate(cast(x, dtype), gate, fill); on the frame tape one op and one launch"""
+    T = _ft.active()
+    if T is not None and x.dtype != dtype and os.environ.get("S2H_CAST_GATE", "1") != "0" \
+            and gate.dtype == torch.float32 and gate.is_contiguous() and gate.numel() == x.shape[0]:
+        return _ft.cast_gate(T, x, dtype, gate, float(fill))
+    return row_gate(cast(x, dtype), gate, fill)
 
 
 class _Cast(torch.autograd.Function):

@@ -1111,6 +1111,16 @@ def row_gate(x, gate, fill, out=None, backward=False):
     return out
 
 
+def row_gate_cast(x, gate, fill, dtype, out=None, backward=False, gate_out=None):
+    """row_gate with the output in `dtype` (s2h_row_gate_cast); gate_out: the gate copied beside it"""
+    rows = x.shape[0]
+    if out is None:
+        out = torch.empty(x.shape, device=x.device, dtype=dtype)
+    call("s2h_row_gate_cast", dt(x), dt(out), rows, x.numel() // rows, ptr(x), ptr(gate), float(fill), ptr(out),
+         int(backward), ptr(gate_out), stream())
+    return out
+
+
 def gate_mix(x, gate, vec, scale_x=False, out=None):
     rows = x.shape[0]
     if out is None:

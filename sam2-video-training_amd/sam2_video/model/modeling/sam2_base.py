@@ -301,8 +301,7 @@ class SAM2Base(nn.Module):
                                                   (self.obj_ptr_proj, token0.detach())])
                 score = ops.cast(score, torch.float32)
         score_flat = score.view(-1).contiguous()
-        low = FN.cast(masks, torch.float32)
-        low = FN.row_gate(low, score_flat, NO_OBJ_SCORE)
+        low = FN.cast_gate(masks, torch.float32, score_flat, NO_OBJ_SCORE)
         low = low.view(O, 4 * h, 4 * w)
         high = FN.bilinear(low, self.image_size, self.image_size)
         with torch.no_grad():

@@ -124,3 +124,20 @@ def test_layernorm_fwd_pe_equals_ln_then_add_bcast(rows, L):
     torch.cuda.synchronize()
     assert torch.equal(y, ry) and torch.equal(mean, rm.view(-1)) and torch.equal(rstd, rr.view(-1))
     assert torch.equal(k, rk.view(rows, C))
+
+
+def test_row_gate_cast_equals_cast_then_gate():
+    """s2h_row_gate_cast (the low-res mask logits' fp32 cast + object-score gate, sam2_base.py:380-389):
+    the bits of ops.cast + ops.row_gate forward, and of the gated gradient cast back to bf16"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(8)
+    x = torch.randn(13, 65536, device=DEV).to(torch.bfloat16)
+    gate = torch.randn(13, device=DEV)
+    gsave = torch.empty_like(gate)
+    y = ops.row_gate_cast(x, gate, -1024.0, torch.float32, gate_out=gsave)
+    ref = ops.row_gate(ops.cast(x, torch.float32), gate, -1024.0)
+    g = torch.randn(13, 65536, device=DEV)
+    dx = ops.row_gate_cast(g, gate, 0.0, torch.bfloat16, backward=True)
+    rdx = ops.cast(ops.row_gate(g, gate, 0.0, backward=True), torch.bfloat16)
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref) and torch.equal(gsave, gate) and torch.equal(dx, rdx)
