@@ -581,9 +581,10 @@ int s2h_pos_embed(int dt, int C, int h, int w, int ws, const float* Y, const flo
 int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void* dout, float* dY, float* dwin,
                       hipStream_t st);
 /* Point prompt embedding: out[r] = pe[r] + table[label[r] + 1] (label -1 = pad:
- * table row 0 = not_a_point_embed, pe zeroed), prompt_encoder.py:79-104. */
+ * table row 0 = not_a_point_embed, pe zeroed), prompt_encoder.py:79-104; labels_out (nullable):
+ * the labels copied (kept for the backward). */
 int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
-                    hipStream_t st);
+                    int* labels_out, hipStream_t st);
 int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, const void* dout, float* dtable, hipStream_t st);
 
 /* ---------------------------------------------------------------- loss + category merge

@@ -1664,14 +1664,17 @@ extern "C" int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void
 // ------------------------------------------------ point-prompt embeddings
 // out[r, :] = pe[r, :] * (label != -1) + table[label + 1, :]   (table rows: not_a_point, pe0..pe3)
 // backward: dtable[label + 1, :] += dout[r, :]  (f32, serial over rows -> deterministic)
+// labels_out (nullable): the labels copied (the frame tape keeps them for the backward)
 template <typename T>
-__global__ void point_embed_kernel(int R, int D, const float* pe, const int* labels, const void* table, void* out) {
+__global__ void point_embed_kernel(int R, int D, const float* pe, const int* labels, const void* table, void* out,
+                                   int* labels_out) {
   const int64_t n = (int64_t)R * D;
   GRID_STRIDE(i, n) {
     const int r = i / D, d = i % D;
     const int l = labels[r];
     float v = (l == -1 ? 0.f : pe[i]) + to_f32(((const T*)table)[(l + 1) * D + d]);
     ((T*)out)[i] = from_f32<T>(v);
+    if (labels_out != nullptr && d == 0) labels_out[r] = l;
   }
 }
 // one thread per column; the 5 label rows' sums in registers in row order (the same additions, in the
@@ -1696,9 +1699,9 @@ __global__ void point_embed_bwd_kernel(int R, int D, const int* labels, const vo
   for (int k = 0; k < 5; ++k) dtable[k * D + d] = acc[k];
 }
 extern "C" int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
-                               hipStream_t st) {
+                               int* labels_out, hipStream_t st) {
   if (R * D <= 0) return 0;
-  DISPATCH_T(dt, point_embed_kernel, ew_grid((int64_t)R * D), R, D, pe, labels, table, out);
+  DISPATCH_T(dt, point_embed_kernel, ew_grid((int64_t)R * D), R, D, pe, labels, table, out, labels_out);
   return (int)hipGetLastError();
 }
 extern "C" int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, const void* dout, float* dtable,

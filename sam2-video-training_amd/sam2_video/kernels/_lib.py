@@ -136,7 +136,7 @@ SIGNATURES = {
     "s2h_adamw": [L, P, P, P, P, P, F, F, F, F, F, I, P, P],
     "s2h_pos_embed": [I, I, I, I, I, P, P, P, P],
     "s2h_pos_embed_bwd": [I, I, I, I, I, P, P, P, P],
-    "s2h_point_embed": [I, I, I, P, P, P, P, P],
+    "s2h_point_embed": [I, I, I, P, P, P, P, P, P],
     "s2h_point_embed_bwd": [I, I, I, P, P, P, P],
     "s2h_prof_enable": [I],
     "s2h_prof_select": [I],

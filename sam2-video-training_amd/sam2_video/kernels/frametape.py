@@ -1433,9 +1433,12 @@ def point_embed(tape: FrameTape, pe, labels, dtype, tables):
     table = torch.cat([p._s2h_compute.reshape(1, -1) for p in tables], 0).contiguous() if first else \
         op.attrs["table"]
     vid, out = tape._out(0, pe.shape, dtype)
-    ops.point_embed(pe.reshape(R, D), labels.reshape(R), table, out.view(R, D))
     lab = tape._aux("labels", (R,), labels.dtype)
-    lab.copy_(labels.reshape(R))
+    if labels.dtype == torch.int32 and labels.is_contiguous():  # the kernel copies them beside the embedding
+        ops.point_embed(pe.reshape(R, D), labels.reshape(R), table, out.view(R, D), labels_out=lab)
+    else:
+        ops.point_embed(pe.reshape(R, D), labels.reshape(R), table, out.view(R, D))
+        lab.copy_(labels.reshape(R))
     if first:
         op.attrs["table"] = table
         op.attrs["D"] = D

@@ -1234,9 +1234,10 @@ def pos_embed_bwd(dout, dY, dwin, ws):
     call("s2h_pos_embed_bwd", dt(dout), C, h, w, ws, ptr(dout), ptr(dY), ptr(dwin), stream())
 
 
-def point_embed(pe, labels, table, out):
+def point_embed(pe, labels, table, out, labels_out=None):
     R, D = pe.shape
-    call("s2h_point_embed", dt(out), R, D, ptr(pe), ptr(labels), ptr(table), ptr(out), stream())
+    assert labels_out is None or (labels_out.dtype == torch.int32 and labels_out.numel() == R)
+    call("s2h_point_embed", dt(out), R, D, ptr(pe), ptr(labels), ptr(table), ptr(out), ptr(labels_out), stream())
     return out
 
 
