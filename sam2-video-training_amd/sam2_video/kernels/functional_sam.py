@@ -399,10 +399,11 @@ class _MergeMasksScores(torch.autograd.Function):
         ops.group_wavg(s.contiguous(), stats, cat_off, cat_obj, ncat, sout)
         ctx.save_for_backward(arg, s, hr, stats, sout, obj_cat, cat_off)
         ctx.shape = hr.shape
-        return out, sout
+        ctx.mark_non_differentiable(stats)
+        return out, sout, stats
 
     @staticmethod
-    def backward(ctx, g, gs):
+    def backward(ctx, g, gs, _gstats):
         arg, s, hr, stats, sout, obj_cat, cat_off = ctx.saved_tensors
         O = ctx.shape[0]
         dx = torch.empty(ctx.shape, device=hr.device, dtype=torch.float32)
@@ -424,8 +425,16 @@ def merge_masks(x, groups):
 
 
 def merge_masks_scores(hr, s, groups):
-    """(merge_masks(hr), merge_scores(s, hr)) as one autograd node"""
+    """(merge_masks(hr), merge_scores(s, hr), the per-object statistics of hr the weights come from) as
+    one autograd node"""
     return _MergeMasksScores.apply(hr, s, groups.cat_off, groups.cat_obj, groups.obj_cat, groups.ncat)
+
+
+def merge_scores_stats(s, stats, groups):
+    """merge_scores(s, hr) without gradient, from hr's statistics already computed (merge_masks_scores)"""
+    out = torch.empty(groups.ncat, s.shape[1], device=s.device, dtype=torch.float32)
+    ops.group_wavg(s.contiguous(), stats, groups.cat_off, groups.cat_obj, groups.ncat, out)
+    return out
 
 
 def merge_scores(s, hr, groups):

@@ -117,7 +117,7 @@ class CategoryGroups:
 def merge_object_results_to_category(previous_stages_out: List[Dict[str, Any]], obj_to_cat: List[int],
                                      num_categories: int) -> List[Dict[str, Any]]:
     """masks.py:53-213 for the per-frame outputs of forward_tracking."""
-    from ..kernels.functional_sam import merge_masks, merge_masks_scores, merge_scores
+    from ..kernels.functional_sam import merge_masks, merge_masks_scores, merge_scores_stats
 
     if not previous_stages_out:
         return []
@@ -131,7 +131,7 @@ def merge_object_results_to_category(previous_stages_out: List[Dict[str, Any]], 
         hr = fo["pred_masks_high_res"]
         m = {}
         # the high-res masks and the IoU scores weighted by them as one autograd node
-        m["pred_masks_high_res"], merged_ious = merge_masks_scores(hr, fo["multistep_pred_ious"][0], groups)
+        m["pred_masks_high_res"], merged_ious, hr_stats = merge_masks_scores(hr, fo["multistep_pred_ious"][0], groups)
         with torch.no_grad():
             m["pred_masks"] = merge_masks(fo["pred_masks"].detach(), groups)
         m["multistep_pred_masks"] = m["pred_masks"]
@@ -140,8 +140,9 @@ def merge_object_results_to_category(previous_stages_out: List[Dict[str, Any]], 
         m["multistep_pred_multimasks_high_res"] = [m["pred_masks_high_res"]]
         m["multistep_pred_ious"] = [merged_ious]
         with torch.no_grad():
-            m["multistep_object_score_logits"] = [merge_scores(fo["multistep_object_score_logits"][0], hr.detach(),
-                                                               groups)]
+            # weighted by the same high-res statistics (computed once, above)
+            m["multistep_object_score_logits"] = [merge_scores_stats(fo["multistep_object_score_logits"][0],
+                                                                     hr_stats, groups)]
         m["point_inputs"] = fo.get("point_inputs")
         m["mask_inputs"] = fo.get("mask_inputs")
         m["multistep_point_inputs"] = [None]

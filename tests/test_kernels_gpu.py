@@ -1060,6 +1060,9 @@ def test_category_merge_multi_object_matches_reference_formulas():
     from sam2_video.kernels.functional_sam import merge_masks as _mm
     ((_mm(x2, grp) * gh).sum() + (merge_scores(s2, x2, grp) * gi).sum()).backward()
     assert torch.equal(x.grad, x2.grad) and torch.equal(s.grad, s2.grad)
+    # the object-score merge reuses the high-res statistics of that node: the bits of merge_scores
+    with torch.no_grad():
+        assert torch.equal(out["multistep_object_score_logits"][0], merge_scores(ious, logits, grp))
     # a NaN logit propagates through the max like torch.max (the kernel once dropped it)
     from sam2_video.kernels.functional_sam import merge_masks
     from sam2_video.utils.masks import CategoryGroups
