@@ -272,36 +272,42 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
       kwords[0] = t2.x;
       kwords[1] = t2.y;
     }
+    // the key-tail test as a separate code path: an in-line `if (!full)` compiled to a compare and a
+    // select per element on every tile (31 of the loop's 276 VALU instructions, gfx950 ISA)
+    auto softmax = [&](auto tail) {
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
-      bool kp[4] = {true, true, true, true};
-      if constexpr (bits) {
-        const uint32_t wd = kwords[kb >> 1] >> (16 * (kb & 1) + 4 * g);
+      for (int kb = 0; kb < 4; ++kb) {
+        bool kp[4] = {true, true, true, true};
+        if constexpr (bits) {
+          const uint32_t wd = kwords[kb >> 1] >> (16 * (kb & 1) + 4 * g);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) kp[e] = (wd >> e) & 1u;
-      } else if constexpr (DROP == DROP_HASH) {
-        const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
-        if ((e0 & 1) == 0) {
-          s2h_keep_pair(seed, e0 >> 1, a.thresh, kp[0], kp[1]);
-          s2h_keep_pair(seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
-        } else {
+          for (int e = 0; e < 4; ++e) kp[e] = (wd >> e) & 1u;
+        } else if constexpr (DROP == DROP_HASH) {
+          const uint64_t e0 = drow + k0 + kb * 16 + 4 * g;
+          if ((e0 & 1) == 0) {
+            s2h_keep_pair(seed, e0 >> 1, a.thresh, kp[0], kp[1]);
+            s2h_keep_pair(seed, (e0 >> 1) + 1, a.thresh, kp[2], kp[3]);
+          } else {
 #pragma unroll
-          for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(seed, e0 + e, a.thresh);
+            for (int e = 0; e < 4; ++e) kp[e] = s2h_keep(seed, e0 + e, a.thresh);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float p = __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2);
+          if constexpr (decltype(tail)::value) p = (k0 + kb * 16 + 4 * g + r < Lk) ? p : 0.f;
+          const float dpr = FOLD ? dp[kb][r] + dr : dp[kb][r];
+          if constexpr (DROP == DROP_NONE) {
+            s[kb][r] = p * (dpr - di);  // dS (scale applied at the end)
+          } else {
+            const float dpd = kp[r] ? dpr : 0.f;
+            s[kb][r] = p * fmaf(dpd, a.inv_keep, -di);
+          }
         }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float p = __builtin_amdgcn_exp2f(s[kb][r] * a.sl2 - lse2);
-        if (!full) p = (k0 + kb * 16 + 4 * g + r < Lk) ? p : 0.f;  // wave-uniform test, then a select
-        const float dpr = FOLD ? dp[kb][r] + dr : dp[kb][r];
-        if constexpr (DROP == DROP_NONE) {
-          s[kb][r] = p * (dpr - di);  // dS (scale applied at the end)
-        } else {
-          const float dpd = kp[r] ? dpr : 0.f;
-          s[kb][r] = p * fmaf(dpd, a.inv_keep, -di);
-        }
-      }
-    }
+    };
+    if (full) softmax(std::false_type{});
+    else softmax(std::true_type{});
     bf16x8 dsb[2];
 #pragma unroll
     for (int c = 0; c < 2; ++c)
