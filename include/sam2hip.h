@@ -586,6 +586,10 @@ int s2h_pos_embed_bwd(int dt, int C, int h, int w, int ws, const void* dout, flo
 int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
                     int* labels_out, hipStream_t st);
 int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, const void* dout, float* dtable, hipStream_t st);
+/* the same with the 5 label rows' gradients at their own addresses (host array of 5 fp32 [D] rows:
+ * not_a_point_embed, point_embeddings[0..3] -- the parameters' arena gradients), accumulated in row order. */
+int s2h_point_embed_bwd_rows(int dt, int R, int D, const int* labels, const void* dout, float* const* drows,
+                             hipStream_t st);
 
 /* ---------------------------------------------------------------- loss + category merge
  * Per-row mask statistics of logits x/T vs uint8 targets: stats[6*r..] = (focal sum,

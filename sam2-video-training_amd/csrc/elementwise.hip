@@ -1680,13 +1680,17 @@ __global__ void point_embed_kernel(int R, int D, const float* pe, const int* lab
 // one thread per column; the 5 label rows' sums in registers in row order (the same additions, in the
 // same order, as adding into dtable row by row -- which made every row wait for the previous row's
 // store: 53 us for the step's ~200 click rows)
+// the 5 label rows' gradient destinations (rows of one table, or the 5 parameters' own gradients)
+struct PeRows {
+  float* r[5];
+};
 template <typename T>
-__global__ void point_embed_bwd_kernel(int R, int D, const int* labels, const void* dout, float* dtable) {
+__global__ void point_embed_bwd_kernel(int R, int D, const int* labels, const void* dout, PeRows rows) {
   const int d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= D) return;
   float acc[5];
 #pragma unroll
-  for (int k = 0; k < 5; ++k) acc[k] = dtable[k * D + d];
+  for (int k = 0; k < 5; ++k) acc[k] = rows.r[k][d];
 #pragma unroll 8
   for (int r = 0; r < R; ++r) {
     const int l = labels[r] + 1;
@@ -1696,7 +1700,7 @@ __global__ void point_embed_bwd_kernel(int R, int D, const int* labels, const vo
       if (l == k) acc[k] += v;
   }
 #pragma unroll
-  for (int k = 0; k < 5; ++k) dtable[k * D + d] = acc[k];
+  for (int k = 0; k < 5; ++k) rows.r[k][d] = acc[k];
 }
 extern "C" int s2h_point_embed(int dt, int R, int D, const float* pe, const int* labels, const void* table, void* out,
                                int* labels_out, hipStream_t st) {
@@ -1707,7 +1711,20 @@ extern "C" int s2h_point_embed(int dt, int R, int D, const float* pe, const int*
 extern "C" int s2h_point_embed_bwd(int dt, int R, int D, const int* labels, const void* dout, float* dtable,
                                    hipStream_t st) {
   if (R * D <= 0) return 0;
-  DISPATCH_T(dt, point_embed_bwd_kernel, dim3((D + 255) / 256), R, D, labels, dout, dtable);
+  PeRows rows;
+  for (int k = 0; k < 5; ++k) rows.r[k] = dtable + (int64_t)k * D;
+  DISPATCH_T(dt, point_embed_bwd_kernel, dim3((D + 255) / 256), R, D, labels, dout, rows);
+  return (int)hipGetLastError();
+}
+extern "C" int s2h_point_embed_bwd_rows(int dt, int R, int D, const int* labels, const void* dout,
+                                        float* const* drows, hipStream_t st) {
+  if (R * D <= 0) return 0;
+  PeRows rows;
+  for (int k = 0; k < 5; ++k) {
+    if (drows[k] == nullptr) return (int)hipErrorInvalidValue;
+    rows.r[k] = drows[k];
+  }
+  DISPATCH_T(dt, point_embed_bwd_kernel, dim3((D + 255) / 256), R, D, labels, dout, rows);
   return (int)hipGetLastError();
 }
 

@@ -138,6 +138,7 @@ SIGNATURES = {
     "s2h_pos_embed_bwd": [I, I, I, I, I, P, P, P, P],
     "s2h_point_embed": [I, I, I, P, P, P, P, P, P],
     "s2h_point_embed_bwd": [I, I, I, P, P, P, P],
+    "s2h_point_embed_bwd_rows": [I, I, I, P, P, P, P],
     "s2h_prof_enable": [I],
     "s2h_prof_select": [I],
     "s2h_prof_reset": [],

@@ -1452,10 +1452,10 @@ def _point_embed_bw(tape, op, gys):
     labels = tape.stores[("aux", op.idx, "labels")].buf
     gps = [_grad_of(p) for p in op.attrs["tables"]]
     n = len(gps)
-    if all(gp is not None and gp.dtype == torch.float32 and gp.is_contiguous() and gp.numel() == D for gp in gps) \
-            and all(gps[i].data_ptr() == gps[0].data_ptr() + 4 * D * i for i in range(n)):
-        # the label embeddings' gradients are consecutive rows of the arena: accumulate straight into them
-        ops.point_embed_bwd(labels, g.contiguous().view(-1, D), torch.as_strided(gps[0], (n, D), (D, 1)))
+    if n == 5 and all(gp is not None and gp.dtype == torch.float32 and gp.is_contiguous() and gp.numel() == D
+                      for gp in gps):
+        # accumulate straight into the label embeddings' arena gradients (no table, no adds)
+        ops.point_embed_bwd_rows(labels, g.contiguous().view(-1, D), [gp.view(-1) for gp in gps])
         return []
     dtable = torch.zeros(n, D, device=g.device)
     ops.point_embed_bwd(labels, g.contiguous().view(-1, D), dtable)

@@ -1246,6 +1246,15 @@ def point_embed_bwd(labels, dout, dtable):
     call("s2h_point_embed_bwd", dt(dout), R, D, ptr(labels), ptr(dout), ptr(dtable), stream())
 
 
+def point_embed_bwd_rows(labels, dout, rows):
+    """point_embed_bwd into 5 separate fp32 [D] rows (each accumulated in row order)"""
+    import ctypes
+    R, D = dout.shape
+    assert len(rows) == 5 and all(r.dtype == torch.float32 and r.numel() == D and r.is_contiguous() for r in rows)
+    arr = (ctypes.c_void_p * 5)(*[ptr(r) for r in rows])
+    call("s2h_point_embed_bwd_rows", dt(dout), R, D, ptr(labels), ptr(dout), ctypes.addressof(arr), stream())
+
+
 def version():
     from ._lib import lib
     return lib().s2h_version()

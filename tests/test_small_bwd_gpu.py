@@ -141,3 +141,23 @@ def test_row_gate_cast_equals_cast_then_gate():
     rdx = ops.cast(ops.row_gate(g, gate, 0.0, backward=True), torch.bfloat16)
     torch.cuda.synchronize()
     assert torch.equal(y, ref) and torch.equal(gsave, gate) and torch.equal(dx, rdx)
+
+
+def test_point_embed_grad_into_separate_rows():
+    """s2h_point_embed_bwd_rows: the 5 label rows' gradients accumulated at their own addresses (the
+    parameters' arena slices) -- the same additions in the same order as the table form"""
+    from sam2_video.kernels import ops
+    torch.manual_seed(9)
+    R, D = 211, 256
+    labels = torch.randint(-1, 4, (R,), device=DEV, dtype=torch.int32)
+    dout = torch.randn(R, D, device=DEV).to(torch.bfloat16)
+    base = torch.randn(5, D, device=DEV)
+    rows = [torch.empty(D + 3, device=DEV)[k % 2:k % 2 + D] for k in range(5)]  # separate, ragged offsets
+    for k in range(5):
+        rows[k].copy_(base[k])
+    table = base.clone()
+    ops.point_embed_bwd_rows(labels, dout, rows)
+    ops.point_embed_bwd(labels, dout, table)
+    torch.cuda.synchronize()
+    for k in range(5):
+        assert torch.equal(rows[k], table[k])
