@@ -153,6 +153,10 @@ int s2h_wgrad_force(int tile, int splits);
  * s2h_grad_defer(NULL, ...) with records pending returns hipErrorNotReady. */
 int s2h_grad_defer(void* ws, int64_t ws_bytes, void* sink, int64_t sink_bytes);
 int s2h_grad_defer_flush(hipStream_t stream);
+/* ends the deferral scope unconditionally, dropping unflushed records (cleanup after a failed flush).
+ * Records are taken from one stream per scope (the first record's); s2h_grad_defer_flush on another
+ * stream with records pending returns hipErrorInvalidResourceHandle. */
+int s2h_grad_defer_reset(void);
 /* records waiting for s2h_grad_defer_flush (not a hipError_t) */
 int s2h_grad_defer_pending(void);
 

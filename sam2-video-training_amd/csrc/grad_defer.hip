@@ -76,6 +76,8 @@ struct DeferState {
   int64_t ws_bytes = 0, used = 0;
   uintptr_t sink_lo = 0, sink_hi = 0;
   std::vector<DeferRec> recs;
+  hipStream_t st = nullptr;  // the stream of the scope's first record: every deferred record and flush runs on it
+  bool have_st = false;
 };
 DeferState g_def;
 
@@ -114,6 +116,7 @@ int flush(hipStream_t st) {
   }
   g_def.recs.clear();
   g_def.used = 0;
+  g_def.have_st = false;
   return 0;
 }
 
@@ -122,9 +125,15 @@ int flush(hipStream_t st) {
 float* s2h_defer_sink(int nb, int n0, float* out0, int n1, float* out1, hipStream_t st) {
   if (g_def.ws == nullptr || nb <= 0 || n0 <= 0 || !in_sink(out0, n0) || (n1 > 0 && !in_sink(out1, n1)))
     return nullptr;
+  // one stream per scope: a record from another stream (the opt-in weight-gradient side stream) keeps its
+  // immediate second pass -- a mid-scope flush on one stream could read partials the other has not written
+  // yet, and reuse workspace regions the other still reads
+  if (g_def.have_st && st != g_def.st) return nullptr;
   const int64_t bytes = ((int64_t)nb * (n0 + n1) * (int64_t)sizeof(float) + 255) & ~(int64_t)255;
   if (bytes > g_def.ws_bytes) return nullptr;
   if (g_def.used + bytes > g_def.ws_bytes && flush(st) != 0) return nullptr;
+  g_def.st = st;
+  g_def.have_st = true;
   float* part = (float*)(g_def.ws + g_def.used);
   g_def.used += bytes;
   g_def.recs.push_back(DeferRec{part, out0, n1 > 0 ? out1 : nullptr, nb, n0, n1 > 0 ? n1 : 0, 0});
@@ -148,6 +157,16 @@ extern "C" int s2h_grad_defer(void* ws, int64_t ws_bytes, void* sink, int64_t si
   return 0;
 }
 
-extern "C" int s2h_grad_defer_flush(hipStream_t st) { return flush(st); }
+extern "C" int s2h_grad_defer_flush(hipStream_t st) {
+  if (!g_def.recs.empty() && st != g_def.st) return (int)hipErrorInvalidResourceHandle;  // not the records' stream
+  return flush(st);
+}
+
+// end the scope whatever is pending (records not flushed are dropped): the caller's cleanup after a failed
+// flush, so later scopes can register
+extern "C" int s2h_grad_defer_reset() {
+  g_def = DeferState{};
+  return 0;
+}
 
 extern "C" int s2h_grad_defer_pending() { return (int)g_def.recs.size(); }

@@ -52,6 +52,7 @@ SIGNATURES = {
     "s2h_wgrad_workspace": [P, L, I],
     "s2h_grad_defer": [P, L, P, L],
     "s2h_grad_defer_flush": [P],
+    "s2h_grad_defer_reset": [],
     "s2h_grad_defer_pending": [],
     "s2h_wgrad_force": [I, I],
     "s2h_flash_fwd_sets": [I],

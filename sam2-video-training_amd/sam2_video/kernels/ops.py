@@ -113,12 +113,37 @@ WGRAD_WS_BYTES = 96 << 20
 _WG_WS = {}
 
 
+def _capturing():
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def _persistent_alloc(what, n, dtype, device):
+    """a buffer the library keeps the address of for the life of the process: never from a graph's
+    private pool (a capture's allocations are released with the graph, the library would keep a
+    dangling pointer) -- allocate it before the first capture (SAM2Model.load / StepRunner's eager
+    warm-up do)"""
+    if _capturing():
+        raise RuntimeError(f"libsam2hip {what}: first use inside a HIP graph capture; allocate it before capturing "
+                           f"(ops.{what}(device))")
+    return torch.empty(n, dtype=dtype, device=device)
+
+
+def _device_of(device):
+    d = torch.device(device if device is not None else "cuda")
+    if d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
 def wgrad_workspace(device=None):
+    d = _device_of(device)
     t = _WG_WS.get("t")
     if t is None:
-        t = torch.empty(WGRAD_WS_BYTES // 4, dtype=torch.float32, device=device if device is not None else "cuda")
+        t = _persistent_alloc("wgrad_workspace", WGRAD_WS_BYTES // 4, torch.float32, d)
         call("s2h_wgrad_workspace", t.data_ptr(), WGRAD_WS_BYTES, 0 if _SIDE["on"] else -1)
         _WG_WS["t"] = t
+    elif t.device != d:  # one registration per process: the library holds one address
+        raise RuntimeError(f"wgrad workspace already registered on {t.device}, requested {d}")
     return t
 
 
@@ -147,15 +172,17 @@ def deferred_grad_sums(sink):
         return
     t = _DEFER["t"]
     if t is None or t.device != sink.device:
-        t = _DEFER["t"] = torch.empty(GRAD_DEFER_BYTES // 4, dtype=torch.float32, device=sink.device)
+        t = _DEFER["t"] = _persistent_alloc("deferred_grad_sums", GRAD_DEFER_BYTES // 4, torch.float32, sink.device)
     call("s2h_grad_defer", t.data_ptr(), GRAD_DEFER_BYTES, sink.data_ptr(), sink.numel() * sink.element_size())
     _DEFER["depth"] += 1
     try:
         yield
     finally:
         _DEFER["depth"] -= 1
-        call("s2h_grad_defer_flush", stream())
-        call("s2h_grad_defer", None, 0, None, 0)
+        try:
+            call("s2h_grad_defer_flush", stream())
+        finally:  # the scope ends even when the flush raised: later scopes must be able to register
+            call("s2h_grad_defer_reset")
 
 
 # ----------------------------------------------------------------- GEMM

@@ -86,10 +86,13 @@ class ArenaOptimizer(torch.optim.Optimizer):
       logging -- sees the real gradients;
     * zero_grad zeroes the arena and keeps the bindings (set_to_none is ignored: a None .grad would
       cut the view);
-    * step(closure) runs the closure (Lightning's training_step + backward), the arena all-reduce
-      when a process group of > 1 rank is up (arena_ddp_strategy: no DistributedDataParallel wrapper),
-      then the fused clip + AdamW kernels over the whole arena with `max_grad_norm`, which
-      SAM2LightningModule.configure_gradient_clipping sets from the Trainer's gradient_clip_val;
+    * step(closure) runs the closure (Lightning's training_step + backward), then the fused clip +
+      AdamW kernels over the whole arena with `max_grad_norm`, which
+      SAM2LightningModule.configure_gradient_clipping sets from the Trainer's gradient_clip_val; with a
+      process group of > 1 rank up (arena_ddp_strategy: no DistributedDataParallel wrapper) the arena
+      was all-reduced before Lightning's GradScaler looked at it -- beside the staged backward by the
+      graph-replayed micro-step, or by the module's backward hook (reduce_now) -- and the 1/world
+      average is folded into the step's gradient scale;
     * the learning rate is param_groups[0]["lr"] (a torch LambdaLR drives it);
     * state_dict carries the arena moments (Lightning checkpoints)."""
 
@@ -102,6 +105,10 @@ class ArenaOptimizer(torch.optim.Optimizer):
         self.arena = arena
         self.max_grad_norm = float(max_grad_norm or 0.0)
         self.reducer = None
+        # set by SAM2LightningModule for the current accumulation window:
+        self.hold_grads = False   # the next zero_grad keeps the arena (the graph-replayed micro-step filled it)
+        self.window_scale = 1.0   # gradient scale of the window's arena (1/accumulate on the graph path)
+        self.reduced = False      # the window's arena was already all-reduced (in the backward)
         self._bind()
 
     def _bind(self):
@@ -114,8 +121,28 @@ class ArenaOptimizer(torch.optim.Optimizer):
                     p.grad = view
 
     def zero_grad(self, set_to_none: bool = True):
-        self.arena.zero_grad()
+        if self.hold_grads:  # Lightning's zero_grad after a graph-replayed first micro-batch: keep them
+            self.hold_grads = False
+        else:  # a new window (also after a step GradScaler skipped): fresh window state
+            self.arena.zero_grad()
+            self.reduced, self.window_scale = False, 1.0
         self._bind()
+
+    @staticmethod
+    def _world():
+        import torch.distributed as dist
+        return dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+
+    def reduce_now(self):
+        """SUM all-reduce of the gradient arena over the process group (DDP without the wrapper,
+        arena_ddp_strategy); called from the module's backward hook on a window's last micro-batch,
+        i.e. before the precision plugin's GradScaler inspects the gradients"""
+        if self._world() > 1 and not self.reduced:
+            if self.reducer is None:
+                from .ddp import ArenaGradReducer
+                self.reducer = ArenaGradReducer(self.arena.grad_region())
+            self.reducer.reduce()
+        self.reduced = True
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -123,14 +150,11 @@ class ArenaOptimizer(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        scale = 1.0
-        import torch.distributed as dist
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            if self.reducer is None:
-                from .ddp import ArenaGradReducer
-                self.reducer = ArenaGradReducer(self.arena.grad_region())
-            self.reducer.reduce()
-            scale = self.reducer.grad_scale
+        world = self._world()
+        if world > 1 and not self.reduced:  # eager path without the module's backward hook
+            self.reduce_now()
+        scale = self.window_scale / world
+        self.reduced, self.window_scale = False, 1.0
         self.impl.max_grad_norm = self.max_grad_norm
         self.impl.step(lr=self.param_groups[0]["lr"], grad_scale=scale)
         return loss

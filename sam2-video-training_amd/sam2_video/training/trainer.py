@@ -179,6 +179,10 @@ class SAM2LightningModule(_ModuleBase):
         o = self.cfg.optimizer
         params = [p for p in self.model.parameters() if getattr(p, "_s2h_grad", None) is not None]
         lr = float(_get(o, "lr", 1e-4))
+        acc = int(getattr(tr, "accumulate_grad_batches", 1) or 1)
+        if self.accumulate_grad_batches not in (None, 1, acc):
+            self._warn_once("acc", "SAM2LightningModule(accumulate_grad_batches=%s) is ignored under a Lightning "
+                            "Trainer, whose accumulate_grad_batches=%s applies" % (self.accumulate_grad_batches, acc))
         opt = ArenaOptimizer(self.model.arena, params, lr=lr, weight_decay=_get(o, "weight_decay", 0.01),
                              betas=tuple(_get(o, "betas", (0.9, 0.999))), eps=1e-8,
                              max_grad_norm=getattr(tr, "gradient_clip_val", None) or 0.0)
@@ -196,18 +200,41 @@ class SAM2LightningModule(_ModuleBase):
     def configure_gradient_clipping(self, optimizer, gradient_clip_val=None, gradient_clip_algorithm=None):
         """Lightning hook (automatic optimization, before each optimizer step): the Trainer's
         gradient_clip_val becomes the fused AdamW kernel's clip (clip_grad_norm_, norm type 2, on the
-        device, no host sync) instead of torch's clip over every `p.grad`"""
+        device, no host sync) instead of torch's clip over every `p.grad`.  With no clip on the Trainer
+        the module's own gradient_clip_val keyword (the StepRunner setting) applies, with a warning."""
         if gradient_clip_algorithm not in (None, "norm"):
             raise NotImplementedError("gradient_clip_algorithm='value' is not built (the reference clips by norm)")
+        if gradient_clip_val is None and self.gradient_clip_val:
+            self._warn_once("clip", "SAM2LightningModule(gradient_clip_val=%s) applies: the Lightning Trainer sets no "
+                            "gradient_clip_val (set it on the Trainer, as best.yaml:105 does)" % self.gradient_clip_val)
+            gradient_clip_val = self.gradient_clip_val
         opt = getattr(optimizer, "_optimizer", optimizer)  # LightningOptimizer wraps the optimizer
         opt.max_grad_norm = float(gradient_clip_val or 0.0)
 
+    def _warn_once(self, key, msg):
+        seen = self.__dict__.setdefault("_warned", set())
+        if key not in seen:
+            seen.add(key)
+            import warnings
+            warnings.warn(msg, UserWarning, stacklevel=3)
+
     def backward(self, loss, *args, **kwargs):
-        """Lightning hook (automatic optimization): loss.backward() with the gradient arena's
-        deferred fixed-order sums flushed at its end (kernels.ops.deferred_grad_sums)"""
+        """Lightning hook (automatic optimization): a no-op after the graph-replayed micro-step (its
+        backward already filled the gradient arena inside training_step); otherwise loss.backward()
+        with the gradient arena's deferred fixed-order sums flushed at its end
+        (kernels.ops.deferred_grad_sums) and, on the last micro-batch of an accumulation window under
+        DDP, the arena all-reduce -- before the precision plugin's GradScaler unscales and checks the
+        gradients for inf / NaN, so every rank sees the same reduced gradients and takes the same
+        skip-or-step decision (what DistributedDataParallel's in-backward reduce guarantees)"""
+        if self.__dict__.pop("_pl_grads_ready", False):
+            return
         from ..kernels.ops import deferred_grad_sums
         with deferred_grad_sums(self.model.arena.grad_region()):
             loss.backward(*args, **kwargs)
+        if self.__dict__.pop("_pl_window_end", False):
+            opt = self.optimizer
+            if opt is not None and hasattr(opt, "reduce_now"):
+                opt.reduce_now()
 
     # --------------------------------------------------------- forward
     def forward(self, batch):
@@ -223,12 +250,75 @@ class SAM2LightningModule(_ModuleBase):
 
     def log(self, name, value, **kw):
         self.logged[name] = value.detach() if torch.is_tensor(value) else value
-        if HAVE_LIGHTNING and self._attached_trainer() is not None:  # pragma: no cover
-            super().log(name, value, batch_size=1, **kw)
+        # not while a StepRunner records / captures the step: Lightning's metric updates would be
+        # captured into the graph; the graph-replayed path logs the step's values after each replay
+        if HAVE_LIGHTNING and self._attached_trainer() is not None and not self.__dict__.get("_in_runner"):
+            super().log(name, value, batch_size=1, **kw)  # pragma: no cover
+
+    # Under a Lightning Trainer (automatic optimization) training_step runs the whole micro-step --
+    # forward, loss and the backward into the gradient arena -- as a replay of the captured HIP graph
+    # (StepRunner's, the bench path) and returns the loss; the backward hook is then a no-op.  False:
+    # the eager module (Lightning's own training_step -> backward order, no graph).
+    lightning_graph = True
+
+    def _pl_runner(self, tr, k):
+        run = self.__dict__.get("_pl_run")
+        if run is None or run.accumulate != k:
+            import torch.distributed as dist
+            world = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+            run = StepRunner(self, graph=True, distributed=world > 1, accumulate_grad_batches=k, optimizer=False)
+            self._pl_run = run
+        return run
+
+    @staticmethod
+    def _pl_is_window_end(tr, batch_idx, k):
+        """Lightning steps the optimizer after this micro-batch (fit_loop._should_accumulate() is
+        False): the k-th batch of a window or the epoch's last batch"""
+        loop = getattr(tr, "fit_loop", None)
+        fn = getattr(loop, "_should_accumulate", None)
+        if fn is not None:
+            return not fn()
+        n = getattr(tr, "num_training_batches", None)
+        return (batch_idx + 1) % k == 0 or (isinstance(n, int) and batch_idx + 1 >= n)
+
+    def _pl_graphed_step(self, batch, batch_idx, tr):
+        """one Lightning micro-batch through the StepRunner: the arena is zeroed when the window starts
+        (Lightning's zero_grad, which follows training_step in its closure, is then skipped for this
+        micro-batch), the backward is seeded with the precision plugin's GradScaler scale (so
+        unscale_ / the inf check see what loss.backward() of the scaled loss would have produced), and on
+        the window's last micro-batch under DDP the arena ranges are all-reduced beside the staged
+        backbone backward, as StepRunner overlaps them.  Lightning's 1/accumulate_grad_batches loss
+        normalisation is folded into the optimizer step's gradient scale (ArenaOptimizer.window_scale),
+        as StepRunner folds it: the arena holds the window's summed gradients, bit-identical to the
+        StepRunner's."""
+        k = max(1, int(getattr(tr, "accumulate_grad_batches", 1) or 1))
+        run = self._pl_runner(tr, k)
+        end = self._pl_is_window_end(tr, batch_idx, k)
+        scaler = getattr(getattr(tr, "precision_plugin", None), "scaler", None)
+        loss = run.lightning_micro_step(batch, window_start=batch_idx % k == 0, reduce=end, scaler=scaler)
+        opt = self.optimizer
+        if opt is not None:
+            opt.hold_grads = batch_idx % k == 0  # the zero_grad Lightning issues after this training_step
+            if end:
+                opt.window_scale = 1.0 / k
+                opt.reduced = run.reducer is not None
+        self._pl_grads_ready = True
+        if HAVE_LIGHTNING:  # pragma: no cover
+            for name, v in self.logged.items():
+                super().log(name, v, batch_size=1)
+        return loss
 
     def training_step(self, batch, batch_idx: int = 0) -> torch.Tensor:
         """trainer.py:256-289: forward, the loss on the gt_stride frames, the logged terms; returns
-        the loss (Lightning / StepRunner run the backward into the gradient arena)"""
+        the loss (Lightning / StepRunner run the backward into the gradient arena).  Under a Lightning
+        Trainer with lightning_graph (default) the micro-step is the StepRunner's graph replay
+        (_pl_graphed_step)."""
+        tr = self._attached_trainer()
+        if tr is not None and not self.__dict__.get("_in_runner"):
+            if self.lightning_graph:
+                return self._pl_graphed_step(batch, batch_idx, tr)
+            k = max(1, int(getattr(tr, "accumulate_grad_batches", 1) or 1))
+            self._pl_window_end = self._pl_is_window_end(tr, batch_idx, k)
         outs_per_frame, obj_to_cat = self.forward(batch)
         self.last_outputs = outs_per_frame
         outs, targets = self._apply_gt_stride(outs_per_frame, batch.masks)
@@ -294,11 +384,15 @@ class StepRunner:
 
     def __init__(self, module: SAM2LightningModule, total_steps: int = 1, distributed: bool = False,
                  graph: bool = False, accumulate_grad_batches: int = 1, gradient_clip_val=None,
-                 split_backward: Optional[bool] = None):
+                 split_backward: Optional[bool] = None, optimizer: bool = True):
+        """optimizer=False: the Lightning path (SAM2LightningModule._pl_graphed_step) -- the runner
+        only runs micro-steps (lightning_micro_step); Lightning's optimizer loop steps the module's
+        ArenaOptimizer"""
         self.module = module
         if gradient_clip_val is not None:
             module.gradient_clip_val = gradient_clip_val
-        module.configure_optimizers(total_steps)
+        if optimizer:
+            module.configure_optimizers(total_steps)
         arena = module.model.arena
         self.reducer = ArenaGradReducer(arena.grad_region(), split=arena.grad_split) if distributed else None
         # overlap: a two-phase backward -- (1) loss -> backbone outputs (the frame-batched
@@ -326,20 +420,29 @@ class StepRunner:
         self.seed_base = FN._SEED[0]
         self._pending = None
         self._segs = None
+        # the backward's seed dL/dL: 1 (StepRunner), or the GradScaler scale of the Lightning path;
+        # a device tensor read by the loss kernels' backward, so a captured graph picks up new values
+        self.grad_seed = torch.ones((), device=arena.device, dtype=torch.float32)
         module.model.arena.zero_grad()
 
     def _device_step(self, batch):
         """forward + loss + backward (phase 1 only when overlapping; _phase2 finishes it)"""
         self._fn.set_seed(self.seed_base)
-        loss = self.module.training_step(batch, self.micro_step)
-        bb = getattr(self.module.model, "last_backbone_outputs", None) if self.overlap else None
+        m = self.module
+        m._in_runner = True
+        try:
+            loss = m.training_step(batch, self.micro_step)
+        finally:
+            m._in_runner = False
+        seed = self.grad_seed.view(loss.shape)
+        bb = getattr(m.model, "last_backbone_outputs", None) if self.overlap else None
         with self._sums():  # each backward phase flushes its deferred gradient sums at its end
             if bb:
-                grads = torch.autograd.grad(loss, bb, allow_unused=True)
+                grads = torch.autograd.grad(loss, bb, grad_outputs=seed, allow_unused=True)
                 self._pending = [(t, g) for t, g in zip(bb, grads) if g is not None]
             else:
                 self._pending = None
-                loss.backward()
+                loss.backward(seed)
         return loss
 
     def _segments(self):
@@ -454,11 +557,46 @@ class StepRunner:
 
     def __call__(self, batch):
         self.begin_micro_step()
+        loss = self._run(batch, (self.micro_step + 1) % self.accumulate == 0)
+        self.after_backward(reduced=self.overlap and self.reducer is not None
+                            and (self.micro_step + 1) % self.accumulate == 0)
+        return loss
+
+    def lightning_micro_step(self, batch, window_start: bool, reduce: bool, scaler=None):
+        """The Lightning path's micro-step (no optimizer step: Lightning's optimizer loop takes it):
+        zero the arena when the accumulation window starts, draw fresh dropout masks, seed the backward
+        with the GradScaler's current scale (device tensor, no host sync; its init_scale before the
+        first scale() call; 1 without a scaler), forward + loss + backward (graph replay), and when
+        `reduce` (the window's last micro-batch) under DDP the arena all-reduce of every range beside
+        the staged backward, finished before this returns -- so Lightning's unscale_ / inf check /
+        clip see the reduced gradients on every rank."""
+        if window_start:
+            self.module.model.arena.zero_grad()
+        self.rng.fill_(self.micro_step + 1)
+        self._fn.set_seed(self.seed_base)
+        if scaler is not None and getattr(scaler, "is_enabled", lambda: True)():
+            s = getattr(scaler, "_scale", None)
+            if s is None:
+                self.grad_seed.fill_(float(getattr(scaler, "_init_scale", 1.0)))
+            else:
+                self.grad_seed.copy_(s.reshape(()))
+        else:
+            self.grad_seed.fill_(1.0)
+        loss = self._run(batch, reduce)
+        if reduce and self.reducer is not None and not self.overlap:
+            self.reducer.reduce()
+        self.micro_step += 1
+        return loss
+
+    def _run(self, batch, boundary):
+        """forward + loss + backward of one micro-step (graph replay or eager); at an accumulation
+        boundary under DDP with the staged backward, each completed arena range is all-reduced beside
+        the following segments (the works are waited for before this returns)"""
         self._segs = None
         loss = self._graphed_step(batch) if self.graph else self._device_step(batch)
         if self._segs is None:
             self._segs = self._segments()
-        reduce = self.overlap and self.reducer is not None and (self.micro_step + 1) % self.accumulate == 0
+        reduce = self.overlap and self.reducer is not None and boundary
         works = []
         if reduce:
             # the tracking gradients are complete: reduce them beside the backbone's backward
@@ -474,7 +612,6 @@ class StepRunner:
             works += self.reducer.reduce_range(self.cuts[done], self.reducer.grad.numel())
             for w in works:
                 w.wait()
-        self.after_backward(reduced=reduce)
         return loss
 
 

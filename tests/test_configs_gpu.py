@@ -93,6 +93,76 @@ def test_config2_bf16_close_to_fp32():
     assert abs(res["fp32"][1] - res["bf16"][1]) <= 0.02 * abs(res["fp32"][1])
 
 
+def _group_drift(a, b, names):
+    """(relative RMS error |a - b| / |b|, cosine(a, b)) over the concatenated tensors `names`"""
+    num = den = dot = na = 0.0
+    for n in names:
+        x, y = a[n].double(), b[n].double()
+        num += float(((x - y) ** 2).sum())
+        den += float((y ** 2).sum())
+        dot += float((x * y).sum())
+        na += float((x ** 2).sum())
+    return math.sqrt(num / max(den, 1e-300)), dot / max(math.sqrt(na * den), 1e-300)
+
+
+def test_config2_bf16_gradients_close_to_fp32():
+    """the bench path's gradients at the bench size.  Config 2 (B+, 512^2, 8 frames,
+    13 objects; dropout off), one clip: the bf16 gradient arena (V-fold cross-attention over banks of up
+    to 7 x 1028 = 7196 keys, the fused decoder, every bench kernel) against this build's fp32 mode on
+    the same clip and weights (the mode pinned to the reference at 128 / 256^2 by test_parity_gpu.py /
+    test_training_step_gpu.py).  Per module group (step_harness.grad_group), over all its parameters:
+    relative RMS error <= 2 x the reference's own bf16-vs-fp32 drift of that group at B+ 256^2 T = 8
+    (tests/golden/bplus256_point_all_t8{,_bf16}.pt, its stored gradient tensors) + 0.02, and
+    1 - cos <= 2 (1 - cos_ref) + 0.002; a mutated group (the memory attention's gradients x 1.15, a
+    wrong dropout 1/keep scale) must fail the bound."""
+    import collections
+
+    from step_harness import grad_group, grads_by_name, load_golden, run_step
+    clip = _clips([77], 8, 512, 13, 13)[0]
+    grads = {}
+    for dt in ("fp32", "bf16"):
+        m = _module("base_plus", 512, dtype=dt, dropout=0.0)
+        run_step(m.model, clip)
+        grads[dt] = grads_by_name(m.model)
+        del m
+        torch.cuda.empty_cache()
+    gf, gb = load_golden("bplus256_point_all_t8"), load_golden("bplus256_point_all_t8_bf16")
+    ref_groups = collections.defaultdict(list)
+    for k in gf:
+        if k.startswith("grad/") and float(gf[k].double().norm()) > 0:
+            ref_groups[grad_group(k[5:])].append(k[5:])
+    gf = {k[5:]: v for k, v in gf.items() if k.startswith("grad/")}
+    gb = {k[5:]: v for k, v in gb.items() if k.startswith("grad/")}
+    ours_groups = collections.defaultdict(list)
+    for n, g in grads["fp32"].items():
+        if float(g.norm()) > 0:
+            ours_groups[grad_group(n)].append(n)
+
+    def check(bf16):
+        bad, rows = [], []
+        for grp, names in sorted(ours_groups.items()):
+            e, c = _group_drift(bf16, grads["fp32"], names)
+            if grp in ref_groups:
+                e_ref, c_ref = _group_drift(gb, gf, ref_groups[grp])
+            else:  # no stored reference tensor in this group: the worst group's drift
+                e_ref, c_ref = max((_group_drift(gb, gf, v) for v in ref_groups.values()), key=lambda t: t[0])
+            rows.append((grp, len(names), e, e_ref, 1 - c, 1 - c_ref))
+            if e > 2 * e_ref + 0.02 or 1 - c > 2 * (1 - c_ref) + 0.002:
+                bad.append(rows[-1])
+        return rows, bad
+
+    rows, bad = check(grads["bf16"])
+    for r in rows:
+        print("group %-40s n=%4d  rel-rms %.4f (ref %.4f)  1-cos %.2e (ref %.2e)" % r)
+    assert not bad, bad
+    # sensitivity: the memory attention's gradients off by 15 %
+    mutated = dict(grads["bf16"])
+    for n in ours_groups["memory_attention"]:
+        mutated[n] = mutated[n] * 1.15
+    _, bad_m = check(mutated)
+    assert any(b[0] == "memory_attention" for b in bad_m), bad_m
+
+
 def test_gradient_accumulation_sums_micro_steps():
     """accumulate_grad_batches = 2: the arena after two micro-steps equals the sum of the two
     single-step gradients (fp32, dropout off), no optimizer step in between"""

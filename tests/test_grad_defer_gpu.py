@@ -105,3 +105,56 @@ def test_scope_close_with_pending_records_is_refused():
     assert h.s2h_grad_defer(None, 0, None, 0) != 0  # records pending: refused
     assert h.s2h_grad_defer_flush(ops.stream()) == 0
     assert h.s2h_grad_defer(None, 0, None, 0) == 0
+
+
+def test_records_from_a_second_stream_keep_the_immediate_pass_and_reset_ends_a_failed_scope():
+    """one stream per scope -- a column sum issued on another stream (the opt-in weight-gradient
+    side stream) is not deferred (its immediate second pass runs on its own stream); a flush on a stream
+    other than the records' is refused, and s2h_grad_defer_reset ends the scope so the next can register"""
+    ops = _ops()
+    from sam2_video.kernels._lib import lib
+    torch.manual_seed(3)
+    h = lib()
+    arena = torch.zeros(512, device=DEV)
+    ws = torch.empty(1 << 18, device=DEV)
+    g = torch.randn(4096, 256, device=DEV).to(torch.bfloat16)
+    side = torch.cuda.Stream()
+    assert h.s2h_grad_defer(ws.data_ptr(), ws.numel() * 4, arena.data_ptr(), arena.numel() * 4) == 0
+    try:
+        ops.colsum(g, arena[:256])  # main stream: deferred
+        assert h.s2h_grad_defer_pending() == 1
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            ops.colsum(g, arena[256:])  # other stream: immediate
+        assert h.s2h_grad_defer_pending() == 1
+        torch.cuda.current_stream().wait_stream(side)
+        assert h.s2h_grad_defer_flush(side.cuda_stream) != 0  # not the records' stream: refused
+        assert h.s2h_grad_defer_pending() == 1
+        assert h.s2h_grad_defer_flush(ops.stream()) == 0
+    finally:
+        h.s2h_grad_defer_reset()
+    torch.cuda.synchronize()
+    ref = g.double().sum(0)
+    _close(arena[:256].double(), ref, 1e-5)
+    _close(arena[256:].double(), ref, 1e-5)
+    # a failed flush inside ops.deferred_grad_sums still ends the scope (reset in its finally)
+    assert h.s2h_grad_defer(ws.data_ptr(), ws.numel() * 4, arena.data_ptr(), arena.numel() * 4) == 0
+    ops.colsum(g, arena[:256])
+    h.s2h_grad_defer_reset()  # drops the pending record
+    assert h.s2h_grad_defer_pending() == 0
+    with ops.deferred_grad_sums(arena):
+        ops.colsum(g, arena[:256])
+    assert h.s2h_grad_defer_pending() == 0
+
+
+def test_persistent_buffers_refuse_first_use_inside_a_capture():
+    """the library keeps the addresses of the weight-gradient workspace and the deferral
+    workspace for the whole process; first allocated inside a graph capture they would come from the
+    graph's private pool and dangle once the graph is released -- refused loudly instead"""
+    ops = _ops()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            with pytest.raises(RuntimeError, match="inside a HIP graph capture"):
+                ops._persistent_alloc("wgrad_workspace", 16, torch.float32, "cuda")

@@ -249,6 +249,7 @@ def _stub_lightning_module(monkeypatch, n, rank, trainer):
     mod.forward = forward
     mod.criterion = _StubCriterion()
     mod._trainer = trainer
+    mod.lightning_graph = False  # the eager module path: no StepRunner / graph on the stub model
     return mod, arena
 
 
@@ -258,37 +259,18 @@ class _StubCriterion(torch.nn.Module):
 
 
 def _lightning_fit(mod, n_batches, acc, clip, scaler=None):
-    """Lightning 2.x automatic optimization over n_batches (training_epoch_loop + optimizer loop +
-    precision plugin): each micro-batch's loss / accumulate_grad_batches is backpropagated; at a
-    window boundary (and on the epoch's last batch) the optimizer steps -- with precision=16 through
-    GradScaler (closure, unscale_, clip, scaler.step, update), else optimizer.step(closure) with the
-    clip after the closure's backward -- then zero_grad and the per-step scheduler"""
-    conf = mod.configure_optimizers()
-    opt, sched = conf["optimizer"], conf["lr_scheduler"]["scheduler"]
-    assert isinstance(opt, torch.optim.Optimizer) and conf["lr_scheduler"]["interval"] == "step"
+    """Lightning 2.x automatic optimization over n_batches (tests/lightning_stub.py: training_step,
+    zero_grad on a window's first batch after it, the precision plugin's scaled module.backward; at a
+    window boundary and on the epoch's last batch the optimizer step -- with precision=16 through
+    GradScaler (unscale_, clip hook, scaler.step, update), else optimizer.step(closure) with the clip
+    after the closure's backward -- then the per-step scheduler)"""
+    from lightning_stub import StubFitLoop, lightning_fit
+    tr = mod._trainer
+    tr.fit_loop = StubFitLoop(acc, n_batches)
+    tr.precision_plugin = SimpleNamespace(scaler=scaler)
     batch = SimpleNamespace(masks=torch.zeros(1, 1, 2, 2))
-    for i in range(n_batches):
-        def closure(i=i):
-            loss = mod.training_step(batch, i) / acc
-            (scaler.scale(loss) if scaler is not None else loss).backward()
-            return loss
-        if (i + 1) % acc and i + 1 < n_batches:
-            closure()
-            continue
-        if scaler is not None:
-            closure()
-            scaler.unscale_(opt)
-            mod.configure_gradient_clipping(opt, clip, "norm")
-            scaler.step(opt)
-            scaler.update()
-        else:
-            def wrapped():
-                out = closure()
-                mod.configure_gradient_clipping(opt, clip, "norm")
-                return out
-            opt.step(closure=wrapped)
-        opt.zero_grad()
-        sched.step()
+    opt = lightning_fit(mod, tr, [batch] * n_batches)
+    assert isinstance(opt, torch.optim.Optimizer)
     return opt
 
 
@@ -316,7 +298,9 @@ def test_lightning_automatic_optimization_clip_and_accumulate_on_the_trainer(mon
     assert impl.lrs[0] == 0.0 and 0.0 < impl.lrs[1] <= 1e-4  # warmup 0.25 x 3 steps, then cosine
     for p in mod.model.parameters():  # the bindings survive zero_grad
         assert p.grad is not None and p.grad.data_ptr() == p._s2h_grad.data_ptr()
-    assert float(arena.grad.abs().max()) == 0.0
+    # Lightning zeroes a window's gradients at the next window's first micro-batch (after its
+    # training_step), not after the optimizer step: the last window's stay in the arena
+    torch.testing.assert_close(arena.grad, exp[-1])
 
 
 def test_configure_gradient_clipping_routes_to_the_kernel(monkeypatch):
@@ -384,6 +368,71 @@ def test_lightning_automatic_optimization_two_ranks_gloo():
     for p in procs:
         p.join(timeout=60)
     assert all(ok for _, ok, _ in res), res
+
+
+def _lightning_scaler_worker(rank, world, port, q):
+    """precision=16 under DDP: rank 1's second micro-batch produces an inf gradient.  The arena is
+    all-reduced in the module's backward hook (before GradScaler.unscale_ looks at it), so BOTH ranks
+    find the inf, skip that window's step and lower the scale alike (with the reduce inside
+    the optimizer step, only rank 1 skipped and the ranks' collectives paired up across iterations)"""
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    try:
+        mp_ = pytest.MonkeyPatch()
+        from sam2_video.training.ddp import init_from_env
+        init_from_env("gloo")
+        n, acc, nb = 64, 2, 6
+        tr = SimpleNamespace(estimated_stepping_batches=3, accumulate_grad_batches=acc, gradient_clip_val=1.0,
+                             precision="16-mixed")
+        mod, arena = _stub_lightning_module(mp_, n, rank, tr)
+        fwd = mod.forward
+        calls = {"n": 0}
+
+        def forward(batch):
+            calls["n"] += 1
+            outs, cats = fwd(batch)
+            if rank == 1 and calls["n"] == 2:  # window 1's last micro-batch on rank 1 only
+                y = outs[0]["y"]
+                outs = [{"y": y * float("inf")}]
+            return outs, cats
+        mod.forward = forward
+        scaler = torch.amp.GradScaler("cpu", init_scale=256.0)
+        scales = []
+        opt = _lightning_fit(mod, nb, acc, 1.0, scaler)
+        scales.append(float(scaler.get_scale()))
+        seen = opt.impl.seen
+        ok = len(seen) == 2 and all(bool(torch.isfinite(x).all()) for x in seen)
+        mp_.undo()
+        q.put((rank, bool(ok), (len(seen), scales)))
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, False, traceback.format_exc()))
+    finally:
+        import torch.distributed as dist
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_lightning_grad_scaler_inf_on_one_rank_skips_on_every_rank():
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_lightning_scaler_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _ in res), res
+    # the same skipped window and the same scale on both ranks (256 halved once by the skip)
+    assert res[0][2] == res[1][2] and res[0][2][0] == 2 and res[0][2][1] == [128.0], res
 
 
 def test_activation_checkpoint_flag_is_a_notice():
