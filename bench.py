@@ -62,6 +62,7 @@ def parse():
     ap.add_argument("--cpu-frames", type=int, default=None,
                     help="frames of the CPU baseline sample clip (default: the workload's own frame count)")
     ap.add_argument("--no-prof", action="store_true")
+    ap.add_argument("--shape-table", default=None, help="write the GEMM shape -> tiling table of the profiled step")
     ap.add_argument("--print-losses", action="store_true", help="diagnostic: print every step's loss (host syncs)")
     ap.add_argument("--no-graph", action="store_true",
                     help="launch every kernel from Python each step instead of replaying the captured HIP graph")
@@ -371,6 +372,34 @@ def dominant_kernel(recs, kind, peak, nsteps=1, overhead_ms=0.0):
             "share_of_family_ms": None}
 
 
+def write_shape_table(recs3, path):
+    """GEMM shape -> tiling table of one profiled eager step: for every (tiling kernel, shape, operand
+    layout) its launches per step and algorithmic flops per launch (so a traced kernel's flops per
+    launch -- the roofline's dominant kernel -- can be recomputed shape by shape), and the event-bracketed
+    time per launch (overstates short launches by the event overhead; the trace is the time reference)"""
+    agg = {}
+    for ms, m, tag in recs3:
+        if m[0] != 4:
+            continue
+        b, M, N, K, lay = m[1:]
+        key = (kernel_name(4, tag), f"b{b} {M}x{N}x{K} {'A' if lay & 2 else 'a'}{'B' if lay & 1 else 'b'}")
+        a = agg.setdefault(key, [0, 0.0, record_flops(4, m)])
+        a[0] += 1
+        a[1] += ms
+    by_kernel = {}
+    for (kn, shape), (n, ms, fl) in agg.items():
+        by_kernel.setdefault(kn, []).append((shape, n, fl, ms))
+    with open(path, "w") as f:
+        f.write("# GEMM shape -> tiling of one profiled eager step (bench.py --shape-table): kernel | shape (batch MxNxK,\n"
+                "# A/a = A K-contiguous or not, B/b likewise) | launches | GFLOP per launch | event us per launch\n")
+        for kn, rows in sorted(by_kernel.items(), key=lambda kv: -sum(r[1] * r[2] for r in kv[1])):
+            n_all = sum(r[1] for r in rows)
+            fl_all = sum(r[1] * r[2] for r in rows)
+            f.write(f"\n{kn}: {n_all} launches, {fl_all / max(n_all, 1) / 1e9:.3f} GFLOP per launch on average\n")
+            for shape, n, fl, ms in sorted(rows, key=lambda r: -r[1] * r[2]):
+                f.write(f"  {shape:32s} n={n:4d}  {fl / 1e9:8.3f} GF  {1e3 * ms / n:8.2f} us\n")
+
+
 def kernel_table(recs):
     """Per-shape time / achieved TFLOP/s of the GEMM and attention launches of one step."""
     agg = {}
@@ -588,6 +617,8 @@ def main():
                 roof["trace"] = note
         if args.kernel_table and rank == 0:
             print(kernel_table(recs), file=sys.stderr, flush=True)
+        if args.shape_table and rank == 0:
+            write_shape_table(recs3, args.shape_table)
         _lib.call("s2h_prof_select", 1)
 
     frames = args.frames * args.steps * world

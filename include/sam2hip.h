@@ -112,6 +112,11 @@ int s2h_gemm_tiny_config(int cfg);
  * 2 x 2 (1: all, the default; 2: only N >= 768; 0: off); results are bit-identical.  Returns the
  * previous mode. */
 int s2h_gemm_w41(int mode);
+/* A/B knob (round 6): tiling (values as s2h_gemm_config, 0 = the shape rules) of one class of
+ * bf16-output GEMMs with M > 128 -- class 0: K >= 1024 and N <= 512; 1: K <= 256, N <= 256 and
+ * M >= 8192; 2: K <= 512 and N >= 768; 3: 256 < K < 1024 and N <= 512.  Returns the previous
+ * setting (-1: no such class). */
+int s2h_gemm_class_config(int cls, int cfg);
 /* A/B knob: GEMMs with a short K that is not a multiple of 64 (K < 256, K-contiguous A, bf16 output)
  * on the A-in-registers tiling (1: on, the default; 0: off); results are bit-identical.  Returns the
  * previous mode. */

@@ -128,11 +128,36 @@ __device__ __forceinline__ uint64_t s2h_seed(uint64_t seed, const uint64_t* off)
   return o ? seed ^ (o * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull) : seed;
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+// GELU (exact erf form, nn.GELU() of the reference's MLPs / CXBlock / mask decoder) through the normal
+// CDF Phi(x) = 0.5 erfc(-x / sqrt 2), with erfc(a) = t exp(-a^2 + P(t)), t = 1 / (1 + a / 2), a >= 0: the
+// Chebyshev fit of Numerical Recipes' erfcc (fractional error < 1.2e-7 for every a), one v_rcp, one
+// v_exp and 9 FMAs, branch-free.  Round 6: it replaces ocml erff (~35 VALU with a |x| < 1 branch that
+// divergent lanes take both ways) in the GEMM epilogues of the Hiera MLP fc1 (462 M elements per bench
+// step, forward and backward) and the memory fuser; erfc's relative accuracy also holds in the far
+// negative tail where 1 + erff(x) cancelled to a few bits.
+__device__ __forceinline__ float s2h_erfc_exp_arg(float a, float t) {  // -a^2 + P(t): erfc(a) = t exp(this)
+  float p = 0.17087277f;
+  p = fmaf(t, p, -0.82215223f);
+  p = fmaf(t, p, 1.48851587f);
+  p = fmaf(t, p, -1.13520398f);
+  p = fmaf(t, p, 0.27886807f);
+  p = fmaf(t, p, -0.18628806f);
+  p = fmaf(t, p, 0.09678418f);
+  p = fmaf(t, p, 0.37409196f);
+  p = fmaf(t, p, 1.00002368f);
+  p = fmaf(t, p, -1.26551223f);
+  return fmaf(-a, a, p);
+}
+__device__ __forceinline__ float s2h_normal_cdf(float x) {  // Phi(x)
+  const float a = fabsf(x) * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.5f, a, 1.f));
+  const float h = 0.5f * t * __builtin_amdgcn_exp2f(s2h_erfc_exp_arg(a, t) * 1.4426950408889634f);  // 0.5 erfc(a)
+  return x >= 0.f ? 1.f - h : h;
+}
+__device__ __forceinline__ float gelu_erf(float x) { return x * s2h_normal_cdf(x); }
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  const float pdf = 0.39894228040143268f * __builtin_amdgcn_exp2f(-0.72134752044448170f * x * x);  // phi(x)
+  return fmaf(x, pdf, s2h_normal_cdf(x));
 }
 
 enum S2HAct { S2H_ACT_NONE = 0, S2H_ACT_RELU = 1, S2H_ACT_GELU = 2, S2H_ACT_SIGMOID = 3 };

@@ -49,6 +49,7 @@ struct FlashArgs {
   int splits, tiles_per_split;
   float* ws_o;   // [splits][BH*Lq][DP] unnormalised partial O (splits > 1)
   float* ws_ml;  // [splits][BH*Lq][2] (m in log2 units, l)
+  int prio;      // waves 4-7 at s_setprio 1 (A/B: s2h_flash_variant bit 3)
 };
 
 // dropout: none / counter hash / counter hash + keep bitmap store (template: no per-tile tests)
@@ -75,6 +76,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   // one LDS array: [2 stages][K tile | V tile]
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
+  if (a.prio && w >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (MI355X_MICROARCH item 4)
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
   const int bh = wi.y, b = bh / a.H, h = bh % a.H;
@@ -436,6 +438,7 @@ int64_t s2h_flash_ws_bytes(int B, int H, int Lq, int Lk, int D) {
 
 template <int DP, int DV = DP, int QS = 1>
 static int flash_launch(FlashArgs& a, hipStream_t st) {
+  a.prio = (s2h_flash_variant() >> 3) & 1;
   dim3 grid((a.Lq + FL_QB * QS - 1) / (FL_QB * QS), pad_bh8(a.BH), a.splits);
   if (a.p_drop <= 0.f)
     hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);

@@ -66,6 +66,7 @@ struct FlashBwdArgs {
   int rope_k, rope_q;
   int fr_nrot[S2H_MAX_FRAMES];
   int fr_nrotq[S2H_MAX_FRAMES];
+  int prio;  // bit 0: dK kernel, bit 1: dQ kernel -- waves 4-7 at s_setprio 1 (A/B: s2h_flash_variant bits 1-2)
 };
 
 // The frame table is read straight from the kernarg segment (scalar loads): indexing the by-value
@@ -154,6 +155,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
   __shared__ __attribute__((aligned(1024))) char smem[2 * STG + 2 * FL_WAVES * 256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
+  if ((a.prio & 2) && w >= 4) __builtin_amdgcn_s_setprio(1);
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
   const int bh = wi.y, b = bh / a.H, h = bh % a.H;
@@ -770,6 +772,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
   const int bh = wi.y, b = bh / a.H, h = bh % a.H;
   const KvFrame fr = kv_frame(a, bh);
   if (wi.x * (NW * 16) >= fr.Lk) return;  // frame-table launch: past this frame's keys
+  if ((a.prio & 1) && w >= 4) __builtin_amdgcn_s_setprio(1);
   const int key = wi.x * (NW * 16) + w * 16 + kl;
   const bool kv = key < fr.Lk;
   const bf16* Q = a.q + b * a.sqb + h * a.sqh;
@@ -1017,6 +1020,7 @@ int64_t s2h_flash_bwd_ws_bytes(int B, int H, int Lq, int Lk, int D) {
 template <int DP, int DV = DP>
 static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   const int64_t rows = (int64_t)a.BH * a.Lq;
+  a.prio = (s2h_flash_variant() >> 1) & 3;
   // Di = rowsum(dO * O) is computed by the dQ kernel and stored for the dK / dV kernel
   const int drop = a.p_drop <= 0.f ? DROP_NONE : (a.keep ? DROP_BITS : DROP_HASH);
   const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);

@@ -53,6 +53,28 @@ extern "C" int s2h_gemm_areg(int mode) {
   return prev;
 }
 
+// A/B knob (round 6): the tiling of one class of bf16-output GEMMs (M > 128), 0 = the shape rules below.
+//   class 0: K >= 1024, N <= 512 (long reduction, narrow output: the memory-attention FFN linear2, the
+//            memory fuser pwconv2, Hiera MLP fc2)
+//   class 1: K <= 256, N <= 256, M >= 8192 (short reduction, narrow output: per-frame projections)
+//   class 2: K <= 512, N >= 768 (wide output: FFN linear1, Hiera qkv / fc1)
+//   class 3: 256 < K < 1024, N <= 512 (mid reduction, narrow output: Hiera proj)
+static int g_gemm_class_cfg[4] = {0, 0, 0, 0};
+extern "C" int s2h_gemm_class_config(int cls, int cfg) {
+  if (cls < 0 || cls > 3) return -1;
+  const int prev = g_gemm_class_cfg[cls];
+  g_gemm_class_cfg[cls] = cfg;
+  return prev;
+}
+static int gemm_class(const GemmArgs16& a) {
+  if (a.out_f32 || a.M <= 128) return -1;
+  if (a.K >= 1024 && a.N <= 512) return 0;
+  if (a.K <= 256 && a.N <= 256 && a.M >= 8192) return 1;
+  if (a.K <= 512 && a.N >= 768) return 2;
+  if (a.K > 256 && a.K < 1024 && a.N <= 512) return 3;
+  return -1;
+}
+
 extern "C" int s2h_gemm_config(int cfg) {
   const int prev = g_gemm_cfg | (g_gemm_dbg << 8);
   g_gemm_cfg = cfg < 0 ? cfg : (cfg & 0xff);
@@ -108,6 +130,10 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   }
   int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
   if (g_gemm_tiny_cfg && !g_gemm_cfg && a.M <= 128) cfg = g_gemm_tiny_cfg;
+  if (!g_gemm_cfg) {
+    const int cls = gemm_class(a);
+    if (cls >= 0 && g_gemm_class_cfg[cls]) cfg = g_gemm_class_cfg[cls];
+  }
   if (g_gemm_w41 && !g_gemm_cfg && !a.out_f32 && (g_gemm_w41 == 1 || a.N >= 768)) cfg = w41_of(cfg);
   if (g_gemm_areg && !g_gemm_cfg && a.K < 256 && a.K % 64 != 0 && !a.out_f32 && a.M > 128 && gemm_areg_ok(a, 256))
     cfg = CFG_64_AREG;

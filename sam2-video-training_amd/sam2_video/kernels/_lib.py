@@ -48,6 +48,7 @@ SIGNATURES = {
     "s2h_gemm_split_target": [I],
     "s2h_gemm_tiny_config": [I],
     "s2h_gemm_w41": [I],
+    "s2h_gemm_class_config": [I, I],
     "s2h_gemm_areg": [I],
     "s2h_wgrad_workspace": [P, L, I],
     "s2h_grad_defer": [P, L, P, L],
@@ -202,6 +203,9 @@ def lib():
             h.s2h_gemm_areg(int(os.environ["S2H_GEMM_AREG"]))
         if os.environ.get("S2H_FLASH_QS"):  # ... forward 16-query sets per wave, V-fold | plain << 4 (A/B)
             h.s2h_flash_fwd_sets(int(os.environ["S2H_FLASH_QS"]))
+        if os.environ.get("S2H_GEMM_CLASS"):  # tiling per GEMM class "c0,c1,c2,c3" (0 = rules; A/B)
+            for i, c in enumerate(os.environ["S2H_GEMM_CLASS"].split(",")[:4]):
+                h.s2h_gemm_class_config(i, int(c or 0))
         if os.environ.get("S2H_GEMM_W41"):  # ... bf16-output GEMMs on 4 x 1 wave grids (A/B)
             h.s2h_gemm_w41(int(os.environ["S2H_GEMM_W41"]))
         _LIB = h
