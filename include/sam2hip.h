@@ -117,6 +117,11 @@ int s2h_gemm_w41(int mode);
  * M >= 8192; 2: K <= 512 and N >= 768; 3: 256 < K < 1024 and N <= 512.  Returns the previous
  * setting (-1: no such class). */
 int s2h_gemm_class_config(int cls, int cfg);
+/* A/B knob (round 6): bf16-output GEMMs with M <= 128, K >= 1024 and at most 16 64 x 64 output tiles as
+ * one split-K fp32 launch into the weight-gradient workspace + one fixed-order reduce running the
+ * GEMM epilogue (1: on; 0: the one-launch tiling, the default -- measured step-neutral); mode < 0 only queries.  Returns the
+ * previous mode. */
+int s2h_gemm_tiny_splitk(int mode);
 /* A/B knob: GEMMs with a short K that is not a multiple of 64 (K < 256, K-contiguous A, bf16 output)
  * on the A-in-registers tiling (1: on, the default; 0: off); results are bit-identical.  Returns the
  * previous mode. */

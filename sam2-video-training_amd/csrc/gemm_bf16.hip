@@ -121,10 +121,86 @@ static int pick_cfg(const GemmArgs16& a, int batch) {
   return CFG_64;
 }
 
+// Tiny-M long-K GEMMs with a bf16 output (M <= 128, K >= 1024, <= 16 output tiles of 64 x 64; round 6):
+// the two-way decoder's token MLP second layer, 104 x 256 x 2048 (transformer.py:219-245, frame-batched
+// forward per frame), ran as 8 workgroups of 32 K steps each (21 us, profiles/r06_v3_shape_table.txt).
+// The K range is split over S batch entries of ONE fp32 launch into the weight-gradient workspace
+// (no epilogue), then ONE launch adds the S partials in fixed order and runs the GEMM epilogue (bias,
+// activation, dropout, residual, pre-activation store: epilogue4) -- deterministic, the fp32 sum rounded
+// once.  Opt-in (S2H_GEMM_TINY_SPLITK=1, s2h_gemm_tiny_splitk): 47.73 / 47.81 ms per bench step against
+// 47.63 / 47.83 for the one-launch tiling (in-call A/B) -- no gain, so the one-launch tiling stays.
+float* s2h_det_ws(int64_t bytes);  // gemm_wgrad.hip: the registered workspace (nullptr: none / off)
+static int g_gemm_tiny_splitk = 0;  // measured neutral in-step (profiles/r06_v9_tiny_splitk_ab.log): opt-in
+extern "C" int s2h_gemm_tiny_splitk(int mode) {
+  const int prev = g_gemm_tiny_splitk;
+  if (mode >= 0) g_gemm_tiny_splitk = mode;
+  return prev;
+}
+
+__global__ __launch_bounds__(256) void gemm_splitk_epi_kernel(GemmArgs16 p, const float* part, int S) {
+  if (p.drop_p > 0.f) p.seed = s2h_seed(p.seed, p.seed_off);  // the device RNG offset, as every dropout site
+  const int nq = (p.N + 3) / 4;
+  const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (q >= (int64_t)p.M * nq) return;
+  const int row = (int)(q / nq), col0 = (int)(q % nq) * 4;
+  const int64_t MN = (int64_t)p.M * p.N;
+  const float* pp = part + (int64_t)row * p.N + col0;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  if (col0 + 4 <= p.N && (p.N & 3) == 0) {
+    for (int sp = 0; sp < S; ++sp) {
+      const float4 t = *(const float4*)(pp + sp * MN);
+      v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+    }
+  } else {
+    for (int sp = 0; sp < S; ++sp)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (col0 + e < p.N) v[e] += pp[sp * MN + e];
+  }
+  float bcol[4];
+  load_bcol(p, col0, bcol);
+  epilogue4(p, 0, row, col0, float4{v[0], v[1], v[2], v[3]}, bcol);
+}
+
+static int gemm_tiny_splitk(const GemmArgs16& a, int batch, hipStream_t st) {
+  if (!g_gemm_tiny_splitk || batch != 1 || a.out_f32 || a.M > 128 || a.K < 1024 || a.lda_k != 1 || a.ldb_k != 1 ||
+      a.rowsum != nullptr || a.rope_cos != nullptr)
+    return -1;
+  const int tiles = ((a.M + 63) / 64) * ((a.N + 63) / 64);
+  if (tiles > 16) return -1;
+  int S = 16;
+  while (S > 1 && (a.K % (64 * S) != 0 || tiles * S > 256)) S /= 2;
+  if (S < 4) return -1;
+  float* ws = s2h_det_ws((int64_t)S * a.M * a.N * 4);
+  if (ws == nullptr) return -1;
+  GemmArgs16 b = {};
+  b.M = a.M; b.N = a.N; b.K = a.K / S;
+  b.A = a.A; b.lda_m = a.lda_m; b.lda_k = 1; b.sA = a.K / S;
+  b.B = a.B; b.ldb_k = 1; b.ldb_n = a.ldb_n; b.sB = a.K / S;
+  b.C = ws; b.ldc = a.N; b.sC = (int64_t)a.M * a.N;
+  b.alpha = 1.f; b.beta = 0.f; b.out_f32 = 1;
+  b.vecA = a.vecA; b.vecB = a.vecB;
+  b.dbg = a.dbg;
+  if (!gemm_glds_ok(b, S)) return -1;
+  int rc = gemm_cfg_launch_1(CFG_64_NS4, b, S, st);
+  if (rc != 0) return rc;
+  GemmArgs16 e = a;
+  e.splits = 1;
+  e.kchunk = a.K;
+  gemm_plan_vec(e, 1);
+  const int64_t nq = (int64_t)a.M * ((a.N + 3) / 4);
+  hipLaunchKernelGGL(gemm_splitk_epi_kernel, dim3((unsigned)((nq + 255) / 256)), dim3(256), 0, st, e, ws, S);
+  return (int)hipGetLastError();
+}
+
 int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   GemmArgs16 a = in;
   a.dbg = g_gemm_dbg;
-  if (!g_gemm_cfg && a.out_f32 && a.K >= 1024) {  // long-reduction weight gradients (gemm_wgrad.hip)
+  if (!g_gemm_cfg && !g_gemm_tiny_cfg) {
+    const int rc = gemm_tiny_splitk(a, batch, st);
+    if (rc >= 0) return rc;
+  }
+  if (!g_gemm_cfg && a.out_f32 && a.K >= 512) {  // long / mid-reduction weight gradients (gemm_wgrad.hip)
     const int rc = s2h_gemm_wgrad_det(a, batch, st);
     if (rc >= 0) return rc;
   }

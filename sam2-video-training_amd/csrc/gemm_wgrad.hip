@@ -316,7 +316,11 @@ int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st) {
   // every reduction the split-K path would split (plan_splits: < 512 tiles of 128 x 64, K >= 1024), and
   // every reduction of >= kmin rows
   const long t128x64 = (long)((a.M + 127) / 128) * ((a.N + 63) / 64);
-  if (!plain || a.K < 1024 || (a.K < g_wg_kmin && t128x64 >= 512)) return -1;
+  // round 6: also the mid-length reductions (512 <= K < 1024) of few output tiles -- the two-way decoder's
+  // frame-batched weight gradients (832 token rows: 256 x 256, 256 x 2048, ...), which ran as 16-64
+  // unsplit 64 x 64 workgroups of 13 K steps (~23 us each, profiles/r06_v3_shape_table.txt)
+  const bool mid = a.K >= 512 && a.K < 1024 && t128x64 <= 64;
+  if (!plain || (a.K < 1024 && !mid) || (a.K < g_wg_kmin && t128x64 >= 512)) return -1;
   if (a.lda_m != 1 || a.ldb_n != 1 || a.M < 16 || a.N < 64) return -1;
   // operand extents rounded up to 8 inside the row pitch (the DMA moves 8-element pieces; the extra
   // rows / columns are read, never stored)
@@ -336,7 +340,7 @@ int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st) {
   for (int c = 0; c < 6; ++c) {
     const int bm = cands[c].bm, bn = cands[c].bn;
     const long tiles = (long)((a.M + bm - 1) / bm) * ((a.N + bn - 1) / bn);
-    const int smax = std::max(1, std::min(256, a.K / 512));
+    const int smax = std::max(1, std::min(256, a.K / (mid ? 128 : 512)));
     for (int sp = 1; sp <= smax; ++sp) {
       const long kchunk = ((a.K + sp - 1) / sp + 63) / 64 * 64;
       const long wgs = tiles * sp;

@@ -49,6 +49,7 @@ SIGNATURES = {
     "s2h_gemm_tiny_config": [I],
     "s2h_gemm_w41": [I],
     "s2h_gemm_class_config": [I, I],
+    "s2h_gemm_tiny_splitk": [I],
     "s2h_gemm_areg": [I],
     "s2h_wgrad_workspace": [P, L, I],
     "s2h_grad_defer": [P, L, P, L],
@@ -206,6 +207,8 @@ def lib():
         if os.environ.get("S2H_GEMM_CLASS"):  # tiling per GEMM class "c0,c1,c2,c3" (0 = rules; A/B)
             for i, c in enumerate(os.environ["S2H_GEMM_CLASS"].split(",")[:4]):
                 h.s2h_gemm_class_config(i, int(c or 0))
+        if os.environ.get("S2H_GEMM_TINY_SPLITK"):  # split-K + reduce-epilogue for tiny-M long-K GEMMs (A/B)
+            h.s2h_gemm_tiny_splitk(int(os.environ["S2H_GEMM_TINY_SPLITK"]))
         if os.environ.get("S2H_GEMM_W41"):  # ... bf16-output GEMMs on 4 x 1 wave grids (A/B)
             h.s2h_gemm_w41(int(os.environ["S2H_GEMM_W41"]))
         _LIB = h

@@ -192,7 +192,7 @@ def gemm(a, b, c, *, M, N, K, lda_m, lda_k, ldb_k, ldb_n, ldc, batch=1, sA=0, sB
     _dev(a, b, c, bias, residual, aux)
     if bias is not None:
         assert bias.dtype == torch.float32 and bias.is_contiguous()
-    if c.dtype == torch.float32 and K >= 1024 and "t" not in _WG_WS:
+    if c.dtype == torch.float32 and K >= 512 and "t" not in _WG_WS:
         wgrad_workspace(c.device)
     call("s2h_gemm", dt(a), dt(c), batch, M, N, K,
          ptr(a), lda_m, lda_k, sA, ptr(b), ldb_k, ldb_n, sB, ptr(c), ldc, sC,
@@ -450,7 +450,7 @@ def linear_wgrad(dy, x, dw, accumulate=True, db=None):
     if db is not None:
         assert db.dtype == torch.float32 and db.numel() == N and db.is_contiguous()
     _dev(dy2, x2, dw, db)
-    if M >= 1024 and "t" not in _WG_WS:
+    if M >= 512 and "t" not in _WG_WS:
         wgrad_workspace(dw.device)
     call("s2h_linear_wgrad", dt(dy2), M, N, K, ptr(dy2), dy2.stride(0), ptr(x2), x2.stride(0), ptr(dw), dw.stride(0),
          ptr(db), int(accumulate), stream())

@@ -1384,3 +1384,40 @@ def test_mlp_heads_bit_identical(M):
             assert torch.equal(a, b)
         if rp is not None:
             assert torch.equal(p, rp)
+
+
+@pytest.mark.parametrize("M,N,K", [(104, 256, 2048), (13, 256, 1024), (128, 64, 4096), (100, 250, 2048)])
+def test_tiny_m_splitk_gemm_matches_one_launch_tiling(M, N, K):
+    """round 6: bf16-output GEMMs with M <= 128 and K >= 1024 run as a split-K fp32 launch + a fixed-order
+    reduce that applies the GEMM epilogue (gemm_bf16.hip gemm_tiny_splitk); against the one-launch tiling
+    (s2h_gemm_tiny_splitk(0)) and the fp32 torch reference, with bias + GELU (+ pre-activation store),
+    dropout and residual; bit-identical on repeat"""
+    ops = _ops()
+    from sam2_video.kernels._lib import lib
+    torch.manual_seed(11)
+    bf = torch.bfloat16
+    x = torch.randn(M, K, device=DEV).to(bf)
+    w = (torch.randn(N, K, device=DEV) * K ** -0.5).to(bf)
+    b = torch.randn(N, device=DEV)
+    r = torch.randn(M, N, device=DEV).to(bf)
+    ref = x.float() @ w.float().t() + b
+    outs = {}
+    for mode in (1, 0, 1):  # (the split path is opt-in: forced on / off here)
+        prev = lib().s2h_gemm_tiny_splitk(mode)
+        try:
+            pre = torch.empty(M, N, device=DEV, dtype=bf)
+            y = ops.linear(x, w, b, act="gelu", pre=pre)
+            yd = ops.linear(x, w, b, residual=r, drop_p=0.1, seed=5)
+        finally:
+            lib().s2h_gemm_tiny_splitk(prev)
+        torch.cuda.synchronize()
+        if mode in outs:
+            assert all(torch.equal(u, v) for u, v in zip(outs[mode], (y, pre, yd)))
+        outs[mode] = (y, pre, yd)
+    y, pre, yd = outs[1]
+    _close(pre, ref, 1e-2)
+    _close(y, torch.nn.functional.gelu(ref), 1e-2)
+    keep = outs[0][2] != r  # the one-launch tiling's dropout mask (same seed and element indices)
+    _close(yd.float(), torch.where(keep, ref / 0.9 + r.float(), r.float()), 2e-2)
+    for u, v in zip(outs[1], outs[0]):
+        _close(u, v, 1e-2)
