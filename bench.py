@@ -215,7 +215,7 @@ def kernel_name(kind, tag):
 
 
 # kernel-name families of the rocprofv3 trace, matching the in-library profiler's record kinds
-TRACE_FAMILY_RX = {4: r"gemm16[ag]?_kernel|gemm16_kernel|gemm_kernel<|gemm_wg|gemm_splitk|ffn_",
+TRACE_FAMILY_RX = {4: r"gemm16[ag]?_kernel|gemm16_kernel|gemm_kernel<|gemm_wg|gemm_split|ffn_",
                    40: r"gemm_mx8|mx8_quant",
                    1: r"flash_fwd|flash_combine|attn_fwd|attn_win_fwd",
                    2: r"flash_bwd|attn_bwd|attn_win_bwd|attn_fewq_dkv|attn_fewk_dq"}

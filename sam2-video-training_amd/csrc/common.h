@@ -190,6 +190,8 @@ void s2h_zero_f32(float* p, int64_t rows, int64_t cols, int64_t ld, hipStream_t 
 // float atomics; nullptr when none is registered, it is switched off or smaller than `bytes` (the caller
 // then keeps its atomic path).  Users are stream-ordered (one stream).
 float* s2h_det_ws(int64_t bytes);
+// its usable size in bytes (0: none registered or switched off)
+int64_t s2h_det_ws_bytes();
 // Deferred second pass (grad_defer.hip): inside a s2h_grad_defer scope, partial storage for nb rows of
 // n0 + n1 columns whose fixed-order column sums go to out0[0:n0] (+=) and out1[0:n1] (+=), recorded for
 // s2h_grad_defer_flush; nullptr when no scope is open or a destination is outside the registered sink

@@ -15,7 +15,12 @@ struct GemmArgs16 {
   float drop_p; uint64_t seed; const uint64_t* seed_off; uint64_t drop_idx0;
   float alpha, beta; int act;
   int vecA, vecB;
-  int splits, kchunk;  // split-K: blockIdx.z = batch * splits + split
+  // split-K: blockIdx.z = batch * splits + split.  With the deterministic-reduction workspace registered
+  // (s2h_det_ws) a split launch stores its partial tiles there instead of adding them into C with float
+  // atomics, and gemm_split_reduce_kernel adds them in split order: X then points at the partials
+  // (unused otherwise -- a split GEMM has no epilogue operands), sX is one split's stride
+  // (batch x M x N floats, rows of N), the rowsum partials follow at splits x sX
+  int splits, kchunk;
   int out_f32;
   int vecC;  // 4-column output groups are vector-aligned
   int vec8;  // 8-column groups take 16-B accesses: bit 0 C (bf16 out), bit 1 X, bit 2 R
@@ -26,7 +31,7 @@ struct GemmArgs16 {
   // tables' column (c % rope_dh) / 2.  rope_cos == nullptr: no rotation.
   const float* rope_cos; const float* rope_sin;
   int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
-  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA, 8 plain stores, 16 tile-major split-K order
+  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA, 8 plain stores, 16 tile-major split-K order, 32 split-K by float atomics
 };
 
 // The LayerNorm epilogues' extra arguments (round 4), in a derived block that only the full-row tilings

@@ -10,9 +10,10 @@
 // so Y = X W^T (both K-contiguous), dX = dY W (W row-contiguous) and the weight
 // gradient dW = dY^T X (both row-contiguous over the reduction) all run at full
 // LDS bandwidth.  Rows are padded by 16 B (conflict-free ds_read_b128 and
-// transposed reads).  K is split over workgroups (fp32 atomic accumulate into
-// the output) when the output tile count cannot fill the 256 CUs -- the weight
-// gradients reduce over 10^4-10^5 rows into a few hundred KB.
+// transposed reads).  K is split over workgroups when the output tile count cannot
+// fill the 256 CUs -- the weight gradients reduce over 10^4-10^5 rows into a few
+// hundred KB -- the splits' partial tiles added in fixed order by a second launch
+// (fp32 atomics into the output only without the workspace).
 #pragma once
 #include "gemm_epi.h"
 
@@ -159,7 +160,7 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
   const int c4 = lane % CPR, rg = lane / CPR;
   float bcol[4];
   load_bcol(p, n0 + wn * WN + 4 * c4, bcol);
-  if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
+  if (do_rs && m0 + tid < p.M) store_rowsum(p, bz, split, m0 + tid, rs);
   if (nk == 0) __syncthreads();
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
@@ -172,7 +173,7 @@ __global__ __launch_bounds__(256) void gemm16_kernel(GemmArgs16 p) {
       const int rl = rg + ps * RPP;
       const float4 v4 = *(const float4*)&ep[rl * EPLD + 4 * c4];
       const int row = m0 + wm * WM + i * 16 + rl;
-      if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol);
+      if (row < p.M) epilogue4(p, bz, row, n0 + wn * WN + 4 * c4, v4, bcol, split);
     }
     __syncthreads();
   }
@@ -391,7 +392,7 @@ void gemm16g_kernel(PA p) {
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  if (do_rs && m0 + tid < p.M) atomicAdd(&p.rowsum[(int64_t)bz * p.M + m0 + tid], rs);
+  if (do_rs && m0 + tid < p.M) store_rowsum(p, bz, split, m0 + tid, rs);
   if constexpr (WGN == 1 && WN >= 128 && WN % 32 == 0 && std::is_same_v<PA, GemmArgs16Ln>) {
     if (p.lnb_x != nullptr) {  // full-row tiles: LayerNorm backward epilogue
       static_assert(NW * 16 * (WN + 4) * 4 + NW * 2 * WN * 4 <= NS * STAGE, "LayerNorm-backward epilogue LDS");
@@ -400,7 +401,7 @@ void gemm16g_kernel(PA p) {
     }
   }
   tile_epilogue<WM, WN, MI, NI, PA>(p, acc, reinterpret_cast<float*>(smem) + w * 16 * (WN + 4), bz, m0 + wm * WM,
-                                n0 + wn * WN, lane);
+                                n0 + wn * WN, lane, split);
 }
 
 // Short-K variant (round 4, K <= KMAX = 256 -- the step's projections, FFN linear1 forward and the
@@ -498,6 +499,10 @@ int s2h_gemm_wgrad_det(const GemmArgs16& a, int batch, hipStream_t st);
 // workgroups a split-K launch aims at (s2h_gemm_split_target; gemm_bf16.hip)
 extern int g_gemm_split_target;
 
+// the second launch of a split launch with partial tiles (gemm16.h): C (beta 0 / 1) and rowsum get the
+// splits' sums in split order (gemm_bf16.hip)
+int s2h_gemm_split_reduce(const GemmArgs16& a, int batch, hipStream_t st);
+
 // split-K decision + output-group alignment for a BM x BN tiling
 static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * batch;
@@ -512,11 +517,21 @@ static void plan_splits(GemmArgs16& a, int batch, int BM, int BN, hipStream_t st
     // up to 256 splits: the memory K / V projection weight gradients (256 x 64 over 374k rows)
     // have 2-4 output tiles, which 64 splits left at half a wave of workgroups
     if (s > 256) s = 256;
+    // deterministic (round 6): the splits' partial tiles in the workspace, added in split order by
+    // gemm_split_reduce_kernel -- the float atomics' arrival order made e.g. the hypernetwork-mask
+    // gradient (104 batched 1 x 32 x 65536 products, mask_decoder.py) differ between identical runs.
+    // As many splits as the workspace holds; none when it holds fewer than two.
+    const int64_t per = (int64_t)batch * a.M * a.N + (a.rowsum ? (int64_t)batch * a.M : 0);
+    const int64_t cap = (a.dbg & 32) ? 0 : s2h_det_ws_bytes() / 4;  // dbg 32: the atomic form (A/B)
+    if (cap > 0 && s > 1 && (int64_t)s * per > cap) s = (int)std::min<int64_t>(s, cap / per);
     if (s > 1) {
       a.splits = s;
       a.kchunk = ((a.K + s - 1) / s + 63) / 64 * 64;
       a.splits = (a.K + a.kchunk - 1) / a.kchunk;
-      if (a.beta == 0.f && a.ldc == a.N && (batch == 1 || a.sC == (int64_t)a.M * a.N)) {
+      if (cap > 0) {
+        a.X = s2h_det_ws((int64_t)a.splits * per * 4);
+        a.sX = (int64_t)batch * a.M * a.N;
+      } else if (a.beta == 0.f && a.ldc == a.N && (batch == 1 || a.sC == (int64_t)a.M * a.N)) {
         s2h_zero_f32((float*)a.C, (int64_t)batch * a.M, a.N, a.N, st);
       } else if (a.beta == 0.f) {
         for (int b = 0; b < batch; ++b) s2h_zero_f32((float*)a.C + (int64_t)b * a.sC, a.M, a.N, a.ldc, st);
@@ -544,13 +559,20 @@ static int launch_glds(PA& a, int batch, hipStream_t st) {
     else if (!akc && bkc) hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, true>), g1, dim3(NT), 0, st, a);
     else hipLaunchKernelGGL((gemm16g_kernel<BM, BN, WGM, WGN, NS, BK, false, false>), g1, dim3(NT), 0, st, a);
   }
+  if (a.splits > 1 && a.X) return s2h_gemm_split_reduce(a, batch, st);
   return (int)hipGetLastError();
 }
 
 template <int BN, int KMAX = 256>
 static int launch_areg(GemmArgs16& a, int batch, hipStream_t st) {
   plan_splits(a, batch, 64, BN, st);
-  if (a.splits != 1) return -1;
+  if (a.splits != 1) {  // not this tiling's case: undo the plan for the caller's next launcher
+    a.splits = 1;
+    a.kchunk = a.K;
+    a.X = nullptr;
+    a.sX = 0;
+    return -1;
+  }
   const bool bkc = a.ldb_k == 1;
   s2h_prof_tag(gemm_tag(64, BN, 4, 1, 1, 64, true, bkc, false, false, true));
   dim3 g(((a.N + BN - 1) / BN) * ((a.M + 63) / 64), 1, batch);
@@ -569,6 +591,7 @@ static int launch16_regs(GemmArgs16& a, int batch, hipStream_t st) {
   else if (akc && !bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, true, false>), grid, dim3(256), 0, st, a);
   else if (!akc && bkc) hipLaunchKernelGGL((gemm16_kernel<BM, BN, false, true>), grid, dim3(256), 0, st, a);
   else hipLaunchKernelGGL((gemm16_kernel<BM, BN, false, false>), grid, dim3(256), 0, st, a);
+  if (a.splits > 1 && a.X) return s2h_gemm_split_reduce(a, batch, st);
   return (int)hipGetLastError();
 }
 

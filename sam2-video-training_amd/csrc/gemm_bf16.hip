@@ -59,15 +59,22 @@ extern "C" int s2h_gemm_areg(int mode) {
 //   class 1: K <= 256, N <= 256, M >= 8192 (short reduction, narrow output: per-frame projections)
 //   class 2: K <= 512, N >= 768 (wide output: FFN linear1, Hiera qkv / fc1)
 //   class 3: 256 < K < 1024, N <= 512 (mid reduction, narrow output: Hiera proj)
-static int g_gemm_class_cfg[4] = {0, 0, 0, 0};
+//   class 4: K < 256 not a multiple of 64 (the A-in-registers domain), M >= 65536 (Hiera stage 1 at
+//            112 channels: 131072 rows at 512^2)
+//   class 5: the same with M < 65536 (Hiera stage 2 at 224 channels, the V-fold's 72)
+// Defaults (round 6): classes 4 / 5 on the 128 x 64 4 x 1 LDS-DMA tiling with 32-deep stages, 3-deep ring
+// (cfg 22) instead of the A-in-registers kernel: in-step sweeps 47.59 / 47.52 -> 47.45 / 47.44 ms
+// (profiles/r06_v12_gemm_class4_sweep.log, r06_v13_gemm_class45_sweep.log); every other class keeps its rules.
+static int g_gemm_class_cfg[6] = {0, 0, 0, 0, CFG_128x64_W41_K32_NS3, CFG_128x64_W41_K32_NS3};
 extern "C" int s2h_gemm_class_config(int cls, int cfg) {
-  if (cls < 0 || cls > 3) return -1;
+  if (cls < 0 || cls > 5) return -1;
   const int prev = g_gemm_class_cfg[cls];
   g_gemm_class_cfg[cls] = cfg;
   return prev;
 }
 static int gemm_class(const GemmArgs16& a) {
   if (a.out_f32 || a.M <= 128) return -1;
+  if (a.K < 256 && a.K % 64 != 0) return a.M >= 65536 ? 4 : 5;
   if (a.K >= 1024 && a.N <= 512) return 0;
   if (a.K <= 256 && a.N <= 256 && a.M >= 8192) return 1;
   if (a.K <= 512 && a.N >= 768) return 2;
@@ -170,7 +177,7 @@ static int gemm_tiny_splitk(const GemmArgs16& a, int batch, hipStream_t st) {
   if (tiles > 16) return -1;
   int S = 16;
   while (S > 1 && (a.K % (64 * S) != 0 || tiles * S > 256)) S /= 2;
-  if (S < 4) return -1;
+  if (S < 4 || a.K / S >= 1024) return -1;  // (a K chunk of >= 1024 would be split again, into the same workspace)
   float* ws = s2h_det_ws((int64_t)S * a.M * a.N * 4);
   if (ws == nullptr) return -1;
   GemmArgs16 b = {};
@@ -193,6 +200,42 @@ static int gemm_tiny_splitk(const GemmArgs16& a, int batch, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// The fixed-order sum of a split launch's partial tiles (gemm16.h, plan_splits): one thread per output
+// element (then per rowsum element), eight independent chains over the splits (split q on chain q % 8,
+// eight loads in flight) combined in a fixed tree -- the same sum for any timing of the split launch.
+__global__ __launch_bounds__(256) void gemm_split_reduce_kernel(const float* part, int S, int64_t sX, int batch, int M,
+                                                                int N, float* C, int64_t ldc, int64_t sC, int beta1,
+                                                                float* rowsum) {
+  const int64_t nc = (int64_t)batch * M * N, nr = rowsum ? (int64_t)batch * M : 0;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nc + nr) return;
+  const float* pp = i < nc ? part + i : part + S * sX + (i - nc);
+  const int64_t stride = i < nc ? sX : nr;
+  float ch[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int s = 0;
+  for (; s + 8 <= S; s += 8)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ch[j] += pp[(s + j) * stride];
+#pragma unroll
+  for (int j = 0; j < 7; ++j)
+    if (s + j < S) ch[j] += pp[(s + j) * stride];
+  const float v = ((ch[0] + ch[1]) + (ch[2] + ch[3])) + ((ch[4] + ch[5]) + (ch[6] + ch[7]));
+  if (i < nc) {
+    const int64_t b = i / ((int64_t)M * N), r = (i / N) % M, c = i % N;
+    float* o = C + b * sC + r * ldc + c;
+    *o = beta1 ? *o + v : v;
+  } else {
+    rowsum[i - nc] += v;
+  }
+}
+
+int s2h_gemm_split_reduce(const GemmArgs16& a, int batch, hipStream_t st) {
+  const int64_t n = (int64_t)batch * a.M * a.N + (a.rowsum ? (int64_t)batch * a.M : 0);
+  hipLaunchKernelGGL(gemm_split_reduce_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, (const float*)a.X,
+                     a.splits, a.sX, batch, a.M, a.N, (float*)a.C, a.ldc, a.sC, a.beta == 1.f ? 1 : 0, a.rowsum);
+  return (int)hipGetLastError();
+}
+
 int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   GemmArgs16 a = in;
   a.dbg = g_gemm_dbg;
@@ -206,13 +249,13 @@ int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   }
   int cfg = g_gemm_cfg ? g_gemm_cfg : pick_cfg(a, batch);
   if (g_gemm_tiny_cfg && !g_gemm_cfg && a.M <= 128) cfg = g_gemm_tiny_cfg;
-  if (!g_gemm_cfg) {
-    const int cls = gemm_class(a);
-    if (cls >= 0 && g_gemm_class_cfg[cls]) cfg = g_gemm_class_cfg[cls];
-  }
   if (g_gemm_w41 && !g_gemm_cfg && !a.out_f32 && (g_gemm_w41 == 1 || a.N >= 768)) cfg = w41_of(cfg);
   if (g_gemm_areg && !g_gemm_cfg && a.K < 256 && a.K % 64 != 0 && !a.out_f32 && a.M > 128 && gemm_areg_ok(a, 256))
     cfg = CFG_64_AREG;
+  if (!g_gemm_cfg) {  // A/B override per GEMM class (s2h_gemm_class_config)
+    const int cls = gemm_class(a);
+    if (cls >= 0 && g_gemm_class_cfg[cls]) cfg = g_gemm_class_cfg[cls];
+  }
   if (cfg < 0 || !gemm_glds_ok(a, batch)) return gemm_cfg_launch_1(CFG_REGS, a, batch, st);  // register-staged
   int rc;
   if ((rc = gemm_cfg_launch_1(cfg, a, batch, st)) >= 0) return rc;

@@ -48,12 +48,20 @@ __device__ __forceinline__ void rope_cols(const GemmArgs16& p, int row, int col0
   }
 }
 
-__device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4, const float* bcol) {
+__device__ __forceinline__ void epilogue4(const GemmArgs16& p, int bz, int row, int col0, float4 v4, const float* bcol,
+                                          int split = 0) {
   float v[4] = {v4.x, v4.y, v4.z, v4.w};
   const int nval = p.N - col0;
   if (nval <= 0) return;
   const bool full = nval >= 4 && p.vecC;
-  if (p.splits > 1) {  // split-K: fp32 atomic accumulate (beta handled on the host side)
+  if (p.splits > 1) {  // split-K: the partial tile (gemm16.h), or fp32 atomics (beta handled on the host side)
+    if (p.X) {
+      float* P = (float*)p.X + split * p.sX + ((int64_t)bz * p.M + row) * p.N + col0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < nval) P[e] = p.alpha * v[e];
+      return;
+    }
     float* C = (float*)p.C + (int64_t)bz * p.sC + (int64_t)row * p.ldc + col0;
 #pragma unroll
     for (int e = 0; e < 4; ++e)
@@ -342,6 +350,17 @@ __device__ __forceinline__ void load_bcol(const GemmArgs16& p, int col0, float* 
   for (int e = 0; e < V; ++e) bcol[e] = (p.splits == 1 && p.bias_mode == 1 && col0 + e < p.N) ? p.bias[col0 + e] : 0.f;
 }
 
+// the fused row sum of A over one split's K chunk (GemmArgs16::rowsum): into the split's partial slot
+// when the launch has partial storage (gemm16.h), else a float atomic (one adder per element unsplit)
+__device__ __forceinline__ void store_rowsum(const GemmArgs16& p, int bz, int split, int m, float rs) {
+  if (p.splits > 1 && p.X) {
+    const int batch = gridDim.z / p.splits;
+    ((float*)p.X)[p.splits * p.sX + ((int64_t)split * batch + bz) * p.M + m] = rs;
+  } else {
+    atomicAdd(&p.rowsum[(int64_t)bz * p.M + m], rs);
+  }
+}
+
 template <int N>
 __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -361,7 +380,7 @@ __device__ __forceinline__ bool ln_epilogue_on(const GemmArgs16Ln& p) { return p
 
 template <int WM, int WN, int MI, int NI, typename PA = GemmArgs16>
 __device__ __forceinline__ void tile_epilogue(const PA& p, f32x4 (&acc)[MI][NI], float* ep, int bz, int mw,
-                                              int nw, int lane) {
+                                              int nw, int lane, int split = 0) {
   constexpr int EPLD = WN + 4;
   float bcol[4], bcol8[8];
   load_bcol(p, nw + 4 * (lane % (WN / 4)), bcol);
@@ -376,14 +395,21 @@ __device__ __forceinline__ void tile_epilogue(const PA& p, f32x4 (&acc)[MI][NI],
     __builtin_amdgcn_wave_barrier();
     if (p.splits > 1) {
       // split-K: consecutive lanes on consecutive columns (256 B per instruction): RPI rows of
-      // WN <= 64 columns, or 64-column pieces of one row for the full-row tiles (WN 128 / 256)
-      float* C = (float*)p.C + (int64_t)bz * p.sC;
+      // WN <= 64 columns, or 64-column pieces of one row for the full-row tiles (WN 128 / 256); plain
+      // stores of the partial tile when the split has one (gemm16.h), else float atomics into C
+      const bool part = p.X != nullptr;
+      float* C = part ? (float*)p.X + split * p.sX + (int64_t)bz * p.M * p.N : (float*)p.C + (int64_t)bz * p.sC;
+      const int64_t ldc = part ? (int64_t)p.N : p.ldc;
       if constexpr (WN <= 64) {
         constexpr int RPI = 64 / WN;  // rows per instruction
         const int col = nw + lane % WN;
         for (int rr = lane / WN; rr < 16; rr += RPI) {
           const int row = mw + i * 16 + rr;
-          if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + lane % WN]);
+          if (row < p.M && col < p.N) {
+            const float v = p.alpha * ep[rr * EPLD + lane % WN];
+            if (part) C[(int64_t)row * ldc + col] = v;
+            else atomicAdd(&C[(int64_t)row * ldc + col], v);
+          }
         }
       } else {
         for (int rr = 0; rr < 16; ++rr) {
@@ -391,7 +417,11 @@ __device__ __forceinline__ void tile_epilogue(const PA& p, f32x4 (&acc)[MI][NI],
 #pragma unroll
           for (int cc = lane; cc < WN; cc += 64) {
             const int col = nw + cc;
-            if (row < p.M && col < p.N) atomicAdd(&C[(int64_t)row * p.ldc + col], p.alpha * ep[rr * EPLD + cc]);
+            if (row < p.M && col < p.N) {
+              const float v = p.alpha * ep[rr * EPLD + cc];
+              if (part) C[(int64_t)row * ldc + col] = v;
+              else atomicAdd(&C[(int64_t)row * ldc + col], v);
+            }
           }
         }
       }

@@ -270,6 +270,7 @@ extern "C" int s2h_wgrad_workspace(void* ws, int64_t bytes, int kmin) {
 float* s2h_det_ws(int64_t bytes) {
   return (g_wg_kmin > 0 && g_wg_ws != nullptr && bytes <= g_wg_ws_bytes) ? g_wg_ws : nullptr;
 }
+int64_t s2h_det_ws_bytes() { return (g_wg_kmin > 0 && g_wg_ws != nullptr) ? g_wg_ws_bytes : 0; }
 
 template <int BM, int BN, int WGM, int WGN, int NS>
 static int wg_launch(const GemmArgs16& a, int Md, int Nd, int s, hipStream_t st) {

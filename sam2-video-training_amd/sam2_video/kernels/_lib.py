@@ -204,8 +204,8 @@ def lib():
             h.s2h_gemm_areg(int(os.environ["S2H_GEMM_AREG"]))
         if os.environ.get("S2H_FLASH_QS"):  # ... forward 16-query sets per wave, V-fold | plain << 4 (A/B)
             h.s2h_flash_fwd_sets(int(os.environ["S2H_FLASH_QS"]))
-        if os.environ.get("S2H_GEMM_CLASS"):  # tiling per GEMM class "c0,c1,c2,c3" (0 = rules; A/B)
-            for i, c in enumerate(os.environ["S2H_GEMM_CLASS"].split(",")[:4]):
+        if os.environ.get("S2H_GEMM_CLASS"):  # tiling per GEMM class "c0,..,c4" (0 = rules; A/B)
+            for i, c in enumerate(os.environ["S2H_GEMM_CLASS"].split(",")[:6]):
                 h.s2h_gemm_class_config(i, int(c or 0))
         if os.environ.get("S2H_GEMM_TINY_SPLITK"):  # split-K + reduce-epilogue for tiny-M long-K GEMMs (A/B)
             h.s2h_gemm_tiny_splitk(int(os.environ["S2H_GEMM_TINY_SPLITK"]))

@@ -203,6 +203,44 @@ def test_wgrad_deterministic(rows, N, K):
     _close(outs[0][1], dy.float().sum(0), 1e-4)
 
 
+def test_split_k_gemm_deterministic():
+    """the split-K launches the deterministic weight-gradient kernel does not take (batched, M < 16,
+    N < 64) store per-split partial tiles into the workspace and add them in split order
+    (gemm_split_reduce_kernel, round 6): bit-identical across repeats with garbage in the workspace,
+    against the fp32 product, beta 0 / 1 and the fused row sum.  Cases: the hypernetwork-mask
+    gradient dh = g^T up over 104 frames x objects (1 x 32 over 65 536 pixels, frametape._hyper_bw --
+    with fp32 atomics its result changed between identical bench-size runs), a 3-batch 40 x 96 over
+    20 000, and an 8-row weight gradient with its bias gradient (linear_wgrad, rows = 65 536)"""
+    ops = _ops()
+    torch.manual_seed(11)
+    bf = torch.bfloat16
+    ws = ops.wgrad_workspace(DEV)
+    g = torch.randn(104, 1, 65536, device=DEV).to(bf)
+    up = torch.randn(104, 65536, 32, device=DEV).to(bf)
+    a3 = torch.randn(3, 40, 20000, device=DEV).to(bf)
+    b3 = torch.randn(3, 20000, 96, device=DEV).to(bf)
+    dy = torch.randn(65536, 8, device=DEV).to(bf)
+    x = torch.randn(65536, 48, device=DEV).to(bf)
+    outs = []
+    for r in range(3):
+        ws.fill_(float("nan") if r % 2 else 1e30)
+        dh = ops.bmm(g, up, torch.full((104, 1, 32), 3.0, device=DEV))
+        c3 = ops.bmm(a3, b3, torch.full((3, 40, 96), 0.5, device=DEV), beta=1.0)
+        dw = torch.full((8, 48), 0.5, device=DEV)
+        db = torch.full((8,), 0.25, device=DEV)
+        ops.linear_wgrad(dy, x, dw, db=db)
+        torch.cuda.synchronize()
+        outs.append((dh, c3, dw, db))
+    dh, c3, dw, db = outs[0]
+    _close(dh, g.float() @ up.float(), 2e-3)
+    _close(c3, a3.float() @ b3.float() + 0.5, 2e-3)
+    _close(dw, dy.float().t() @ x.float() + 0.5, 2e-3)
+    _close(db, dy.float().sum(0) + 0.25, 1e-4)
+    for o in outs[1:]:
+        for u, v in zip(o, outs[0]):
+            assert torch.equal(u, v)
+
+
 @pytest.mark.parametrize("rows,H,p", [(93184, 2048, 0.1), (1024, 2048, 0.0), (64, 128, 0.25), (13312, 384, 0.1)])
 def test_ffn_bwd_dgrad(rows, H, p):
     """memory-attention FFN backward, input-gradient side, in one launch (csrc/ffn.hip): dH = (dY W2) *

@@ -265,10 +265,47 @@ def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
         rel = ((g0[n] - g1[n]).abs().max() / g0[n].abs().max()).item()  # max error relative to the tensor's scale
         worst[n] = (round(cos, 6), round(rel, 5))
     print("out_proj / v_proj gradients, fused vs two GEMMs (cosine, max rel err):", worst)
+    # two bf16 computations of the same step that differ in rounding only, compared after the step's
+    # chaotic amplification: measured cosine 0.99983 / max rel 2.2 % with libm erff GELU, 0.99855-0.99885
+    # / 4.3-6.5 % with the branch-free GELU (round 6) -- every other input identical; the bound is the
+    # sibling test's bf16-drift model (test_vfold_step_matches_unfolded_step_bf16: cosine >= 0.98).  A
+    # systematic error of the fused weight gradients is pinned exactly, without the amplification, by
+    # test_vfold_out_projection_weight_gradients_exact below.
     for n, (cos, rel) in worst.items():
-        assert cos >= 0.999, (n, cos)
-        # a systematic bias of the fused weight gradients (G rounded to bf16) would show here
-        assert rel <= 0.03, (n, rel)
+        assert cos >= 0.995, (n, cos)
+        assert rel <= 0.10, (n, rel)
+
+
+def test_vfold_out_projection_weight_gradients_exact():
+    """FN.VFoldOutProj.wgrad (the fused value + output projection's weight gradients: G = dY^T u' in fp32,
+    dWo += G V^T, dV = Wo^T G scattered to dWv / dbv, dbo += colsum dY) against fp64 torch on the same
+    bf16 operands -- the unamplified check of a systematic bias (G rounded to bf16)"""
+    from step_harness import build_model
+    model = build_model("base_plus", 128, ["memory_attention"], "point", dtype="bf16")
+    att = model.memory_attention.layers[1].cross_attn_image
+    fo = att._vfold_out
+    assert fo is not None
+    torch.manual_seed(3)
+    rows = 3000
+    N = fo.out_features
+    dy = (torch.randn(rows, N, device=DEV) * 0.1).to(torch.bfloat16)
+    x = torch.randn(rows, 72, device=DEV).to(torch.bfloat16)
+    x[:, 65:] = 0  # u' = [D M | rowsum(D) | 0]
+    model.arena.zero_grad()
+    fo.wgrad(dy, x)
+    torch.cuda.synchronize()
+    from sam2_video.kernels.functional import _grad_of
+    got = {k: _grad_of(p).detach().double().cpu().clone() for k, p in
+           (("wo", fo.out.weight), ("bo", fo.out.bias), ("wv", fo.vf.lin.weight), ("bv", fo.vf.lin.bias))}
+    v = fo.vf.compute_weight().double().cpu()     # [Nv, 72] = [Wv | bv | 0] (bf16 values)
+    wo = fo.out.compute_weight().double().cpu()   # [N, Nv]
+    G = dy.double().cpu().t() @ x.double().cpu()  # [N, 72]
+    dV = wo.t() @ G
+    ref = {"wo": G @ v.t(), "bo": dy.double().cpu().sum(0), "wv": dV[:, :64], "bv": dV[:, 64]}
+    for k in ref:
+        r, g = ref[k].reshape(got[k].shape), got[k]
+        err = float((g - r).abs().max() / r.abs().max())
+        assert err <= 2e-4, (k, err)
 
 
 @pytest.mark.parametrize("lks,nrots,p_drop", [([1028, 2060], [1024, 2048], 0.1), ([1024, 516], [1024, 512], 0.0)])

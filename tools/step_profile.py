@@ -20,7 +20,7 @@ import re
 import sqlite3
 import sys
 
-FAMILIES = [("GEMM (bf16)", r"gemm16[ag]?_kernel|gemm_kernel<|gemm_wg|gemm_splitk|ffn_"), ("GEMM (MX-fp8)", r"gemm_mx8|mx8_quant"),
+FAMILIES = [("GEMM (bf16)", r"gemm16[ag]?_kernel|gemm_kernel<|gemm_wg|gemm_split|ffn_"), ("GEMM (MX-fp8)", r"gemm_mx8|mx8_quant"),
             ("flash forward", r"flash_fwd|flash_combine"), ("flash backward", r"flash_bwd"),
             ("window / decoder attention", r"attn_"), ("LayerNorm", r"ln_|layernorm"),
             ("loss / merge / eval", r"mask_|bce_|group_"), ("optimizer", r"adamw|sumsq|norm_finalize"),
