@@ -143,8 +143,11 @@ __device__ __forceinline__ void rope_apply(float (&v)[4], const RopeCS& t) {
 enum { DROP_NONE = 0, DROP_BITS = 1, DROP_HASH = 2 };
 
 // ------------------------------------------------------------------ dQ
-template <int DP, int DROP, int DV = DP>
+// NSB: stages in the K / V ring (2, or 3: a tile in flight across the next one's compute, one barrier
+// per tile); PF: LDS fragment reads kept ahead of their MFMAs in the S / dP phase.
+template <int DP, int DROP, int DV = DP, int NSB = 2, int PF = 4>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwdArgs a) {
+  static_assert(NSB == 2 || NSB == 3, "ring depth");
   constexpr bool FOLD = DV != DP;
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   using C = FlashCfg<DP, 64>;
@@ -153,7 +156,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   constexpr int NTV = DV / 32;  // 32-deep d steps of dP
   constexpr int STG = I::TILEB + IV::TILEB;
   // [stage][K | V] + [stage][wave][16 queries x 2 keep words]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + 2 * FL_WAVES * 256];
+  __shared__ __attribute__((aligned(1024))) char smem[NSB * STG + NSB * FL_WAVES * 256];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   if ((a.prio & 2) && w >= 4) __builtin_amdgcn_s_setprio(1);
   const WgIdx wi = wg_xcd_order();
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   constexpr bool bits = DROP == DROP_BITS;
   const uint32_t* KEEPQ = bits ? fr.keep + (int64_t)min(wi.x * FL_QB + w * 16 + ((lane >> 1) & 15), a.Lq - 1) * fr.kw
                                : nullptr;
-  char* bits_lds = smem + 2 * STG + w * 256;
+  char* bits_lds = smem + NSB * STG + w * 256;
   const int npw = I::pieces(w), npv = IV::pieces(w);
   auto dma_bits = [&](int stage, int k0) { lds_dma4(KEEPQ + (k0 >> 5) + (lane & 1), bits_lds + stage * FL_WAVES * 256); };
 
@@ -183,6 +186,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     dma_tile_pad<DP, 64, FL_WAVES, true>(smem, K, a.skl, t0 * C::KT, Lk, w, lane, a.D);
     dma_tile_pad<DV, 64, FL_WAVES, true>(smem + I::TILEB, V, a.svl, t0 * C::KT, Lk, w, lane, FOLD ? DV : a.D);
     if constexpr (bits) dma_bits(0, t0 * C::KT);
+  }
+  if (NSB == 3 && nt > 1) {
+    dma_tile_pad<DP, 64, FL_WAVES, true>(smem + STG, K, a.skl, (t0 + 1) * C::KT, Lk, w, lane, a.D);
+    dma_tile_pad<DV, 64, FL_WAVES, true>(smem + STG + I::TILEB, V, a.svl, (t0 + 1) * C::KT, Lk, w, lane, FOLD ? DV : a.D);
+    if constexpr (bits) dma_bits(1, (t0 + 1) * C::KT);
   }
   const bool qv = q < a.Lq;
   bf16x8 qf[C::NT], gf[NTV];
@@ -228,25 +236,40 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
   for (int d = 0; d < C::ND; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint64_t drow = fr.drow0 + (uint64_t)q * (uint64_t)Lk;
 
+  int cur = 0;  // it % NSB
   for (int it = 0; it < nt; ++it) {
     const int k0 = (t0 + it) * C::KT;
-    char* Kb = smem + (it & 1) * STG;
+    char* Kb = smem + cur * STG;
     char* Vb = Kb + I::TILEB;
-    if (it + 1 < nt) {
-      char* Kn = smem + ((it + 1) & 1) * STG;
-      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, Lk, w, lane, a.D);
-      dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, Lk, w, lane, FOLD ? DV : a.D);
-      // this wave's pieces of tile `it` have landed once all but the ones just issued retired
-      if constexpr (bits) {
-        dma_bits((it + 1) & 1, k0 + C::KT);
-        wait_kv_pieces<I::PPW_LO + 1, IV::PPW_LO>(npw + 1, npv);
+    const int bstage = cur;
+    // this wave's pieces of tile `it` have landed once all but one later tile's retired
+    auto wait_one_ahead = [&]() {
+      if constexpr (bits) wait_kv_pieces<I::PPW_LO + 1, IV::PPW_LO>(npw + 1, npv);
+      else wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
+    };
+    auto issue = [&](int stage, int kk) {
+      char* Kn = smem + stage * STG;
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, kk, Lk, w, lane, a.D);
+      dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, kk, Lk, w, lane, FOLD ? DV : a.D);
+      if constexpr (bits) dma_bits(stage, kk);
+    };
+    if constexpr (NSB == 2) {
+      if (it + 1 < nt) {
+        issue(cur ^ 1, k0 + C::KT);
+        wait_one_ahead();
       } else {
-        wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
+        wait_vmcnt<0>();
       }
+      wg_barrier();
     } else {
-      wait_vmcnt<0>();
+      // tile it + 1 stays in flight across this one; tile it + 2 goes after the barrier into the
+      // buffer every wave finished reading in iteration it - 1
+      if (it + 1 < nt) wait_one_ahead();
+      else wait_vmcnt<0>();
+      wg_barrier();
+      if (it + 2 < nt) issue(cur == 0 ? 2 : cur - 1, k0 + 2 * C::KT);
     }
-    wg_barrier();
+    cur = cur == NSB - 1 ? 0 : cur + 1;
 
     f32x4 s[4], dp[4];
     __builtin_amdgcn_sched_barrier(0);
@@ -265,12 +288,12 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
         }
       }
     }
-    sched_reads_ahead<4 * (C::NT + (NTV < C::NT ? NTV : C::NT)), 4, 1>();
+    sched_reads_ahead<4 * (C::NT + (NTV < C::NT ? NTV : C::NT)), PF, 1>();
     __builtin_amdgcn_sched_barrier(0);
     const bool full = k0 + C::KT <= Lk;
     uint32_t kwords[2] = {0u, 0u};
     if constexpr (bits) {
-      const uint2 t2 = *(const uint2*)(bits_lds + (it & 1) * FL_WAVES * 256 + ql * 8);
+      const uint2 t2 = *(const uint2*)(bits_lds + bstage * FL_WAVES * 256 + ql * 8);
       kwords[0] = t2.x;
       kwords[1] = t2.y;
     }
@@ -324,8 +347,10 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dq_kernel(FlashBwd
     sched_reads_ahead<2 * C::ND, 4, 2>();
     __builtin_amdgcn_sched_barrier(0);
 
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wg_barrier();
+    if constexpr (NSB == 2) {  // every wave's reads of this stage retired before it is refilled
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wg_barrier();
+    }
   }
 
   if (!qv) return;
@@ -754,8 +779,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
 // consecutive queries with one b128.  DMA pieces per stage and wave: Q pieces w, w + 8 (16: wave 0);
 // DV = 256 dO the same (16: wave 1), DV = 64 du' pieces 0..4 on waves 1..5; lse | Di on wave 6;
 // dr (DV = 64) and the keep words on wave 7.
-template <int DV, int DROP>
+// NSB: stages in the Q / du' ring -- 3 (default): tile it + 1 in flight across tile it's compute, one
+// barrier per tile; 2: the round-5 ring, two barriers per tile.  PF: LDS fragment reads kept ahead of
+// their MFMAs in the S / dP phase.  3 stages + 8 ahead: V-fold backward 1.231 -> 1.192 ms (dQ + dK,
+// tools/vfold_bwd_bench.py).  Measured and dropped: waves 4-7 staggered by one phase (each tile's dK
+// phase after the next barrier, 4-stage ring): 1.213 vs 1.177 ms (profiles/r06_v28_vfold_bwd.log).
+template <int DV, int DROP, int NSB = 3, int PF = 8>
 __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a) {
+  static_assert(NSB == 2 || NSB == 3, "ring depth");
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   constexpr int DP = 256, QT = 32, NW = 8;
   constexpr bool FOLD = DV != DP;
@@ -765,7 +796,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
   constexpr int RB = 384 + 512;
   constexpr int STAGE = IQ::TILEB + IG::TILEB + RB;
   constexpr bool bits = DROP == DROP_BITS;
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[NSB * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, kl = lane & 15;
   const WgIdx wi = wg_xcd_order();
   if (wi.y >= a.BH) return;  // grid padding
@@ -828,6 +859,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
   };
 
   issue(smem, 0);
+  if (NSB >= 3 && nt > 1) issue(smem + STAGE, QT);
   bf16x8 kf[DP / 32], vf[DV / 32];  // B operands K^T / V^T: [k = d = 32t + 8g + j][n = key]
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
@@ -844,16 +876,39 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
   const int kword = (w & 1) * 16 + kl;  // this lane's bit in its keep word
   const int kwsel = w >> 1;             // which of the block's 4 words
 
+  // dK^T += Q^T dS, dV^T += dO^T P_drop (transposing reads of the padded Q / dO images)
+  auto dk_phase = [&](const char* Qb, const char* Gb, bf16x8 ds, bf16x8 pd) {
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int d = 0; d < DP / 16; ++d) {
+      dk[d] = mfma16(tr_frag_pad<IQ::ROWB>(Qb, 0, 16 * d, lane), ds, dk[d]);
+      if constexpr (!FOLD) dv[d] = mfma16(tr_frag_pad<IG::ROWB>(Gb, 0, 16 * d, lane), pd, dv[d]);
+    }
+    sched_reads_ahead<(FOLD ? 1 : 2) * DP / 16, 4, 2>();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  int cur = 0;  // it % NSB
   for (int it = 0; it < nt; ++it) {
     const int q0 = it * QT;
-    char* st = smem + (it & 1) * STAGE;
-    if (it + 1 < nt) {
-      issue(smem + ((it + 1) & 1) * STAGE, q0 + QT);
-      wait_stage();
+    char* st = smem + cur * STAGE;
+    if constexpr (NSB == 2) {
+      if (it + 1 < nt) {
+        issue(smem + (cur ^ 1) * STAGE, q0 + QT);
+        wait_stage();
+      } else {
+        wait_vmcnt<0>();
+      }
+      wg_barrier();
     } else {
-      wait_vmcnt<0>();
+      // one barrier per tile: tile it + 1 stays in flight across it; tile it + 2 is issued after the
+      // barrier into the buffer every wave finished reading in iteration it - 1
+      if (it + 1 < nt) wait_stage();
+      else wait_vmcnt<0>();
+      wg_barrier();
+      if (it + 2 < nt) issue(smem + ((cur + 2) % NSB) * STAGE, q0 + 2 * QT);
     }
-    wg_barrier();
+    cur = cur == NSB - 1 ? 0 : cur + 1;
     const char* Qi = st;
     const char* Gi = st + IQ::TILEB;
     const char* rb = st + IQ::TILEB + IG::TILEB;
@@ -871,7 +926,7 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
 #pragma unroll
       for (int t = 0; t < DV / 32; ++t) dp[qb] = mfma16(*(const bf16x8*)(grow + 64 * t), vf[t], dp[qb]);
     }
-    sched_reads_ahead<2 * (DP / 32 + DV / 32), 4, 1>();
+    sched_reads_ahead<2 * (DP / 32 + DV / 32), PF, 1>();
     __builtin_amdgcn_sched_barrier(0);
     // B operands over 32 queries: k index 8g + j <-> q 16(j >> 2) + 4g + (j & 3)
     bf16x8 dsb, pdb;
@@ -911,17 +966,11 @@ __global__ __launch_bounds__(512, 1) void flash_bwd_dkv16_kernel(FlashBwdArgs a)
     };
     if (q0 + QT <= a.Lq) softmax(std::false_type{});
     else softmax(std::true_type{});
-    // dK^T += Q^T dS, dV^T += dO^T P_drop (transposing reads of the padded Q / dO images)
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int d = 0; d < DP / 16; ++d) {
-      dk[d] = mfma16(tr_frag_pad<IQ::ROWB>(Qi, 0, 16 * d, lane), dsb, dk[d]);
-      if constexpr (!FOLD) dv[d] = mfma16(tr_frag_pad<IG::ROWB>(Gi, 0, 16 * d, lane), pdb, dv[d]);
+    dk_phase(Qi, Gi, dsb, pdb);
+    if constexpr (NSB == 2) {  // every wave's reads of this stage retired before it is refilled
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wg_barrier();
     }
-    sched_reads_ahead<(FOLD ? 1 : 2) * DP / 16, 4, 2>();
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wg_barrier();
   }
 
   if (!kv) return;
@@ -1024,9 +1073,21 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   // Di = rowsum(dO * O) is computed by the dQ kernel and stored for the dK / dV kernel
   const int drop = a.p_drop <= 0.f ? DROP_NONE : (a.keep ? DROP_BITS : DROP_HASH);
   const dim3 gq((a.Lq + FL_QB - 1) / FL_QB, pad_bh8(a.BH), a.splits);
-  if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
-  else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
-  else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  // the V-fold dQ kernel on the 3-stage ring with 8 reads ahead (A/B: variant bit 6 the 2-stage form)
+  bool dq_done = false;
+  if constexpr (DP == 256 && DV == 64) {
+    if (((s2h_flash_variant() >> 6) & 1) == 0) {
+      if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      dq_done = true;
+    }
+  }
+  if (!dq_done) {
+    if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
+    else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
+    else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV>), gq, dim3(FL_WAVES * 64), 0, st, a);
+  }
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_bwd_dq_combine_kernel<DP>), dim3((unsigned)((rows * DP / 4 + 255) / 256)), dim3(256), 0,
                        st, a);
@@ -1034,13 +1095,21 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
     const dim3 gk((a.Lk + 127) / 128, pad_bh8(a.BH), a.kv_splits);
     // V-fold: two waves per SIMD (flash_bwd_dkv16_kernel) unless variant bit 1 asks for the 32x32
     // kernel below; it takes a single query range per workgroup (no fp32 partials).  The DV = 256
-    // instance (memory self-attention) spills at 256 VGPRs and measured slower than the 32x32 kernel
-    // (tools/attn_ab.py --variants: self-attention backward 0.565 vs 0.513 ms), so it is not launched.
-    if (DV == 64 && a.kv_splits == 1 && (s2h_flash_variant() & 1) == 0) {
-      if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_NONE>), gk, dim3(512), 0, st, a);
-      else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_BITS>), gk, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_HASH>), gk, dim3(512), 0, st, a);
-      return (int)hipGetLastError();
+    // instance (memory self-attention) spilled at 256 VGPRs and measured slower than the 32x32 kernel
+    // (tools/attn_ab.py --variants: self-attention backward 0.565 vs 0.513 ms), so it is not built.
+    if constexpr (DV == 64) {
+      if (a.kv_splits == 1 && (s2h_flash_variant() & 1) == 0) {
+        if ((s2h_flash_variant() >> 4) & 1) {  // A/B: variant bit 4 the round-5 2-stage ring
+          if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_NONE, 2, 4>), gk, dim3(512), 0, st, a);
+          else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_BITS, 2, 4>), gk, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_HASH, 2, 4>), gk, dim3(512), 0, st, a);
+        } else {
+          if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_NONE>), gk, dim3(512), 0, st, a);
+          else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_BITS>), gk, dim3(512), 0, st, a);
+          else hipLaunchKernelGGL((flash_bwd_dkv16_kernel<DV, DROP_HASH>), gk, dim3(512), 0, st, a);
+        }
+        return (int)hipGetLastError();
+      }
     }
     if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV>), gk, dim3(256), 0, st, a);
     else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV>), gk, dim3(256), 0, st, a);

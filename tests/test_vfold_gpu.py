@@ -190,7 +190,9 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
     """the two-waves-per-SIMD V-fold dK kernel (flash_bwd_dkv16_kernel, default) against the
     one-wave-per-SIMD 32x32 kernel it replaced (s2h_attn_config(3)) on the same frame table: dK
     equal to fp32-summation-order rounding (query tails, key tails, keep bitmap on and off); dQ is
-    the same kernel in both and must be bit-identical"""
+    the same kernel in both and must be bit-identical.  The round-5 2-stage rings of the dK kernel
+    (variant bit 4, s2h_attn_config(33)) and of the dQ kernel (bit 6: 129; both: 161) against the
+    default 3-stage rings with one barrier per tile and 8 reads ahead: the same sums, bit-identical"""
     from sam2_video.kernels._lib import lib
     ops = _ops()
     B, seed = 3, 21
@@ -217,7 +219,7 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
     out = {}
     prev = lib().s2h_attn_config(1)
     try:
-        for variant in (1, 3):
+        for variant in (1, 3, 33, 129, 161):
             lib().s2h_attn_config(variant)
             dq = torch.empty_like(q_all)
             dk = torch.full_like(k_all, float("nan"))
@@ -229,8 +231,9 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
             out[variant] = (dq, dk)
     finally:
         lib().s2h_attn_config(prev)
-    assert torch.equal(out[1][0], out[3][0])
+    assert all(torch.equal(out[1][0], out[v][0]) for v in (3, 33, 129, 161))
     assert not torch.isnan(out[1][1]).any()
+    assert all(torch.equal(out[1][1], out[v][1]) for v in (33, 129, 161))
     _close(out[1][1], out[3][1], 1e-2, "dk two-wave vs one-wave")
 
 
