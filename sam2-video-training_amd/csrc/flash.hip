@@ -62,8 +62,11 @@ enum { FDROP_NONE = 0, FDROP_HASH = 1, FDROP_BITS = 2 };
 
 // QS: 16-query sets per wave (QS = 2: every K / V fragment read from LDS feeds two MFMAs -- the
 // kernel's LDS read traffic per query halves; the workgroup covers 128 QS query rows)
-template <int DP, int DROP, int DV = DP, int QS = 1>
+// NSB: stages in the K / V ring -- 2: two barriers per tile; 3 (the V-fold default, flash_launch): tile
+// it + 1 in flight across tile it's compute, one barrier per tile (the backward's round-6 ring)
+template <int DP, int DROP, int DV = DP, int QS = 1, int NSB = 2>
 __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a) {
+  static_assert(NSB == 2 || NSB == 3, "ring depth");
   constexpr bool FOLD = DV != DP;
   constexpr int QB = FL_QB * QS;
   const uint32_t hkey = DROP != FDROP_NONE ? s2h_hash_key(s2h_seed(a.seed, a.seed_off)) : 0u;
@@ -73,8 +76,8 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   using IV = PadImg<DV>;  // padded V image (V-fold: the 64-channel memory rows)
   constexpr int NDV = DV / 16;
   constexpr int STG = I::TILEB + IV::TILEB;
-  // one LDS array: [2 stages][K tile | V tile]
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STG];
+  // one LDS array: [NSB stages][K tile | V tile]
+  __shared__ __attribute__((aligned(1024))) char smem[NSB * STG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, g = lane >> 4, ql = lane & 15;
   if (a.prio && w >= 4) __builtin_amdgcn_s_setprio(1);  // the second-dispatched half (MI355X_MICROARCH item 4)
   const WgIdx wi = wg_xcd_order();
@@ -102,6 +105,16 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   PadDma<DV> vdma;
   kdma.init(a.skl, w, lane, a.D);
   vdma.init(a.svl, w, lane, FOLD ? DV : a.D);
+  auto issue = [&](char* Kn, int kk) {  // the K / V tile of keys kk.. into stage Kn
+    if (kk + C::KT <= a.Lk) {  // whole tile: precomputed offsets on an SGPR row base
+      kdma.issue(Kn, K, a.skl, kk, wu);
+      vdma.issue(Kn + I::TILEB, V, a.svl, kk, wu);
+    } else {
+      dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, kk, a.Lk, w, lane, a.D);
+      dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, kk, a.Lk, w, lane, FOLD ? DV : a.D);
+    }
+  };
+  if (NSB == 3 && nt > 1) issue(smem + STG, (t0 + 1) * C::KT);
 
   // Q^T fragments (B operand of K Q^T): lane -> query q, d = 32t + 8g + j
   bf16x8 qf[QS][C::NT];
@@ -133,27 +146,32 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
   }
   const int qq = (lane >> 2) & 3, pp = lane & 3;  // transposing-read lane roles
 
+  int cur = 0;  // it % NSB
   for (int it = 0; it < nt; ++it) {
     const int kt = t0 + it;
     const int k0 = kt * C::KT;
-    char* Kb = smem + (it & 1) * STG;
+    char* Kb = smem + cur * STG;
     char* Vb = Kb + I::TILEB;
-    if (it + 1 < nt) {
-      char* Kn = smem + ((it + 1) & 1) * STG;
-      if (k0 + 2 * C::KT <= a.Lk) {  // whole next tile: precomputed offsets on an SGPR row base
-        kdma.issue(Kn, K, a.skl, k0 + C::KT, wu);
-        vdma.issue(Kn + I::TILEB, V, a.svl, k0 + C::KT, wu);
+    if constexpr (NSB == 2) {
+      if (it + 1 < nt) {
+        issue(smem + (cur ^ 1) * STG, k0 + C::KT);
+        // this wave's pieces of tile `it` have landed once all but the npw + npv just issued retired
+        wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
       } else {
-        dma_tile_pad<DP, 64, FL_WAVES, true>(Kn, K, a.skl, k0 + C::KT, a.Lk, w, lane, a.D);
-        dma_tile_pad<DV, 64, FL_WAVES, true>(Kn + I::TILEB, V, a.svl, k0 + C::KT, a.Lk, w, lane, FOLD ? DV : a.D);
+        wait_vmcnt<0>();
       }
-      // this wave's pieces of tile `it` have landed once all but the npw + npv just issued retired
-      wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     } else {
-      wait_vmcnt<0>();
+      // tile it + 1 (issued after the previous barrier) stays in flight; tile it + 2 goes after this
+      // barrier into the buffer every wave finished reading in iteration it - 1
+      if (it + 1 < nt) wait_kv_pieces<I::PPW_LO, IV::PPW_LO>(npw, npv);
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (it + 2 < nt) issue(smem + (cur == 0 ? 2 : cur - 1) * STG, k0 + 2 * C::KT);
     }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    cur = cur == NSB - 1 ? 0 : cur + 1;
 
     // ---- S^T = K Q^T: four 16-key blocks, key = 16*kb + 4g + r on the accumulator row
     f32x4 s[QS][4];
@@ -295,10 +313,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_fwd_kernel(FlashArgs a
     }
     sched_reads_ahead<2 * NDV, 4, 2, QS>();
     __builtin_amdgcn_sched_barrier(0);
-    // every wave done reading this stage before it is refilled (LDS reads retired first)
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
+    if constexpr (NSB == 2) {  // every wave done reading this stage before it is refilled (LDS reads retired first)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
   }
 
 #pragma unroll
@@ -440,12 +459,26 @@ template <int DP, int DV = DP, int QS = 1>
 static int flash_launch(FlashArgs& a, hipStream_t st) {
   a.prio = (s2h_flash_variant() >> 3) & 1;
   dim3 grid((a.Lq + FL_QB * QS - 1) / (FL_QB * QS), pad_bh8(a.BH), a.splits);
-  if (a.p_drop <= 0.f)
-    hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
-  else if (a.keep)
-    hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
-  else
-    hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  bool done = false;
+  if constexpr (DV == 64 && DP == 256) {  // V-fold: the 3-stage ring (A/B: variant bit 5 the 2-stage one)
+    if (((s2h_flash_variant() >> 5) & 1) == 0) {
+      if (a.p_drop <= 0.f)
+        hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
+      else if (a.keep)
+        hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
+      else
+        hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
+      done = true;
+    }
+  }
+  if (!done) {
+    if (a.p_drop <= 0.f)
+      hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+    else if (a.keep)
+      hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+    else
+      hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
+  }
   if (a.splits > 1)
     hipLaunchKernelGGL((flash_combine_kernel<DP, DV>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0,
                        st, a);

@@ -237,6 +237,31 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
     _close(out[1][1], out[3][1], 1e-2, "dk two-wave vs one-wave")
 
 
+@pytest.mark.parametrize("B,Lq,Lk,p_drop", [(13, 1024, 2056, 0.1), (3, 200, 300, 0.0), (2, 160, 70, 0.1)])
+def test_vfold_forward_ring_depths_bit_identical(B, Lq, Lk, p_drop):
+    """the V-fold flash forward on its default 3-stage K / M ring with one barrier per tile against the
+    round-5 2-stage ring (variant bit 5, s2h_attn_config(65)): the same u', LSE and keep bitmap"""
+    from sam2_video.kernels._lib import lib
+    ops = _ops()
+    q, k, m, _, _ = _inputs(B, Lq, Lk, 5)
+    out = {}
+    prev = lib().s2h_attn_config(1)
+    try:
+        for variant in (1, 65):
+            lib().s2h_attn_config(variant)
+            u = torch.full((B, Lq, 1, 72), float("nan"), device=DEV, dtype=torch.bfloat16)
+            lse = torch.empty(B, 1, Lq, device=DEV)
+            keep = torch.zeros(ops.keep_words(B, 1, Lq, Lk), device=DEV, dtype=torch.int32)
+            ops.attn_fwd_vfold(q, k, m, u, lse, 256 ** -0.5, p_drop, 9, keep=keep if p_drop > 0 else None)
+            torch.cuda.synchronize()
+            out[variant] = (u, lse, keep)
+    finally:
+        lib().s2h_attn_config(prev)
+    assert not torch.isnan(out[1][0][..., :65].float()).any()
+    for a, b in zip(out[1], out[65]):
+        assert torch.equal(a, b)
+
+
 def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
     """the fused value + output projection (FN.VFoldOutProj: one GEMM with W' = Wo [Wv | bv]) against
     the two GEMMs (S2H_VFOLD_OUT=0) in a bf16 B+ 256^2 training step, dropout off: logits, loss and
