@@ -224,6 +224,10 @@ int64_t s2h_attn_fwd_ws_bytes(int dt, int B, int H, int Lq, int Lk, int D);
  * tile kernels.  Returns the previous setting. */
 int s2h_attn_win(int on);
 int s2h_attn_config(int flash_enable);
+/* A/B bits (round 6, default 0) of the non-V-fold flash kernels: 1 the head-dim-256 self-attention dQ
+ * kernel with 8 fragment reads ahead, 2 the head-dim <= 128 dQ kernel on a 3-stage ring, 4 the
+ * head-dim <= 128 forward on a 3-stage ring.  Returns the previous bits (mode < 0: query only). */
+int s2h_flash_variant2(int mode);
 int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                  const void* k, int64_t skb, int64_t skh, int64_t skl,

@@ -430,6 +430,16 @@ static void flash_plan(int BH, int Lq, int Lk, int& splits, int& tps, int qs = 1
 static int g_flash_enabled = 1;
 // bits 1+ of the flash switch select older kernel variants for A/B runs (flash_bwd.hip)
 int s2h_flash_variant() { return g_flash_enabled >> 1; }
+// round-6 A/B bits of the non-V-fold flash kernels (default 0): 1 the self-attention dQ kernel (head dim
+// 256) with 8 fragment reads ahead; 2 the head-dim <= 128 dQ kernel on the 3-stage ring with 8 ahead;
+// 4 the head-dim <= 128 forward on the 3-stage ring.  Returns the previous bits (mode < 0: query).
+static int g_flash_v2 = 0;
+extern "C" int s2h_flash_variant2(int mode) {
+  const int prev = g_flash_v2;
+  if (mode >= 0) g_flash_v2 = mode;
+  return prev;
+}
+int s2h_flash_v2() { return g_flash_v2; }
 
 // A/B switch for tests and benchmarks: 0 routes every attention to the generic kernels;
 // 3 keeps the flash path with the one-wave-per-SIMD V-fold dK kernel (flash_bwd_dkv32_kernel).
@@ -462,6 +472,17 @@ static int flash_launch(FlashArgs& a, hipStream_t st) {
   bool done = false;
   if constexpr (DV == 64 && DP == 256) {  // V-fold: the 3-stage ring (A/B: variant bit 5 the 2-stage one)
     if (((s2h_flash_variant() >> 5) & 1) == 0) {
+      if (a.p_drop <= 0.f)
+        hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
+      else if (a.keep)
+        hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_BITS, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
+      else
+        hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
+      done = true;
+    }
+  }
+  if constexpr (DV == DP && DP <= 128) {
+    if (s2h_flash_v2() & 4) {
       if (a.p_drop <= 0.f)
         hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_NONE, DV, QS, 3>), grid, dim3(FL_WAVES * 64), 0, st, a);
       else if (a.keep)

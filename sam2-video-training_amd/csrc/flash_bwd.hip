@@ -24,6 +24,7 @@
 
 int s2h_prof_begin(hipStream_t st, int kind, int64_t m0, int64_t m1, int64_t m2, int64_t m3, int64_t m4);
 int s2h_flash_variant();  // flash.hip: A/B selection of older kernels
+int s2h_flash_v2();       // flash.hip: round-6 A/B bits (s2h_flash_variant2)
 void s2h_prof_end(int slot, hipStream_t st);
 
 struct FlashBwdArgs {
@@ -1077,6 +1078,22 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
   bool dq_done = false;
   if constexpr (DP == 256 && DV == 64) {
     if (((s2h_flash_variant() >> 6) & 1) == 0) {
+      if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      dq_done = true;
+    }
+  }
+  if constexpr (DV == DP && DP == 256) {  // self-attention: 8 reads ahead (A/B bit 1 of s2h_flash_variant2)
+    if (s2h_flash_v2() & 1) {
+      if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV, 2, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV, 2, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV, 2, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
+      dq_done = true;
+    }
+  }
+  if constexpr (DV == DP && DP <= 128) {  // Hiera: the 3-stage ring, 8 ahead (A/B bit 2)
+    if (s2h_flash_v2() & 2) {
       if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_NONE, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
       else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_BITS, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);
       else hipLaunchKernelGGL((flash_bwd_dq_kernel<DP, DROP_HASH, DV, 3, 8>), gq, dim3(FL_WAVES * 64), 0, st, a);

@@ -44,6 +44,7 @@ SIGNATURES = {
     "s2h_mlp_heads": [I, I, P, P, P, P, P, P, P, P, P, P, P, P],
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
+    "s2h_flash_variant2": [I],
     "s2h_gemm_config": [I],
     "s2h_gemm_split_target": [I],
     "s2h_gemm_tiny_config": [I],
@@ -198,6 +199,8 @@ def lib():
             h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
         if os.environ.get("S2H_ATTN_CFG"):  # flash switch | forward key-split target << 8 (A/B)
             h.s2h_attn_config(int(os.environ["S2H_ATTN_CFG"]))
+        if os.environ.get("S2H_FLASH_V2"):  # round-6 flash kernel variants (A/B bits, s2h_flash_variant2)
+            h.s2h_flash_variant2(int(os.environ["S2H_FLASH_V2"]))
         if os.environ.get("S2H_ATTN_WIN"):  # small-window attention kernels on / off (A/B)
             h.s2h_attn_win(int(os.environ["S2H_ATTN_WIN"]))
         if os.environ.get("S2H_GEMM_AREG"):  # ... short-K GEMMs with A in registers (A/B)
