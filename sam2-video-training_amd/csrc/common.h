@@ -208,6 +208,38 @@ __device__ __forceinline__ void lds_dma16(const void* src, const void* lds_piece
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_piece);
   asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
 }
+// one 1-KiB LDS-DMA piece from a wave-uniform row base (SGPR pair) + this lane's 32-bit byte offset
+// (global_load_lds_dwordx4, saddr form): the building block of PadDma and of the backward kernels'
+// precomputed-offset stage loads
+__device__ __forceinline__ uint64_t sgpr_base(const void* p) {
+  const uint64_t b = (uint64_t)(uintptr_t)p;
+  // (readfirstlane returns int: through uint32_t, or the low word's sign bit smears into the high one)
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+}
+__device__ __forceinline__ void lds_dma16_so(uint64_t sbase, uint32_t voff, const void* lds_piece) {
+  const uint32_t m0 =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_piece);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+// the same with the piece's LDS byte address given as an integer (lds_u32 of the __shared__ array plus
+// an offset): no generic -> LDS pointer cast at the call (its null test came out as an illegal VALU
+// compare against src_shared_base in some GEMM instantiations)
+__device__ __forceinline__ void lds_dma16_sm(uint64_t sbase, uint32_t voff, uint32_t lds_addr) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
+}
+// LDS byte address of a __shared__ array (call it on the array itself)
+template <typename T>
+__device__ __forceinline__ uint32_t lds_u32(T* shared_array) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) T*)shared_array;
+}
+
+// lds_dma16 with the LDS byte address as an integer (see lds_dma16_sm)
+__device__ __forceinline__ void lds_dma16_m(const void* src, uint32_t lds_addr) {
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane(lds_addr);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory", "m0");
+}
 __device__ __forceinline__ void lds_dma4(const void* src, const void* lds_piece) {
   const uint32_t m0 =
       __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_piece);

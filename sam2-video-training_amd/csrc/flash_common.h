@@ -168,21 +168,6 @@ __device__ __forceinline__ void dma_tile_pad(char* lds_tile, const bf16* src, in
   }
 }
 
-// one 1-KiB LDS-DMA piece from a wave-uniform row base (SGPR pair) + this lane's 32-bit byte offset
-// (global_load_lds_dwordx4, saddr form): the building block of PadDma and of the backward kernels'
-// precomputed-offset stage loads
-__device__ __forceinline__ uint64_t sgpr_base(const void* p) {
-  const uint64_t b = (uint64_t)(uintptr_t)p;
-  // (readfirstlane returns int: through uint32_t, or the low word's sign bit smears into the high one)
-  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
-         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
-}
-__device__ __forceinline__ void lds_dma16_so(uint64_t sbase, uint32_t voff, const void* lds_piece) {
-  const uint32_t m0 =
-      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(__attribute__((address_space(3))) const void*)lds_piece);
-  asm volatile("s_mov_b32 m0, %2\n\tglobal_load_lds_dwordx4 %0, %1" ::"v"(voff), "s"(sbase), "s"(m0) : "memory", "m0");
-}
-
 // dma_tile_pad with the lane-constant part of the addresses computed once (init) and the tile's row
 // base a wave-uniform SGPR pair: per piece one s_mov m0 + global_load_lds_dwordx4 on a 32-bit VGPR
 // byte offset (the saddr form) -- dma_tile_pad's per-tile VALU address arithmetic (a division by the

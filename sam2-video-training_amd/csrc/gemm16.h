@@ -31,7 +31,7 @@ struct GemmArgs16 {
   // tables' column (c % rope_dh) / 2.  rope_cos == nullptr: no rotation.
   const float* rope_cos; const float* rope_sin;
   int rope_L, rope_nrot, rope_period, rope_ncol, rope_dh;
-  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA, 8 plain stores, 16 tile-major split-K order, 32 split-K by float atomics
+  int dbg;       // measurement-only ablations (s2h_gemm_config bits 8+): 1 skip epilogue stores, 2 skip MFMAs, 4 skip operand DMA, 8 plain stores, 16 tile-major split-K order, 32 split-K by float atomics, 64 per-piece DMA address arithmetic (gemm16g_kernel)
 };
 
 // The LayerNorm epilogues' extra arguments (round 4), in a derived block that only the full-row tilings

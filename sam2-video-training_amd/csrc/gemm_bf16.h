@@ -221,8 +221,9 @@ struct GImg {
   }
   // DMA rows/k of the tile at (row0, k0); rows >= nrows / k >= kend are clamped to valid
   // addresses (garbage rows are never stored; the K tail is zeroed in LDS afterwards)
+  // (img_lds: the image's LDS byte address when the caller has it as an integer -- GDma -- else ~0u)
   __device__ static __forceinline__ void dma(char* img, const bf16* base, int64_t ld_row, int64_t ld_k, int row0, int k0,
-                                            int nrows, int kend, int w, int lane) {
+                                            int nrows, int kend, int w, int lane, uint32_t img_lds = ~0u) {
 #pragma unroll
     for (int i = 0; i < PPW; ++i) {
       const int piece = w * PPW + i;
@@ -240,7 +241,8 @@ struct GImg {
         const int r = row0 + 8 * c < nrows ? row0 + 8 * c : row0;
         src = base + (k * (int)ld_k + r);
       }
-      lds_dma16(src, img + piece * 1024);
+      if (img_lds != ~0u) lds_dma16_m(src, img_lds + piece * 1024);
+      else lds_dma16(src, img + piece * 1024);
     }
   }
   // zero the k >= kvalid part of the image (last K step only)
@@ -275,6 +277,37 @@ struct GImg {
     typedef short v8i16 __attribute__((ext_vector_type(8)));
     v8i16 cat = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
     return __builtin_bit_cast(bf16x8, cat);
+  }
+};
+
+// GImg::dma with the lane-constant part of every piece's source address computed once per workgroup:
+// a whole K step (k0 + BK <= kend) is one SGPR base (the operand at k0) + this lane's 32-bit byte
+// offset per piece (global_load_lds_dwordx4, saddr form) -- no VALU per piece (GImg::dma spent 27 VALU
+// per K step of the 64 x 64 tile on clamps and 64-bit address arithmetic, gfx950 ISA).  The ragged last
+// step takes GImg::dma.  Same bytes into the same image slots.
+template <class IMG, bool KC>
+struct GDma {
+  uint32_t off[IMG::PPW];
+  __device__ __forceinline__ void init(int64_t ld_row, int64_t ld_k, int row0, int nrows, int w, int lane) {
+#pragma unroll
+    for (int i = 0; i < IMG::PPW; ++i) {
+      const int piece = w * IMG::PPW + i;
+      const int irow = piece * (1024 / IMG::RB) + lane / IMG::LPR;
+      const int c = IMG::swz(irow, lane % IMG::LPR);
+      if (KC) off[i] = (uint32_t)(min(row0 + irow, nrows - 1) * (int)ld_row + 8 * c) * 2u;
+      else off[i] = (uint32_t)(irow * (int)ld_k + (row0 + 8 * c < nrows ? row0 + 8 * c : row0)) * 2u;
+    }
+  }
+  // img: the stage image; img_lds: its LDS byte address
+  __device__ __forceinline__ void issue(char* img, uint32_t img_lds, const bf16* base, int64_t ld_row, int64_t ld_k,
+                                        int row0, int k0, int nrows, int kend, int w, int wu, int lane) const {
+    if (k0 + IMG::BK > kend) {  // ragged last step: clamped addresses
+      IMG::dma(img, base, ld_row, ld_k, row0, k0, nrows, kend, w, lane, img_lds);
+      return;
+    }
+    const uint64_t bs = sgpr_base(KC ? base + k0 : base + (int64_t)k0 * ld_k);
+#pragma unroll
+    for (int i = 0; i < IMG::PPW; ++i) lds_dma16_sm(bs, off[i], img_lds + (wu * IMG::PPW + i) * 1024);
   }
 };
 
@@ -343,14 +376,27 @@ void gemm16g_kernel(PA p) {
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const bool do_rs = p.rowsum != nullptr && n0 == 0 && tid < BM;
   float rs = 0.f;
+  GDma<IA, AKC> adma;
+  GDma<IB, BKC> bdma;
+  adma.init(p.lda_m, p.lda_k, m0, p.M, w, lane);
+  bdma.init(p.ldb_n, p.ldb_k, n0, p.N, w, lane);
+  const int wu = __builtin_amdgcn_readfirstlane(w);
+  const uint32_t smem_lds = lds_u32(smem);
+  auto stage_dma = [&](int stg, int k) {  // dbg 64: the per-piece address arithmetic (A/B)
+    char* sa = smem + stg * STAGE;
+    if (p.dbg & 64) {
+      IA::dma(sa, A, p.lda_m, p.lda_k, m0, k, p.M, kend, w, lane, smem_lds + stg * STAGE);
+      IB::dma(sa + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, k, p.N, kend, w, lane, smem_lds + stg * STAGE + IA::BYTES);
+    } else {
+      adma.issue(sa, smem_lds + stg * STAGE, A, p.lda_m, p.lda_k, m0, k, p.M, kend, w, wu, lane);
+      bdma.issue(sa + IA::BYTES, smem_lds + stg * STAGE + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, k, p.N, kend, w, wu,
+                 lane);
+    }
+  };
 
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {  // prologue: stages 0 .. NS-2 in flight
-    if (st < nk && !(p.dbg & 4)) {
-      char* sa = smem + st * STAGE;
-      IA::dma(sa, A, p.lda_m, p.lda_k, m0, kbeg + st * BK, p.M, kend, w, lane);
-      IB::dma(sa + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + st * BK, p.N, kend, w, lane);
-    }
+    if (st < nk && !(p.dbg & 4)) stage_dma(st, kbeg + st * BK);
   }
   for (int kt = 0; kt < nk; ++kt) {
     char* sa = smem + (kt % NS) * STAGE;
@@ -359,11 +405,8 @@ void gemm16g_kernel(PA p) {
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + NS - 1 < nk && !(p.dbg & 4)) {  // refill the buffer step kt-1 read; runs under this step's MFMAs
-      char* na = smem + ((kt + NS - 1) % NS) * STAGE;
-      IA::dma(na, A, p.lda_m, p.lda_k, m0, kbeg + (kt + NS - 1) * BK, p.M, kend, w, lane);
-      IB::dma(na + IA::BYTES, B, p.ldb_n, p.ldb_k, n0, kbeg + (kt + NS - 1) * BK, p.N, kend, w, lane);
-    }
+    if (kt + NS - 1 < nk && !(p.dbg & 4))  // refill the buffer step kt-1 read; runs under this step's MFMAs
+      stage_dma((kt + NS - 1) % NS, kbeg + (kt + NS - 1) * BK);
     const int kvalid = kend - (kbeg + kt * BK);
     if (kvalid < BK) {  // K tail: zero the invalid k of both images (last step only)
       IA::zero_tail(sa, kvalid, tid);
