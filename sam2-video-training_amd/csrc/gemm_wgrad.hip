@@ -74,13 +74,20 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_wg_kernel(WgArgs p) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.f;
 
+  // the operands' DMA on precomputed per-lane offsets + one SGPR base per K step (GDma, gemm_bf16.h)
+  GDma<IA, false> adma;
+  GDma<IB, false> bdma;
+  adma.init(1, p.lda, m0, p.M, w, lane);
+  bdma.init(1, p.ldb, n0, p.N, w, lane);
+  const uint32_t smem_lds = lds_u32(smem);
+  auto stage_dma = [&](int stg, int k) {
+    adma.issue(smem + stg * STAGE, smem_lds + stg * STAGE, p.A, 1, p.lda, m0, k, p.M, kend, w, w, lane);
+    bdma.issue(smem + stg * STAGE + IA::BYTES, smem_lds + stg * STAGE + IA::BYTES, p.B, 1, p.ldb, n0, k, p.N, kend, w,
+               w, lane);
+  };
 #pragma unroll
   for (int st = 0; st < NS - 1; ++st) {
-    if (st < nk) {
-      char* sa = smem + st * STAGE;
-      IA::dma(sa, p.A, 1, p.lda, m0, kbeg + st * BK, p.M, kend, w, lane);
-      IB::dma(sa + IA::BYTES, p.B, 1, p.ldb, n0, kbeg + st * BK, p.N, kend, w, lane);
-    }
+    if (st < nk) stage_dma(st, kbeg + st * BK);
   }
   for (int kt = 0; kt < nk; ++kt) {
     char* sa = smem + (kt % NS) * STAGE;
@@ -89,11 +96,7 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void gemm_wg_kernel(WgArgs p) {
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (kt + NS - 1 < nk) {
-      char* na = smem + ((kt + NS - 1) % NS) * STAGE;
-      IA::dma(na, p.A, 1, p.lda, m0, kbeg + (kt + NS - 1) * BK, p.M, kend, w, lane);
-      IB::dma(na + IA::BYTES, p.B, 1, p.ldb, n0, kbeg + (kt + NS - 1) * BK, p.N, kend, w, lane);
-    }
+    if (kt + NS - 1 < nk) stage_dma((kt + NS - 1) % NS, kbeg + (kt + NS - 1) * BK);
     const int kvalid = kend - (kbeg + kt * BK);
     if (kvalid < BK) {  // K tail: zero the invalid k of both images (last step only)
       IA::zero_tail(sa, kvalid, tid);
