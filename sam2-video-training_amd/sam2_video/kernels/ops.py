@@ -52,6 +52,7 @@ class SideWork:
 
     def __init__(self):
         self.cur = self.ws = None
+        _det_workspace_mode(not _SIDE["on"])
         if _SIDE["on"] and torch.cuda.is_available():
             self.cur = torch.cuda.current_stream()
             dev = self.cur.device
@@ -135,13 +136,28 @@ def _device_of(device):
     return d
 
 
+WGRAD_KMIN = 4096  # csrc/gemm_wgrad.hip g_wg_kmin: reductions at least this long take the deterministic kernel
+
+
+def _det_workspace_mode(on):
+    """the library's deterministic-reduction workspace on (the default) or off: every user of it (the
+    weight-gradient kernel, split-K partial tiles, fixed-order column sums) is ordered on ONE stream, so
+    with the weight-gradient side stream (S2H_WGRAD_STREAM=1) they fall back to their atomic forms"""
+    t = _WG_WS.get("t")
+    if t is not None and _WG_WS.get("on", True) != on:
+        call("s2h_wgrad_workspace", t.data_ptr(), WGRAD_WS_BYTES, WGRAD_KMIN if on else 0)
+    _WG_WS["on"] = on
+
+
 def wgrad_workspace(device=None):
     d = _device_of(device)
     t = _WG_WS.get("t")
     if t is None:
         t = _persistent_alloc("wgrad_workspace", WGRAD_WS_BYTES // 4, torch.float32, d)
-        call("s2h_wgrad_workspace", t.data_ptr(), WGRAD_WS_BYTES, 0 if _SIDE["on"] else -1)
+        on = not _SIDE["on"]
+        call("s2h_wgrad_workspace", t.data_ptr(), WGRAD_WS_BYTES, WGRAD_KMIN if on else 0)
         _WG_WS["t"] = t
+        _WG_WS["on"] = on
     elif t.device != d:  # one registration per process: the library holds one address
         raise RuntimeError(f"wgrad workspace already registered on {t.device}, requested {d}")
     return t

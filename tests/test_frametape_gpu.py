@@ -239,14 +239,19 @@ def test_wgrad_side_stream_equals_one_stream(monkeypatch):
     g = load_golden("bplus256_point_all")
     size, prompt, trainable = CASES["bplus256_point_all"]
     out = []
-    for on in (False, True):
-        monkeypatch.setitem(ops._SIDE, "on", on)
-        m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype="bf16", seed=int(g["meta/seed"]))
-        m.frame_batched = True
-        stages, merged, losses, _ = run_step(m, golden_batch(g).to("cuda"))
-        torch.cuda.synchronize()
-        out.append(([s["pred_masks"].detach().float().cpu() for s in stages], grads_by_name(m)))
-        del m
+    try:
+        for on in (False, True):
+            monkeypatch.setitem(ops._SIDE, "on", on)
+            m = build_model(size, int(g["meta/image_size"]), trainable, prompt, dtype="bf16", seed=int(g["meta/seed"]))
+            m.frame_batched = True
+            stages, merged, losses, _ = run_step(m, golden_batch(g).to("cuda"))
+            torch.cuda.synchronize()
+            # with the side stream the deterministic workspace is switched off (ops._det_workspace_mode)
+            assert ops._WG_WS["on"] == (not on)
+            out.append(([s["pred_masks"].detach().float().cpu() for s in stages], grads_by_name(m)))
+            del m
+    finally:
+        ops._det_workspace_mode(True)  # the default for the tests that follow
     (la, ga), (lb, gb) = out
     for a, b in zip(la, lb):
         assert torch.equal(a, b)
