@@ -71,21 +71,53 @@ extern "C" int s2h_grad_norm(int64_t n, const float* g, float* partial_ws, float
   return (int)hipGetLastError();
 }
 
+// One element's AdamW update (torch.optim.AdamW, decoupled weight decay), every rounding step written
+// out (explicit fmaf) so the scalar and the 16-B kernels below produce the same bits for any compiler
+// contraction choice
+__device__ __forceinline__ void adamw_elem(float g, float& p, float& m, float& v, float cf, float decay, float w1,
+                                           float beta2, float omb2, float eps, float step_size, float bc2_sqrt) {
+  const float gi = g * cf;
+  const float mi = fmaf(w1, gi - m, m);
+  const float vi = fmaf(omb2, gi * gi, v * beta2);
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p = fmaf(-step_size, mi / denom, p * decay);
+  m = mi;
+  v = vi;
+}
 __global__ __launch_bounds__(256) void adamw_kernel(int64_t n, float* p, const float* g, float* m, float* v,
                                                     const float* clip, float lr, float beta1, float beta2, float eps,
                                                     float wd, float step_size, float bc2_sqrt, bf16* shadow) {
   const float cf = clip ? clip[1] : 1.f;
-  const float w1 = 1.f - beta1;
+  const float decay = 1.f - lr * wd, w1 = 1.f - beta1, omb2 = 1.f - beta2;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
-    const float gi = g[i] * cf;
-    float pi = p[i] * (1.f - lr * wd);
-    float mi = m[i];
-    mi = mi + w1 * (gi - mi);
-    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
-    const float denom = sqrtf(vi) / bc2_sqrt + eps;
-    pi = pi - step_size * (mi / denom);
+    float pi = p[i], mi = m[i], vi = v[i];
+    adamw_elem(g[i], pi, mi, vi, cf, decay, w1, beta2, omb2, eps, step_size, bc2_sqrt);
     p[i] = pi; m[i] = mi; v[i] = vi;
     if (shadow) shadow[i] = (bf16)pi;
+  }
+}
+// The same update 4 elements per lane with 16-B loads / stores (8-B shadow stores): one pass over the
+// arena is 30 B per parameter (p, g, m, v read; p, m, v, shadow written) -- HBM-bound, and the scalar
+// form's 4-B accesses reached 4.7 TB/s on the B+ arena (484 us per step).  Bit-identical per element.
+__global__ __launch_bounds__(256) void adamw_vec_kernel(int64_t n4, float4* p, const float4* g, float4* m, float4* v,
+                                                        const float* clip, float lr, float beta1, float beta2, float eps,
+                                                        float wd, float step_size, float bc2_sqrt, uint2* shadow) {
+  const float cf = clip ? clip[1] : 1.f;
+  const float decay = 1.f - lr * wd, w1 = 1.f - beta1, omb2 = 1.f - beta2;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    const float4 g4 = g[i], p4 = p[i], m4 = m[i], v4 = v[i];
+    const float ga[4] = {g4.x, g4.y, g4.z, g4.w};
+    float po[4] = {p4.x, p4.y, p4.z, p4.w}, mo[4] = {m4.x, m4.y, m4.z, m4.w}, vo[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      adamw_elem(ga[e], po[e], mo[e], vo[e], cf, decay, w1, beta2, omb2, eps, step_size, bc2_sqrt);
+    p[i] = float4{po[0], po[1], po[2], po[3]};
+    m[i] = float4{mo[0], mo[1], mo[2], mo[3]};
+    v[i] = float4{vo[0], vo[1], vo[2], vo[3]};
+    if (shadow) {
+      bf16 t4[4] = {(bf16)po[0], (bf16)po[1], (bf16)po[2], (bf16)po[3]};
+      shadow[i] = *(const uint2*)t4;
+    }
   }
 }
 extern "C" int s2h_adamw(int64_t n, float* p, const float* g, float* m, float* v, const float* clip, float lr,
@@ -95,9 +127,22 @@ extern "C" int s2h_adamw(int64_t n, float* p, const float* g, float* m, float* v
   const double bc2 = 1.0 - pow((double)beta2, (double)step);
   const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
-  int64_t b = (n + 255) / 256;
-  if (b > 4096) b = 4096;
-  hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)b), dim3(256), 0, st, n, p, g, m, v, clip, lr, beta1, beta2, eps, wd,
-                     step_size, bc2_sqrt, (bf16*)bf16_shadow);
+  const bool vec = (((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 &&
+                   ((uintptr_t)bf16_shadow & 7) == 0;
+  const int64_t n4 = vec ? n / 4 : 0;
+  if (n4 > 0) {
+    int64_t b = (n4 + 255) / 256;
+    if (b > 8192) b = 8192;
+    hipLaunchKernelGGL(adamw_vec_kernel, dim3((unsigned)b), dim3(256), 0, st, n4, (float4*)p, (const float4*)g,
+                       (float4*)m, (float4*)v, clip, lr, beta1, beta2, eps, wd, step_size, bc2_sqrt, (uint2*)bf16_shadow);
+  }
+  const int64_t done = 4 * n4, rest = n - done;  // the tail (or everything when unaligned)
+  if (rest > 0) {
+    int64_t b = (rest + 255) / 256;
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(adamw_kernel, dim3((unsigned)b), dim3(256), 0, st, rest, p + done, g + done, m + done, v + done,
+                       clip, lr, beta1, beta2, eps, wd, step_size, bc2_sqrt,
+                       bf16_shadow ? (bf16*)bf16_shadow + done : (bf16*)nullptr);
+  }
   return (int)hipGetLastError();
 }

@@ -1054,6 +1054,27 @@ def test_clip_adamw_matches_torch(max_norm, grad_scale):
     _close(p, pt.detach(), 1e-5)
 
 
+def test_adamw_vector_and_scalar_paths_bit_identical():
+    """s2h_adamw's 16-B-per-lane kernel (aligned arena, the step's case) and its scalar form (unaligned
+    pointers, and the n % 4 tail) compute the same update element for element, bf16 shadow included"""
+    ops = _ops()
+    torch.manual_seed(12)
+    n = 100_003
+    src = [torch.randn(n, device=DEV) for _ in range(4)]
+    src[3] = src[3].abs()  # v >= 0
+    clip = torch.tensor([0.0, 0.7], device=DEV)
+    out = []
+    for off in (0, 1):  # 0: 16-B aligned (vector kernel + 3-element tail), 1: 4-B offset (scalar kernel)
+        p, g, m, v = (torch.empty(n + 1, device=DEV)[off:off + n].copy_(t) for t in src)
+        sh = torch.empty(n + 4, device=DEV, dtype=torch.bfloat16)[4 * off:4 * off + n]
+        for step in (1, 2):
+            ops.adamw(p, g, m, v, clip, 1e-3, 0.9, 0.999, 1e-8, 0.01, step, shadow=sh)
+        torch.cuda.synchronize()
+        out.append((p, m, v, sh))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
+
+
 def test_category_merge_multi_object_matches_reference_formulas():
     """merge_masks / merge_scores over categories of 1, 2 and 3 objects (a tie and a NaN included)
     vs the reference's _grouped_max / _grouped_weighted_avg (masks.py:92-143) under autograd:
