@@ -838,10 +838,54 @@ extern "C" int s2h_bilinear_fwd(int N, int hi, int wi, int ho, int wo, const flo
   hipLaunchKernelGGL(bilinear_fwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, x, y);
   return (int)hipGetLastError();
 }
+// The same gather with the column taps' weights computed once per input pixel (MAXC candidate output
+// columns in registers) instead of once per (candidate row, candidate column): the same candidates, the
+// same skipped zeros, the same (wy * wx) * dy products added in the same order -- bit-identical.  The
+// per-candidate index arithmetic made the kernel VALU-bound (126 us for the 104-plane 256^2 -> 512^2
+// mask upsampling backward).
+template <int MAXC>
+__global__ __launch_bounds__(256) void bilinear_bwd_hoist_kernel(int N, int hi, int wi, int ho, int wo, const float* dy,
+                                                                 float* dx) {
+  const float sh = (float)hi / ho, sw = (float)wi / wo;
+  const int64_t n = (int64_t)N * hi * wi;
+  GRID_STRIDE(i, n) {
+    const int ix = i % wi;
+    const int64_t r = i / wi;
+    const int iy = r % hi;
+    const int p = r / hi;
+    const int oy0 = max(0, (int)floorf((iy - 0.5f) / sh - 0.5f) - 1);
+    const int oy1 = min(ho - 1, (int)ceilf((iy + 1.5f) / sh - 0.5f) + 1);
+    const int ox0 = max(0, (int)floorf((ix - 0.5f) / sw - 0.5f) - 1);
+    const int ox1 = min(wo - 1, (int)ceilf((ix + 1.5f) / sw - 0.5f) + 1);
+    float wxs[MAXC];
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
+      int x0, x1; float lx;
+      bil_src(ox0 + c, sw, wi, x0, x1, lx);
+      wxs[c] = ox0 + c <= ox1 ? (x0 == ix ? 1.f - lx : 0.f) + (x1 == ix ? lx : 0.f) : 0.f;
+    }
+    float acc = 0.f;
+    for (int oy = oy0; oy <= oy1; ++oy) {
+      int y0, y1; float ly;
+      bil_src(oy, sh, hi, y0, y1, ly);
+      const float wy = (y0 == iy ? 1.f - ly : 0.f) + (y1 == iy ? ly : 0.f);
+      if (wy == 0.f) continue;
+      const float* row = dy + ((int64_t)p * ho + oy) * wo + ox0;
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c)
+        if (wxs[c] != 0.f) acc += wy * wxs[c] * row[c];
+    }
+    dx[i] = acc;
+  }
+}
 extern "C" int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const float* dy, float* dx, hipStream_t st) {
   const int64_t n = (int64_t)N * hi * wi;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(bilinear_bwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  // candidate output columns per input column: ox1 - ox0 + 1 <= ceil(2 wo / wi) + 4 (2x: 8)
+  const int maxc = (int)ceilf(2.f * wo / wi) + 4;
+  if (maxc <= 8) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<8>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  else if (maxc <= 16) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<16>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  else hipLaunchKernelGGL(bilinear_bwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   return (int)hipGetLastError();
 }
 

@@ -1054,6 +1054,20 @@ def test_clip_adamw_matches_torch(max_norm, grad_scale):
     _close(p, pt.detach(), 1e-5)
 
 
+@pytest.mark.parametrize("N,hi,wi,ho,wo", [(104, 256, 256, 512, 512), (3, 64, 64, 256, 256), (2, 30, 17, 100, 61),
+                                          (2, 64, 64, 32, 32)])
+def test_bilinear_backward_matches_torch(N, hi, wi, ho, wo):
+    """s2h_bilinear_bwd (the gather form with the column taps hoisted, round 6) against torch's
+    upsample_bilinear2d backward (align_corners=False): the step's 104-plane 256^2 -> 512^2 mask
+    upsampling, 4x, a non-integer ratio and a down-sampling"""
+    ops = _ops()
+    torch.manual_seed(13)
+    x = torch.randn(N, hi, wi, device=DEV, requires_grad=True)
+    g = torch.randn(N, ho, wo, device=DEV)
+    torch.nn.functional.interpolate(x[:, None], size=(ho, wo), mode="bilinear", align_corners=False)[:, 0].backward(g)
+    _close(ops.bilinear_bwd(g, hi, wi), x.grad, 1e-5)
+
+
 def test_adamw_vector_and_scalar_paths_bit_identical():
     """s2h_adamw's 16-B-per-lane kernel (aligned arena, the step's case) and its scalar form (unaligned
     pointers, and the n % 4 tail) compute the same update element for element, bf16 shadow included"""
