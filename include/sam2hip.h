@@ -115,7 +115,7 @@ int s2h_gemm_w41(int mode);
 /* A/B knob (round 6): tiling (values as s2h_gemm_config, 0 = the shape rules) of one class of
  * bf16-output GEMMs with M > 128 -- class 0: K >= 1024 and N <= 512; 1: K <= 256, N <= 256 and
  * M >= 8192; 2: K <= 512 and N >= 768; 3: 256 < K < 1024 and N <= 512; 4 / 5: K < 256 not a multiple
- * of 64 with M >= / < 65536.  Returns the previous setting (-1: no such class). */
+ * of 64 with M >= 65536 / with M < 65536 and K >= 128.  Returns the previous setting (-1: no such class). */
 int s2h_gemm_class_config(int cls, int cfg);
 /* A/B knob (round 6): bf16-output GEMMs with M <= 128, K >= 1024 and at most 16 64 x 64 output tiles as
  * one split-K fp32 launch into the weight-gradient workspace + one fixed-order reduce running the

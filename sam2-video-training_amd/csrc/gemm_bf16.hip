@@ -61,7 +61,7 @@ extern "C" int s2h_gemm_areg(int mode) {
 //   class 3: 256 < K < 1024, N <= 512 (mid reduction, narrow output: Hiera proj)
 //   class 4: K < 256 not a multiple of 64 (the A-in-registers domain), M >= 65536 (Hiera stage 1 at
 //            112 channels: 131072 rows at 512^2)
-//   class 5: the same with M < 65536 (Hiera stage 2 at 224 channels, the V-fold's 72)
+//   class 5: the same with M < 65536 and K >= 128 (Hiera stage 2 at 224 channels)
 // Defaults (round 6): classes 4 / 5 on the 128 x 64 4 x 1 LDS-DMA tiling with 32-deep stages, 3-deep ring
 // (cfg 22) instead of the A-in-registers kernel: in-step sweeps 47.59 / 47.52 -> 47.45 / 47.44 ms
 // (profiles/r06_v12_gemm_class4_sweep.log, r06_v13_gemm_class45_sweep.log); every other class keeps its rules.
@@ -74,7 +74,9 @@ extern "C" int s2h_gemm_class_config(int cls, int cfg) {
 }
 static int gemm_class(const GemmArgs16& a) {
   if (a.out_f32 || a.M <= 128) return -1;
-  if (a.K < 256 && a.K % 64 != 0) return a.M >= 65536 ? 4 : 5;
+  // (K < 128 with M < 65536 -- the V-fold out projection, 13312x256x72 -- stays on the A-in-registers
+  // rule: 12.45 us there vs 14.21 on cfg 22, profiles/r06_v3 vs r06_v37 shape tables)
+  if (a.K < 256 && a.K % 64 != 0) return a.M >= 65536 ? 4 : (a.K >= 128 ? 5 : -1);
   if (a.K >= 1024 && a.N <= 512) return 0;
   if (a.K <= 256 && a.N <= 256 && a.M >= 8192) return 1;
   if (a.K <= 512 && a.N >= 768) return 2;
@@ -236,9 +238,62 @@ int s2h_gemm_split_reduce(const GemmArgs16& a, int batch, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+// K = 1 (an outer product, e.g. the hypernetwork-mask gradient dup[o] = g[o]^T h[o] over 104 frames x
+// objects of 16384 x 32, frametape._hyper_bw): C = alpha * a b^T element-wise, 8 output columns per lane
+// with one 16-B store.  The bf16 x bf16 product is exact in fp32 and rounded once, as the MFMA tile's
+// single accumulation is -- the same bits as the tiled GEMM, which spent 134 us per launch on K-step
+// prologue / tail zeroing for 109 MB of output.
+__global__ __launch_bounds__(256) void gemm_outer_kernel(GemmArgs16 p, int batch) {
+  const int ng = (p.N + 7) / 8;
+  const int64_t total = (int64_t)batch * p.M * ng;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int gcol = (int)(i % ng);
+    const int64_t r = i / ng;
+    const int m = (int)(r % p.M), bz = (int)(r / p.M);
+    const float av = p.alpha * (float)p.A[(int64_t)bz * p.sA + (int64_t)m * p.lda_m];
+    const bf16* B = p.B + (int64_t)bz * p.sB;
+    const int n0 = gcol * 8;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = n0 + e < p.N ? av * (float)B[(int64_t)(n0 + e) * p.ldb_n] : 0.f;
+    if (p.out_f32) {
+      float* C = (float*)p.C + (int64_t)bz * p.sC + (int64_t)m * p.ldc + n0;
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (n0 + e < p.N) C[e] = v[e];
+    } else {
+      bf16* C = (bf16*)p.C + (int64_t)bz * p.sC + (int64_t)m * p.ldc + n0;
+      bf16 t[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) t[e] = (bf16)v[e];
+      if (n0 + 8 <= p.N && (((uintptr_t)C) & 15) == 0) {
+        *(uint4*)C = *(const uint4*)t;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (n0 + e < p.N) C[e] = t[e];
+      }
+    }
+  }
+}
+static int gemm_outer(const GemmArgs16& a, int batch, hipStream_t st) {
+  if (a.K != 1 || a.beta != 0.f || a.bias || a.R || a.X || a.cscale || a.drop_p != 0.f || a.act != 0 || a.rowsum ||
+      a.rope_cos != nullptr)
+    return -1;
+  const int64_t total = (int64_t)batch * a.M * ((a.N + 7) / 8);
+  if (total <= 0) return 0;
+  const int64_t blocks = std::min<int64_t>((total + 255) / 256, 16384);
+  hipLaunchKernelGGL(gemm_outer_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, batch);
+  return (int)hipGetLastError();
+}
+
 int s2h_gemm_bf16(const GemmArgs16& in, int batch, hipStream_t st) {
   GemmArgs16 a = in;
   a.dbg = g_gemm_dbg;
+  if (!g_gemm_cfg) {
+    const int rc = gemm_outer(a, batch, st);
+    if (rc >= 0) return rc;
+  }
   if (!g_gemm_cfg && !g_gemm_tiny_cfg) {
     const int rc = gemm_tiny_splitk(a, batch, st);
     if (rc >= 0) return rc;

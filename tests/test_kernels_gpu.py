@@ -1068,6 +1068,33 @@ def test_bilinear_backward_matches_torch(N, hi, wi, ho, wo):
     _close(ops.bilinear_bwd(g, hi, wi), x.grad, 1e-5)
 
 
+@pytest.mark.parametrize("out_dtype,alpha", [(torch.bfloat16, 1.0), (torch.float32, 0.5)])
+def test_k1_outer_product_path_equals_tiled_gemm(out_dtype, alpha):
+    """K = 1 GEMMs (the hypernetwork-mask gradient dup[o] = g[o]^T h[o], 104 x 16384 x 32) take the
+    element-wise outer-product kernel (round 6): the same bits as the tiled MFMA GEMM (forced with
+    s2h_gemm_config), batched with strides, N not a multiple of 8 included"""
+    from sam2_video.kernels import _lib
+    ops = _ops()
+    torch.manual_seed(14)
+    for Bt, M, N in ((104, 16384, 32), (3, 100, 37)):
+        g = torch.randn(Bt, 1, M, device=DEV).to(torch.bfloat16)
+        h = torch.randn(Bt, 1, N, device=DEV).to(torch.bfloat16)
+        outs = []
+        for cfg in (0, 1):  # 0: the shape rules (outer-product path), 1: the 64 x 64 tiling
+            prev = _lib.lib().s2h_gemm_config(cfg)
+            try:
+                out = torch.full((Bt, M, N), float("nan"), device=DEV, dtype=out_dtype)
+                ops.gemm(g, h, out, M=M, N=N, K=1, lda_m=1, lda_k=M, ldb_k=N, ldb_n=1, ldc=N, batch=Bt, sA=M, sB=N,
+                         sC=M * N, alpha=alpha)
+                torch.cuda.synchronize()
+                outs.append(out)
+            finally:
+                _lib.lib().s2h_gemm_config(prev)
+        assert torch.equal(outs[0], outs[1])
+        ref = alpha * g.float().transpose(1, 2) @ h.float()
+        _close(outs[0].float(), ref, 1e-2)
+
+
 def test_adamw_vector_and_scalar_paths_bit_identical():
     """s2h_adamw's 16-B-per-lane kernel (aligned arena, the step's case) and its scalar form (unaligned
     pointers, and the n % 4 tail) compute the same update element for element, bf16 shadow included"""
