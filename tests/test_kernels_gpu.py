@@ -814,6 +814,23 @@ def test_im2col_conv_matches_torch():
     _close(yd, ref, 2e-5)
 
 
+@pytest.mark.parametrize("B,H,W,C,k,s,p,pad8", [(8, 512, 512, 3, 7, 4, 3, True), (2, 17, 19, 3, 7, 4, 3, True),
+                                               (13, 32, 32, 16, 4, 4, 0, False), (2, 9, 7, 5, 3, 2, 1, False)])
+def test_im2col_bf16_equals_unfold(B, H, W, C, k, s, p, pad8):
+    """bf16 im2col (the 8-columns-per-lane kernel when the row pitch allows, round 6) is an exact copy:
+    equal to torch's unfold of the NCHW image, column order (c, ky, kx), padding rows zero"""
+    ops = _ops()
+    torch.manual_seed(15)
+    x = torch.randn(B, H, W, C, device=DEV).to(torch.bfloat16)
+    col, Ho, Wo = ops.im2col(x, k, k, s, p, pad8=pad8)
+    ref = torch.nn.functional.unfold(x.permute(0, 3, 1, 2).float(), k, padding=p, stride=s)  # [B, C*k*k, L]
+    ref = ref.transpose(1, 2).reshape(B * Ho * Wo, C * k * k).to(torch.bfloat16)
+    assert torch.equal(col, ref)
+    if pad8 and col.stride(0) != col.shape[1]:  # the padding columns of the pitch are zero
+        full = col.as_strided((col.shape[0], col.stride(0)), (col.stride(0), 1))
+        assert not full[:, col.shape[1]:].float().abs().sum().item()
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,H,W,C", [(13, 32, 32, 256), (2, 7, 45, 128), (13, 64, 64, 256), (1, 5, 3, 64)])
 def test_dwconv_vectorised(dtype, tol, B, H, W, C):
