@@ -228,6 +228,9 @@ int s2h_attn_config(int flash_enable);
  * kernel with 8 fragment reads ahead, 2 the head-dim <= 128 dQ kernel on a 3-stage ring, 4 the
  * head-dim <= 128 forward on a 3-stage ring.  Returns the previous bits (mode < 0: query only). */
 int s2h_flash_variant2(int mode);
+/* A/B knob (round 6): fp32 GEMMs of fewer than 64 tiles of 64 x 64 on 32 x 32 tiles (1, default) or 64 x 64
+ * (0).  Returns the previous mode (mode < 0: query only). */
+int s2h_gemm_f32_small(int mode);
 int s2h_attn_fwd(int dt, int B, int H, int Lq, int Lk, int D,
                  const void* q, int64_t sqb, int64_t sqh, int64_t sql,
                  const void* k, int64_t skb, int64_t skh, int64_t skl,

@@ -171,11 +171,24 @@ static int launch_gemm_tiles(const GemmArgs& a, int batch, hipStream_t st) {
   return (int)hipGetLastError();
 }
 
+static int g_gemm32_small = 1;  // A/B knob (s2h_gemm_f32_small): fp32 GEMMs of < 64 tiles on 32 x 32 tiles
+extern "C" int s2h_gemm_f32_small(int mode) {
+  const int prev = g_gemm32_small;
+  if (mode >= 0) g_gemm32_small = mode;
+  return prev;
+}
+
 template <typename T, typename TC>
 static int launch_gemm(const GemmArgs& a, int batch, hipStream_t st) {
   // Small problems: 64x64 tiles keep enough workgroups in flight on 256 CUs.
   long tiles128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128) * batch;
   if (tiles128 >= 512) return launch_gemm_tiles<T, TC, 128, 128>(a, batch, st);
+  // fp32 problems of fewer than 64 tiles of 64^2 (the V-fold weight gradients dWo += G V^T, 256 x 256 x 72,
+  // and dV = Wo^T G, 256 x 72 x 256, once per layer and step): 32 x 32 tiles, 4x the workgroups
+  if constexpr (sizeof(T) == 4) {
+    const long tiles64 = (long)((a.M + 63) / 64) * ((a.N + 63) / 64) * batch;
+    if (g_gemm32_small && tiles64 < 64) return launch_gemm_tiles<T, TC, 32, 32>(a, batch, st);
+  }
   return launch_gemm_tiles<T, TC, 64, 64>(a, batch, st);
 }
 

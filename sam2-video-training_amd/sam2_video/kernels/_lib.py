@@ -45,6 +45,7 @@ SIGNATURES = {
     "s2h_attn_fwd_ws_bytes": [I, I, I, I, I, I],
     "s2h_attn_config": [I],
     "s2h_flash_variant2": [I],
+    "s2h_gemm_f32_small": [I],
     "s2h_gemm_config": [I],
     "s2h_gemm_split_target": [I],
     "s2h_gemm_tiny_config": [I],
@@ -199,6 +200,8 @@ def lib():
             h.s2h_gemm_tiny_config(int(os.environ["S2H_GEMM_TINY_CFG"]))
         if os.environ.get("S2H_ATTN_CFG"):  # flash switch | forward key-split target << 8 (A/B)
             h.s2h_attn_config(int(os.environ["S2H_ATTN_CFG"]))
+        if os.environ.get("S2H_GEMM_F32_SMALL"):  # small fp32 GEMMs on 32 x 32 tiles (1) / 64 x 64 (0)
+            h.s2h_gemm_f32_small(int(os.environ["S2H_GEMM_F32_SMALL"]))
         if os.environ.get("S2H_FLASH_V2"):  # round-6 flash kernel variants (A/B bits, s2h_flash_variant2)
             h.s2h_flash_variant2(int(os.environ["S2H_FLASH_V2"]))
         if os.environ.get("S2H_ATTN_WIN"):  # small-window attention kernels on / off (A/B)

@@ -1112,6 +1112,32 @@ def test_k1_outer_product_path_equals_tiled_gemm(out_dtype, alpha):
         _close(outs[0].float(), ref, 1e-2)
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 72), (256, 72, 256), (100, 37, 130)])
+def test_small_fp32_gemm_tilings(M, N, K):
+    """fp32 GEMMs of fewer than 64 tiles of 64^2 (the V-fold weight gradients) on 32 x 32 tiles (round 6,
+    s2h_gemm_f32_small(1)) and on 64 x 64: both against the fp64 product, NN / TN layouts, beta 1"""
+    from sam2_video.kernels._lib import lib
+    ops = _ops()
+    torch.manual_seed(17)
+    a = torch.randn(M, K, device=DEV)
+    at = a.t().contiguous()  # [K, M]: A with m contiguous
+    b = torch.randn(K, N, device=DEV)
+    c0 = torch.randn(M, N, device=DEV)
+    ref = a.double() @ b.double()
+    prev = lib().s2h_gemm_f32_small(-1)
+    try:
+        for mode in (1, 0):
+            lib().s2h_gemm_f32_small(mode)
+            c = torch.empty(M, N, device=DEV)
+            ops.gemm(a, b, c, M=M, N=N, K=K, lda_m=K, lda_k=1, ldb_k=N, ldb_n=1, ldc=N)
+            _close(c, ref.float(), 1e-5)
+            c = c0.clone()
+            ops.gemm(at, b, c, M=M, N=N, K=K, lda_m=1, lda_k=M, ldb_k=N, ldb_n=1, ldc=N, beta=1.0)
+            _close(c, (ref + c0.double()).float(), 1e-5)
+    finally:
+        lib().s2h_gemm_f32_small(prev)
+
+
 def test_adamw_vector_and_scalar_paths_bit_identical():
     """s2h_adamw's 16-B-per-lane kernel (aligned arena, the step's case) and its scalar form (unaligned
     pointers, and the n % 4 tail) compute the same update element for element, bf16 shadow included"""
