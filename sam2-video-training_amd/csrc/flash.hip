@@ -432,7 +432,8 @@ static int g_flash_enabled = 1;
 int s2h_flash_variant() { return g_flash_enabled >> 1; }
 // round-6 A/B bits of the non-V-fold flash kernels (default 0): 1 the self-attention dQ kernel (head dim
 // 256) with 8 fragment reads ahead; 2 the head-dim <= 128 dQ kernel on the 3-stage ring with 8 ahead;
-// 4 the head-dim <= 128 forward on the 3-stage ring.  Returns the previous bits (mode < 0: query).
+// 4 the head-dim <= 128 forward on the 3-stage ring; 8 the 32x32 dK / dV kernel (self-attention) on the
+// 3-stage ring.  Returns the previous bits (mode < 0: query).
 static int g_flash_v2 = 0;
 extern "C" int s2h_flash_variant2(int mode) {
   const int prev = g_flash_v2;

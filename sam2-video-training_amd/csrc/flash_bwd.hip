@@ -559,8 +559,11 @@ __global__ __launch_bounds__(FL_WAVES * 64, 1) void flash_bwd_dkv_kernel(FlashBw
 // KREG: K fragments held in registers like V (64 more VGPRs, no K block in LDS): the S / dP
 // phase re-read the constant K block from LDS every 32-query tile -- a third of that phase's
 // LDS traffic, and the phase is LDS-bandwidth-bound (4 waves x 48 b128 reads against 32 MFMAs).
-template <int DP, int DROP, bool KREG = true, int DV = DP>
+// NSB: stages of the Q / dO ring -- 2 (two barriers per tile), 3 (one barrier per tile, tile it + 1
+// in flight across tile it; the dkv16 / dQ kernels' round-6 ring)
+template <int DP, int DROP, bool KREG = true, int DV = DP, int NSB = 2>
 __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a) {
+  static_assert(NSB == 2 || NSB == 3, "ring depth");
   constexpr bool FOLD = DV != DP;  // V-fold: dO tile = du' (DV wide + dr), no dV
   const uint64_t seed = DROP == DROP_HASH ? s2h_seed(a.seed, a.seed_off) : 0;
   constexpr int NWV = 4, QT = 32;
@@ -574,7 +577,7 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   constexpr int RWB = FOLD ? 768 : 512;  // per wave [lse | Di | keep words (x2) | dr words (x2, V-fold)]
   constexpr int STAGE = C::TILEB + CG::TILEB + NWV * RWB;
   constexpr int KBLK = KREG ? 0 : CK::TILEB;
-  __shared__ __attribute__((aligned(1024))) char smem[KBLK + 2 * STAGE];
+  __shared__ __attribute__((aligned(1024))) char smem[KBLK + NSB * STAGE];
   char* Kblk = smem;
   char* stages = smem + KBLK;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, hi = lane >> 5, kl = lane & 31;
@@ -620,6 +623,14 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   dma_rows(stages, qbase);
   if constexpr (bits) dma_bits(stages, qbase);
   if constexpr (FOLD) dma_dr(stages, qbase);
+  auto issue = [&](char* Qn, int qn) {
+    dma_tile<DP, QT, NWV, true, 1>(Qn, Q, a.sql, qn, a.Lq, w, lane);
+    dma_tile<DV, QT, NWV, true, SWG>(Qn + C::TILEB, G, a.sgl, qn, a.Lq, w, lane);
+    dma_rows(Qn, qn);
+    if constexpr (bits) dma_bits(Qn, qn);
+    if constexpr (FOLD) dma_dr(Qn, qn);
+  };
+  if (NSB == 3 && nt > 1) issue(stages + STAGE, qbase + QT);
   bf16x8 vf[NTV];  // B operand V^T (V-fold: M^T): [k = d = 16t + 8hi + j][n = key]
   const int64_t vkey = min(key, fr.Lk - 1);
 #pragma unroll
@@ -637,26 +648,33 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
   for (int d = 0; d < ND; ++d) dk[d] = f32x16{};
 #pragma unroll
   for (int d = 0; d < NDV; ++d) dv[d] = f32x16{};
+  int cur = 0;  // it % NSB
   for (int it = 0; it < nt; ++it) {
     const int q0 = qbase + it * QT;
-    char* Qb = stages + (it & 1) * STAGE;
+    char* Qb = stages + cur * STAGE;
     char* Gb = Qb + C::TILEB;
     // [lse(32) | Di(32) | keep(32) | - | dr words(32) | -]
     const float* rows = (const float*)(Qb + C::TILEB + CG::TILEB + w * RWB);
     const uint32_t* kwd = (const uint32_t*)(rows + 64);
     const uint32_t* drw = (const uint32_t*)(rows + 128);
-    if (it + 1 < nt) {
-      char* Qn = stages + ((it + 1) & 1) * STAGE;
-      dma_tile<DP, QT, NWV, true, 1>(Qn, Q, a.sql, q0 + QT, a.Lq, w, lane);
-      dma_tile<DV, QT, NWV, true, SWG>(Qn + C::TILEB, G, a.sgl, q0 + QT, a.Lq, w, lane);
-      dma_rows(Qn, q0 + QT);
-      if constexpr (bits) dma_bits(Qn, q0 + QT);
-      if constexpr (FOLD) dma_dr(Qn, q0 + QT);
-      wait_vmcnt<C::PPW + CG::PPW + 1 + (bits ? 1 : 0) + (FOLD ? 1 : 0)>();
+    constexpr int PER_STAGE = C::PPW + CG::PPW + 1 + (bits ? 1 : 0) + (FOLD ? 1 : 0);  // DMAs per wave and stage
+    if constexpr (NSB == 2) {
+      if (it + 1 < nt) {
+        issue(stages + (cur ^ 1) * STAGE, q0 + QT);
+        wait_vmcnt<PER_STAGE>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      wg_barrier();
     } else {
-      wait_vmcnt<0>();
+      // tile it + 1 stays in flight across this one; tile it + 2 goes after the barrier into the buffer
+      // every wave finished reading in iteration it - 1
+      if (it + 1 < nt) wait_vmcnt<PER_STAGE>();
+      else wait_vmcnt<0>();
+      wg_barrier();
+      if (it + 2 < nt) issue(stages + (cur == 0 ? 2 : cur - 1) * STAGE, q0 + 2 * QT);
     }
-    wg_barrier();
+    cur = cur == NSB - 1 ? 0 : cur + 1;
 
     f32x16 s = f32x16{}, dp = f32x16{};  // S / dP: row q = 8(r>>2) + 4hi + (r&3), column key
 #pragma unroll
@@ -706,8 +724,10 @@ __global__ __launch_bounds__(256, 1) void flash_bwd_dkv32_kernel(FlashBwdArgs a)
         dk[d] = mfma32(tr_frag_perm32<DP, 1>(Qb, 16 * c, 32 * d, lane), dsb[c], dk[d]);
         if (d & 1) __builtin_amdgcn_sched_barrier(0);
       }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wg_barrier();
+    if constexpr (NSB == 2) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      wg_barrier();
+    }
   }
 
   if (!kv) return;
@@ -1128,9 +1148,17 @@ static int flash_bwd_launch(FlashBwdArgs& a, hipStream_t st) {
         return (int)hipGetLastError();
       }
     }
-    if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV>), gk, dim3(256), 0, st, a);
-    else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV>), gk, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH, true, DV>), gk, dim3(256), 0, st, a);
+    if (s2h_flash_v2() & 8) {  // the 3-stage ring (A/B bit 8 of s2h_flash_variant2)
+      if (drop == DROP_NONE) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV, 3>), gk, dim3(256), 0, st, a);
+      else if (drop == DROP_BITS) hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV, 3>), gk, dim3(256), 0, st, a);
+      else hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH, true, DV, 3>), gk, dim3(256), 0, st, a);
+    } else if (drop == DROP_NONE) {
+      hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_NONE, true, DV>), gk, dim3(256), 0, st, a);
+    } else if (drop == DROP_BITS) {
+      hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_BITS, true, DV>), gk, dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((flash_bwd_dkv32_kernel<DP, DROP_HASH, true, DV>), gk, dim3(256), 0, st, a);
+    }
     if (DV == DP && a.kv_splits > 1) {
       const int64_t n4 = (int64_t)a.BH * a.Lk * 2 * DP / 4;
       hipLaunchKernelGGL((flash_bwd_dkv_combine_kernel<DP>), dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, a);
