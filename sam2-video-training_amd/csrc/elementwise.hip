@@ -843,7 +843,10 @@ extern "C" int s2h_bilinear_fwd(int N, int hi, int wi, int ho, int wo, const flo
 // same skipped zeros, the same (wy * wx) * dy products added in the same order -- bit-identical.  The
 // per-candidate index arithmetic made the kernel VALU-bound (126 us for the 104-plane 256^2 -> 512^2
 // mask upsampling backward).
-template <int MAXC>
+// X2: exact 2x upsampling (ho = 2 hi, wo = 2 wi): the taps of input i come from outputs 2i - 1 .. 2i + 2
+// only (the wider search's other candidates all have zero weight), so 4 x 4 candidates instead of 8 x 8
+// -- the same nonzero terms in the same order
+template <int MAXC, bool X2 = false>
 __global__ __launch_bounds__(256) void bilinear_bwd_hoist_kernel(int N, int hi, int wi, int ho, int wo, const float* dy,
                                                                  float* dx) {
   const float sh = (float)hi / ho, sw = (float)wi / wo;
@@ -853,10 +856,10 @@ __global__ __launch_bounds__(256) void bilinear_bwd_hoist_kernel(int N, int hi, 
     const int64_t r = i / wi;
     const int iy = r % hi;
     const int p = r / hi;
-    const int oy0 = max(0, (int)floorf((iy - 0.5f) / sh - 0.5f) - 1);
-    const int oy1 = min(ho - 1, (int)ceilf((iy + 1.5f) / sh - 0.5f) + 1);
-    const int ox0 = max(0, (int)floorf((ix - 0.5f) / sw - 0.5f) - 1);
-    const int ox1 = min(wo - 1, (int)ceilf((ix + 1.5f) / sw - 0.5f) + 1);
+    const int oy0 = X2 ? max(0, 2 * iy - 1) : max(0, (int)floorf((iy - 0.5f) / sh - 0.5f) - 1);
+    const int oy1 = X2 ? min(ho - 1, 2 * iy + 2) : min(ho - 1, (int)ceilf((iy + 1.5f) / sh - 0.5f) + 1);
+    const int ox0 = X2 ? max(0, 2 * ix - 1) : max(0, (int)floorf((ix - 0.5f) / sw - 0.5f) - 1);
+    const int ox1 = X2 ? min(wo - 1, 2 * ix + 2) : min(wo - 1, (int)ceilf((ix + 1.5f) / sw - 0.5f) + 1);
     float wxs[MAXC];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -883,7 +886,9 @@ extern "C" int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const flo
   if (n <= 0) return 0;
   // candidate output columns per input column: ox1 - ox0 + 1 <= ceil(2 wo / wi) + 4 (2x: 8)
   const int maxc = (int)ceilf(2.f * wo / wi) + 4;
-  if (maxc <= 8) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<8>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  if (ho == 2 * hi && wo == 2 * wi)
+    hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<4, true>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  else if (maxc <= 8) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<8>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   else if (maxc <= 16) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<16>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   else hipLaunchKernelGGL(bilinear_bwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   return (int)hipGetLastError();
