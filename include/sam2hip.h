@@ -226,7 +226,9 @@ int s2h_attn_win(int on);
 int s2h_attn_config(int flash_enable);
 /* A/B bits (round 6, default 0) of the non-V-fold flash kernels: 1 the head-dim-256 self-attention dQ
  * kernel with 8 fragment reads ahead, 2 the head-dim <= 128 dQ kernel on a 3-stage ring, 4 the
- * head-dim <= 128 forward on a 3-stage ring, 8 the 32x32 dK / dV kernel on a 3-stage ring.  Returns the previous bits (mode < 0: query only). */
+ * head-dim <= 128 forward on a 3-stage ring, 8 the 32x32 dK / dV kernel on a 3-stage ring, 16 the
+ * one-row-per-wave key-split combine (all flash forwards, V-fold included).  Returns the previous bits
+ * (mode < 0: query only). */
 int s2h_flash_variant2(int mode);
 /* A/B knob (round 6): fp32 GEMMs of fewer than 64 tiles of 64 x 64 on 32 x 32 tiles (1, default) or 64 x 64
  * (0).  Returns the previous mode (mode < 0: query only). */

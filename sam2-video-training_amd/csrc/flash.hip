@@ -396,6 +396,56 @@ __global__ __launch_bounds__(256) void flash_combine_kernel(FlashArgs a) {
   if (lane == 0) a.lse[rowg] = (Mr + log2f(L)) * FL_LN2;
 }
 
+// Round 6: the same merge with DV / 4 lanes per query row and 4 columns per lane, so each split's
+// partial row and its (m, l[, r]) record are 16-B loads (flash_combine_kernel above gives the V-fold's
+// 64-wide rows one float per lane and one row per wave); the same sums in the same order, bit for bit
+// (variant2 bit 16 launches the kernel above)
+// SPL > 0: the split count as a constant (the loops unroll and every load issues before the merge)
+template <int DP, int DV = DP, int SPL = 0>
+__global__ __launch_bounds__(256) void flash_combine_vec_kernel(FlashArgs a) {
+  constexpr bool FOLD = DV != DP;
+  constexpr int MLW = FL_MLW(FOLD);
+  constexpr int LPR = DV / 4, RPB = 256 / LPR;
+  const int sub = threadIdx.x & (LPR - 1);
+  const int64_t rowg = (int64_t)blockIdx.x * RPB + threadIdx.x / LPR;  // bh*Lq + q
+  if (rowg >= (int64_t)a.BH * a.Lq) return;
+  const int bh = rowg / a.Lq, q = rowg % a.Lq, b = bh / a.H, h = bh % a.H;
+  const int64_t stride = (int64_t)a.BH * a.Lq;
+  const int ns = SPL > 0 ? SPL : a.splits;
+  float M = -INFINITY;
+  for (int s = 0; s < ns; ++s) M = fmaxf(M, a.ws_ml[MLW * (s * stride + rowg)]);
+  const float Mr = M == -INFINITY ? 0.f : M;
+  float L = 0.f, R = 0.f, acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < ns; ++s) {
+    const int64_t r = s * stride + rowg;
+    float ms, ls, rs = 0.f;
+    if constexpr (FOLD) {
+      const f32x4 ml = *(const f32x4*)(a.ws_ml + 4 * r);
+      ms = ml[0]; ls = ml[1]; rs = ml[2];
+    } else {
+      ms = a.ws_ml[2 * r]; ls = a.ws_ml[2 * r + 1];
+    }
+    const float f = ms == -INFINITY ? 0.f : exp2f(ms - Mr);
+    L += ls * f;
+    if constexpr (FOLD) R += rs * f;
+    const f32x4 o = *(const f32x4*)(a.ws_o + r * DV + sub * 4);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] += f * o[j];
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  bf16* O = a.o + b * a.sob + h * a.soh + (int64_t)q * a.sol;
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (FOLD || sub * 4 + j < a.D) O[sub * 4 + j] = (bf16)(acc[j] * inv);
+  if constexpr (FOLD) {
+    if (sub < 2) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) O[DV + sub * 4 + j] = (bf16)(sub == 0 && j == 0 ? R * inv : 0.f);
+    }
+  }
+  if (sub == 0) a.lse[rowg] = (Mr + log2f(L)) * FL_LN2;
+}
+
 // Split count: as many key splits as keep the grid within one round of 256 workgroups (one
 // per CU), never fewer than 2 key tiles per split.  Measured on the memory-attention shapes
 // (13 objects x 1024 queries x 1024..7196 keys, d 256, tools/attn_bench.py --targets): 2 splits
@@ -433,7 +483,8 @@ int s2h_flash_variant() { return g_flash_enabled >> 1; }
 // round-6 A/B bits of the non-V-fold flash kernels (default 0): 1 the self-attention dQ kernel (head dim
 // 256) with 8 fragment reads ahead; 2 the head-dim <= 128 dQ kernel on the 3-stage ring with 8 ahead;
 // 4 the head-dim <= 128 forward on the 3-stage ring; 8 the 32x32 dK / dV kernel (self-attention) on the
-// 3-stage ring.  Returns the previous bits (mode < 0: query).
+// 3-stage ring; 16 the one-row-per-wave key-split combine (flash_combine_kernel).  Returns the previous
+// bits (mode < 0: query).
 static int g_flash_v2 = 0;
 extern "C" int s2h_flash_variant2(int mode) {
   const int prev = g_flash_v2;
@@ -501,9 +552,18 @@ static int flash_launch(FlashArgs& a, hipStream_t st) {
     else
       hipLaunchKernelGGL((flash_fwd_kernel<DP, FDROP_HASH, DV, QS>), grid, dim3(FL_WAVES * 64), 0, st, a);
   }
-  if (a.splits > 1)
-    hipLaunchKernelGGL((flash_combine_kernel<DP, DV>), dim3((unsigned)(((int64_t)a.BH * a.Lq + 3) / 4)), dim3(256), 0,
-                       st, a);
+  if (a.splits > 1) {
+    const int64_t rows = (int64_t)a.BH * a.Lq;
+    constexpr int RPB = 256 / (DV / 4);
+    if ((s2h_flash_v2() & 16) || (((uintptr_t)a.ws_o | (uintptr_t)a.ws_ml) & 15))
+      hipLaunchKernelGGL((flash_combine_kernel<DP, DV>), dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, a);
+    else if (a.splits == 2)
+      hipLaunchKernelGGL((flash_combine_vec_kernel<DP, DV, 2>), dim3((unsigned)((rows + RPB - 1) / RPB)), dim3(256), 0,
+                         st, a);
+    else
+      hipLaunchKernelGGL((flash_combine_vec_kernel<DP, DV>), dim3((unsigned)((rows + RPB - 1) / RPB)), dim3(256), 0,
+                         st, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
 """Round-6 flash kernel variants (s2h_flash_variant2 A/B bits): the head-dim-256 self-attention dQ kernel
 with 8 fragment reads ahead (bit 1), the head-dim <= 128 dQ kernel (bit 2) and forward (bit 4) on the
-3-stage LDS ring with one barrier per tile, the 32x32 dK / dV kernel on that ring (bit 8).  Each computes the same sums in the same order as the
+3-stage LDS ring with one barrier per tile, the 32x32 dK / dV kernel on that ring (bit 8), the
+one-row-per-wave key-split combine (bit 16).  Each computes the same sums in the same order as the
 default kernel, so the outputs are bit-identical (forward O / LSE / keep bitmap, backward dQ / dK / dV),
 with and without dropout (hashed, and the keep bitmap at head dim 256), with key and query tails."""
 import pytest
@@ -12,7 +13,8 @@ DEV = "cuda"
 
 @pytest.mark.parametrize("B,H,Lq,Lk,D,p", [(2, 2, 300, 260, 56, 0.1), (3, 1, 256, 200, 128, 0.0),
                                            (2, 1, 1024, 1024, 256, 0.1), (2, 2, 128, 70, 64, 0.0),
-                                           (104, 1, 160, 300, 256, 0.1)])
+                                           (104, 1, 160, 300, 256, 0.1),
+                                           (13, 1, 1024, 1024, 256, 0.1)])
 def test_flash_round6_variants_bit_identical(B, H, Lq, Lk, D, p):
     from sam2_video.kernels import ops
     from sam2_video.kernels._lib import lib
@@ -26,7 +28,7 @@ def test_flash_round6_variants_bit_identical(B, H, Lq, Lk, D, p):
     out = {}
     prev = lib().s2h_flash_variant2(-1)
     try:
-        for bits in (0, 15):
+        for bits in (0, 31):
             lib().s2h_flash_variant2(bits)
             o = torch.empty(B, Lq, H, D, device=DEV, dtype=bf)
             lse = torch.empty(B, H, Lq, device=DEV)
@@ -40,5 +42,5 @@ def test_flash_round6_variants_bit_identical(B, H, Lq, Lk, D, p):
     finally:
         lib().s2h_flash_variant2(prev)
     assert not torch.isnan(out[0][2].float()).any()
-    for a, b in zip(out[0], out[15]):
+    for a, b in zip(out[0], out[31]):
         assert torch.equal(a, b)

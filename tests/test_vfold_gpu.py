@@ -240,15 +240,19 @@ def test_vfold_dk_two_wave_kernel_matches_one_wave_kernel(Lq, lks, p_drop):
 @pytest.mark.parametrize("B,Lq,Lk,p_drop", [(13, 1024, 2056, 0.1), (3, 200, 300, 0.0), (2, 160, 70, 0.1)])
 def test_vfold_forward_ring_depths_bit_identical(B, Lq, Lk, p_drop):
     """the V-fold flash forward on its default 3-stage K / M ring with one barrier per tile against the
-    round-5 2-stage ring (variant bit 5, s2h_attn_config(65)): the same u', LSE and keep bitmap"""
+    round-5 2-stage ring (variant bit 5, s2h_attn_config(65)): the same u', LSE and keep bitmap; and the
+    key-split combine with 16 lanes per row against the one-row-per-wave one (s2h_flash_variant2 bit 16,
+    keyed -1 here)"""
     from sam2_video.kernels._lib import lib
     ops = _ops()
     q, k, m, _, _ = _inputs(B, Lq, Lk, 5)
     out = {}
     prev = lib().s2h_attn_config(1)
+    prev2 = lib().s2h_flash_variant2(0)
     try:
-        for variant in (1, 65):
-            lib().s2h_attn_config(variant)
+        for variant in (1, 65, -1):
+            lib().s2h_attn_config(1 if variant < 0 else variant)
+            lib().s2h_flash_variant2(16 if variant < 0 else 0)
             u = torch.full((B, Lq, 1, 72), float("nan"), device=DEV, dtype=torch.bfloat16)
             lse = torch.empty(B, 1, Lq, device=DEV)
             keep = torch.zeros(ops.keep_words(B, 1, Lq, Lk), device=DEV, dtype=torch.int32)
@@ -257,9 +261,11 @@ def test_vfold_forward_ring_depths_bit_identical(B, Lq, Lk, p_drop):
             out[variant] = (u, lse, keep)
     finally:
         lib().s2h_attn_config(prev)
-    assert not torch.isnan(out[1][0][..., :65].float()).any()
-    for a, b in zip(out[1], out[65]):
-        assert torch.equal(a, b)
+        lib().s2h_flash_variant2(prev2)
+    assert not torch.isnan(out[1][0].float()).any()
+    for v in (65, -1):
+        for a, b in zip(out[1], out[v]):
+            assert torch.equal(a, b)
 
 
 def test_vfold_out_projection_fusion_matches_two_gemms(monkeypatch):
