@@ -490,10 +490,92 @@ __global__ void maxpool2_bwd_kernel(int B, int H, int W, int C, const void* x, i
     }
   }
 }
+// 16-B forms (round 6): VEC channels per lane, 32-bit index math -- the scalar kernels above move 2 B
+// per load and pay a 64-bit division chain per element (19.7 / 24.0 us per Hiera q-pool launch).
+// The same per-channel scan (window order, NaN propagates, first maximum gets the gradient).
+template <typename T>
+__global__ void maxpool2_fwd_vec_kernel(int B, int H, int W, int C, const T* x, int ldx, T* y) {
+  constexpr int VEC = V16<T>::VEC;
+  const int Ho = H / 2, Wo = W / 2, cc = C / VEC;
+  const int n = B * Ho * Wo * cc;
+  GRID_STRIDE(i, n) {
+    const int ii = (int)i;
+    int p = ii / cc;
+    const int c = (ii - p * cc) * VEC;
+    const int xo = p % Wo; p /= Wo;
+    const int yo = p % Ho;
+    const int b = p / Ho;
+    float m[VEC];
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) m[j] = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int pix = (b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1);
+      float v[VEC];
+      V16<T>::load(x + (int64_t)pix * ldx + c, v);
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (v[j] > m[j] || isnan(v[j])) m[j] = v[j];
+    }
+    V16<T>::store(y + (int64_t)ii * VEC, m);
+  }
+}
+template <typename T>
+__global__ void maxpool2_bwd_vec_kernel(int B, int H, int W, int C, const T* x, int ldx, const T* dy, T* dx,
+                                        int lddx) {
+  constexpr int VEC = V16<T>::VEC;
+  const int Ho = H / 2, Wo = W / 2, cc = C / VEC;
+  const int n = B * Ho * Wo * cc;
+  GRID_STRIDE(i, n) {
+    const int ii = (int)i;
+    int p = ii / cc;
+    const int c = (ii - p * cc) * VEC;
+    const int xo = p % Wo; p /= Wo;
+    const int yo = p % Ho;
+    const int b = p / Ho;
+    float v[4][VEC], m[VEC], g[VEC];
+    int best[VEC];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      V16<T>::load(x + (int64_t)((b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1)) * ldx + c, v[k]);
+    V16<T>::load(dy + (int64_t)ii * VEC, g);
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) { m[j] = -INFINITY; best[j] = 0; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < VEC; ++j)
+        if (v[k][j] > m[j] || isnan(v[k][j])) { m[j] = v[k][j]; best[j] = k; }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float o[VEC];
+#pragma unroll
+      for (int j = 0; j < VEC; ++j) o[j] = best[j] == k ? g[j] : 0.f;
+      V16<T>::store(dx + (int64_t)((b * H + 2 * yo + (k >> 1)) * W + 2 * xo + (k & 1)) * lddx + c, o);
+    }
+  }
+}
+// the 16-B forms need VEC | C, VEC | the row strides, 16-B aligned pointers and 32-bit indices
+static bool maxpool_vec_ok(int dt, int B, int H, int W, int C, int64_t ld0, int64_t ld1, const void* p0,
+                           const void* p1, const void* p2) {
+  const int vec = dt == S2H_BF16 ? 8 : 4;
+  return (dt == S2H_BF16 || dt == S2H_F32) && C % vec == 0 && ld0 % vec == 0 && ld1 % vec == 0 && al16(p0) &&
+         al16(p1) && (!p2 || al16(p2)) && (int64_t)B * H * W * std::max(ld0, ld1) < (1ll << 31);
+}
 extern "C" int s2h_maxpool2_fwd(int dt, int B, int H, int W, int C, const void* x, int64_t ldx, void* y,
                                 hipStream_t st) {
   const int64_t n = (int64_t)B * (H / 2) * (W / 2) * C;
   if (n <= 0) return 0;
+  if (maxpool_vec_ok(dt, B, H, W, C, ldx, C, x, y, nullptr)) {
+    const int vec = dt == S2H_BF16 ? 8 : 4;
+    if (dt == S2H_BF16)
+      hipLaunchKernelGGL(maxpool2_fwd_vec_kernel<bf16>, ew_grid(n / vec), dim3(256), 0, st, B, H, W, C,
+                         (const bf16*)x, (int)ldx, (bf16*)y);
+    else
+      hipLaunchKernelGGL(maxpool2_fwd_vec_kernel<float>, ew_grid(n / vec), dim3(256), 0, st, B, H, W, C,
+                         (const float*)x, (int)ldx, (float*)y);
+    return (int)hipGetLastError();
+  }
   DISPATCH_T(dt, maxpool2_fwd_kernel, ew_grid(n), B, H, W, C, x, ldx, y);
   return (int)hipGetLastError();
 }
@@ -501,6 +583,16 @@ extern "C" int s2h_maxpool2_bwd(int dt, int B, int H, int W, int C, const void* 
                                 void* dx, int64_t lddx, hipStream_t st) {
   const int64_t n = (int64_t)B * (H / 2) * (W / 2) * C;
   if (n <= 0) return 0;
+  if (maxpool_vec_ok(dt, B, H, W, C, ldx, lddx, x, dx, dy)) {
+    const int vec = dt == S2H_BF16 ? 8 : 4;
+    if (dt == S2H_BF16)
+      hipLaunchKernelGGL(maxpool2_bwd_vec_kernel<bf16>, ew_grid(n / vec), dim3(256), 0, st, B, H, W, C,
+                         (const bf16*)x, (int)ldx, (const bf16*)dy, (bf16*)dx, (int)lddx);
+    else
+      hipLaunchKernelGGL(maxpool2_bwd_vec_kernel<float>, ew_grid(n / vec), dim3(256), 0, st, B, H, W, C,
+                         (const float*)x, (int)ldx, (const float*)dy, (float*)dx, (int)lddx);
+    return (int)hipGetLastError();
+  }
   DISPATCH_T(dt, maxpool2_bwd_kernel, ew_grid(n), B, H, W, C, x, ldx, dy, dx, lddx);
   return (int)hipGetLastError();
 }
@@ -843,10 +935,11 @@ extern "C" int s2h_bilinear_fwd(int N, int hi, int wi, int ho, int wo, const flo
 // same skipped zeros, the same (wy * wx) * dy products added in the same order -- bit-identical.  The
 // per-candidate index arithmetic made the kernel VALU-bound (126 us for the 104-plane 256^2 -> 512^2
 // mask upsampling backward).
-// X2: exact 2x upsampling (ho = 2 hi, wo = 2 wi): the taps of input i come from outputs 2i - 1 .. 2i + 2
-// only (the wider search's other candidates all have zero weight), so 4 x 4 candidates instead of 8 x 8
-// -- the same nonzero terms in the same order
-template <int MAXC, bool X2 = false>
+// F: exact integer upsampling (ho = F hi, wo = F wi; 0 otherwise): the taps of input i come from outputs
+// F i - F / 2 .. F i + 3 F / 2 - 1 only (the wider search's other candidates all have zero weight), so
+// 2F x 2F candidates (2x: 4 x 4 instead of 8 x 8, 4x: 8 x 8 instead of 12 x 16) -- the same nonzero terms
+// in the same order
+template <int MAXC, int F = 0>
 __global__ __launch_bounds__(256) void bilinear_bwd_hoist_kernel(int N, int hi, int wi, int ho, int wo, const float* dy,
                                                                  float* dx) {
   const float sh = (float)hi / ho, sw = (float)wi / wo;
@@ -856,10 +949,10 @@ __global__ __launch_bounds__(256) void bilinear_bwd_hoist_kernel(int N, int hi, 
     const int64_t r = i / wi;
     const int iy = r % hi;
     const int p = r / hi;
-    const int oy0 = X2 ? max(0, 2 * iy - 1) : max(0, (int)floorf((iy - 0.5f) / sh - 0.5f) - 1);
-    const int oy1 = X2 ? min(ho - 1, 2 * iy + 2) : min(ho - 1, (int)ceilf((iy + 1.5f) / sh - 0.5f) + 1);
-    const int ox0 = X2 ? max(0, 2 * ix - 1) : max(0, (int)floorf((ix - 0.5f) / sw - 0.5f) - 1);
-    const int ox1 = X2 ? min(wo - 1, 2 * ix + 2) : min(wo - 1, (int)ceilf((ix + 1.5f) / sw - 0.5f) + 1);
+    const int oy0 = F ? max(0, F * iy - F / 2) : max(0, (int)floorf((iy - 0.5f) / sh - 0.5f) - 1);
+    const int oy1 = F ? min(ho - 1, F * iy + 3 * F / 2 - 1) : min(ho - 1, (int)ceilf((iy + 1.5f) / sh - 0.5f) + 1);
+    const int ox0 = F ? max(0, F * ix - F / 2) : max(0, (int)floorf((ix - 0.5f) / sw - 0.5f) - 1);
+    const int ox1 = F ? min(wo - 1, F * ix + 3 * F / 2 - 1) : min(wo - 1, (int)ceilf((ix + 1.5f) / sw - 0.5f) + 1);
     float wxs[MAXC];
 #pragma unroll
     for (int c = 0; c < MAXC; ++c) {
@@ -887,7 +980,9 @@ extern "C" int s2h_bilinear_bwd(int N, int hi, int wi, int ho, int wo, const flo
   // candidate output columns per input column: ox1 - ox0 + 1 <= ceil(2 wo / wi) + 4 (2x: 8)
   const int maxc = (int)ceilf(2.f * wo / wi) + 4;
   if (ho == 2 * hi && wo == 2 * wi)
-    hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<4, true>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+    hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<4, 2>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
+  else if (ho == 4 * hi && wo == 4 * wi)
+    hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<8, 4>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   else if (maxc <= 8) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<8>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   else if (maxc <= 16) hipLaunchKernelGGL((bilinear_bwd_hoist_kernel<16>), ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);
   else hipLaunchKernelGGL(bilinear_bwd_kernel, ew_grid(n), dim3(256), 0, st, N, hi, wi, ho, wo, dy, dx);

@@ -754,6 +754,29 @@ def test_layernorm(dtype, tol, rows, C):
     _close(y2, torch.nn.functional.layer_norm(xs.float(), (C,), g, b, 1e-6), tol)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_maxpool2_vector_path_matches_torch(dtype):
+    """the 16-B maxpool forms (round 6; C a multiple of 8 / 4, strided pixels): values with many ties and a
+    few NaNs, odd H / W -- the same pooled values and the same gradient routing (first maximum of the
+    window scan, NaN wins) as torch's max_pool2d"""
+    ops = _ops()
+    torch.manual_seed(5)
+    full = torch.randint(-3, 4, (3, 17, 14, 64), device=DEV).to(dtype)
+    full.view(-1)[torch.randperm(full.numel(), device=DEV)[:40]] = float("nan")
+    x = full[..., :48]  # pixel stride 64
+    y = ops.maxpool2(x)
+    xr = x.float().permute(0, 3, 1, 2).contiguous().requires_grad_(True)
+    ref = torch.nn.functional.max_pool2d(xr, 2)
+    torch.testing.assert_close(y.float(), ref.permute(0, 2, 3, 1), rtol=0, atol=0, equal_nan=True)
+    g = torch.randn(y.shape, device=DEV).to(dtype)
+    ref.backward(g.float().permute(0, 3, 1, 2))
+    dx = torch.full_like(x, 7.0)
+    ops.maxpool2_bwd(x, g.contiguous(), dx)
+    exp = xr.grad.permute(0, 2, 3, 1)
+    torch.testing.assert_close(dx[:, :16, :14].float(), exp[:, :16, :14], rtol=0, atol=0)
+    assert bool((dx[:, 16] == 7.0).all())  # the odd last row is outside every window: untouched
+
+
 def test_elementwise_misc():
     ops = _ops()
     x = torch.randn(2, 10, 12, 6, device=DEV)
