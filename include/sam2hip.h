@@ -401,6 +401,12 @@ int s2h_dec_self(int R, int T, int skip, float scale, const void* x, const void*
                  const float* g1, const float* b1, float eps1, const void* wqc, const float* bqc, void* qa, void* qs,
                  void* ks, void* vs, void* os, float* lse, void* y1, void* x1, float* mean1, float* rstd1, void* qt,
                  void* qq, hipStream_t st);
+/* A/B knob (round 6): 1 (default) the s2h_dec_* kernels issue each projection's weight fragments a phase
+ * ahead (s2h_dec_self: the q / k / v weights together, the out- and q-projection weights under the
+ * attention and norm1; the others: under their row loads and LayerNorms), 0 each projection loads its own
+ * before its MFMAs; the same sums either way.  Returns the previous setting
+ * (mode < 0: query only). */
+int s2h_dec_sched(int mode);
 /* The second half's token side around the MLP (whose two GEMMs stay s2h_gemm launches; transformer.py:170-173):
  * s2h_dec_post_a: y2 = ot Wo^T + bo + x1, x2 = norm2(y2);
  * s2h_dec_post_b: x3 = norm3(y3) (y3 = MLP output + x2), q2 = x3 + pe, kio = q2 Wki^T + bki,

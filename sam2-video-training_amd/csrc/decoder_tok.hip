@@ -164,6 +164,42 @@ __device__ __forceinline__ void dt_gemm(const bf16* A, int pa, const bf16* W, fl
     }
   }
 }
+// The weight fragments of one C[16][N] = A[16][256] W^T (dt_gemm with WK = 1: 8 waves split N, each
+// wave the whole K) held apart from their MFMAs, so a later GEMM's weights can be issued a phase early
+// and their memory round trip overlaps the work before it (round 6; the same MFMAs in the same order as
+// dt_gemm, bit for bit).  N = 256, K = 256: 2 n-blocks x 8 k-steps per wave (64 VGPRs), N = 128: 1 x 8.
+template <int N, int K = DT_C>
+struct DtWFrag {
+  static constexpr int NBW = N / 16 / DT_NW, KS = K / 32;
+  bf16x8 b[NBW][KS];
+  __device__ __forceinline__ void load(const bf16* W) {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#pragma unroll
+    for (int g = 0; g < NBW; ++g) {
+      const bf16* wp = W + (int64_t)((w * NBW + g) * 16 + (lane & 15)) * K + 8 * (lane >> 4);
+#pragma unroll
+      for (int s = 0; s < KS; ++s) b[g][s] = *(const bf16x8*)(wp + s * 32);
+    }
+  }
+  template <typename Epi>
+  __device__ __forceinline__ void mma(const bf16* A, int pa, Epi epi) const {
+    const int lane = threadIdx.x & 63;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    f32x4 acc[NBW];
+#pragma unroll
+    for (int g = 0; g < NBW; ++g) acc[g] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const bf16x8 a = *(const bf16x8*)(A + (lane & 15) * pa + s * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int g = 0; g < NBW; ++g) acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b[g][s], acc[g], 0, 0, 0);
+    }
+#pragma unroll
+    for (int g = 0; g < NBW; ++g) epi(w * NBW + g, acc[g]);
+  }
+};
+
 template <int N, int WK, typename EpiEl>
 __device__ __forceinline__ void dt_gemm_reduce(const float* part, EpiEl epi_el) {
   __syncthreads();
@@ -238,21 +274,34 @@ __device__ __forceinline__ void dt_layernorm(bf16* out, const float* y, DtNorm n
 }
 
 // -------------------------------------------------------------------------------- dt_self
+template <bool SCHED>
 __global__ __launch_bounds__(DT_NT) void dt_self_kernel(DtSelfArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 sx[DT_R * DT_PA], spe[DT_R * DT_PA], sqa[DT_R * DT_PA],
       sq[DT_R * DT_PA], sk[DT_R * DT_PA], sv[DT_R * DT_PA], so[DT_R * DT_PA], sx1[DT_R * DT_PA];
   __shared__ __attribute__((aligned(16))) float sy[DT_R * DT_PF];
   int r0, nr;
   dt_rows(p.R, p.T, r0, nr);
+  // the q / k / v weights first (one round trip for all three, under the row loads); the out- and
+  // q-projection weights are issued ahead of the attention and of norm1 below
+  DtWFrag<DT_C> wq, wk, wv;
+  if constexpr (SCHED) { wq.load(p.q.w); wk.load(p.k.w); wv.load(p.v.w); }
   dt_load<DT_C>(sx, DT_PA, p.x, r0, nr);
   dt_load<DT_C>(spe, DT_PA, p.pe, r0, nr);
   __syncthreads();
   if (!p.skip) dt_add(sqa, sx, spe, p.qa, r0, nr);
   __syncthreads();
   const bf16* qin = p.skip ? sx : sqa;
-  dt_gemm<DT_C, DT_C, 1>(qin, DT_PA, p.q.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sq, DT_PA, p.q.b, nb, a); });
-  dt_gemm<DT_C, DT_C, 1>(qin, DT_PA, p.k.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sk, DT_PA, p.k.b, nb, a); });
-  dt_gemm<DT_C, DT_C, 1>(sx, DT_PA, p.v.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sv, DT_PA, p.v.b, nb, a); });
+  if constexpr (SCHED) {
+    wq.mma(qin, DT_PA, [&](int nb, const f32x4& a) { dt_epi_bf16(sq, DT_PA, p.q.b, nb, a); });
+    wk.mma(qin, DT_PA, [&](int nb, const f32x4& a) { dt_epi_bf16(sk, DT_PA, p.k.b, nb, a); });
+    wv.mma(sx, DT_PA, [&](int nb, const f32x4& a) { dt_epi_bf16(sv, DT_PA, p.v.b, nb, a); });
+  } else {
+    dt_gemm<DT_C, DT_C, 1>(qin, DT_PA, p.q.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sq, DT_PA, p.q.b, nb, a); });
+    dt_gemm<DT_C, DT_C, 1>(qin, DT_PA, p.k.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sk, DT_PA, p.k.b, nb, a); });
+    dt_gemm<DT_C, DT_C, 1>(sx, DT_PA, p.v.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sv, DT_PA, p.v.b, nb, a); });
+  }
+  DtWFrag<DT_C> wo;
+  if constexpr (SCHED) wo.load(p.o.w);
   __syncthreads();
   dt_store<DT_C>(p.qs, sq, DT_PA, r0, nr);
   dt_store<DT_C>(p.ks, sk, DT_PA, r0, nr);
@@ -306,8 +355,13 @@ __global__ __launch_bounds__(DT_NT) void dt_self_kernel(DtSelfArgs p) {
   for (int i = threadIdx.x; i < (DT_R - nr) * DT_C; i += blockDim.x) so[(nr + i / DT_C) * DT_PA + i % DT_C] = (bf16)0.f;
   __syncthreads();
   dt_store<DT_C>(p.os, so, DT_PA, r0, nr);
-  dt_gemm<DT_C, DT_C, 1>(so, DT_PA, p.o.w, nullptr,
-                         [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, p.skip ? nullptr : sx, nb, a); });
+  if constexpr (SCHED)
+    wo.mma(so, DT_PA, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, p.skip ? nullptr : sx, nb, a); });
+  else
+    dt_gemm<DT_C, DT_C, 1>(so, DT_PA, p.o.w, nullptr,
+                           [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, p.skip ? nullptr : sx, nb, a); });
+  DtWFrag<DT_I> wc;
+  if constexpr (SCHED) wc.load(p.qc.w);
   __syncthreads();
   dt_store_f(p.y1, sy, r0, nr);
   dt_layernorm(sx1, sy, p.n1, p.mean1, p.rstd1, r0, nr);
@@ -315,7 +369,10 @@ __global__ __launch_bounds__(DT_NT) void dt_self_kernel(DtSelfArgs p) {
   dt_store<DT_C>(p.x1, sx1, DT_PA, r0, nr);
   dt_add(sqa, sx1, spe, p.qt, r0, nr);
   __syncthreads();
-  dt_gemm<DT_C, DT_I, 1>(sqa, DT_PA, p.qc.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sq, DT_PI, p.qc.b, nb, a); });
+  if constexpr (SCHED)
+    wc.mma(sqa, DT_PA, [&](int nb, const f32x4& a) { dt_epi_bf16(sq, DT_PI, p.qc.b, nb, a); });
+  else
+    dt_gemm<DT_C, DT_I, 1>(sqa, DT_PA, p.qc.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sq, DT_PI, p.qc.b, nb, a); });
   __syncthreads();
   dt_store<DT_I>(p.qq, sq, DT_PI, r0, nr);
 }
@@ -325,15 +382,21 @@ __global__ __launch_bounds__(DT_NT) void dt_self_kernel(DtSelfArgs p) {
 // per workgroup took longer (a single-launch dt_post with the MLP inside: 79 us per launch) than the
 // separate GEMMs, which spread them over the chip.
 // dt_post_a: token -> image out-projection (+ x1) -> norm2
+template <bool SCHED>
 __global__ __launch_bounds__(DT_NT) void dt_post_a_kernel(DtPostArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 sot[DT_R * DT_PI], sx1[DT_R * DT_PA], sx2[DT_R * DT_PA];
   __shared__ __attribute__((aligned(16))) float sy[DT_R * DT_PF];
   int r0, nr;
   dt_rows(p.R, p.T, r0, nr);
+  DtWFrag<DT_C, DT_I> wo;  // under the row loads (SCHED)
+  if constexpr (SCHED) wo.load(p.o.w);
   dt_load<DT_I>(sot, DT_PI, p.ot, r0, nr);
   dt_load<DT_C>(sx1, DT_PA, p.x1, r0, nr);
   __syncthreads();
-  dt_gemm<DT_I, DT_C, 1>(sot, DT_PI, p.o.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, sx1, nb, a); });
+  if constexpr (SCHED)
+    wo.mma(sot, DT_PI, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, sx1, nb, a); });
+  else
+    dt_gemm<DT_I, DT_C, 1>(sot, DT_PI, p.o.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, sx1, nb, a); });
   __syncthreads();
   dt_store_f(p.y2, sy, r0, nr);
   dt_layernorm(sx2, sy, p.n2, p.mean2, p.rstd2, r0, nr);
@@ -343,12 +406,15 @@ __global__ __launch_bounds__(DT_NT) void dt_post_a_kernel(DtPostArgs p) {
 
 // dt_post_b: norm3 of the MLP output (fc2's GEMM already added x2) -> x3; q2 = x3 + pe -> the image ->
 // token k / v projections [and the final token -> image query]
+template <bool SCHED>
 __global__ __launch_bounds__(DT_NT) void dt_post_b_kernel(DtPostArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 spe[DT_R * DT_PA], sx3[DT_R * DT_PA], sq2[DT_R * DT_PA],
       sk[DT_R * DT_PI], sv[DT_R * DT_PI];
   __shared__ __attribute__((aligned(16))) float sy[DT_R * DT_PF];
   int r0, nr;
   dt_rows(p.R, p.T, r0, nr);
+  DtWFrag<DT_I> wki, wvi;  // under the row loads and norm3 (SCHED)
+  if constexpr (SCHED) { wki.load(p.ki.w); wvi.load(p.vi.w); }
   dt_load<DT_C>(spe, DT_PA, p.pe, r0, nr);
   for (int i = threadIdx.x; i < DT_R * DT_C; i += blockDim.x) {
     const int r = i / DT_C, c = i % DT_C;
@@ -360,8 +426,13 @@ __global__ __launch_bounds__(DT_NT) void dt_post_b_kernel(DtPostArgs p) {
   dt_store<DT_C>(p.x3, sx3, DT_PA, r0, nr);
   dt_add(sq2, sx3, spe, p.q2, r0, nr);
   __syncthreads();
-  dt_gemm<DT_C, DT_I, 1>(sq2, DT_PA, p.ki.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sk, DT_PI, p.ki.b, nb, a); });
-  dt_gemm<DT_C, DT_I, 1>(sx3, DT_PA, p.vi.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sv, DT_PI, p.vi.b, nb, a); });
+  if constexpr (SCHED) {
+    wki.mma(sq2, DT_PA, [&](int nb, const f32x4& a) { dt_epi_bf16(sk, DT_PI, p.ki.b, nb, a); });
+    wvi.mma(sx3, DT_PA, [&](int nb, const f32x4& a) { dt_epi_bf16(sv, DT_PI, p.vi.b, nb, a); });
+  } else {
+    dt_gemm<DT_C, DT_I, 1>(sq2, DT_PA, p.ki.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sk, DT_PI, p.ki.b, nb, a); });
+    dt_gemm<DT_C, DT_I, 1>(sx3, DT_PA, p.vi.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_bf16(sv, DT_PI, p.vi.b, nb, a); });
+  }
   __syncthreads();
   dt_store<DT_I>(p.kio, sk, DT_PI, r0, nr);
   dt_store<DT_I>(p.vio, sv, DT_PI, r0, nr);
@@ -375,15 +446,21 @@ __global__ __launch_bounds__(DT_NT) void dt_post_b_kernel(DtPostArgs p) {
 }
 
 // -------------------------------------------------------------------------------- dt_final
+template <bool SCHED>
 __global__ __launch_bounds__(DT_NT) void dt_final_kernel(DtFinalArgs p) {
   __shared__ __attribute__((aligned(16))) bf16 sof[DT_R * DT_PI], sx3[DT_R * DT_PA], shs[DT_R * DT_PA];
   __shared__ __attribute__((aligned(16))) float sy[DT_R * DT_PF];
   int r0, nr;
   dt_rows(p.R, p.T, r0, nr);
+  DtWFrag<DT_C, DT_I> wo;  // under the row loads (SCHED)
+  if constexpr (SCHED) wo.load(p.o.w);
   dt_load<DT_I>(sof, DT_PI, p.of, r0, nr);
   dt_load<DT_C>(sx3, DT_PA, p.x3, r0, nr);
   __syncthreads();
-  dt_gemm<DT_I, DT_C, 1>(sof, DT_PI, p.o.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, sx3, nb, a); });
+  if constexpr (SCHED)
+    wo.mma(sof, DT_PI, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, sx3, nb, a); });
+  else
+    dt_gemm<DT_I, DT_C, 1>(sof, DT_PI, p.o.w, nullptr, [&](int nb, const f32x4& a) { dt_epi_res(sy, p.o.b, sx3, nb, a); });
   __syncthreads();
   dt_store_f(p.y, sy, r0, nr);
   dt_layernorm(shs, sy, p.n, p.mean, p.rstd, r0, nr);
@@ -397,6 +474,7 @@ int dt_blocks(int R, int T) {
   return (R / T + per - 1) / per;
 }
 DtLin lin(const void* w, const float* b) { return DtLin{(const bf16*)w, b}; }
+int g_dt_sched = 1;  // the dt_* kernels <true>: weights issued a phase ahead (s2h_dec_sched A/B knob)
 
 }  // namespace
 
@@ -406,6 +484,14 @@ DtLin lin(const void* w, const float* b) { return DtLin{(const bf16*)w, b}; }
 //   os = softmax(scale q k^T per object, head) v     (lse [objects, 8, T], natural log)
 //   y1 = os Wo^T + bo (+ x if !skip)    x1 = norm1(y1) (mean1 / rstd1)    qt = x1 + pe    qq = qt Wqc^T + bqc
 // Weights [N, K] bf16, biases fp32; outputs at the given slots (row-major, contiguous).
+// A/B knob (round 6): 1 (default) the token-side kernels with their weight fragments issued a phase ahead
+// (DtWFrag), 0 each projection loading its own before its MFMAs.  Returns the previous setting
+// (mode < 0: query only).
+extern "C" int s2h_dec_sched(int mode) {
+  const int prev = g_dt_sched;
+  if (mode >= 0) g_dt_sched = mode;
+  return prev;
+}
 extern "C" int s2h_dec_self(int R, int T, int skip, float scale, const void* x, const void* pe, const void* wq,
                             const float* bq, const void* wk, const float* bk, const void* wv, const float* bv,
                             const void* wo, const float* bo, const float* g1, const float* b1, float eps1,
@@ -420,7 +506,10 @@ extern "C" int s2h_dec_self(int R, int T, int skip, float scale, const void* x, 
   p.n1 = DtNorm{g1, b1, eps1};
   p.qa = (bf16*)qa; p.qs = (bf16*)qs; p.ks = (bf16*)ks; p.vs = (bf16*)vs; p.os = (bf16*)os; p.lse = lse;
   p.y1 = (bf16*)y1; p.x1 = (bf16*)x1; p.mean1 = mean1; p.rstd1 = rstd1; p.qt = (bf16*)qt; p.qq = (bf16*)qq;
-  hipLaunchKernelGGL(dt_self_kernel, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  if (g_dt_sched)
+    hipLaunchKernelGGL(dt_self_kernel<true>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  else
+    hipLaunchKernelGGL(dt_self_kernel<false>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -439,7 +528,10 @@ extern "C" int s2h_dec_post_a(int R, int T, const void* ot, const void* x1, cons
   p.o = lin(wo, bo);
   p.n2 = DtNorm{g2, b2n, eps2};
   p.y2 = (bf16*)y2; p.x2 = (bf16*)x2; p.mean2 = mean2; p.rstd2 = rstd2;
-  hipLaunchKernelGGL(dt_post_a_kernel, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  if (g_dt_sched)
+    hipLaunchKernelGGL(dt_post_a_kernel<true>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  else
+    hipLaunchKernelGGL(dt_post_a_kernel<false>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -455,7 +547,10 @@ extern "C" int s2h_dec_post_b(int R, int T, int final_q, const void* y3, const v
   p.n3 = DtNorm{g3, b3n, eps3};
   p.x3 = (bf16*)x3; p.mean3 = mean3; p.rstd3 = rstd3; p.q2 = (bf16*)q2; p.kio = (bf16*)kio; p.vio = (bf16*)vio;
   p.qfa = (bf16*)qfa; p.qqf = (bf16*)qqf;
-  hipLaunchKernelGGL(dt_post_b_kernel, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  if (g_dt_sched)
+    hipLaunchKernelGGL(dt_post_b_kernel<true>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  else
+    hipLaunchKernelGGL(dt_post_b_kernel<false>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
   return (int)hipGetLastError();
 }
 
@@ -470,6 +565,9 @@ extern "C" int s2h_dec_final(int R, int T, const void* of, const void* x3, const
   p.o = lin(wo, bo);
   p.n = DtNorm{g, bn, eps};
   p.y = (bf16*)y; p.hs = (bf16*)hs; p.mean = mean; p.rstd = rstd;
-  hipLaunchKernelGGL(dt_final_kernel, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  if (g_dt_sched)
+    hipLaunchKernelGGL(dt_final_kernel<true>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
+  else
+    hipLaunchKernelGGL(dt_final_kernel<false>, dim3(dt_blocks(R, T)), dim3(DT_NT), 0, st, p);
   return (int)hipGetLastError();
 }

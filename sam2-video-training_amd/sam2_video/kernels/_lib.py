@@ -35,6 +35,7 @@ SIGNATURES = {
     "s2h_linear_dgrad_ln_bwd_ws_bytes": [I, I],
     "s2h_linear_dgrad_ln_bwd": [I, I, I, P, L, P, L, F, P, L, P, P, P, P, L, P, L, P, P, P, P],
     "s2h_ffn_bwd_dgrad": [I, I, P, L, P, P, P, L, F, P, L, P, L, P],
+    "s2h_dec_sched": [I],
     "s2h_dec_self": [I, I, I, F, P, P, P, P, P, P, P, P, P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
     "s2h_dec_post_a": [I, I, P, P, P, P, P, P, F, P, P, P, P, P],
     "s2h_dec_post_b": [I, I, I, P, P, P, P, F, P, P, P, P, P, P, P, P, P, P, P, P, P, P, P],
@@ -204,6 +205,8 @@ def lib():
             h.s2h_gemm_f32_small(int(os.environ["S2H_GEMM_F32_SMALL"]))
         if os.environ.get("S2H_FLASH_V2"):  # round-6 flash kernel variants (A/B bits, s2h_flash_variant2)
             h.s2h_flash_variant2(int(os.environ["S2H_FLASH_V2"]))
+        if os.environ.get("S2H_DEC_SCHED"):  # token self-attention block weights a phase ahead (A/B)
+            h.s2h_dec_sched(int(os.environ["S2H_DEC_SCHED"]))
         if os.environ.get("S2H_ATTN_WIN"):  # small-window attention kernels on / off (A/B)
             h.s2h_attn_win(int(os.environ["S2H_ATTN_WIN"]))
         if os.environ.get("S2H_GEMM_AREG"):  # ... short-K GEMMs with A in registers (A/B)

@@ -69,3 +69,34 @@ def test_decoder_token_side_fused_matches_unfused_bf16(golden, monkeypatch):
     flat0 = torch.cat([v.flatten() for v in g0.values()]).double()
     flat1 = torch.cat([v.flatten() for v in g1.values()]).double()
     assert torch.nn.functional.cosine_similarity(flat0, flat1, dim=0).item() >= 0.999
+
+
+def test_decoder_token_kernels_weight_prefetch_bit_identical():
+    """the token-side kernels with each projection's weight fragments issued a phase ahead (round 6,
+    s2h_dec_sched(1), default) against each projection loading its own (0): the same MFMAs in the same
+    order, so the whole bf16 training step -- masks, loss, every gradient -- is bit-identical"""
+    from step_harness import build_model, golden_batch, grads_by_name, load_golden, run_step
+
+    from sam2_video.kernels._lib import lib
+    g = load_golden("bplus256_point_all")
+    batch = golden_batch(g).to(DEV)
+    res = {}
+    prev = lib().s2h_dec_sched(-1)
+    try:
+        for mode in (0, 1):
+            lib().s2h_dec_sched(mode)
+            model = build_model("base_plus", 256, ["image_encoder", "memory_attention", "memory_encoder",
+                                                   "mask_decoder", "prompt_encoder"], "point", dtype="bf16")
+            stages, _, losses, _ = run_step(model, batch)
+            torch.cuda.synchronize()
+            res[mode] = ([s["pred_masks"].detach().float().cpu() for s in stages], float(losses["total_loss"]),
+                         grads_by_name(model))
+    finally:
+        lib().s2h_dec_sched(prev)
+    (m0, l0, g0), (m1, l1, g1) = res[0], res[1]
+    assert l0 == l1
+    for a, b in zip(m0, m1):
+        assert torch.equal(a, b)
+    assert g0.keys() == g1.keys()
+    for n in g0:
+        assert torch.equal(g0[n], g1[n]), n
